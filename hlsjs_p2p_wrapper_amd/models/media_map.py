@@ -1,0 +1,108 @@
+"""MediaMap — the peer agent's read-only view of the player's playlists.
+
+Parity: ``lib/integration/mapping/media-map.js:4-88`` (component C9).
+
+* ``getSegmentTime(sv)``   → ``sv.time``; throws if undefined (``:14-19``).
+* ``getSegmentList(track, beginTime, duration)`` → the fragments of
+  ``levels[track.level]`` with ``beginTime <= start <= beginTime + duration`` (closed on
+  both ends), in playlist order, as ``SegmentView{sn, trackView: track, time: start}``.
+  Throws if the level does not exist, warns and returns ``[]`` if it is not parsed yet
+  (``:27-54``).  Like the reference it ignores ``track.urlId`` when picking the level.
+* ``getTrackList()`` → level-major / urlId-minor ``TrackView`` list (``:60-73``).
+* ``getSegmentDuration(sv)`` → duration of the *first* fragment of the segment's level
+  (reference quirk kept on purpose, ``:81-87``; only the debug buffer display uses it).
+
+Hot-path note (K1 in SURVEY §2.2): the reference does a linear scan per query.  HLS
+fragment lists are sorted by ``start``, so the closed interval maps to one contiguous
+index range; we cache a start-time array per ``details`` object and answer with two
+binary searches (falling back to the literal scan if the list is ever unsorted).  Batched
+multi-track queries go to the HIP range-select kernel (:mod:`..ops.range_select`).
+"""
+from __future__ import annotations
+
+import bisect
+import logging
+from typing import Any, List
+
+from .segment_view import SegmentView
+from .track_view import TrackView
+
+log = logging.getLogger("hlsjs_p2p_wrapper_amd.media_map")
+
+
+class _StartIndex:
+    __slots__ = ("frags_id", "n", "starts", "sorted")
+
+    def __init__(self, fragments: List[Any]) -> None:
+        self.frags_id = id(fragments)
+        self.n = len(fragments)
+        self.starts = [f.start for f in fragments]
+        s = self.starts
+        self.sorted = all(s[i] <= s[i + 1] for i in range(len(s) - 1))
+
+
+class MediaMap:
+    def __init__(self, hls: Any) -> None:
+        self.hls = hls
+        self._idx: dict = {}
+
+    def getSegmentTime(self, segmentView: SegmentView) -> Any:
+        if segmentView.time is None:
+            raise Exception("getSegmentTime: segmentView.time is undefined")
+        return segmentView.time
+
+    def _level(self, index: Any) -> Any:
+        levels = self.hls.levels
+        if levels is None:
+            raise TypeError("Cannot read property of undefined (hls.levels)")
+        if not isinstance(index, int) or index < 0 or index >= len(levels):
+            return None
+        return levels[index]
+
+    def getSegmentList(self, trackView: TrackView, beginTime: float, duration: float) -> List[SegmentView]:
+        level = self._level(trackView.level)
+        if not level:
+            raise Exception("getSegmentList: level doesn't exist")
+        details = getattr(level, "details", None)
+        if not details:
+            log.warning("getSegmentList: level not parsed yet")
+            return []
+        fragments = details.fragments
+        end = beginTime + duration
+        idx = self._idx.get(trackView.level)
+        if idx is None or idx.frags_id != id(fragments) or idx.n != len(fragments):
+            idx = _StartIndex(fragments)
+            self._idx[trackView.level] = idx
+        if idx.sorted:
+            lo = bisect.bisect_left(idx.starts, beginTime)
+            hi = bisect.bisect_right(idx.starts, end)
+            rng = range(lo, hi)
+        else:
+            rng = [i for i, s in enumerate(idx.starts) if beginTime <= s <= end]
+        out = []
+        for i in rng:
+            f = fragments[i]
+            out.append(SegmentView(sn=f.sn, trackView=trackView, time=f.start))
+        return out
+
+    def getTrackList(self) -> List[TrackView]:
+        levels = self.hls.levels
+        if not levels:
+            return []
+        tracks = []
+        for i, level in enumerate(levels):
+            for j in range(len(level.url)):
+                tracks.append(TrackView(level=i, urlId=j))
+        return tracks
+
+    def getSegmentDuration(self, segmentView: SegmentView) -> Any:
+        level = self._level(segmentView.trackView.level)
+        for fragment in level.details.fragments:
+            return fragment.duration
+        raise Exception("All segments should have a duration")
+
+    # python aliases
+    get_segment_time = getSegmentTime
+    get_segment_list = getSegmentList
+    get_track_list = getTrackList
+    get_segment_duration = getSegmentDuration

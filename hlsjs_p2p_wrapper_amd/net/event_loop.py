@@ -1,0 +1,232 @@
+"""Single-threaded timer loop: the ``setTimeout`` / ``performance.now()`` platform (L0).
+
+The reference is browser JavaScript: everything asynchronous — the per-attempt request
+timeout (``lib/integration/p2p-loader-generator.js:163``), the exponential-backoff retry
+(``:114-120``), the stream controller's tick, the peer agent's scheduler — hangs off the
+browser's timer queue, and every loader timestamp comes from ``performance.now()``
+(``:77,98,181``).  This module is that platform for the MI355X engine.
+
+Two clocks:
+
+* ``clock="real"``    — ``time.perf_counter`` in milliseconds; timers fire when due.  Used
+  by ``bench.py`` and production players.
+* ``clock="virtual"`` — a discrete-event clock: when no callback is ready the loop *jumps*
+  to the next timer.  Tests run minutes of playback (retries with 64 s back-off, live
+  playlist refreshes) in milliseconds, deterministically.
+
+One loop per thread (``get_event_loop()``), mirroring the one-timer-queue-per-tab model;
+the in-process multi-peer swarm test runs one peer per thread.
+"""
+from __future__ import annotations
+
+import heapq
+import itertools
+import threading
+import time
+from typing import Any, Callable, List, Optional, Tuple
+
+
+class TimerHandle:
+    __slots__ = ("when", "seq", "fn", "args", "cancelled", "interval")
+
+    def __init__(self, when: float, seq: int, fn: Callable[..., Any], args: tuple,
+                 interval: Optional[float] = None) -> None:
+        self.when = when
+        self.seq = seq
+        self.fn = fn
+        self.args = args
+        self.cancelled = False
+        self.interval = interval
+
+    def cancel(self) -> None:
+        self.cancelled = True
+
+    def __lt__(self, other: "TimerHandle") -> bool:  # heap order
+        return (self.when, self.seq) < (other.when, other.seq)
+
+
+class EventLoop:
+    """Timer queue with a real or virtual millisecond clock."""
+
+    def __init__(self, clock: str = "real") -> None:
+        if clock not in ("real", "virtual"):
+            raise ValueError("clock must be 'real' or 'virtual'")
+        self.clock = clock
+        self._t0 = time.perf_counter()
+        self._vnow = 0.0
+        self._heap: List[TimerHandle] = []
+        self._ready: List[Tuple[Callable[..., Any], tuple]] = []
+        self._seq = itertools.count()
+        self._idle_hooks: List[Callable[[], bool]] = []
+
+    # ------------------------------------------------------------------ clock
+    def now(self) -> float:
+        """``performance.now()``: milliseconds since loop creation."""
+        if self.clock == "virtual":
+            return self._vnow
+        return (time.perf_counter() - self._t0) * 1000.0
+
+    performance_now = now
+
+    def advance(self, ms: float) -> None:
+        """Virtual clock only: move time forward without running callbacks."""
+        if self.clock != "virtual":
+            raise RuntimeError("advance() needs a virtual clock")
+        self._vnow += max(0.0, float(ms))
+
+    # ----------------------------------------------------------------- timers
+    def set_timeout(self, fn: Callable[..., Any], delay_ms: float = 0.0, *args: Any) -> TimerHandle:
+        delay = 0.0 if delay_ms is None else max(0.0, float(delay_ms))
+        h = TimerHandle(self.now() + delay, next(self._seq), fn, args)
+        heapq.heappush(self._heap, h)
+        return h
+
+    setTimeout = set_timeout
+
+    def set_interval(self, fn: Callable[..., Any], interval_ms: float, *args: Any) -> TimerHandle:
+        interval = max(0.0, float(interval_ms))
+        h = TimerHandle(self.now() + interval, next(self._seq), fn, args, interval)
+        heapq.heappush(self._heap, h)
+        return h
+
+    setInterval = set_interval
+
+    @staticmethod
+    def clear_timeout(handle: Optional[TimerHandle]) -> None:
+        if handle is not None:
+            handle.cancel()
+
+    clearTimeout = clear_timeout
+    clear_interval = clear_timeout
+    clearInterval = clear_timeout
+
+    def call_soon(self, fn: Callable[..., Any], *args: Any) -> None:
+        self._ready.append((fn, args))
+
+    def add_idle_hook(self, hook: Callable[[], bool]) -> None:
+        """``hook()`` runs when the loop would otherwise sleep; returns True if it did work."""
+        self._idle_hooks.append(hook)
+
+    def remove_idle_hook(self, hook: Callable[[], bool]) -> None:
+        try:
+            self._idle_hooks.remove(hook)
+        except ValueError:
+            pass
+
+    # ---------------------------------------------------------------- running
+    def _pop_due(self, now: float) -> Optional[TimerHandle]:
+        heap = self._heap
+        while heap:
+            h = heap[0]
+            if h.cancelled:
+                heapq.heappop(heap)
+                continue
+            if h.when <= now:
+                heapq.heappop(heap)
+                return h
+            return None
+        return None
+
+    def _next_deadline(self) -> Optional[float]:
+        heap = self._heap
+        while heap and heap[0].cancelled:
+            heapq.heappop(heap)
+        return heap[0].when if heap else None
+
+    def _fire(self, h: TimerHandle) -> None:
+        if h.interval is not None and not h.cancelled:
+            h.when = max(h.when + h.interval, self.now()) if self.clock == "real" else h.when + h.interval
+            h.seq = next(self._seq)
+            heapq.heappush(self._heap, h)
+        h.fn(*h.args)
+
+    def run_once(self, block: bool = True, max_wait_ms: float = 50.0) -> bool:
+        """Run ready callbacks and due timers.  Returns False when nothing is left."""
+        did = False
+        if self._ready:
+            ready, self._ready = self._ready, []
+            for fn, args in ready:
+                fn(*args)
+            did = True
+        now = self.now()
+        h = self._pop_due(now)
+        while h is not None:
+            self._fire(h)
+            did = True
+            if self._ready:
+                return True
+            h = self._pop_due(self.now())
+        if did:
+            return True
+        for hook in tuple(self._idle_hooks):
+            if hook():
+                did = True
+        if did:
+            return True
+        deadline = self._next_deadline()
+        if deadline is None:
+            return bool(self._ready)
+        if self.clock == "virtual":
+            self._vnow = max(self._vnow, deadline)
+            return True
+        if block:
+            wait = min(max(0.0, deadline - self.now()), max_wait_ms) / 1000.0
+            if wait > 0:
+                time.sleep(wait)
+        return True
+
+    def run_until(self, predicate: Callable[[], bool], timeout_ms: float = 60_000.0) -> bool:
+        """Run until ``predicate()`` is true or ``timeout_ms`` of loop time elapses."""
+        end = self.now() + timeout_ms
+        while not predicate():
+            if self.now() >= end:
+                return False
+            if self.clock == "virtual":
+                nd = self._next_deadline()
+                if not self._ready and nd is not None and nd > end and not self._idle_hooks:
+                    self._vnow = end
+                    return predicate()
+            if not self.run_once():
+                return predicate()
+        return True
+
+    def run_for(self, duration_ms: float) -> None:
+        end = self.now() + duration_ms
+        self.run_until(lambda: self.now() >= end, timeout_ms=duration_ms + 1.0)
+
+    def pending(self) -> int:
+        return len(self._ready) + sum(1 for h in self._heap if not h.cancelled)
+
+
+_local = threading.local()
+
+
+def get_event_loop() -> EventLoop:
+    """The calling thread's loop (created on first use with a real clock)."""
+    loop = getattr(_local, "loop", None)
+    if loop is None:
+        loop = EventLoop("real")
+        _local.loop = loop
+    return loop
+
+
+def set_event_loop(loop: Optional[EventLoop]) -> None:
+    _local.loop = loop
+
+
+def new_event_loop(clock: str = "real") -> EventLoop:
+    loop = EventLoop(clock)
+    set_event_loop(loop)
+    return loop
+
+
+def performance_now() -> float:
+    return get_event_loop().now()
+
+
+def set_timeout(fn: Callable[..., Any], delay_ms: float = 0.0, *args: Any) -> TimerHandle:
+    return get_event_loop().set_timeout(fn, delay_ms, *args)
+
+
+def clear_timeout(handle: Optional[TimerHandle]) -> None:
+    EventLoop.clear_timeout(handle)

@@ -1,0 +1,130 @@
+"""The "HTTP" layer: URL -> origin resolution, responses, errors, bandwidth shaping.
+
+There is no network on an MI355X node's data path: the CDN is modelled by in-process
+*origins* (:mod:`.origin`) registered under URL prefixes, holding playlists as text and
+segments in pinned host memory.  :func:`fetch` resolves a URL (with an optional
+``Range: bytes=s-e`` header, inclusive end as in HTTP — the P2P loader converts hls.js's
+exclusive ``byteRangeEndOffset``, ``lib/integration/p2p-loader-generator.js:142-144``).
+
+:class:`Shaper` reproduces the xhr-shaper global the reference's browser tests use to
+throttle and inject latency (``test/html/tests.js:6``, ``p2p-loader-generator.js:37``):
+``Shaper.maxBandwidth`` is in kbit/s (``inf`` = unshaped) and ``Shaper.minLatency`` in ms.
+"""
+from __future__ import annotations
+
+import math
+import re
+import threading
+from dataclasses import dataclass
+from typing import Any, Dict, List, Optional, Tuple
+
+
+class HttpError(Exception):
+    """Error delivered to loaders; the reference expects an object with ``status``
+    (``CHANGELOG.md:17-18`` "Expect HttpError instance passed in loadError callback")."""
+
+    def __init__(self, status: int, url: str = "", message: str = "") -> None:
+        super().__init__(message or f"HTTP {status} for {url}")
+        self.status = status
+        self.url = url
+
+
+@dataclass
+class Response:
+    status: int
+    body: Any              # str (text) or a uint8 view (numpy / torch CPU tensor)
+    url: str
+    length: int
+    source: Any = None     # (origin, resource) for zero-copy device fetches
+    offset: int = 0        # byte offset inside the resource for range requests
+
+
+class Shaper:
+    """Process-wide request shaping (xhr-shaper analog)."""
+
+    maxBandwidth: float = math.inf  # kbit/s
+    minLatency: float = 0.0         # ms
+
+    @classmethod
+    def reset(cls) -> None:
+        cls.maxBandwidth = math.inf
+        cls.minLatency = 0.0
+
+    @classmethod
+    def transfer_ms(cls, nbytes: int) -> float:
+        """Wall time a transfer of ``nbytes`` takes under the current shaping."""
+        t = float(cls.minLatency)
+        if math.isfinite(cls.maxBandwidth) and cls.maxBandwidth > 0:
+            t += nbytes * 8.0 / cls.maxBandwidth  # kbit/s == bit/ms
+        return t
+
+
+_registry: Dict[str, Any] = {}
+_reg_lock = threading.Lock()
+
+
+def register_origin(base_url: str, origin: Any) -> None:
+    if not base_url.endswith("/"):
+        base_url += "/"
+    with _reg_lock:
+        _registry[base_url] = origin
+
+
+def unregister_origin(base_url: str) -> None:
+    if not base_url.endswith("/"):
+        base_url += "/"
+    with _reg_lock:
+        _registry.pop(base_url, None)
+
+
+def clear_origins() -> None:
+    with _reg_lock:
+        _registry.clear()
+
+
+def resolve(url: str) -> Tuple[Any, str]:
+    best = None
+    for base, origin in list(_registry.items()):
+        if url.startswith(base) and (best is None or len(base) > len(best[0])):
+            best = (base, origin)
+    if best is None:
+        raise HttpError(0, url, f"no origin serves {url}")  # status 0 = network error
+    return best[1], url[len(best[0]):]
+
+
+_RANGE = re.compile(r"bytes=(\d+)-(\d*)")
+
+
+def parse_range(headers: Optional[Dict[str, str]]) -> Optional[Tuple[int, Optional[int]]]:
+    if not headers:
+        return None
+    v = headers.get("Range") or headers.get("range")
+    if not v:
+        return None
+    m = _RANGE.fullmatch(v.strip())
+    if not m:
+        raise HttpError(416, "", f"bad range {v!r}")
+    start = int(m.group(1))
+    end = int(m.group(2)) if m.group(2) else None
+    return start, end
+
+
+def fetch(url: str, headers: Optional[Dict[str, str]] = None, with_credentials: bool = False) -> Response:
+    """Synchronous origin fetch (the transfer time is modelled by the caller)."""
+    origin, path = resolve(url)
+    rng = parse_range(headers)
+    return origin.serve(path, url, rng, headers or {}, with_credentials)
+
+
+def head(url: str, headers: Optional[Dict[str, str]] = None) -> int:
+    """Size of a resource (or of the requested range) without transferring it."""
+    origin, path = resolve(url)
+    rng = parse_range(headers)
+    return origin.size(path, url, rng)
+
+
+def request_log() -> List[Tuple[str, str]]:
+    out = []
+    for base, origin in list(_registry.items()):
+        out.extend((base, p) for p in getattr(origin, "requests", []))
+    return out

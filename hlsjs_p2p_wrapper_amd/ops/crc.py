@@ -1,0 +1,97 @@
+"""CRC-32 (zlib) integrity check of segment payloads on the MFMA cores.
+
+Every segment that enters a node (CDN fetch or peer transfer) is checksummed on device;
+peer transfers carry the sender's CRC and the receiver compares on device, so corrupted
+bytes from a peer are caught before the player sees them (fault injection: §5.3).
+
+Device path: ``kernels/crc32_mfma.hip`` (``v_mfma_i32_32x32x32_i8`` GF(2) products +
+shift-operator combine).  CPU path: slice-by-8 host oracle (== ``zlib.crc32``).
+"""
+from __future__ import annotations
+
+import threading
+from typing import Dict, Optional, Sequence, Tuple
+
+import numpy as np
+import torch
+
+from ._native import device as _dev
+from ._native import runtime as _rt
+from .desc import pack_to_device
+
+_consts: Dict[str, tuple] = {}
+_lock = threading.Lock()
+
+
+def _device_consts(device: torch.device):
+    k = str(device)
+    c = _consts.get(k)
+    if c is None:
+        rt = _rt()
+        w = torch.from_numpy(rt.crc_mfma_weights()).to(device)
+        t = torch.from_numpy(rt.crc_shift_tables().view(np.int32)).to(device)
+        c = (w, t)
+        with _lock:
+            _consts[k] = c
+    return c
+
+
+def crc32_batch(buf: torch.Tensor, offs: Sequence[int], lens: Sequence[int],
+                expect: Optional[Sequence[int]] = None,
+                expect_dev: Optional[torch.Tensor] = None) -> Tuple[torch.Tensor, Optional[torch.Tensor]]:
+    """CRC-32 of ``buf[offs[i]:offs[i]+lens[i]]``.
+
+    Returns ``(crc int32[B], ok uint8[B] | None)`` on ``buf.device``; ``ok`` is produced
+    when expected values are given (host list ``expect`` or device tensor ``expect_dev``).
+    """
+    B = len(offs)
+    o = np.asarray(offs, dtype=np.int64)
+    n = np.asarray(lens, dtype=np.int64)
+    if B == 0:
+        z = torch.empty(0, dtype=torch.int32, device=buf.device)
+        return z, (torch.empty(0, dtype=torch.uint8, device=buf.device) if (expect is not None or expect_dev is not None) else None)
+    if np.any(o < 0) or np.any(n < 0) or np.any(o + n > buf.numel()):
+        raise ValueError("crc32_batch: range out of bounds")
+    if buf.device.type == "cpu":
+        crc = _rt().crc32_batch(buf.numpy(), o, n).view(np.int32)
+        crc_t = torch.from_numpy(crc.copy())
+        ok = None
+        if expect_dev is not None:
+            ok = (crc_t == expect_dev.to(torch.int32)).to(torch.uint8)
+        elif expect is not None:
+            exp = np.asarray(expect, dtype=np.uint32).view(np.int32)
+            ok = torch.from_numpy((crc == exp).astype(np.uint8))
+        return crc_t, ok
+    if np.any(o % 16):
+        raise ValueError("crc32_batch: offsets must be 16-byte aligned on device")
+    groups = (n + 255) // 256
+    tiles = (groups + 31) // 32
+    tile_prefix = np.zeros(B + 1, dtype=np.int64)
+    np.cumsum(tiles, out=tile_prefix[1:])
+    res_off = np.zeros(B, dtype=np.int64)
+    if B > 1:
+        np.cumsum(groups[:-1], out=res_off[1:])
+    arrays = {"o": o, "n": n, "tp": tile_prefix, "ro": res_off}
+    if expect is not None and expect_dev is None:
+        arrays["ex"] = np.asarray(expect, dtype=np.uint32)
+    d = pack_to_device(arrays, buf.device)
+    w, tables = _device_consts(buf.device)
+    residues = torch.empty(max(1, int(groups.sum())), dtype=torch.int32, device=buf.device)
+    crc = torch.empty(B, dtype=torch.int32, device=buf.device)
+    exp_t = expect_dev if expect_dev is not None else d.get("ex")
+    ok = torch.empty(B, dtype=torch.uint8, device=buf.device) if exp_t is not None else None
+    _dev().crc32_batch(buf, d["o"], d["n"], d["tp"], d["ro"], w, tables, residues, crc, exp_t, ok,
+                       int(tile_prefix[-1]))
+    return crc, ok
+
+
+def crc32(data) -> int:
+    """Host CRC-32 of bytes / numpy / CPU tensor (== zlib.crc32)."""
+    if isinstance(data, torch.Tensor):
+        data = data.detach().cpu().numpy()
+    arr = np.frombuffer(data, dtype=np.uint8) if isinstance(data, (bytes, bytearray, memoryview)) else np.asarray(data, dtype=np.uint8)
+    return int(_rt().crc32(np.ascontiguousarray(arr)))
+
+
+def to_u32(x: int) -> int:
+    return int(x) & 0xFFFFFFFF

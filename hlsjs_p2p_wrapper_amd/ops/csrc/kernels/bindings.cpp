@@ -1,0 +1,222 @@
+// torch binding module `_C`: argument checking + current-HIP-stream launch of the gfx950
+// kernels.  Host-only translation unit; kernels live in *.hip objects.
+#include <c10/hip/HIPStream.h>
+#include <hip/hip_runtime_api.h>
+#include <torch/extension.h>
+
+namespace hlsp2p {
+namespace dev {
+hipError_t launch_aes128_cbc_decrypt(const uint8_t*, uint8_t*, const int64_t*, const int64_t*, const int64_t*,
+                                     const uint32_t*, const uint32_t*, const uint32_t*, const uint8_t*, int64_t*, int,
+                                     int64_t, int, hipStream_t);
+hipError_t launch_crc32_batch(const uint8_t*, const int64_t*, const int64_t*, const int64_t*, const int64_t*,
+                              const void*, const uint32_t*, uint32_t*, uint32_t*, const uint32_t*, uint8_t*, int,
+                              int64_t, int, hipStream_t);
+hipError_t launch_ts_demux(const uint8_t*, const int64_t*, const int64_t*, const int64_t*, int, int64_t, uint32_t*,
+                           int64_t*, int32_t*, uint8_t*, const int64_t*, int64_t*, int64_t, int64_t*, hipStream_t);
+hipError_t launch_range_select(const double*, const int64_t*, const int64_t*, const double*, const double*, int64_t*,
+                               int64_t*, int64_t, int64_t, hipStream_t);
+hipError_t launch_key_hash(const int32_t*, uint64_t*, int64_t, hipStream_t);
+hipError_t launch_table_insert(void*, uint64_t, const int32_t*, const int64_t*, int64_t, int32_t*, hipStream_t);
+hipError_t launch_table_lookup(const void*, uint64_t, const int32_t*, int64_t*, int64_t, int, hipStream_t);
+hipError_t launch_segment_copy(const uint8_t*, uint8_t*, const int64_t*, const int64_t*, const int64_t*,
+                               const int64_t*, int, int64_t, hipStream_t);
+}  // namespace dev
+}  // namespace hlsp2p
+
+namespace {
+
+using torch::Tensor;
+namespace D = hlsp2p::dev;
+
+void check(const Tensor& t, const char* name, c10::ScalarType dt, int64_t min_numel = 0) {
+  TORCH_CHECK(t.is_cuda(), name, " must be a GPU tensor");
+  TORCH_CHECK(t.is_contiguous(), name, " must be contiguous");
+  TORCH_CHECK(t.scalar_type() == dt, name, " has dtype ", t.scalar_type(), ", expected ", dt);
+  TORCH_CHECK(t.numel() >= min_numel, name, " too small: ", t.numel(), " < ", min_numel);
+}
+
+void same_device(const Tensor& a, const Tensor& b) {
+  TORCH_CHECK(a.device() == b.device(), "tensors on different devices");
+}
+
+hipStream_t stream() { return c10::hip::getCurrentHIPStream().stream(); }
+
+void ok(hipError_t e, const char* what) {
+  TORCH_CHECK(e == hipSuccess, what, " launch failed: ", hipGetErrorString(e));
+}
+
+int num_cus(const Tensor& t) {
+  static int cached[64] = {0};
+  const int dev = t.get_device();
+  if (dev >= 0 && dev < 64 && cached[dev]) return cached[dev];
+  int n = 0;
+  hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev);
+  if (n <= 0) n = 256;
+  if (dev >= 0 && dev < 64) cached[dev] = n;
+  return n;
+}
+
+template <typename T>
+const T* cptr(const Tensor& t) { return reinterpret_cast<const T*>(t.data_ptr()); }
+template <typename T>
+T* mptr(const Tensor& t) { return reinterpret_cast<T*>(t.data_ptr()); }
+
+void aes128_cbc_decrypt(Tensor src, Tensor dst, Tensor src_off, Tensor dst_off, Tensor blk_prefix, Tensor drk,
+                        Tensor iv, Tensor td0, Tensor isb, Tensor out_len, int64_t total_blocks) {
+  const int64_t B = src_off.numel();
+  check(src, "src", torch::kUInt8);
+  check(dst, "dst", torch::kUInt8);
+  check(src_off, "src_off", torch::kInt64);
+  check(dst_off, "dst_off", torch::kInt64, B);
+  check(blk_prefix, "blk_prefix", torch::kInt64, B + 1);
+  check(drk, "drk", torch::kInt32, B * 44);
+  check(iv, "iv", torch::kUInt8, B * 16);
+  check(td0, "td0", torch::kInt32, 256);
+  check(isb, "isb", torch::kUInt8, 256);
+  check(out_len, "out_len", torch::kInt64, B);
+  TORCH_CHECK(src.data_ptr() != dst.data_ptr(), "CBC decrypt cannot run in place");
+  TORCH_CHECK((reinterpret_cast<uintptr_t>(src.data_ptr()) & 15) == 0 &&
+                  (reinterpret_cast<uintptr_t>(dst.data_ptr()) & 15) == 0,
+              "src/dst must be 16-byte aligned");
+  same_device(src, dst);
+  ok(D::launch_aes128_cbc_decrypt(cptr<uint8_t>(src), mptr<uint8_t>(dst), cptr<int64_t>(src_off),
+                                  cptr<int64_t>(dst_off), cptr<int64_t>(blk_prefix), cptr<uint32_t>(drk),
+                                  cptr<uint32_t>(iv), cptr<uint32_t>(td0), cptr<uint8_t>(isb), mptr<int64_t>(out_len),
+                                  static_cast<int>(B), total_blocks, num_cus(src), stream()),
+     "aes128_cbc_decrypt");
+}
+
+void crc32_batch(Tensor buf, Tensor seg_off, Tensor seg_len, Tensor tile_prefix, Tensor res_off, Tensor wfrag,
+                 Tensor tables, Tensor residues, Tensor crc_out, c10::optional<Tensor> expect,
+                 c10::optional<Tensor> ok_out, int64_t total_tiles) {
+  const int64_t B = seg_off.numel();
+  check(buf, "buf", torch::kUInt8);
+  check(seg_off, "seg_off", torch::kInt64);
+  check(seg_len, "seg_len", torch::kInt64, B);
+  check(tile_prefix, "tile_prefix", torch::kInt64, B + 1);
+  check(res_off, "res_off", torch::kInt64, B);
+  check(wfrag, "wfrag", torch::kInt8, 64 * 64 * 16);
+  check(tables, "tables", torch::kInt32, 48 * 1024);
+  check(residues, "residues", torch::kInt32);
+  check(crc_out, "crc_out", torch::kInt32, B);
+  TORCH_CHECK((reinterpret_cast<uintptr_t>(buf.data_ptr()) & 15) == 0, "buf must be 16-byte aligned");
+  const uint32_t* ex = nullptr;
+  uint8_t* okp = nullptr;
+  if (expect.has_value()) {
+    check(*expect, "expect", torch::kInt32, B);
+    ex = cptr<uint32_t>(*expect);
+  }
+  if (ok_out.has_value()) {
+    check(*ok_out, "ok_out", torch::kUInt8, B);
+    okp = mptr<uint8_t>(*ok_out);
+  }
+  ok(D::launch_crc32_batch(cptr<uint8_t>(buf), cptr<int64_t>(seg_off), cptr<int64_t>(seg_len),
+                           cptr<int64_t>(tile_prefix), cptr<int64_t>(res_off), wfrag.data_ptr(),
+                           cptr<uint32_t>(tables), mptr<uint32_t>(residues), mptr<uint32_t>(crc_out), ex, okp,
+                           static_cast<int>(B), total_tiles, num_cus(buf), stream()),
+     "crc32_batch");
+}
+
+void ts_demux(Tensor buf, Tensor seg_off, Tensor seg_len, Tensor blk_prefix, int64_t total_blocks, Tensor meta,
+              Tensor pts_dts, Tensor blk_sums, Tensor es, Tensor es_off, Tensor pes, int64_t max_pes, Tensor info) {
+  const int64_t B = seg_off.numel();
+  check(buf, "buf", torch::kUInt8);
+  check(seg_off, "seg_off", torch::kInt64);
+  check(seg_len, "seg_len", torch::kInt64, B);
+  check(blk_prefix, "blk_prefix", torch::kInt64, B + 1);
+  check(meta, "meta", torch::kInt32, total_blocks * 256);
+  check(pts_dts, "pts_dts", torch::kInt64, total_blocks * 256 * 2);
+  check(blk_sums, "blk_sums", torch::kInt32, total_blocks * 6);
+  check(es, "es", torch::kUInt8);
+  check(es_off, "es_off", torch::kInt64, B);
+  check(pes, "pes", torch::kInt64, B * 3 * max_pes * 3);
+  check(info, "info", torch::kInt64, B * 16);
+  TORCH_CHECK((reinterpret_cast<uintptr_t>(buf.data_ptr()) & 3) == 0, "buf must be 4-byte aligned");
+  ok(D::launch_ts_demux(cptr<uint8_t>(buf), cptr<int64_t>(seg_off), cptr<int64_t>(seg_len),
+                        cptr<int64_t>(blk_prefix), static_cast<int>(B), total_blocks, mptr<uint32_t>(meta),
+                        mptr<int64_t>(pts_dts), mptr<int32_t>(blk_sums), mptr<uint8_t>(es), cptr<int64_t>(es_off),
+                        mptr<int64_t>(pes), max_pes, mptr<int64_t>(info), stream()),
+     "ts_demux");
+}
+
+void range_select(Tensor starts, Tensor track_off, Tensor q_track, Tensor q_begin, Tensor q_dur, Tensor out_lo,
+                  Tensor out_hi) {
+  const int64_t nq = q_track.numel();
+  check(starts, "starts", torch::kFloat64);
+  check(track_off, "track_off", torch::kInt64, 1);
+  check(q_track, "q_track", torch::kInt64);
+  check(q_begin, "q_begin", torch::kFloat64, nq);
+  check(q_dur, "q_dur", torch::kFloat64, nq);
+  check(out_lo, "out_lo", torch::kInt64, nq);
+  check(out_hi, "out_hi", torch::kInt64, nq);
+  ok(D::launch_range_select(cptr<double>(starts), cptr<int64_t>(track_off), cptr<int64_t>(q_track),
+                            cptr<double>(q_begin), cptr<double>(q_dur), mptr<int64_t>(out_lo), mptr<int64_t>(out_hi),
+                            nq, track_off.numel() - 1, stream()),
+     "range_select");
+}
+
+void key_hash(Tensor keys, Tensor out) {
+  const int64_t n = keys.numel() / 4;
+  check(keys, "keys", torch::kInt32);
+  check(out, "out", torch::kInt64, n);
+  ok(D::launch_key_hash(cptr<int32_t>(keys), mptr<uint64_t>(out), n, stream()), "key_hash");
+}
+
+void table_insert(Tensor slots, Tensor keys, Tensor values, Tensor ok_out) {
+  const int64_t n = keys.numel() / 4;
+  check(slots, "slots", torch::kInt64);
+  check(keys, "keys", torch::kInt32);
+  check(values, "values", torch::kInt64, n);
+  check(ok_out, "ok", torch::kInt32, n);
+  const int64_t cap = slots.numel() / 4;
+  TORCH_CHECK(cap > 0 && (cap & (cap - 1)) == 0, "slot count must be a power of two");
+  ok(D::launch_table_insert(slots.data_ptr(), static_cast<uint64_t>(cap - 1), cptr<int32_t>(keys),
+                            cptr<int64_t>(values), n, mptr<int32_t>(ok_out), stream()),
+     "table_insert");
+}
+
+void table_lookup(Tensor slots, Tensor keys, Tensor out, bool erase) {
+  const int64_t n = keys.numel() / 4;
+  check(slots, "slots", torch::kInt64);
+  check(keys, "keys", torch::kInt32);
+  check(out, "out", torch::kInt64, n);
+  const int64_t cap = slots.numel() / 4;
+  TORCH_CHECK(cap > 0 && (cap & (cap - 1)) == 0, "slot count must be a power of two");
+  ok(D::launch_table_lookup(slots.data_ptr(), static_cast<uint64_t>(cap - 1), cptr<int32_t>(keys), mptr<int64_t>(out),
+                            n, erase ? 1 : 0, stream()),
+     "table_lookup");
+}
+
+void segment_copy(Tensor src, Tensor dst, Tensor src_off, Tensor dst_off, Tensor len, Tensor chunk_prefix,
+                  int64_t total_chunks) {
+  const int64_t n = src_off.numel();
+  check(src, "src", torch::kUInt8);
+  check(dst, "dst", torch::kUInt8);
+  check(src_off, "src_off", torch::kInt64);
+  check(dst_off, "dst_off", torch::kInt64, n);
+  check(len, "len", torch::kInt64, n);
+  check(chunk_prefix, "chunk_prefix", torch::kInt64, n + 1);
+  ok(D::launch_segment_copy(cptr<uint8_t>(src), mptr<uint8_t>(dst), cptr<int64_t>(src_off), cptr<int64_t>(dst_off),
+                            cptr<int64_t>(len), cptr<int64_t>(chunk_prefix), static_cast<int>(n), total_chunks,
+                            stream()),
+     "segment_copy");
+}
+
+int64_t device_cus(Tensor t) { return num_cus(t); }
+
+}  // namespace
+
+PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
+  m.doc() = "hlsjs-p2p-wrapper-amd CDNA4 (gfx950) kernels";
+  m.def("aes128_cbc_decrypt", &aes128_cbc_decrypt);
+  m.def("crc32_batch", &crc32_batch);
+  m.def("ts_demux", &ts_demux);
+  m.def("range_select", &range_select);
+  m.def("key_hash", &key_hash);
+  m.def("table_insert", &table_insert);
+  m.def("table_lookup", &table_lookup);
+  m.def("segment_copy", &segment_copy);
+  m.def("device_cus", &device_cus);
+  m.attr("ARCH") = "gfx950";
+}

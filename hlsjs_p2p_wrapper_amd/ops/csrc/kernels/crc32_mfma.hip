@@ -1,0 +1,199 @@
+// CRC-32 (zlib) of a batch of segments on the MFMA matrix cores.
+//
+// CRC is linear over GF(2).  For a 256-byte group g, its zero-init register contribution
+// is a 32-bit vector r_g = W^T bits(g) (mod 2) with W a fixed 2048 x 32 binary matrix.
+// Integer accumulation followed by "& 1" equals the GF(2) sum, so the 8-bit integer MFMA
+// computes 32 groups x 32 CRC bits per wave tile:
+//
+//     D[32 groups][32 bits] += A[32 groups][32 k] * B[32 k][32 bits]   (i8 -> i32)
+//     v_mfma_i32_32x32x32_i8, 64 k-steps per 256-byte group (k = 2048 data bits)
+//
+// Layout choice (so no LDS transpose of the data is needed): lane l = (row r = l & 31,
+// half h = l >> 5) owns bytes [128h, 128h + 128) of group r and loads them with 8
+// dwordx4 loads; at k-step s it expands its 2 bytes (2s, 2s+1) into 16 int8 {0,1}
+// (nibble * 0x00204081 & 0x01010101: 3 VALU per 4 bits).  The B fragment for the same
+// 16 k's — W rows in exactly that (s, h, j) order — is precomputed on the host
+// (runtime/crc_host.cpp) in MFMA fragment order, 64 KiB, staged once per workgroup in LDS
+// and read with one ds_read_b128 per lane per step.  Because A and B use the same k
+// permutation the product is independent of the MFMA's internal k ordering.
+//
+// The 16 accumulator registers hold rows (i&3)+8(i>>2)+4h, column = lane&31 (gfx950 C/D
+// map); a wave ballot of the parity bits yields two 32-bit group residues per register.
+// A second kernel (one workgroup per segment) folds the residues with GF(2) shift
+// operators (byte-slice tables in LDS): Horner over runs of groups, then a log tree, then
+// it undoes the zero padding of the last group (A^-8p) and adds the init/xor-out terms.
+// Result is bit-identical to zlib.crc32.
+#include "common.h"
+
+namespace hlsp2p {
+namespace dev {
+
+typedef int v4i __attribute__((ext_vector_type(4)));
+typedef int v16i __attribute__((ext_vector_type(16)));
+
+constexpr int kCrcThreads = 256;  // 4 waves, each owns 8 KiB tiles
+constexpr int kTileBytes = 32 * 256;
+constexpr int kNumP = 40;
+constexpr int kSlice = 1024;  // u32 per byte-slice table set
+
+__device__ __forceinline__ uint32_t expand_nibble(uint32_t nib) { return (nib * 0x00204081u) & 0x01010101u; }
+
+__global__ __launch_bounds__(kCrcThreads, 2) void crc32_group_residue_kernel(
+    const uint8_t* __restrict__ buf, const int64_t* __restrict__ seg_off, const int64_t* __restrict__ seg_len,
+    const int64_t* __restrict__ tile_prefix, const int64_t* __restrict__ res_off, const v4i* __restrict__ wfrag,
+    uint32_t* __restrict__ residues, int nseg, int64_t total_tiles, int64_t tiles_per_wave) {
+  __shared__ v4i s_w[64 * 64];  // 64 KiB: [step][lane] fragments
+  const int tid = threadIdx.x;
+  for (int i = tid; i < 64 * 64; i += kCrcThreads) s_w[i] = wfrag[i];
+  __syncthreads();
+
+  const int lane = tid & 63;
+  const int wave = tid >> 6;
+  const int r = lane & 31, h = lane >> 5;
+  const int64_t gwave = static_cast<int64_t>(blockIdx.x) * (kCrcThreads / 64) + wave;
+  const int64_t t_begin = gwave * tiles_per_wave;
+  const int64_t t_end = t_begin + tiles_per_wave < total_tiles ? t_begin + tiles_per_wave : total_tiles;
+  int seg = -1;
+  int64_t base = 0, len = 0, tstart = 0, tend = 0, roff = 0;
+  for (int64_t t = t_begin; t < t_end; ++t) {
+    if (seg < 0 || t >= tend) {
+      seg = seg < 0 ? find_seg(tile_prefix, nseg, t) : advance_seg(tile_prefix, seg, t);
+      base = seg_off[seg];
+      len = seg_len[seg];
+      tstart = tile_prefix[seg];
+      tend = tile_prefix[seg + 1];
+      roff = res_off[seg];
+    }
+    const int64_t tile = t - tstart;
+    const int64_t my = tile * kTileBytes + r * 256 + h * 128;  // byte offset of this lane's 128 B
+    uint32_t d[32];
+    if (my + 128 <= len) {
+      const uint4* p = reinterpret_cast<const uint4*>(buf + base + my);
+#pragma unroll
+      for (int q = 0; q < 8; ++q) {
+        const uint4 v = p[q];
+        d[4 * q] = v.x; d[4 * q + 1] = v.y; d[4 * q + 2] = v.z; d[4 * q + 3] = v.w;
+      }
+    } else {
+#pragma unroll
+      for (int q = 0; q < 32; ++q) {
+        uint32_t w = 0;
+#pragma unroll
+        for (int b = 0; b < 4; ++b) {
+          const int64_t o = my + 4 * q + b;
+          const uint32_t byte = o < len ? buf[base + o] : 0u;
+          w |= byte << (8 * b);
+        }
+        d[q] = w;
+      }
+    }
+    v16i acc = {};
+#pragma unroll
+    for (int s = 0; s < 64; ++s) {
+      const uint32_t bits = (d[s >> 1] >> (16 * (s & 1))) & 0xffffu;
+      v4i a;
+      a.x = static_cast<int>(expand_nibble(bits & 0xf));
+      a.y = static_cast<int>(expand_nibble((bits >> 4) & 0xf));
+      a.z = static_cast<int>(expand_nibble((bits >> 8) & 0xf));
+      a.w = static_cast<int>(expand_nibble(bits >> 12));
+      const v4i b = s_w[s * 64 + lane];
+      acc = __builtin_amdgcn_mfma_i32_32x32x32_i8(a, b, acc, 0, 0, 0);
+    }
+    const int64_t groups = (len + 255) >> 8;
+    const int64_t g0 = tile * 32;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+      const uint64_t m = __ballot(acc[i] & 1);
+      const int row = (i & 3) + 8 * (i >> 2);
+      if (lane == 0) {
+        if (g0 + row < groups) residues[roff + g0 + row] = static_cast<uint32_t>(m);
+        if (g0 + row + 4 < groups) residues[roff + g0 + row + 4] = static_cast<uint32_t>(m >> 32);
+      }
+    }
+  }
+}
+
+__device__ __forceinline__ uint32_t apply_tab(const uint32_t* __restrict__ t, uint32_t v) {
+  return t[v & 0xff] ^ t[256 + ((v >> 8) & 0xff)] ^ t[512 + ((v >> 16) & 0xff)] ^ t[768 + (v >> 24)];
+}
+
+constexpr int kCombineThreads = 1024;
+constexpr int kCombineLdsTables = 15;  // P_8 .. P_22
+
+// One workgroup per segment.  tables: P_0..P_39 then Q_0..Q_7 (each kSlice u32).
+__global__ __launch_bounds__(kCombineThreads) void crc32_combine_kernel(
+    const uint32_t* __restrict__ residues, const int64_t* __restrict__ res_off, const int64_t* __restrict__ seg_len,
+    const uint32_t* __restrict__ tables, uint32_t* __restrict__ crc_out, const uint32_t* __restrict__ expect,
+    uint8_t* __restrict__ ok_out) {
+  __shared__ uint32_t s_tab[kCombineLdsTables * kSlice];  // 60 KiB
+  __shared__ uint32_t s_acc[kCombineThreads];
+  const int seg = blockIdx.x;
+  const int tid = threadIdx.x;
+  const int64_t n = seg_len[seg];
+  const int64_t G = (n + 255) >> 8;
+  // run length L = next pow2 of ceil(G / threads)
+  int lgL = 0;
+  while ((static_cast<int64_t>(kCombineThreads) << lgL) < G) ++lgL;
+  const int lds_tables = 1 + lgL + 10 <= kCombineLdsTables ? 1 + lgL + 10 : kCombineLdsTables;
+  for (int i = tid; i < lds_tables * kSlice; i += kCombineThreads) s_tab[i] = tables[8 * kSlice + i];
+  __syncthreads();
+  const int64_t L = int64_t(1) << lgL;
+  const int64_t span = L * kCombineThreads;
+  const int64_t front = span - G;  // virtual zero groups in front
+  const uint32_t* __restrict__ res = residues + res_off[seg];
+  uint32_t acc = 0;
+  const uint32_t* p8 = s_tab;  // A^(8*256): one group
+  for (int64_t k = 0; k < L; ++k) {
+    const int64_t g = static_cast<int64_t>(tid) * L + k - front;
+    acc = apply_tab(p8, acc) ^ (g >= 0 ? res[g] : 0u);
+  }
+  s_acc[tid] = acc;
+  __syncthreads();
+  // tree: level m merges runs of L*2^m groups: left = A^(8*256*L*2^m) left ^ right
+  for (int m = 0; (1 << m) < kCombineThreads; ++m) {
+    const int stride = 1 << m;
+    const int b = 8 + lgL + m;  // shift of 2^b bytes
+    if ((tid & (2 * stride - 1)) == 0) {
+      const uint32_t* tab = (b - 8) < lds_tables ? s_tab + (b - 8) * kSlice : tables + static_cast<int64_t>(b) * kSlice;
+      s_acc[tid] = apply_tab(tab, s_acc[tid]) ^ s_acc[tid + stride];
+    }
+    __syncthreads();
+  }
+  if (tid == 0) {
+    uint32_t raw = s_acc[0];
+    const int64_t pad = G * 256 - n;
+    for (int b = 0; b < 8; ++b)
+      if ((pad >> b) & 1) raw = apply_tab(tables + static_cast<int64_t>(kNumP + b) * kSlice, raw);
+    uint32_t init = 0xFFFFFFFFu;
+    for (int b = 0; b < kNumP; ++b)
+      if ((n >> b) & 1) init = apply_tab(tables + static_cast<int64_t>(b) * kSlice, init);
+    const uint32_t crc = raw ^ init ^ 0xFFFFFFFFu;
+    crc_out[seg] = crc;
+    if (ok_out) ok_out[seg] = (expect && expect[seg] == crc) ? 1 : 0;
+  }
+}
+
+hipError_t launch_crc32_batch(const uint8_t* buf, const int64_t* seg_off, const int64_t* seg_len,
+                              const int64_t* tile_prefix, const int64_t* res_off, const void* wfrag,
+                              const uint32_t* tables, uint32_t* residues, uint32_t* crc_out, const uint32_t* expect,
+                              uint8_t* ok_out, int nseg, int64_t total_tiles, int num_cu, hipStream_t stream) {
+  if (nseg <= 0) return hipSuccess;
+  if (total_tiles > 0) {
+    const int64_t waves_max = static_cast<int64_t>(num_cu) * 2 * (kCrcThreads / 64);
+    int64_t tiles_per_wave = (total_tiles + waves_max - 1) / waves_max;
+    if (tiles_per_wave < 1) tiles_per_wave = 1;
+    const int64_t waves = (total_tiles + tiles_per_wave - 1) / tiles_per_wave;
+    const int64_t grid = (waves + (kCrcThreads / 64) - 1) / (kCrcThreads / 64);
+    hipLaunchKernelGGL(crc32_group_residue_kernel, dim3(static_cast<unsigned>(grid)), dim3(kCrcThreads), 0, stream,
+                       buf, seg_off, seg_len, tile_prefix, res_off, reinterpret_cast<const v4i*>(wfrag), residues,
+                       nseg, total_tiles, tiles_per_wave);
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return e;
+  }
+  hipLaunchKernelGGL(crc32_combine_kernel, dim3(static_cast<unsigned>(nseg)), dim3(kCombineThreads), 0, stream,
+                     residues, res_off, seg_len, tables, crc_out, expect, ok_out);
+  return hipGetLastError();
+}
+
+}  // namespace dev
+}  // namespace hlsp2p

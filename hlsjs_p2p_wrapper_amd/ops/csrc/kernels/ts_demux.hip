@@ -1,0 +1,372 @@
+// MPEG-TS demux of a batch of decrypted segments — CDNA4 / gfx950.
+//
+// Output contract (identical to the CPU oracle runtime/ts.cpp demux_segment):
+//   es:   per segment, [video ES | audio ES | id3 ES] written at es_off[seg]
+//   pes:  int64[seg][3 classes][max_pes][3] = (ES byte offset, PTS, DTS)  (-1 = absent)
+//   info: int64[seg][16] (status bits, PIDs, packet count, per-class bytes / PES counts)
+//
+// Three launches, no host round trip (segment lengths come from the decrypt kernel's
+// on-device out_len):
+//   1. ts_psi_kernel     — one wave per segment: PAT -> PMT PID, PMT -> ES PIDs/types
+//                          (first 64 packets), zero-inits info / PES tables.
+//   2. ts_scan_kernel    — one lane per 188-byte packet: sync check, PID class, payload
+//                          start/len, PES header (PTS/DTS, header skip); per-256-packet
+//                          block sums of (payload bytes, PES starts) per class.
+//   3. ts_gather_kernel  — same grid: block prefix + in-block wave scans give every
+//                          packet its ES destination; payload copy is done cooperatively
+//                          by the whole wave per packet with dword-aligned stores
+//                          (v_alignbyte funnel for the unaligned source), so each store
+//                          instruction writes up to 256 contiguous bytes.
+#include "common.h"
+
+namespace hlsp2p {
+namespace dev {
+
+constexpr int kPkt = 188;
+constexpr int kTsThreads = 256;
+constexpr int kClasses = 3;
+constexpr int kInfo = 16;
+constexpr int kPsiScan = 64;
+// info slots / status bits (must match runtime/ts.hpp)
+constexpr int kStatus = 0, kPmtPid = 1, kVideoPid = 2, kNumPackets = 5, kBytes0 = 6, kPes0 = 9, kVideoType = 12,
+              kAudioType = 13, kPayloadBytes = 14;
+constexpr int64_t kBadSync = 1, kNoPat = 2, kNoPmt = 4, kPesOverflow = 8, kPesHeaderError = 16, kBadLength = 32;
+
+__device__ __forceinline__ int64_t read_pts(const uint8_t* p) {
+  return (int64_t((p[0] >> 1) & 0x07) << 30) | (int64_t(p[1]) << 22) | (int64_t(p[2] >> 1) << 15) |
+         (int64_t(p[3]) << 7) | int64_t(p[4] >> 1);
+}
+
+__device__ __forceinline__ int64_t seg_length(const int64_t* len_dev, int seg) {
+  const int64_t n = len_dev[seg];
+  return n < 0 ? 0 : n;
+}
+
+// ---------------------------------------------------------------- 1. PSI
+__global__ __launch_bounds__(64) void ts_psi_kernel(const uint8_t* __restrict__ buf, const int64_t* __restrict__ seg_off,
+                                                    const int64_t* __restrict__ seg_len, int64_t* __restrict__ info,
+                                                    int64_t* __restrict__ pes, int64_t max_pes) {
+  const int seg = blockIdx.x;
+  const int lane = threadIdx.x;
+  int64_t* inf = info + static_cast<int64_t>(seg) * kInfo;
+  int64_t* pe = pes + static_cast<int64_t>(seg) * kClasses * max_pes * 3;
+  for (int64_t i = lane; i < static_cast<int64_t>(kClasses) * max_pes * 3; i += 64) pe[i] = -1;
+  if (lane != 0) return;
+  const int64_t raw_len = seg_len[seg];
+  const int64_t n = raw_len < 0 ? 0 : raw_len;
+  const uint8_t* d = buf + seg_off[seg];
+  const int64_t np = n / kPkt;
+  int64_t status = (raw_len < 0 || n % kPkt) ? kBadLength : 0;
+  int pmt_pid = -1, vpid = -1, apid = -1, ipid = -1, vtype = 0, atype = 0;
+  const int64_t scan = np < kPsiScan ? np : kPsiScan;
+  for (int64_t i = 0; i < scan && pmt_pid < 0; ++i) {
+    const uint8_t* p = d + i * kPkt;
+    if (p[0] != 0x47) continue;
+    const int pid = ((p[1] & 0x1f) << 8) | p[2];
+    if (pid != 0 || !(p[1] & 0x40)) continue;
+    const int afc = (p[3] >> 4) & 3;
+    int ps = 4 + ((afc & 2) ? 1 + p[4] : 0);
+    if (!(afc & 1) || ps >= kPkt) continue;
+    ps += 1 + p[ps];
+    if (ps + 8 > kPkt || p[ps] != 0x00) continue;
+    const int slen = ((p[ps + 1] & 0x0f) << 8) | p[ps + 2];
+    const int end = ps + 3 + slen - 4 < kPkt ? ps + 3 + slen - 4 : kPkt;
+    for (int q = ps + 8; q + 4 <= end; q += 4) {
+      const int prog = (p[q] << 8) | p[q + 1];
+      if (prog != 0) {
+        pmt_pid = ((p[q + 2] & 0x1f) << 8) | p[q + 3];
+        break;
+      }
+    }
+  }
+  if (pmt_pid < 0) status |= kNoPat;
+  bool pmt_found = false;
+  for (int64_t i = 0; i < scan && pmt_pid >= 0 && !pmt_found; ++i) {
+    const uint8_t* p = d + i * kPkt;
+    if (p[0] != 0x47) continue;
+    const int pid = ((p[1] & 0x1f) << 8) | p[2];
+    if (pid != pmt_pid || !(p[1] & 0x40)) continue;
+    const int afc = (p[3] >> 4) & 3;
+    int ps = 4 + ((afc & 2) ? 1 + p[4] : 0);
+    if (!(afc & 1) || ps >= kPkt) continue;
+    ps += 1 + p[ps];
+    if (ps + 12 > kPkt || p[ps] != 0x02) continue;
+    pmt_found = true;
+    const int slen = ((p[ps + 1] & 0x0f) << 8) | p[ps + 2];
+    const int end = ps + 3 + slen - 4 < kPkt ? ps + 3 + slen - 4 : kPkt;
+    const int pil = ((p[ps + 10] & 0x0f) << 8) | p[ps + 11];
+    for (int q = ps + 12 + pil; q + 5 <= end;) {
+      const int type = p[q];
+      const int epid = ((p[q + 1] & 0x1f) << 8) | p[q + 2];
+      const int eil = ((p[q + 3] & 0x0f) << 8) | p[q + 4];
+      if ((type == 0x1B || type == 0x24) && vpid < 0) {
+        vpid = epid;
+        vtype = type;
+      } else if ((type == 0x0F || type == 0x03 || type == 0x04) && apid < 0) {
+        apid = epid;
+        atype = type;
+      } else if (type == 0x15 && ipid < 0) {
+        ipid = epid;
+      }
+      q += 5 + eil;
+    }
+  }
+  if (pmt_pid >= 0 && !pmt_found) status |= kNoPmt;
+  for (int k = 0; k < kInfo; ++k) inf[k] = 0;
+  inf[kStatus] = status;
+  inf[kPmtPid] = pmt_pid;
+  inf[kVideoPid] = vpid;
+  inf[kVideoPid + 1] = apid;
+  inf[kVideoPid + 2] = ipid;
+  inf[kNumPackets] = np;
+  inf[kVideoType] = vtype;
+  inf[kAudioType] = atype;
+}
+
+// per-packet meta word: class (2b, 3 = none) | payload start (8b) << 2 | payload len (8b) << 10 | pes (1b) << 18
+__device__ __forceinline__ uint32_t pack_meta(int c, int ps, int len, int pes) {
+  return static_cast<uint32_t>(c & 3) | (static_cast<uint32_t>(ps) << 2) | (static_cast<uint32_t>(len) << 10) |
+         (static_cast<uint32_t>(pes) << 18);
+}
+
+// ---------------------------------------------------------------- 2. scan
+__global__ __launch_bounds__(kTsThreads) void ts_scan_kernel(
+    const uint8_t* __restrict__ buf, const int64_t* __restrict__ seg_off, const int64_t* __restrict__ seg_len,
+    const int64_t* __restrict__ blk_prefix, int nseg, int64_t* __restrict__ info, uint32_t* __restrict__ meta,
+    int64_t* __restrict__ pts_dts, int32_t* __restrict__ blk_sums) {
+  __shared__ int32_t s_sum[2 * kClasses];
+  __shared__ int32_t s_err;
+  const int64_t gblk = blockIdx.x;
+  const int seg = find_seg(blk_prefix, nseg, gblk);  // wave-uniform
+  const int64_t blk = gblk - blk_prefix[seg];
+  const int tid = threadIdx.x;
+  if (tid < 2 * kClasses) s_sum[tid] = 0;
+  if (tid == 0) s_err = 0;
+  __syncthreads();
+  const int64_t* inf = info + static_cast<int64_t>(seg) * kInfo;
+  const int cpid0 = static_cast<int>(inf[kVideoPid]), cpid1 = static_cast<int>(inf[kVideoPid + 1]),
+            cpid2 = static_cast<int>(inf[kVideoPid + 2]);
+  const int64_t np = seg_length(seg_len, seg) / kPkt;
+  const int64_t pk = blk * kTsThreads + tid;
+  const int64_t gpk = gblk * kTsThreads + tid;  // global packet slot (meta index)
+  int c = 3, ps = 0, len = 0, pes = 0;
+  int err = 0;
+  if (pk < np) {
+    const uint8_t* p = buf + seg_off[seg] + pk * kPkt;
+    const uint32_t hdr = *reinterpret_cast<const uint32_t*>(p);  // packets are 4-byte aligned
+    const int sync = hdr & 0xff;
+    const int b1 = (hdr >> 8) & 0xff, b2 = (hdr >> 16) & 0xff, b3 = hdr >> 24;
+    if (sync != 0x47) {
+      err |= static_cast<int>(kBadSync);
+    } else {
+      const int pid = ((b1 & 0x1f) << 8) | b2;
+      const int cls = (cpid0 >= 0 && pid == cpid0) ? 0 : (cpid1 >= 0 && pid == cpid1) ? 1 : (cpid2 >= 0 && pid == cpid2) ? 2 : 3;
+      const int afc = (b3 >> 4) & 3;
+      if (cls < 3 && (afc & 1)) {
+        int s = 4 + ((afc & 2) ? 1 + p[4] : 0);
+        if (s > kPkt) {
+          err |= static_cast<int>(kBadLength);
+        } else {
+          int l = kPkt - s;
+          bool ok = true;
+          if (b1 & 0x40) {
+            const uint8_t* h = p + s;
+            if (l < 9 || h[0] != 0 || h[1] != 0 || h[2] != 1 || 9 + h[8] > l) {
+              err |= static_cast<int>(kPesHeaderError);
+              ok = false;
+            } else {
+              const int64_t pts = ((h[7] & 0x80) && l >= 14) ? read_pts(h + 9) : -1;
+              const int64_t dts = ((h[7] & 0xC0) == 0xC0 && l >= 19) ? read_pts(h + 14) : -1;
+              pts_dts[2 * gpk] = pts;
+              pts_dts[2 * gpk + 1] = dts;
+              pes = 1;
+              s += 9 + h[8];
+              l -= 9 + h[8];
+            }
+          }
+          if (ok) {
+            c = cls;
+            ps = s;
+            len = l;
+          }
+        }
+      }
+    }
+  }
+  meta[gpk] = pack_meta(c, ps, len, pes);
+  // wave-level sums per class, then one LDS atomic per wave per class
+#pragma unroll
+  for (int k = 0; k < kClasses; ++k) {
+    int vb = (c == k) ? len : 0;
+    int vp = (c == k) ? pes : 0;
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+      vb += __shfl_xor(vb, o);
+      vp += __shfl_xor(vp, o);
+    }
+    if ((tid & 63) == 0) {
+      if (vb) atomicAdd(&s_sum[2 * k], vb);
+      if (vp) atomicAdd(&s_sum[2 * k + 1], vp);
+    }
+  }
+  if (err) atomicOr(&s_err, err);
+  __syncthreads();
+  if (tid < 2 * kClasses) blk_sums[gblk * 2 * kClasses + tid] = s_sum[tid];
+  if (tid == 0 && s_err) atomicOr(reinterpret_cast<unsigned long long*>(info + static_cast<int64_t>(seg) * kInfo + kStatus),
+                                  static_cast<unsigned long long>(s_err));
+}
+
+// inclusive wave prefix sum (wave64)
+__device__ __forceinline__ int wave_incl_scan(int v, int lane) {
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const int t = __shfl_up(v, o);
+    if (lane >= o) v += t;
+  }
+  return v;
+}
+
+// ---------------------------------------------------------------- 3. gather
+__global__ __launch_bounds__(kTsThreads) void ts_gather_kernel(
+    const uint8_t* __restrict__ buf, const int64_t* __restrict__ seg_off, const int64_t* __restrict__ seg_len,
+    const int64_t* __restrict__ blk_prefix, int nseg, const uint32_t* __restrict__ meta,
+    const int64_t* __restrict__ pts_dts, const int32_t* __restrict__ blk_sums, uint8_t* __restrict__ es,
+    const int64_t* __restrict__ es_off, int64_t* __restrict__ pes, int64_t max_pes, int64_t* __restrict__ info) {
+  __shared__ int64_t s_tot[2 * kClasses];     // segment totals
+  __shared__ int64_t s_pre[2 * kClasses];     // prefix of blocks before this one
+  __shared__ int32_t s_wave[4][2 * kClasses];  // per-wave totals
+  const int64_t gblk = blockIdx.x;
+  const int seg = find_seg(blk_prefix, nseg, gblk);
+  const int64_t b0 = blk_prefix[seg];
+  const int64_t nblk = blk_prefix[seg + 1] - b0;
+  const int64_t blk = gblk - b0;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  if (tid < 2 * kClasses) {
+    s_tot[tid] = 0;
+    s_pre[tid] = 0;
+  }
+  __syncthreads();
+  {  // segment totals and this block's exclusive prefix (nblk is small: <= ~350 for 16 MB)
+    int64_t tot[2 * kClasses] = {0, 0, 0, 0, 0, 0}, pre[2 * kClasses] = {0, 0, 0, 0, 0, 0};
+    for (int64_t b = tid; b < nblk; b += kTsThreads) {
+      const int32_t* bs = blk_sums + (b0 + b) * 2 * kClasses;
+#pragma unroll
+      for (int k = 0; k < 2 * kClasses; ++k) {
+        tot[k] += bs[k];
+        if (b < blk) pre[k] += bs[k];
+      }
+    }
+#pragma unroll
+    for (int k = 0; k < 2 * kClasses; ++k) {
+      int64_t t = tot[k], p = pre[k];
+#pragma unroll
+      for (int o = 32; o > 0; o >>= 1) {
+        t += __shfl_xor(t, o);
+        p += __shfl_xor(p, o);
+      }
+      if (lane == 0) {
+        if (t) atomicAdd(reinterpret_cast<unsigned long long*>(&s_tot[k]), static_cast<unsigned long long>(t));
+        if (p) atomicAdd(reinterpret_cast<unsigned long long*>(&s_pre[k]), static_cast<unsigned long long>(p));
+      }
+    }
+  }
+  const int64_t gpk = gblk * kTsThreads + tid;
+  const uint32_t m = meta[gpk];
+  const int c = m & 3, ps = (m >> 2) & 0xff, len = (m >> 10) & 0xff, pes_flag = (m >> 18) & 1;
+  // in-block exclusive scans per class (bytes and PES starts)
+  int inc_b[kClasses], inc_p[kClasses];
+#pragma unroll
+  for (int k = 0; k < kClasses; ++k) {
+    inc_b[k] = wave_incl_scan(c == k ? len : 0, lane);
+    inc_p[k] = wave_incl_scan(c == k ? pes_flag : 0, lane);
+  }
+  if (lane == 63) {
+#pragma unroll
+    for (int k = 0; k < kClasses; ++k) {
+      s_wave[wave][2 * k] = inc_b[k];
+      s_wave[wave][2 * k + 1] = inc_p[k];
+    }
+  }
+  __syncthreads();
+  int64_t dst_b = 0, pes_idx = 0;
+  if (c < 3) {
+    int64_t wb = 0, wp = 0;
+    for (int w = 0; w < wave; ++w) {
+      wb += s_wave[w][2 * c];
+      wp += s_wave[w][2 * c + 1];
+    }
+    const int64_t class_base = (c >= 1 ? s_tot[0] : 0) + (c >= 2 ? s_tot[2] : 0);
+    const int64_t es_in_class = s_pre[2 * c] + wb + inc_b[c] - len;  // exclusive
+    dst_b = class_base + es_in_class;
+    pes_idx = s_pre[2 * c + 1] + wp + inc_p[c] - pes_flag;
+    if (pes_flag) {
+      if (pes_idx < max_pes) {
+        int64_t* r = pes + ((static_cast<int64_t>(seg) * kClasses + c) * max_pes + pes_idx) * 3;
+        r[0] = es_in_class;
+        r[1] = pts_dts[2 * gpk];
+        r[2] = pts_dts[2 * gpk + 1];
+      }
+    }
+  }
+  // cooperative per-packet copy: the whole wave moves one packet payload at a time
+  const uint8_t* sbase = buf + seg_off[seg] + (blk * kTsThreads + wave * 64) * kPkt;
+  uint8_t* ebase = es + es_off[seg];
+  uint64_t active = __ballot(c < 3 && len > 0);
+  while (active) {
+    const int j = __builtin_ctzll(active);
+    active &= active - 1;
+    const int jlen = __shfl(len, j);
+    const int jps = __shfl(ps, j);
+    const int64_t jdst = __shfl(dst_b, j);
+    const uint8_t* s = sbase + static_cast<int64_t>(j) * kPkt + jps;
+    uint8_t* d = ebase + jdst;
+    const int head = static_cast<int>((4 - (reinterpret_cast<uintptr_t>(d) & 3)) & 3) < jlen
+                         ? static_cast<int>((4 - (reinterpret_cast<uintptr_t>(d) & 3)) & 3)
+                         : jlen;
+    const int body = (jlen - head) >> 2;
+    const int tail = jlen - head - 4 * body;
+    if (lane < head) d[lane] = s[lane];
+    if (lane < body) {
+      const uint8_t* a = s + head + 4 * lane;
+      const uintptr_t ai = reinterpret_cast<uintptr_t>(a);
+      const uint32_t* al = reinterpret_cast<const uint32_t*>(ai & ~uintptr_t(3));
+      const uint32_t sh = static_cast<uint32_t>(ai & 3);
+      const uint32_t lo = al[0];
+      const uint32_t hi = sh ? al[1] : 0u;
+      const uint32_t v = sh ? __builtin_amdgcn_alignbyte(hi, lo, sh) : lo;
+      reinterpret_cast<uint32_t*>(d + head)[lane] = v;
+    }
+    if (lane < tail) d[head + 4 * body + lane] = s[head + 4 * body + lane];
+  }
+  if (blk == 0 && tid == 0) {
+    int64_t* inf = info + static_cast<int64_t>(seg) * kInfo;
+    int64_t over = 0;
+    for (int k = 0; k < kClasses; ++k) {
+      inf[kBytes0 + k] = s_tot[2 * k];
+      inf[kPes0 + k] = s_tot[2 * k + 1];
+      if (s_tot[2 * k + 1] > max_pes) over = kPesOverflow;
+    }
+    inf[kPayloadBytes] = s_tot[0] + s_tot[2] + s_tot[4];
+    if (over) atomicOr(reinterpret_cast<unsigned long long*>(inf + kStatus), static_cast<unsigned long long>(over));
+  }
+}
+
+hipError_t launch_ts_demux(const uint8_t* buf, const int64_t* seg_off, const int64_t* seg_len,
+                           const int64_t* blk_prefix, int nseg, int64_t total_blocks, uint32_t* meta,
+                           int64_t* pts_dts, int32_t* blk_sums, uint8_t* es, const int64_t* es_off, int64_t* pes,
+                           int64_t max_pes, int64_t* info, hipStream_t stream) {
+  if (nseg <= 0) return hipSuccess;
+  hipLaunchKernelGGL(ts_psi_kernel, dim3(nseg), dim3(64), 0, stream, buf, seg_off, seg_len, info, pes, max_pes);
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess || total_blocks <= 0) return e;
+  hipLaunchKernelGGL(ts_scan_kernel, dim3(static_cast<unsigned>(total_blocks)), dim3(kTsThreads), 0, stream, buf,
+                     seg_off, seg_len, blk_prefix, nseg, info, meta, pts_dts, blk_sums);
+  e = hipGetLastError();
+  if (e != hipSuccess) return e;
+  hipLaunchKernelGGL(ts_gather_kernel, dim3(static_cast<unsigned>(total_blocks)), dim3(kTsThreads), 0, stream, buf,
+                     seg_off, seg_len, blk_prefix, nseg, meta, pts_dts, blk_sums, es, es_off, pes, max_pes, info);
+  return hipGetLastError();
+}
+
+}  // namespace dev
+}  // namespace hlsp2p

@@ -1,0 +1,375 @@
+// pybind11 module `_runtime`: the host-native runtime of the swarm node.
+//
+// Pure C++ (no torch, no HIP): cache layout + swarm directory + exchange planner, the
+// origin packager (TS mux + AES-128-CBC), and CPU reference implementations of every
+// device kernel (decrypt, demux, CRC) used as test oracles and by the CPU (no-GPU) mode.
+// Batch entry points take numpy arrays (torch CPU tensors pass via .numpy()).
+#include <pybind11/numpy.h>
+#include <pybind11/pybind11.h>
+#include <pybind11/stl.h>
+
+#include <algorithm>
+#include <cstring>
+#include <stdexcept>
+#include <thread>
+#include <vector>
+
+#include "aes_host.hpp"
+#include "crc_host.hpp"
+#include "planner.hpp"
+#include "store.hpp"
+#include "ts.hpp"
+
+namespace py = pybind11;
+using namespace hlsp2p;
+
+namespace {
+
+template <typename T>
+using Arr = py::array_t<T, py::array::c_style | py::array::forcecast>;
+
+template <typename T>
+T* mut_ptr(py::array& a, const char* name) {
+  if (!(a.flags() & py::array::c_style)) throw std::invalid_argument(std::string(name) + " must be C-contiguous");
+  if (a.itemsize() != sizeof(T)) throw std::invalid_argument(std::string(name) + " has the wrong dtype");
+  if (!a.writeable()) throw std::invalid_argument(std::string(name) + " must be writeable");
+  return static_cast<T*>(a.mutable_data());
+}
+
+template <typename F>
+void parallel_for(int64_t n, F&& f) {
+  unsigned hw = std::max(1u, std::thread::hardware_concurrency());
+  int64_t nt = std::min<int64_t>(n, std::min<unsigned>(hw, 16u));
+  if (nt <= 1) {
+    for (int64_t i = 0; i < n; ++i) f(i);
+    return;
+  }
+  std::vector<std::thread> th;
+  for (int64_t t = 0; t < nt; ++t)
+    th.emplace_back([&, t] {
+      for (int64_t i = t; i < n; i += nt) f(i);
+    });
+  for (auto& x : th) x.join();
+}
+
+SegKey key_from(const int64_t* p) {
+  return SegKey{uint32_t(p[0]), uint32_t(p[1]), uint32_t(p[2]), uint32_t(p[3])};
+}
+
+py::array_t<uint8_t> to_u8(const std::vector<uint8_t>& v) {
+  py::array_t<uint8_t> a(static_cast<py::ssize_t>(v.size()));
+  std::memcpy(a.mutable_data(), v.data(), v.size());
+  return a;
+}
+
+}  // namespace
+
+PYBIND11_MODULE(_runtime, m) {
+  m.doc() = "hlsjs-p2p-wrapper-amd host runtime (store, planner, packager, CPU oracles)";
+
+  // ------------------------------------------------------------------ AES
+  m.def("aes_tables", [] {
+    const aes::Tables& t = aes::tables();
+    Arr<uint32_t> td0(256), te0(256);
+    Arr<uint8_t> sbox(256), inv(256);
+    std::memcpy(td0.mutable_data(), t.td0, sizeof t.td0);
+    std::memcpy(te0.mutable_data(), t.te0, sizeof t.te0);
+    std::memcpy(sbox.mutable_data(), t.sbox, 256);
+    std::memcpy(inv.mutable_data(), t.inv_sbox, 256);
+    return py::make_tuple(td0, inv, te0, sbox);
+  });
+  m.def("expand_key_dec", [](py::bytes key) {
+    std::string k = key;
+    if (k.size() != 16) throw std::invalid_argument("AES-128 key must be 16 bytes");
+    Arr<uint32_t> out(44);
+    aes::expand_key_dec(reinterpret_cast<const uint8_t*>(k.data()), out.mutable_data());
+    return out;
+  });
+  m.def("expand_key_enc", [](py::bytes key) {
+    std::string k = key;
+    if (k.size() != 16) throw std::invalid_argument("AES-128 key must be 16 bytes");
+    Arr<uint32_t> out(44);
+    aes::expand_key_enc(reinterpret_cast<const uint8_t*>(k.data()), out.mutable_data());
+    return out;
+  });
+  m.def("aes_encrypt_block", [](py::bytes key, py::bytes block) {
+    std::string k = key, b = block;
+    if (k.size() != 16 || b.size() != 16) throw std::invalid_argument("16-byte key and block");
+    uint32_t rk[44];
+    aes::expand_key_enc(reinterpret_cast<const uint8_t*>(k.data()), rk);
+    uint8_t out[16];
+    aes::encrypt_block(rk, reinterpret_cast<const uint8_t*>(b.data()), out);
+    return py::bytes(reinterpret_cast<char*>(out), 16);
+  });
+  m.def("cbc_encrypt", [](py::bytes key, py::bytes iv, Arr<uint8_t> data) {
+    std::string k = key, v = iv;
+    if (k.size() != 16 || v.size() != 16) throw std::invalid_argument("16-byte key and iv");
+    const size_t n = static_cast<size_t>(data.size());
+    std::vector<uint8_t> out(n + 16);
+    size_t total;
+    {
+      py::gil_scoped_release nogil;
+      total = aes::cbc_encrypt_pkcs7(reinterpret_cast<const uint8_t*>(k.data()),
+                                     reinterpret_cast<const uint8_t*>(v.data()), data.data(), n, out.data());
+    }
+    out.resize(total);
+    return to_u8(out);
+  });
+  m.def("cbc_decrypt", [](py::bytes key, py::bytes iv, Arr<uint8_t> data) -> py::object {
+    std::string k = key, v = iv;
+    if (k.size() != 16 || v.size() != 16) throw std::invalid_argument("16-byte key and iv");
+    const size_t n = static_cast<size_t>(data.size());
+    std::vector<uint8_t> out(n);
+    int64_t len;
+    {
+      py::gil_scoped_release nogil;
+      len = aes::cbc_decrypt_pkcs7(reinterpret_cast<const uint8_t*>(k.data()),
+                                   reinterpret_cast<const uint8_t*>(v.data()), data.data(), n, out.data());
+    }
+    if (len < 0) return py::none();
+    out.resize(static_cast<size_t>(len));
+    return to_u8(out);
+  });
+  // Batched CPU decrypt with the device kernel's argument layout.
+  //   src/dst: flat uint8; src_off/dst_off/nbytes: int64[B]; drk: uint32[B,44]; iv: uint8[B,16]
+  //   out_len: int64[B] (plaintext length after PKCS#7, -1 on bad padding)
+  m.def("cbc_decrypt_batch", [](Arr<uint8_t> src, py::array dst, Arr<int64_t> src_off, Arr<int64_t> dst_off,
+                                Arr<int64_t> nbytes, Arr<uint32_t> drk, Arr<uint8_t> iv, py::array out_len) {
+    const int64_t B = src_off.size();
+    uint8_t* d = mut_ptr<uint8_t>(dst, "dst");
+    int64_t* ol = mut_ptr<int64_t>(out_len, "out_len");
+    const uint8_t* s = src.data();
+    const int64_t* so = src_off.data();
+    const int64_t* dof = dst_off.data();
+    const int64_t* nb = nbytes.data();
+    const uint32_t* k = drk.data();
+    const uint8_t* ivp = iv.data();
+    const int64_t src_n = src.size(), dst_n = dst.size();
+    for (int64_t b = 0; b < B; ++b)
+      if (nb[b] < 0 || nb[b] % 16 || so[b] < 0 || so[b] + nb[b] > src_n || dof[b] < 0 || dof[b] + nb[b] > dst_n)
+        throw std::invalid_argument("cbc_decrypt_batch: segment out of bounds or not a multiple of 16");
+    py::gil_scoped_release nogil;
+    parallel_for(B, [&](int64_t b) {
+      const uint8_t* in = s + so[b];
+      uint8_t* out = d + dof[b];
+      const uint32_t* rk = k + 44 * b;
+      uint8_t prev[16], cur[16], tmp[16];
+      std::memcpy(prev, ivp + 16 * b, 16);
+      for (int64_t off = 0; off < nb[b]; off += 16) {
+        std::memcpy(cur, in + off, 16);
+        aes::decrypt_block(rk, cur, tmp);
+        for (int i = 0; i < 16; ++i) out[off + i] = tmp[i] ^ prev[i];
+        std::memcpy(prev, cur, 16);
+      }
+      int64_t len = -1;
+      if (nb[b] >= 16) {
+        uint8_t pad = out[nb[b] - 1];
+        if (pad >= 1 && pad <= 16) {
+          len = nb[b] - pad;
+          for (int64_t i = len; i < nb[b]; ++i)
+            if (out[i] != pad) { len = -1; break; }
+        }
+      }
+      ol[b] = len;
+    });
+  });
+
+  // ------------------------------------------------------------------ CRC
+  m.def("crc32", [](Arr<uint8_t> data, uint32_t crc) {
+    return crc::crc32(data.data(), static_cast<size_t>(data.size()), crc);
+  }, py::arg("data"), py::arg("crc") = 0u);
+  m.def("crc32_batch", [](Arr<uint8_t> buf, Arr<int64_t> off, Arr<int64_t> len) {
+    const int64_t B = off.size();
+    Arr<uint32_t> out(B);
+    uint32_t* o = out.mutable_data();
+    const uint8_t* p = buf.data();
+    const int64_t* of = off.data();
+    const int64_t* ln = len.data();
+    for (int64_t b = 0; b < B; ++b)
+      if (of[b] < 0 || ln[b] < 0 || of[b] + ln[b] > buf.size()) throw std::invalid_argument("crc32_batch: out of bounds");
+    py::gil_scoped_release nogil;
+    parallel_for(B, [&](int64_t b) { o[b] = crc::crc32(p + of[b], static_cast<size_t>(ln[b])); });
+    return out;
+  });
+  m.def("crc_mfma_weights", [] {
+    auto w = crc::mfma_group_weights();
+    Arr<int8_t> a(static_cast<py::ssize_t>(w.size()));
+    std::memcpy(a.mutable_data(), w.data(), w.size());
+    return a;
+  });
+  m.def("crc_shift_tables", [] {
+    auto t = crc::shift_tables();
+    Arr<uint32_t> a(static_cast<py::ssize_t>(t.size()));
+    std::memcpy(a.mutable_data(), t.data(), t.size() * 4);
+    return a;
+  });
+  m.attr("CRC_NUM_P") = crc::kNumP;
+  m.attr("CRC_NUM_Q") = crc::kNumQ;
+  m.attr("CRC_GROUP_BYTES") = crc::kGroupBytes;
+
+  // ------------------------------------------------------------------ TS
+  m.def("mux_segment", [](double duration, double fps, int64_t target_bytes, int audio_kbps, bool with_id3,
+                          uint64_t seed, int64_t sn, double start_time) {
+    ts::MuxConfig c;
+    c.duration = duration; c.fps = fps; c.target_bytes = target_bytes; c.audio_kbps = audio_kbps;
+    c.with_id3 = with_id3; c.seed = seed; c.sn = sn; c.start_time = start_time;
+    ts::MuxStats st;
+    std::vector<uint8_t> v;
+    {
+      py::gil_scoped_release nogil;
+      v = ts::mux_segment(c, &st);
+    }
+    py::dict d;
+    d["es_bytes"] = py::make_tuple(st.es_bytes[0], st.es_bytes[1], st.es_bytes[2]);
+    d["n_pes"] = py::make_tuple(st.n_pes[0], st.n_pes[1], st.n_pes[2]);
+    d["first_pts"] = py::make_tuple(st.first_pts[0], st.first_pts[1], st.first_pts[2]);
+    d["last_pts"] = py::make_tuple(st.last_pts[0], st.last_pts[1], st.last_pts[2]);
+    d["n_packets"] = st.n_packets;
+    return py::make_tuple(to_u8(v), d);
+  }, py::arg("duration"), py::arg("fps"), py::arg("target_bytes"), py::arg("audio_kbps"), py::arg("with_id3"),
+     py::arg("seed"), py::arg("sn"), py::arg("start_time"));
+  // Batched CPU demux with the device kernels' layout.
+  //   buf: flat uint8 plaintext; off/len: int64[B]; es: flat uint8 (segment b writes at es_off[b])
+  //   pes: int64[B, 3, max_pes, 3]; info: int64[B, 16]
+  m.def("demux_batch", [](Arr<uint8_t> buf, Arr<int64_t> off, Arr<int64_t> len, py::array es, Arr<int64_t> es_off,
+                          py::array pes, py::array info, int64_t max_pes) {
+    const int64_t B = off.size();
+    uint8_t* e = mut_ptr<uint8_t>(es, "es");
+    int64_t* pp = mut_ptr<int64_t>(pes, "pes");
+    int64_t* ip = mut_ptr<int64_t>(info, "info");
+    if (pes.size() < B * ts::kClasses * max_pes * 3 || info.size() < B * ts::kInfoWords)
+      throw std::invalid_argument("demux_batch: pes/info too small");
+    for (int64_t b = 0; b < B; ++b)
+      if (off.data()[b] < 0 || len.data()[b] < 0 || off.data()[b] + len.data()[b] > buf.size() ||
+          es_off.data()[b] < 0 || es_off.data()[b] + len.data()[b] > es.size())
+        throw std::invalid_argument("demux_batch: segment out of bounds");
+    const uint8_t* p = buf.data();
+    const int64_t* o = off.data();
+    const int64_t* l = len.data();
+    const int64_t* eo = es_off.data();
+    py::gil_scoped_release nogil;
+    parallel_for(B, [&](int64_t b) {
+      ts::demux_segment(p + o[b], l[b], e + eo[b], pp + b * ts::kClasses * max_pes * 3, max_pes,
+                        ip + b * ts::kInfoWords);
+    });
+  });
+  m.def("mpeg_crc32", [](Arr<uint8_t> data) { return ts::mpeg_crc32(data.data(), static_cast<size_t>(data.size())); });
+  m.attr("TS_INFO_WORDS") = ts::kInfoWords;
+  m.attr("TS_CLASSES") = ts::kClasses;
+
+  // ------------------------------------------------------------------ store
+  py::class_<SegmentStore>(m, "SegmentStore")
+      .def(py::init<int64_t, int64_t>(), py::arg("capacity"), py::arg("align") = 256)
+      .def_property_readonly("capacity", &SegmentStore::capacity)
+      .def_property_readonly("used_bytes", &SegmentStore::used_bytes)
+      .def_property_readonly("num_entries", &SegmentStore::num_entries)
+      .def_property_readonly("evictions", &SegmentStore::evictions)
+      .def_property_readonly("max_entries", &SegmentStore::max_entries)
+      .def("lookup", [](const SegmentStore& s, Arr<int64_t> keys, bool include_pending) {
+        const int64_t n = keys.size() / 4;
+        Arr<int64_t> out(n);
+        const int64_t* k = keys.data();
+        int64_t* o = out.mutable_data();
+        for (int64_t i = 0; i < n; ++i) o[i] = s.lookup(key_from(k + 4 * i), include_pending);
+        return out;
+      }, py::arg("keys"), py::arg("include_pending") = false)
+      .def("lookup1", [](const SegmentStore& s, uint32_t swarm, uint32_t level, uint32_t url_id, uint32_t sn) {
+        return s.lookup(SegKey{swarm, level, url_id, sn}, false);
+      })
+      .def("entries", [](const SegmentStore& s, Arr<int64_t> ids) {
+        // -> int64[n, 4]: offset, length, state, pins
+        const int64_t n = ids.size();
+        Arr<int64_t> out({n, int64_t(4)});
+        int64_t* o = out.mutable_data();
+        for (int64_t i = 0; i < n; ++i) {
+          int64_t id = ids.data()[i];
+          if (id < 0 || id >= s.max_entries()) throw std::out_of_range("bad entry id");
+          const Entry& e = s.entry(id);
+          o[4 * i] = e.offset; o[4 * i + 1] = e.length; o[4 * i + 2] = e.state; o[4 * i + 3] = e.pins;
+        }
+        return out;
+      })
+      .def("reserve_run", [](SegmentStore& s, Arr<int64_t> keys, Arr<int64_t> lens, int64_t tick) -> py::object {
+        const int64_t n = lens.size();
+        if (keys.size() != 4 * n) throw std::invalid_argument("keys must be int64[n,4]");
+        std::vector<SegKey> k(n);
+        for (int64_t i = 0; i < n; ++i) k[i] = key_from(keys.data() + 4 * i);
+        Arr<int64_t> ids(n), offs(n);
+        int64_t base = s.reserve_run(k.data(), lens.data(), n, tick, ids.mutable_data(), offs.mutable_data());
+        if (base < 0) return py::none();
+        return py::make_tuple(base, ids, offs);
+      })
+      .def("commit", [](SegmentStore& s, Arr<int64_t> ids) {
+        for (int64_t i = 0; i < ids.size(); ++i) s.commit(ids.data()[i]);
+      })
+      .def("drop", [](SegmentStore& s, Arr<int64_t> ids) {
+        for (int64_t i = 0; i < ids.size(); ++i) s.drop(ids.data()[i]);
+      })
+      .def("pin", [](SegmentStore& s, Arr<int64_t> ids) {
+        for (int64_t i = 0; i < ids.size(); ++i) s.pin(ids.data()[i]);
+      })
+      .def("unpin", [](SegmentStore& s, Arr<int64_t> ids) {
+        for (int64_t i = 0; i < ids.size(); ++i) s.unpin(ids.data()[i]);
+      })
+      .def("evict_below", &SegmentStore::evict_below)
+      .def("take_delta", [](SegmentStore& s) {
+        std::vector<SegKey> add, rm;
+        std::vector<int64_t> add_len;
+        s.take_delta(&add, &add_len, &rm);
+        Arr<int64_t> a({int64_t(add.size()), int64_t(5)}), r({int64_t(rm.size()), int64_t(4)});
+        int64_t* ap = a.mutable_data();
+        for (size_t i = 0; i < add.size(); ++i) {
+          ap[5 * i] = add[i].swarm; ap[5 * i + 1] = add[i].level; ap[5 * i + 2] = add[i].url_id;
+          ap[5 * i + 3] = add[i].sn; ap[5 * i + 4] = add_len[i];
+        }
+        int64_t* rp = r.mutable_data();
+        for (size_t i = 0; i < rm.size(); ++i) {
+          rp[4 * i] = rm[i].swarm; rp[4 * i + 1] = rm[i].level; rp[4 * i + 2] = rm[i].url_id; rp[4 * i + 3] = rm[i].sn;
+        }
+        return py::make_tuple(a, r);
+      });
+
+  // ------------------------------------------------------------------ directory / planner
+  py::class_<Directory>(m, "Directory")
+      .def(py::init<>())
+      .def_property_readonly("size", &Directory::size)
+      .def("apply", [](Directory& d, int rank, Arr<int64_t> adds, Arr<int64_t> removes) {
+        // adds int64[n,5] (key4, len); removes int64[m,4]
+        for (int64_t i = 0; i < adds.size() / 5; ++i) d.apply_add(rank, key_from(adds.data() + 5 * i), adds.data()[5 * i + 4]);
+        for (int64_t i = 0; i < removes.size() / 4; ++i) d.apply_remove(rank, key_from(removes.data() + 4 * i));
+      })
+      .def("drop_rank", &Directory::drop_rank)
+      .def("holders", [](const Directory& d, uint32_t swarm, uint32_t level, uint32_t url_id, uint32_t sn) {
+        const DirEntry* e = d.find(SegKey{swarm, level, url_id, sn});
+        return e ? e->holders : uint64_t(0);
+      });
+  // wants: int64[n, 7] = (key4, size, want_id, rank); flags int64[world]
+  // -> int64[m, 10] = (key4, size, src, dst, want_id, seeded, reserved)
+  m.def("plan_round", [](const Directory& d, Arr<int64_t> wants, Arr<int64_t> flags, int world) {
+    const int64_t n = wants.size() / 7;
+    std::vector<Want> w(n);
+    const int64_t* p = wants.data();
+    for (int64_t i = 0; i < n; ++i) {
+      w[i].key = key_from(p + 7 * i);
+      w[i].size = p[7 * i + 4];
+      w[i].want_id = p[7 * i + 5];
+      w[i].rank = static_cast<int32_t>(p[7 * i + 6]);
+      if (w[i].rank < 0 || w[i].rank >= world) throw std::invalid_argument("want rank out of range");
+    }
+    if (flags.size() != world) throw std::invalid_argument("flags must have world entries");
+    std::vector<int64_t> f(flags.data(), flags.data() + world);
+    std::vector<Transfer> t = plan_round(d, w, f, world);
+    Arr<int64_t> out({int64_t(t.size()), int64_t(10)});
+    int64_t* o = out.mutable_data();
+    for (size_t i = 0; i < t.size(); ++i) {
+      int64_t* r = o + 10 * i;
+      r[0] = t[i].key.swarm; r[1] = t[i].key.level; r[2] = t[i].key.url_id; r[3] = t[i].key.sn;
+      r[4] = t[i].size; r[5] = t[i].src; r[6] = t[i].dst; r[7] = t[i].want_id; r[8] = t[i].seeded; r[9] = 0;
+    }
+    return out;
+  });
+  m.attr("FLAG_ONLINE") = int64_t(kOnline);
+  m.attr("FLAG_UPLOAD") = int64_t(kUploadOn);
+  m.attr("FLAG_DOWNLOAD") = int64_t(kDownloadOn);
+  m.attr("FLAG_CDN_DEDUP") = int64_t(kCdnDedup);
+}

@@ -1,0 +1,158 @@
+#include "crc_host.hpp"
+
+#include <cstring>
+
+namespace hlsp2p {
+namespace crc {
+namespace {
+
+struct ByteTable {
+  uint32_t t[8][256];
+  ByteTable() {
+    for (uint32_t i = 0; i < 256; ++i) {
+      uint32_t r = i;
+      for (int k = 0; k < 8; ++k) r = (r >> 1) ^ (kPoly & (0u - (r & 1u)));
+      t[0][i] = r;
+    }
+    for (int s = 1; s < 8; ++s)
+      for (uint32_t i = 0; i < 256; ++i) t[s][i] = (t[s - 1][i] >> 8) ^ t[0][t[s - 1][i] & 0xff];
+  }
+};
+
+const ByteTable& table() {
+  static const ByteTable tb;
+  return tb;
+}
+
+}  // namespace
+
+uint32_t crc32(const uint8_t* p, size_t n, uint32_t crc) {
+  const ByteTable& T = table();
+  uint32_t r = ~crc;
+  while (n >= 8) {  // slice-by-8
+    uint32_t lo, hi;
+    std::memcpy(&lo, p, 4);
+    std::memcpy(&hi, p + 4, 4);
+    lo ^= r;
+    r = T.t[7][lo & 0xff] ^ T.t[6][(lo >> 8) & 0xff] ^ T.t[5][(lo >> 16) & 0xff] ^ T.t[4][lo >> 24] ^
+        T.t[3][hi & 0xff] ^ T.t[2][(hi >> 8) & 0xff] ^ T.t[1][(hi >> 16) & 0xff] ^ T.t[0][hi >> 24];
+    p += 8;
+    n -= 8;
+  }
+  while (n--) r = (r >> 8) ^ T.t[0][(r ^ *p++) & 0xff];
+  return ~r;
+}
+
+uint32_t apply(const Mat& m, uint32_t v) {
+  uint32_t out = 0;
+  for (int i = 0; v; ++i, v >>= 1)
+    if (v & 1u) out ^= m.col[i];
+  return out;
+}
+
+Mat mul(const Mat& a, const Mat& b) {
+  Mat c;
+  for (int i = 0; i < 32; ++i) c.col[i] = apply(a, b.col[i]);
+  return c;
+}
+
+Mat zero_byte_op() {
+  const ByteTable& T = table();
+  Mat m;
+  for (int i = 0; i < 32; ++i) {
+    uint32_t r = 1u << i;
+    m.col[i] = (r >> 8) ^ T.t[0][r & 0xff];
+  }
+  return m;
+}
+
+Mat power(const Mat& m, uint64_t e) {
+  Mat result;
+  for (int i = 0; i < 32; ++i) result.col[i] = 1u << i;
+  Mat base = m;
+  while (e) {
+    if (e & 1) result = mul(base, result);
+    base = mul(base, base);
+    e >>= 1;
+  }
+  return result;
+}
+
+bool inverse(const Mat& m, Mat* out) {
+  // Gauss-Jordan on rows: build row-major bit matrix [M | I].
+  uint64_t rows[32];
+  for (int r = 0; r < 32; ++r) {
+    uint32_t row = 0;
+    for (int c = 0; c < 32; ++c)
+      if ((m.col[c] >> r) & 1u) row |= 1u << c;
+    rows[r] = uint64_t(row) | (uint64_t(1u << r) << 32);
+  }
+  for (int c = 0; c < 32; ++c) {
+    int piv = -1;
+    for (int r = c; r < 32; ++r)
+      if ((rows[r] >> c) & 1u) { piv = r; break; }
+    if (piv < 0) return false;
+    std::swap(rows[c], rows[piv]);
+    for (int r = 0; r < 32; ++r)
+      if (r != c && ((rows[r] >> c) & 1u)) rows[r] ^= rows[c];
+  }
+  for (int c = 0; c < 32; ++c) {
+    uint32_t col = 0;
+    for (int r = 0; r < 32; ++r)
+      if ((rows[r] >> (32 + c)) & 1u) col |= 1u << r;
+    out->col[c] = col;
+  }
+  return true;
+}
+
+void slice_table(const Mat& m, uint32_t* out) {
+  for (int b = 0; b < 4; ++b)
+    for (uint32_t x = 0; x < 256; ++x) out[b * 256 + x] = apply(m, x << (8 * b));
+}
+
+std::vector<int8_t> mfma_group_weights() {
+  const ByteTable& T = table();
+  // v[byte][bit]: raw CRC (zero init) of a 256-byte group with only that bit set.
+  static uint32_t v[kGroupBytes][8];
+  for (int bit = 0; bit < 8; ++bit) {
+    uint32_t r = T.t[0][1u << bit];  // one byte (1<<bit) from a zero register
+    for (int b = kGroupBytes - 1; b >= 0; --b) {
+      v[b][bit] = r;
+      r = (r >> 8) ^ T.t[0][r & 0xff];  // one more zero byte after it
+    }
+  }
+  // Fragment order: lane l (r = l & 31 = CRC bit column, h = l >> 5) at step s holds
+  // B[k][r] for its 16 k's; k(s, h, j) <-> group byte 128h + 2s + (j >> 3), bit j & 7.
+  std::vector<int8_t> w(64 * 64 * 16);
+  for (int s = 0; s < 64; ++s)
+    for (int lane = 0; lane < 64; ++lane) {
+      int col = lane & 31, h = lane >> 5;
+      for (int j = 0; j < 16; ++j) {
+        int byte = 128 * h + 2 * s + (j >> 3);
+        int bit = j & 7;
+        w[(s * 64 + lane) * 16 + j] = static_cast<int8_t>((v[byte][bit] >> col) & 1u);
+      }
+    }
+  return w;
+}
+
+std::vector<uint32_t> shift_tables() {
+  std::vector<uint32_t> out(size_t(kNumP + kNumQ) * kSliceWords);
+  Mat a8 = zero_byte_op();
+  Mat p = a8;  // A^(8 * 2^0)
+  for (int b = 0; b < kNumP; ++b) {
+    slice_table(p, out.data() + size_t(b) * kSliceWords);
+    p = mul(p, p);
+  }
+  Mat inv;
+  inverse(a8, &inv);
+  Mat q = inv;
+  for (int b = 0; b < kNumQ; ++b) {
+    slice_table(q, out.data() + size_t(kNumP + b) * kSliceWords);
+    q = mul(q, q);
+  }
+  return out;
+}
+
+}  // namespace crc
+}  // namespace hlsp2p

@@ -1,0 +1,48 @@
+// CRC-32 (IEEE 802.3 / zlib, reflected polynomial 0xEDB88320) host side.
+//
+// * crc32(): oracle (bit-identical to zlib.crc32) for tests and CPU mode;
+// * GF(2) operator algebra used to build the constant tables the MFMA CRC kernel consumes
+//   (kernels/crc32_mfma.hip):
+//     - the 256-byte "group" weight matrix W (2048 data bits x 32 CRC bits), emitted in the
+//       exact MFMA B-fragment order the kernel loads with one ds_read_b128 per step;
+//     - byte-slice tables of the zero-byte shift operators P_b = A^(8*2^b) (b = 0..39) and
+//       their inverses Q_b = A^(-8*2^b) (b = 0..7) that combine group residues and undo the
+//       zero padding of the last group.
+//
+// CRC algebra: with raw(M, r0) the register after processing M from r0 (no final xor),
+//   raw(M1||M2, 0) = A^(8|M2|) raw(M1, 0) xor raw(M2, 0),
+//   crc(M)         = raw(M, 0) xor A^(8|M|)(0xFFFFFFFF) xor 0xFFFFFFFF.
+#pragma once
+#include <cstddef>
+#include <cstdint>
+#include <vector>
+
+namespace hlsp2p {
+namespace crc {
+
+constexpr uint32_t kPoly = 0xEDB88320u;
+constexpr int kGroupBytes = 256;      // data bytes per MFMA output row
+constexpr int kNumP = 40;             // P_b tables, b = 0..39  (shift up to 2^39 bytes)
+constexpr int kNumQ = 8;              // Q_b tables, b = 0..7   (undo pad < 256 bytes)
+constexpr int kSliceWords = 4 * 256;  // one byte-slice table set (4 KiB)
+
+uint32_t crc32(const uint8_t* data, size_t n, uint32_t crc = 0);  // zlib-compatible update
+
+// 32x32 GF(2) matrix as 32 column vectors.
+struct Mat {
+  uint32_t col[32];
+};
+uint32_t apply(const Mat& m, uint32_t v);
+Mat mul(const Mat& a, const Mat& b);
+Mat zero_byte_op();              // A^8
+Mat power(const Mat& m, uint64_t e);
+bool inverse(const Mat& m, Mat* out);
+void slice_table(const Mat& m, uint32_t* out /* kSliceWords */);
+
+// MFMA B-fragment weight table: [step s=0..63][lane=0..63][16 int8] = 65536 bytes.
+std::vector<int8_t> mfma_group_weights();
+// Byte-slice tables: P_0..P_39 then Q_0..Q_7, each kSliceWords u32.
+std::vector<uint32_t> shift_tables();
+
+}  // namespace crc
+}  // namespace hlsp2p

@@ -1,0 +1,140 @@
+#include "planner.hpp"
+
+#include <algorithm>
+#include <stdexcept>
+
+namespace hlsp2p {
+
+void Directory::apply_add(int rank, const SegKey& k, int64_t length) {
+  DirEntry& e = map_[k];
+  e.holders |= (uint64_t(1) << rank);
+  e.length = length;
+}
+
+void Directory::apply_remove(int rank, const SegKey& k) {
+  auto it = map_.find(k);
+  if (it == map_.end()) return;
+  it->second.holders &= ~(uint64_t(1) << rank);
+  if (it->second.holders == 0) map_.erase(it);
+}
+
+void Directory::drop_rank(int rank) {
+  const uint64_t mask = ~(uint64_t(1) << rank);
+  for (auto it = map_.begin(); it != map_.end();) {
+    it->second.holders &= mask;
+    if (it->second.holders == 0)
+      it = map_.erase(it);
+    else
+      ++it;
+  }
+}
+
+const DirEntry* Directory::find(const SegKey& k) const {
+  auto it = map_.find(k);
+  return it == map_.end() ? nullptr : &it->second;
+}
+
+std::vector<Transfer> plan_round(const Directory& dir, const std::vector<Want>& wants_in,
+                                 const std::vector<int64_t>& flags, int world) {
+  if (world <= 0 || world > kMaxRanks) throw std::invalid_argument("world size out of range");
+  std::vector<Want> wants(wants_in);
+  std::stable_sort(wants.begin(), wants.end(), [](const Want& a, const Want& b) {
+    if (!(a.key == b.key)) return a.key < b.key;
+    if (a.rank != b.rank) return a.rank < b.rank;
+    return a.want_id < b.want_id;
+  });
+  auto flag = [&](int r, int64_t f) { return (flags[r] & f) != 0; };
+
+  std::vector<int64_t> link(size_t(world) * world, 0);  // bytes src->dst this round
+  std::vector<int64_t> send_total(world, 0), cdn_total(world, 0);
+  std::vector<Transfer> cdn, p2p;
+
+  size_t i = 0;
+  while (i < wants.size()) {
+    size_t j = i;
+    while (j < wants.size() && wants[j].key == wants[i].key) ++j;
+    const SegKey key = wants[i].key;
+    const DirEntry* de = dir.find(key);
+    uint64_t holders = 0;
+    if (de) {
+      for (int r = 0; r < world; ++r)
+        if (((de->holders >> r) & 1u) && flag(r, kOnline) && flag(r, kUploadOn)) holders |= uint64_t(1) << r;
+    }
+    std::vector<size_t> unserved;
+    for (size_t w = i; w < j; ++w) {
+      const Want& wt = wants[w];
+      const int d = wt.rank;
+      if (!flag(d, kOnline) || !flag(d, kDownloadOn)) {
+        cdn.push_back({key, wt.size, -1, d, wt.want_id, 0});
+        cdn_total[d] += wt.size;
+        continue;
+      }
+      uint64_t cand = holders & ~(uint64_t(1) << d);
+      if (!cand) {
+        unserved.push_back(w);
+        continue;
+      }
+      int best = -1;
+      for (int k = 1; k <= world; ++k) {  // rotation start: the rank after d
+        int h = (d + k) % world;
+        if (!((cand >> h) & 1u)) continue;
+        if (best < 0) { best = h; continue; }
+        int64_t lh = link[size_t(h) * world + d], lb = link[size_t(best) * world + d];
+        if (lh < lb || (lh == lb && send_total[h] < send_total[best])) best = h;
+      }
+      const int64_t size = de ? de->length : wt.size;
+      p2p.push_back({key, size, best, d, wt.want_id, 0});
+      link[size_t(best) * world + d] += size;
+      send_total[best] += size;
+    }
+    if (!unserved.empty()) {
+      int seeder = -1;
+      bool dedup = true;
+      for (size_t w : unserved) dedup = dedup && flag(wants[w].rank, kCdnDedup);
+      if (dedup && unserved.size() > 1) {
+        const uint64_t h = mix64((uint64_t(key.level) << 40) ^ (uint64_t(key.url_id) << 32) ^ key.sn ^
+                                 (uint64_t(key.swarm) << 48));
+        const size_t n = unserved.size();
+        for (size_t k = 0; k < n; ++k) {
+          const Want& cand = wants[unserved[(h + k) % n]];
+          if (!flag(cand.rank, kUploadOn)) continue;
+          if (seeder < 0 || cdn_total[cand.rank] < cdn_total[seeder]) seeder = cand.rank;
+        }
+      }
+      if (seeder < 0) {
+        for (size_t w : unserved) {
+          cdn.push_back({key, wants[w].size, -1, wants[w].rank, wants[w].want_id, 0});
+          cdn_total[wants[w].rank] += wants[w].size;
+        }
+      } else {
+        for (size_t w : unserved) {
+          const Want& wt = wants[w];
+          if (wt.rank == seeder) {
+            cdn.push_back({key, wt.size, -1, seeder, wt.want_id, 0});
+            cdn_total[seeder] += wt.size;
+          }
+        }
+        for (size_t w : unserved) {
+          const Want& wt = wants[w];
+          if (wt.rank == seeder) continue;
+          p2p.push_back({key, wt.size, seeder, wt.rank, wt.want_id, 1});
+          link[size_t(seeder) * world + wt.rank] += wt.size;
+          send_total[seeder] += wt.size;
+        }
+      }
+    }
+    i = j;
+  }
+  std::stable_sort(p2p.begin(), p2p.end(), [](const Transfer& a, const Transfer& b) {
+    if (a.src != b.src) return a.src < b.src;
+    if (a.dst != b.dst) return a.dst < b.dst;
+    return a.key < b.key;
+  });
+  std::vector<Transfer> out;
+  out.reserve(cdn.size() + p2p.size());
+  out.insert(out.end(), cdn.begin(), cdn.end());
+  out.insert(out.end(), p2p.begin(), p2p.end());
+  return out;
+}
+
+}  // namespace hlsp2p

@@ -1,0 +1,72 @@
+// Swarm directory + deterministic exchange planner.
+//
+// The reference hands segment exchange to the closed-source peer agent over WebRTC
+// DataChannels with a tracker.  RCCL point-to-point is two-sided and
+// ordered, so on the MI355X node on-demand request/response becomes *exchange rounds*:
+// every rank all-gathers a small control message (its wants and its cache delta), applies
+// the deltas to an identical replicated directory, and runs this planner — pure,
+// deterministic, same inputs on every rank — so all ranks agree on who sends what to whom
+// without any further negotiation.  Each rank then posts exactly the matching RCCL
+// send/recv batch.
+//
+// Planning policy per wanted key (keys processed in sorted order, wanters in rank order):
+//   1. wanter offline or P2P download off              -> CDN fetch by the wanter;
+//   2. some other online, upload-enabled rank holds it -> P2P from the holder whose link
+//      to the wanter is least loaded this round (then least total send bytes, then a
+//      rotation), spreading traffic over the 7 point-to-point xGMI links;
+//   3. nobody holds it: with CDN de-duplication one wanter (least CDN bytes this round,
+//      hash rotation on ties) "seeds" it from the CDN and forwards it to the other wanters
+//      in the same round; without it every wanter goes to the CDN.
+#pragma once
+#include <cstdint>
+#include <unordered_map>
+#include <vector>
+
+#include "store.hpp"
+
+namespace hlsp2p {
+
+constexpr int kMaxRanks = 64;
+
+enum RankFlag : int64_t { kOnline = 1, kUploadOn = 2, kDownloadOn = 4, kCdnDedup = 8 };
+
+struct DirEntry {
+  uint64_t holders = 0;
+  int64_t length = 0;
+};
+
+struct Want {
+  SegKey key;
+  int64_t size;
+  int64_t want_id;
+  int32_t rank;
+};
+
+struct Transfer {  // one segment moving src -> dst
+  SegKey key;
+  int64_t size;
+  int32_t src;      // -1 = CDN
+  int32_t dst;
+  int64_t want_id;  // want id at dst
+  int32_t seeded;   // 1: src fetched it from the CDN this round (forwarding)
+};
+
+class Directory {
+ public:
+  void apply_add(int rank, const SegKey& k, int64_t length);
+  void apply_remove(int rank, const SegKey& k);
+  void drop_rank(int rank);  // a rank left: forget everything it held
+  const DirEntry* find(const SegKey& k) const;
+  int64_t size() const { return static_cast<int64_t>(map_.size()); }
+
+ private:
+  std::unordered_map<SegKey, DirEntry, SegKeyHash> map_;
+};
+
+// Returns every transfer of the round (CDN fetches have src = -1), in a canonical order:
+// all CDN fetches first, then P2P transfers grouped by (src, dst) in key order — the order
+// in which both sides pack / unpack their per-pair buffers.
+std::vector<Transfer> plan_round(const Directory& dir, const std::vector<Want>& wants,
+                                 const std::vector<int64_t>& rank_flags, int world);
+
+}  // namespace hlsp2p

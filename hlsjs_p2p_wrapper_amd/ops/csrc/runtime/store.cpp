@@ -1,0 +1,168 @@
+#include "store.hpp"
+
+#include <algorithm>
+#include <stdexcept>
+
+namespace hlsp2p {
+
+SegmentStore::SegmentStore(int64_t capacity, int64_t align) : capacity_(capacity), align_(align) {
+  if (capacity <= 0) throw std::invalid_argument("capacity must be > 0");
+  if (align <= 0 || (align & (align - 1))) throw std::invalid_argument("align must be a power of two");
+}
+
+int64_t SegmentStore::lookup(const SegKey& k, bool include_pending) const {
+  auto it = index_.find(k);
+  if (it == index_.end()) return -1;
+  const Entry& e = entries_[it->second];
+  if (e.state == kResident || (include_pending && e.state == kPending)) return it->second;
+  return -1;
+}
+
+int64_t SegmentStore::new_entry() {
+  if (!free_ids_.empty()) {
+    int64_t id = free_ids_.back();
+    free_ids_.pop_back();
+    return id;
+  }
+  entries_.emplace_back();
+  return static_cast<int64_t>(entries_.size()) - 1;
+}
+
+void SegmentStore::release(int64_t id, bool log_remove) {
+  Entry& e = entries_[id];
+  if (e.state == kFree) return;
+  auto it = index_.find(e.key);
+  const bool owned = it != index_.end() && it->second == id;
+  if (owned) index_.erase(it);
+  // Only announce a removal when the node actually stops holding the key (a detached,
+  // replaced copy going away is not news to the swarm).
+  if (log_remove && owned && e.state == kResident) delta_rm_.push_back(e.key);
+  used_ -= e.alloc_bytes;
+  e.gen += 1;
+  e.state = kFree;
+  e.pins = 0;
+  free_ids_.push_back(id);
+}
+
+// Pop FIFO entries living inside the region we are about to overwrite.  Live entries
+// occupy one cyclic interval [tail, head) in allocation order, so the region starting at
+// `head` (plus [head, capacity) when wrapping) is always at the FIFO front.
+bool SegmentStore::make_room(int64_t start, int64_t len, bool wrapped) {
+  const int64_t end = start + len;
+  while (!fifo_.empty()) {
+    const int64_t id = fifo_.front().first;
+    const Entry& e = entries_[id];
+    if (e.state == kFree || e.gen != fifo_.front().second) {  // stale (dropped, maybe reused)
+      fifo_.pop_front();
+      continue;
+    }
+    bool in_skip = wrapped && e.offset >= head_;
+    bool overlaps = e.offset < end && e.offset + e.alloc_bytes > start;
+    if (!in_skip && !overlaps) break;
+    if (e.pins > 0) return false;
+    fifo_.pop_front();
+    release(id, true);
+    evictions_ += 1;
+  }
+  return true;
+}
+
+int64_t SegmentStore::reserve_run(const SegKey* keys, const int64_t* lens, int64_t n, int64_t tick, int64_t* ids,
+                                  int64_t* offsets) {
+  int64_t total = 0;
+  std::vector<int64_t> rel(n);
+  for (int64_t i = 0; i < n; ++i) {
+    rel[i] = total;
+    int64_t a = (lens[i] + align_ - 1) & ~(align_ - 1);
+    if (a == 0) a = align_;
+    total += a;
+  }
+  if (n == 0) return head_;
+  if (total > capacity_) return -1;
+  int64_t start = head_;
+  bool wrapped = false;
+  if (start + total > capacity_) {
+    start = 0;
+    wrapped = true;
+  }
+  if (!make_room(start, total, wrapped)) return -1;
+  // Replace existing keys (their old copies become stale).
+  for (int64_t i = 0; i < n; ++i) {
+    auto it = index_.find(keys[i]);
+    if (it != index_.end()) {
+      Entry& old = entries_[it->second];
+      if (old.pins > 0) {
+        if (old.state == kResident) delta_rm_.push_back(old.key);
+        index_.erase(it);  // detach; bytes freed when the FIFO reaches it and pins drop
+      } else {
+        release(it->second, true);
+      }
+    }
+  }
+  for (int64_t i = 0; i < n; ++i) {
+    int64_t id = new_entry();
+    Entry& e = entries_[id];
+    e.key = keys[i];
+    e.offset = start + rel[i];
+    e.length = lens[i];
+    e.alloc_bytes = (i + 1 < n ? rel[i + 1] : total) - rel[i];
+    e.state = kPending;
+    e.pins = 0;
+    e.tick = tick;
+    used_ += e.alloc_bytes;
+    index_[keys[i]] = id;
+    fifo_.emplace_back(id, e.gen);
+    ids[i] = id;
+    offsets[i] = e.offset;
+  }
+  head_ = start + total;
+  if (head_ >= capacity_) head_ = 0;
+  return start;
+}
+
+void SegmentStore::commit(int64_t id) {
+  Entry& e = entries_[id];
+  if (e.state != kPending) return;
+  e.state = kResident;
+  delta_add_.push_back(e.key);
+  delta_add_len_.push_back(e.length);
+}
+
+void SegmentStore::drop(int64_t id) {
+  if (id < 0 || id >= static_cast<int64_t>(entries_.size())) return;
+  release(id, true);
+}
+
+int64_t SegmentStore::evict_below(uint32_t swarm, uint32_t min_sn) {
+  std::vector<int64_t> victims;
+  for (const auto& kv : index_) {
+    const Entry& e = entries_[kv.second];
+    if (kv.first.swarm == swarm && kv.first.sn < min_sn && e.state == kResident && e.pins == 0)
+      victims.push_back(kv.second);
+  }
+  for (int64_t id : victims) release(id, true);
+  evictions_ += static_cast<int64_t>(victims.size());
+  return static_cast<int64_t>(victims.size());
+}
+
+void SegmentStore::take_delta(std::vector<SegKey>* added, std::vector<int64_t>* added_len,
+                              std::vector<SegKey>* removed) {
+  added->swap(delta_add_);
+  added_len->swap(delta_add_len_);
+  removed->swap(delta_rm_);
+  delta_add_.clear();
+  delta_add_len_.clear();
+  delta_rm_.clear();
+}
+
+void SegmentStore::all_resident(std::vector<SegKey>* keys, std::vector<int64_t>* lens) const {
+  for (const auto& kv : index_) {
+    const Entry& e = entries_[kv.second];
+    if (e.state == kResident) {
+      keys->push_back(kv.first);
+      lens->push_back(e.length);
+    }
+  }
+}
+
+}  // namespace hlsp2p

@@ -1,0 +1,139 @@
+"""Numerics of the gfx950 kernels against host oracles (zlib / FIPS-197-validated AES /
+CPU demux).  All marked ``gpu``."""
+import zlib
+
+import numpy as np
+import pytest
+import torch
+
+from hlsjs_p2p_wrapper_amd.ops import aes, crc, segment, tsdemux
+
+pytestmark = pytest.mark.gpu
+
+
+def _rand(n, seed):
+    return np.random.default_rng(seed).integers(0, 256, size=n, dtype=np.uint8)
+
+
+def test_crc32_mfma_matches_zlib(cuda):
+    rng = np.random.default_rng(0)
+    lens = [0, 1, 15, 16, 255, 256, 257, 4096, 8191, 8192, 8193, 100003, 3_000_064, 1 << 20, 5_000_011]
+    offs, blob = [], []
+    pos = 0
+    for i, n in enumerate(lens):
+        offs.append(pos)
+        blob.append(_rand(n, i))
+        pad = (-(pos + n)) % 256
+        blob.append(np.zeros(pad, np.uint8))
+        pos += n + pad
+    buf = np.concatenate(blob)
+    t = torch.from_numpy(buf).to(cuda)
+    expect = [zlib.crc32(buf[o:o + n].tobytes()) for o, n in zip(offs, lens)]
+    got, ok = crc.crc32_batch(t, offs, lens, expect=expect)
+    got = got.cpu().numpy().view(np.uint32)
+    assert [int(x) for x in got] == expect
+    assert ok.cpu().numpy().tolist() == [1] * len(lens)
+    # corrupt one byte -> mismatch detected
+    t[offs[7] + 3] ^= 0x40
+    _, ok2 = crc.crc32_batch(t, offs, lens, expect=expect)
+    assert ok2.cpu().numpy().tolist()[7] == 0
+    _ = rng
+
+
+def test_aes_cbc_decrypt_matches_host(cuda):
+    B = 9
+    keys = [bytes(np.random.default_rng(100 + i).integers(0, 256, 16, dtype=np.uint8)) for i in range(B)]
+    ivs = [aes.iv_from_sn(1000 + i) for i in range(B)]
+    plains = [_rand(n, i) for i, n in enumerate([0, 1, 15, 16, 17, 1000, 65536, 188 * 1000, 3_000_001])]
+    cts = [aes.cbc_encrypt(k, v, p) for k, v, p in zip(keys, ivs, plains)]
+    offs, pos = [], 0
+    for c in cts:
+        offs.append(pos)
+        pos += (len(c) + 255) // 256 * 256
+    src = np.zeros(pos, np.uint8)
+    for o, c in zip(offs, cts):
+        src[o:o + len(c)] = c
+    s = torch.from_numpy(src).to(cuda)
+    d = torch.zeros_like(s)
+    out_len = aes.cbc_decrypt_batch(s, offs, [len(c) for c in cts], keys, ivs, d, offs)
+    out_len = out_len.cpu().numpy()
+    host = d.cpu().numpy()
+    for i, p in enumerate(plains):
+        assert out_len[i] == len(p)
+        assert np.array_equal(host[offs[i]:offs[i] + len(p)], p)
+    # wrong key -> padding check fails (overwhelmingly likely)
+    bad = aes.cbc_decrypt_batch(s, offs[-1:], [len(cts[-1])], [bytes(16)], ivs[-1:], d, offs[-1:])
+    assert int(bad.cpu()[0]) == -1 or not np.array_equal(d.cpu().numpy()[offs[-1]:offs[-1] + 64], plains[-1][:64])
+
+
+def test_ts_demux_matches_cpu_oracle(cuda):
+    segs = []
+    for i, (tb, id3) in enumerate([(3_000_000, False), (400_000, True), (1_000_000, False), (188 * 300, True)]):
+        seg, _ = tsdemux.mux_segment(target_bytes=tb, with_id3=id3, seed=11 + i, sn=i, start_time=4.0 * i)
+        segs.append(seg)
+    offs, pos = [], 0
+    for s in segs:
+        offs.append(pos)
+        pos += (len(s) + 255) // 256 * 256
+    buf = np.zeros(pos + 256, np.uint8)
+    for o, s in zip(offs, segs):
+        buf[o:o + len(s)] = s
+    lens = [len(s) for s in segs]
+    cpu = tsdemux.demux_batch(torch.from_numpy(buf), offs, lens, torch.zeros(pos + 256, dtype=torch.uint8), offs)
+    g_buf = torch.from_numpy(buf).to(cuda)
+    g_es = torch.zeros(pos + 256, dtype=torch.uint8, device=cuda)
+    gpu = tsdemux.demux_batch(g_buf, offs, lens, g_es, offs)
+    assert torch.equal(gpu.info.cpu(), cpu.info)
+    assert torch.equal(gpu.pes.cpu(), cpu.pes)
+    ci = cpu.info.numpy()
+    for i, o in enumerate(offs):
+        n = int(ci[i, 14])
+        assert torch.equal(g_es[o:o + n].cpu(), cpu.es[o:o + n])
+        assert ci[i, 0] == 0
+
+
+def test_decrypt_then_demux_on_device(cuda):
+    seg, st = tsdemux.mux_segment(target_bytes=1_500_000, seed=5, sn=42, start_time=168.0)
+    key = bytes(range(16))
+    iv = aes.iv_from_sn(42)
+    ct = aes.cbc_encrypt(key, iv, seg)
+    src = torch.zeros(len(ct) + 256, dtype=torch.uint8, device=cuda)
+    src[:len(ct)] = torch.from_numpy(ct).to(cuda)
+    dec = torch.zeros_like(src)
+    out_len = aes.cbc_decrypt_batch(src, [0], [len(ct)], [key], [iv], dec, [0])
+    es = torch.zeros_like(src)
+    res = tsdemux.demux_batch(dec, [0], out_len, es, [0], caps=[len(ct)])
+    info = res.info.cpu().numpy()[0]
+    assert info[0] == 0
+    assert tuple(info[6:9]) == tuple(st["es_bytes"])
+    assert tuple(info[9:12]) == tuple(st["n_pes"])
+
+
+def test_range_select_and_keys(cuda):
+    starts = [[10.0 * i for i in range(25, 200)], [4.0 * i for i in range(10)]]
+    queries = [(0, 365, 33), (0, 10, 275), (0, 1975, 3000), (0, 240, 2100), (0, 2100, 3000), (1, 0, 8), (5, 0, 1)]
+    lo, hi = segment.range_select(starts, queries, cuda)
+    clo, chi = segment.range_select(starts, queries, torch.device("cpu"))
+    assert lo.tolist() == clo.tolist() and hi.tolist() == chi.tolist()
+    assert (lo[0], hi[0]) == (12, 15)
+    keys = segment.pack_keys([0, 1, 2], [1, 1, 0], [25, 26, 27], swarm=3)
+    h = segment.key_hash(torch.from_numpy(keys).to(cuda)).cpu().numpy().view(np.uint64)
+    assert np.array_equal(h, segment.key_hash_host(keys.view(np.uint32)))
+    tab = segment.DeviceSegmentTable(1000, cuda)
+    ks = segment.pack_keys(np.arange(500) % 5, np.arange(500) % 2, np.arange(500), swarm=1)
+    assert tab.insert(ks, np.arange(500) * 7).all()
+    got = tab.lookup(ks)
+    assert got.tolist() == (np.arange(500) * 7).tolist()
+    miss = segment.pack_keys([9], [9], [9], swarm=1)
+    assert tab.lookup(miss).tolist() == [-1]
+    assert tab.erase(ks[:10]).tolist() == (np.arange(10) * 7).tolist()
+    assert tab.lookup(ks[:12]).tolist() == [-1] * 10 + [70, 77]
+
+
+def test_copy_segments(cuda):
+    src = torch.randint(0, 256, (1 << 20,), dtype=torch.uint8, device=cuda)
+    dst = torch.zeros_like(src)
+    so, do, n = [0, 1000, 70001, 500000], [16, 300000, 400001, 900000], [70000, 3, 200000, 100000]
+    segment.copy_segments(src, dst, so, do, n)
+    for a, b, c in zip(so, do, n):
+        assert torch.equal(dst[b:b + c], src[a:a + c])
