@@ -1,0 +1,117 @@
+"""PeerAgent — the ``streamroot-p2p`` module contract, backed by a :class:`SwarmNode`.
+
+Contract as seen from the reference:
+
+* ``PeerAgent(playerInterface, contentUrl, mediaMap, p2pConfig, SegmentView,
+  PeerAgent.StreamTypes.HLS, 'v2')`` (``lib/hlsjs-p2p-wrapper-private.js:201-224``);
+* ``getSegment(reqInfo{url, headers, withCredentials}, callbacks{onSuccess, onError,
+  onProgress}, segmentView)`` → handle with ``abort()`` (``p2p-loader-generator.js:164``);
+* ``dispose()``, ``setMediaElement(el)`` (``private.js:111,176``);
+* ``stats`` = ``{cdn, p2p, upload, peers}`` (``README.md:232-237``),
+  ``p2pDownloadOn`` / ``p2pUploadOn`` read/write (``hlsjs-p2p-wrapper.js:20-36``).
+
+The swarm is keyed by ``p2pConfig.contentId`` (default: ``contentUrl``,
+``MIGRATION.md:43``).  ``p2pConfig.gpuSwarm`` selects the node backend / device / cache
+size (namespaced so it never collides with the reference's keys).
+"""
+from __future__ import annotations
+
+import logging
+from typing import Any, Dict, Optional
+
+from ..utils.events import JsObject
+from .node import SwarmNode, node_for_config, swarm_id_for
+
+log = logging.getLogger("hlsjs_p2p_wrapper_amd.agent")
+
+
+class PeerAgent:
+    StreamTypes = JsObject(HLS="hls", DASH="dash", SMOOTH="smooth")
+
+    def __init__(self, playerInterface: Any, contentUrl: str, mediaMap: Any, p2pConfig: Dict[str, Any],
+                 SegmentViewClass: Any = None, streamType: str = "hls", integrationVersion: str = "v2",
+                 node: Optional[SwarmNode] = None) -> None:
+        self.player = playerInterface
+        self.contentUrl = contentUrl
+        self.mediaMap = mediaMap
+        self.p2pConfig = p2pConfig if p2pConfig is not None else {}
+        self.SegmentView = SegmentViewClass
+        self.streamType = streamType
+        self.integrationVersion = integrationVersion
+        content_id = self.p2pConfig.get("contentId") if isinstance(self.p2pConfig, dict) else None
+        self.contentId = content_id or contentUrl
+        self.swarm_id = swarm_id_for(str(self.contentId))
+        self.node = node or node_for_config(self.p2pConfig)
+        self.node.attach(self)
+        self.media = None
+        self.currentTrack = None
+        self._stats = {"cdn": 0, "p2p": 0, "upload_base": self.node.stats["upload"], "cache": 0}
+        self.disposed = False
+        self._requests = []
+        if playerInterface is not None and hasattr(playerInterface, "addEventListener"):
+            playerInterface.addEventListener("onTrackChange", self._on_track_change)
+
+    # ------------------------------------------------------------------ contract
+    def getSegment(self, reqInfo: Any, callbacks: Any, segmentView: Any):
+        if self.disposed:
+            raise RuntimeError("PeerAgent is disposed")
+        url = _get(reqInfo, "url")
+        headers = _get(reqInfo, "headers") or {}
+        tv = segmentView.trackView
+        key = (self.swarm_id, int(tv.level or 0), int(tv.urlId or 0), int(segmentView.sn or 0))
+        req = self.node.request(key, url, headers, callbacks, agent=self)
+        return req
+
+    get_segment = getSegment
+
+    def setMediaElement(self, media: Any) -> None:
+        self.media = media
+
+    def dispose(self) -> None:
+        if self.disposed:
+            return
+        self.disposed = True
+        if self.player is not None and hasattr(self.player, "removeEventListener"):
+            self.player.removeEventListener("onTrackChange", self._on_track_change)
+        self.node.detach(self)
+
+    @property
+    def stats(self) -> JsObject:
+        node = self.node
+        peers = int(node.peer_online.sum()) - 1 if node.online else 0
+        return JsObject(cdn=self._stats["cdn"], p2p=self._stats["p2p"],
+                        upload=node.stats["upload"] - self._stats["upload_base"], peers=max(0, peers))
+
+    @property
+    def p2pDownloadOn(self) -> bool:
+        return self.node.download_on
+
+    @p2pDownloadOn.setter
+    def p2pDownloadOn(self, on: bool) -> None:
+        self.node.download_on = bool(on)
+
+    @property
+    def p2pUploadOn(self) -> bool:
+        return self.node.upload_on
+
+    @p2pUploadOn.setter
+    def p2pUploadOn(self, on: bool) -> None:
+        self.node.upload_on = bool(on)
+
+    # ------------------------------------------------------------------ internals
+    def _account(self, source: str, nbytes: int) -> None:
+        if source == "cdn":
+            self._stats["cdn"] += nbytes
+        elif source == "p2p":
+            self._stats["p2p"] += nbytes
+        else:
+            self._stats["cache"] += nbytes
+
+    def _on_track_change(self, data: Any) -> None:
+        self.currentTrack = _get(data, "video")
+
+
+def _get(obj: Any, name: str) -> Any:
+    if isinstance(obj, dict):
+        return obj.get(name)
+    return getattr(obj, name, None)

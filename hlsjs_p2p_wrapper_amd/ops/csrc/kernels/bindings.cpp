@@ -131,7 +131,7 @@ void ts_demux(Tensor buf, Tensor seg_off, Tensor seg_len, Tensor blk_prefix, int
   check(es, "es", torch::kUInt8);
   check(es_off, "es_off", torch::kInt64, B);
   check(pes, "pes", torch::kInt64, B * 3 * max_pes * 3);
-  check(info, "info", torch::kInt64, B * 16);
+  check(info, "info", torch::kInt64, B * 24);
   TORCH_CHECK((reinterpret_cast<uintptr_t>(buf.data_ptr()) & 3) == 0, "buf must be 4-byte aligned");
   ok(D::launch_ts_demux(cptr<uint8_t>(buf), cptr<int64_t>(seg_off), cptr<int64_t>(seg_len),
                         cptr<int64_t>(blk_prefix), static_cast<int>(B), total_blocks, mptr<uint32_t>(meta),

@@ -25,11 +25,11 @@ namespace dev {
 constexpr int kPkt = 188;
 constexpr int kTsThreads = 256;
 constexpr int kClasses = 3;
-constexpr int kInfo = 16;
+constexpr int kInfo = 24;
 constexpr int kPsiScan = 64;
 // info slots / status bits (must match runtime/ts.hpp)
 constexpr int kStatus = 0, kPmtPid = 1, kVideoPid = 2, kNumPackets = 5, kBytes0 = 6, kPes0 = 9, kVideoType = 12,
-              kAudioType = 13, kPayloadBytes = 14;
+              kAudioType = 13, kPayloadBytes = 14, kFirstPts = 16, kLastPts = 19;
 constexpr int64_t kBadSync = 1, kNoPat = 2, kNoPmt = 4, kPesOverflow = 8, kPesHeaderError = 16, kBadLength = 32;
 
 __device__ __forceinline__ int64_t read_pts(const uint8_t* p) {
@@ -121,6 +121,10 @@ __global__ __launch_bounds__(64) void ts_psi_kernel(const uint8_t* __restrict__ 
   inf[kNumPackets] = np;
   inf[kVideoType] = vtype;
   inf[kAudioType] = atype;
+  for (int c = 0; c < kClasses; ++c) {
+    inf[kFirstPts + c] = -1;
+    inf[kLastPts + c] = -1;
+  }
 }
 
 // per-packet meta word: class (2b, 3 = none) | payload start (8b) << 2 | payload len (8b) << 10 | pes (1b) << 18
@@ -300,6 +304,10 @@ __global__ __launch_bounds__(kTsThreads) void ts_gather_kernel(
     dst_b = class_base + es_in_class;
     pes_idx = s_pre[2 * c + 1] + wp + inc_p[c] - pes_flag;
     if (pes_flag) {
+      const int64_t tot_pes = s_tot[2 * c + 1];
+      int64_t* infc = info + static_cast<int64_t>(seg) * kInfo;
+      if (pes_idx == 0) infc[kFirstPts + c] = pts_dts[2 * gpk];
+      if (pes_idx == tot_pes - 1) infc[kLastPts + c] = pts_dts[2 * gpk];
       if (pes_idx < max_pes) {
         int64_t* r = pes + ((static_cast<int64_t>(seg) * kClasses + c) * max_pes + pes_idx) * 3;
         r[0] = es_in_class;

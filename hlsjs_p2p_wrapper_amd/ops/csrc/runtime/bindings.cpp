@@ -343,17 +343,18 @@ PYBIND11_MODULE(_runtime, m) {
         const DirEntry* e = d.find(SegKey{swarm, level, url_id, sn});
         return e ? e->holders : uint64_t(0);
       });
-  // wants: int64[n, 7] = (key4, size, want_id, rank); flags int64[world]
+  // wants: int64[n, 8] = (key4, size, want_id, rank, want_flags); flags int64[world]
   // -> int64[m, 10] = (key4, size, src, dst, want_id, seeded, reserved)
   m.def("plan_round", [](const Directory& d, Arr<int64_t> wants, Arr<int64_t> flags, int world) {
-    const int64_t n = wants.size() / 7;
+    const int64_t n = wants.size() / 8;
     std::vector<Want> w(n);
     const int64_t* p = wants.data();
     for (int64_t i = 0; i < n; ++i) {
-      w[i].key = key_from(p + 7 * i);
-      w[i].size = p[7 * i + 4];
-      w[i].want_id = p[7 * i + 5];
-      w[i].rank = static_cast<int32_t>(p[7 * i + 6]);
+      w[i].key = key_from(p + 8 * i);
+      w[i].size = p[8 * i + 4];
+      w[i].want_id = p[8 * i + 5];
+      w[i].rank = static_cast<int32_t>(p[8 * i + 6]);
+      w[i].flags = p[8 * i + 7];
       if (w[i].rank < 0 || w[i].rank >= world) throw std::invalid_argument("want rank out of range");
     }
     if (flags.size() != world) throw std::invalid_argument("flags must have world entries");

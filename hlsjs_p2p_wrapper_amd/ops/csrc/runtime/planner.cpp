@@ -64,7 +64,7 @@ std::vector<Transfer> plan_round(const Directory& dir, const std::vector<Want>& 
     for (size_t w = i; w < j; ++w) {
       const Want& wt = wants[w];
       const int d = wt.rank;
-      if (!flag(d, kOnline) || !flag(d, kDownloadOn)) {
+      if (!flag(d, kOnline) || !flag(d, kDownloadOn) || (wt.flags & kForceCdn)) {
         cdn.push_back({key, wt.size, -1, d, wt.want_id, 0});
         cdn_total[d] += wt.size;
         continue;

@@ -35,11 +35,14 @@ struct DirEntry {
   int64_t length = 0;
 };
 
+enum WantFlag : int64_t { kForceCdn = 1 };
+
 struct Want {
   SegKey key;
   int64_t size;
   int64_t want_id;
   int32_t rank;
+  int64_t flags = 0;  // WantFlag bits (kForceCdn: a previous peer copy failed its CRC)
 };
 
 struct Transfer {  // one segment moving src -> dst

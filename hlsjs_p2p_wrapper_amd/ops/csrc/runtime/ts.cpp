@@ -360,6 +360,8 @@ void demux_segment(const uint8_t* data, int64_t n, uint8_t* es_out, int64_t* pes
   // --- two passes: sizes, then copy
   int64_t bytes[kClasses] = {0, 0, 0};
   int64_t npes[kClasses] = {0, 0, 0};
+  int64_t first_pts[kClasses] = {-1, -1, -1};
+  int64_t last_pts[kClasses] = {-1, -1, -1};
   for (int pass = 0; pass < 2; ++pass) {
     int64_t base[kClasses] = {0, bytes[0], bytes[0] + bytes[1]};
     int64_t cur[kClasses] = {0, 0, 0};
@@ -386,6 +388,8 @@ void demux_segment(const uint8_t* data, int64_t n, uint8_t* es_out, int64_t* pes
         if ((h[7] & 0x80) && len >= 14) pts = read_pts(h + 9);
         if ((h[7] & 0xC0) == 0xC0 && len >= 19) dts = read_pts(h + 14);
         if (pass == 1) {
+          if (cnt[c] == 0) first_pts[c] = pts;
+          last_pts[c] = pts;
           if (cnt[c] < max_pes) {
             int64_t* r = pes_out + (int64_t(c) * max_pes + cnt[c]) * 3;
             r[0] = cur[c]; r[1] = pts; r[2] = dts;
@@ -404,7 +408,13 @@ void demux_segment(const uint8_t* data, int64_t n, uint8_t* es_out, int64_t* pes
   for (int k = 0; k < kClasses; ++k) {
     info[kVideoBytes + k] = bytes[k];
     info[kNumVideoPes + k] = npes[k];
+    info[kFirstPts + k] = -1;
+    info[kLastPts + k] = -1;
     if (npes[k] > max_pes) status |= kPesOverflow;
+  }
+  for (int k = 0; k < kClasses; ++k) {  // first / last PES PTS (recorded in pass 1)
+    if (npes[k] > 0) info[kFirstPts + k] = first_pts[k];
+    if (npes[k] > 0) info[kLastPts + k] = last_pts[k];
   }
   info[kPayloadBytes] = bytes[0] + bytes[1] + bytes[2];
   info[kStatus] = status;

@@ -17,7 +17,7 @@ namespace ts {
 constexpr int kPacket = 188;
 constexpr int kPsiScanPackets = 64;  // PAT/PMT must appear within the first 64 packets
 constexpr int kClasses = 3;          // 0 video, 1 audio, 2 id3/metadata
-constexpr int kInfoWords = 16;
+constexpr int kInfoWords = 24;
 
 // info[] layout (int64), identical on host and device
 enum Info : int {
@@ -32,6 +32,8 @@ enum Info : int {
   kVideoType = 12,
   kAudioType = 13,
   kPayloadBytes = 14,  // total ES bytes (video+audio+id3)
+  kFirstPts = 16,      // kFirstPts + class: PTS of the class's first PES (-1 if none)
+  kLastPts = 19,       // kLastPts + class: PTS of the class's last PES
 };
 // status bits
 enum Status : int64_t {

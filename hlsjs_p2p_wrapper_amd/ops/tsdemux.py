@@ -27,7 +27,10 @@ PACKET = 188
 CLASSES = ("video", "audio", "id3")
 INFO = {"status": 0, "pmt_pid": 1, "video_pid": 2, "audio_pid": 3, "id3_pid": 4, "n_packets": 5,
         "video_bytes": 6, "audio_bytes": 7, "id3_bytes": 8, "n_video_pes": 9, "n_audio_pes": 10,
-        "n_id3_pes": 11, "video_type": 12, "audio_type": 13, "payload_bytes": 14}
+        "n_id3_pes": 11, "video_type": 12, "audio_type": 13, "payload_bytes": 14,
+        "video_first_pts": 16, "audio_first_pts": 17, "id3_first_pts": 18,
+        "video_last_pts": 19, "audio_last_pts": 20, "id3_last_pts": 21}
+INFO_WORDS = 24
 STATUS = {"bad_sync": 1, "no_pat": 2, "no_pmt": 4, "pes_overflow": 8, "pes_header_error": 16, "bad_length": 32}
 DEFAULT_MAX_PES = 512
 
@@ -72,7 +75,7 @@ def demux_batch(buf: torch.Tensor, offs: Sequence[int], lens: Union[Sequence[int
     if dev.type == "cpu":
         n = lens.numpy().astype(np.int64) if isinstance(lens, torch.Tensor) else cap
         n = np.minimum(np.maximum(n, 0), cap)
-        info = np.zeros((B, 16), dtype=np.int64)
+        info = np.zeros((B, INFO_WORDS), dtype=np.int64)
         pes = np.zeros((B, 3, max_pes, 3), dtype=np.int64)
         _rt().demux_batch(buf.numpy(), o, n, es.numpy(), eo, pes, info, max_pes)
         if isinstance(lens, torch.Tensor):
@@ -94,7 +97,7 @@ def demux_batch(buf: torch.Tensor, offs: Sequence[int], lens: Union[Sequence[int
     meta = torch.empty(nb * 256, dtype=torch.int32, device=dev)
     pts_dts = torch.empty(nb * 256 * 2, dtype=torch.int64, device=dev)
     blk_sums = torch.empty(nb * 6, dtype=torch.int32, device=dev)
-    info = torch.empty((B, 16), dtype=torch.int64, device=dev)
+    info = torch.empty((B, INFO_WORDS), dtype=torch.int64, device=dev)
     pes = torch.empty((B, 3, max_pes, 3), dtype=torch.int64, device=dev)
     _dev().ts_demux(buf, d["o"], n_dev, d["bp"], total_blocks, meta, pts_dts, blk_sums, es, d["eo"], pes, max_pes, info)
     return DemuxResult(info, pes, es, eo)

@@ -1,0 +1,176 @@
+"""Swarm communication backends (the WebRTC-DataChannel + tracker analog).
+
+Interface used by the swarm node (every method is *collective*: all ranks call it in the
+same order, like an RCCL communicator):
+
+* ``allgather_control(msg: np.int64[n]) -> list[np.int64[...]]`` — control plane: the
+  per-round wants / cache deltas / flags.  Tiny and latency bound.
+* ``exchange(sends, recvs)`` — data plane: ``sends = [(dst, tensor)]``,
+  ``recvs = [(src, tensor)]``; per (src, dst) pair the i-th send matches the i-th recv
+  (two-sided, ordered — RCCL point-to-point semantics).
+* ``allreduce_sum(np.int64[n])`` — swarm-wide counters (stats offload ratio, K8).
+
+Backends:
+
+* :class:`LocalComm`  — world of one.
+* :class:`ThreadHub` / :class:`ThreadComm` — N peers as N threads of one process sharing
+  queues and a barrier (the CPU "fake swarm" of SURVEY §4.3); tensors may live on the
+  CPU or all on one GPU (then a transfer is an HBM->HBM copy).
+* :class:`DistComm` — ``torch.distributed``: a **gloo** group carries the control plane
+  on CPU tensors (no GPU sync on the metadata path) and the default group — **nccl, i.e.
+  RCCL over xGMI** on MI355X, gloo in CPU tests — carries segment bytes with
+  ``batch_isend_irecv`` (coalesced: one RCCL group call on the world communicator per
+  round, one contiguous buffer per peer pair).
+"""
+from __future__ import annotations
+
+import threading
+from typing import List, Optional, Sequence, Tuple
+
+import numpy as np
+import torch
+
+
+class SwarmComm:
+    rank: int = 0
+    world_size: int = 1
+
+    def allgather_control(self, msg: np.ndarray) -> List[np.ndarray]:
+        raise NotImplementedError
+
+    def exchange(self, sends: Sequence[Tuple[int, torch.Tensor]], recvs: Sequence[Tuple[int, torch.Tensor]]) -> None:
+        raise NotImplementedError
+
+    def allreduce_sum(self, values: np.ndarray) -> np.ndarray:
+        parts = self.allgather_control(np.asarray(values, dtype=np.int64))
+        return np.sum(np.stack(parts), axis=0)
+
+    def barrier(self) -> None:
+        self.allgather_control(np.zeros(1, dtype=np.int64))
+
+    def close(self) -> None:
+        pass
+
+
+class LocalComm(SwarmComm):
+    def __init__(self) -> None:
+        self.rank = 0
+        self.world_size = 1
+
+    def allgather_control(self, msg: np.ndarray) -> List[np.ndarray]:
+        return [np.asarray(msg, dtype=np.int64).copy()]
+
+    def exchange(self, sends, recvs) -> None:
+        if sends or recvs:
+            raise RuntimeError("LocalComm has no peers")
+
+
+class ThreadHub:
+    """Shared state of an in-process swarm of ``world_size`` peer threads."""
+
+    def __init__(self, world_size: int, timeout: float = 120.0) -> None:
+        self.world_size = world_size
+        self.timeout = timeout
+        self._barrier = threading.Barrier(world_size)
+        self._slots: List[Optional[np.ndarray]] = [None] * world_size
+        self._mail: dict = {}
+        self._lock = threading.Lock()
+
+    def comm(self, rank: int) -> "ThreadComm":
+        return ThreadComm(self, rank)
+
+    def wait(self) -> None:
+        self._barrier.wait(self.timeout)
+
+    def abort(self) -> None:
+        self._barrier.abort()
+
+
+class ThreadComm(SwarmComm):
+    def __init__(self, hub: ThreadHub, rank: int) -> None:
+        self.hub = hub
+        self.rank = rank
+        self.world_size = hub.world_size
+
+    def allgather_control(self, msg: np.ndarray) -> List[np.ndarray]:
+        hub = self.hub
+        hub._slots[self.rank] = np.asarray(msg, dtype=np.int64).copy()
+        hub.wait()
+        out = [s.copy() for s in hub._slots]  # type: ignore[union-attr]
+        hub.wait()
+        return out
+
+    def exchange(self, sends, recvs) -> None:
+        hub = self.hub
+        with hub._lock:
+            for dst, t in sends:
+                hub._mail.setdefault((self.rank, dst), []).append(t)
+        hub.wait()
+        per_src: dict = {}
+        for src, t in recvs:
+            q = hub._mail.get((src, self.rank), [])
+            i = per_src.get(src, 0)
+            if i >= len(q):
+                raise RuntimeError(f"rank {self.rank}: no matching send from {src}")
+            s = q[i]
+            per_src[src] = i + 1
+            if s.numel() != t.numel():
+                raise RuntimeError(f"rank {self.rank}: size mismatch from {src}: {s.numel()} != {t.numel()}")
+            t.copy_(s.to(t.device), non_blocking=False)
+        hub.wait()
+        with hub._lock:
+            for src in range(self.world_size):
+                hub._mail.pop((src, self.rank), None)
+        hub.wait()
+
+
+class DistComm(SwarmComm):
+    """torch.distributed backend: gloo control group + default (RCCL/gloo) data group."""
+
+    def __init__(self, control_group=None, data_group=None) -> None:
+        import torch.distributed as dist
+
+        if not dist.is_initialized():
+            raise RuntimeError("torch.distributed is not initialized")
+        self.dist = dist
+        self.rank = dist.get_rank()
+        self.world_size = dist.get_world_size()
+        backend = dist.get_backend()
+        if control_group is None:
+            control_group = dist.new_group(backend="gloo") if backend != "gloo" else None
+        self.control_group = control_group
+        self.data_group = data_group
+
+    def allgather_control(self, msg: np.ndarray) -> List[np.ndarray]:
+        dist = self.dist
+        msg = np.asarray(msg, dtype=np.int64)
+        n = torch.tensor([msg.size], dtype=torch.int64)
+        sizes = [torch.zeros(1, dtype=torch.int64) for _ in range(self.world_size)]
+        dist.all_gather(sizes, n, group=self.control_group)
+        mx = int(max(int(s.item()) for s in sizes))
+        buf = torch.zeros(max(mx, 1), dtype=torch.int64)
+        buf[:msg.size] = torch.from_numpy(msg)
+        outs = [torch.zeros(max(mx, 1), dtype=torch.int64) for _ in range(self.world_size)]
+        dist.all_gather(outs, buf, group=self.control_group)
+        return [o[:int(s.item())].numpy().copy() for o, s in zip(outs, sizes)]
+
+    def exchange(self, sends, recvs) -> None:
+        dist = self.dist
+        ops = []
+        for dst, t in sends:
+            ops.append(dist.P2POp(dist.isend, t, dst, group=self.data_group))
+        for src, t in recvs:
+            ops.append(dist.P2POp(dist.irecv, t, src, group=self.data_group))
+        if not ops:
+            return
+        reqs = dist.batch_isend_irecv(ops)
+        for r in reqs:
+            r.wait()
+
+    def allreduce_sum(self, values: np.ndarray) -> np.ndarray:
+        t = torch.from_numpy(np.asarray(values, dtype=np.int64).copy())
+        self.dist.all_reduce(t, group=self.control_group)
+        return t.numpy()
+
+    def barrier(self) -> None:
+        self.dist.barrier(group=self.control_group)

@@ -1,0 +1,648 @@
+"""Player controllers: playlist / level / key / fragment loading and the stream loop.
+
+These recreate the slice of hls.js the reference wrapper depends on:
+``MANIFEST_LOADING`` → ``MANIFEST_LOADED`` → ``MANIFEST_PARSED``, level switching
+(``LEVEL_SWITCH``, ``LEVEL_LOADING``/``LOADED`` with live reloads), key loading through
+the *default* loader (never the P2P ``fLoader``, ``private.js:82-85``), fragment loading
+through ``config.fLoader`` with the exact 10-argument call
+(``p2p-loader-generator.js:52``), ``FRAG_LOAD_PROGRESS``/``FRAG_LOADED``, batched
+decrypt+demux (:mod:`.transmux`), buffer append and ``FRAG_BUFFERED``.
+
+Extension over hls.js: ``config.maxFragLoadsInFlight`` fragments may load concurrently
+(1 = hls.js behaviour), so a serving deployment moves many segments per swarm round.
+"""
+from __future__ import annotations
+
+import bisect
+import logging
+from typing import Any, Dict, List, Optional, Tuple
+
+from ..net.event_loop import get_event_loop
+from ..utils.events import JsObject
+from .events import ErrorDetails, ErrorTypes, Events
+from .level import Fragment, Level, LevelDetails
+from .playlist import PlaylistError, is_master, parse_master, parse_media
+from .transmux import TransmuxJob, default_transmux_device, pipeline_for
+
+log = logging.getLogger("hlsjs_p2p_wrapper_amd.player")
+
+
+def _loader_class(cfg, key: str):
+    cls = cfg.get(key)
+    return cls if cls is not None else cfg.get("loader")
+
+
+# ---------------------------------------------------------------------------- playlists
+class PlaylistLoader:
+    def __init__(self, hls) -> None:
+        self.hls = hls
+        self.loaders: Dict[str, Any] = {}
+        hls.on(Events.MANIFEST_LOADING, self.onManifestLoading)
+        hls.on(Events.LEVEL_LOADING, self.onLevelLoading)
+
+    def destroy(self) -> None:
+        for l in self.loaders.values():
+            l.destroy()
+        self.loaders.clear()
+
+    def _load(self, kind: str, url: str, ctx: dict) -> None:
+        cfg = self.hls.config
+        old = self.loaders.pop(kind, None)
+        if old is not None:
+            old.abort()
+        loader = _loader_class(cfg, "pLoader")(cfg)
+        self.loaders[kind] = loader
+        if kind == "manifest":
+            timeout, retry, delay = cfg.manifestLoadingTimeOut, cfg.manifestLoadingMaxRetry, cfg.manifestLoadingRetryDelay
+        else:
+            timeout, retry, delay = cfg.levelLoadingTimeOut, cfg.levelLoadingMaxRetry, cfg.levelLoadingRetryDelay
+        loader.load(url, "text", lambda e, s: self._success(kind, url, ctx, e, s),
+                    lambda e: self._error(kind, url, ctx, e), lambda e, s: self._timeout(kind, url, ctx, e, s),
+                    timeout, retry, delay)
+
+    def onManifestLoading(self, event: str, data: Any) -> None:
+        self._load("manifest", data["url"], {})
+
+    def onLevelLoading(self, event: str, data: Any) -> None:
+        self._load("level", data["url"], {"level": data["level"], "id": data.get("id", 0)})
+
+    def _success(self, kind: str, url: str, ctx: dict, event: Any, stats: Any) -> None:
+        self.loaders.pop(kind, None)
+        text = event.currentTarget.response
+        if isinstance(text, (bytes, bytearray)):
+            text = text.decode()
+        hls = self.hls
+        stats.tparsed = hls.loop.now()
+        try:
+            if kind == "manifest":
+                if is_master(text):
+                    levels = parse_master(text, url)
+                    hls.trigger(Events.MANIFEST_LOADED, {"levels": levels, "url": url, "stats": stats})
+                else:  # a media playlist given directly: one level
+                    details = parse_media(text, url, 0)
+                    lvl = Level(url=[url], bitrate=0)
+                    hls.trigger(Events.MANIFEST_LOADED, {"levels": [lvl], "url": url, "stats": stats})
+                    hls.trigger(Events.LEVEL_LOADED, {"details": details, "level": 0, "id": 0, "stats": stats})
+            else:
+                details = parse_media(text, url, ctx["level"])
+                details.tload = stats.tload or hls.loop.now()
+                hls.trigger(Events.LEVEL_LOADED, {"details": details, "level": ctx["level"], "id": ctx["id"],
+                                                  "stats": stats})
+        except PlaylistError as e:
+            det = ErrorDetails.MANIFEST_PARSING_ERROR if kind == "manifest" else ErrorDetails.LEVEL_LOAD_ERROR
+            hls.trigger(Events.ERROR, {"type": ErrorTypes.NETWORK_ERROR, "details": det, "fatal": True,
+                                       "url": url, "reason": str(e)})
+
+    def _error(self, kind: str, url: str, ctx: dict, event: Any) -> None:
+        self.loaders.pop(kind, None)
+        if kind == "manifest":
+            self.hls.trigger(Events.ERROR, {"type": ErrorTypes.NETWORK_ERROR,
+                                            "details": ErrorDetails.MANIFEST_LOAD_ERROR, "fatal": True, "url": url,
+                                            "response": event})
+        else:
+            self.hls.trigger(Events.ERROR, {"type": ErrorTypes.NETWORK_ERROR,
+                                            "details": ErrorDetails.LEVEL_LOAD_ERROR, "fatal": False, "url": url,
+                                            "level": ctx["level"], "response": event})
+
+    def _timeout(self, kind: str, url: str, ctx: dict, event: Any, stats: Any) -> None:
+        loader = self.loaders.pop(kind, None)
+        if loader is not None:
+            loader.abort()
+        det = ErrorDetails.MANIFEST_LOAD_TIMEOUT if kind == "manifest" else ErrorDetails.LEVEL_LOAD_TIMEOUT
+        self.hls.trigger(Events.ERROR, {"type": ErrorTypes.NETWORK_ERROR, "details": det,
+                                        "fatal": kind == "manifest", "url": url, "level": ctx.get("level")})
+
+
+# ---------------------------------------------------------------------------- levels
+class LevelController:
+    def __init__(self, hls) -> None:
+        self.hls = hls
+        self._levels: Optional[List[Level]] = None
+        self._level = -1
+        self._manualLevel = -1
+        self.firstLevel = 0
+        self._reload_timer = None
+        hls.on(Events.MANIFEST_LOADED, self.onManifestLoaded)
+        hls.on(Events.LEVEL_LOADED, self.onLevelLoaded)
+        hls.on(Events.ERROR, self.onError)
+
+    def destroy(self) -> None:
+        if self._reload_timer is not None:
+            self._reload_timer.cancel()
+            self._reload_timer = None
+
+    @property
+    def levels(self) -> Optional[List[Level]]:
+        return self._levels
+
+    def onManifestLoaded(self, event: str, data: Any) -> None:
+        self._levels = list(data["levels"])
+        start = self.hls.config.get("startLevel")
+        self.firstLevel = start if isinstance(start, int) and 0 <= start < len(self._levels) else 0
+        self.hls.trigger(Events.MANIFEST_PARSED, {"levels": self._levels, "firstLevel": self.firstLevel,
+                                                  "stats": data.get("stats")})
+
+    @property
+    def level(self) -> int:
+        return self._level
+
+    @level.setter
+    def level(self, new: int) -> None:
+        levels = self._levels
+        if not levels or not (0 <= new < len(levels)):
+            self.hls.trigger(Events.ERROR, {"type": ErrorTypes.OTHER_ERROR,
+                                            "details": ErrorDetails.LEVEL_SWITCH_ERROR, "level": new,
+                                            "fatal": False, "reason": "invalid level idx"})
+            return
+        if self._level != new or levels[new].details is None:
+            self._set_level(new)
+
+    def _set_level(self, new: int) -> None:
+        if self._reload_timer is not None:
+            self._reload_timer.cancel()
+            self._reload_timer = None
+        switched = self._level != new
+        self._level = new
+        lvl = self._levels[new]  # type: ignore[index]
+        if switched:
+            self.hls.trigger(Events.LEVEL_SWITCH, {"level": new})
+        if lvl.details is None or lvl.details.live:
+            self._request(new)
+
+    def _request(self, idx: int) -> None:
+        lvl = self._levels[idx]  # type: ignore[index]
+        url_id = lvl.urlId if 0 <= lvl.urlId < len(lvl.url) else 0
+        self.hls.trigger(Events.LEVEL_LOADING, {"url": lvl.url[url_id], "level": idx, "id": url_id})
+
+    @property
+    def manualLevel(self) -> int:
+        return self._manualLevel
+
+    @manualLevel.setter
+    def manualLevel(self, v: int) -> None:
+        self._manualLevel = v
+        if v != -1:
+            self.level = v
+
+    def onLevelLoaded(self, event: str, data: Any) -> None:
+        idx = data["level"]
+        levels = self._levels
+        if not levels or idx >= len(levels):
+            return
+        lvl = levels[idx]
+        details: LevelDetails = data["details"]
+        old = lvl.details
+        if old is not None and old.fragments and details.fragments:
+            # keep Fragment identity for sn present in both (in-flight loads refer to them)
+            by_sn = {f.sn: f for f in old.fragments}
+            merged = []
+            for f in details.fragments:
+                o = by_sn.get(f.sn)
+                if o is not None:
+                    o.start, o.duration, o.url = f.start, f.duration, f.url
+                    merged.append(o)
+                else:
+                    merged.append(f)
+            details.fragments = merged
+        lvl.details = details
+        self.hls.trigger(Events.LEVEL_UPDATED, {"details": details, "level": idx})
+        if details.live and idx == self._level:
+            interval = 1000.0 * (details.averagetargetduration or details.targetduration or 1.0)
+            self._reload_timer = self.hls.loop.set_timeout(self._reload, interval, idx)
+
+    def _reload(self, idx: int) -> None:
+        self._reload_timer = None
+        if idx == self._level and self._levels:
+            self._request(idx)
+
+    def onError(self, event: str, data: Any) -> None:
+        det = data.get("details")
+        if det in (ErrorDetails.LEVEL_LOAD_ERROR, ErrorDetails.LEVEL_LOAD_TIMEOUT, ErrorDetails.FRAG_LOAD_ERROR,
+                   ErrorDetails.FRAG_LOAD_TIMEOUT):
+            idx = data.get("level")
+            if idx is None and data.get("frag") is not None:
+                idx = data["frag"].level
+            if idx is None or not self._levels or idx >= len(self._levels):
+                return
+            lvl = self._levels[idx]
+            if len(lvl.url) > 1:  # redundant stream failover: next urlId is a different track
+                lvl.urlId = (lvl.urlId + 1) % len(lvl.url)
+                data["fatal"] = False
+                if det in (ErrorDetails.LEVEL_LOAD_ERROR, ErrorDetails.LEVEL_LOAD_TIMEOUT):
+                    self._request(idx)
+
+
+# ---------------------------------------------------------------------------- keys
+class KeyLoader:
+    def __init__(self, hls) -> None:
+        self.hls = hls
+        self.keys: Dict[str, bytes] = {}
+        self._pending: Dict[str, List[Fragment]] = {}
+        self.loaders: Dict[str, Any] = {}
+        hls.on(Events.KEY_LOADING, self.onKeyLoading)
+
+    def destroy(self) -> None:
+        for l in self.loaders.values():
+            l.destroy()
+        self.loaders.clear()
+
+    def onKeyLoading(self, event: str, data: Any) -> None:
+        frag: Fragment = data["frag"]
+        dd = frag.decryptdata
+        uri = dd.uri
+        if uri in self.keys:
+            dd.key = self.keys[uri]
+            self.hls.trigger(Events.KEY_LOADED, {"frag": frag})
+            return
+        waiting = self._pending.setdefault(uri, [])
+        waiting.append(frag)
+        if len(waiting) > 1:
+            return
+        cfg = self.hls.config
+        loader = cfg.loader(cfg)  # the default loader: keys never go through the P2P fLoader
+        self.loaders[uri] = loader
+        loader.load(uri, "arraybuffer", lambda e, s: self._ok(uri, e), lambda e: self._fail(uri, e, False),
+                    lambda e, s: self._fail(uri, e, True), cfg.fragLoadingTimeOut, cfg.fragLoadingMaxRetry,
+                    cfg.fragLoadingRetryDelay)
+
+    def _ok(self, uri: str, event: Any) -> None:
+        self.loaders.pop(uri, None)
+        key = event.currentTarget.response
+        if not isinstance(key, (bytes, bytearray)):
+            key = bytes(memoryview(key.numpy() if hasattr(key, "numpy") else key))
+        key = bytes(key)
+        self.keys[uri] = key
+        for frag in self._pending.pop(uri, []):
+            frag.decryptdata.key = key
+            self.hls.trigger(Events.KEY_LOADED, {"frag": frag})
+
+    def _fail(self, uri: str, event: Any, timeout: bool) -> None:
+        loader = self.loaders.pop(uri, None)
+        if loader is not None:
+            loader.abort()
+        for frag in self._pending.pop(uri, []):
+            self.hls.trigger(Events.ERROR, {"type": ErrorTypes.NETWORK_ERROR,
+                                            "details": ErrorDetails.KEY_LOAD_TIMEOUT if timeout else
+                                            ErrorDetails.KEY_LOAD_ERROR, "fatal": False, "frag": frag,
+                                            "response": event})
+
+
+# ---------------------------------------------------------------------------- fragments
+class FragmentLoader:
+    """Creates one ``config.fLoader`` (or ``config.loader``) per fragment and calls it with
+    the hls.js 10-argument signature."""
+
+    def __init__(self, hls) -> None:
+        self.hls = hls
+        self.loaders: Dict[int, Any] = {}
+        hls.on(Events.FRAG_LOADING, self.onFragLoading)
+
+    def destroy(self) -> None:
+        for l in list(self.loaders.values()):
+            l.destroy()
+        self.loaders.clear()
+
+    def abort(self, frag: Fragment) -> None:
+        loader = self.loaders.pop(id(frag), None)
+        if loader is not None:
+            loader.abort()
+        frag.loader = None
+
+    def onFragLoading(self, event: str, data: Any) -> None:
+        frag: Fragment = data["frag"]
+        frag.loaded = 0
+        cfg = self.hls.config
+        cls = _loader_class(cfg, "fLoader")
+        loader = cls(cfg)
+        frag.loader = loader
+        self.loaders[id(frag)] = loader
+        loader.load(frag.url, "arraybuffer", lambda e, s: self._success(frag, e, s), lambda e: self._error(frag, e),
+                    lambda e, s: self._timeout(frag, e, s), cfg.fragLoadingTimeOut, cfg.fragLoadingMaxRetry,
+                    cfg.fragLoadingRetryDelay, lambda e, s: self._progress(frag, e, s), frag)
+
+    def _success(self, frag: Fragment, event: Any, stats: Any) -> None:
+        payload = event.currentTarget.response if hasattr(event, "currentTarget") else event["currentTarget"]["response"]
+        stats.length = _byte_length(payload)
+        self.loaders.pop(id(frag), None)
+        frag.loader = None
+        self.hls.trigger(Events.FRAG_LOADED, {"payload": payload, "frag": frag, "stats": stats})
+
+    def _error(self, frag: Fragment, event: Any) -> None:
+        loader = self.loaders.pop(id(frag), None)
+        if loader is not None:
+            loader.abort()
+        self.hls.trigger(Events.ERROR, {"type": ErrorTypes.NETWORK_ERROR, "details": ErrorDetails.FRAG_LOAD_ERROR,
+                                        "fatal": False, "frag": frag, "response": event})
+
+    def _timeout(self, frag: Fragment, event: Any, stats: Any) -> None:
+        loader = self.loaders.pop(id(frag), None)
+        if loader is not None:
+            loader.abort()
+        self.hls.trigger(Events.ERROR, {"type": ErrorTypes.NETWORK_ERROR, "details": ErrorDetails.FRAG_LOAD_TIMEOUT,
+                                        "fatal": False, "frag": frag})
+
+    def _progress(self, frag: Fragment, event: Any, stats: Any) -> None:
+        frag.loaded = stats.loaded
+        self.hls.trigger(Events.FRAG_LOAD_PROGRESS, {"frag": frag, "stats": stats})
+
+
+def _byte_length(payload: Any) -> int:
+    if payload is None:
+        return 0
+    if hasattr(payload, "numel"):
+        return int(payload.numel())
+    if hasattr(payload, "nbytes"):
+        return int(payload.nbytes)
+    return len(payload)
+
+
+# ---------------------------------------------------------------------------- stream
+class StreamController:
+    STOPPED, IDLE, ERROR, ENDED = "STOPPED", "IDLE", "ERROR", "ENDED"
+
+    def __init__(self, hls) -> None:
+        self.hls = hls
+        self.loop = hls.loop
+        self.state = self.STOPPED
+        self.inflight: Dict[Tuple[int, int], Fragment] = {}
+        self.fragPrevious: Optional[Fragment] = None
+        self.fragLastKbps = 0
+        self.stats = None
+        self.startPosition = -1.0
+        self._start_pending = False
+        self._timer = None
+        self._retry: Dict[Tuple[int, int], int] = {}
+        self._retry_until = 0.0
+        self._eos = False
+        self._init_levels: set = set()
+        self._starts_cache: Tuple[int, int, List[float]] = (0, 0, [])
+        self.fragments_buffered = 0
+        self.bytes_buffered = 0
+        on = hls.on
+        on(Events.MEDIA_ATTACHED, self.onMediaAttached)
+        on(Events.MEDIA_DETACHING, self.onMediaDetaching)
+        on(Events.MANIFEST_PARSED, self.onManifestParsed)
+        on(Events.LEVEL_LOADED, lambda e, d: self._kick())
+        on(Events.KEY_LOADED, self.onKeyLoaded)
+        on(Events.FRAG_LOADED, self.onFragLoaded)
+        on(Events.ERROR, self.onError)
+
+    # ------------------------------------------------------------ lifecycle
+    def destroy(self) -> None:
+        self.stopLoad()
+
+    def startLoad(self, startPosition: float = -1) -> None:
+        self.startPosition = float(startPosition if startPosition is not None else -1)
+        self._start_pending = True
+        self.state = self.IDLE
+        self._eos = False
+        if self._timer is None:
+            self._timer = self.loop.set_interval(self.tick, self.hls.config.get("tickInterval", 100))
+        self._kick()
+
+    def stopLoad(self) -> None:
+        for frag in list(self.inflight.values()):
+            self.hls.fragmentLoader.abort(frag)
+        self.inflight.clear()
+        if self._timer is not None:
+            self._timer.cancel()
+            self._timer = None
+        self.state = self.STOPPED
+
+    def _kick(self) -> None:
+        if self.state not in (self.STOPPED, self.ERROR):
+            self.loop.call_soon(self.tick)
+
+    def onMediaAttached(self, event: str, data: Any) -> None:
+        media = data["media"]
+        media.on("seeking", self._on_seeking)
+        media.on("ended", self._on_ended)
+        self._kick()
+
+    def onMediaDetaching(self, event: str, data: Any) -> None:
+        media = self.hls.media
+        if media is not None:
+            media.remove_listener("seeking", self._on_seeking)
+            media.remove_listener("ended", self._on_ended)
+
+    def onManifestParsed(self, event: str, data: Any) -> None:
+        self.hls.levelController.level = data["firstLevel"]
+        if self.hls.config.autoStartLoad:
+            self.startLoad(self.hls.config.startPosition)
+
+    def _on_seeking(self) -> None:
+        media = self.hls.media
+        pos = media.currentTime
+        for key, frag in list(self.inflight.items()):
+            if not (frag.start - 0.5 <= pos < frag.end + 0.5) and frag.end <= pos or frag.start > pos + 60:
+                self.hls.fragmentLoader.abort(frag)
+                self.inflight.pop(key, None)
+        self._eos = False
+        if self.state == self.ENDED:
+            self.state = self.IDLE
+        self._kick()
+
+    def _on_ended(self) -> None:
+        self.state = self.ENDED
+
+    # ------------------------------------------------------------ buffering loop
+    def _frag_at(self, details: LevelDetails, t: float) -> Optional[Fragment]:
+        frags = details.fragments
+        if not frags:
+            return None
+        key = (id(frags), len(frags))
+        if self._starts_cache[:2] != key:
+            self._starts_cache = (key[0], key[1], [f.start for f in frags])
+        starts = self._starts_cache[2]
+        tol = self.hls.config.get("maxFragLookUpTolerance", 0.2)
+        i = bisect.bisect_right(starts, t + tol) - 1
+        if i < 0:
+            return frags[0] if details.live else frags[0]
+        f = frags[i]
+        if t >= f.end - 1e-6:
+            return frags[i + 1] if i + 1 < len(frags) else None
+        return f
+
+    def _live_start(self, details: LevelDetails) -> float:
+        cfg = self.hls.config
+        if cfg.get("liveSyncDuration") is not None:
+            back = float(cfg.liveSyncDuration)
+        else:
+            back = float(cfg.get("liveSyncDurationCount", 3)) * (details.targetduration or 1.0)
+        start = details.fragments[0].start if details.fragments else 0.0
+        return max(start, details.totalduration - back)
+
+    def tick(self) -> None:
+        hls = self.hls
+        if self.state in (self.STOPPED, self.ERROR):
+            return
+        media = hls.media
+        levels = hls.levels
+        if media is None or not levels:
+            return
+        if self.loop.now() < self._retry_until:
+            return
+        lvl_idx = hls.nextLoadLevel
+        lc = hls.levelController
+        if lvl_idx != lc.level:
+            lc.level = lvl_idx
+        level = levels[lvl_idx]
+        details = level.details
+        if details is None:
+            return
+        if self._start_pending:
+            self._start_pending = False
+            if self.startPosition >= 0:
+                pos0 = self.startPosition
+            elif details.live:
+                pos0 = self._live_start(details)
+            else:
+                pos0 = 0.0
+            if abs(media.currentTime - pos0) > 1e-9:
+                media.currentTime = pos0
+        cfg = hls.config
+        pos = media.currentTime
+        buf_end = pos
+        for s, e in media.buffered:
+            if s - cfg.maxBufferHole <= pos < e:
+                buf_end = e
+                break
+        bitrate = level.bitrate or 1
+        max_buf = max(8.0 * (cfg.maxBufferSize or 0) / bitrate, float(cfg.maxBufferLength))
+        max_buf = min(max_buf, float(cfg.maxMaxBufferLength))
+        max_inflight = max(1, int(cfg.get("maxFragLoadsInFlight", 1) or 1))
+        nxt = buf_end
+        for f in self.inflight.values():
+            if f.end > nxt and f.start <= nxt + 0.5:
+                nxt = f.end
+        while len(self.inflight) < max_inflight and nxt - pos < max_buf:
+            frag = self._frag_at(details, nxt)
+            if frag is None:
+                if not details.live and nxt >= details.totalduration - 0.05 and not self.inflight and not self._eos:
+                    self._eos = True
+                    media.duration = details.totalduration
+                    hls.trigger(Events.BUFFER_EOS, {})
+                break
+            key = (frag.level, frag.sn)
+            if key in self.inflight:
+                nxt = frag.end
+                continue
+            self._load(frag)
+            nxt = frag.end
+
+    def _load(self, frag: Fragment) -> None:
+        frag.loadCounter += 1
+        frag.autoLevel = self.hls.autoLevelEnabled
+        self.inflight[(frag.level, frag.sn)] = frag
+        dd = frag.decryptdata
+        if dd is not None and dd.needs_key:
+            self.hls.trigger(Events.KEY_LOADING, {"frag": frag})
+        else:
+            self.hls.trigger(Events.FRAG_LOADING, {"frag": frag})
+
+    def onKeyLoaded(self, event: str, data: Any) -> None:
+        frag = data["frag"]
+        if self.inflight.get((frag.level, frag.sn)) is frag:
+            self.hls.trigger(Events.FRAG_LOADING, {"frag": frag})
+
+    def onFragLoaded(self, event: str, data: Any) -> None:
+        frag: Fragment = data["frag"]
+        if self.inflight.get((frag.level, frag.sn)) is not frag:
+            return  # aborted / stale
+        self.stats = data["stats"]
+        self._retry.pop((frag.level, frag.sn), None)
+        dd = frag.decryptdata
+        key = dd.key if (dd is not None and dd.method == "AES-128") else None
+        iv = frag.iv_for_decrypt() if key is not None else None
+        stats = data["stats"]
+        payload = data["payload"]
+        dev = self.hls.transmux_device(payload)
+        pipeline_for(dev, self.loop).submit(
+            TransmuxJob(payload, key, iv, lambda r: self._on_parsed(frag, stats, r), frag))
+
+    def _on_parsed(self, frag: Fragment, stats: Any, r: Dict[str, Any]) -> None:
+        hls = self.hls
+        key = (frag.level, frag.sn)
+        if self.inflight.get(key) is not frag:
+            return
+        if r.get("error") is not None or r.get("status", 0) & 0b111111:
+            self.inflight.pop(key, None)
+            details = ErrorDetails.FRAG_DECRYPT_ERROR if r.get("plain_bytes", 0) < 0 else ErrorDetails.FRAG_PARSING_ERROR
+            hls.trigger(Events.ERROR, {"type": ErrorTypes.MEDIA_ERROR, "details": details, "fatal": False,
+                                       "frag": frag, "reason": str(r.get("error") or r.get("status"))})
+            self._kick()
+            return
+        info = r["info"]
+        if frag.level not in self._init_levels:
+            self._init_levels.add(frag.level)
+            hls.trigger(Events.FRAG_PARSING_INIT_SEGMENT, {"frag": frag, "tracks": {
+                "video": {"pid": info["video_pid"], "type": info["video_type"]},
+                "audio": {"pid": info["audio_pid"], "type": info["audio_type"]}}})
+        if r["id3"].numel():
+            hls.trigger(Events.FRAG_PARSING_METADATA, {"frag": frag, "samples": r["id3"]})
+        vfirst, vlast, nv = info["video_first_pts"], info["video_last_pts"], info["n_video_pes"]
+        if vfirst >= 0 and vlast >= vfirst and nv > 1:
+            frame = (vlast - vfirst) / (nv - 1)
+            dur = (vlast - vfirst + frame) / 90000.0
+        else:
+            dur = frag.duration
+        start = frag.start
+        end = start + dur
+        hls.trigger(Events.FRAG_PARSING_DATA, {"frag": frag, "type": "video", "startPTS": start, "endPTS": end,
+                                               "data1": r["video"], "nb": nv, "pts": (vfirst, vlast)})
+        hls.trigger(Events.FRAG_PARSING_DATA, {"frag": frag, "type": "audio", "startPTS": start, "endPTS": end,
+                                               "data1": r["audio"], "nb": info["n_audio_pes"],
+                                               "pts": (info["audio_first_pts"], info["audio_last_pts"])})
+        hls.trigger(Events.FRAG_PARSED, {"frag": frag})
+        media = hls.media
+        nbytes = int(r["video"].numel() + r["audio"].numel())
+        hls.trigger(Events.BUFFER_APPENDING, {"type": "video", "parent": "main", "bytes": nbytes})
+        if media is not None:
+            retain = (r["video"], r["audio"]) if hls.config.get("retainMediaData") else None
+            if retain is not None:
+                media.retain = True
+            media.append(start, end, nbytes, retain)
+        now = self.loop.now()
+        stats.tbuffered = now
+        tfirst = stats.tfirst if stats.tfirst is not None else stats.trequest
+        dt = max(now - tfirst, 1e-3)
+        self.fragLastKbps = round(8 * (stats.length or 0) / dt)
+        self.inflight.pop(key, None)
+        self.fragPrevious = frag
+        self.fragments_buffered += 1
+        self.bytes_buffered += int(stats.length or 0)
+        hls.trigger(Events.BUFFER_APPENDED, {"parent": "main", "pending": 0})
+        hls.trigger(Events.FRAG_BUFFERED, {"stats": stats, "frag": frag})
+        self._kick()
+
+    def onError(self, event: str, data: Any) -> None:
+        det = data.get("details")
+        frag = data.get("frag")
+        if det in (ErrorDetails.FRAG_LOAD_ERROR, ErrorDetails.FRAG_LOAD_TIMEOUT, ErrorDetails.KEY_LOAD_ERROR,
+                   ErrorDetails.KEY_LOAD_TIMEOUT) and frag is not None:
+            key = (frag.level, frag.sn)
+            self.inflight.pop(key, None)
+            n = self._retry.get(key, 0) + 1
+            cfg = self.hls.config
+            if det == ErrorDetails.FRAG_LOAD_ERROR and not data.get("fatal") and len(
+                    self.hls.levels[frag.level].url) <= 1:
+                # the loader already retried maxRetry times with back-off: give up
+                data["fatal"] = True
+            elif n <= cfg.fragLoadingMaxRetry:
+                self._retry[key] = n
+                delay = min(2 ** (n - 1) * cfg.fragLoadingRetryDelay, 64000)
+                self._retry_until = self.loop.now() + delay
+                self.loop.set_timeout(self._kick, delay)
+                return
+            else:
+                data["fatal"] = True
+            if data.get("fatal"):
+                # escalate in place (listeners registered after the controllers — i.e. the
+                # application — observe fatal=True on this same ERROR event)
+                log.error("fragment sn=%s level=%s failed: %s", frag.sn, frag.level, det)
+                self.state = self.ERROR
+            else:
+                self._kick()
+        elif data.get("fatal") and det in (ErrorDetails.MANIFEST_LOAD_ERROR, ErrorDetails.MANIFEST_LOAD_TIMEOUT,
+                                           ErrorDetails.MANIFEST_PARSING_ERROR):
+            self.state = self.ERROR

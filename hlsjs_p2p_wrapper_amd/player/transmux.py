@@ -1,0 +1,189 @@
+"""Batched decrypt + demux stage between ``FRAG_LOADED`` and the buffer (hls.js's
+decrypter + TS demuxer, moved onto the MI355X).
+
+Every fragment loaded during one event-loop iteration — typically all fragments
+completed by one swarm exchange round — is decrypted by ONE AES-CBC launch and demuxed
+by ONE demux launch sequence, then a single small device->host copy of the per-segment
+``info`` rows delivers timing/status to the players.  Payloads that are views of the
+node's HBM arena are consumed in place (no copy); host payloads (default CDN loader) are
+staged with one H2D copy.
+
+The batching point is per (thread, device): the peer threads of an in-process swarm each
+get their own pipeline.
+"""
+from __future__ import annotations
+
+import threading
+from dataclasses import dataclass
+from typing import Any, Callable, Dict, List, Optional, Tuple
+
+import numpy as np
+import torch
+
+from ..net.event_loop import get_event_loop
+from ..ops import aes as _aes
+from ..ops import tsdemux as _ts
+
+ALIGN = 256
+
+
+@dataclass
+class TransmuxJob:
+    payload: Any                       # torch uint8 tensor (any device) / numpy / bytes
+    key: Optional[bytes]               # AES-128 key or None
+    iv: Optional[bytes]
+    callback: Callable[[Dict[str, Any]], None]
+    frag: Any = None
+
+
+def _as_tensor(payload: Any) -> torch.Tensor:
+    if isinstance(payload, torch.Tensor):
+        return payload.reshape(-1)
+    if isinstance(payload, np.ndarray):
+        return torch.from_numpy(np.ascontiguousarray(payload.reshape(-1)).view(np.uint8))
+    if isinstance(payload, (bytes, bytearray, memoryview)):
+        return torch.frombuffer(bytearray(payload), dtype=torch.uint8)
+    raise TypeError(f"unsupported payload type {type(payload)!r}")
+
+
+def _align(n: int) -> int:
+    return (n + ALIGN - 1) // ALIGN * ALIGN
+
+
+class MediaPipeline:
+    def __init__(self, device: torch.device, loop=None) -> None:
+        self.device = torch.device(device)
+        self.loop = loop or get_event_loop()
+        self._jobs: List[TransmuxJob] = []
+        self._scheduled = False
+        self.segments = 0
+        self.bytes_in = 0
+        self.batches = 0
+
+    def submit(self, job: TransmuxJob) -> None:
+        self._jobs.append(job)
+        if not self._scheduled:
+            self._scheduled = True
+            self.loop.call_soon(self.flush)
+
+    def flush(self) -> None:
+        self._scheduled = False
+        jobs, self._jobs = self._jobs, []
+        if not jobs:
+            return
+        try:
+            results = self._run(jobs)
+        except Exception as e:  # deliver the failure to every job of the batch
+            for j in jobs:
+                j.callback({"error": e})
+            return
+        for j, r in zip(jobs, results):
+            j.callback(r)
+
+    # ------------------------------------------------------------------ batch
+    def _stage(self, tensors: List[torch.Tensor]) -> Tuple[torch.Tensor, List[int]]:
+        """One source buffer + offsets: in place when every payload is a view of the same
+        device storage (the HBM arena), otherwise one staging copy."""
+        dev = self.device
+        if all(t.device == dev for t in tensors):
+            ptrs = [t.untyped_storage().data_ptr() for t in tensors]
+            if len(set(ptrs)) == 1:
+                base_t = tensors[0]
+                storage = base_t.untyped_storage()
+                base = torch.empty(0, dtype=torch.uint8, device=dev).set_(storage, 0, (storage.nbytes(),))
+                offs = [t.data_ptr() - ptrs[0] for t in tensors]
+                if all(o % 16 == 0 for o in offs):
+                    return base, offs
+        offs, pos = [], 0
+        for t in tensors:
+            offs.append(pos)
+            pos += _align(t.numel())
+        buf = torch.empty(pos + ALIGN, dtype=torch.uint8, device=dev)
+        for o, t in zip(offs, tensors):
+            buf[o:o + t.numel()].copy_(t, non_blocking=True)
+        return buf, offs
+
+    def _run(self, jobs: List[TransmuxJob]) -> List[Dict[str, Any]]:
+        dev = self.device
+        tensors = [_as_tensor(j.payload) for j in jobs]
+        sizes = [t.numel() for t in tensors]
+        self.segments += len(jobs)
+        self.bytes_in += sum(sizes)
+        self.batches += 1
+        src, src_offs = self._stage(tensors)
+        enc = [i for i, j in enumerate(jobs) if j.key is not None]
+        clear = [i for i, j in enumerate(jobs) if j.key is None]
+        results: List[Optional[Dict[str, Any]]] = [None] * len(jobs)
+        groups = []
+        if enc:
+            bad = [i for i in enc if sizes[i] == 0 or sizes[i] % 16]
+            for i in bad:
+                results[i] = {"error": ValueError("encrypted payload is not a multiple of 16 bytes"), "status": -1}
+            enc = [i for i in enc if i not in bad]
+        if enc:
+            dec_offs, pos = [], 0
+            for i in enc:
+                dec_offs.append(pos)
+                pos += _align(sizes[i])
+            dec = torch.empty(pos + ALIGN, dtype=torch.uint8, device=dev)
+            out_len = _aes.cbc_decrypt_batch(src, [src_offs[i] for i in enc], [sizes[i] for i in enc],
+                                             [jobs[i].key for i in enc], [jobs[i].iv for i in enc], dec, dec_offs)
+            groups.append((enc, dec, dec_offs, out_len, [sizes[i] for i in enc]))
+        if clear:
+            groups.append((clear, src, [src_offs[i] for i in clear], [sizes[i] for i in clear],
+                           [sizes[i] for i in clear]))
+        infos = []
+        for idx, buf, offs, lens, caps in groups:
+            es_offs, pos = [], 0
+            for c in caps:
+                es_offs.append(pos)
+                pos += _align(c)
+            es = torch.empty(pos + ALIGN, dtype=torch.uint8, device=dev)
+            res = _ts.demux_batch(buf, offs, lens, es, es_offs, caps=caps)
+            infos.append((idx, res, es_offs, lens))
+        # one D2H copy of all info rows (the only sync of the stage)
+        host_infos = [r.info.cpu().numpy() for _, r, _, _ in infos] if dev.type != "cpu" else \
+            [r.info.numpy() for _, r, _, _ in infos]
+        for (idx, res, es_offs, lens), hinfo in zip(infos, host_infos):
+            plain_lens = lens.cpu().numpy() if isinstance(lens, torch.Tensor) else np.asarray(lens)
+            for k, i in enumerate(idx):
+                row = hinfo[k]
+                info = {name: int(row[slot]) for name, slot in _ts.INFO.items()}
+                base = es_offs[k]
+                vb, ab, ib = info["video_bytes"], info["audio_bytes"], info["id3_bytes"]
+                r = {
+                    "status": info["status"],
+                    "info": info,
+                    "plain_bytes": int(plain_lens[k]),
+                    "video": res.es[base:base + vb],
+                    "audio": res.es[base + vb:base + vb + ab],
+                    "id3": res.es[base + vb + ab:base + vb + ab + ib],
+                    "demux": res,
+                    "index": k,
+                }
+                if plain_lens[k] < 0:
+                    r["error"] = ValueError("decryption failed (bad PKCS#7 padding)")
+                results[i] = r
+        return results  # type: ignore[return-value]
+
+
+_local = threading.local()
+
+
+def pipeline_for(device: torch.device, loop=None) -> MediaPipeline:
+    """The calling thread's pipeline for ``device``."""
+    cache = getattr(_local, "pipes", None)
+    if cache is None:
+        cache = {}
+        _local.pipes = cache
+    loop = loop or get_event_loop()
+    key = (str(device), id(loop))
+    p = cache.get(key)
+    if p is None:
+        p = MediaPipeline(device, loop)
+        cache[key] = p
+    return p
+
+
+def default_transmux_device() -> torch.device:
+    return torch.device("cuda", torch.cuda.current_device()) if torch.cuda.is_available() else torch.device("cpu")

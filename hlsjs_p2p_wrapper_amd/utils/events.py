@@ -127,3 +127,28 @@ class Observer:
             fn(event, data)
 
     emit = trigger
+
+
+class JsObject(dict):
+    """Plain JS-object analog: a dict with attribute access (``undefined`` -> ``None``).
+
+    Used for event payloads (``{currentTarget: {response}}``, ``{target: {status}}``) and
+    loader stats (``{trequest, tfirst, tload, loaded, retry, aborted}``) so both
+    ``stats.tload`` and ``stats["tload"]`` work, as they do in JavaScript.
+    """
+
+    __slots__ = ()
+
+    def __getattr__(self, name: str) -> Any:
+        try:
+            return self[name]
+        except KeyError:
+            if name.startswith("__"):
+                raise AttributeError(name)
+            return None
+
+    def __setattr__(self, name: str, value: Any) -> None:
+        self[name] = value
+
+    def __delattr__(self, name: str) -> None:
+        self.pop(name, None)
