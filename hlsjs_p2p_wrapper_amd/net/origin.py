@@ -290,3 +290,75 @@ class SyntheticHlsOrigin:
             return Response(status, body, url, end - start + 1, source=(data, off + start), offset=start)
         text = self._text(path)
         return Response(200, text, url, len(text.encode()))
+
+
+class StaticOrigin:
+    """Serves fixed resources (``path -> bytes/str``) — for tests and hand-made streams."""
+
+    def __init__(self, base_url: str, resources: Optional[Dict[str, object]] = None, register: bool = True,
+                 pin_memory: bool = False) -> None:
+        self.base_url = base_url if base_url.endswith("/") else base_url + "/"
+        self.requests: List[str] = []
+        self._res: Dict[str, object] = {}
+        self.pin_memory = pin_memory
+        for k, v in (resources or {}).items():
+            self.put(k, v)
+        self._failures: List[Tuple[re.Pattern, int, int]] = []
+        if register:
+            register_origin(self.base_url, self)
+
+    def put(self, path: str, value) -> None:
+        if isinstance(value, (bytes, bytearray, np.ndarray)):
+            arr = np.frombuffer(bytes(value), dtype=np.uint8) if not isinstance(value, np.ndarray) else value
+            t = torch.empty(max(len(arr), 1), dtype=torch.uint8, pin_memory=self.pin_memory)
+            t[:len(arr)] = torch.from_numpy(np.ascontiguousarray(arr))
+            self._res[path] = (t, len(arr))
+        else:
+            self._res[path] = str(value)
+
+    def fail(self, pattern: str, status: int = 404, times: int = -1) -> None:
+        self._failures.append((re.compile(pattern), status, times))
+
+    def should_corrupt(self, path: str) -> bool:
+        return False
+
+    def _check(self, path: str) -> None:
+        for i, (rx, status, times) in enumerate(self._failures):
+            if rx.search(path) and times != 0:
+                if times > 0:
+                    self._failures[i] = (rx, status, times - 1)
+                raise HttpError(status, path)
+        if path not in self._res:
+            raise HttpError(404, path)
+
+    def resource(self, path: str):
+        self._check(path)
+        v = self._res[path]
+        if isinstance(v, str):
+            raise HttpError(415, path)
+        t, n = v
+        return t, 0, n, 0
+
+    def size(self, path: str, url: str = "", rng=None) -> int:
+        self._check(path)
+        v = self._res[path]
+        n = len(v.encode()) if isinstance(v, str) else v[1]
+        if rng is not None:
+            s, e = rng
+            e = n - 1 if e is None else min(e, n - 1)
+            return max(0, e - s + 1)
+        return n
+
+    def serve(self, path: str, url: str, rng, headers, with_credentials) -> Response:
+        self.requests.append(path)
+        self._check(path)
+        v = self._res[path]
+        if isinstance(v, str):
+            return Response(200, v, url, len(v.encode()))
+        t, n = v
+        start, end, status = 0, n - 1, 200
+        if rng is not None:
+            start, e = rng
+            end = n - 1 if e is None else min(e, n - 1)
+            status = 206
+        return Response(status, t[start:end + 1], url, end - start + 1, source=(t, start), offset=start)

@@ -193,17 +193,30 @@ class LevelController:
         details: LevelDetails = data["details"]
         old = lvl.details
         if old is not None and old.fragments and details.fragments:
-            # keep Fragment identity for sn present in both (in-flight loads refer to them)
+            # live reload: a refreshed playlist restarts its timeline at 0; align it on the
+            # previous one through a common sn (hls.js mergeDetails) and keep Fragment
+            # identity for sn present in both (in-flight loads refer to them)
             by_sn = {f.sn: f for f in old.fragments}
+            delta = None
+            for f in details.fragments:
+                o = by_sn.get(f.sn)
+                if o is not None:
+                    delta = o.start - f.start
+                    break
+            if delta is None:  # no overlap: continue after the old playlist's end
+                gap = details.fragments[0].sn - old.fragments[-1].sn - 1
+                delta = old.fragments[-1].end + gap * (details.targetduration or 0) - details.fragments[0].start
             merged = []
             for f in details.fragments:
                 o = by_sn.get(f.sn)
                 if o is not None:
-                    o.start, o.duration, o.url = f.start, f.duration, f.url
+                    o.duration, o.url = f.duration, f.url
                     merged.append(o)
                 else:
+                    f.start += delta
                     merged.append(f)
             details.fragments = merged
+            details.totalduration = merged[-1].end
         lvl.details = details
         self.hls.trigger(Events.LEVEL_UPDATED, {"details": details, "level": idx})
         if details.live and idx == self._level:

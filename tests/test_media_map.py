@@ -1,0 +1,74 @@
+"""Port of ``test/media-map.js`` plus the batched range-select (K1) oracle agreement."""
+import pytest
+import torch
+
+from hlsjs_p2p_wrapper_amd.models import MediaMap, SegmentView, TrackView
+from hlsjs_p2p_wrapper_amd.ops import segment
+from mocks import HlsMock
+
+
+def _mm(*a):
+    return MediaMap(HlsMock(*a))
+
+
+def test_get_segment_time():
+    tv = TrackView(level=1, urlId=1)
+    assert _mm(3, False, 1).getSegmentTime(SegmentView(sn=56, trackView=tv, time=560)) == 560
+    assert _mm(3, False, 1).getSegmentTime(SegmentView(sn=24, trackView=tv, time=240)) == 240
+    assert _mm(3, False, 0).getSegmentTime(SegmentView(sn=56, trackView=tv, time=560)) == 560
+    with pytest.raises(Exception, match="getSegmentTime: segmentView.time is undefined"):
+        _mm(3, False, 0).getSegmentTime(SegmentView(sn=56, trackView=tv))
+
+
+def _svs(tv, sns):
+    return [SegmentView(sn=s, trackView=tv, time=s * 10) for s in sns]
+
+
+@pytest.mark.parametrize("begin,dur,sns", [
+    (365, 33, range(37, 40)),      # timerange included in index
+    (10, 275, range(25, 29)),      # left intersection
+    (1975, 3000, range(198, 200)),  # right intersection
+    (240, 2100, range(25, 200)),   # timerange includes the index
+    (2100, 3000, []),              # disjoint
+])
+def test_get_segment_list(begin, dur, sns):
+    tv = TrackView(level=1, urlId=1)
+    assert _mm(3, False, 1).getSegmentList(tv, begin, dur) == _svs(tv, sns)
+
+
+def test_get_segment_list_unparsed_level_is_empty():
+    assert _mm(3, False, 0).getSegmentList(TrackView(level=1, urlId=1), 2100, 3000) == []
+
+
+def test_get_segment_list_missing_level_throws():
+    with pytest.raises(Exception, match="getSegmentList: level doesn't exist"):
+        _mm(3, False, 0).getSegmentList(TrackView(level=4, urlId=1), 2100, 3000)
+
+
+def test_get_segment_list_closed_interval_edges():
+    tv = TrackView(level=1, urlId=0)
+    got = _mm(3, False, 1).getSegmentList(tv, 370, 20)  # starts 370, 380, 390 (both ends inclusive)
+    assert [s.sn for s in got] == [37, 38, 39]
+
+
+def test_get_track_list():
+    assert _mm(0, False, 0).getTrackList() == []
+    tracks = _mm(3, False, 1).getTrackList()
+    assert len(tracks) == 6  # 3 levels x 2 urlIds
+    assert [t.viewToString() for t in tracks[:3]] == ["L0U0", "L0U1", "L1U0"]
+
+
+def test_get_segment_duration_is_first_fragment_duration():
+    mm = _mm(3, False, 1)
+    assert mm.getSegmentDuration(SegmentView(sn=100, trackView=TrackView(level=1, urlId=0))) == 10
+
+
+def test_range_select_cpu_matches_media_map():
+    mock = HlsMock(3, False, 1)
+    starts = [[f.start for f in mock.levels[1].details.fragments]]
+    queries = [(0, 365, 33), (0, 10, 275), (0, 1975, 3000), (0, 240, 2100), (0, 2100, 3000)]
+    lo, hi = segment.range_select(starts, queries, torch.device("cpu"))
+    mm = MediaMap(mock)
+    for (t, b, d), l, h in zip(queries, lo, hi):
+        want = [s.sn for s in mm.getSegmentList(TrackView(level=1, urlId=0), b, d)]
+        assert [25 + i for i in range(l, h)] == want

@@ -1,0 +1,140 @@
+"""In-process multi-peer swarm (the CPU analog of N MI355X peers): P2P
+exchange + CDN de-duplication, offload ratio, CRC fault injection -> CDN fallback,
+churn (offline peer), P2P toggles, live streams."""
+import threading
+
+import pytest
+
+from hlsjs_p2p_wrapper_amd import Hls
+from hlsjs_p2p_wrapper_amd.agent import current_node, node_for_config, set_current_node
+from hlsjs_p2p_wrapper_amd.api.wrapper import HlsjsP2PWrapper
+from hlsjs_p2p_wrapper_amd.net import clear_origins, new_event_loop
+from hlsjs_p2p_wrapper_amd.net.origin import Rendition, SyntheticHlsOrigin
+from hlsjs_p2p_wrapper_amd.parallel import ThreadHub
+from hlsjs_p2p_wrapper_amd.player import MediaElement
+from hlsjs_p2p_wrapper_amd.player.hls import Hls as Engine
+
+
+@pytest.fixture(autouse=True)
+def fresh():
+    clear_origins()
+    yield
+    clear_origins()
+
+
+def run_swarm(n, origin, until=38.0, before=None, cfg_extra=None, hls_cfg=None, start_delay=None, timeout=120_000):
+    hub = ThreadHub(n)
+    out, errs = {}, []
+
+    def peer(r):
+        try:
+            set_current_node(None)
+            loop = new_event_loop("virtual")
+            w = HlsjsP2PWrapper(Engine)
+            gs = {"backend": "thread", "hub": hub, "rank": r, "device": "cpu", "cacheBytes": 128 << 20,
+                  "roundIntervalMs": 20}
+            gs.update(cfg_extra or {})
+            node_for_config({"gpuSwarm": gs})  # join the swarm's rounds from the start
+            hls = w.createPlayer(dict(hls_cfg or {}), {"gpuSwarm": gs})
+            media = MediaElement()
+            delay = start_delay(r) if start_delay else 0
+            if delay:  # keeps joining the rounds, but only starts playing later
+                loop.set_timeout(hls.loadSource, delay, origin.master_url())
+            else:
+                hls.loadSource(origin.master_url())
+            hls.attachMedia(media)
+            hls.on(Hls.Events.MANIFEST_PARSED, lambda e, d: media.play())
+            node = current_node()
+            if before:
+                before(r, node, w)
+            if callable(until):
+                ok = loop.run_until(lambda: until(media), timeout_ms=timeout)
+            else:
+                ok = loop.run_until(lambda: media.currentTime > until, timeout_ms=timeout)
+            out[r] = {"ok": ok, "t": media.currentTime, "stats": dict(w.stats), "node": dict(node.stats),
+                      "offload": None}
+            node.close()
+            out[r]["offload"] = node.swarm_offload_ratio()
+        except BaseException as e:  # noqa: BLE001
+            errs.append(e)
+            hub.abort()
+
+    ts = [threading.Thread(target=peer, args=(r,)) for r in range(n)]
+    [t.start() for t in ts]
+    [t.join(300) for t in ts]
+    if errs:
+        raise errs[0]
+    return out
+
+
+@pytest.fixture
+def vod():
+    return SyntheticHlsOrigin("http://cdn.test/vod/", renditions=[Rendition(1_000_000, 640, 360)], num_segments=10,
+                              encrypted=True)
+
+
+def test_two_peers_share_cdn_fetches(vod):
+    out = run_swarm(2, vod)
+    total_cdn = sum(o["stats"]["cdn"] for o in out.values())
+    total_p2p = sum(o["stats"]["p2p"] for o in out.values())
+    seg_total = sum(vod.pools[0].lengths)
+    assert all(o["ok"] for o in out.values())
+    assert total_cdn == seg_total  # every segment fetched from the CDN exactly once
+    assert total_p2p == seg_total  # ... and delivered to the other peer over P2P
+    assert out[0]["stats"]["upload"] == out[1]["stats"]["p2p"]
+    assert out[0]["stats"]["peers"] == 1
+    assert out[0]["offload"] == pytest.approx(0.5)
+
+
+def test_four_peers_offload(vod):
+    out = run_swarm(4, vod)
+    cdn = sum(o["stats"]["cdn"] for o in out.values())
+    p2p = sum(o["stats"]["p2p"] for o in out.values())
+    assert all(o["ok"] for o in out.values())
+    assert p2p / (p2p + cdn) == pytest.approx(0.75)  # (N-1)/N with de-duplication
+
+
+def test_late_joiner_served_from_peers_cache(vod):
+    # peer 1 starts 60 s later: everything it needs is already cached on peer 0
+    out = run_swarm(2, vod, start_delay=lambda r: 60_000 if r == 1 else 0, timeout=400_000)
+    assert out[1]["stats"]["cdn"] == 0
+    assert out[1]["stats"]["p2p"] == sum(vod.pools[0].lengths)
+
+
+def test_crc_failure_falls_back_to_cdn(vod):
+    def corrupt(r, node, w):
+        if r == 1:
+            node.corrupt_next_recv = 2
+    out = run_swarm(2, vod, before=corrupt)
+    assert all(o["ok"] for o in out.values())
+    assert out[1]["node"]["crc_failures"] >= 1
+    assert out[1]["stats"]["cdn"] > 0  # refetched from the CDN after the bad peer copy
+
+
+def test_offline_peer_neither_serves_nor_receives(vod):
+    def offline(r, node, w):
+        if r == 1:
+            node.set_online(False)
+    out = run_swarm(2, vod, before=offline)
+    seg_total = sum(vod.pools[0].lengths)
+    assert out[1]["stats"]["p2p"] == 0 and out[1]["stats"]["cdn"] == seg_total
+    assert out[0]["stats"]["p2p"] == 0 and out[0]["stats"]["cdn"] == seg_total
+
+
+def test_p2p_download_toggle(vod):
+    def no_dl(r, node, w):
+        if r == 1:
+            node.download_on = False
+    out = run_swarm(2, vod, before=no_dl)
+    assert out[1]["stats"]["p2p"] == 0
+
+
+def test_live_stream_swarm():
+    origin = SyntheticHlsOrigin("http://cdn.test/live/", renditions=[Rendition(800_000, 640, 360)], live=True,
+                                window=6, num_segments=None, pool_size=8, encrypted=True)
+    origin.advance(4)  # live edge at sn 9: window sn 4..9 = 24 s of media (frozen clock)
+    # live start = 24 - 2 * targetduration = 16 s; play to the live edge
+    out = run_swarm(2, origin, until=lambda m: m.currentTime > 22.0, hls_cfg={"liveSyncDurationCount": 2})
+    assert all(o["ok"] for o in out.values())
+    assert sum(o["stats"]["p2p"] for o in out.values()) > 0
+    assert sum(o["stats"]["cdn"] for o in out.values()) == sum(o["stats"]["p2p"] for o in out.values())
