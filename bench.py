@@ -1,0 +1,198 @@
+#!/usr/bin/env python3
+"""Headline benchmark: segments/s + P2P offload ratio, 1080p 6 Mb/s HLS, 1/2/4/8 MI355X.
+
+Metric and config come from BASELINE.json.  One rank per GPU (``torchrun``), each rank a
+swarm peer running the full public API path:
+
+    Hls(hlsjsConfig, p2pConfig)  (bundle)  ->  P2PLoader (fLoader)  ->  PeerAgent
+    ->  SwarmNode round:  CDN phase (pinned host -> HBM, side stream) + MFMA CRC ingest
+                          P2P phase (RCCL batch_isend_irecv over xGMI, CRC-verified)
+    ->  onProgress/onSuccess  ->  FRAG_LOADED  ->  batched AES-128-CBC decrypt + TS demux
+    ->  buffer append  ->  FRAG_BUFFERED
+
+Workload (synthetic, see ``--help``): every peer plays the same 1080p 6 Mb/s AES-128
+stream (4 s MPEG-TS segments of ~3.0 MB) as fast as the engine delivers ("drain" media
+sink, e.g. an edge/restream node catching up a DVR window), with ``--inflight``
+fragments in flight per peer.  One step = one swarm exchange round in which every peer
+completes ``--inflight`` segments end to end.  Per-GPU work is fixed (weak scaling).
+
+``value`` = completed (loaded + decrypted + demuxed + buffered) segments per second over
+all ranks (timed region bracketed by barrier + device sync, max time over ranks).
+``offload_ratio`` = sum p2p / (sum p2p + sum cdn) bytes over the timed region.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+import torch
+
+CONFIGS = {
+    # name: (renditions preset, encrypted, segment seconds, description)
+    "1080p6m": ("1080p", True, 4.0, "1080p 6 Mb/s HLS live (AES-128, 4 s TS segments, 8 peers)"),
+    "1080p6m-clear": ("1080p", False, 4.0, "1080p 6 Mb/s HLS (clear, 4 s TS segments)"),
+    "abr5": ("abr5", True, 4.0, "5-rendition ABR ladder (AES-128, 4 s TS)"),
+    "4k25m": ("4k", True, 4.0, "4K 25 Mb/s HLS (AES-128, 4 s TS segments)"),
+}
+
+
+def parse():
+    p = argparse.ArgumentParser(description=__doc__, formatter_class=argparse.RawDescriptionHelpFormatter)
+    p.add_argument("--gpus", type=int, default=1)
+    p.add_argument("--steps", type=int, default=20)
+    p.add_argument("--warmup", type=int, default=5)
+    p.add_argument("--config", default="1080p6m", choices=sorted(CONFIGS))
+    p.add_argument("--inflight", type=int, default=64, help="fragments in flight per peer (per step)")
+    p.add_argument("--pool", type=int, default=64, help="distinct packaged segments per rendition")
+    p.add_argument("--cache-gb", type=float, default=8.0, help="HBM segment-cache arena per GPU")
+    p.add_argument("--no-dedup", action="store_true", help="disable CDN de-duplication (seeding)")
+    p.add_argument("--cpu", action="store_true", help="CPU rehearsal (gloo, no GPU)")
+    p.add_argument("--verbose", action="store_true")
+    return p.parse_args()
+
+
+def main() -> int:
+    args = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    use_gpu = torch.cuda.is_available() and not args.cpu
+    if use_gpu:
+        torch.cuda.set_device(local_rank)
+        device = torch.device("cuda", local_rank)
+    else:
+        device = torch.device("cpu")
+    import torch.distributed as dist
+
+    if world > 1:
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        dist.init_process_group("nccl" if use_gpu else "gloo", device_id=device if use_gpu else None)
+
+    from hlsjs_p2p_wrapper_amd import Hls
+    from hlsjs_p2p_wrapper_amd.agent import node_for_config
+    from hlsjs_p2p_wrapper_amd.net import new_event_loop
+    from hlsjs_p2p_wrapper_amd.net.origin import PRESET_1080P_6M, PRESET_4K_25M, PRESET_ABR5, SyntheticHlsOrigin
+    from hlsjs_p2p_wrapper_amd.player import MediaElement
+    from hlsjs_p2p_wrapper_amd.player.transmux import pipeline_for
+
+    preset, encrypted, seg_dur, desc = CONFIGS[args.config]
+    rends = {"1080p": PRESET_1080P_6M, "4k": PRESET_4K_25M, "abr5": PRESET_ABR5}[preset]
+    K = args.inflight
+    total_steps = args.warmup + args.steps
+    n_segments = (total_steps + 4) * K
+    loop = new_event_loop("real")
+    t_pack = time.perf_counter()
+    origin = SyntheticHlsOrigin("http://cdn.bench/live/", renditions=rends, num_segments=n_segments,
+                                segment_duration=seg_dur, encrypted=encrypted, pool_size=args.pool,
+                                pin_memory=use_gpu, seed=7)
+    t_pack = time.perf_counter() - t_pack
+    p2p_config = {"streamrootKey": "bench", "contentId": "bench-1080p",
+                  "gpuSwarm": {"backend": "dist" if world > 1 else "local", "device": str(device),
+                               "cacheBytes": int(args.cache_gb * (1 << 30)), "autoTick": False,
+                               "cdnDedup": not args.no_dedup}}
+    node = node_for_config(p2p_config)
+    hls_config = {"maxFragLoadsInFlight": K, "maxBufferLength": 1e9, "maxMaxBufferLength": 1e9,
+                  "startPosition": 0, "fragLoadingTimeOut": 600_000, "tickInterval": 1e9}
+    if preset != "abr5":
+        hls_config["startLevel"] = 0
+    hls = Hls(hls_config, p2p_config)
+    media = MediaElement(mode="drain", loop=loop)
+    counters = {"buffered": 0, "errors": 0}
+    hls.on(Hls.Events.FRAG_BUFFERED, lambda e, d: counters.__setitem__("buffered", counters["buffered"] + 1))
+    hls.on(Hls.Events.ERROR, lambda e, d: counters.__setitem__("errors", counters["errors"] + 1))
+    hls.loadSource(origin.master_url())
+    hls.attachMedia(media)
+    hls.on(Hls.Events.MANIFEST_PARSED, lambda e, d: media.play())
+    sc = hls.streamController
+    pipe = pipeline_for(device, loop)
+
+    def drain_ready():
+        for _ in range(1000):
+            if not loop._ready:
+                return
+            loop.run_once(block=False)
+
+    # bring the player up to its first fragment requests (manifest, level, key)
+    t_end = time.perf_counter() + 60
+    while time.perf_counter() < t_end and not sc.inflight:
+        loop.run_once(block=False)
+        sc.tick()
+        drain_ready()
+    if not sc.inflight:
+        raise RuntimeError("player did not start loading fragments")
+
+    def step():
+        sc.tick()
+        drain_ready()
+        node.tick()
+        drain_ready()
+        pipe.flush()
+        drain_ready()
+
+    def sync():
+        if use_gpu:
+            torch.cuda.synchronize(device)
+        if world > 1:
+            node.comm.barrier()
+        if use_gpu:
+            torch.cuda.synchronize(device)
+
+    for _ in range(args.warmup):
+        step()
+    sync()
+    b0, s0 = counters["buffered"], dict(node.stats)
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    sync()
+    elapsed = time.perf_counter() - t0
+    done = counters["buffered"] - b0
+    d_cdn = node.stats["cdn"] - s0["cdn"]
+    d_p2p = node.stats["p2p"] - s0["p2p"]
+    vals = np.array([done, d_cdn, d_p2p, int(elapsed * 1e9), counters["errors"]], dtype=np.int64)
+    if world > 1:
+        parts = node.comm.allgather_control(vals)
+        tot = np.sum(np.stack(parts), axis=0)
+        max_ns = max(int(p[3]) for p in parts)
+    else:
+        tot, max_ns = vals, int(vals[3])
+    max_s = max_ns / 1e9
+    seg_bytes = int(np.mean(origin.pools[0].lengths))
+    result = {
+        "metric": "segments/sec + P2P offload ratio, 1080p 6 Mb/s HLS at 1/2/4/8 MI355X",
+        "value": round(float(tot[0]) / max_s, 2),
+        "unit": "segments/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(max_s * 1e3 / args.steps, 3),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "uint8",
+        "data": "synthetic",
+        "offload_ratio": round(float(tot[2]) / max(1.0, float(tot[1] + tot[2])), 4),
+        "goodput_GBps": round(float(tot[0]) * seg_bytes / max_s / 1e9, 3),
+        "errors": int(tot[4]),
+        "config": {"model": desc, "global_batch": K * world, "seq_len": seg_bytes,
+                   "parallelism": f"swarm{world}" + ("-rccl" if (world > 1 and use_gpu) else ""),
+                   "inflight_per_gpu": K, "encrypted": encrypted, "segment_s": seg_dur,
+                   "device": "MI355X" if use_gpu else "cpu"},
+    }
+    if args.verbose and rank == 0:
+        print(f"# pack {t_pack:.2f}s node stats {node.stats} last round {node.last_round} "
+              f"pipe batches {pipe.batches}", file=sys.stderr)
+    if rank == 0:
+        print(json.dumps(result), flush=True)
+    if world > 1:
+        node.comm.barrier()
+        dist.destroy_process_group()
+    return 0
+
+
+if __name__ == "__main__":
+    sys.exit(main())
