@@ -9,27 +9,32 @@ This is the engine behind the peer agent's ``getSegment`` (the closed-source
 * **Rounds** (SURVEY §5.8): requests accumulate; every rank then runs one collective
   round — all-gather of a small control message (wants, cache delta, flags, counters) on
   the control plane, identical deterministic planning everywhere (native
-  ``plan_round``), a CDN phase (pinned-host → HBM ``hipMemcpyAsync`` on a side stream)
-  with ingest CRC on the MFMA CRC kernel, and a P2P phase: ONE contiguous buffer per peer
-  pair over RCCL (``batch_isend_irecv``), with the sender's CRCs as a trailer, verified on
-  device by the receiver.
+  ``plan_round``), a CDN phase (pinned-host -> HBM ``hipMemcpyAsync`` batch on a side
+  stream, the DMA engines) with ingest CRC on the MFMA CRC kernel, and a P2P phase: ONE
+  contiguous buffer per peer pair over RCCL (``batch_isend_irecv``), the sender's CRCs as
+  a trailer, verified on device by the receiver.
+* **Asynchronous rounds**: :meth:`launch_round` (collective) only *enqueues* device work
+  and records an event; :meth:`complete_round` (local) waits for it, commits/drops and
+  delivers.  A throughput deployment keeps round ``t+1`` in flight on the device while the
+  host completes round ``t`` (``tick()`` = launch + complete for event-loop players).
 * **Faults**: a peer copy failing its CRC is dropped and re-requested from the CDN next
   round; churn is modelled by ranks announcing ``online=False`` (they still join the
   collectives, as an RCCL communicator cannot shrink).
 
 Completion semantics match the reference loader contract: ``onProgress({cdnDownloaded,
 p2pDownloaded, cdnDuration, p2pDuration})`` then ``onSuccess(data)`` where ``data`` is a
-zero-copy ``uint8`` view of the arena (valid until the next round), or
-``onError(HttpError)`` (``p2p-loader-generator.js:164-208``).
+zero-copy ``uint8`` view of the arena, or ``onError(HttpError)``
+(``lib/integration/p2p-loader-generator.js:164-208``).
 """
 from __future__ import annotations
 
+import contextlib
 import logging
 import threading
 import time
 import zlib
 from dataclasses import dataclass, field
-from typing import Any, Callable, Dict, List, Optional, Sequence, Tuple
+from typing import Any, Dict, List, Optional, Tuple
 
 import numpy as np
 import torch
@@ -40,6 +45,7 @@ from ..ops import crc as _crc
 from ..ops import segment as _seg
 from ..ops._native import runtime as _rt
 from ..parallel.comm import LocalComm, SwarmComm
+from ..utils.trace import PhaseTimer
 
 log = logging.getLogger("hlsjs_p2p_wrapper_amd.node")
 
@@ -47,6 +53,7 @@ MAGIC = 0x48505032  # "HPP2"
 HDR = 16
 ALIGN = 256
 SLACK = 4096
+PIN_DELAY_ROUNDS = 2  # delivered segments stay pinned this many launches (consumers run async)
 
 
 def swarm_id_for(content_id: str) -> int:
@@ -79,27 +86,52 @@ class _Want:
     waiters: List[Request] = field(default_factory=list)
     force_cdn: bool = False
     attempts: int = 0
+    round: int = -1  # round it is in flight in (-1: waiting)
 
 
 class _Completion:
-    __slots__ = ("req", "data", "source", "nbytes", "cdn_ms", "p2p_ms", "error", "entry", "delay")
+    __slots__ = ("req", "data", "source", "nbytes", "cdn_ms", "p2p_ms", "entry", "delay")
 
-    def __init__(self, req, data, source, nbytes, cdn_ms, p2p_ms, error=None, entry=-1):
+    def __init__(self, req, data, source, nbytes, cdn_ms, p2p_ms, entry=-1, delay=0.0):
         self.req = req
         self.data = data
         self.source = source
         self.nbytes = nbytes
         self.cdn_ms = cdn_ms
         self.p2p_ms = p2p_ms
-        self.error = error
         self.entry = entry
-        self.delay = 0.0
+        self.delay = delay
+
+
+@dataclass(eq=False)
+class RoundHandle:
+    round: int
+    all_leaving: bool
+    empty: bool = True
+    wants: List[_Want] = field(default_factory=list)
+    by_id: Dict[int, _Want] = field(default_factory=dict)
+    cdn_entries: List[Tuple[_Want, int, int, int]] = field(default_factory=list)
+    recv_entries: List[Tuple[np.ndarray, int, int]] = field(default_factory=list)
+    send_pins: Optional[np.ndarray] = None
+    sent_bytes: int = 0
+    ev_cdn: Any = None
+    ev_p2p: Any = None
+    cdn_ms: float = 0.0
+    p2p_ms: float = 0.0
+    shaped_ms: float = 0.0
+    ok_dev: Any = None
+    ok_host: Any = None
+    done: Any = None
+    n_wants: int = 0
+    n_send: int = 0
+    t0: float = 0.0
+    completed: bool = False
 
 
 class SwarmNode:
     def __init__(self, comm: Optional[SwarmComm] = None, device: Any = "auto", cache_bytes: int = 1 << 30,
                  loop=None, cdn_dedup: bool = True, round_interval_ms: Optional[float] = None,
-                 auto_tick: bool = True) -> None:
+                 auto_tick: bool = True, max_wants_per_round: Optional[int] = None) -> None:
         self.comm = comm or LocalComm()
         self.rank = self.comm.rank
         self.world = self.comm.world_size
@@ -113,8 +145,10 @@ class SwarmNode:
         self.store = self.rt.SegmentStore(self.cache_bytes, ALIGN)
         self.directory = self.rt.Directory()
         self.arena = torch.empty(self.cache_bytes + SLACK, dtype=torch.uint8, device=self.device)
-        self.crc_dev = torch.zeros(1024, dtype=torch.int32, device=self.device)  # ingest CRC per entry id
-        self.cdn_stream = torch.cuda.Stream(self.device) if self.is_cuda else None
+        self.crc_dev = torch.zeros(1024, dtype=torch.int32, device=self.device)  # CRC per entry id
+        # all node device work (CDN H2D, ingest CRC, RCCL, verify CRC) runs on its own stream:
+        # consumers (decrypt/demux of the previous round) on the default stream overlap it
+        self.stream = torch.cuda.Stream(self.device) if self.is_cuda else None
         self.online = True
         self.upload_on = True
         self.download_on = True
@@ -122,13 +156,14 @@ class SwarmNode:
         self.round = 0
         self.round_interval_ms = round_interval_ms
         self.auto_tick = auto_tick
+        self.max_wants_per_round = max_wants_per_round
         self.leaving = False
         self.closed = False
         self._wants: Dict[Tuple[int, int, int, int], _Want] = {}
         self._next_want_id = 1
         self._tick_scheduled = False
         self._timer = None
-        self._pinned_last: List[int] = []
+        self._pins: List[Tuple[int, np.ndarray]] = []  # (release at launch #, entry ids)
         self._agents: List[Any] = []
         self.peer_online = np.ones(self.world, dtype=bool)
         self.stats = {"cdn": 0, "p2p": 0, "upload": 0, "cache": 0, "rounds": 0, "crc_failures": 0,
@@ -136,7 +171,7 @@ class SwarmNode:
         self.swarm_stats = {"cdn": 0, "p2p": 0, "upload": 0}
         self.last_round: Dict[str, Any] = {}
         self.corrupt_next_recv = 0  # fault injection: flip a byte in the next N received rounds
-        self._cdn_shaped_ms = 0.0
+        self.timer = PhaseTimer()
         self._lock = threading.RLock()
         if self.world > 1 and auto_tick:
             self._timer = self.loop.set_interval(self._timer_tick, round_interval_ms or 10.0)
@@ -208,7 +243,7 @@ class SwarmNode:
                 return
             off, n = (int(x) for x in self.store.entries(np.array([eid], dtype=np.int64))[0][:2])
             self.stats["cache"] += n
-            self._deliver([_Completion(req, self.arena[off:off + n], "cache", n, 0.0, 0.0)])
+            self._deliver_now([_Completion(req, self.arena[off:off + n], "cache", n, 0.0, 0.0)])
         finally:
             self.store.unpin(np.array([eid], dtype=np.int64))
 
@@ -221,7 +256,7 @@ class SwarmNode:
         if on_error is not None:
             on_error(err)
 
-    # ------------------------------------------------------------------ round protocol
+    # ------------------------------------------------------------------ control messages
     def _encode(self, wants: List[_Want], adds: np.ndarray, rms: np.ndarray) -> np.ndarray:
         hdr = np.zeros(HDR, dtype=np.int64)
         hdr[0] = MAGIC
@@ -234,11 +269,11 @@ class SwarmNode:
         hdr[7] = self.stats["cdn"]
         hdr[8] = self.stats["p2p"]
         hdr[9] = self.stats["upload"]
-        w = np.zeros((len(wants), 6), dtype=np.int64)
-        for i, x in enumerate(wants):
-            w[i, :4] = x.key
-            w[i, 4] = x.size
-            w[i, 5] = x.want_id | ((1 if x.force_cdn else 0) << 62)
+        if wants:
+            w = np.array([(*x.key, x.size, x.want_id | ((1 if x.force_cdn else 0) << 62)) for x in wants],
+                         dtype=np.int64)
+        else:
+            w = np.zeros((0, 6), dtype=np.int64)
         return np.concatenate([hdr, w.reshape(-1), adds.reshape(-1).astype(np.int64),
                                rms.reshape(-1).astype(np.int64)])
 
@@ -261,31 +296,43 @@ class SwarmNode:
             new[:self.crc_dev.numel()] = self.crc_dev
             self.crc_dev = new
 
-    def _sync(self) -> None:
-        if self.is_cuda:
-            torch.cuda.current_stream(self.device).synchronize()
-
+    # ------------------------------------------------------------------ rounds
     def tick(self) -> bool:
-        """One collective exchange round.  Returns True when every rank is leaving."""
+        """One synchronous collective round (launch + complete).  True when every rank
+        is leaving."""
         with self._lock:
-            return self._round()
+            h = self.launch_round()
+            self.complete_round(h)
+            return h.all_leaving
 
-    def _round(self) -> bool:
+    def launch_round(self) -> RoundHandle:
+        """Collective: exchange control messages, plan, and ENQUEUE this round's device
+        work (CDN copies, ingest CRC, RCCL transfers, verify CRC).  Host does not wait."""
         rt = self.rt
         t0 = time.perf_counter()
-        self._cdn_shaped_ms = 0.0
-        if self._pinned_last:
-            self.store.unpin(np.asarray(self._pinned_last, dtype=np.int64))
-            self._pinned_last = []
-        # ---------------- 1. control plane
-        wants = [w for w in self._wants.values() if any(not r.aborted for r in w.waiters)]
-        for k in [k for k, w in self._wants.items() if w not in wants]:
-            del self._wants[k]
-        adds, rms = self.store.take_delta()
-        msg = self._encode(wants, adds, rms)
-        parts = self.comm.allgather_control(msg)
         self.round += 1
         self.stats["rounds"] += 1
+        keep = []
+        for rel, ids in self._pins:
+            if rel <= self.round:
+                self.store.unpin(ids)
+            else:
+                keep.append((rel, ids))
+        self._pins = keep
+        # ---------------- 1. control plane
+        wants = []
+        for k in list(self._wants):
+            w = self._wants[k]
+            if w.round >= 0:
+                continue
+            if not any(not r.aborted for r in w.waiters):
+                del self._wants[k]
+                continue
+            wants.append(w)
+            if self.max_wants_per_round is not None and len(wants) >= self.max_wants_per_round:
+                break
+        adds, rms = self.store.take_delta()
+        parts = self.comm.allgather_control(self._encode(wants, adds, rms))
         all_leaving = True
         flags = np.zeros(self.world, dtype=np.int64)
         want_rows = []
@@ -298,7 +345,7 @@ class SwarmNode:
             if len(a) or len(rm):
                 self.directory.apply(r, np.ascontiguousarray(a), np.ascontiguousarray(rm))
             if len(w):
-                rows = np.zeros((len(w), 8), dtype=np.int64)
+                rows = np.empty((len(w), 8), dtype=np.int64)
                 rows[:, :5] = w[:, :5]
                 rows[:, 5] = w[:, 5] & ((1 << 62) - 1)
                 rows[:, 6] = r
@@ -306,124 +353,151 @@ class SwarmNode:
                 want_rows.append(rows)
         self.peer_online = (flags & rt.FLAG_ONLINE) != 0
         self.swarm_stats = {"cdn": int(swarm_tot[0]), "p2p": int(swarm_tot[1]), "upload": int(swarm_tot[2])}
+        h = RoundHandle(self.round, all_leaving, t0=t0)
+        t_ctrl = time.perf_counter()
+        self.timer.add("control", t_ctrl - t0)
         if not want_rows:
-            self.last_round = {"wants": 0, "ms": (time.perf_counter() - t0) * 1e3}
-            return all_leaving
+            return h
+        h.empty = False
         all_wants = np.ascontiguousarray(np.concatenate(want_rows))
         plan = rt.plan_round(self.directory, all_wants, flags, self.world)
         me = self.rank
-        by_id = {w.want_id: w for w in wants}
+        h.wants = wants
+        h.by_id = {w.want_id: w for w in wants}
+        for w in wants:
+            w.round = self.round
+        h.n_wants = len(all_wants)
         cdn_rows = plan[(plan[:, 5] == -1) & (plan[:, 6] == me)]
         send_rows = plan[plan[:, 5] == me]
         recv_rows = plan[(plan[:, 6] == me) & (plan[:, 5] >= 0)]
-        # ---------------- 2. pin what we send from cache (seeded rows are fetched below)
+        h.n_send = len(send_rows)
+        # ---------------- 2. pin what we send from cache (seeded rows come from the CDN phase)
         cached_send = send_rows[send_rows[:, 8] == 0]
         send_ids: Dict[Tuple[int, int, int, int], int] = {}
         if len(cached_send):
             ids = self.store.lookup(np.ascontiguousarray(cached_send[:, :4]), False)
-            for row, eid in zip(cached_send, ids):
-                send_ids[tuple(int(x) for x in row[:4])] = int(eid)
+            for row, eid in zip(cached_send.tolist(), ids.tolist()):
+                send_ids[tuple(row[:4])] = eid
             valid = ids[ids >= 0]
             if len(valid):
                 self.store.pin(valid)
-        # ---------------- 3. CDN phase (pinned host -> HBM on the side stream)
+                h.send_pins = valid
         t_cdn0 = time.perf_counter()
+        self.timer.add("plan", t_cdn0 - t_ctrl)
+        with (torch.cuda.stream(self.stream) if self.is_cuda else contextlib.nullcontext()):
+            # ---------------- 3. CDN phase (pinned host -> HBM, DMA engines)
+            if len(cdn_rows):
+                self._cdn_phase(h, cdn_rows)
+                for w, eid, off, n in h.cdn_entries:
+                    send_ids.setdefault(w.key, eid)
+            t_p2p0 = time.perf_counter()
+            self.timer.add("cdn_enqueue", t_p2p0 - t_cdn0)
+            # ---------------- 4. P2P phase
+            if len(send_rows) or len(recv_rows):
+                self._p2p_phase(h, send_rows, recv_rows, send_ids)
+            h.sent_bytes = int(send_rows[:, 4].sum()) if len(send_rows) else 0
+            if self.is_cuda:
+                h.done = torch.cuda.Event()
+                h.done.record()
+        self.timer.add("p2p_enqueue", time.perf_counter() - t_p2p0)
+        return h
+
+    def complete_round(self, h: RoundHandle) -> None:
+        """Local: wait for the round's device work, verify, commit and deliver."""
+        if h.completed:
+            return
+        h.completed = True
+        if h.empty:
+            self.last_round = {"wants": 0, "ms": (time.perf_counter() - h.t0) * 1e3}
+            return
+        t0 = time.perf_counter()
+        if h.done is not None:
+            h.done.synchronize()
+        t1 = time.perf_counter()
+        self.timer.add("wait_device", t1 - t0)
+        if h.ev_cdn is not None:
+            h.cdn_ms = h.ev_cdn[0].elapsed_time(h.ev_cdn[1])
+        if h.ev_p2p is not None:
+            h.p2p_ms = h.ev_p2p[0].elapsed_time(h.ev_p2p[1])
+        ok = None
+        if h.ok_host is not None:
+            ok = h.ok_host.numpy()
+        good, bad = [], []
+        for i, ent in enumerate(h.recv_entries):
+            (good if ok is None or ok[i] else bad).append(ent)
+        if good:
+            self.store.commit(np.asarray([r[-1] for r, _, _ in good], dtype=np.int64))
+        if bad:
+            self.store.drop(np.asarray([r[-1] for r, _, _ in bad], dtype=np.int64))
+            self.stats["crc_failures"] += len(bad)
+        if h.send_pins is not None:
+            self.store.unpin(h.send_pins)
+        self.stats["upload"] += h.sent_bytes
         completions: List[_Completion] = []
-        cdn_entries: List[Tuple[_Want, int, int, int]] = []  # (want, entry, off, n)
-        cdn_ms = 0.0
-        ev_cdn = None
-        if len(cdn_rows):
-            cdn_entries, cdn_ms, ev_cdn = self._cdn_phase(cdn_rows, by_id, completions)
-            for w, eid, off, n in cdn_entries:
-                send_ids.setdefault(w.key, eid)
-        # ---------------- 4. P2P phase
-        t_p2p0 = time.perf_counter()
-        recv_entries, p2p_ms, ev_p2p, recv_meta = self._p2p_phase(send_rows, recv_rows, send_ids)
-        # ---------------- 5. verify + commit
-        ok_host = None
-        if recv_entries:
-            offs = [off for _, off, _ in recv_entries]
-            lens = [n for _, _, n in recv_entries]
-            _, ok = _crc.crc32_batch(self.arena, offs, lens, expect_dev=recv_meta)
-            ok_host = ok.cpu().numpy() if ok is not None else None  # sync point
-        else:
-            self._sync()
-        if ev_cdn is not None:
-            cdn_ms = ev_cdn[0].elapsed_time(ev_cdn[1])
-        if ev_p2p is not None:
-            p2p_ms = ev_p2p[0].elapsed_time(ev_p2p[1])
-        if cdn_entries:
-            self.store.commit(np.asarray([e for _, e, _, _ in cdn_entries], dtype=np.int64))
-        good_recv, bad_recv = [], []
-        for i, (row, off, n) in enumerate(recv_entries):
-            (good_recv if ok_host is None or ok_host[i] else bad_recv).append((row, off, n))
-        if good_recv:
-            self.store.commit(np.asarray([r[-1] for r, _, _ in good_recv], dtype=np.int64))
-        if bad_recv:
-            self.store.drop(np.asarray([r[-1] for r, _, _ in bad_recv], dtype=np.int64))
-            self.stats["crc_failures"] += len(bad_recv)
-        if len(cached_send):
-            ids = np.asarray([send_ids[tuple(int(x) for x in r[:4])] for r in cached_send], dtype=np.int64)
-            ids = ids[ids >= 0]
-            if len(ids):
-                self.store.unpin(ids)
-        # ---------------- 6. completions
-        sent_bytes = int(send_rows[:, 4].sum()) if len(send_rows) else 0
-        self.stats["upload"] += sent_bytes
-        shaped_ms = self._cdn_shaped_ms
-        for w, eid, off, n in cdn_entries:
-            if w.key in self._wants and self._wants[w.key] is w:
+        arena = self.arena
+        for w, eid, off, n in h.cdn_entries:
+            if self._wants.get(w.key) is w:
                 del self._wants[w.key]
-                for req in w.waiters:
-                    c = _Completion(req, self.arena[off:off + n], "cdn", n, max(cdn_ms, shaped_ms), 0.0, entry=eid)
-                    c.delay = shaped_ms
-                    completions.append(c)
-        for row, off, n in good_recv:
-            wid = int(row[7])
-            w = by_id.get(wid)
-            if w is None or self._wants.get(w.key) is not w:
-                continue
-            del self._wants[w.key]
             for req in w.waiters:
-                completions.append(_Completion(req, self.arena[off:off + n], "p2p", n, 0.0, p2p_ms, entry=row[-1]))
-        for row, off, n in bad_recv:
-            w = by_id.get(int(row[7]))
+                completions.append(_Completion(req, arena[off:off + n], "cdn", n, max(h.cdn_ms, h.shaped_ms), 0.0,
+                                               eid, h.shaped_ms))
+        for row, off, n in good:
+            w = h.by_id.get(int(row[7]))
+            if w is None:
+                continue
+            if self._wants.get(w.key) is w:
+                del self._wants[w.key]
+            for req in w.waiters:
+                completions.append(_Completion(req, arena[off:off + n], "p2p", n, 0.0, h.p2p_ms, int(row[-1])))
+        for row, off, n in bad:
+            w = h.by_id.get(int(row[7]))
             if w is not None:
                 w.force_cdn = True  # corrupted peer copy: go to the CDN next round
                 w.attempts += 1
+                w.round = -1
+        for w in h.wants:  # planned but not served (e.g. a CDN error already reported)
+            if w.round == h.round and self._wants.get(w.key) is w and not any(
+                    e[0] is w for e in h.cdn_entries) and not any(
+                    h.by_id.get(int(r[7])) is w for r, _, _ in h.recv_entries):
+                w.round = -1
+        t2 = time.perf_counter()
+        self.timer.add("commit", t2 - t1)
         self._deliver(completions)
-        self.last_round = {"wants": int(len(all_wants)), "cdn": int(len(cdn_rows)), "send": int(len(send_rows)),
-                           "recv": int(len(recv_rows)), "cdn_ms": cdn_ms, "p2p_ms": p2p_ms,
-                           "ms": (time.perf_counter() - t0) * 1e3}
-        if self._wants:
+        self.timer.add("deliver", time.perf_counter() - t2)
+        self.timer.add("dev_cdn_ms", h.cdn_ms / 1e3)
+        self.timer.add("dev_p2p_ms", h.p2p_ms / 1e3)
+        self.last_round = {"wants": h.n_wants, "cdn": len(h.cdn_entries), "send": h.n_send,
+                           "recv": len(h.recv_entries), "cdn_ms": h.cdn_ms, "p2p_ms": h.p2p_ms,
+                           "ms": (time.perf_counter() - h.t0) * 1e3}
+        if any(w.round < 0 for w in self._wants.values()):
             self._schedule()
-        return all_leaving
 
-    def _cdn_phase(self, cdn_rows: np.ndarray, by_id: Dict[int, _Want], completions: List[_Completion]):
-        wants = []
-        sources = []
-        for row in cdn_rows:
-            w = by_id.get(int(row[7]))
+    # ------------------------------------------------------------------ phases
+    def _cdn_phase(self, h: RoundHandle, cdn_rows: np.ndarray) -> None:
+        wants, sources = [], []
+        for wid in cdn_rows[:, 7].tolist():
+            w = h.by_id.get(wid)
             if w is None:
                 continue
             try:
                 origin, path = http.resolve(w.url)
                 data, off, n, _ = origin.resource(path)
-                rng = http.parse_range(w.headers)
+                rng = http.parse_range(w.headers) if w.headers else None
                 if rng is not None:
                     s, e = rng
                     e = n - 1 if e is None else min(e, n - 1)
                     off, n = off + s, max(0, e - s + 1)
                 corrupt = origin.should_corrupt(path)
             except http.HttpError as e:
-                del self._wants[w.key]
+                if self._wants.get(w.key) is w:
+                    del self._wants[w.key]
                 for req in w.waiters:
                     self.loop.call_soon(self._fail, req, e)
                 continue
             wants.append(w)
             sources.append((data, off, n, corrupt))
         if not wants:
-            return [], 0.0, None
+            return
         keys = np.asarray([w.key for w in wants], dtype=np.int64)
         lens = np.asarray([s[2] for s in sources], dtype=np.int64)
         res = self.store.reserve_run(keys, lens, self.round)
@@ -431,82 +505,69 @@ class SwarmNode:
             raise RuntimeError("segment cache cannot make room (pinned entries block eviction)")
         _, ids, offs = res
         self._grow_crc(int(ids.max()) + 1)
-        ev = None
         if self.is_cuda:
             start = torch.cuda.Event(enable_timing=True)
             end = torch.cuda.Event(enable_timing=True)
-            cur = torch.cuda.current_stream(self.device)
-            self.cdn_stream.wait_stream(cur)
-            with torch.cuda.stream(self.cdn_stream):
-                start.record()
-                for (data, off, n, _), doff in zip(sources, offs):
-                    self.arena[doff:doff + n].copy_(data[off:off + n], non_blocking=True)
-                end.record()
-            cur.wait_stream(self.cdn_stream)
-            ev = (start, end)
+            start.record()
+            _h2d_batch(self.arena, offs, sources)
+            end.record()
+            h.ev_cdn = (start, end)
         else:
             t = time.perf_counter()
-            for (data, off, n, _), doff in zip(sources, offs):
+            for (data, off, n, _), doff in zip(sources, offs.tolist()):
                 self.arena[doff:doff + n].copy_(data[off:off + n])
-            ms = (time.perf_counter() - t) * 1e3
-        for (_, _, n, corrupt), doff in zip(sources, offs):
+            h.cdn_ms = (time.perf_counter() - t) * 1e3
+        for (_, _, n, corrupt), doff in zip(sources, offs.tolist()):
             if corrupt and n:
                 self.arena[doff + n // 2] ^= 0xFF
         crc, _ = _crc.crc32_batch(self.arena, offs.tolist(), lens.tolist())
-        self.crc_dev[torch.from_numpy(ids).to(self.device)] = crc
+        self.crc_dev[torch.from_numpy(ids).to(self.device, non_blocking=True)] = crc
+        self.store.commit(ids)  # announced next round; peers' reads are stream-ordered after the H2D
         # CDN bandwidth shaping (xhr-shaper analog): completions are deferred by the modelled
         # transfer time of this round's CDN bytes
-        self._cdn_shaped_ms = http.Shaper.transfer_ms(int(lens.sum()))
-        nbytes = int(lens.sum())
-        self.stats["cdn"] += nbytes
+        h.shaped_ms = http.Shaper.transfer_ms(int(lens.sum()))
+        self.stats["cdn"] += int(lens.sum())
         self.stats["cdn_segments"] += len(wants)
-        entries = [(w, int(eid), int(o), int(n)) for w, eid, o, n in zip(wants, ids, offs, lens)]
-        return entries, (0.0 if self.is_cuda else ms), ev
+        h.cdn_entries = [(w, eid, o, n) for w, eid, o, n in zip(wants, ids.tolist(), offs.tolist(), lens.tolist())]
 
-    def _p2p_phase(self, send_rows: np.ndarray, recv_rows: np.ndarray, send_ids: Dict):
-        if not len(send_rows) and not len(recv_rows):
-            return [], 0.0, None, None
+    def _p2p_phase(self, h: RoundHandle, send_rows: np.ndarray, recv_rows: np.ndarray, send_ids: Dict) -> None:
         sends: List[Tuple[int, torch.Tensor]] = []
         recvs: List[Tuple[int, torch.Tensor]] = []
+        dev = self.device
         # --- sends: one contiguous buffer (+ CRC trailer) per destination
-        for dst in np.unique(send_rows[:, 6]) if len(send_rows) else []:
+        for dst in (np.unique(send_rows[:, 6]).tolist() if len(send_rows) else []):
             rows = send_rows[send_rows[:, 6] == dst]
-            ids = np.asarray([send_ids.get(tuple(int(x) for x in r[:4]), -1) for r in rows], dtype=np.int64)
+            ids = np.asarray([send_ids.get(tuple(r[:4]), -1) for r in rows.tolist()], dtype=np.int64)
             present = ids >= 0
+            sizes = rows[:, 4]
+            contiguous = False
             if present.all():
                 ent = self.store.entries(ids)
                 offs, lens = ent[:, 0], ent[:, 1]
-                contiguous = bool(np.all(offs[1:] == offs[:-1] + (lens[:-1] + ALIGN - 1) // ALIGN * ALIGN)) \
-                    and np.all(lens == rows[:, 4])
-            else:
-                contiguous = False
-            sizes = rows[:, 4]
+                contiguous = bool(np.all(offs[1:] == offs[:-1] + (lens[:-1] + ALIGN - 1) // ALIGN * ALIGN)
+                                  and np.all(lens == sizes))
             if contiguous:
                 total = int(offs[-1] + lens[-1] - offs[0])
                 buf = self.arena[int(offs[0]):int(offs[0]) + total]
-                trailer = self.crc_dev[torch.from_numpy(ids).to(self.device)]
+                trailer = self.crc_dev[torch.from_numpy(ids).to(dev, non_blocking=True)]
             else:
                 layout = np.zeros(len(rows), dtype=np.int64)
                 if len(rows) > 1:
                     layout[1:] = np.cumsum((sizes[:-1] + ALIGN - 1) // ALIGN * ALIGN)
                 total = int(layout[-1] + sizes[-1])
-                buf = torch.zeros(total, dtype=torch.uint8, device=self.device)
-                trailer = torch.full((len(rows),), 0, dtype=torch.int32, device=self.device)
+                buf = torch.zeros(total, dtype=torch.uint8, device=dev)
+                trailer = torch.full((len(rows),), -1, dtype=torch.int32, device=dev)  # missing: bad CRC
                 if present.any():
                     ent = self.store.entries(ids[present])
                     n_copy = np.minimum(ent[:, 1], sizes[present])
                     _seg.copy_segments(self.arena, buf, ent[:, 0], layout[present], n_copy)
-                    pidx = torch.from_numpy(np.nonzero(present)[0]).to(self.device)
-                    trailer[pidx] = self.crc_dev[torch.from_numpy(ids[present]).to(self.device)]
-                if (~present).any():  # stale directory: send a guaranteed-bad CRC
-                    midx = torch.from_numpy(np.nonzero(~present)[0]).to(self.device)
-                    trailer[midx] = -1
+                    pidx = torch.from_numpy(np.nonzero(present)[0]).to(dev)
+                    trailer[pidx] = self.crc_dev[torch.from_numpy(ids[present]).to(dev)]
             sends.append((int(dst), buf))
             sends.append((int(dst), trailer.contiguous()))
         # --- recvs: reserve one contiguous run per source
-        recv_entries = []
         trailers = []
-        for src in np.unique(recv_rows[:, 5]) if len(recv_rows) else []:
+        for src in (np.unique(recv_rows[:, 5]).tolist() if len(recv_rows) else []):
             rows = recv_rows[recv_rows[:, 5] == src]
             keys = np.ascontiguousarray(rows[:, :4])
             lens = np.ascontiguousarray(rows[:, 4])
@@ -517,13 +578,11 @@ class SwarmNode:
             self._grow_crc(int(ids.max()) + 1)
             total = int(offs[-1] + lens[-1] - offs[0])
             recvs.append((int(src), self.arena[int(base):int(base) + total]))
-            tr = torch.empty(len(rows), dtype=torch.int32, device=self.device)
+            tr = torch.empty(len(rows), dtype=torch.int32, device=dev)
             recvs.append((int(src), tr))
             trailers.append(tr)
-            for r, eid, o, n in zip(rows, ids, offs, lens):
-                row = np.concatenate([r, [eid]])
-                recv_entries.append((row, int(o), int(n)))
-        ev = None
+            for r, eid, o, n in zip(rows, ids.tolist(), offs.tolist(), lens.tolist()):
+                h.recv_entries.append((np.append(r, eid), o, n))
         t = time.perf_counter()
         if self.is_cuda:
             start = torch.cuda.Event(enable_timing=True)
@@ -532,21 +591,29 @@ class SwarmNode:
         self.comm.exchange(sends, recvs)
         if self.is_cuda:
             end.record()
-            ev = (start, end)
-        ms = (time.perf_counter() - t) * 1e3
-        if self.corrupt_next_recv > 0 and recv_entries:  # fault injection: transport corruption
+            h.ev_p2p = (start, end)
+        else:
+            h.p2p_ms = (time.perf_counter() - t) * 1e3
+        if not h.recv_entries:
+            return
+        if self.corrupt_next_recv > 0:  # fault injection: transport corruption
             self.corrupt_next_recv -= 1
-            _, o, n = recv_entries[0]
+            _, o, n = h.recv_entries[0]
             if n:
                 self.arena[o + n // 2] ^= 0x5A
-        expect = torch.cat(trailers) if trailers else None
-        if recv_entries:
-            ids = torch.from_numpy(np.asarray([r[-1] for r, _, _ in recv_entries], dtype=np.int64)).to(self.device)
-            self.crc_dev[ids] = expect
-        nbytes = int(recv_rows[:, 4].sum()) if len(recv_rows) else 0
-        self.stats["p2p"] += nbytes
+        expect = torch.cat(trailers)
+        ids_t = torch.from_numpy(np.asarray([r[-1] for r, _, _ in h.recv_entries], dtype=np.int64)).to(
+            dev, non_blocking=True)
+        self.crc_dev[ids_t] = expect
+        _, ok = _crc.crc32_batch(self.arena, [o for _, o, _ in h.recv_entries],
+                                 [n for _, _, n in h.recv_entries], expect_dev=expect)
+        if self.is_cuda:
+            h.ok_host = torch.empty(ok.numel(), dtype=torch.uint8, pin_memory=True)
+            h.ok_host.copy_(ok, non_blocking=True)
+        else:
+            h.ok_host = ok
+        self.stats["p2p"] += int(recv_rows[:, 4].sum())
         self.stats["p2p_segments"] += len(recv_rows)
-        return recv_entries, ms, ev, expect
 
     # ------------------------------------------------------------------ delivery
     def _deliver(self, completions: List[_Completion]) -> None:
@@ -574,7 +641,7 @@ class SwarmNode:
         if pin:
             arr = np.asarray(pin, dtype=np.int64)
             self.store.pin(arr)
-            self._pinned_last.extend(pin)
+            self._pins.append((self.round + PIN_DELAY_ROUNDS, arr))
         for c in completions:
             req = c.req
             if req.aborted or req.done:
@@ -584,17 +651,16 @@ class SwarmNode:
             if req.agent is not None:
                 req.agent._account(c.source, c.nbytes)
             cb = req.callbacks
-            get = cb.get if isinstance(cb, dict) else (lambda k, _cb=cb: getattr(_cb, k, None))
-            on_progress = get("onProgress")
+            if isinstance(cb, dict):
+                on_progress, on_success = cb.get("onProgress"), cb.get("onSuccess")
+            else:
+                on_progress, on_success = getattr(cb, "onProgress", None), getattr(cb, "onSuccess", None)
             if on_progress is not None:
-                evt = {"cdnDownloaded": c.nbytes if c.source == "cdn" else 0,
-                       "p2pDownloaded": c.nbytes if c.source in ("p2p", "cache") else 0,
-                       "cdnDuration": c.cdn_ms if c.source == "cdn" else 0.0,
-                       "p2pDuration": c.p2p_ms if c.source == "p2p" else 0.0}
-                on_progress(evt)
+                p2p = c.source in ("p2p", "cache")
+                on_progress({"cdnDownloaded": 0 if p2p else c.nbytes, "p2pDownloaded": c.nbytes if p2p else 0,
+                             "cdnDuration": 0.0 if p2p else c.cdn_ms, "p2pDuration": c.p2p_ms if p2p else 0.0})
             if req.aborted:
                 continue
-            on_success = get("onSuccess")
             if on_success is not None:
                 on_success(c.data)
 
@@ -619,6 +685,19 @@ class SwarmNode:
         return p / (p + c) if (p + c) else 0.0
 
 
+def _h2d_batch(arena: torch.Tensor, dst_offs: np.ndarray, sources: List[Tuple[torch.Tensor, int, int, bool]]) -> None:
+    """Enqueue one pinned-host -> HBM copy per segment on the current stream, in a single
+    native call (``hipMemcpyAsync`` loop) instead of one Python/ATen dispatch per segment."""
+    from ..ops._native import device as _dev
+
+    src_ptrs = np.asarray([d.data_ptr() + o for d, o, _, _ in sources], dtype=np.int64)
+    lens = np.asarray([n for _, _, n, _ in sources], dtype=np.int64)
+    for d, _, _, _ in sources:
+        if not d.is_pinned():
+            raise RuntimeError("CDN origin buffers must be pinned host memory for the async H2D path")
+    _dev().h2d_batch(arena, np.ascontiguousarray(dst_offs, dtype=np.int64), src_ptrs, lens)
+
+
 # ---------------------------------------------------------------------- registry
 _local = threading.local()
 
@@ -636,7 +715,7 @@ def node_for_config(p2p_config: Any) -> SwarmNode:
 
     ``gpuSwarm`` keys: ``backend`` ("auto" | "local" | "dist" | "thread"), ``hub`` and
     ``rank`` (thread backend), ``device``, ``cacheBytes``, ``cdnDedup``,
-    ``roundIntervalMs``, ``autoTick``.
+    ``roundIntervalMs``, ``autoTick``, ``maxWantsPerRound``.
     """
     node = current_node()
     if node is not None and not node.closed:
@@ -662,6 +741,6 @@ def node_for_config(p2p_config: Any) -> SwarmNode:
         raise ValueError(f"unknown gpuSwarm backend {backend!r}")
     node = SwarmNode(comm, device=cfg.get("device", "auto"), cache_bytes=int(cfg.get("cacheBytes", 1 << 30)),
                      cdn_dedup=bool(cfg.get("cdnDedup", True)), round_interval_ms=cfg.get("roundIntervalMs"),
-                     auto_tick=bool(cfg.get("autoTick", True)))
+                     auto_tick=bool(cfg.get("autoTick", True)), max_wants_per_round=cfg.get("maxWantsPerRound"))
     set_current_node(node)
     return node

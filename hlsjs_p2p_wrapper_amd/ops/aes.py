@@ -76,11 +76,13 @@ def cbc_decrypt_batch(src: torch.Tensor, src_offs: Sequence[int], nbytes: Sequen
         return torch.from_numpy(out_len)
     blk_prefix = np.zeros(B + 1, dtype=np.int64)
     np.cumsum(nb // 16, out=blk_prefix[1:])
-    d = pack_to_device({"so": so, "do": do, "bp": blk_prefix, "drk": drk, "iv": iv}, src.device)
+    pair_prefix = np.zeros(B + 1, dtype=np.int64)  # work unit: 2 blocks of one segment
+    np.cumsum((nb // 16 + 1) // 2, out=pair_prefix[1:])
+    d = pack_to_device({"so": so, "do": do, "bp": blk_prefix, "pp": pair_prefix, "drk": drk, "iv": iv}, src.device)
     out_len = torch.empty(B, dtype=torch.int64, device=src.device)
     td0, isb = _device_tables(src.device)
-    _dev().aes128_cbc_decrypt(src, dst, d["so"], d["do"], d["bp"], d["drk"], d["iv"], td0, isb, out_len,
-                              int(blk_prefix[-1]))
+    _dev().aes128_cbc_decrypt(src, dst, d["so"], d["do"], d["bp"], d["pp"], d["drk"], d["iv"], td0, isb, out_len,
+                              int(pair_prefix[-1]))
     return out_len
 
 

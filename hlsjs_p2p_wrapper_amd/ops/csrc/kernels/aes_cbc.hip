@@ -1,140 +1,156 @@
 // AES-128-CBC decryption of a batch of HLS segments — CDNA4 / gfx950.
 //
-// CBC *decryption* is block-parallel: P_i = D_K(C_i) xor C_{i-1}.  One lane decrypts one
-// 16-byte block per iteration; consecutive lanes take consecutive blocks, so every wave
-// moves 1 KiB with fully coalesced dwordx4 loads/stores (the C_{i-1} re-load hits L1).
+// CBC *decryption* is block-parallel: P_i = D_K(C_i) xor C_{i-1}.  Work unit = a PAIR of
+// consecutive 16-byte blocks of one segment: each lane runs two independent AES chains
+// interleaved (ILP hides the LDS latency of each round's 16 dependent table lookups) and
+// moves 32 contiguous bytes, so a wave streams 2 KiB with dwordx4 loads/stores
+// (C_{i-1} for the pair's first block is an L1 hit: the neighbour lane loaded it).
 //
-// AES is table/bit bound, not matmul shaped (no MFMA).  The limiter is LDS: each block
-// does 144 T-table lookups + 16 inverse-S-box lookups.  Random 32-bit lookups into a
-// 1 KiB table from 32 lanes hit the 32 banks of ds_read_b32 with ~3-4-way conflicts, so
-// the tables are REPLICATED 32x with entry e of copy c at word e*32 + c and lane l reads
-// copy (l & 31): every lane of a 32-lane group owns a bank -> conflict-free, 2 LDS
-// cycles per wave lookup.  Td1..Td3 are byte rotations of Td0 (v_alignbit), so the
-// whole working set is Td0 x32 (32 KiB) + InvSbox x32 (32 KiB) = 64 KiB -> 2
-// workgroups (8 waves) per CU; the VALU work (~700 ops/block) and LDS work balance at
-// roughly 5 CU-cycles per block.
+// AES is table bound, not matmul shaped (no MFMA).  Random 32-bit lookups from 32 lanes
+// into a 1 KiB table hit the 32 ds_read_b32 banks with 3-4-way conflicts, so the Td0
+// table (9 rounds x 16 lookups) is REPLICATED 32x: entry e of copy c at word e*32 + c, lane
+// l reads copy (l & 31) -> every lane of a 32-lane half owns a bank, conflict-free.
+// Td1..Td3 are byte rotations of Td0 (v_alignbit).  The final-round inverse S-box (16 of
+// 160 lookups) is replicated 8x only (<= 4-way conflicts on 10% of the lookups), which
+// keeps the LDS footprint at 40 KiB -> 4 workgroups (16 waves) per CU.
 //
-// Persistent grid: 2 workgroups per CU, each streams one contiguous range of the batch's
-// global block index space (good DRAM locality), walking the segment table monotonically
-// so the per-segment state (44 round keys, IV, offsets) is reloaded only at boundaries.
-// PKCS#7: the lane that decrypts a segment's last block validates the padding and writes
-// the plaintext length (or -1) to out_len[seg] — the demux kernels read it on device, so
-// no host round trip sits between decrypt and demux.
+// Persistent grid (4 workgroups per CU), each streaming one contiguous range of the batch's
+// pair index space; the segment table is walked monotonically so per-segment state (44
+// round keys, IV, offsets) reloads only at boundaries.  PKCS#7: the lane holding a
+// segment's last block validates the padding and writes the plaintext length (or -1) to
+// out_len[seg] on device — the demux kernels read it directly (no host round trip).
 #include "common.h"
 
 namespace hlsp2p {
 namespace dev {
 
 constexpr int kAesThreads = 256;
-constexpr int kRep = 32;
+constexpr int kAesWgPerCu = 4;
+constexpr int kRepTd = 32;
+constexpr int kRepIs = 8;
 
-__global__ __launch_bounds__(kAesThreads, 2) void aes128_cbc_decrypt_kernel(
-    const uint8_t* __restrict__ src, uint8_t* __restrict__ dst, const int64_t* __restrict__ src_off,
-    const int64_t* __restrict__ dst_off, const int64_t* __restrict__ blk_prefix, const uint32_t* __restrict__ drk,
-    const uint32_t* __restrict__ ivw, const uint32_t* __restrict__ td0_g, const uint8_t* __restrict__ isb_g,
-    int64_t* __restrict__ out_len, int nseg, int64_t total, int64_t per_wg) {
-  __shared__ uint32_t s_td[256 * kRep];
-  __shared__ uint32_t s_is[256 * kRep];
-  const int tid = threadIdx.x;
-  const uint32_t l32 = tid & 31;
-  for (int i = tid; i < 256 * kRep; i += kAesThreads) {
-    s_td[i] = td0_g[i >> 5];
-    s_is[i] = isb_g[i >> 5];
+#define TD(x) s_td[((x) << 5) | l32]
+#define IS(x) s_is[((x) << 3) | l8]
+
+#define AES_ROUND(s0, s1, s2, s3, t0, t1, t2, t3, k)                                                          \
+  t0 = TD(s0 >> 24) ^ rotr(TD((s3 >> 16) & 0xff), 8) ^ rotr(TD((s2 >> 8) & 0xff), 16) ^ rotr(TD(s1 & 0xff), 24) ^ \
+       (k)[0];                                                                                                 \
+  t1 = TD(s1 >> 24) ^ rotr(TD((s0 >> 16) & 0xff), 8) ^ rotr(TD((s3 >> 8) & 0xff), 16) ^ rotr(TD(s2 & 0xff), 24) ^ \
+       (k)[1];                                                                                                 \
+  t2 = TD(s2 >> 24) ^ rotr(TD((s1 >> 16) & 0xff), 8) ^ rotr(TD((s0 >> 8) & 0xff), 16) ^ rotr(TD(s3 & 0xff), 24) ^ \
+       (k)[2];                                                                                                 \
+  t3 = TD(s3 >> 24) ^ rotr(TD((s2 >> 16) & 0xff), 8) ^ rotr(TD((s1 >> 8) & 0xff), 16) ^ rotr(TD(s0 & 0xff), 24) ^ \
+       (k)[3];
+
+#define AES_FINAL(s0, s1, s2, s3, o0, o1, o2, o3, k)                                                        \
+  o0 = ((IS(s0 >> 24) << 24) | (IS((s3 >> 16) & 0xff) << 16) | (IS((s2 >> 8) & 0xff) << 8) | IS(s1 & 0xff)) ^ \
+       (k)[0];                                                                                               \
+  o1 = ((IS(s1 >> 24) << 24) | (IS((s0 >> 16) & 0xff) << 16) | (IS((s3 >> 8) & 0xff) << 8) | IS(s2 & 0xff)) ^ \
+       (k)[1];                                                                                               \
+  o2 = ((IS(s2 >> 24) << 24) | (IS((s1 >> 16) & 0xff) << 16) | (IS((s0 >> 8) & 0xff) << 8) | IS(s3 & 0xff)) ^ \
+       (k)[2];                                                                                               \
+  o3 = ((IS(s3 >> 24) << 24) | (IS((s2 >> 16) & 0xff) << 16) | (IS((s1 >> 8) & 0xff) << 8) | IS(s0 & 0xff)) ^ \
+       (k)[3];
+
+__device__ __forceinline__ int64_t pkcs7_len(uint4 p, int64_t nbytes) {
+  const uint32_t pad = p.w >> 24;
+  if (pad < 1 || pad > 16) return -1;
+  const uint32_t w[4] = {p.x, p.y, p.z, p.w};
+  bool ok = true;
+#pragma unroll
+  for (int b = 0; b < 16; ++b) {
+    const uint32_t byte = (w[b >> 2] >> (8 * (b & 3))) & 0xff;
+    if (b >= 16 - static_cast<int>(pad) && byte != pad) ok = false;
   }
+  return ok ? nbytes - static_cast<int64_t>(pad) : -1;
+}
+
+__global__ __launch_bounds__(kAesThreads, kAesWgPerCu) void aes128_cbc_decrypt_kernel(
+    const uint8_t* __restrict__ src, uint8_t* __restrict__ dst, const int64_t* __restrict__ src_off,
+    const int64_t* __restrict__ dst_off, const int64_t* __restrict__ blk_prefix,
+    const int64_t* __restrict__ pair_prefix, const uint32_t* __restrict__ drk, const uint32_t* __restrict__ ivw,
+    const uint32_t* __restrict__ td0_g, const uint8_t* __restrict__ isb_g, int64_t* __restrict__ out_len, int nseg,
+    int64_t total_pairs, int64_t per_wg) {
+  __shared__ uint32_t s_td[256 * kRepTd];
+  __shared__ uint32_t s_is[256 * kRepIs];
+  const int tid = threadIdx.x;
+  const uint32_t l32 = tid & 31, l8 = tid & 7;
+  for (int i = tid; i < 256 * kRepTd; i += kAesThreads) s_td[i] = td0_g[i >> 5];
+  for (int i = tid; i < 256 * kRepIs; i += kAesThreads) s_is[i] = isb_g[i >> 3];
   __syncthreads();
 
   const int64_t begin = static_cast<int64_t>(blockIdx.x) * per_wg;
-  const int64_t end = begin + per_wg < total ? begin + per_wg : total;
-
-#define TD(x) s_td[((x) << 5) | l32]
-#define IS(x) s_is[((x) << 5) | l32]
-
+  const int64_t end = begin + per_wg < total_pairs ? begin + per_wg : total_pairs;
   int cur = -1;
   uint32_t rk[44];
   uint32_t iv0 = 0, iv1 = 0, iv2 = 0, iv3 = 0;
-  int64_t so = 0, dof = 0, bstart = 0, bend = 0;
-  for (int64_t gb = begin + tid; gb < end; gb += kAesThreads) {
-    if (cur < 0 || gb >= bend) {
-      cur = cur < 0 ? find_seg(blk_prefix, nseg, gb) : advance_seg(blk_prefix, cur, gb);
+  int64_t so = 0, dof = 0, pstart = 0, pend = 0, nblk = 0;
+  for (int64_t gp = begin + tid; gp < end; gp += kAesThreads) {
+    if (cur < 0 || gp >= pend) {
+      cur = cur < 0 ? find_seg(pair_prefix, nseg, gp) : advance_seg(pair_prefix, cur, gp);
 #pragma unroll
       for (int k = 0; k < 44; ++k) rk[k] = drk[cur * 44 + k];
       iv0 = ivw[cur * 4 + 0]; iv1 = ivw[cur * 4 + 1]; iv2 = ivw[cur * 4 + 2]; iv3 = ivw[cur * 4 + 3];
       so = src_off[cur];
       dof = dst_off[cur];
-      bstart = blk_prefix[cur];
-      bend = blk_prefix[cur + 1];
+      pstart = pair_prefix[cur];
+      pend = pair_prefix[cur + 1];
+      nblk = blk_prefix[cur + 1] - blk_prefix[cur];
     }
-    const int64_t i = gb - bstart;
-    const uint4* cp = reinterpret_cast<const uint4*>(src + so) + i;
-    const uint4 c = *cp;
+    const int64_t i0 = 2 * (gp - pstart);
+    const bool has2 = i0 + 1 < nblk;
+    const uint4* cp = reinterpret_cast<const uint4*>(src + so) + i0;
+    const uint4 c0 = cp[0];
+    const uint4 c1 = has2 ? cp[1] : c0;
     uint4 pv;
-    if (i == 0) {
-      pv.x = iv0; pv.y = iv1; pv.z = iv2; pv.w = iv3;
+    if (i0 == 0) {
+      pv = make_uint4(iv0, iv1, iv2, iv3);
     } else {
       pv = cp[-1];
     }
-    uint32_t s0 = bswap32(c.x) ^ rk[0], s1 = bswap32(c.y) ^ rk[1], s2 = bswap32(c.z) ^ rk[2],
-             s3 = bswap32(c.w) ^ rk[3];
+    uint32_t a0 = bswap32(c0.x) ^ rk[0], a1 = bswap32(c0.y) ^ rk[1], a2 = bswap32(c0.z) ^ rk[2],
+             a3 = bswap32(c0.w) ^ rk[3];
+    uint32_t b0 = bswap32(c1.x) ^ rk[0], b1 = bswap32(c1.y) ^ rk[1], b2 = bswap32(c1.z) ^ rk[2],
+             b3 = bswap32(c1.w) ^ rk[3];
 #pragma unroll
     for (int r = 1; r < 10; ++r) {
-      const uint32_t t0 = TD(s0 >> 24) ^ rotr(TD((s3 >> 16) & 0xff), 8) ^ rotr(TD((s2 >> 8) & 0xff), 16) ^
-                          rotr(TD(s1 & 0xff), 24) ^ rk[4 * r + 0];
-      const uint32_t t1 = TD(s1 >> 24) ^ rotr(TD((s0 >> 16) & 0xff), 8) ^ rotr(TD((s3 >> 8) & 0xff), 16) ^
-                          rotr(TD(s2 & 0xff), 24) ^ rk[4 * r + 1];
-      const uint32_t t2 = TD(s2 >> 24) ^ rotr(TD((s1 >> 16) & 0xff), 8) ^ rotr(TD((s0 >> 8) & 0xff), 16) ^
-                          rotr(TD(s3 & 0xff), 24) ^ rk[4 * r + 2];
-      const uint32_t t3 = TD(s3 >> 24) ^ rotr(TD((s2 >> 16) & 0xff), 8) ^ rotr(TD((s1 >> 8) & 0xff), 16) ^
-                          rotr(TD(s0 & 0xff), 24) ^ rk[4 * r + 3];
-      s0 = t0; s1 = t1; s2 = t2; s3 = t3;
+      uint32_t t0, t1, t2, t3, u0, u1, u2, u3;
+      AES_ROUND(a0, a1, a2, a3, t0, t1, t2, t3, rk + 4 * r)
+      AES_ROUND(b0, b1, b2, b3, u0, u1, u2, u3, rk + 4 * r)
+      a0 = t0; a1 = t1; a2 = t2; a3 = t3;
+      b0 = u0; b1 = u1; b2 = u2; b3 = u3;
     }
-    const uint32_t o0 = ((IS(s0 >> 24) << 24) | (IS((s3 >> 16) & 0xff) << 16) | (IS((s2 >> 8) & 0xff) << 8) |
-                         IS(s1 & 0xff)) ^ rk[40];
-    const uint32_t o1 = ((IS(s1 >> 24) << 24) | (IS((s0 >> 16) & 0xff) << 16) | (IS((s3 >> 8) & 0xff) << 8) |
-                         IS(s2 & 0xff)) ^ rk[41];
-    const uint32_t o2 = ((IS(s2 >> 24) << 24) | (IS((s1 >> 16) & 0xff) << 16) | (IS((s0 >> 8) & 0xff) << 8) |
-                         IS(s3 & 0xff)) ^ rk[42];
-    const uint32_t o3 = ((IS(s3 >> 24) << 24) | (IS((s2 >> 16) & 0xff) << 16) | (IS((s1 >> 8) & 0xff) << 8) |
-                         IS(s0 & 0xff)) ^ rk[43];
-    uint4 p;
-    p.x = bswap32(o0) ^ pv.x;
-    p.y = bswap32(o1) ^ pv.y;
-    p.z = bswap32(o2) ^ pv.z;
-    p.w = bswap32(o3) ^ pv.w;
-    reinterpret_cast<uint4*>(dst + dof)[i] = p;
-    if (gb == bend - 1) {  // last block of the segment: PKCS#7 check
-      const uint32_t pad = p.w >> 24;
-      int64_t len = -1;
-      if (pad >= 1 && pad <= 16) {
-        bool ok = true;
-        const uint32_t w[4] = {p.x, p.y, p.z, p.w};
-#pragma unroll
-        for (int b = 0; b < 16; ++b) {
-          const uint32_t byte = (w[b >> 2] >> (8 * (b & 3))) & 0xff;
-          if (b >= 16 - static_cast<int>(pad) && byte != pad) ok = false;
-        }
-        if (ok) len = (bend - bstart) * 16 - static_cast<int64_t>(pad);
-      }
-      out_len[cur] = len;
-    }
+    uint32_t o0, o1, o2, o3, q0, q1, q2, q3;
+    AES_FINAL(a0, a1, a2, a3, o0, o1, o2, o3, rk + 40)
+    AES_FINAL(b0, b1, b2, b3, q0, q1, q2, q3, rk + 40)
+    uint4 p0, p1;
+    p0.x = bswap32(o0) ^ pv.x; p0.y = bswap32(o1) ^ pv.y; p0.z = bswap32(o2) ^ pv.z; p0.w = bswap32(o3) ^ pv.w;
+    p1.x = bswap32(q0) ^ c0.x; p1.y = bswap32(q1) ^ c0.y; p1.z = bswap32(q2) ^ c0.z; p1.w = bswap32(q3) ^ c0.w;
+    uint4* dp = reinterpret_cast<uint4*>(dst + dof) + i0;
+    dp[0] = p0;
+    if (has2) dp[1] = p1;
+    if (i0 == nblk - 1) out_len[cur] = pkcs7_len(p0, nblk * 16);
+    if (has2 && i0 + 1 == nblk - 1) out_len[cur] = pkcs7_len(p1, nblk * 16);
   }
+}
 #undef TD
 #undef IS
-}
 
 hipError_t launch_aes128_cbc_decrypt(const uint8_t* src, uint8_t* dst, const int64_t* src_off, const int64_t* dst_off,
-                                     const int64_t* blk_prefix, const uint32_t* drk, const uint32_t* ivw,
-                                     const uint32_t* td0, const uint8_t* isb, int64_t* out_len, int nseg,
-                                     int64_t total_blocks, int num_cu, hipStream_t stream) {
-  if (total_blocks <= 0) return hipSuccess;
-  const int64_t max_wg = static_cast<int64_t>(num_cu) * 2;
-  int64_t grid = (total_blocks + kAesThreads * 4 - 1) / (kAesThreads * 4);
+                                     const int64_t* blk_prefix, const int64_t* pair_prefix, const uint32_t* drk,
+                                     const uint32_t* ivw, const uint32_t* td0, const uint8_t* isb, int64_t* out_len,
+                                     int nseg, int64_t total_pairs, int num_cu, hipStream_t stream) {
+  if (total_pairs <= 0) return hipSuccess;
+  const int64_t max_wg = static_cast<int64_t>(num_cu) * kAesWgPerCu;
+  int64_t grid = (total_pairs + kAesThreads * 4 - 1) / (kAesThreads * 4);
   if (grid > max_wg) grid = max_wg;
   if (grid < 1) grid = 1;
-  int64_t per_wg = (total_blocks + grid - 1) / grid;
+  int64_t per_wg = (total_pairs + grid - 1) / grid;
   per_wg = (per_wg + kAesThreads - 1) / kAesThreads * kAesThreads;
-  grid = (total_blocks + per_wg - 1) / per_wg;
+  grid = (total_pairs + per_wg - 1) / per_wg;
   hipLaunchKernelGGL(aes128_cbc_decrypt_kernel, dim3(static_cast<unsigned>(grid)), dim3(kAesThreads), 0, stream, src,
-                     dst, src_off, dst_off, blk_prefix, drk, ivw, td0, isb, out_len, nseg, total_blocks, per_wg);
+                     dst, src_off, dst_off, blk_prefix, pair_prefix, drk, ivw, td0, isb, out_len, nseg, total_pairs,
+                     per_wg);
   return hipGetLastError();
 }
 

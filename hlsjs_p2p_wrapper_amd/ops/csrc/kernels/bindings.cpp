@@ -3,12 +3,13 @@
 #include <c10/hip/HIPStream.h>
 #include <hip/hip_runtime_api.h>
 #include <torch/extension.h>
+#include <pybind11/numpy.h>
 
 namespace hlsp2p {
 namespace dev {
 hipError_t launch_aes128_cbc_decrypt(const uint8_t*, uint8_t*, const int64_t*, const int64_t*, const int64_t*,
-                                     const uint32_t*, const uint32_t*, const uint32_t*, const uint8_t*, int64_t*, int,
-                                     int64_t, int, hipStream_t);
+                                     const int64_t*, const uint32_t*, const uint32_t*, const uint32_t*,
+                                     const uint8_t*, int64_t*, int, int64_t, int, hipStream_t);
 hipError_t launch_crc32_batch(const uint8_t*, const int64_t*, const int64_t*, const int64_t*, const int64_t*,
                               const void*, const uint32_t*, uint32_t*, uint32_t*, const uint32_t*, uint8_t*, int,
                               int64_t, int, hipStream_t);
@@ -62,14 +63,16 @@ const T* cptr(const Tensor& t) { return reinterpret_cast<const T*>(t.data_ptr())
 template <typename T>
 T* mptr(const Tensor& t) { return reinterpret_cast<T*>(t.data_ptr()); }
 
-void aes128_cbc_decrypt(Tensor src, Tensor dst, Tensor src_off, Tensor dst_off, Tensor blk_prefix, Tensor drk,
-                        Tensor iv, Tensor td0, Tensor isb, Tensor out_len, int64_t total_blocks) {
+void aes128_cbc_decrypt(Tensor src, Tensor dst, Tensor src_off, Tensor dst_off, Tensor blk_prefix,
+                        Tensor pair_prefix, Tensor drk, Tensor iv, Tensor td0, Tensor isb, Tensor out_len,
+                        int64_t total_pairs) {
   const int64_t B = src_off.numel();
   check(src, "src", torch::kUInt8);
   check(dst, "dst", torch::kUInt8);
   check(src_off, "src_off", torch::kInt64);
   check(dst_off, "dst_off", torch::kInt64, B);
   check(blk_prefix, "blk_prefix", torch::kInt64, B + 1);
+  check(pair_prefix, "pair_prefix", torch::kInt64, B + 1);
   check(drk, "drk", torch::kInt32, B * 44);
   check(iv, "iv", torch::kUInt8, B * 16);
   check(td0, "td0", torch::kInt32, 256);
@@ -81,9 +84,9 @@ void aes128_cbc_decrypt(Tensor src, Tensor dst, Tensor src_off, Tensor dst_off, 
               "src/dst must be 16-byte aligned");
   same_device(src, dst);
   ok(D::launch_aes128_cbc_decrypt(cptr<uint8_t>(src), mptr<uint8_t>(dst), cptr<int64_t>(src_off),
-                                  cptr<int64_t>(dst_off), cptr<int64_t>(blk_prefix), cptr<uint32_t>(drk),
-                                  cptr<uint32_t>(iv), cptr<uint32_t>(td0), cptr<uint8_t>(isb), mptr<int64_t>(out_len),
-                                  static_cast<int>(B), total_blocks, num_cus(src), stream()),
+                                  cptr<int64_t>(dst_off), cptr<int64_t>(blk_prefix), cptr<int64_t>(pair_prefix),
+                                  cptr<uint32_t>(drk), cptr<uint32_t>(iv), cptr<uint32_t>(td0), cptr<uint8_t>(isb),
+                                  mptr<int64_t>(out_len), static_cast<int>(B), total_pairs, num_cus(src), stream()),
      "aes128_cbc_decrypt");
 }
 
@@ -132,7 +135,7 @@ void ts_demux(Tensor buf, Tensor seg_off, Tensor seg_len, Tensor blk_prefix, int
   check(es_off, "es_off", torch::kInt64, B);
   check(pes, "pes", torch::kInt64, B * 3 * max_pes * 3);
   check(info, "info", torch::kInt64, B * 24);
-  TORCH_CHECK((reinterpret_cast<uintptr_t>(buf.data_ptr()) & 3) == 0, "buf must be 4-byte aligned");
+  TORCH_CHECK((reinterpret_cast<uintptr_t>(buf.data_ptr()) & 15) == 0, "buf must be 16-byte aligned");
   ok(D::launch_ts_demux(cptr<uint8_t>(buf), cptr<int64_t>(seg_off), cptr<int64_t>(seg_len),
                         cptr<int64_t>(blk_prefix), static_cast<int>(B), total_blocks, mptr<uint32_t>(meta),
                         mptr<int64_t>(pts_dts), mptr<int32_t>(blk_sums), mptr<uint8_t>(es), cptr<int64_t>(es_off),
@@ -205,6 +208,28 @@ void segment_copy(Tensor src, Tensor dst, Tensor src_off, Tensor dst_off, Tensor
 
 int64_t device_cus(Tensor t) { return num_cus(t); }
 
+// CDN ingest: one hipMemcpyAsync per segment (pinned host -> HBM arena) on the current
+// stream — issued in one native call so a round's copies cost microseconds of host time.
+void h2d_batch(Tensor dst, pybind11::array_t<int64_t> dst_off, pybind11::array_t<int64_t> src_ptr,
+               pybind11::array_t<int64_t> len) {
+  check(dst, "dst", torch::kUInt8);
+  const int64_t n = dst_off.size();
+  TORCH_CHECK(src_ptr.size() == n && len.size() == n, "h2d_batch: argument sizes differ");
+  const int64_t* o = dst_off.data();
+  const int64_t* s = src_ptr.data();
+  const int64_t* l = len.data();
+  uint8_t* base = mptr<uint8_t>(dst);
+  const int64_t cap = dst.numel();
+  hipStream_t st = stream();
+  for (int64_t i = 0; i < n; ++i) {
+    TORCH_CHECK(o[i] >= 0 && l[i] >= 0 && o[i] + l[i] <= cap, "h2d_batch: destination out of bounds");
+    if (l[i] == 0) continue;
+    ok(hipMemcpyAsync(base + o[i], reinterpret_cast<const void*>(s[i]), static_cast<size_t>(l[i]),
+                      hipMemcpyHostToDevice, st),
+       "hipMemcpyAsync");
+  }
+}
+
 }  // namespace
 
 PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
@@ -218,5 +243,6 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("table_lookup", &table_lookup);
   m.def("segment_copy", &segment_copy);
   m.def("device_cus", &device_cus);
+  m.def("h2d_batch", &h2d_batch);
   m.attr("ARCH") = "gfx950";
 }

@@ -31,14 +31,32 @@ namespace dev {
 typedef int v4i __attribute__((ext_vector_type(4)));
 typedef int v16i __attribute__((ext_vector_type(16)));
 
-constexpr int kCrcThreads = 256;  // 4 waves, each owns 8 KiB tiles
+// 8 waves share one 64 KiB LDS copy of W: 2 workgroups per CU = 4 waves per SIMD, so one
+// wave's global loads / nibble expansion overlap other waves' MFMAs.
+constexpr int kCrcThreads = 512;
 constexpr int kTileBytes = 32 * 256;
 constexpr int kNumP = 40;
 constexpr int kSlice = 1024;  // u32 per byte-slice table set
 
 __device__ __forceinline__ uint32_t expand_nibble(uint32_t nib) { return (nib * 0x00204081u) & 0x01010101u; }
 
-__global__ __launch_bounds__(kCrcThreads, 2) void crc32_group_residue_kernel(
+// 16 bytes at byte offset `o` of a segment of `len` bytes, zero beyond the end (last group).
+__device__ __forceinline__ uint4 load_tail(const uint8_t* __restrict__ buf, int64_t base, int64_t o, int64_t len) {
+  uint32_t w[4];
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    uint32_t v = 0;
+#pragma unroll
+    for (int b = 0; b < 4; ++b) {
+      const int64_t i = o + 4 * q + b;
+      v |= (i < len ? static_cast<uint32_t>(buf[base + i]) : 0u) << (8 * b);
+    }
+    w[q] = v;
+  }
+  return make_uint4(w[0], w[1], w[2], w[3]);
+}
+
+__global__ __launch_bounds__(kCrcThreads) void crc32_group_residue_kernel(
     const uint8_t* __restrict__ buf, const int64_t* __restrict__ seg_off, const int64_t* __restrict__ seg_len,
     const int64_t* __restrict__ tile_prefix, const int64_t* __restrict__ res_off, const v4i* __restrict__ wfrag,
     uint32_t* __restrict__ residues, int nseg, int64_t total_tiles, int64_t tiles_per_wave) {
@@ -66,38 +84,30 @@ __global__ __launch_bounds__(kCrcThreads, 2) void crc32_group_residue_kernel(
     }
     const int64_t tile = t - tstart;
     const int64_t my = tile * kTileBytes + r * 256 + h * 128;  // byte offset of this lane's 128 B
-    uint32_t d[32];
-    if (my + 128 <= len) {
-      const uint4* p = reinterpret_cast<const uint4*>(buf + base + my);
-#pragma unroll
-      for (int q = 0; q < 8; ++q) {
-        const uint4 v = p[q];
-        d[4 * q] = v.x; d[4 * q + 1] = v.y; d[4 * q + 2] = v.z; d[4 * q + 3] = v.w;
-      }
-    } else {
-#pragma unroll
-      for (int q = 0; q < 32; ++q) {
-        uint32_t w = 0;
-#pragma unroll
-        for (int b = 0; b < 4; ++b) {
-          const int64_t o = my + 4 * q + b;
-          const uint32_t byte = o < len ? buf[base + o] : 0u;
-          w |= byte << (8 * b);
-        }
-        d[q] = w;
-      }
-    }
+    const bool full = my + 128 <= len;
+    const uint4* p = reinterpret_cast<const uint4*>(buf + base + my);
+    // 16-byte chunks streamed with one chunk of prefetch: 8 VGPRs of data live instead of
+    // 32, so the 64-step MFMA loop fits without spilling.
+    uint4 cur = full ? p[0] : load_tail(buf, base, my, len);
     v16i acc = {};
+#pragma unroll 1
+    for (int q = 0; q < 8; ++q) {
+      uint4 nxt = cur;
+      if (q < 7) nxt = full ? p[q + 1] : load_tail(buf, base, my + 16 * (q + 1), len);
+      const uint32_t w4[4] = {cur.x, cur.y, cur.z, cur.w};
 #pragma unroll
-    for (int s = 0; s < 64; ++s) {
-      const uint32_t bits = (d[s >> 1] >> (16 * (s & 1))) & 0xffffu;
-      v4i a;
-      a.x = static_cast<int>(expand_nibble(bits & 0xf));
-      a.y = static_cast<int>(expand_nibble((bits >> 4) & 0xf));
-      a.z = static_cast<int>(expand_nibble((bits >> 8) & 0xf));
-      a.w = static_cast<int>(expand_nibble(bits >> 12));
-      const v4i b = s_w[s * 64 + lane];
-      acc = __builtin_amdgcn_mfma_i32_32x32x32_i8(a, b, acc, 0, 0, 0);
+      for (int k = 0; k < 8; ++k) {
+        const int s = 8 * q + k;
+        const uint32_t bits = (w4[k >> 1] >> (16 * (k & 1))) & 0xffffu;
+        v4i a;
+        a.x = static_cast<int>(expand_nibble(bits & 0xf));
+        a.y = static_cast<int>(expand_nibble((bits >> 4) & 0xf));
+        a.z = static_cast<int>(expand_nibble((bits >> 8) & 0xf));
+        a.w = static_cast<int>(expand_nibble(bits >> 12));
+        const v4i b = s_w[s * 64 + lane];
+        acc = __builtin_amdgcn_mfma_i32_32x32x32_i8(a, b, acc, 0, 0, 0);
+      }
+      cur = nxt;
     }
     const int64_t groups = (len + 255) >> 8;
     const int64_t g0 = tile * 32;

@@ -236,6 +236,7 @@ __global__ __launch_bounds__(kTsThreads) void ts_gather_kernel(
     const int64_t* __restrict__ blk_prefix, int nseg, const uint32_t* __restrict__ meta,
     const int64_t* __restrict__ pts_dts, const int32_t* __restrict__ blk_sums, uint8_t* __restrict__ es,
     const int64_t* __restrict__ es_off, int64_t* __restrict__ pes, int64_t max_pes, int64_t* __restrict__ info) {
+  __shared__ uint32_t s_pk[kTsThreads * kPkt / 4 + 4];  // this block's 256 packets (47 KiB)
   __shared__ int64_t s_tot[2 * kClasses];     // segment totals
   __shared__ int64_t s_pre[2 * kClasses];     // prefix of blocks before this one
   __shared__ int32_t s_wave[4][2 * kClasses];  // per-wave totals
@@ -245,6 +246,15 @@ __global__ __launch_bounds__(kTsThreads) void ts_gather_kernel(
   const int64_t nblk = blk_prefix[seg + 1] - b0;
   const int64_t blk = gblk - b0;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  {  // stage the block's packets into LDS: fully coalesced 16-byte loads
+    const int64_t np = seg_length(seg_len, seg) / kPkt;
+    const int64_t first = blk * kTsThreads;
+    const int64_t npk = np - first < kTsThreads ? (np - first > 0 ? np - first : 0) : kTsThreads;
+    const int nvec = static_cast<int>((npk * kPkt + 15) / 16);
+    const uint4* g = reinterpret_cast<const uint4*>(buf + seg_off[seg] + first * kPkt);
+    uint4* l = reinterpret_cast<uint4*>(s_pk);
+    for (int i = tid; i < nvec; i += kTsThreads) l[i] = g[i];
+  }
   if (tid < 2 * kClasses) {
     s_tot[tid] = 0;
     s_pre[tid] = 0;
@@ -316,8 +326,9 @@ __global__ __launch_bounds__(kTsThreads) void ts_gather_kernel(
       }
     }
   }
-  // cooperative per-packet copy: the whole wave moves one packet payload at a time
-  const uint8_t* sbase = buf + seg_off[seg] + (blk * kTsThreads + wave * 64) * kPkt;
+  // cooperative per-packet copy out of the LDS-staged block: the whole wave moves one packet
+  // payload at a time with dword-aligned global stores (v_alignbyte funnel on LDS reads)
+  const uint8_t* s_bytes = reinterpret_cast<const uint8_t*>(s_pk);
   uint8_t* ebase = es + es_off[seg];
   uint64_t active = __ballot(c < 3 && len > 0);
   while (active) {
@@ -326,25 +337,22 @@ __global__ __launch_bounds__(kTsThreads) void ts_gather_kernel(
     const int jlen = __shfl(len, j);
     const int jps = __shfl(ps, j);
     const int64_t jdst = __shfl(dst_b, j);
-    const uint8_t* s = sbase + static_cast<int64_t>(j) * kPkt + jps;
+    const int s = (wave * 64 + j) * kPkt + jps;  // LDS byte offset of the payload
     uint8_t* d = ebase + jdst;
-    const int head = static_cast<int>((4 - (reinterpret_cast<uintptr_t>(d) & 3)) & 3) < jlen
-                         ? static_cast<int>((4 - (reinterpret_cast<uintptr_t>(d) & 3)) & 3)
-                         : jlen;
+    const int mis = static_cast<int>((4 - (reinterpret_cast<uintptr_t>(d) & 3)) & 3);
+    const int head = mis < jlen ? mis : jlen;
     const int body = (jlen - head) >> 2;
     const int tail = jlen - head - 4 * body;
-    if (lane < head) d[lane] = s[lane];
+    if (lane < head) d[lane] = s_bytes[s + lane];
     if (lane < body) {
-      const uint8_t* a = s + head + 4 * lane;
-      const uintptr_t ai = reinterpret_cast<uintptr_t>(a);
-      const uint32_t* al = reinterpret_cast<const uint32_t*>(ai & ~uintptr_t(3));
-      const uint32_t sh = static_cast<uint32_t>(ai & 3);
-      const uint32_t lo = al[0];
-      const uint32_t hi = sh ? al[1] : 0u;
+      const int a = s + head + 4 * lane;
+      const uint32_t sh = static_cast<uint32_t>(a & 3);
+      const uint32_t lo = s_pk[a >> 2];
+      const uint32_t hi = s_pk[(a >> 2) + 1];
       const uint32_t v = sh ? __builtin_amdgcn_alignbyte(hi, lo, sh) : lo;
       reinterpret_cast<uint32_t*>(d + head)[lane] = v;
     }
-    if (lane < tail) d[head + 4 * body + lane] = s[head + 4 * body + lane];
+    if (lane < tail) d[head + 4 * body + lane] = s_bytes[s + head + 4 * body + lane];
   }
   if (blk == 0 && tid == 0) {
     int64_t* inf = info + static_cast<int64_t>(seg) * kInfo;

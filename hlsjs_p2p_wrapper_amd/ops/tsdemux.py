@@ -82,8 +82,8 @@ def demux_batch(buf: torch.Tensor, offs: Sequence[int], lens: Union[Sequence[int
             bad = lens.numpy() < 0
             info[bad, 0] |= STATUS["bad_length"]
         return DemuxResult(torch.from_numpy(info), torch.from_numpy(pes), es, eo)
-    if np.any(o % 4):
-        raise ValueError("demux_batch: offsets must be 4-byte aligned on device")
+    if np.any(o % 16):
+        raise ValueError("demux_batch: offsets must be 16-byte aligned on device")
     blocks = ((cap + PACKET - 1) // PACKET + 255) // 256
     blk_prefix = np.zeros(B + 1, dtype=np.int64)
     np.cumsum(blocks, out=blk_prefix[1:])

@@ -14,6 +14,7 @@ get their own pipeline.
 from __future__ import annotations
 
 import threading
+import time
 from dataclasses import dataclass
 from typing import Any, Callable, Dict, List, Optional, Tuple
 
@@ -23,6 +24,7 @@ import torch
 from ..net.event_loop import get_event_loop
 from ..ops import aes as _aes
 from ..ops import tsdemux as _ts
+from ..utils.trace import PhaseTimer
 
 ALIGN = 256
 
@@ -59,26 +61,45 @@ class MediaPipeline:
         self.segments = 0
         self.bytes_in = 0
         self.batches = 0
+        self.timer = PhaseTimer()
+        # event-loop players flush at the end of the loop iteration; a throughput driver
+        # sets auto_flush=False and overlaps launch() / complete() of consecutive batches
+        self.auto_flush = True
 
     def submit(self, job: TransmuxJob) -> None:
         self._jobs.append(job)
-        if not self._scheduled:
+        if self.auto_flush and not self._scheduled:
             self._scheduled = True
             self.loop.call_soon(self.flush)
 
     def flush(self) -> None:
+        """Synchronous batch: launch the kernels for everything submitted, then complete."""
         self._scheduled = False
+        self.complete(self.launch())
+
+    def launch(self) -> Optional["_Batch"]:
+        """Enqueue decrypt + demux for every submitted job; the host does not wait."""
         jobs, self._jobs = self._jobs, []
         if not jobs:
-            return
+            return None
         try:
-            results = self._run(jobs)
+            return self._launch(jobs)
         except Exception as e:  # deliver the failure to every job of the batch
-            for j in jobs:
-                j.callback({"error": e})
+            return _Batch(jobs, error=e)
+
+    def complete(self, batch: Optional["_Batch"]) -> None:
+        """Wait for a launched batch and run the per-fragment callbacks."""
+        if batch is None:
             return
-        for j, r in zip(jobs, results):
+        if batch.error is not None:
+            for j in batch.jobs:
+                j.callback({"error": batch.error})
+            return
+        results = self._complete(batch)
+        t = time.perf_counter()
+        for j, r in zip(batch.jobs, results):
             j.callback(r)
+        self.timer.add("callbacks", time.perf_counter() - t)
 
     # ------------------------------------------------------------------ batch
     def _stage(self, tensors: List[torch.Tensor]) -> Tuple[torch.Tensor, List[int]]:
@@ -103,14 +124,18 @@ class MediaPipeline:
             buf[o:o + t.numel()].copy_(t, non_blocking=True)
         return buf, offs
 
-    def _run(self, jobs: List[TransmuxJob]) -> List[Dict[str, Any]]:
+    def _launch(self, jobs: List[TransmuxJob]) -> "_Batch":
         dev = self.device
         tensors = [_as_tensor(j.payload) for j in jobs]
         sizes = [t.numel() for t in tensors]
         self.segments += len(jobs)
         self.bytes_in += sum(sizes)
         self.batches += 1
+        tm = self.timer
+        t0 = time.perf_counter()
         src, src_offs = self._stage(tensors)
+        t1 = time.perf_counter()
+        tm.add("stage", t1 - t0)
         enc = [i for i, j in enumerate(jobs) if j.key is not None]
         clear = [i for i, j in enumerate(jobs) if j.key is None]
         results: List[Optional[Dict[str, Any]]] = [None] * len(jobs)
@@ -132,6 +157,8 @@ class MediaPipeline:
         if clear:
             groups.append((clear, src, [src_offs[i] for i in clear], [sizes[i] for i in clear],
                            [sizes[i] for i in clear]))
+        t2 = time.perf_counter()
+        tm.add("decrypt_launch", t2 - t1)
         infos = []
         for idx, buf, offs, lens, caps in groups:
             es_offs, pos = [], 0
@@ -141,14 +168,44 @@ class MediaPipeline:
             es = torch.empty(pos + ALIGN, dtype=torch.uint8, device=dev)
             res = _ts.demux_batch(buf, offs, lens, es, es_offs, caps=caps)
             infos.append((idx, res, es_offs, lens))
-        # one D2H copy of all info rows (the only sync of the stage)
-        host_infos = [r.info.cpu().numpy() for _, r, _, _ in infos] if dev.type != "cpu" else \
-            [r.info.numpy() for _, r, _, _ in infos]
-        for (idx, res, es_offs, lens), hinfo in zip(infos, host_infos):
-            plain_lens = lens.cpu().numpy() if isinstance(lens, torch.Tensor) else np.asarray(lens)
+        # async D2H of the small per-segment info rows (+ plaintext lengths) into pinned
+        # host memory, then one event: completing the batch is the stage's only sync
+        host = []
+        for _, r, _, lens in infos:
+            if dev.type == "cpu":
+                host.append((r.info.numpy(), lens.numpy() if isinstance(lens, torch.Tensor) else np.asarray(lens)))
+                continue
+            hi = torch.empty(r.info.shape, dtype=torch.int64, pin_memory=True)
+            hi.copy_(r.info, non_blocking=True)
+            if isinstance(lens, torch.Tensor):
+                hl = torch.empty(lens.shape, dtype=torch.int64, pin_memory=True)
+                hl.copy_(lens, non_blocking=True)
+            else:
+                hl = np.asarray(lens)
+            host.append((hi, hl))
+        ev = None
+        if dev.type != "cpu":
+            ev = torch.cuda.Event()
+            ev.record()
+        tm.add("demux_launch", time.perf_counter() - t2)
+        return _Batch(jobs, infos=infos, host=host, event=ev, results=results)
+
+    def _complete(self, b: "_Batch") -> List[Dict[str, Any]]:
+        tm = self.timer
+        t3 = time.perf_counter()
+        if b.event is not None:
+            b.event.synchronize()
+        t4 = time.perf_counter()
+        tm.add("wait_device", t4 - t3)
+        results = b.results
+        keys = list(_ts.INFO.keys())
+        slots = list(_ts.INFO.values())
+        for (idx, res, es_offs, lens), (hinfo, hlens) in zip(b.infos, b.host):
+            hinfo = hinfo.numpy() if isinstance(hinfo, torch.Tensor) else hinfo
+            plain_lens = hlens.numpy() if isinstance(hlens, torch.Tensor) else hlens
+            rows = hinfo[:, slots].tolist()
             for k, i in enumerate(idx):
-                row = hinfo[k]
-                info = {name: int(row[slot]) for name, slot in _ts.INFO.items()}
+                info = dict(zip(keys, rows[k]))
                 base = es_offs[k]
                 vb, ab, ib = info["video_bytes"], info["audio_bytes"], info["id3_bytes"]
                 r = {
@@ -164,7 +221,18 @@ class MediaPipeline:
                 if plain_lens[k] < 0:
                     r["error"] = ValueError("decryption failed (bad PKCS#7 padding)")
                 results[i] = r
+        tm.add("results", time.perf_counter() - t4)
         return results  # type: ignore[return-value]
+
+
+@dataclass(eq=False)
+class _Batch:
+    jobs: List[TransmuxJob]
+    infos: Any = None
+    host: Any = None
+    event: Any = None
+    results: Any = None
+    error: Optional[BaseException] = None
 
 
 _local = threading.local()
