@@ -31,12 +31,20 @@ import time
 import numpy as np
 import torch
 
+_PROF = None
+if os.environ.get("HLSP2P_PROFILE_LOADS"):  # cProfile the player's load-issue phase only
+    import cProfile
+
+    _PROF = cProfile.Profile()
+
 CONFIGS = {
     # name: (renditions preset, encrypted, segment seconds, description)
     "1080p6m": ("1080p", True, 4.0, "1080p 6 Mb/s HLS live (AES-128, 4 s TS segments, 8 peers)"),
     "1080p6m-clear": ("1080p", False, 4.0, "1080p 6 Mb/s HLS (clear, 4 s TS segments)"),
     "abr5": ("abr5", True, 4.0, "5-rendition ABR ladder (AES-128, 4 s TS)"),
     "4k25m": ("4k", True, 4.0, "4K 25 Mb/s HLS (AES-128, 4 s TS segments)"),
+    # diagnostic only: ~30 KB segments, so per-segment host (Python) cost dominates
+    "hostcost": ("tiny", True, 4.0, "60 kb/s HLS (AES-128) - host-overhead probe"),
 }
 
 
@@ -77,12 +85,14 @@ def main() -> int:
     from hlsjs_p2p_wrapper_amd import Hls
     from hlsjs_p2p_wrapper_amd.agent import node_for_config
     from hlsjs_p2p_wrapper_amd.net import new_event_loop
-    from hlsjs_p2p_wrapper_amd.net.origin import PRESET_1080P_6M, PRESET_4K_25M, PRESET_ABR5, SyntheticHlsOrigin
+    from hlsjs_p2p_wrapper_amd.net.origin import (PRESET_1080P_6M, PRESET_4K_25M, PRESET_ABR5, Rendition,
+                                                SyntheticHlsOrigin)
     from hlsjs_p2p_wrapper_amd.player import MediaElement
     from hlsjs_p2p_wrapper_amd.player.transmux import pipeline_for
 
     preset, encrypted, seg_dur, desc = CONFIGS[args.config]
-    rends = {"1080p": PRESET_1080P_6M, "4k": PRESET_4K_25M, "abr5": PRESET_ABR5}[preset]
+    rends = {"1080p": PRESET_1080P_6M, "4k": PRESET_4K_25M, "abr5": PRESET_ABR5,
+             "tiny": [Rendition(60_000, 320, 180, name="180p")]}[preset]
     K = args.inflight
     total_steps = args.warmup + args.steps
     n_segments = (total_steps + 4) * K
@@ -161,9 +171,15 @@ def main() -> int:
             b = pipe.launch()
             pipe.complete(state["b"])
             drain_ready()
+            t25 = time.perf_counter()
+            if _PROF is not None:
+                _PROF.enable()
             sc.tick()
             drain_ready()
+            if _PROF is not None:
+                _PROF.disable()
             state["h"], state["b"] = h, b
+            bt.add("d_player_loads", time.perf_counter() - t25)
         t3 = time.perf_counter()
         bt.add("a_launch_or_tick", t1 - t0)
         bt.add("b_node", t2 - t1)
@@ -227,6 +243,8 @@ def main() -> int:
               f"#   step ms {bt.summary_ms(args.steps)}\n"
               f"#   node ms {node.timer.summary_ms(args.steps)}\n"
               f"#   transmux ms {pipe.timer.summary_ms(args.steps)}", file=sys.stderr)
+    if _PROF is not None:
+        _PROF.dump_stats(os.environ["HLSP2P_PROFILE_LOADS"] + f".{rank}")
     if rank == 0:
         print(json.dumps(result), flush=True)
     if world > 1:

@@ -46,7 +46,9 @@ def _device_tables(device: torch.device):
     t = _tables.get(k)
     if t is None:
         td0, inv, _, _ = _rt().aes_tables()
-        t = (torch.from_numpy(td0.view(np.int32).copy()).to(device), torch.from_numpy(inv.copy()).to(device))
+        # the kernel works on little-endian column words: TdL = bswap(Td0)
+        tdl = td0.astype(np.uint32).byteswap()
+        t = (torch.from_numpy(tdl.view(np.int32).copy()).to(device), torch.from_numpy(inv.copy()).to(device))
         with _lock:
             _tables[k] = t
     return t
@@ -78,7 +80,9 @@ def cbc_decrypt_batch(src: torch.Tensor, src_offs: Sequence[int], nbytes: Sequen
     np.cumsum(nb // 16, out=blk_prefix[1:])
     pair_prefix = np.zeros(B + 1, dtype=np.int64)  # work unit: 2 blocks of one segment
     np.cumsum((nb // 16 + 1) // 2, out=pair_prefix[1:])
-    d = pack_to_device({"so": so, "do": do, "bp": blk_prefix, "pp": pair_prefix, "drk": drk, "iv": iv}, src.device)
+    drk_le = drk.byteswap()  # state words are used as loaded (little-endian) on device
+    d = pack_to_device({"so": so, "do": do, "bp": blk_prefix, "pp": pair_prefix, "drk": drk_le, "iv": iv},
+                       src.device)
     out_len = torch.empty(B, dtype=torch.int64, device=src.device)
     td0, isb = _device_tables(src.device)
     _dev().aes128_cbc_decrypt(src, dst, d["so"], d["do"], d["bp"], d["pp"], d["drk"], d["iv"], td0, isb, out_len,

@@ -2,19 +2,24 @@
 //
 // CBC *decryption* is block-parallel: P_i = D_K(C_i) xor C_{i-1}.  Work unit = a PAIR of
 // consecutive 16-byte blocks of one segment: each lane runs two independent AES chains
-// interleaved (ILP hides the LDS latency of each round's 16 dependent table lookups) and
-// moves 32 contiguous bytes, so a wave streams 2 KiB with dwordx4 loads/stores
-// (C_{i-1} for the pair's first block is an L1 hit: the neighbour lane loaded it).
+// interleaved (ILP hides the LDS latency of a round's dependent lookups) and moves 32
+// contiguous bytes; C_{i-1} for the pair's first block is an L1 hit (neighbour lane).
 //
-// AES is table bound, not matmul shaped (no MFMA).  Random 32-bit lookups from 32 lanes
-// into a 1 KiB table hit the 32 ds_read_b32 banks with 3-4-way conflicts, so the Td0
-// table (9 rounds x 16 lookups) is REPLICATED 32x: entry e of copy c at word e*32 + c, lane
-// l reads copy (l & 31) -> every lane of a 32-lane half owns a bank, conflict-free.
-// Td1..Td3 are byte rotations of Td0 (v_alignbit).  The final-round inverse S-box (16 of
-// 160 lookups) is replicated 8x only (<= 4-way conflicts on 10% of the lookups), which
-// keeps the LDS footprint at 40 KiB -> 4 workgroups (16 waves) per CU.
+// AES is table bound, not matmul shaped (no MFMA).  Design for the CDNA4 LDS + VALU:
+//  * Tables in LITTLE-ENDIAN column form (TdL = bswap(Td0), round keys pre-swapped on the
+//    host), so state words are used exactly as loaded — no byte swaps in the kernel.
+//  * One 64 KiB LDS image of 256 rows x 256 B: row x = [32 lane copies of TdL[x] | 32 lane
+//    copies of InvSbox[x]].  Lane l reads word l (Td) or word 32+l (S-box) of the row, so
+//    for ds_read_b32 (bank = dword % 32) every lane of a 32-lane half owns a bank: both the
+//    144 Td lookups and the 16 final-round S-box lookups per block are conflict-free.
+//  * With 256-byte rows the LDS byte address of entry x for lane l is  (x << 8) | (l << 2)
+//    [| 128 for the S-box] — ONE v_perm_b32 builds it from the state word (selects byte k
+//    into bits 8..15, the lane offset into bits 0..7), instead of extract + shift-or.
+//    Per round: 16 v_perm + 16 ds_read_b32 + 12 v_alignbit (Td1..Td3 are rotations of Td0)
+//    + 16 v_xor.
+//  * 512-thread workgroups (8 waves) share the 64 KiB image: 2 per CU = 4 waves per SIMD.
 //
-// Persistent grid (4 workgroups per CU), each streaming one contiguous range of the batch's
+// Persistent grid (2 workgroups per CU), each streaming one contiguous range of the batch's
 // pair index space; the segment table is walked monotonically so per-segment state (44
 // round keys, IV, offsets) reloads only at boundaries.  PKCS#7: the lane holding a
 // segment's last block validates the padding and writes the plaintext length (or -1) to
@@ -24,33 +29,28 @@
 namespace hlsp2p {
 namespace dev {
 
-constexpr int kAesThreads = 256;
-constexpr int kAesWgPerCu = 4;
-constexpr int kRepTd = 32;
-constexpr int kRepIs = 8;
+constexpr int kAesThreads = 512;
+constexpr int kAesWgPerCu = 2;
 
-#define TD(x) s_td[((x) << 5) | l32]
-#define IS(x) s_is[((x) << 3) | l8]
+// v_perm_b32 selectors: byte k of the state word -> bits 8..15, lane offset byte -> 0..7
+#define SEL(k) (0x0c0c0000u | ((4u + (k)) << 8))
+#define LDS32(addr) (*reinterpret_cast<const uint32_t*>(s_bytes + (addr)))
+#define TD(w, k) LDS32(__builtin_amdgcn_perm((w), td_base, SEL(k)))
+#define IS(w, k) LDS32(__builtin_amdgcn_perm((w), is_base, SEL(k)))
+#define ROTL(x, s) __builtin_amdgcn_alignbit((x), (x), 32 - (s))
 
-#define AES_ROUND(s0, s1, s2, s3, t0, t1, t2, t3, k)                                                          \
-  t0 = TD(s0 >> 24) ^ rotr(TD((s3 >> 16) & 0xff), 8) ^ rotr(TD((s2 >> 8) & 0xff), 16) ^ rotr(TD(s1 & 0xff), 24) ^ \
-       (k)[0];                                                                                                 \
-  t1 = TD(s1 >> 24) ^ rotr(TD((s0 >> 16) & 0xff), 8) ^ rotr(TD((s3 >> 8) & 0xff), 16) ^ rotr(TD(s2 & 0xff), 24) ^ \
-       (k)[1];                                                                                                 \
-  t2 = TD(s2 >> 24) ^ rotr(TD((s1 >> 16) & 0xff), 8) ^ rotr(TD((s0 >> 8) & 0xff), 16) ^ rotr(TD(s3 & 0xff), 24) ^ \
-       (k)[2];                                                                                                 \
-  t3 = TD(s3 >> 24) ^ rotr(TD((s2 >> 16) & 0xff), 8) ^ rotr(TD((s1 >> 8) & 0xff), 16) ^ rotr(TD(s0 & 0xff), 24) ^ \
-       (k)[3];
+// little-endian column form of the equivalent inverse cipher round
+#define AES_ROUND(s0, s1, s2, s3, t0, t1, t2, t3, k)                                            \
+  t0 = TD(s0, 0) ^ ROTL(TD(s3, 1), 8) ^ ROTL(TD(s2, 2), 16) ^ ROTL(TD(s1, 3), 24) ^ (k)[0];     \
+  t1 = TD(s1, 0) ^ ROTL(TD(s0, 1), 8) ^ ROTL(TD(s3, 2), 16) ^ ROTL(TD(s2, 3), 24) ^ (k)[1];     \
+  t2 = TD(s2, 0) ^ ROTL(TD(s1, 1), 8) ^ ROTL(TD(s0, 2), 16) ^ ROTL(TD(s3, 3), 24) ^ (k)[2];     \
+  t3 = TD(s3, 0) ^ ROTL(TD(s2, 1), 8) ^ ROTL(TD(s1, 2), 16) ^ ROTL(TD(s0, 3), 24) ^ (k)[3];
 
-#define AES_FINAL(s0, s1, s2, s3, o0, o1, o2, o3, k)                                                        \
-  o0 = ((IS(s0 >> 24) << 24) | (IS((s3 >> 16) & 0xff) << 16) | (IS((s2 >> 8) & 0xff) << 8) | IS(s1 & 0xff)) ^ \
-       (k)[0];                                                                                               \
-  o1 = ((IS(s1 >> 24) << 24) | (IS((s0 >> 16) & 0xff) << 16) | (IS((s3 >> 8) & 0xff) << 8) | IS(s2 & 0xff)) ^ \
-       (k)[1];                                                                                               \
-  o2 = ((IS(s2 >> 24) << 24) | (IS((s1 >> 16) & 0xff) << 16) | (IS((s0 >> 8) & 0xff) << 8) | IS(s3 & 0xff)) ^ \
-       (k)[2];                                                                                               \
-  o3 = ((IS(s3 >> 24) << 24) | (IS((s2 >> 16) & 0xff) << 16) | (IS((s1 >> 8) & 0xff) << 8) | IS(s0 & 0xff)) ^ \
-       (k)[3];
+#define AES_FINAL(s0, s1, s2, s3, o0, o1, o2, o3, k)                                               \
+  o0 = (IS(s0, 0) | (IS(s3, 1) << 8) | (IS(s2, 2) << 16) | (IS(s1, 3) << 24)) ^ (k)[0];           \
+  o1 = (IS(s1, 0) | (IS(s0, 1) << 8) | (IS(s3, 2) << 16) | (IS(s2, 3) << 24)) ^ (k)[1];           \
+  o2 = (IS(s2, 0) | (IS(s1, 1) << 8) | (IS(s0, 2) << 16) | (IS(s3, 3) << 24)) ^ (k)[2];           \
+  o3 = (IS(s3, 0) | (IS(s2, 1) << 8) | (IS(s1, 2) << 16) | (IS(s0, 3) << 24)) ^ (k)[3];
 
 __device__ __forceinline__ int64_t pkcs7_len(uint4 p, int64_t nbytes) {
   const uint32_t pad = p.w >> 24;
@@ -65,19 +65,25 @@ __device__ __forceinline__ int64_t pkcs7_len(uint4 p, int64_t nbytes) {
   return ok ? nbytes - static_cast<int64_t>(pad) : -1;
 }
 
-__global__ __launch_bounds__(kAesThreads, kAesWgPerCu) void aes128_cbc_decrypt_kernel(
+// tdl: little-endian Td0 (256 words); isb: inverse S-box (256 bytes)
+// drk: per-segment little-endian equivalent-inverse-cipher round keys (44 words)
+__global__ __launch_bounds__(kAesThreads, 1) void aes128_cbc_decrypt_kernel(
     const uint8_t* __restrict__ src, uint8_t* __restrict__ dst, const int64_t* __restrict__ src_off,
     const int64_t* __restrict__ dst_off, const int64_t* __restrict__ blk_prefix,
     const int64_t* __restrict__ pair_prefix, const uint32_t* __restrict__ drk, const uint32_t* __restrict__ ivw,
-    const uint32_t* __restrict__ td0_g, const uint8_t* __restrict__ isb_g, int64_t* __restrict__ out_len, int nseg,
+    const uint32_t* __restrict__ tdl_g, const uint8_t* __restrict__ isb_g, int64_t* __restrict__ out_len, int nseg,
     int64_t total_pairs, int64_t per_wg) {
-  __shared__ uint32_t s_td[256 * kRepTd];
-  __shared__ uint32_t s_is[256 * kRepIs];
+  __shared__ uint32_t s_tab[256 * 64];  // 64 KiB: [row x][32 TdL copies | 32 InvSbox copies]
   const int tid = threadIdx.x;
-  const uint32_t l32 = tid & 31, l8 = tid & 7;
-  for (int i = tid; i < 256 * kRepTd; i += kAesThreads) s_td[i] = td0_g[i >> 5];
-  for (int i = tid; i < 256 * kRepIs; i += kAesThreads) s_is[i] = isb_g[i >> 3];
+  for (int i = tid; i < 256 * 64; i += kAesThreads) {
+    const int row = i >> 6, col = i & 63;
+    s_tab[i] = col < 32 ? tdl_g[row] : static_cast<uint32_t>(isb_g[row]);
+  }
   __syncthreads();
+  const uint8_t* s_bytes = reinterpret_cast<const uint8_t*>(s_tab);
+  const uint32_t l32 = tid & 31;
+  const uint32_t td_base = l32 << 2;          // byte offset of this lane's Td copy in a row
+  const uint32_t is_base = 128u | (l32 << 2);  // ... and of its S-box copy
 
   const int64_t begin = static_cast<int64_t>(blockIdx.x) * per_wg;
   const int64_t end = begin + per_wg < total_pairs ? begin + per_wg : total_pairs;
@@ -108,10 +114,8 @@ __global__ __launch_bounds__(kAesThreads, kAesWgPerCu) void aes128_cbc_decrypt_k
     } else {
       pv = cp[-1];
     }
-    uint32_t a0 = bswap32(c0.x) ^ rk[0], a1 = bswap32(c0.y) ^ rk[1], a2 = bswap32(c0.z) ^ rk[2],
-             a3 = bswap32(c0.w) ^ rk[3];
-    uint32_t b0 = bswap32(c1.x) ^ rk[0], b1 = bswap32(c1.y) ^ rk[1], b2 = bswap32(c1.z) ^ rk[2],
-             b3 = bswap32(c1.w) ^ rk[3];
+    uint32_t a0 = c0.x ^ rk[0], a1 = c0.y ^ rk[1], a2 = c0.z ^ rk[2], a3 = c0.w ^ rk[3];
+    uint32_t b0 = c1.x ^ rk[0], b1 = c1.y ^ rk[1], b2 = c1.z ^ rk[2], b3 = c1.w ^ rk[3];
 #pragma unroll
     for (int r = 1; r < 10; ++r) {
       uint32_t t0, t1, t2, t3, u0, u1, u2, u3;
@@ -123,9 +127,8 @@ __global__ __launch_bounds__(kAesThreads, kAesWgPerCu) void aes128_cbc_decrypt_k
     uint32_t o0, o1, o2, o3, q0, q1, q2, q3;
     AES_FINAL(a0, a1, a2, a3, o0, o1, o2, o3, rk + 40)
     AES_FINAL(b0, b1, b2, b3, q0, q1, q2, q3, rk + 40)
-    uint4 p0, p1;
-    p0.x = bswap32(o0) ^ pv.x; p0.y = bswap32(o1) ^ pv.y; p0.z = bswap32(o2) ^ pv.z; p0.w = bswap32(o3) ^ pv.w;
-    p1.x = bswap32(q0) ^ c0.x; p1.y = bswap32(q1) ^ c0.y; p1.z = bswap32(q2) ^ c0.z; p1.w = bswap32(q3) ^ c0.w;
+    const uint4 p0 = make_uint4(o0 ^ pv.x, o1 ^ pv.y, o2 ^ pv.z, o3 ^ pv.w);
+    const uint4 p1 = make_uint4(q0 ^ c0.x, q1 ^ c0.y, q2 ^ c0.z, q3 ^ c0.w);
     uint4* dp = reinterpret_cast<uint4*>(dst + dof) + i0;
     dp[0] = p0;
     if (has2) dp[1] = p1;
@@ -135,10 +138,13 @@ __global__ __launch_bounds__(kAesThreads, kAesWgPerCu) void aes128_cbc_decrypt_k
 }
 #undef TD
 #undef IS
+#undef LDS32
+#undef SEL
+#undef ROTL
 
 hipError_t launch_aes128_cbc_decrypt(const uint8_t* src, uint8_t* dst, const int64_t* src_off, const int64_t* dst_off,
                                      const int64_t* blk_prefix, const int64_t* pair_prefix, const uint32_t* drk,
-                                     const uint32_t* ivw, const uint32_t* td0, const uint8_t* isb, int64_t* out_len,
+                                     const uint32_t* ivw, const uint32_t* tdl, const uint8_t* isb, int64_t* out_len,
                                      int nseg, int64_t total_pairs, int num_cu, hipStream_t stream) {
   if (total_pairs <= 0) return hipSuccess;
   const int64_t max_wg = static_cast<int64_t>(num_cu) * kAesWgPerCu;
@@ -149,7 +155,7 @@ hipError_t launch_aes128_cbc_decrypt(const uint8_t* src, uint8_t* dst, const int
   per_wg = (per_wg + kAesThreads - 1) / kAesThreads * kAesThreads;
   grid = (total_pairs + per_wg - 1) / per_wg;
   hipLaunchKernelGGL(aes128_cbc_decrypt_kernel, dim3(static_cast<unsigned>(grid)), dim3(kAesThreads), 0, stream, src,
-                     dst, src_off, dst_off, blk_prefix, pair_prefix, drk, ivw, td0, isb, out_len, nseg, total_pairs,
+                     dst, src_off, dst_off, blk_prefix, pair_prefix, drk, ivw, tdl, isb, out_len, nseg, total_pairs,
                      per_wg);
   return hipGetLastError();
 }

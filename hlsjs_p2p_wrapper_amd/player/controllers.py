@@ -384,6 +384,7 @@ class StreamController:
         self.startPosition = -1.0
         self._start_pending = False
         self._timer = None
+        self._tick_pending = False
         self._retry: Dict[Tuple[int, int], int] = {}
         self._retry_until = 0.0
         self._eos = False
@@ -423,8 +424,16 @@ class StreamController:
         self.state = self.STOPPED
 
     def _kick(self) -> None:
-        if self.state not in (self.STOPPED, self.ERROR):
-            self.loop.call_soon(self.tick)
+        # hls.js's tick() is re-entrant and cheap per call; here one pending tick per loop
+        # iteration serves every state change of that iteration (a swarm round completes
+        # dozens of fragments at once)
+        if self.state not in (self.STOPPED, self.ERROR) and not self._tick_pending:
+            self._tick_pending = True
+            self.loop.call_soon(self._kicked_tick)
+
+    def _kicked_tick(self) -> None:
+        self._tick_pending = False
+        self.tick()
 
     def onMediaAttached(self, event: str, data: Any) -> None:
         media = data["media"]

@@ -1,0 +1,70 @@
+"""Multi-process swarm over torch.distributed (gloo here; the same DistComm runs RCCL on
+MI355X): control plane all-gather + batch_isend_irecv data plane, world_size 2."""
+import os
+import socket
+
+import pytest
+import torch.multiprocessing as mp
+
+
+def _free_port() -> int:
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _peer(rank: int, world: int, port: int, q) -> None:
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world))
+    import torch.distributed as dist
+
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from hlsjs_p2p_wrapper_amd import Hls
+        from hlsjs_p2p_wrapper_amd.agent import node_for_config
+        from hlsjs_p2p_wrapper_amd.api.wrapper import HlsjsP2PWrapper
+        from hlsjs_p2p_wrapper_amd.net import new_event_loop
+        from hlsjs_p2p_wrapper_amd.net.origin import Rendition, SyntheticHlsOrigin
+        from hlsjs_p2p_wrapper_amd.player import MediaElement
+        from hlsjs_p2p_wrapper_amd.player.hls import Hls as Engine
+
+        loop = new_event_loop("virtual")
+        origin = SyntheticHlsOrigin("http://cdn.dist/vod/", renditions=[Rendition(1_000_000, 640, 360)],
+                                    num_segments=8, encrypted=True, pin_memory=False)
+        cfg = {"gpuSwarm": {"backend": "dist", "device": "cpu", "cacheBytes": 64 << 20, "roundIntervalMs": 20}}
+        node = node_for_config(cfg)
+        w = HlsjsP2PWrapper(Engine)
+        hls = w.createPlayer({}, cfg)
+        media = MediaElement()
+        hls.loadSource(origin.master_url())
+        hls.attachMedia(media)
+        hls.on(Hls.Events.MANIFEST_PARSED, lambda e, d: media.play())
+        ok = loop.run_until(lambda: media.currentTime > 30.0, timeout_ms=300_000)
+        stats = dict(w.stats)
+        node.close()
+        q.put((rank, ok, stats, sum(origin.pools[0].lengths), node.swarm_offload_ratio()))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_two_process_gloo_swarm():
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_peer, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    out = {}
+    for _ in range(2):
+        rank, ok, stats, total, offload = q.get(timeout=300)
+        out[rank] = (ok, stats, total, offload)
+    for p in procs:
+        p.join(60)
+        assert p.exitcode == 0
+    assert all(v[0] for v in out.values())
+    total = out[0][2]
+    assert out[0][1]["cdn"] + out[1][1]["cdn"] == total
+    assert out[0][1]["p2p"] + out[1][1]["p2p"] == total
+    assert out[0][1]["peers"] == 1
+    assert out[0][3] == pytest.approx(0.5)
