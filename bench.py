@@ -32,7 +32,7 @@ import numpy as np
 import torch
 
 _PROF = None
-if os.environ.get("HLSP2P_PROFILE_LOADS"):  # cProfile the player's load-issue phase only
+if os.environ.get("HLSP2P_PROFILE"):  # cProfile the timed steps (host-overhead analysis)
     import cProfile
 
     _PROF = cProfile.Profile()
@@ -172,12 +172,8 @@ def main() -> int:
             pipe.complete(state["b"])
             drain_ready()
             t25 = time.perf_counter()
-            if _PROF is not None:
-                _PROF.enable()
             sc.tick()
             drain_ready()
-            if _PROF is not None:
-                _PROF.disable()
             state["h"], state["b"] = h, b
             bt.add("d_player_loads", time.perf_counter() - t25)
         t3 = time.perf_counter()
@@ -201,9 +197,13 @@ def main() -> int:
     pipe.timer.reset()
     b0, s0 = counters["buffered"], dict(node.stats)
     t0 = time.perf_counter()
+    if _PROF is not None:
+        _PROF.enable()
     for _ in range(args.steps):
         step()
     sync()
+    if _PROF is not None:
+        _PROF.disable()
     elapsed = time.perf_counter() - t0
     done = counters["buffered"] - b0
     d_cdn = node.stats["cdn"] - s0["cdn"]
@@ -244,7 +244,15 @@ def main() -> int:
               f"#   node ms {node.timer.summary_ms(args.steps)}\n"
               f"#   transmux ms {pipe.timer.summary_ms(args.steps)}", file=sys.stderr)
     if _PROF is not None:
-        _PROF.dump_stats(os.environ["HLSP2P_PROFILE_LOADS"] + f".{rank}")
+        import io
+        import pstats
+
+        out = io.StringIO()
+        st = pstats.Stats(_PROF, stream=out)
+        st.sort_stats("tottime").print_stats(45)
+        st.sort_stats("cumtime").print_stats(60)
+        with open(os.environ["HLSP2P_PROFILE"] + f".{rank}.txt", "w") as f:
+            f.write(out.getvalue())
     if rank == 0:
         print(json.dumps(result), flush=True)
     if world > 1:

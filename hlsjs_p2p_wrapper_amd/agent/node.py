@@ -115,6 +115,7 @@ class RoundHandle:
     send_pins: Optional[np.ndarray] = None
     sent_bytes: int = 0
     ev_cdn: Any = None
+    dmas: int = 0
     ev_p2p: Any = None
     cdn_ms: float = 0.0
     p2p_ms: float = 0.0
@@ -467,7 +468,7 @@ class SwarmNode:
         self.timer.add("dev_cdn_ms", h.cdn_ms / 1e3)
         self.timer.add("dev_p2p_ms", h.p2p_ms / 1e3)
         self.last_round = {"wants": h.n_wants, "cdn": len(h.cdn_entries), "send": h.n_send,
-                           "recv": len(h.recv_entries), "cdn_ms": h.cdn_ms, "p2p_ms": h.p2p_ms,
+                           "recv": len(h.recv_entries), "cdn_ms": h.cdn_ms, "dmas": h.dmas, "p2p_ms": h.p2p_ms,
                            "ms": (time.perf_counter() - h.t0) * 1e3}
         if any(w.round < 0 for w in self._wants.values()):
             self._schedule()
@@ -509,7 +510,7 @@ class SwarmNode:
             start = torch.cuda.Event(enable_timing=True)
             end = torch.cuda.Event(enable_timing=True)
             start.record()
-            _h2d_batch(self.arena, offs, sources)
+            h.dmas = _h2d_batch(self.arena, offs, sources)
             end.record()
             h.ev_cdn = (start, end)
         else:
@@ -686,16 +687,26 @@ class SwarmNode:
 
 
 def _h2d_batch(arena: torch.Tensor, dst_offs: np.ndarray, sources: List[Tuple[torch.Tensor, int, int, bool]]) -> None:
-    """Enqueue one pinned-host -> HBM copy per segment on the current stream, in a single
-    native call (``hipMemcpyAsync`` loop) instead of one Python/ATen dispatch per segment."""
+    """Enqueue the pinned-host -> HBM copies of a round on the current stream in a single
+    native call; copies contiguous in both the origin pool and the arena are merged into
+    one DMA (see ``h2d_batch`` in ``kernels/bindings.cpp``)."""
     from ..ops._native import device as _dev
 
-    src_ptrs = np.asarray([d.data_ptr() + o for d, o, _, _ in sources], dtype=np.int64)
-    lens = np.asarray([n for _, _, n, _ in sources], dtype=np.int64)
+    bases = []
     for d, _, _, _ in sources:
-        if not d.is_pinned():
-            raise RuntimeError("CDN origin buffers must be pinned host memory for the async H2D path")
-    _dev().h2d_batch(arena, np.ascontiguousarray(dst_offs, dtype=np.int64), src_ptrs, lens)
+        p = d.data_ptr()
+        if p not in _PINNED_OK:
+            if not d.is_pinned():
+                raise RuntimeError("CDN origin buffers must be pinned host memory for the async H2D path")
+            _PINNED_OK.add(p)
+        bases.append(p)
+    src_alloc = np.asarray(bases, dtype=np.int64)
+    src_ptrs = src_alloc + np.asarray([o for _, o, _, _ in sources], dtype=np.int64)
+    lens = np.asarray([n for _, _, n, _ in sources], dtype=np.int64)
+    return _dev().h2d_batch(arena, np.ascontiguousarray(dst_offs, dtype=np.int64), src_ptrs, lens, src_alloc, ALIGN)
+
+
+_PINNED_OK: set = set()  # base pointers of origin tensors already checked to be pinned
 
 
 # ---------------------------------------------------------------------- registry

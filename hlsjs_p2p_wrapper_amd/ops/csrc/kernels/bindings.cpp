@@ -208,26 +208,48 @@ void segment_copy(Tensor src, Tensor dst, Tensor src_off, Tensor dst_off, Tensor
 
 int64_t device_cus(Tensor t) { return num_cus(t); }
 
-// CDN ingest: one hipMemcpyAsync per segment (pinned host -> HBM arena) on the current
-// stream — issued in one native call so a round's copies cost microseconds of host time.
-void h2d_batch(Tensor dst, pybind11::array_t<int64_t> dst_off, pybind11::array_t<int64_t> src_ptr,
-               pybind11::array_t<int64_t> len) {
+// CDN ingest: pinned host -> HBM arena on the current stream, issued in one native call.
+// Copies whose source (same pinned allocation, src_alloc[i]) and destination advance by the
+// same delta, with a gap below max_gap, are merged into one DMA: a round's segments sit
+// back to back in both the origin pool and the arena run (same 256-B alignment), and one
+// 192 MB copy moves at ~57 GB/s where 64 x 3 MB copies reach ~48 GB/s on MI355X.
+// A gap below the arena alignment is the previous entry's own padding (entries start on
+// aligned offsets), so a merged copy never touches another entry.  Returns #DMAs issued.
+int64_t h2d_batch(Tensor dst, pybind11::array_t<int64_t> dst_off, pybind11::array_t<int64_t> src_ptr,
+                  pybind11::array_t<int64_t> len, pybind11::array_t<int64_t> src_alloc, int64_t max_gap) {
   check(dst, "dst", torch::kUInt8);
   const int64_t n = dst_off.size();
-  TORCH_CHECK(src_ptr.size() == n && len.size() == n, "h2d_batch: argument sizes differ");
+  TORCH_CHECK(src_ptr.size() == n && len.size() == n && src_alloc.size() == n, "h2d_batch: argument sizes differ");
   const int64_t* o = dst_off.data();
   const int64_t* s = src_ptr.data();
   const int64_t* l = len.data();
+  const int64_t* a = src_alloc.data();
   uint8_t* base = mptr<uint8_t>(dst);
   const int64_t cap = dst.numel();
   hipStream_t st = stream();
-  for (int64_t i = 0; i < n; ++i) {
+  int64_t issued = 0;
+  int64_t i = 0;
+  while (i < n) {
     TORCH_CHECK(o[i] >= 0 && l[i] >= 0 && o[i] + l[i] <= cap, "h2d_batch: destination out of bounds");
-    if (l[i] == 0) continue;
-    ok(hipMemcpyAsync(base + o[i], reinterpret_cast<const void*>(s[i]), static_cast<size_t>(l[i]),
+    if (l[i] == 0) {
+      ++i;
+      continue;
+    }
+    int64_t j = i;
+    while (j + 1 < n && l[j + 1] > 0 && a[j + 1] == a[j]) {
+      const int64_t ds = o[j + 1] - o[j], ss = s[j + 1] - s[j];
+      if (ds != ss || ds < l[j] || ds - l[j] >= max_gap) break;
+      TORCH_CHECK(o[j + 1] + l[j + 1] <= cap, "h2d_batch: destination out of bounds");
+      ++j;
+    }
+    const int64_t bytes = o[j] + l[j] - o[i];
+    ok(hipMemcpyAsync(base + o[i], reinterpret_cast<const void*>(s[i]), static_cast<size_t>(bytes),
                       hipMemcpyHostToDevice, st),
        "hipMemcpyAsync");
+    ++issued;
+    i = j + 1;
   }
+  return issued;
 }
 
 }  // namespace

@@ -135,24 +135,44 @@ class DistComm(SwarmComm):
         self.dist = dist
         self.rank = dist.get_rank()
         self.world_size = dist.get_world_size()
-        backend = dist.get_backend()
+        backend = dist.get_backend(data_group)
         if control_group is None:
             control_group = dist.new_group(backend="gloo") if backend != "gloo" else None
         self.control_group = control_group
         self.data_group = data_group
+        self._cap = 64  # int64 words per rank in the one-shot control all-gather
+        if backend == "nccl" and torch.cuda.is_available():
+            # batch_isend_irecv runs on the group's full communicator; when that is created
+            # lazily every rank must take part in its first use.  Node construction is
+            # collective, so create it here rather than at the first (partial) exchange.
+            t = torch.zeros(1, dtype=torch.int64, device=torch.device("cuda", torch.cuda.current_device()))
+            dist.all_reduce(t, group=data_group)
+            torch.cuda.synchronize()
 
     def allgather_control(self, msg: np.ndarray) -> List[np.ndarray]:
+        """Variable-length all-gather in ONE collective on the common path: each rank sends
+        ``[len, payload...]`` padded to a shared capacity.  Only when some rank's message
+        exceeds it does a second all-gather move the full padded messages; the capacity
+        then grows so the following rounds fit again."""
         dist = self.dist
-        msg = np.asarray(msg, dtype=np.int64)
-        n = torch.tensor([msg.size], dtype=torch.int64)
-        sizes = [torch.zeros(1, dtype=torch.int64) for _ in range(self.world_size)]
-        dist.all_gather(sizes, n, group=self.control_group)
-        mx = int(max(int(s.item()) for s in sizes))
-        buf = torch.zeros(max(mx, 1), dtype=torch.int64)
-        buf[:msg.size] = torch.from_numpy(msg)
-        outs = [torch.zeros(max(mx, 1), dtype=torch.int64) for _ in range(self.world_size)]
+        msg = np.asarray(msg, dtype=np.int64).reshape(-1)
+        cap = self._cap
+        buf = torch.zeros(cap + 1, dtype=torch.int64)
+        buf[0] = msg.size
+        k = min(msg.size, cap)
+        buf[1:1 + k] = torch.from_numpy(msg[:k])
+        outs = [torch.empty(cap + 1, dtype=torch.int64) for _ in range(self.world_size)]
         dist.all_gather(outs, buf, group=self.control_group)
-        return [o[:int(s.item())].numpy().copy() for o, s in zip(outs, sizes)]
+        sizes = [int(o[0]) for o in outs]
+        mx = max(sizes)
+        if mx <= cap:
+            return [o[1:1 + n].numpy().copy() for o, n in zip(outs, sizes)]
+        full = torch.zeros(mx, dtype=torch.int64)
+        full[:msg.size] = torch.from_numpy(msg)
+        outs = [torch.empty(mx, dtype=torch.int64) for _ in range(self.world_size)]
+        dist.all_gather(outs, full, group=self.control_group)
+        self._cap = max(cap, int(mx * 1.5) + 16)
+        return [o[:n].numpy().copy() for o, n in zip(outs, sizes)]
 
     def exchange(self, sends, recvs) -> None:
         dist = self.dist
