@@ -45,7 +45,7 @@ from ..ops import crc as _crc
 from ..ops import segment as _seg
 from ..ops._native import runtime as _rt
 from ..parallel.comm import LocalComm, SwarmComm
-from ..utils.trace import PhaseTimer
+from ..utils.trace import PhaseTimer, RequestTrace, TraceLog
 
 log = logging.getLogger("hlsjs_p2p_wrapper_amd.node")
 
@@ -90,9 +90,10 @@ class _Want:
 
 
 class _Completion:
-    __slots__ = ("req", "data", "source", "nbytes", "cdn_ms", "p2p_ms", "entry", "delay")
+    __slots__ = ("req", "data", "source", "nbytes", "cdn_ms", "p2p_ms", "entry", "delay", "peer")
 
-    def __init__(self, req, data, source, nbytes, cdn_ms, p2p_ms, entry=-1, delay=0.0):
+    def __init__(self, req, data, source, nbytes, cdn_ms, p2p_ms, entry=-1, delay=0.0, peer=-1):
+        self.peer = peer
         self.req = req
         self.data = data
         self.source = source
@@ -173,6 +174,9 @@ class SwarmNode:
         self.last_round: Dict[str, Any] = {}
         self.corrupt_next_recv = 0  # fault injection: flip a byte in the next N received rounds
         self.timer = PhaseTimer()
+        # per-request trace records {key, trequest, tfirst, tload, source, bytes, peer, round}
+        # (SURVEY §5.1); None = off (p2pConfig["gpuSwarm"]["trace"] or enable_trace())
+        self.trace: Optional[TraceLog] = None
         self._lock = threading.RLock()
         if self.world > 1 and auto_tick:
             self._timer = self.loop.set_interval(self._timer_tick, round_interval_ms or 10.0)
@@ -449,7 +453,8 @@ class SwarmNode:
             if self._wants.get(w.key) is w:
                 del self._wants[w.key]
             for req in w.waiters:
-                completions.append(_Completion(req, arena[off:off + n], "p2p", n, 0.0, h.p2p_ms, int(row[-1])))
+                completions.append(_Completion(req, arena[off:off + n], "p2p", n, 0.0, h.p2p_ms, int(row[-1]),
+                                               peer=int(row[5])))
         for row, off, n in bad:
             w = h.by_id.get(int(row[7]))
             if w is not None:
@@ -643,12 +648,18 @@ class SwarmNode:
             arr = np.asarray(pin, dtype=np.int64)
             self.store.pin(arr)
             self._pins.append((self.round + PIN_DELAY_ROUNDS, arr))
+        trace = self.trace
+        now = self.loop.now() if trace is not None else 0.0
         for c in completions:
             req = c.req
             if req.aborted or req.done:
                 continue
             req.done = True
             self.stats["segments"] += 1
+            if trace is not None:
+                xfer = c.p2p_ms if c.source == "p2p" else c.cdn_ms
+                trace.add(RequestTrace(req.key, req.t_submit, max(req.t_submit, now - xfer), now, c.source,
+                                       c.nbytes, c.peer if c.source == "p2p" else self.rank, self.round))
             if req.agent is not None:
                 req.agent._account(c.source, c.nbytes)
             cb = req.callbacks
@@ -666,6 +677,11 @@ class SwarmNode:
                 on_success(c.data)
 
     # ------------------------------------------------------------------ lifecycle
+    def enable_trace(self, maxlen: int = 100_000) -> TraceLog:
+        if self.trace is None:
+            self.trace = TraceLog(maxlen)
+        return self.trace
+
     def set_online(self, online: bool) -> None:
         self.online = bool(online)
 
@@ -726,7 +742,7 @@ def node_for_config(p2p_config: Any) -> SwarmNode:
 
     ``gpuSwarm`` keys: ``backend`` ("auto" | "local" | "dist" | "thread"), ``hub`` and
     ``rank`` (thread backend), ``device``, ``cacheBytes``, ``cdnDedup``,
-    ``roundIntervalMs``, ``autoTick``, ``maxWantsPerRound``.
+    ``roundIntervalMs``, ``autoTick``, ``maxWantsPerRound``, ``trace``.
     """
     node = current_node()
     if node is not None and not node.closed:
@@ -753,5 +769,7 @@ def node_for_config(p2p_config: Any) -> SwarmNode:
     node = SwarmNode(comm, device=cfg.get("device", "auto"), cache_bytes=int(cfg.get("cacheBytes", 1 << 30)),
                      cdn_dedup=bool(cfg.get("cdnDedup", True)), round_interval_ms=cfg.get("roundIntervalMs"),
                      auto_tick=bool(cfg.get("autoTick", True)), max_wants_per_round=cfg.get("maxWantsPerRound"))
+    if cfg.get("trace"):
+        node.enable_trace()
     set_current_node(node)
     return node

@@ -64,6 +64,10 @@ def runtime_path() -> Path:
     return HERE / f"_runtime{EXT_SUFFIX}"
 
 
+def asan_runtime_path() -> Path:
+    return BUILD / "asan" / f"_runtime{EXT_SUFFIX}"
+
+
 def device_path() -> Path:
     return HERE / f"_C{EXT_SUFFIX}"
 
@@ -71,7 +75,10 @@ def device_path() -> Path:
 def build_runtime(force: bool = False, sanitize: bool = False, verbose: bool = False) -> Path:
     srcs = sorted(RUNTIME_SRC.glob("*.cpp"))
     hdrs = sorted(RUNTIME_SRC.glob("*.hpp"))
-    out = runtime_path() if not sanitize else HERE / f"_runtime_asan{EXT_SUFFIX}"
+    # the sanitizer build keeps the module name (_runtime) in its own directory; load it
+    # with asan_runtime_path() under LD_PRELOAD=libasan (tests/test_asan_runtime.py)
+    out = runtime_path() if not sanitize else asan_runtime_path()
+    out.parent.mkdir(parents=True, exist_ok=True)
     if not force and not _stale(out, srcs + hdrs):
         return out
     cxx = os.environ.get("CXX", "g++")

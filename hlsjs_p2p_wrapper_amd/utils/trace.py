@@ -52,8 +52,14 @@ class PhaseTimer:
 
 @dataclass
 class RequestTrace:
+    """One delivered request.  Times are event-loop milliseconds (``performance.now``
+    analog): ``trequest`` = submitted to the node, ``tfirst`` = device transfer start
+    (``tload`` minus the HIP-event-timed H2D / RCCL duration of its round), ``tload`` =
+    delivered.  ``peer`` = rank the bytes came from (own rank for CDN / cache)."""
+
     key: Tuple[int, int, int, int]
     trequest: float
+    tfirst: float
     tload: float
     source: str
     bytes: int
@@ -70,3 +76,22 @@ class TraceLog:
 
     def __len__(self) -> int:
         return len(self.records)
+
+    def by_source(self) -> Dict[str, Tuple[int, int]]:
+        """``{source: (requests, bytes)}``."""
+        out: Dict[str, Tuple[int, int]] = {}
+        for r in self.records:
+            n, b = out.get(r.source, (0, 0))
+            out[r.source] = (n + 1, b + r.bytes)
+        return out
+
+    def latency_ms(self, q: float = 0.5, source: Optional[str] = None) -> float:
+        """``q``-quantile of ``tload - trequest``."""
+        xs = sorted(r.tload - r.trequest for r in self.records if source is None or r.source == source)
+        if not xs:
+            return 0.0
+        return xs[min(len(xs) - 1, int(q * len(xs)))]
+
+    def to_dicts(self):
+        return [{"key": list(r.key), "trequest": r.trequest, "tfirst": r.tfirst, "tload": r.tload,
+                 "source": r.source, "bytes": r.bytes, "peer": r.peer, "round": r.round} for r in self.records]

@@ -138,3 +138,25 @@ def test_live_stream_swarm():
     assert all(o["ok"] for o in out.values())
     assert sum(o["stats"]["p2p"] for o in out.values()) > 0
     assert sum(o["stats"]["cdn"] for o in out.values()) == sum(o["stats"]["p2p"] for o in out.values())
+
+
+def test_request_trace_records(vod):
+    # per-request {trequest, tfirst, tload, source, bytes, peer} records
+    traces = {}
+
+    def grab(r, node, w):
+        traces[r] = node.trace
+
+    out = run_swarm(2, vod, before=grab, cfg_extra={"trace": True})
+    assert all(o["ok"] for o in out.values())
+    for r, tr in traces.items():
+        assert len(tr) > 0
+        for rec in tr.records:
+            assert rec.trequest <= rec.tfirst <= rec.tload
+            assert rec.source in ("cdn", "p2p", "cache")
+            assert rec.peer == (1 - r if rec.source == "p2p" else r)
+        by = tr.by_source()
+        assert by.get("cdn", (0, 0))[1] == out[r]["stats"]["cdn"]
+        assert by.get("p2p", (0, 0))[1] == out[r]["stats"]["p2p"]
+        assert tr.latency_ms(0.5) >= 0
+        assert tr.to_dicts()[0]["bytes"] > 0
