@@ -16,11 +16,14 @@ Layout:
   ops/          native: gfx950 kernels (_C) + host runtime (_runtime)
   net/          event loop / timers, CDN origins, HTTP semantics           (L0)
 """
-from .version import _BASE as __version__
+from .version import _STAMPED as __version__
+from .utils import log as _log
 from .models import MediaMap, SegmentView, TrackView
 from .api import Hls, HlsjsP2PWrapper, HlsjsP2PWrapperPrivate, StreamrootHlsjsBundle
 from .agent import PeerAgent, SwarmNode
 from .integration import PlayerInterface, p2p_loader_generator
+
+_log.configure()
 
 __all__ = [
     "Hls", "HlsjsP2PWrapper", "HlsjsP2PWrapperPrivate", "StreamrootHlsjsBundle", "PeerAgent", "SwarmNode",

@@ -38,6 +38,10 @@ class PeerAgent:
         self.SegmentView = SegmentViewClass
         self.streamType = streamType
         self.integrationVersion = integrationVersion
+        if isinstance(self.p2pConfig, dict) and self.p2pConfig.get("debug"):
+            from ..utils.log import configure
+
+            configure(debug=True)
         content_id = self.p2pConfig.get("contentId") if isinstance(self.p2pConfig, dict) else None
         self.contentId = content_id or contentUrl
         self.swarm_id = swarm_id_for(str(self.contentId))

@@ -50,8 +50,10 @@ class Hls:
 
     def __init__(self, config: Optional[Mapping[str, Any]] = None) -> None:
         self.config: HlsConfig = merge_config(config)
-        if config is not None and isinstance(config, dict) and not isinstance(config, HlsConfig):
-            pass
+        if self.config.get("debug"):  # hlsjsConfig.debug -> engine debug logging
+            from ..utils.log import configure
+
+            configure(debug=True)
         self.loop = get_event_loop()
         self._observer = Observer()
         self.url: Optional[str] = None

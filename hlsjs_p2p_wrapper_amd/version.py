@@ -12,8 +12,14 @@ class _Version(str):
     pass
 
 
+try:  # stamped by setup.py at build time (HLSJS_P2P_VERSION then)
+    from ._build_info import VERSION as _STAMPED
+except ImportError:
+    _STAMPED = _BASE
+
+
 def _current() -> str:
-    return os.environ.get("HLSJS_P2P_VERSION", _BASE)
+    return os.environ.get("HLSJS_P2P_VERSION", _STAMPED)
 
 
 def __getattr__(name):  # module-level dynamic VERSION (PEP 562)
