@@ -87,6 +87,7 @@ class _Want:
     force_cdn: bool = False
     attempts: int = 0
     round: int = -1  # round it is in flight in (-1: waiting)
+    prefetch: bool = False  # issued by an agent's prefetch planner (may have no waiters)
 
 
 class _Completion:
@@ -167,12 +168,14 @@ class SwarmNode:
         self._timer = None
         self._pins: List[Tuple[int, np.ndarray]] = []  # (release at launch #, entry ids)
         self._agents: List[Any] = []
+        self._prefetched: Dict[Tuple[int, int, int, int], str] = {}  # key -> "cdn" | "p2p"
         self.peer_online = np.ones(self.world, dtype=bool)
         self.stats = {"cdn": 0, "p2p": 0, "upload": 0, "cache": 0, "rounds": 0, "crc_failures": 0,
-                      "segments": 0, "cdn_segments": 0, "p2p_segments": 0}
+                      "segments": 0, "cdn_segments": 0, "p2p_segments": 0, "prefetched": 0}
         self.swarm_stats = {"cdn": 0, "p2p": 0, "upload": 0}
         self.last_round: Dict[str, Any] = {}
         self.corrupt_next_recv = 0  # fault injection: flip a byte in the next N received rounds
+        self.link_kbps: Dict[int, float] = {}  # fault injection: slow link from peer -> kbit/s
         self.timer = PhaseTimer()
         # per-request trace records {key, trequest, tfirst, tload, source, bytes, peer, round}
         # (SURVEY §5.1); None = off (p2pConfig["gpuSwarm"]["trace"] or enable_trace())
@@ -214,6 +217,7 @@ class SwarmNode:
             self.store.pin(np.array([eid], dtype=np.int64))
             self.loop.call_soon(self._serve_local, req, eid)
             return req
+        self._prefetched.pop(req.key, None)  # evicted before use
         w = self._wants.get(req.key)
         if w is None:
             try:
@@ -227,6 +231,24 @@ class SwarmNode:
         w.waiters.append(req)
         self._schedule()
         return req
+
+    def prefetch(self, key: Tuple[int, int, int, int], url: str, headers: Optional[Dict[str, str]] = None) -> bool:
+        """Fill the cache with a segment no player asked for yet (agent prefetch planning,
+        SURVEY §2.3).  It travels in the next round like any want (P2P from a holder, or
+        the CDN); a player request arriving meanwhile simply joins it.  True if issued."""
+        key = tuple(int(k) & 0xFFFFFFFF for k in key)
+        if key in self._wants or self.store.lookup1(*key) >= 0:
+            return False
+        try:
+            size = http.head(url, dict(headers or {}))
+        except http.HttpError:
+            return False
+        w = _Want(key, url, dict(headers or {}), int(size), self._next_want_id, prefetch=True)
+        self._next_want_id += 1
+        self._wants[key] = w
+        self.stats["prefetched"] += 1
+        self._schedule()
+        return True
 
     def _schedule(self) -> None:
         if self.world == 1 and self.auto_tick and not self._tick_scheduled:
@@ -247,8 +269,11 @@ class SwarmNode:
             if req.aborted:
                 return
             off, n = (int(x) for x in self.store.entries(np.array([eid], dtype=np.int64))[0][:2])
-            self.stats["cache"] += n
-            self._deliver_now([_Completion(req, self.arena[off:off + n], "cache", n, 0.0, 0.0)])
+            # first delivery of a prefetched segment is accounted where its bytes came from
+            src = self._prefetched.pop(req.key, None)
+            if src is None:
+                self.stats["cache"] += n
+            self._deliver_now([_Completion(req, self.arena[off:off + n], src or "cache", n, 0.0, 0.0)])
         finally:
             self.store.unpin(np.array([eid], dtype=np.int64))
 
@@ -325,17 +350,27 @@ class SwarmNode:
                 keep.append((rel, ids))
         self._pins = keep
         # ---------------- 1. control plane
-        wants = []
+        for agent in self._agents:  # agents plan their prefetch just before wants are sent
+            plan = getattr(agent, "plan_prefetch", None)
+            if plan is not None:
+                plan()
+        wants, spec = [], []  # player requests first, then speculative (prefetch-only) wants
+        cap = self.max_wants_per_round
         for k in list(self._wants):
             w = self._wants[k]
             if w.round >= 0:
+                continue
+            if not w.waiters and w.prefetch:
+                spec.append(w)
                 continue
             if not any(not r.aborted for r in w.waiters):
                 del self._wants[k]
                 continue
             wants.append(w)
-            if self.max_wants_per_round is not None and len(wants) >= self.max_wants_per_round:
+            if cap is not None and len(wants) >= cap:
                 break
+        if spec and (cap is None or len(wants) < cap):
+            wants.extend(spec if cap is None else spec[:cap - len(wants)])
         adds, rms = self.store.take_delta()
         parts = self.comm.allgather_control(self._encode(wants, adds, rms))
         all_leaving = True
@@ -443,18 +478,30 @@ class SwarmNode:
         for w, eid, off, n in h.cdn_entries:
             if self._wants.get(w.key) is w:
                 del self._wants[w.key]
+            if w.prefetch and not w.waiters:
+                self._prefetched[w.key] = "cdn"
             for req in w.waiters:
                 completions.append(_Completion(req, arena[off:off + n], "cdn", n, max(h.cdn_ms, h.shaped_ms), 0.0,
                                                eid, h.shaped_ms))
+        link_q: Dict[int, int] = {}  # slow-link fault injection: bytes queued per source link
         for row, off, n in good:
             w = h.by_id.get(int(row[7]))
             if w is None:
                 continue
             if self._wants.get(w.key) is w:
                 del self._wants[w.key]
+            if w.prefetch and not w.waiters:
+                self._prefetched[w.key] = "p2p"
+            src = int(row[5])
+            p2p_ms, delay = h.p2p_ms, 0.0
+            kbps = self.link_kbps.get(src)
+            if kbps:
+                link_q[src] = link_q.get(src, 0) + n
+                delay = link_q[src] * 8.0 / kbps  # kbit/s == bit/ms
+                p2p_ms = max(p2p_ms, delay)
             for req in w.waiters:
-                completions.append(_Completion(req, arena[off:off + n], "p2p", n, 0.0, h.p2p_ms, int(row[-1]),
-                                               peer=int(row[5])))
+                completions.append(_Completion(req, arena[off:off + n], "p2p", n, 0.0, p2p_ms, int(row[-1]),
+                                               delay, peer=src))
         for row, off, n in bad:
             w = h.by_id.get(int(row[7]))
             if w is not None:
@@ -625,7 +672,7 @@ class SwarmNode:
     def _deliver(self, completions: List[_Completion]) -> None:
         now_list = [c for c in completions if c.delay <= 0]
         later = [c for c in completions if c.delay > 0]
-        if later:  # shaped CDN transfers complete after their modelled duration
+        if later:  # shaped CDN / slowed-link transfers complete after their modelled duration
             ids = np.asarray([c.entry for c in later if c.entry is not None and c.entry >= 0], dtype=np.int64)
             if len(ids):
                 self.store.pin(ids)
@@ -681,6 +728,15 @@ class SwarmNode:
         if self.trace is None:
             self.trace = TraceLog(maxlen)
         return self.trace
+
+    def set_link_bandwidth(self, peer: int, kbps: Optional[float]) -> None:
+        """Fault injection (SURVEY §5.3 "slow link"): model the link from ``peer`` to this
+        node at ``kbps`` kbit/s — segments received from it complete after their modelled
+        transfer time (None / 0 restores the real xGMI link)."""
+        if kbps:
+            self.link_kbps[int(peer)] = float(kbps)
+        else:
+            self.link_kbps.pop(int(peer), None)
 
     def set_online(self, online: bool) -> None:
         self.online = bool(online)
@@ -742,7 +798,9 @@ def node_for_config(p2p_config: Any) -> SwarmNode:
 
     ``gpuSwarm`` keys: ``backend`` ("auto" | "local" | "dist" | "thread"), ``hub`` and
     ``rank`` (thread backend), ``device``, ``cacheBytes``, ``cdnDedup``,
-    ``roundIntervalMs``, ``autoTick``, ``maxWantsPerRound``, ``trace``.
+    ``roundIntervalMs``, ``autoTick``, ``maxWantsPerRound``, ``trace``, ``linkKbps``
+    (``{peer: kbit/s}`` slow-link fault injection); the agent reads ``prefetchSeconds`` /
+    ``prefetchMaxSegments``.
     """
     node = current_node()
     if node is not None and not node.closed:
@@ -771,5 +829,7 @@ def node_for_config(p2p_config: Any) -> SwarmNode:
                      auto_tick=bool(cfg.get("autoTick", True)), max_wants_per_round=cfg.get("maxWantsPerRound"))
     if cfg.get("trace"):
         node.enable_trace()
+    for peer, kbps in (cfg.get("linkKbps") or {}).items():
+        node.set_link_bandwidth(int(peer), kbps)
     set_current_node(node)
     return node

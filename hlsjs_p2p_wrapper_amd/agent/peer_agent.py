@@ -50,6 +50,12 @@ class PeerAgent:
         self.media = None
         self.currentTrack = None
         self._stats = {"cdn": 0, "p2p": 0, "upload_base": self.node.stats["upload"], "cache": 0}
+        gs = (self.p2pConfig.get("gpuSwarm") or {}) if isinstance(self.p2pConfig, dict) else {}
+        # prefetch planning (the agent plans ahead of the player with
+        # MediaMap.getSegmentList / getSegmentTime and the playhead from setMediaElement)
+        self.prefetch_seconds = float(gs.get("prefetchSeconds", 0.0) or 0.0)
+        self.prefetch_max = int(gs.get("prefetchMaxSegments", 8))
+        self._prefetch_mark = None
         self.disposed = False
         self._requests = []
         if playerInterface is not None and hasattr(playerInterface, "addEventListener"):
@@ -70,6 +76,39 @@ class PeerAgent:
 
     def setMediaElement(self, media: Any) -> None:
         self.media = media
+
+    def plan_prefetch(self) -> None:
+        """Called by the node right before each round's wants are sent: request the
+        current track's segments in ``[currentTime, currentTime + prefetchSeconds]`` that
+        are neither cached nor in flight.  The player's own later request for one of them
+        is then a local cache hit (or joins the in-flight want)."""
+        if self.prefetch_seconds <= 0 or self.disposed or self.media is None or not self.node.download_on:
+            return
+        track = self.currentTrack
+        if track is None:
+            return
+        t = float(getattr(self.media, "currentTime", 0.0) or 0.0)
+        mark = (round(t, 1), track.level, track.urlId)
+        if mark == self._prefetch_mark:
+            return
+        try:
+            svs = self.mediaMap.getSegmentLists([(track, t, self.prefetch_seconds)])[0]
+        except Exception:  # noqa: BLE001  (level gone: nothing to plan)
+            return
+        if not svs:
+            return  # not parsed yet: retry next round
+        self._prefetch_mark = mark
+        for sv in svs[:self.prefetch_max]:
+            frag = self.mediaMap.fragment(sv)
+            url = getattr(frag, "url", None) if frag is not None else None
+            if not url:
+                continue
+            headers = {}
+            s, e = getattr(frag, "byteRangeStartOffset", None), getattr(frag, "byteRangeEndOffset", None)
+            if isinstance(s, int) and isinstance(e, int):
+                headers["Range"] = f"bytes={s}-{e - 1}"
+            self.node.prefetch((self.swarm_id, int(track.level or 0), int(track.urlId or 0), int(sv.sn)), url,
+                               headers)
 
     def dispose(self) -> None:
         if self.disposed:

@@ -85,6 +85,65 @@ class MediaMap:
             out.append(SegmentView(sn=f.sn, trackView=trackView, time=f.start))
         return out
 
+    # ------------------------------------------------------------------ batched (K1)
+    DEVICE_BATCH_MIN = 64  # below this many queries two host bisects beat a kernel launch
+
+    def getSegmentLists(self, queries: List[Any], device: Any = None) -> List[List[SegmentView]]:
+        """Batched ``getSegmentList`` over ``[(trackView, beginTime, duration), ...]`` —
+        one HIP range-select launch (``ops.segment.range_select``, K1) for all queries
+        when ``device`` is a GPU and the batch is large, host bisects otherwise.  Same
+        semantics per query as :meth:`getSegmentList` (closed interval, playlist order;
+        unparsed level -> ``[]``, missing level -> raises)."""
+        import torch
+
+        dev = torch.device(device) if device is not None else torch.device("cpu")
+        tracks, rows, slots = {}, [], []
+        out: List[List[SegmentView]] = [[] for _ in queries]
+        for qi, (tv, begin, dur) in enumerate(queries):
+            level = self._level(tv.level)
+            if not level:
+                raise Exception("getSegmentList: level doesn't exist")
+            details = getattr(level, "details", None)
+            if not details:
+                log.warning("getSegmentList: level not parsed yet")
+                continue
+            t = tracks.setdefault(tv.level, len(tracks))
+            rows.append((t, float(begin), float(dur)))
+            slots.append(qi)
+        if not rows:
+            return out
+        levels = sorted(tracks, key=tracks.get)
+        frag_lists = [self.hls.levels[lv].details.fragments for lv in levels]
+        if dev.type == "cpu" or len(rows) < self.DEVICE_BATCH_MIN:
+            for (t, b, d), qi in zip(rows, slots):
+                out[qi] = self.getSegmentList(queries[qi][0], b, d)
+            return out
+        from ..ops.segment import range_select
+
+        starts = [[f.start for f in fl] for fl in frag_lists]
+        lo, hi = range_select(starts, rows, dev)
+        for (t, _, _), qi, a, b in zip(rows, slots, lo.tolist(), hi.tolist()):
+            tv = queries[qi][0]
+            fl = frag_lists[t]
+            out[qi] = [SegmentView(sn=fl[i].sn, trackView=tv, time=fl[i].start) for i in range(max(a, 0), max(b, 0))]
+        return out
+
+    def fragment(self, segmentView: SegmentView) -> Any:
+        """The playlist fragment behind a SegmentView (url / byte range for the agent's
+        own prefetch requests), or None."""
+        level = self._level(segmentView.trackView.level)
+        details = getattr(level, "details", None) if level else None
+        if not details or not details.fragments:
+            return None
+        frags = details.fragments
+        i = int(segmentView.sn) - int(frags[0].sn)
+        if 0 <= i < len(frags) and frags[i].sn == segmentView.sn:
+            return frags[i]
+        for f in frags:
+            if f.sn == segmentView.sn:
+                return f
+        return None
+
     def getTrackList(self) -> List[TrackView]:
         levels = self.hls.levels
         if not levels:

@@ -72,3 +72,33 @@ def test_range_select_cpu_matches_media_map():
     for (t, b, d), l, h in zip(queries, lo, hi):
         want = [s.sn for s in mm.getSegmentList(TrackView(level=1, urlId=0), b, d)]
         assert [25 + i for i in range(l, h)] == want
+
+
+_QUERIES = [(365, 33), (10, 275), (1975, 3000), (240, 2100), (2100, 3000), (0, 0), (250, 0), (-50, 60)]
+
+
+def test_batched_segment_lists_match_single_queries():
+    mm = _mm(3, False, 1)
+    tv = TrackView(level=1, urlId=1)
+    qs = [(tv, b, d) for b, d in _QUERIES]
+    assert mm.getSegmentLists(qs) == [mm.getSegmentList(tv, b, d) for b, d in _QUERIES]
+    with pytest.raises(Exception, match="level doesn't exist"):
+        mm.getSegmentLists([(TrackView(level=7, urlId=0), 0, 10)])
+
+
+def test_fragment_lookup():
+    mm = _mm(3, False, 1)
+    tv = TrackView(level=1, urlId=0)
+    f = mm.fragment(SegmentView(sn=42, trackView=tv, time=420))
+    assert f is not None and f.sn == 42
+    assert mm.fragment(SegmentView(sn=100000, trackView=tv, time=0)) is None
+
+
+@pytest.mark.gpu
+def test_batched_segment_lists_on_device(cuda):
+    # >= DEVICE_BATCH_MIN queries: answered by the HIP range-select kernel (K1)
+    mm = _mm(3, False, 1)
+    tv = TrackView(level=1, urlId=1)
+    qs = [(tv, b + 7 * i, d) for i in range(12) for b, d in _QUERIES]
+    assert len(qs) >= MediaMap.DEVICE_BATCH_MIN
+    assert mm.getSegmentLists(qs, device=cuda) == [mm.getSegmentList(tv, b, d) for _, b, d in qs]

@@ -160,3 +160,32 @@ def test_request_trace_records(vod):
         assert by.get("p2p", (0, 0))[1] == out[r]["stats"]["p2p"]
         assert tr.latency_ms(0.5) >= 0
         assert tr.to_dicts()[0]["bytes"] > 0
+
+
+def test_agent_prefetch_fills_cache_ahead_of_player(vod):
+    # the late joiner prefetches ahead of its playhead; its player's requests then hit
+    # the local cache, and the bytes are still accounted as P2P (where they came from)
+    out = run_swarm(2, vod, start_delay=lambda r: 60_000 if r == 1 else 0, timeout=400_000,
+                    cfg_extra={"prefetchSeconds": 16.0}, hls_cfg={"maxBufferLength": 4})
+    assert all(o["ok"] for o in out.values())
+    assert out[1]["node"]["prefetched"] > 0
+    seg_total = sum(vod.pools[0].lengths)
+    assert out[1]["stats"]["cdn"] == 0
+    assert out[1]["stats"]["p2p"] == seg_total  # every segment played once, counted once
+    assert out[0]["stats"]["cdn"] == seg_total
+
+
+def test_slow_link_fault_injection(vod):
+    # a slow peer link delays P2P completions by their modelled transfer time
+    def lat(out_traces, r):
+        return out_traces[r].latency_ms(0.5, source="p2p")
+
+    fast, slow = {}, {}
+    run_swarm(2, vod, before=lambda r, node, w: fast.__setitem__(r, node.trace), cfg_extra={"trace": True})
+    out = run_swarm(2, vod, before=lambda r, node, w: slow.__setitem__(r, node.trace),
+                    cfg_extra={"trace": True, "linkKbps": {0: 8000, 1: 8000}})
+    assert all(o["ok"] for o in out.values())
+    # ~250 KB segments over an 8 Mb/s link: >= 250 ms each, far above the unshaped case
+    assert lat(slow, 1) > 200 and lat(slow, 1) > 5 * max(lat(fast, 1), 1.0)
+    recs = [r for r in slow[1].records if r.source == "p2p"]
+    assert recs and all(r.tload - r.tfirst >= r.bytes * 8 / 8000 - 1e-6 for r in recs)
