@@ -20,6 +20,7 @@ from ._native import device as _dev
 from ._native import runtime as _rt
 from .desc import pack_to_device
 
+CHUNK_BLOCKS = 256  # 16-B blocks per wave iteration in kernels/aes_cbc.hip (64 lanes x kBlk)
 _key_cache: Dict[bytes, np.ndarray] = {}
 _tables: Dict[str, tuple] = {}
 _lock = threading.Lock()
@@ -78,15 +79,17 @@ def cbc_decrypt_batch(src: torch.Tensor, src_offs: Sequence[int], nbytes: Sequen
         return torch.from_numpy(out_len)
     blk_prefix = np.zeros(B + 1, dtype=np.int64)
     np.cumsum(nb // 16, out=blk_prefix[1:])
-    pair_prefix = np.zeros(B + 1, dtype=np.int64)  # work unit: 2 blocks of one segment
-    np.cumsum((nb // 16 + 1) // 2, out=pair_prefix[1:])
+    # work unit: one wave-chunk of CHUNK_BLOCKS consecutive blocks of one segment
+    units = (nb // 16 + CHUNK_BLOCKS - 1) // CHUNK_BLOCKS
+    unit_prefix = np.zeros(B + 1, dtype=np.int64)
+    np.cumsum(units, out=unit_prefix[1:])
     drk_le = drk.byteswap()  # state words are used as loaded (little-endian) on device
-    d = pack_to_device({"so": so, "do": do, "bp": blk_prefix, "pp": pair_prefix, "drk": drk_le, "iv": iv},
+    d = pack_to_device({"so": so, "do": do, "bp": blk_prefix, "pp": unit_prefix, "drk": drk_le, "iv": iv},
                        src.device)
     out_len = torch.empty(B, dtype=torch.int64, device=src.device)
     td0, isb = _device_tables(src.device)
     _dev().aes128_cbc_decrypt(src, dst, d["so"], d["do"], d["bp"], d["pp"], d["drk"], d["iv"], td0, isb, out_len,
-                              int(pair_prefix[-1]))
+                              int(unit_prefix[-1]))
     return out_len
 
 

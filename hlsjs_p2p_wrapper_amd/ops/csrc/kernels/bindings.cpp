@@ -64,15 +64,15 @@ template <typename T>
 T* mptr(const Tensor& t) { return reinterpret_cast<T*>(t.data_ptr()); }
 
 void aes128_cbc_decrypt(Tensor src, Tensor dst, Tensor src_off, Tensor dst_off, Tensor blk_prefix,
-                        Tensor pair_prefix, Tensor drk, Tensor iv, Tensor td0, Tensor isb, Tensor out_len,
-                        int64_t total_pairs) {
+                        Tensor chunk_prefix, Tensor drk, Tensor iv, Tensor td0, Tensor isb, Tensor out_len,
+                        int64_t total_chunks) {
   const int64_t B = src_off.numel();
   check(src, "src", torch::kUInt8);
   check(dst, "dst", torch::kUInt8);
   check(src_off, "src_off", torch::kInt64);
   check(dst_off, "dst_off", torch::kInt64, B);
   check(blk_prefix, "blk_prefix", torch::kInt64, B + 1);
-  check(pair_prefix, "pair_prefix", torch::kInt64, B + 1);
+  check(chunk_prefix, "chunk_prefix", torch::kInt64, B + 1);
   check(drk, "drk", torch::kInt32, B * 44);
   check(iv, "iv", torch::kUInt8, B * 16);
   check(td0, "td0", torch::kInt32, 256);
@@ -84,9 +84,9 @@ void aes128_cbc_decrypt(Tensor src, Tensor dst, Tensor src_off, Tensor dst_off, 
               "src/dst must be 16-byte aligned");
   same_device(src, dst);
   ok(D::launch_aes128_cbc_decrypt(cptr<uint8_t>(src), mptr<uint8_t>(dst), cptr<int64_t>(src_off),
-                                  cptr<int64_t>(dst_off), cptr<int64_t>(blk_prefix), cptr<int64_t>(pair_prefix),
+                                  cptr<int64_t>(dst_off), cptr<int64_t>(blk_prefix), cptr<int64_t>(chunk_prefix),
                                   cptr<uint32_t>(drk), cptr<uint32_t>(iv), cptr<uint32_t>(td0), cptr<uint8_t>(isb),
-                                  mptr<int64_t>(out_len), static_cast<int>(B), total_pairs, num_cus(src), stream()),
+                                  mptr<int64_t>(out_len), static_cast<int>(B), total_chunks, num_cus(src), stream()),
      "aes128_cbc_decrypt");
 }
 

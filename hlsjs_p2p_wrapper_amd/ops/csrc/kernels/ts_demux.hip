@@ -240,6 +240,7 @@ __global__ __launch_bounds__(kTsThreads) void ts_gather_kernel(
   __shared__ int64_t s_tot[2 * kClasses];     // segment totals
   __shared__ int64_t s_pre[2 * kClasses];     // prefix of blocks before this one
   __shared__ int32_t s_wave[4][2 * kClasses];  // per-wave totals
+  __shared__ uint8_t s_order[4][64];           // per wave: active-packet rank -> lane
   const int64_t gblk = blockIdx.x;
   const int seg = find_seg(blk_prefix, nseg, gblk);
   const int64_t b0 = blk_prefix[seg];
@@ -326,33 +327,51 @@ __global__ __launch_bounds__(kTsThreads) void ts_gather_kernel(
       }
     }
   }
-  // cooperative per-packet copy out of the LDS-staged block: the whole wave moves one packet
-  // payload at a time with dword-aligned global stores (v_alignbyte funnel on LDS reads)
+  // Copy out of the LDS-staged block, FOUR packets per wave iteration: each 16-lane group
+  // moves one payload (<= 184 B = 46 dwords -> 3 dword-aligned stores per lane, v_alignbyte
+  // funnel on the LDS reads, byte stores only for the <= 3 + 3 unaligned head/tail bytes).
+  // Active packets are ranked with mbcnt; s_order maps rank -> lane so group g of iteration
+  // i takes rank 4i+g.
   const uint8_t* s_bytes = reinterpret_cast<const uint8_t*>(s_pk);
   uint8_t* ebase = es + es_off[seg];
-  uint64_t active = __ballot(c < 3 && len > 0);
-  while (active) {
-    const int j = __builtin_ctzll(active);
-    active &= active - 1;
-    const int jlen = __shfl(len, j);
+  const bool act = c < 3 && len > 0;
+  const uint64_t amask = __ballot(act);
+  const int nact = __popcll(amask);
+  if (act) {
+    const int rank = __builtin_amdgcn_mbcnt_hi(static_cast<uint32_t>(amask >> 32),
+                                               __builtin_amdgcn_mbcnt_lo(static_cast<uint32_t>(amask), 0));
+    s_order[wave][rank] = static_cast<uint8_t>(lane);
+  }
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  const int grp = lane >> 4, sub = lane & 15;
+  for (int base = 0; base < nact; base += 4) {
+    const int r = base + grp;
+    const int j = r < nact ? s_order[wave][r] : 0;
+    const int jlen_all = __shfl(len, j);
     const int jps = __shfl(ps, j);
     const int64_t jdst = __shfl(dst_b, j);
+    const int jlen = r < nact ? jlen_all : 0;
     const int s = (wave * 64 + j) * kPkt + jps;  // LDS byte offset of the payload
     uint8_t* d = ebase + jdst;
     const int mis = static_cast<int>((4 - (reinterpret_cast<uintptr_t>(d) & 3)) & 3);
     const int head = mis < jlen ? mis : jlen;
     const int body = (jlen - head) >> 2;
     const int tail = jlen - head - 4 * body;
-    if (lane < head) d[lane] = s_bytes[s + lane];
-    if (lane < body) {
-      const int a = s + head + 4 * lane;
-      const uint32_t sh = static_cast<uint32_t>(a & 3);
-      const uint32_t lo = s_pk[a >> 2];
-      const uint32_t hi = s_pk[(a >> 2) + 1];
-      const uint32_t v = sh ? __builtin_amdgcn_alignbyte(hi, lo, sh) : lo;
-      reinterpret_cast<uint32_t*>(d + head)[lane] = v;
+    if (sub < head) d[sub] = s_bytes[s + sub];
+    uint32_t* dw = reinterpret_cast<uint32_t*>(d + head);
+#pragma unroll
+    for (int q = 0; q < 3; ++q) {
+      const int k = sub + 16 * q;
+      if (k < body) {
+        const int a = s + head + 4 * k;
+        const uint32_t sh = static_cast<uint32_t>(a & 3);
+        const uint32_t lo = s_pk[a >> 2];
+        const uint32_t hi = s_pk[(a >> 2) + 1];
+        dw[k] = sh ? __builtin_amdgcn_alignbyte(hi, lo, sh) : lo;
+      }
     }
-    if (lane < tail) d[head + 4 * body + lane] = s_bytes[s + head + 4 * body + lane];
+    if (sub < tail) d[head + 4 * body + sub] = s_bytes[s + head + 4 * body + sub];
   }
   if (blk == 0 && tid == 0) {
     int64_t* inf = info + static_cast<int64_t>(seg) * kInfo;
