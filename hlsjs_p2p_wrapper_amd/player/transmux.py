@@ -198,23 +198,32 @@ class MediaPipeline:
         t4 = time.perf_counter()
         tm.add("wait_device", t4 - t3)
         results = b.results
-        keys = list(_ts.INFO.keys())
-        slots = list(_ts.INFO.values())
         for (idx, res, es_offs, lens), (hinfo, hlens) in zip(b.infos, b.host):
             hinfo = hinfo.numpy() if isinstance(hinfo, torch.Tensor) else hinfo
             plain_lens = hlens.numpy() if isinstance(hlens, torch.Tensor) else hlens
-            rows = hinfo[:, slots].tolist()
+            rows = hinfo.tolist()
+            # ES views of the whole group in ONE split (video | audio | id3 | pad per
+            # segment) instead of three ATen slicing calls per fragment
+            cuts, first, pos = [], [], 0
+            for k in range(len(idx)):
+                row, base = rows[k], es_offs[k]
+                if base > pos:
+                    cuts.append(base - pos)  # alignment gap before this segment's ES
+                first.append(len(cuts))
+                cuts += [row[_VB], row[_AB], row[_IB]]
+                pos = base + row[_VB] + row[_AB] + row[_IB]
+            cuts.append(res.es.numel() - pos)
+            views = torch.split(res.es, cuts)
             for k, i in enumerate(idx):
-                info = dict(zip(keys, rows[k]))
-                base = es_offs[k]
-                vb, ab, ib = info["video_bytes"], info["audio_bytes"], info["id3_bytes"]
+                row = rows[k]
+                video, audio, id3 = views[first[k]], views[first[k] + 1], views[first[k] + 2]
                 r = {
-                    "status": info["status"],
-                    "info": info,
+                    "status": row[0],
+                    "info": InfoRow(row),
                     "plain_bytes": int(plain_lens[k]),
-                    "video": res.es[base:base + vb],
-                    "audio": res.es[base + vb:base + vb + ab],
-                    "id3": res.es[base + vb + ab:base + vb + ab + ib],
+                    "video": video,
+                    "audio": audio,
+                    "id3": id3,
                     "demux": res,
                     "index": k,
                 }
@@ -223,6 +232,48 @@ class MediaPipeline:
                 results[i] = r
         tm.add("results", time.perf_counter() - t4)
         return results  # type: ignore[return-value]
+
+
+_VB, _AB, _IB = _ts.INFO["video_bytes"], _ts.INFO["audio_bytes"], _ts.INFO["id3_bytes"]
+
+
+class InfoRow:
+    """Read-only ``{name: value}`` view of one demux ``info`` row (names of
+    :data:`ops.tsdemux.INFO`), sharing one key->slot schema instead of a dict per fragment."""
+
+    __slots__ = ("_row",)
+    _SLOTS = _ts.INFO
+
+    def __init__(self, row) -> None:
+        self._row = row
+
+    def __getitem__(self, name: str) -> int:
+        return self._row[self._SLOTS[name]]
+
+    def get(self, name: str, default=None):
+        slot = self._SLOTS.get(name)
+        return default if slot is None else self._row[slot]
+
+    def keys(self):
+        return self._SLOTS.keys()
+
+    def items(self):
+        return ((k, self._row[v]) for k, v in self._SLOTS.items())
+
+    def __contains__(self, name: str) -> bool:
+        return name in self._SLOTS
+
+    def __iter__(self):
+        return iter(self._SLOTS)
+
+    def __len__(self) -> int:
+        return len(self._SLOTS)
+
+    def to_dict(self):
+        return dict(self.items())
+
+    def __repr__(self) -> str:
+        return f"InfoRow({self.to_dict()})"
 
 
 @dataclass(eq=False)
