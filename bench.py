@@ -36,6 +36,7 @@ if os.environ.get("HLSP2P_PROFILE"):  # cProfile the timed steps (host-overhead 
     import cProfile
 
     _PROF = cProfile.Profile()
+_PROF_C3 = _PROF is not None and os.environ.get("HLSP2P_PROFILE_SECTION") == "c3"  # only the post-transmux drain
 
 CONFIGS = {
     # name: (renditions preset, encrypted, segment seconds, description)
@@ -45,6 +46,7 @@ CONFIGS = {
     "4k25m": ("4k", True, 4.0, "4K 25 Mb/s HLS (AES-128, 4 s TS segments)"),
     # diagnostic only: ~30 KB segments, so per-segment host (Python) cost dominates
     "hostcost": ("tiny", True, 4.0, "60 kb/s HLS (AES-128) - host-overhead probe"),
+    "hostcost-abr": ("tiny-abr", True, 4.0, "5 x 20-100 kb/s ABR ladder (AES-128) - host-overhead probe"),
 }
 
 
@@ -61,6 +63,7 @@ def parse():
     p.add_argument("--cpu", action="store_true", help="CPU rehearsal (gloo, no GPU)")
     p.add_argument("--sync-steps", action="store_true",
                    help="no software pipelining: each step = load, round, transmux, synchronously")
+    p.add_argument("--no-gc-tune", action="store_true", help="keep Python's default GC settings")
     p.add_argument("--verbose", action="store_true")
     return p.parse_args()
 
@@ -92,7 +95,8 @@ def main() -> int:
 
     preset, encrypted, seg_dur, desc = CONFIGS[args.config]
     rends = {"1080p": PRESET_1080P_6M, "4k": PRESET_4K_25M, "abr5": PRESET_ABR5,
-             "tiny": [Rendition(60_000, 320, 180, name="180p")]}[preset]
+             "tiny": [Rendition(60_000, 320, 180, name="180p")],
+             "tiny-abr": [Rendition(20_000 * (i + 1), 160 * (i + 1), 90 * (i + 1), name=f"t{i}") for i in range(5)]}[preset]
     K = args.inflight
     total_steps = args.warmup + args.steps
     n_segments = (total_steps + 4) * K
@@ -114,9 +118,10 @@ def main() -> int:
         hls_config["startLevel"] = 0
     hls = Hls(hls_config, p2p_config)
     media = MediaElement(mode="drain", loop=loop)
-    counters = {"buffered": 0, "errors": 0}
+    counters = {"buffered": 0, "errors": 0, "level_switches": 0}
     hls.on(Hls.Events.FRAG_BUFFERED, lambda e, d: counters.__setitem__("buffered", counters["buffered"] + 1))
     hls.on(Hls.Events.ERROR, lambda e, d: counters.__setitem__("errors", counters["errors"] + 1))
+    hls.on(Hls.Events.LEVEL_SWITCH, lambda e, d: counters.__setitem__("level_switches", counters["level_switches"] + 1))
     hls.loadSource(origin.master_url())
     hls.attachMedia(media)
     hls.on(Hls.Events.MANIFEST_PARSED, lambda e, d: media.play())
@@ -138,7 +143,11 @@ def main() -> int:
     if not sc.inflight:
         raise RuntimeError("player did not start loading fragments")
 
+    from hlsjs_p2p_wrapper_amd.utils.runtime import tune_gc
     from hlsjs_p2p_wrapper_amd.utils.trace import PhaseTimer
+
+    if not args.no_gc_tune:
+        tune_gc()  # freeze the start-up heap (playlists, engine, node): no full-GC pauses mid-round
 
     bt = PhaseTimer()
 
@@ -169,9 +178,18 @@ def main() -> int:
             drain_ready()
             t2 = time.perf_counter()
             b = pipe.launch()
+            t21 = time.perf_counter()
             pipe.complete(state["b"])
+            t22 = time.perf_counter()
+            if _PROF_C3:
+                _PROF.enable()
             drain_ready()
+            if _PROF_C3:
+                _PROF.disable()
             t25 = time.perf_counter()
+            bt.add("c1_tx_launch", t21 - t2)
+            bt.add("c2_tx_complete", t22 - t21)
+            bt.add("c3_drain", t25 - t22)
             sc.tick()
             drain_ready()
             state["h"], state["b"] = h, b
@@ -197,7 +215,7 @@ def main() -> int:
     pipe.timer.reset()
     b0, s0 = counters["buffered"], dict(node.stats)
     t0 = time.perf_counter()
-    if _PROF is not None:
+    if _PROF is not None and not _PROF_C3:
         _PROF.enable()
     for _ in range(args.steps):
         step()
@@ -239,7 +257,8 @@ def main() -> int:
                    "device": "MI355X" if use_gpu else "cpu"},
     }
     if args.verbose:
-        print(f"# rank {rank} pack {t_pack:.2f}s node stats {node.stats} last round {node.last_round}\n"
+        print(f"# rank {rank} pack {t_pack:.2f}s counters {counters} level {hls.currentLevel}\n"
+              f"#   node stats {node.stats} last round {node.last_round}\n"
               f"#   step ms {bt.summary_ms(args.steps)}\n"
               f"#   node ms {node.timer.summary_ms(args.steps)}\n"
               f"#   transmux ms {pipe.timer.summary_ms(args.steps)}", file=sys.stderr)

@@ -115,6 +115,7 @@ class RoundHandle:
     cdn_entries: List[Tuple[_Want, int, int, int]] = field(default_factory=list)
     recv_entries: List[Tuple[np.ndarray, int, int]] = field(default_factory=list)
     send_pins: Optional[np.ndarray] = None
+    hold: List[np.ndarray] = field(default_factory=list)  # in-flight entries pinned until delivered
     sent_bytes: int = 0
     ev_cdn: Any = None
     dmas: int = 0
@@ -371,6 +372,7 @@ class SwarmNode:
                 break
         if spec and (cap is None or len(wants) < cap):
             wants.extend(spec if cap is None else spec[:cap - len(wants)])
+        wants = self._admit(wants)
         adds, rms = self.store.take_delta()
         parts = self.comm.allgather_control(self._encode(wants, adds, rms))
         all_leaving = True
@@ -515,7 +517,10 @@ class SwarmNode:
                 w.round = -1
         t2 = time.perf_counter()
         self.timer.add("commit", t2 - t1)
-        self._deliver(completions)
+        self._deliver(completions)  # delivered entries stay pinned PIN_DELAY_ROUNDS launches
+        for ids in h.hold:  # in-flight pins from reservation (dropped entries: no-op)
+            self.store.unpin(ids)
+        h.hold = []
         self.timer.add("deliver", time.perf_counter() - t2)
         self.timer.add("dev_cdn_ms", h.cdn_ms / 1e3)
         self.timer.add("dev_p2p_ms", h.p2p_ms / 1e3)
@@ -526,6 +531,35 @@ class SwarmNode:
             self._schedule()
 
     # ------------------------------------------------------------------ phases
+    def _admit(self, wants: List[_Want]) -> List[_Want]:
+        """Backpressure: a rank only ever receives what it asked for, so cap this round's
+        wants to what the ring can place now without evicting pinned (in-flight or
+        being-consumed) entries; the rest wait for the next round."""
+        if not wants:
+            return wants
+        st = self.store
+        sizes = [st.aligned(w.size) for w in wants]
+        total = sum(sizes)
+        if st.fits(total):
+            return wants
+        lo, hi = 0, len(wants)  # largest prefix that fits
+        while lo < hi:
+            mid = (lo + hi + 1) // 2
+            if st.fits(sum(sizes[:mid])):
+                lo = mid
+            else:
+                hi = mid - 1
+        kept = wants[:lo]
+        for w, a in zip(wants[lo:], sizes[lo:]):
+            if a > self.cache_bytes:  # can never fit: fail it
+                if self._wants.get(w.key) is w:
+                    del self._wants[w.key]
+                err = http.HttpError(507, f"segment of {w.size} bytes exceeds the {self.cache_bytes}-byte cache")
+                for req in w.waiters:
+                    self.loop.call_soon(self._fail, req, err)
+        self.stats["deferred"] = self.stats.get("deferred", 0) + len(wants) - lo
+        return kept
+
     def _cdn_phase(self, h: RoundHandle, cdn_rows: np.ndarray) -> None:
         wants, sources = [], []
         for wid in cdn_rows[:, 7].tolist():
@@ -554,9 +588,11 @@ class SwarmNode:
         keys = np.asarray([w.key for w in wants], dtype=np.int64)
         lens = np.asarray([s[2] for s in sources], dtype=np.int64)
         res = self.store.reserve_run(keys, lens, self.round)
-        if res is None:
+        if res is None:  # _admit guarantees room; reaching this is a bookkeeping bug
             raise RuntimeError("segment cache cannot make room (pinned entries block eviction)")
         _, ids, offs = res
+        self.store.pin(ids)  # in flight until delivered (complete_round unpins)
+        h.hold.append(ids)
         self._grow_crc(int(ids.max()) + 1)
         if self.is_cuda:
             start = torch.cuda.Event(enable_timing=True)
@@ -625,9 +661,11 @@ class SwarmNode:
             keys = np.ascontiguousarray(rows[:, :4])
             lens = np.ascontiguousarray(rows[:, 4])
             res = self.store.reserve_run(keys, lens, self.round)
-            if res is None:
+            if res is None:  # _admit guarantees room
                 raise RuntimeError("segment cache cannot make room for peer data")
             base, ids, offs = res
+            self.store.pin(ids)
+            h.hold.append(ids)
             self._grow_crc(int(ids.max()) + 1)
             total = int(offs[-1] + lens[-1] - offs[0])
             recvs.append((int(src), self.arena[int(base):int(base) + total]))

@@ -299,6 +299,8 @@ PYBIND11_MODULE(_runtime, m) {
         if (base < 0) return py::none();
         return py::make_tuple(base, ids, offs);
       })
+      .def("fits", &SegmentStore::fits)
+      .def("aligned", &SegmentStore::aligned)
       .def("commit", [](SegmentStore& s, Arr<int64_t> ids) {
         for (int64_t i = 0; i < ids.size(); ++i) s.commit(ids.data()[i]);
       })

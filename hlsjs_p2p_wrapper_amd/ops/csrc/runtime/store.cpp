@@ -67,6 +67,29 @@ bool SegmentStore::make_room(int64_t start, int64_t len, bool wrapped) {
   return true;
 }
 
+bool SegmentStore::fits(int64_t total) const {
+  if (total <= 0) return true;
+  if (total > capacity_) return false;
+  int64_t start = head_;
+  bool wrapped = false;
+  if (start + total > capacity_) {
+    start = 0;
+    wrapped = true;
+  }
+  const int64_t end = start + total;
+  // same walk as make_room, without evicting: every FIFO entry it would have to evict
+  // must be unpinned
+  for (const auto& fe : fifo_) {
+    const Entry& e = entries_[fe.first];
+    if (e.state == kFree || e.gen != fe.second) continue;
+    const bool in_skip = wrapped && e.offset >= head_;
+    const bool overlaps = e.offset < end && e.offset + e.alloc_bytes > start;
+    if (!in_skip && !overlaps) break;
+    if (e.pins > 0) return false;
+  }
+  return true;
+}
+
 int64_t SegmentStore::reserve_run(const SegKey* keys, const int64_t* lens, int64_t n, int64_t tick, int64_t* ids,
                                   int64_t* offsets) {
   int64_t total = 0;

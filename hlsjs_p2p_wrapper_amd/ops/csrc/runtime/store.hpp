@@ -79,6 +79,13 @@ class SegmentStore {
   // are replaced.
   int64_t reserve_run(const SegKey* keys, const int64_t* lens, int64_t n, int64_t tick, int64_t* ids,
                       int64_t* offsets);
+  // Would a run of `total` aligned bytes fit at the head now (no pinned entry in its way)?
+  // Non-mutating; consecutive smaller runs of the same total then fit too (backpressure).
+  bool fits(int64_t total) const;
+  int64_t aligned(int64_t len) const {
+    const int64_t a = (len + align_ - 1) & ~(align_ - 1);
+    return a == 0 ? align_ : a;
+  }
   void commit(int64_t id);  // pending -> resident (+ "add" delta)
   void drop(int64_t id);    // remove now (+ "remove" delta if it was resident)
   void pin(int64_t id) { entries_[id].pins += 1; }

@@ -189,3 +189,36 @@ def test_slow_link_fault_injection(vod):
     assert lat(slow, 1) > 200 and lat(slow, 1) > 5 * max(lat(fast, 1), 1.0)
     recs = [r for r in slow[1].records if r.source == "p2p"]
     assert recs and all(r.tload - r.tfirst >= r.bytes * 8 / 8000 - 1e-6 for r in recs)
+
+
+def test_small_cache_backpressure():
+    # SURVEY config 5 analog: a cache far smaller than the stream, and many fragments in
+    # flight: wants are deferred (never evicting in-flight / being-consumed segments) and
+    # playback completes with correct bytes
+    origin = SyntheticHlsOrigin("http://cdn.test/small/", renditions=[Rendition(4_000_000, 1280, 720)],
+                                num_segments=12, encrypted=True)
+    seg = max(origin.pools[0].lengths)
+    out = run_swarm(2, origin, until=44.0, cfg_extra={"cacheBytes": 3 * (seg + 4096), "maxWantsPerRound": 8},
+                    hls_cfg={"maxFragLoadsInFlight": 6, "maxBufferLength": 60})
+    assert all(o["ok"] for o in out.values())
+    assert sum(o["node"].get("deferred", 0) for o in out.values()) > 0
+    total = sum(origin.pools[0].lengths[i % len(origin.pools[0].lengths)] for i in range(12))
+    for o in out.values():
+        assert o["stats"]["cdn"] + o["stats"]["p2p"] == total
+
+
+def test_segment_larger_than_cache_fails_cleanly():
+    # a segment that can never fit the cache fails its request with an HTTP-like error
+    # (the loader contract: errors surface as {status}) instead of waiting forever
+    from hlsjs_p2p_wrapper_amd.agent import SwarmNode
+
+    origin = SyntheticHlsOrigin("http://cdn.test/huge/", renditions=[Rendition(2_000_000, 640, 360)],
+                                num_segments=2, encrypted=False)
+    loop = new_event_loop("virtual")
+    node = SwarmNode(device="cpu", cache_bytes=64 << 10, loop=loop)
+    got = {}
+    url = origin.base_url + origin.segment_path(0, 0)
+    node.request((1, 0, 0, 0), url, {}, {"onSuccess": lambda d: got.setdefault("ok", d),
+                                          "onError": lambda e: got.setdefault("err", e)})
+    loop.run_until(lambda: got, timeout_ms=5_000)
+    assert "err" in got and getattr(got["err"], "status", None) == 507
