@@ -434,8 +434,10 @@ class SwarmNode:
                     send_ids.setdefault(w.key, eid)
             t_p2p0 = time.perf_counter()
             self.timer.add("cdn_enqueue", t_p2p0 - t_cdn0)
-            # ---------------- 4. P2P phase
-            if len(send_rows) or len(recv_rows):
+            # ---------------- 4. P2P phase: entered by EVERY rank when the (identical) plan
+            # has any transfer, so a collective transport (the in-process hub) stays in step;
+            # RCCL point-to-point with no local ops posts nothing
+            if bool((plan[:, 5] >= 0).any()):
                 self._p2p_phase(h, send_rows, recv_rows, send_ids)
             h.sent_bytes = int(send_rows[:, 4].sum()) if len(send_rows) else 0
             if self.is_cuda:

@@ -222,3 +222,65 @@ def test_segment_larger_than_cache_fails_cleanly():
                                           "onError": lambda e: got.setdefault("err", e)})
     loop.run_until(lambda: got, timeout_ms=5_000)
     assert "err" in got and getattr(got["err"], "status", None) == 507
+
+
+def test_abr_ladder_track_switching_under_churn():
+    # BASELINE config 3 analog: 3 peers on a 3-rendition ladder; level switches mid-stream
+    # (track-view changes reach the agents through PlayerInterface 'onTrackChange') while
+    # peer 2 churns offline and back.  Everyone plays through, P2P keeps flowing, and no
+    # peer receives P2P bytes while it is masked offline.
+    origin = SyntheticHlsOrigin("http://cdn.test/abr/", renditions=[Rendition(400_000, 480, 270),
+                                                                    Rendition(800_000, 640, 360),
+                                                                    Rendition(1_600_000, 960, 540)],
+                                num_segments=12, encrypted=True)
+    hub = ThreadHub(3)
+    out, errs = {}, []
+
+    def peer(r):
+        try:
+            set_current_node(None)
+            loop = new_event_loop("virtual")
+            gs = {"backend": "thread", "hub": hub, "rank": r, "device": "cpu", "cacheBytes": 256 << 20,
+                  "roundIntervalMs": 20}
+            node = node_for_config({"gpuSwarm": gs})
+            w = HlsjsP2PWrapper(Engine)
+            hls = w.createPlayer({"startLevel": 0}, {"gpuSwarm": gs})
+            media = MediaElement()
+            hls.loadSource(origin.master_url())
+            hls.attachMedia(media)
+            hls.on(Hls.Events.MANIFEST_PARSED, lambda e, d: media.play())
+            tracks, offline_p2p = [], []
+            agent = node._agents[0]
+            agent.player.addEventListener("onTrackChange", lambda d: tracks.append(d["video"].level))
+            loop.set_timeout(lambda: setattr(hls, "nextLevel", 2), 8_000)
+            loop.set_timeout(lambda: setattr(hls, "nextLevel", 1), 20_000)
+            if r == 2:
+                def go_offline():
+                    node.set_online(False)
+                    offline_p2p.append(node.stats["p2p"])
+
+                def back_online():
+                    offline_p2p.append(node.stats["p2p"])
+                    node.set_online(True)
+                loop.set_timeout(go_offline, 6_000)
+                loop.set_timeout(back_online, 16_000)
+            ok = loop.run_until(lambda: media.currentTime > 44.0, timeout_ms=200_000)
+            out[r] = {"ok": ok, "tracks": tracks, "stats": dict(w.stats), "offline_p2p": offline_p2p,
+                      "agent_track": agent.currentTrack.level if agent.currentTrack else None}
+            node.close()
+        except BaseException as e:  # noqa: BLE001
+            errs.append(e)
+            hub.abort()
+
+    ts = [threading.Thread(target=peer, args=(r,)) for r in range(3)]
+    [t.start() for t in ts]
+    [t.join(300) for t in ts]
+    if errs:
+        primary = [e for e in errs if not isinstance(e, threading.BrokenBarrierError)]
+        raise (primary or errs)[0]
+    for r, o in out.items():
+        assert o["ok"], r
+        assert 2 in o["tracks"] and o["tracks"][-1] == 1 and o["agent_track"] == 1
+    assert sum(o["stats"]["p2p"] for o in out.values()) > 0
+    a, b = out[2]["offline_p2p"]
+    assert a == b  # masked offline: no P2P bytes received in that window
