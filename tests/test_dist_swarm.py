@@ -68,3 +68,62 @@ def test_two_process_gloo_swarm():
     assert out[0][1]["p2p"] + out[1][1]["p2p"] == total
     assert out[0][1]["peers"] == 1
     assert out[0][3] == pytest.approx(0.5)
+
+
+def _peer4(rank: int, world: int, port: int, q) -> None:
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world))
+    import torch.distributed as dist
+
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from hlsjs_p2p_wrapper_amd import Hls
+        from hlsjs_p2p_wrapper_amd.agent import node_for_config
+        from hlsjs_p2p_wrapper_amd.api.wrapper import HlsjsP2PWrapper
+        from hlsjs_p2p_wrapper_amd.net import new_event_loop
+        from hlsjs_p2p_wrapper_amd.net.origin import Rendition, SyntheticHlsOrigin
+        from hlsjs_p2p_wrapper_amd.player import MediaElement
+        from hlsjs_p2p_wrapper_amd.player.hls import Hls as Engine
+
+        loop = new_event_loop("virtual")
+        origin = SyntheticHlsOrigin("http://cdn.dist4/vod/", renditions=[Rendition(800_000, 640, 360),
+                                                                         Rendition(1_600_000, 960, 540)],
+                                    num_segments=8, encrypted=True, pin_memory=False)
+        cfg = {"gpuSwarm": {"backend": "dist", "device": "cpu", "cacheBytes": 64 << 20, "roundIntervalMs": 20}}
+        node = node_for_config(cfg)
+        w = HlsjsP2PWrapper(Engine)
+        hls = w.createPlayer({"startLevel": rank % 2}, cfg)
+        media = MediaElement()
+        start = 20_000 if rank == 3 else 0  # late joiner: served from the others' caches
+        loop.set_timeout(hls.loadSource, start, origin.master_url())
+        hls.attachMedia(media)
+        hls.on(Hls.Events.MANIFEST_PARSED, lambda e, d: media.play())
+        if rank == 2:  # churn: masked offline for a while
+            loop.set_timeout(node.set_online, 3_000, False)
+            loop.set_timeout(node.set_online, 12_000, True)
+        ok = loop.run_until(lambda: media.currentTime > 30.0, timeout_ms=400_000)
+        stats = dict(w.stats)
+        node.close()
+        q.put((rank, ok, stats, node.swarm_offload_ratio()))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.slow
+def test_four_process_gloo_swarm_with_churn_and_late_joiner():
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_peer4, args=(r, 4, port, q)) for r in range(4)]
+    for p in procs:
+        p.start()
+    out = {}
+    for _ in range(4):
+        rank, ok, stats, offload = q.get(timeout=400)
+        out[rank] = (ok, stats, offload)
+    for p in procs:
+        p.join(60)
+        assert p.exitcode == 0
+    assert all(v[0] for v in out.values())
+    assert out[3][1]["cdn"] == 0 or out[3][1]["p2p"] > 0  # the late joiner mostly rides the swarm
+    assert sum(v[1]["p2p"] for v in out.values()) > 0
+    assert 0 < out[0][2] < 1
