@@ -769,6 +769,18 @@ class SwarmNode:
             self.trace = TraceLog(maxlen)
         return self.trace
 
+    def save_cache(self, path: str) -> Dict[str, int]:
+        """Checkpoint the resident segments (SURVEY §5.4 warm restart; see checkpoint.py)."""
+        from .checkpoint import save_cache
+
+        return save_cache(self, path)
+
+    def load_cache(self, path: str) -> Dict[str, int]:
+        """Restore a checkpoint; restored segments are announced in the next round."""
+        from .checkpoint import load_cache
+
+        return load_cache(self, path)
+
     def set_link_bandwidth(self, peer: int, kbps: Optional[float]) -> None:
         """Fault injection (SURVEY §5.3 "slow link"): model the link from ``peer`` to this
         node at ``kbps`` kbit/s — segments received from it complete after their modelled

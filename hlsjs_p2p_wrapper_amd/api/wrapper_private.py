@@ -23,6 +23,7 @@ from ..integration.p2p_loader import p2p_loader_generator
 from ..integration.player_interface import PlayerInterface
 from ..models.media_map import MediaMap
 from ..models.segment_view import SegmentView
+from ..utils.js import truthy
 
 log = logging.getLogger("hlsjs_p2p_wrapper_amd.wrapper")
 
@@ -91,7 +92,7 @@ class HlsjsP2PWrapperPrivate:
     def startSession(self, hlsjs: Any, hlsjsConfig: Optional[Dict[str, Any]], p2pConfig: Any,
                      contentUrl: Optional[str]):
         Hlsjs = self.Hlsjs
-        if not p2pConfig or not isinstance(p2pConfig, dict):
+        if not truthy(p2pConfig) or not isinstance(p2pConfig, dict):  # JS: {} is a valid object
             raise Exception("p2pConfig must be a valid config object")
         mediaEngine = hlsjs or self.newMediaEngine(hlsjsConfig if hlsjsConfig is not None else {})
         self.createPeerAgent(p2pConfig, mediaEngine, Hlsjs.Events, contentUrl)
@@ -135,7 +136,7 @@ class HlsjsP2PWrapperPrivate:
         contentUrl = url or hlsjs.url
         if not contentUrl:
             raise Exception("Hls.js instance must have valid `url` property or `contentUrl` must be passed")
-        if not hlsEventsEnum:
+        if not truthy(hlsEventsEnum):
             raise Exception("Need valid Hls.js Events enumeration")
         hlsjs.on(hlsEventsEnum.ERROR, self.onMediaEngineError)
         playerBridge = PlayerInterface(hlsjs, hlsEventsEnum, self.onDispose)

@@ -300,6 +300,20 @@ PYBIND11_MODULE(_runtime, m) {
         return py::make_tuple(base, ids, offs);
       })
       .def("fits", &SegmentStore::fits)
+      .def("resident", [](const SegmentStore& s) {
+        // -> (ids int64[n], keys int64[n,4]) of resident entries, oldest first
+        std::vector<int64_t> ids;
+        s.resident_ids(&ids);
+        const int64_t n = static_cast<int64_t>(ids.size());
+        Arr<int64_t> id_arr(n), keys({n, int64_t(4)});
+        int64_t* k = keys.mutable_data();
+        for (int64_t i = 0; i < n; ++i) {
+          id_arr.mutable_data()[i] = ids[i];
+          const SegKey& key = s.entry(ids[i]).key;
+          k[4 * i] = key.swarm; k[4 * i + 1] = key.level; k[4 * i + 2] = key.url_id; k[4 * i + 3] = key.sn;
+        }
+        return py::make_tuple(id_arr, keys);
+      })
       .def("aligned", &SegmentStore::aligned)
       .def("commit", [](SegmentStore& s, Arr<int64_t> ids) {
         for (int64_t i = 0; i < ids.size(); ++i) s.commit(ids.data()[i]);

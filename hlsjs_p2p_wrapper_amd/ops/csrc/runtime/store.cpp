@@ -67,6 +67,17 @@ bool SegmentStore::make_room(int64_t start, int64_t len, bool wrapped) {
   return true;
 }
 
+void SegmentStore::resident_ids(std::vector<int64_t>* ids) const {
+  ids->clear();
+  for (const auto& fe : fifo_) {
+    const Entry& e = entries_[fe.first];
+    if (e.state != kResident || e.gen != fe.second) continue;
+    auto it = index_.find(e.key);
+    if (it == index_.end() || it->second != fe.first) continue;  // detached, replaced copy
+    ids->push_back(fe.first);
+  }
+}
+
 bool SegmentStore::fits(int64_t total) const {
   if (total <= 0) return true;
   if (total > capacity_) return false;

@@ -98,6 +98,9 @@ class SegmentStore {
   // Delta log since the last call.
   void take_delta(std::vector<SegKey>* added, std::vector<int64_t>* added_len, std::vector<SegKey>* removed);
   void all_resident(std::vector<SegKey>* keys, std::vector<int64_t>* lens) const;
+  // Resident entry ids, oldest first (allocation order: restoring them in this order keeps
+  // the eviction order of a checkpointed cache).
+  void resident_ids(std::vector<int64_t>* ids) const;
 
  private:
   int64_t new_entry();

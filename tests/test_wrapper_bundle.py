@@ -64,6 +64,13 @@ def test_start_session_and_create_peer_agent_errors():
     hls = w.newMediaEngine({})
     with pytest.raises(Exception, match="p2pConfig must be a valid config object"):
         w.startSession(hls, {}, None, "http://x")
+    for bad in ("", 0, "cfg", 5):  # JS `!p2pConfig || typeof p2pConfig !== 'object'`
+        with pytest.raises(Exception, match="p2pConfig must be a valid config object"):
+            w.startSession(hls, {}, bad, "http://x")
+    # ... but an EMPTY object is a valid config in JS ({} is truthy): no Python-falsy rejection
+    w2 = HlsjsP2PWrapperPrivate(Engine, PeerAgentMock)
+    assert w2.startSession(w2.newMediaEngine({}), {}, {}, "http://x") is not None
+    assert w2.hasSession()
     with pytest.raises(Exception, match="Hls.js instance must have valid `url` property"):
         w.createPeerAgent({}, hls, Engine.Events, None)
     with pytest.raises(Exception, match="Need valid Hls.js Events enumeration"):
