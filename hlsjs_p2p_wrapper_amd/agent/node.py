@@ -351,10 +351,10 @@ class SwarmNode:
                 keep.append((rel, ids))
         self._pins = keep
         # ---------------- 1. control plane
-        for agent in self._agents:  # agents plan their prefetch just before wants are sent
-            plan = getattr(agent, "plan_prefetch", None)
-            if plan is not None:
-                plan()
+        for agent in self._agents:  # agents plan (prefetch, live-window eviction) before wants go out
+            hook = getattr(agent, "before_round", None)
+            if hook is not None:
+                hook()
         wants, spec = [], []  # player requests first, then speculative (prefetch-only) wants
         cap = self.max_wants_per_round
         for k in list(self._wants):

@@ -56,6 +56,11 @@ class PeerAgent:
         self.prefetch_seconds = float(gs.get("prefetchSeconds", 0.0) or 0.0)
         self.prefetch_max = int(gs.get("prefetchMaxSegments", 8))
         self._prefetch_mark = None
+        # live streams: segments that slid out of the playlist window can no longer be
+        # requested -> evict them ("evict by sn < head - window")
+        self.live_evict = bool(gs.get("liveWindowEvict", True))
+        self._evicted_below = -1
+        self.evicted = 0
         self.disposed = False
         self._requests = []
         if playerInterface is not None and hasattr(playerInterface, "addEventListener"):
@@ -76,6 +81,36 @@ class PeerAgent:
 
     def setMediaElement(self, media: Any) -> None:
         self.media = media
+
+    def before_round(self) -> None:
+        """Node hook, run right before each round's wants are sent."""
+        if self.live_evict:
+            self.evict_live_window()
+        self.plan_prefetch()
+
+    def evict_live_window(self) -> int:
+        """Drop this content's cached segments older than every parsed level's live window."""
+        if self.disposed or self.player is None:
+            return 0
+        hls = getattr(self.player, "hls", None)
+        levels = getattr(hls, "levels", None) if hls is not None else None
+        if not levels:
+            return 0
+        first = []
+        for lv in levels:
+            d = getattr(lv, "details", None)
+            if d is None or not getattr(d, "live", False) or not d.fragments:
+                continue
+            first.append(int(d.fragments[0].sn))
+        if not first:
+            return 0
+        min_sn = min(first)
+        if min_sn <= self._evicted_below:
+            return 0
+        self._evicted_below = min_sn
+        n = int(self.node.store.evict_below(self.swarm_id, min_sn))
+        self.evicted += n
+        return n
 
     def plan_prefetch(self) -> None:
         """Called by the node right before each round's wants are sent: request the

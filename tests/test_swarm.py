@@ -284,3 +284,30 @@ def test_abr_ladder_track_switching_under_churn():
     assert sum(o["stats"]["p2p"] for o in out.values()) > 0
     a, b = out[2]["offline_p2p"]
     assert a == b  # masked offline: no P2P bytes received in that window
+
+
+def test_live_window_eviction():
+    # the live window slides with sn; segments that left the playlist can no
+    # longer be requested and are evicted from the cache (and the swarm is told)
+    from hlsjs_p2p_wrapper_amd.agent import SwarmNode
+
+    set_current_node(None)
+    loop = new_event_loop("virtual")
+    origin = SyntheticHlsOrigin("http://cdn.test/slide/", renditions=[Rendition(800_000, 640, 360)], live=True,
+                                window=5, num_segments=None, pool_size=8, encrypted=True, loop=loop)
+    node = SwarmNode(device="cpu", cache_bytes=256 << 20, loop=loop)
+    set_current_node(node)
+    w = HlsjsP2PWrapper(Engine)
+    hls = w.createPlayer({"liveSyncDurationCount": 2}, {})
+    media = MediaElement()
+    hls.loadSource(origin.master_url())
+    hls.attachMedia(media)
+    hls.on(Hls.Events.MANIFEST_PARSED, lambda e, d: media.play())
+    assert loop.run_until(lambda: media.currentTime > 60.0, timeout_ms=400_000)
+    agent = node._agents[0]
+    assert agent.evicted > 0
+    ids, keys = node.store.resident()
+    first = hls.levels[0].details.fragments[0].sn
+    assert len(keys) and keys[:, 3].min() >= agent._evicted_below and agent._evicted_below <= first
+    hls.destroy()
+    set_current_node(None)
