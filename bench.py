@@ -61,6 +61,9 @@ def parse():
     p.add_argument("--cache-gb", type=float, default=8.0, help="HBM segment-cache arena per GPU")
     p.add_argument("--no-dedup", action="store_true", help="disable CDN de-duplication (seeding)")
     p.add_argument("--cpu", action="store_true", help="CPU rehearsal (gloo, no GPU)")
+    p.add_argument("--dist-backend", default="auto", choices=["auto", "nccl", "gloo"],
+                   help="data-plane backend for N>1 (auto: nccl = RCCL on GPUs; gloo stages GPU "
+                        "tensors through host memory: multi-rank rehearsal on a single GPU)")
     p.add_argument("--sync-steps", action="store_true",
                    help="no software pipelining: each step = load, round, transmux, synchronously")
     p.add_argument("--no-gc-tune", action="store_true", help="keep Python's default GC settings")
@@ -75,15 +78,17 @@ def main() -> int:
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
     use_gpu = torch.cuda.is_available() and not args.cpu
     if use_gpu:
-        torch.cuda.set_device(local_rank)
-        device = torch.device("cuda", local_rank)
+        local_dev = local_rank % torch.cuda.device_count()  # rehearsals may share one GPU
+        torch.cuda.set_device(local_dev)
+        device = torch.device("cuda", local_dev)
     else:
         device = torch.device("cpu")
     import torch.distributed as dist
 
     if world > 1:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        dist.init_process_group("nccl" if use_gpu else "gloo", device_id=device if use_gpu else None)
+        backend = args.dist_backend if args.dist_backend != "auto" else ("nccl" if use_gpu else "gloo")
+        dist.init_process_group(backend, device_id=device if (use_gpu and backend == "nccl") else None)
 
     from hlsjs_p2p_wrapper_amd import Hls
     from hlsjs_p2p_wrapper_amd.agent import node_for_config
@@ -252,7 +257,8 @@ def main() -> int:
         "goodput_GBps": round(float(tot[0]) * seg_bytes / max_s / 1e9, 3),
         "errors": int(tot[4]),
         "config": {"model": desc, "global_batch": K * world, "seq_len": seg_bytes,
-                   "parallelism": f"swarm{world}" + ("-rccl" if (world > 1 and use_gpu) else ""),
+                   "parallelism": f"swarm{world}" + (f"-{'rccl' if dist.get_backend() == 'nccl' else 'gloo'}"
+                                                     if world > 1 else ""),
                    "inflight_per_gpu": K, "encrypted": encrypted, "segment_s": seg_dur,
                    "device": "MI355X" if use_gpu else "cpu"},
     }

@@ -48,6 +48,15 @@ std::vector<Transfer> plan_round(const Directory& dir, const std::vector<Want>& 
   std::vector<int64_t> link(size_t(world) * world, 0);  // bytes src->dst this round
   std::vector<int64_t> send_total(world, 0), cdn_total(world, 0);
   std::vector<Transfer> cdn, p2p;
+  // keys no peer holds yet but several ranks want: ONE rank fetches from the CDN and
+  // forwards in the same round ("seeding"); assigned after the pass (run-affine, below)
+  struct SeedGroup {
+    SegKey key;
+    size_t i, j;
+    std::vector<size_t> unserved;
+    uint64_t cands;  // wanting ranks that may upload
+  };
+  std::vector<SeedGroup> seeds;
 
   size_t i = 0;
   while (i < wants.size()) {
@@ -88,42 +97,73 @@ std::vector<Transfer> plan_round(const Directory& dir, const std::vector<Want>& 
       send_total[best] += size;
     }
     if (!unserved.empty()) {
-      int seeder = -1;
-      bool dedup = true;
+      bool dedup = unserved.size() > 1;
       for (size_t w : unserved) dedup = dedup && flag(wants[w].rank, kCdnDedup);
-      if (dedup && unserved.size() > 1) {
-        const uint64_t h = mix64((uint64_t(key.level) << 40) ^ (uint64_t(key.url_id) << 32) ^ key.sn ^
-                                 (uint64_t(key.swarm) << 48));
-        const size_t n = unserved.size();
-        for (size_t k = 0; k < n; ++k) {
-          const Want& cand = wants[unserved[(h + k) % n]];
-          if (!flag(cand.rank, kUploadOn)) continue;
-          if (seeder < 0 || cdn_total[cand.rank] < cdn_total[seeder]) seeder = cand.rank;
-        }
-      }
-      if (seeder < 0) {
+      uint64_t cands = 0;
+      if (dedup)
+        for (size_t w : unserved)
+          if (flag(wants[w].rank, kUploadOn)) cands |= uint64_t(1) << wants[w].rank;
+      if (cands) {
+        seeds.push_back({key, i, j, std::move(unserved), cands});  // seeder chosen below
+      } else {
         for (size_t w : unserved) {
           cdn.push_back({key, wants[w].size, -1, wants[w].rank, wants[w].want_id, 0});
           cdn_total[wants[w].rank] += wants[w].size;
         }
-      } else {
-        for (size_t w : unserved) {
-          const Want& wt = wants[w];
-          if (wt.rank == seeder) {
-            cdn.push_back({key, wt.size, -1, seeder, wt.want_id, 0});
-            cdn_total[seeder] += wt.size;
-          }
-        }
-        for (size_t w : unserved) {
-          const Want& wt = wants[w];
-          if (wt.rank == seeder) continue;
-          p2p.push_back({key, wt.size, seeder, wt.rank, wt.want_id, 1});
-          link[size_t(seeder) * world + wt.rank] += wt.size;
-          send_total[seeder] += wt.size;
-        }
       }
     }
     i = j;
+  }
+  // Seeder assignment, run-affine: consecutive keys (sorted: same track, ascending sn) go
+  // to the same rank until it holds its share of the round's seed bytes.  Load stays
+  // balanced, and each rank's CDN fetches form ONE contiguous sn run, i.e. one merged
+  // pinned-host -> HBM DMA instead of every world-th segment.
+  if (!seeds.empty()) {
+    int64_t seed_bytes = 0;
+    uint64_t all = 0;
+    for (const auto& g : seeds) {
+      seed_bytes += wants[g.unserved[0]].size;
+      all |= g.cands;
+    }
+    int nseed = 0;
+    for (int r = 0; r < world; ++r) nseed += int((all >> r) & 1u);
+    const int64_t quota = (seed_bytes + nseed - 1) / std::max(nseed, 1);
+    std::vector<int64_t> seeded(world, 0);
+    int cur = -1;
+    for (const auto& g : seeds) {
+      int seeder = -1;
+      if (cur >= 0 && ((g.cands >> cur) & 1u) && seeded[cur] < quota) seeder = cur;
+      if (seeder < 0) {  // next rank (in rank order) with room, else the least loaded
+        for (int k = 1; k <= world && seeder < 0; ++k) {
+          const int r = ((cur < 0 ? -1 : cur) + k + world) % world;
+          if (((g.cands >> r) & 1u) && seeded[r] < quota) seeder = r;
+        }
+        for (int r = 0; r < world && seeder < 0; ++r) {
+          if (!((g.cands >> r) & 1u)) continue;
+          int best = r;
+          for (int q = r + 1; q < world; ++q)
+            if (((g.cands >> q) & 1u) && seeded[q] < seeded[best]) best = q;
+          seeder = best;
+        }
+      }
+      cur = seeder;
+      const int64_t sz = wants[g.unserved[0]].size;
+      seeded[seeder] += sz;
+      for (size_t w : g.unserved) {
+        const Want& wt = wants[w];
+        if (wt.rank == seeder) {
+          cdn.push_back({g.key, wt.size, -1, seeder, wt.want_id, 0});
+          cdn_total[seeder] += wt.size;
+        }
+      }
+      for (size_t w : g.unserved) {
+        const Want& wt = wants[w];
+        if (wt.rank == seeder) continue;
+        p2p.push_back({g.key, wt.size, seeder, wt.rank, wt.want_id, 1});
+        link[size_t(seeder) * world + wt.rank] += wt.size;
+        send_total[seeder] += wt.size;
+      }
+    }
   }
   std::stable_sort(p2p.begin(), p2p.end(), [](const Transfer& a, const Transfer& b) {
     if (a.src != b.src) return a.src < b.src;

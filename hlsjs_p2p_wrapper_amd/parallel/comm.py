@@ -140,6 +140,7 @@ class DistComm(SwarmComm):
             control_group = dist.new_group(backend="gloo") if backend != "gloo" else None
         self.control_group = control_group
         self.data_group = data_group
+        self.data_backend = backend
         self._cap = 64  # int64 words per rank in the one-shot control all-gather
         if backend == "nccl" and torch.cuda.is_available():
             # batch_isend_irecv runs on the group's full communicator; when that is created
@@ -176,6 +177,9 @@ class DistComm(SwarmComm):
 
     def exchange(self, sends, recvs) -> None:
         dist = self.dist
+        if self.data_backend == "gloo" and any(t.is_cuda for _, t in list(sends) + list(recvs)):
+            self._exchange_staged(sends, recvs)
+            return
         ops = []
         for dst, t in sends:
             ops.append(dist.P2POp(dist.isend, t, dst, group=self.data_group))
@@ -186,6 +190,25 @@ class DistComm(SwarmComm):
         reqs = dist.batch_isend_irecv(ops)
         for r in reqs:
             r.wait()
+
+    def _exchange_staged(self, sends, recvs) -> None:
+        """gloo data plane with GPU tensors (several ranks sharing one GPU, e.g. rehearsing
+        the multi-rank path on a single MI355X): stage through host memory.  Synchronous
+        and slow by design; production multi-GPU runs use RCCL."""
+        dist = self.dist
+        torch.cuda.current_stream().synchronize()  # payloads/trailers are produced on this stream
+        ops, staged = [], []
+        for dst, t in sends:
+            ops.append(dist.P2POp(dist.isend, t.detach().to("cpu"), dst, group=self.data_group))
+        for src, t in recvs:
+            h = torch.empty(t.numel(), dtype=t.dtype)
+            staged.append((t, h))
+            ops.append(dist.P2POp(dist.irecv, h, src, group=self.data_group))
+        if ops:
+            for r in dist.batch_isend_irecv(ops):
+                r.wait()
+        for t, h in staged:
+            t.view(-1).copy_(h, non_blocking=False)
 
     def allreduce_sum(self, values: np.ndarray) -> np.ndarray:
         t = torch.from_numpy(np.asarray(values, dtype=np.int64).copy())

@@ -182,3 +182,18 @@ def test_mux_demux_roundtrip_and_pts(rt):
     buf[188 * 50] = 0
     r2 = tsdemux.demux_batch(buf, [0], [len(seg)], es, [0])
     assert r2.segment(0)["status"] & tsdemux.STATUS["bad_sync"]
+
+
+def test_planner_seeds_contiguous_runs(rt):
+    # 4 ranks want the same 64 fresh segments: each seeds ONE contiguous sn run of 16 (a
+    # single merged pinned-host -> HBM DMA per rank) and forwards it to the other three
+    d = rt.Directory()
+    rows = [(sn, 3_000_000, 1000 * r + sn, r, 0) for r in range(4) for sn in range(64)]
+    plan = rt.plan_round(d, wants(rows), flags(rt, 4), 4)
+    cdn = plan[plan[:, 5] == -1]
+    assert len(cdn) == 64
+    for r in range(4):
+        sns = sorted(int(x) for x in cdn[cdn[:, 6] == r][:, 3])
+        assert len(sns) == 16 and sns == list(range(sns[0], sns[0] + 16))
+    p2p = plan[plan[:, 5] >= 0]
+    assert len(p2p) == 64 * 3 and np.all(p2p[:, 8] == 1)
