@@ -1,0 +1,39 @@
+"""multi-rank runs on the GPU box.  The pool's box has ONE MI355X and RCCL
+cannot place two ranks on one GPU, so two torchrun ranks share the card with a gloo data
+plane (GPU tensors staged through host memory).  Everything else is the production N>1
+path of bench.py: control all-gather, native planning, CDN seeding + same-round
+forwarding, per-pair buffers with CRC trailers verified on device, async rounds, batched
+decrypt + demux, FRAG_BUFFERED accounting."""
+import json
+import os
+import socket
+import subprocess
+import sys
+from pathlib import Path
+
+import pytest
+
+REPO = Path(__file__).resolve().parents[1]
+
+
+def _free_port() -> int:
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+@pytest.mark.gpu
+def test_two_ranks_share_one_gpu_bench_path(cuda):
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2", "--master-addr",
+           "127.0.0.1", "--master-port", str(_free_port()), str(REPO / "bench.py"), "--gpus", "2", "--steps", "4",
+           "--warmup", "2", "--inflight", "16", "--pool", "16", "--cache-gb", "1", "--dist-backend", "gloo"]
+    env = dict(os.environ, PYTHONPATH=str(REPO))
+    p = subprocess.run(cmd, cwd=REPO, env=env, capture_output=True, text=True, timeout=420)
+    assert p.returncode == 0, p.stderr[-4000:]
+    line = [ln for ln in p.stdout.splitlines() if ln.startswith("{")][-1]
+    res = json.loads(line)
+    assert res["n_gpus"] == 2 and res["errors"] == 0
+    assert res["offload_ratio"] == pytest.approx(0.5, abs=0.02)  # every segment fetched once, shared once
+    assert res["value"] > 0 and res["config"]["parallelism"] == "swarm2-gloo"
