@@ -9,13 +9,15 @@
 //     v_mfma_i32_32x32x32_i8, 64 k-steps per 256-byte group (k = 2048 data bits)
 //
 // Layout choice (so no LDS transpose of the data is needed): lane l = (row r = l & 31,
-// half h = l >> 5) owns bytes [128h, 128h + 128) of group r and loads them with 8
-// dwordx4 loads; at k-step s it expands its 2 bytes (2s, 2s+1) into 16 int8 {0,1}
-// (nibble * 0x00204081 & 0x01010101: 3 VALU per 4 bits).  The B fragment for the same
-// 16 k's — W rows in exactly that (s, h, j) order — is precomputed on the host
-// (runtime/crc_host.cpp) in MFMA fragment order, 64 KiB, staged once per workgroup in LDS
-// and read with one ds_read_b128 per lane per step.  Because A and B use the same k
-// permutation the product is independent of the MFMA's internal k ordering.
+// half h = l >> 5) owns bytes [128h, 128h + 128) of group r and loads them as 8
+// dwordx4 chunks.  k-step s = 8q + jb feeds chunk q's 16 RAW bytes masked to bit jb
+// (one v_and per dword: values 2^jb, -128 as i8 for jb = 7) — no bit expansion.  The B
+// fragment of the same 16 k's is W scaled by 2^(7-jb) (-128 for jb = 0), so every nonzero
+// product is +-128 and the accumulator is 128 x (the GF(2) sum): the residue bit is bit 7.
+// Fragments are precomputed on the host (runtime/crc_host.cpp) in MFMA order, 64 KiB,
+// staged once per workgroup in LDS and read with one ds_read_b128 per lane per step.
+// Because A and B use the same k permutation the product is independent of the MFMA's
+// internal k ordering.
 //
 // The 16 accumulator registers hold rows (i&3)+8(i>>2)+4h, column = lane&31 (gfx950 C/D
 // map); a wave ballot of the parity bits yields two 32-bit group residues per register.
@@ -37,8 +39,6 @@ constexpr int kCrcThreads = 512;
 constexpr int kTileBytes = 32 * 256;
 constexpr int kNumP = 40;
 constexpr int kSlice = 1024;  // u32 per byte-slice table set
-
-__device__ __forceinline__ uint32_t expand_nibble(uint32_t nib) { return (nib * 0x00204081u) & 0x01010101u; }
 
 // 16 bytes at byte offset `o` of a segment of `len` bytes, zero beyond the end (last group).
 __device__ __forceinline__ uint4 load_tail(const uint8_t* __restrict__ buf, int64_t base, int64_t o, int64_t len) {
@@ -86,34 +86,44 @@ __global__ __launch_bounds__(kCrcThreads) void crc32_group_residue_kernel(
     const int64_t my = tile * kTileBytes + r * 256 + h * 128;  // byte offset of this lane's 128 B
     const bool full = my + 128 <= len;
     const uint4* p = reinterpret_cast<const uint4*>(buf + base + my);
-    // 16-byte chunks streamed with one chunk of prefetch: 8 VGPRs of data live instead of
-    // 32, so the 64-step MFMA loop fits without spilling.
-    uint4 cur = full ? p[0] : load_tail(buf, base, my, len);
+    // The lane's whole 128 bytes are loaded up front (8 x dwordx4 in flight per lane, 8 KB
+    // per wave): the kernel is bound by memory-level parallelism, not by the MFMAs (one
+    // chunk of prefetch held ~1 KB per wave in flight: ~2 TB/s chip-wide).
+    uint4 c0, c1, c2, c3, c4, c5, c6, c7;
+    if (full) {
+      c0 = p[0]; c1 = p[1]; c2 = p[2]; c3 = p[3]; c4 = p[4]; c5 = p[5]; c6 = p[6]; c7 = p[7];
+    } else {
+      c0 = load_tail(buf, base, my, len);       c1 = load_tail(buf, base, my + 16, len);
+      c2 = load_tail(buf, base, my + 32, len);  c3 = load_tail(buf, base, my + 48, len);
+      c4 = load_tail(buf, base, my + 64, len);  c5 = load_tail(buf, base, my + 80, len);
+      c6 = load_tail(buf, base, my + 96, len);  c7 = load_tail(buf, base, my + 112, len);
+    }
     v16i acc = {};
+    // not unrolled (an unrolled q loop hoists all 64 B fragments into registers); the chunk
+    // registers rotate instead of being indexed, so nothing goes to scratch
 #pragma unroll 1
     for (int q = 0; q < 8; ++q) {
-      uint4 nxt = cur;
-      if (q < 7) nxt = full ? p[q + 1] : load_tail(buf, base, my + 16 * (q + 1), len);
-      const uint32_t w4[4] = {cur.x, cur.y, cur.z, cur.w};
+      // 8 MFMAs per 16-byte chunk, one per bit position jb: A = the raw bytes masked to
+      // bit jb (4 v_and), B pre-scaled by 2^(7-jb) on the host, so each nonzero product is
+      // +-128 and the GF(2) sum lands in bit 7 of the accumulator
 #pragma unroll
-      for (int k = 0; k < 8; ++k) {
-        const int s = 8 * q + k;
-        const uint32_t bits = (w4[k >> 1] >> (16 * (k & 1))) & 0xffffu;
+      for (int jb = 0; jb < 8; ++jb) {
+        const uint32_t m = 0x01010101u << jb;
         v4i a;
-        a.x = static_cast<int>(expand_nibble(bits & 0xf));
-        a.y = static_cast<int>(expand_nibble((bits >> 4) & 0xf));
-        a.z = static_cast<int>(expand_nibble((bits >> 8) & 0xf));
-        a.w = static_cast<int>(expand_nibble(bits >> 12));
-        const v4i b = s_w[s * 64 + lane];
+        a.x = static_cast<int>(c0.x & m);
+        a.y = static_cast<int>(c0.y & m);
+        a.z = static_cast<int>(c0.z & m);
+        a.w = static_cast<int>(c0.w & m);
+        const v4i b = s_w[(8 * q + jb) * 64 + lane];
         acc = __builtin_amdgcn_mfma_i32_32x32x32_i8(a, b, acc, 0, 0, 0);
       }
-      cur = nxt;
+      c0 = c1; c1 = c2; c2 = c3; c3 = c4; c4 = c5; c5 = c6; c6 = c7;
     }
     const int64_t groups = (len + 255) >> 8;
     const int64_t g0 = tile * 32;
 #pragma unroll
     for (int i = 0; i < 16; ++i) {
-      const uint64_t m = __ballot(acc[i] & 1);
+      const uint64_t m = __ballot(acc[i] & 0x80);  // 128 x GF(2) sum: parity is bit 7
       const int row = (i & 3) + 8 * (i >> 2);
       if (lane == 0) {
         if (g0 + row < groups) residues[roff + g0 + row] = static_cast<uint32_t>(m);

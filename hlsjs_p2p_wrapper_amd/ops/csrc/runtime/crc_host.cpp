@@ -121,18 +121,23 @@ std::vector<int8_t> mfma_group_weights() {
       r = (r >> 8) ^ T.t[0][r & 0xff];  // one more zero byte after it
     }
   }
-  // Fragment order: lane l (r = l & 31 = CRC bit column, h = l >> 5) at step s holds
-  // B[k][r] for its 16 k's; k(s, h, j) <-> group byte 128h + 2s + (j >> 3), bit j & 7.
+  // Fragment order: lane l (col = l & 31 = CRC bit column, h = l >> 5) at step s = 8q + jb
+  // holds B[k][col] for its 16 k's; k(s, h, e) <-> group byte 128h + 16q + e, bit jb.
+  // The kernel feeds RAW data bytes masked to bit jb (value 2^jb; -128 as i8 for jb = 7),
+  // so B is scaled by 2^(7-jb) (-128 for jb = 0): every nonzero product is +-128 and the
+  // accumulator is 128 x (the GF(2) sum) -> the residue bit is bit 7 of the accumulator.
   std::vector<int8_t> w(64 * 64 * 16);
-  for (int s = 0; s < 64; ++s)
+  for (int s = 0; s < 64; ++s) {
+    const int q = s >> 3, jb = s & 7;
+    const int scale = jb == 0 ? -128 : (1 << (7 - jb));
     for (int lane = 0; lane < 64; ++lane) {
       int col = lane & 31, h = lane >> 5;
-      for (int j = 0; j < 16; ++j) {
-        int byte = 128 * h + 2 * s + (j >> 3);
-        int bit = j & 7;
-        w[(s * 64 + lane) * 16 + j] = static_cast<int8_t>((v[byte][bit] >> col) & 1u);
+      for (int e = 0; e < 16; ++e) {
+        int byte = 128 * h + 16 * q + e;
+        w[(s * 64 + lane) * 16 + e] = static_cast<int8_t>(((v[byte][jb] >> col) & 1u) ? scale : 0);
       }
     }
+  }
   return w;
 }
 

@@ -16,21 +16,23 @@ def _emulate(data: bytes, w: np.ndarray, tab: np.ndarray) -> int:
     G = (n + 255) // 256
     buf = np.zeros(G * 256, np.uint8)
     buf[:n] = np.frombuffer(data, np.uint8)
-    # W as a [k][col] matrix in the kernel's (s, h, j) k-order: fragments [s][lane][j]
-    wf = w.reshape(64, 64, 16)
+    # W fragments [s][lane][e] in the kernel's order: s = 8q + jb, element e = byte
+    # 128h + 16q + e of the group masked to bit jb (i8 value 2^jb, -128 for jb = 7)
+    wf = w.reshape(64, 64, 16).astype(np.int64)
     residues = []
     for g in range(G):
         grp = buf[g * 256:(g + 1) * 256]
         acc = np.zeros(32, np.int64)
         for s in range(64):
+            q, jb = s >> 3, s & 7
             for h in range(2):
-                bits16 = int(grp[128 * h + 2 * s]) | (int(grp[128 * h + 2 * s + 1]) << 8)
-                a = np.array([(bits16 >> j) & 1 for j in range(16)], np.int64)
+                chunk = grp[128 * h + 16 * q:128 * h + 16 * q + 16].astype(np.int64) & (1 << jb)
+                a = np.where(chunk >= 128, chunk - 256, chunk)  # signed i8
                 for col in range(32):
-                    acc[col] += int((a * wf[s, col + 32 * h, :].astype(np.int64)).sum())
+                    acc[col] += int((a * wf[s, col + 32 * h, :]).sum())
         r = 0
         for col in range(32):
-            r |= (int(acc[col]) & 1) << col
+            r |= ((int(acc[col]) >> 7) & 1) << col
         residues.append(r)
     raw = 0
     for r in residues:  # Horner with P_8 = one 256-byte group
@@ -49,7 +51,7 @@ def _emulate(data: bytes, w: np.ndarray, tab: np.ndarray) -> int:
 def test_mfma_crc_formulation_matches_zlib(rt):
     w = rt.crc_mfma_weights()
     tab = rt.crc_shift_tables()
-    assert w.shape == (65536,) and set(np.unique(w)) <= {0, 1}
+    assert w.shape == (65536,) and set(np.unique(w)) <= {0, 1, 2, 4, 8, 16, 32, 64, -128}
     rng = np.random.default_rng(1)
     for n in (1, 3, 255, 256, 300, 700):
         data = rng.integers(0, 256, n, dtype=np.uint8).tobytes()
