@@ -11,7 +11,7 @@ Round keys (equivalent inverse cipher) are expanded once per key on the host and
 from __future__ import annotations
 
 import threading
-from typing import Dict, List, Optional, Sequence
+from typing import Dict, Optional, Sequence
 
 import numpy as np
 import torch

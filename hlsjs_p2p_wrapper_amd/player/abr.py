@@ -12,7 +12,7 @@ estimate being the min of the two — hls.js's ``EwmaBandWidthEstimator``.
 from __future__ import annotations
 
 import math
-from typing import Any, Optional
+from typing import Any
 
 from ..net.event_loop import get_event_loop
 from .events import Events

@@ -17,12 +17,10 @@ import bisect
 import logging
 from typing import Any, Dict, List, Optional, Tuple
 
-from ..net.event_loop import get_event_loop
-from ..utils.events import JsObject
 from .events import ErrorDetails, ErrorTypes, Events
 from .level import Fragment, Level, LevelDetails
 from .playlist import PlaylistError, is_master, parse_master, parse_media
-from .transmux import TransmuxJob, default_transmux_device, pipeline_for
+from .transmux import TransmuxJob, pipeline_for
 
 log = logging.getLogger("hlsjs_p2p_wrapper_amd.player")
 

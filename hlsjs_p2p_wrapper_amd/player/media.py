@@ -17,7 +17,7 @@ browser tests assert on ``currentTime``, ``timeupdate`` and ``seeked``
 """
 from __future__ import annotations
 
-from typing import Any, Callable, Dict, List, Optional, Tuple
+from typing import Any, Callable, List, Optional, Tuple
 
 from ..net.event_loop import get_event_loop
 from ..utils.events import EventEmitter

@@ -1,7 +1,6 @@
 """Warm restart of the HBM segment cache: a node checkpoints what it played,
 a fresh node restores it (CRC re-verified, eviction order kept) and its player is then
 served entirely from the restored cache.  Safetensors only: loading executes nothing."""
-import numpy as np
 import pytest
 import torch
 

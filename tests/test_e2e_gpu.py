@@ -3,7 +3,6 @@ swarm on one GPU (HBM->HBM transfers), and the smoke entry point.  All ``gpu``."
 import threading
 
 import pytest
-import torch
 
 from hlsjs_p2p_wrapper_amd import Hls
 from hlsjs_p2p_wrapper_amd.agent import current_node, node_for_config, set_current_node

@@ -1,7 +1,6 @@
 """Native host runtime: ring-allocated segment store, swarm directory + deterministic
 exchange planner, AES known-answer vectors, TS mux/demux oracle."""
 import numpy as np
-import pytest
 
 from hlsjs_p2p_wrapper_amd.ops import aes
 

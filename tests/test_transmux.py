@@ -2,7 +2,6 @@
 fragment's result — status, info row, plaintext length, video/audio/id3 ES views — matches
 the per-segment host oracle, for a mixed batch (encrypted + clear, varied sizes, one bad
 key) staged from host payloads.  Runs on CPU (host kernels) and on the GPU (HIP kernels)."""
-import numpy as np
 import pytest
 import torch
 
