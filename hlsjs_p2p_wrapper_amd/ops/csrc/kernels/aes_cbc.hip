@@ -119,13 +119,25 @@ __global__ __launch_bounds__(kAesThreads, 1) void aes128_cbc_decrypt_kernel(
     int64_t total_chunks, int64_t per_wg) {
   __shared__ uint32_t s_tab[kTdDwords + kIsDwords];  // 160 KiB (layout above)
   const int tid = threadIdx.x;
-  for (int i = tid; i < kTdDwords; i += kAesThreads) {
-    const int region = i >> 14, rem = i & 16383, row = rem >> 6, half = (rem >> 5) & 1;
-    const uint32_t v = tdl_g[row];
-    const int rot = 8 * (2 * region + half);
-    s_tab[i] = rot ? __builtin_amdgcn_alignbit(v, v, 32 - rot) : v;
+  {  // image fill: thread tid writes dwords tid + 1024k, i.e. Td rows (tid >> 6) + 16(k & 15) in region
+     // k >> 4 and InvSbox rows (tid >> 5) + 32k; all 24 source loads are issued before the
+     // first LDS store (a strided load/store loop paid ~40 serialised L2 round trips)
+    static_assert(kAesThreads == 1024 && kTdDwords == 32 * kAesThreads && kIsDwords == 8 * kAesThreads, "fill map");
+    uint32_t td[16], is[8];
+#pragma unroll
+    for (int k = 0; k < 16; ++k) td[k] = tdl_g[(tid >> 6) + 16 * k];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) is[k] = isb_g[(tid >> 5) + 32 * k];
+    const int half = (tid >> 5) & 1;
+#pragma unroll
+    for (int k = 0; k < 32; ++k) {
+      const uint32_t v = td[k & 15];
+      const int rot = 8 * (2 * (k >> 4) + half);
+      s_tab[tid + k * kAesThreads] = rot ? __builtin_amdgcn_alignbit(v, v, 32 - rot) : v;
+    }
+#pragma unroll
+    for (int k = 0; k < 8; ++k) s_tab[kTdDwords + tid + k * kAesThreads] = is[k];
   }
-  for (int i = tid; i < kIsDwords; i += kAesThreads) s_tab[kTdDwords + i] = static_cast<uint32_t>(isb_g[i >> 5]);
   __syncthreads();
   const uint8_t* s_bytes = reinterpret_cast<const uint8_t*>(s_tab);
   const uint32_t l4 = static_cast<uint32_t>(tid & 31) << 2;
@@ -143,8 +155,8 @@ __global__ __launch_bounds__(kAesThreads, 1) void aes128_cbc_decrypt_kernel(
   int64_t so = 0, dof = 0, cstart = 0, cend = 0, nblk = 0;
   for (int64_t ch = uniform64(begin + (tid >> 6)); ch < end; ch += kWaves) {
     if (cur < 0 || ch >= cend) {
-      cur = __builtin_amdgcn_readfirstlane(cur < 0 ? find_seg(chunk_prefix, nseg, ch)
-                                                   : advance_seg(chunk_prefix, cur, ch));
+      cur = cur < 0 ? find_seg_wave(chunk_prefix, nseg, ch)  // whole wave active: ch is uniform
+                    : __builtin_amdgcn_readfirstlane(advance_seg(chunk_prefix, cur, ch));
 #pragma unroll
       for (int k = 0; k < 44; ++k) rk[k] = drk[cur * 44 + k];
       so = src_off[cur];

@@ -40,20 +40,21 @@ constexpr int kTileBytes = 32 * 256;
 constexpr int kNumP = 40;
 constexpr int kSlice = 1024;  // u32 per byte-slice table set
 
-// 16 bytes at byte offset `o` of a segment of `len` bytes, zero beyond the end (last group).
+// 16 bytes at byte offset `o` of a segment of `len` > 0 bytes, zero beyond the end (last
+// tile).  Segment starts are 16-byte aligned, so the aligned 16-byte chunk holding a
+// segment's last byte never crosses a page: load it whole and mask; chunks entirely past
+// the end re-read the segment's first chunk and mask it to zero (no branches, no scratch).
+__device__ __forceinline__ uint32_t keep_mask(int64_t rem) {
+  return rem >= 4 ? 0xFFFFFFFFu : rem <= 0 ? 0u : (1u << (8 * rem)) - 1u;
+}
 __device__ __forceinline__ uint4 load_tail(const uint8_t* __restrict__ buf, int64_t base, int64_t o, int64_t len) {
-  uint32_t w[4];
-#pragma unroll
-  for (int q = 0; q < 4; ++q) {
-    uint32_t v = 0;
-#pragma unroll
-    for (int b = 0; b < 4; ++b) {
-      const int64_t i = o + 4 * q + b;
-      v |= (i < len ? static_cast<uint32_t>(buf[base + i]) : 0u) << (8 * b);
-    }
-    w[q] = v;
-  }
-  return make_uint4(w[0], w[1], w[2], w[3]);
+  const int64_t rem = len - o;
+  uint4 v = *reinterpret_cast<const uint4*>(buf + base + (rem > 0 ? o : 0));
+  v.x &= keep_mask(rem);
+  v.y &= keep_mask(rem - 4);
+  v.z &= keep_mask(rem - 8);
+  v.w &= keep_mask(rem - 12);
+  return v;
 }
 
 __global__ __launch_bounds__(kCrcThreads) void crc32_group_residue_kernel(
@@ -62,7 +63,7 @@ __global__ __launch_bounds__(kCrcThreads) void crc32_group_residue_kernel(
     uint32_t* __restrict__ residues, int nseg, int64_t total_tiles, int64_t tiles_per_wave) {
   __shared__ v4i s_w[64 * 64];  // 64 KiB: [step][lane] fragments
   const int tid = threadIdx.x;
-  for (int i = tid; i < 64 * 64; i += kCrcThreads) s_w[i] = wfrag[i];
+  lds_fill<64 * 64 / kCrcThreads>(s_w, wfrag, 64 * 64, tid, kCrcThreads);
   __syncthreads();
 
   const int lane = tid & 63;
@@ -71,32 +72,41 @@ __global__ __launch_bounds__(kCrcThreads) void crc32_group_residue_kernel(
   const int64_t gwave = static_cast<int64_t>(blockIdx.x) * (kCrcThreads / 64) + wave;
   const int64_t t_begin = gwave * tiles_per_wave;
   const int64_t t_end = t_begin + tiles_per_wave < total_tiles ? t_begin + tiles_per_wave : total_tiles;
-  int seg = -1;
-  int64_t base = 0, len = 0, tstart = 0, tend = 0, roff = 0;
-  for (int64_t t = t_begin; t < t_end; ++t) {
-    if (seg < 0 || t >= tend) {
-      seg = seg < 0 ? find_seg(tile_prefix, nseg, t) : advance_seg(tile_prefix, seg, t);
-      base = seg_off[seg];
-      len = seg_len[seg];
-      tstart = tile_prefix[seg];
-      tend = tile_prefix[seg + 1];
-      roff = res_off[seg];
-    }
-    const int64_t tile = t - tstart;
+  if (t_begin >= t_end) return;
+  // Software pipeline over the wave's tiles: the lane's 128 bytes of tile t+1 (8 x dwordx4,
+  // 8 KB per wave) are in flight while tile t's 64 MFMAs run.  Without it every tile paid a
+  // full HBM round trip before its MFMAs (~2.5 TB/s chip-wide).
+  int seg = find_seg_wave(tile_prefix, nseg, t_begin);
+  int64_t base = seg_off[seg], len = seg_len[seg], tstart = tile_prefix[seg], tend = tile_prefix[seg + 1];
+  int64_t roff = res_off[seg];
+  uint4 n0, n1, n2, n3, n4, n5, n6, n7;  // the next tile's chunks
+  auto load_tile = [&](int64_t tile) {
     const int64_t my = tile * kTileBytes + r * 256 + h * 128;  // byte offset of this lane's 128 B
-    const bool full = my + 128 <= len;
-    const uint4* p = reinterpret_cast<const uint4*>(buf + base + my);
-    // The lane's whole 128 bytes are loaded up front (8 x dwordx4 in flight per lane, 8 KB
-    // per wave): the kernel is bound by memory-level parallelism, not by the MFMAs (one
-    // chunk of prefetch held ~1 KB per wave in flight: ~2 TB/s chip-wide).
-    uint4 c0, c1, c2, c3, c4, c5, c6, c7;
-    if (full) {
-      c0 = p[0]; c1 = p[1]; c2 = p[2]; c3 = p[3]; c4 = p[4]; c5 = p[5]; c6 = p[6]; c7 = p[7];
+    if ((tile + 1) * kTileBytes <= len) {  // wave-uniform: only a segment's last tile is partial
+      const uint4* p = reinterpret_cast<const uint4*>(buf + base + my);
+      n0 = p[0]; n1 = p[1]; n2 = p[2]; n3 = p[3]; n4 = p[4]; n5 = p[5]; n6 = p[6]; n7 = p[7];
     } else {
-      c0 = load_tail(buf, base, my, len);       c1 = load_tail(buf, base, my + 16, len);
-      c2 = load_tail(buf, base, my + 32, len);  c3 = load_tail(buf, base, my + 48, len);
-      c4 = load_tail(buf, base, my + 64, len);  c5 = load_tail(buf, base, my + 80, len);
-      c6 = load_tail(buf, base, my + 96, len);  c7 = load_tail(buf, base, my + 112, len);
+      n0 = load_tail(buf, base, my, len);       n1 = load_tail(buf, base, my + 16, len);
+      n2 = load_tail(buf, base, my + 32, len);  n3 = load_tail(buf, base, my + 48, len);
+      n4 = load_tail(buf, base, my + 64, len);  n5 = load_tail(buf, base, my + 80, len);
+      n6 = load_tail(buf, base, my + 96, len);  n7 = load_tail(buf, base, my + 112, len);
+    }
+  };
+  load_tile(t_begin - tstart);
+  for (int64_t t = t_begin; t < t_end; ++t) {
+    uint4 c0 = n0, c1 = n1, c2 = n2, c3 = n3, c4 = n4, c5 = n5, c6 = n6, c7 = n7;
+    const int64_t tile = t - tstart;
+    const int64_t c_len = len, c_roff = roff;
+    if (t + 1 < t_end) {
+      if (t + 1 >= tend) {
+        seg = advance_seg(tile_prefix, seg, t + 1);
+        base = seg_off[seg];
+        len = seg_len[seg];
+        tstart = tile_prefix[seg];
+        tend = tile_prefix[seg + 1];
+        roff = res_off[seg];
+      }
+      load_tile(t + 1 - tstart);
     }
     v16i acc = {};
     // not unrolled (an unrolled q loop hoists all 64 B fragments into registers); the chunk
@@ -119,15 +129,15 @@ __global__ __launch_bounds__(kCrcThreads) void crc32_group_residue_kernel(
       }
       c0 = c1; c1 = c2; c2 = c3; c3 = c4; c4 = c5; c5 = c6; c6 = c7;
     }
-    const int64_t groups = (len + 255) >> 8;
+    const int64_t groups = (c_len + 255) >> 8;
     const int64_t g0 = tile * 32;
 #pragma unroll
     for (int i = 0; i < 16; ++i) {
       const uint64_t m = __ballot(acc[i] & 0x80);  // 128 x GF(2) sum: parity is bit 7
       const int row = (i & 3) + 8 * (i >> 2);
       if (lane == 0) {
-        if (g0 + row < groups) residues[roff + g0 + row] = static_cast<uint32_t>(m);
-        if (g0 + row + 4 < groups) residues[roff + g0 + row + 4] = static_cast<uint32_t>(m >> 32);
+        if (g0 + row < groups) residues[c_roff + g0 + row] = static_cast<uint32_t>(m);
+        if (g0 + row + 4 < groups) residues[c_roff + g0 + row + 4] = static_cast<uint32_t>(m >> 32);
       }
     }
   }
@@ -139,13 +149,20 @@ __device__ __forceinline__ uint32_t apply_tab(const uint32_t* __restrict__ t, ui
 
 constexpr int kCombineThreads = 1024;
 constexpr int kCombineLdsTables = 15;  // P_8 .. P_22
+constexpr int kNumQ = 8;               // Q_b = A^(-8 * 2^b): pad removal
+// Residue of the 256-byte group [FF FF FF FF 00 .. 00]: for n >= 4 the zlib init value
+// 0xFFFFFFFF equals XOR-ing FF into the message's first 4 bytes, so it folds into group 0's
+// residue (= zlib(FF^4 0^252) ^ zlib(0^256)) instead of a 20-step chain of dependent
+// global table lookups on one thread after the tree (that tail was most of the kernel).
+constexpr uint32_t kInitFold = 0xf2697aa7u;
 
 // One workgroup per segment.  tables: P_0..P_39 then Q_0..Q_7 (each kSlice u32).
 __global__ __launch_bounds__(kCombineThreads) void crc32_combine_kernel(
     const uint32_t* __restrict__ residues, const int64_t* __restrict__ res_off, const int64_t* __restrict__ seg_len,
     const uint32_t* __restrict__ tables, uint32_t* __restrict__ crc_out, const uint32_t* __restrict__ expect,
     uint8_t* __restrict__ ok_out) {
-  __shared__ uint32_t s_tab[kCombineLdsTables * kSlice];  // 60 KiB
+  __shared__ __attribute__((aligned(16))) uint32_t s_tab[kCombineLdsTables * kSlice];  // 60 KiB
+  __shared__ __attribute__((aligned(16))) uint32_t s_q[kNumQ * kSlice];                // 32 KiB
   __shared__ uint32_t s_acc[kCombineThreads];
   const int seg = blockIdx.x;
   const int tid = threadIdx.x;
@@ -155,17 +172,37 @@ __global__ __launch_bounds__(kCombineThreads) void crc32_combine_kernel(
   int lgL = 0;
   while ((static_cast<int64_t>(kCombineThreads) << lgL) < G) ++lgL;
   const int lds_tables = 1 + lgL + 10 <= kCombineLdsTables ? 1 + lgL + 10 : kCombineLdsTables;
-  for (int i = tid; i < lds_tables * kSlice; i += kCombineThreads) s_tab[i] = tables[8 * kSlice + i];
+  lds_fill<kCombineLdsTables * kSlice / 4 / kCombineThreads + 1>(
+      reinterpret_cast<uint4*>(s_tab), reinterpret_cast<const uint4*>(tables + 8 * kSlice), lds_tables * kSlice / 4,
+      tid, kCombineThreads);
+  lds_fill<kNumQ * kSlice / 4 / kCombineThreads>(reinterpret_cast<uint4*>(s_q),
+                                                  reinterpret_cast<const uint4*>(tables + kNumP * kSlice),
+                                                  kNumQ * kSlice / 4, tid, kCombineThreads);
   __syncthreads();
   const int64_t L = int64_t(1) << lgL;
   const int64_t span = L * kCombineThreads;
   const int64_t front = span - G;  // virtual zero groups in front
   const uint32_t* __restrict__ res = residues + res_off[seg];
+  const uint32_t fold0 = n >= 4 ? kInitFold : 0u;
   uint32_t acc = 0;
   const uint32_t* p8 = s_tab;  // A^(8*256): one group
-  for (int64_t k = 0; k < L; ++k) {
-    const int64_t g = static_cast<int64_t>(tid) * L + k - front;
-    acc = apply_tab(p8, acc) ^ (g >= 0 ? res[g] : 0u);
+  // Horner over this thread's run of L groups, 8 residues loaded ahead per step (a
+  // load-per-iteration loop paid one global round trip per group: L of them in series)
+  constexpr int kAhead = 8;
+  for (int64_t k0 = 0; k0 < L; k0 += kAhead) {
+    uint32_t rv[kAhead];
+#pragma unroll
+    for (int j = 0; j < kAhead; ++j) {
+      const int64_t g = static_cast<int64_t>(tid) * L + k0 + j - front;
+      rv[j] = (k0 + j < L && g >= 0) ? res[g] : 0u;
+    }
+#pragma unroll
+    for (int j = 0; j < kAhead; ++j) {
+      if (k0 + j < L) {
+        const int64_t g = static_cast<int64_t>(tid) * L + k0 + j - front;
+        acc = apply_tab(p8, acc) ^ rv[j] ^ (g == 0 ? fold0 : 0u);
+      }
+    }
   }
   s_acc[tid] = acc;
   __syncthreads();
@@ -182,11 +219,14 @@ __global__ __launch_bounds__(kCombineThreads) void crc32_combine_kernel(
   if (tid == 0) {
     uint32_t raw = s_acc[0];
     const int64_t pad = G * 256 - n;
-    for (int b = 0; b < 8; ++b)
-      if ((pad >> b) & 1) raw = apply_tab(tables + static_cast<int64_t>(kNumP + b) * kSlice, raw);
-    uint32_t init = 0xFFFFFFFFu;
-    for (int b = 0; b < kNumP; ++b)
-      if ((n >> b) & 1) init = apply_tab(tables + static_cast<int64_t>(b) * kSlice, init);
+    for (int b = 0; b < kNumQ; ++b)
+      if ((pad >> b) & 1) raw = apply_tab(s_q + b * kSlice, raw);
+    uint32_t init = 0;  // folded into group 0 (n >= 4)
+    if (n < 4) {
+      init = 0xFFFFFFFFu;
+      for (int b = 0; b < 2; ++b)
+        if ((n >> b) & 1) init = apply_tab(tables + static_cast<int64_t>(b) * kSlice, init);
+    }
     const uint32_t crc = raw ^ init ^ 0xFFFFFFFFu;
     crc_out[seg] = crc;
     if (ok_out) ok_out[seg] = (expect && expect[seg] == crc) ? 1 : 0;

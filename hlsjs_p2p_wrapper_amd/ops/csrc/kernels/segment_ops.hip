@@ -141,7 +141,7 @@ __global__ __launch_bounds__(kCopyThreads) void segment_copy_kernel(
     const int64_t* __restrict__ dst_off, const int64_t* __restrict__ len, const int64_t* __restrict__ chunk_prefix,
     int ncopy) {
   const int64_t gchunk = blockIdx.x;
-  const int c = find_seg(chunk_prefix, ncopy, gchunk);
+  const int c = find_seg_wave(chunk_prefix, ncopy, gchunk);
   const int64_t chunk = gchunk - chunk_prefix[c];
   const int64_t n = len[c];
   const int64_t beg = chunk * kCopyChunk;
@@ -152,8 +152,24 @@ __global__ __launch_bounds__(kCopyThreads) void segment_copy_kernel(
   int64_t i = beg;
   if (vec) {
     const int64_t vend = beg + ((end - beg) & ~int64_t(15));
-    for (int64_t o = beg + 16 * threadIdx.x; o < vend; o += 16 * kCopyThreads)
-      *reinterpret_cast<uint4*>(d + o) = *reinterpret_cast<const uint4*>(s + o);
+    // 8 x 16 B per lane in flight per step (a load/store-per-iteration loop waited one HBM
+    // round trip per 16 B); tail lanes re-copy the last vector (unconditional stores keep
+    // the loads from being sunk next to guarded stores)
+    constexpr int kUnroll = 8;
+    const int64_t last = vend - 16;
+    for (int64_t o0 = beg + 16 * threadIdx.x; o0 < vend; o0 += 16 * kCopyThreads * kUnroll) {
+      uint4 v[kUnroll];
+#pragma unroll
+      for (int u = 0; u < kUnroll; ++u) {
+        const int64_t o = o0 + 16 * kCopyThreads * u;
+        v[u] = *reinterpret_cast<const uint4*>(s + (o < last ? o : last));
+      }
+#pragma unroll
+      for (int u = 0; u < kUnroll; ++u) {
+        const int64_t o = o0 + 16 * kCopyThreads * u;
+        *reinterpret_cast<uint4*>(d + (o < last ? o : last)) = v[u];  // tail: same bytes again
+      }
+    }
     i = vend;
   }
   for (int64_t o = i + threadIdx.x; o < end; o += kCopyThreads) d[o] = s[o];

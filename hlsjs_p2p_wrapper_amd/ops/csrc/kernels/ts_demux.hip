@@ -141,7 +141,7 @@ __global__ __launch_bounds__(kTsThreads) void ts_scan_kernel(
   __shared__ int32_t s_sum[2 * kClasses];
   __shared__ int32_t s_err;
   const int64_t gblk = blockIdx.x;
-  const int seg = find_seg(blk_prefix, nseg, gblk);  // wave-uniform
+  const int seg = find_seg_wave(blk_prefix, nseg, gblk);
   const int64_t blk = gblk - blk_prefix[seg];
   const int tid = threadIdx.x;
   if (tid < 2 * kClasses) s_sum[tid] = 0;
@@ -236,26 +236,44 @@ __global__ __launch_bounds__(kTsThreads) void ts_gather_kernel(
     const int64_t* __restrict__ blk_prefix, int nseg, const uint32_t* __restrict__ meta,
     const int64_t* __restrict__ pts_dts, const int32_t* __restrict__ blk_sums, uint8_t* __restrict__ es,
     const int64_t* __restrict__ es_off, int64_t* __restrict__ pes, int64_t max_pes, int64_t* __restrict__ info) {
-  __shared__ uint32_t s_pk[kTsThreads * kPkt / 4 + 4];  // this block's 256 packets (47 KiB)
+  // this block's 256 packets (47 KiB), rounded up to whole 16-byte-per-lane LDS-DMA waves
+  constexpr int kStageVec = (kTsThreads * kPkt + 16 * kTsThreads - 1) / (16 * kTsThreads);  // 12
+  __shared__ __attribute__((aligned(16))) uint32_t s_pk[kStageVec * kTsThreads * 4];
   __shared__ int64_t s_tot[2 * kClasses];     // segment totals
   __shared__ int64_t s_pre[2 * kClasses];     // prefix of blocks before this one
   __shared__ int32_t s_wave[4][2 * kClasses];  // per-wave totals
   __shared__ uint8_t s_order[4][64];           // per wave: active-packet rank -> lane
   const int64_t gblk = blockIdx.x;
-  const int seg = find_seg(blk_prefix, nseg, gblk);
+  const int seg = find_seg_wave(blk_prefix, nseg, gblk);
   const int64_t b0 = blk_prefix[seg];
   const int64_t nblk = blk_prefix[seg + 1] - b0;
   const int64_t blk = gblk - b0;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  {  // stage the block's packets into LDS: fully coalesced 16-byte loads
+  // Stage the block's packets (<= 47 KiB) into LDS by LDS-DMA: 12 global_load_lds_dwordx4 per
+  // wave (1 KiB each, lane-linear image), all in flight at once and drained by the barrier.
+  // (A register-staged loop compiled to load / vmcnt(0) / ds_write per 16 B: ~12 serialised
+  // HBM round trips per block.)
+  {
     const int64_t np = seg_length(seg_len, seg) / kPkt;
     const int64_t first = blk * kTsThreads;
     const int64_t npk = np - first < kTsThreads ? (np - first > 0 ? np - first : 0) : kTsThreads;
     const int nvec = static_cast<int>((npk * kPkt + 15) / 16);
-    const uint4* g = reinterpret_cast<const uint4*>(buf + seg_off[seg] + first * kPkt);
-    uint4* l = reinterpret_cast<uint4*>(s_pk);
-    for (int i = tid; i < nvec; i += kTsThreads) l[i] = g[i];
+    const uint8_t* g = buf + seg_off[seg] + first * kPkt;
+    const int last = nvec - 1;
+#pragma unroll
+    for (int k = 0; k < kStageVec; ++k) {
+      const int wbase = k * kTsThreads + wave * 64;  // wave-uniform
+      if (wbase < nvec) {
+        const int i = wbase + lane < last ? wbase + lane : last;  // tail lanes re-read the last vector
+        __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)(g + 16 * static_cast<int64_t>(i)),
+                                         (__attribute__((address_space(3))) void*)(
+                                             reinterpret_cast<uint8_t*>(s_pk) + 16 * wbase),
+                                         16, 0, 0);
+      }
+    }
   }
+  const int64_t gpk = gblk * kTsThreads + tid;
+  const uint32_t m = meta[gpk];
   if (tid < 2 * kClasses) {
     s_tot[tid] = 0;
     s_pre[tid] = 0;
@@ -285,8 +303,6 @@ __global__ __launch_bounds__(kTsThreads) void ts_gather_kernel(
       }
     }
   }
-  const int64_t gpk = gblk * kTsThreads + tid;
-  const uint32_t m = meta[gpk];
   const int c = m & 3, ps = (m >> 2) & 0xff, len = (m >> 10) & 0xff, pes_flag = (m >> 18) & 1;
   // in-block exclusive scans per class (bytes and PES starts)
   int inc_b[kClasses], inc_p[kClasses];

@@ -24,7 +24,7 @@ def test_crc32_mfma_matches_zlib(cuda):
         offs.append(pos)
         blob.append(_rand(n, i))
         pad = (-(pos + n)) % 256
-        blob.append(np.zeros(pad, np.uint8))
+        blob.append(np.full(pad, 0xA5, np.uint8))  # nonzero: a read past the end must not count
         pos += n + pad
     buf = np.concatenate(blob)
     t = torch.from_numpy(buf).to(cuda)

@@ -12,7 +12,7 @@ import numpy as np
 import torch
 
 from hlsjs_p2p_wrapper_amd.net.origin import PRESET_1080P_6M, SyntheticHlsOrigin
-from hlsjs_p2p_wrapper_amd.ops import aes, crc, tsdemux
+from hlsjs_p2p_wrapper_amd.ops import aes, crc, segment, tsdemux
 
 
 def timed(fn, iters):
@@ -61,7 +61,12 @@ def main():
     res["crc_us"] = timed(lambda: crc.crc32_batch(src, offs, lens), args.iters)
     got = crc.crc32_batch(src, offs, lens)[0].cpu().numpy().view(np.uint32)
     assert int(got[0]) == crc.crc32(pool.data[offs[0]:offs[0] + lens[0]].numpy()), "CRC mismatch"
-    for k in ("aes", "demux", "crc"):
+    # byte-moving rooflines on the same bytes: the batched K4 segment copy and torch's copy_
+    cp = torch.empty_like(src)
+    res["copy_us"] = timed(lambda: segment.copy_segments(src, cp, offs, offs, lens), args.iters)
+    assert torch.equal(cp[offs[5]:offs[5] + lens[5]], src[offs[5]:offs[5] + lens[5]]), "copy mismatch"
+    res["torch_copy_us"] = timed(lambda: cp.copy_(src), args.iters)
+    for k in ("aes", "demux", "crc", "copy", "torch_copy"):
         res[f"{k}_GBps"] = round(total / (res[f"{k}_us"] * 1e-6) / 1e9, 1)
         res[f"{k}_us"] = round(res[f"{k}_us"], 1)
     res["bytes"] = total
