@@ -130,7 +130,7 @@ void ts_demux(Tensor buf, Tensor seg_off, Tensor seg_len, Tensor blk_prefix, int
   check(blk_prefix, "blk_prefix", torch::kInt64, B + 1);
   check(meta, "meta", torch::kInt32, total_blocks * 256);
   check(pts_dts, "pts_dts", torch::kInt64, total_blocks * 256 * 2);
-  check(blk_sums, "blk_sums", torch::kInt32, total_blocks * 6);
+  check(blk_sums, "aux", torch::kInt32, total_blocks * 12 + B * 7);  // sums | prefixes | totals | counters
   check(es, "es", torch::kUInt8);
   check(es_off, "es_off", torch::kInt64, B);
   check(pes, "pes", torch::kInt64, B * 3 * max_pes * 3);

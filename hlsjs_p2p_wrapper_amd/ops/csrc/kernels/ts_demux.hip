@@ -5,18 +5,19 @@
 //   pes:  int64[seg][3 classes][max_pes][3] = (ES byte offset, PTS, DTS)  (-1 = absent)
 //   info: int64[seg][16] (status bits, PIDs, packet count, per-class bytes / PES counts)
 //
-// Three launches, no host round trip (segment lengths come from the decrypt kernel's
+// Four launches, no host round trip (segment lengths come from the decrypt kernel's
 // on-device out_len):
 //   1. ts_psi_kernel     — one wave per segment: PAT -> PMT PID, PMT -> ES PIDs/types
 //                          (first 64 packets), zero-inits info / PES tables.
 //   2. ts_scan_kernel    — one lane per 188-byte packet: sync check, PID class, payload
 //                          start/len, PES header (PTS/DTS, header skip); per-256-packet
 //                          block sums of (payload bytes, PES starts) per class.
-//   3. ts_gather_kernel  — same grid: block prefix + in-block wave scans give every
-//                          packet its ES destination; payload copy is done cooperatively
-//                          by the whole wave per packet with dword-aligned stores
-//                          (v_alignbyte funnel for the unaligned source), so each store
-//                          instruction writes up to 256 contiguous bytes.
+//   3. ts_prefix_kernel  — one wave per segment: exclusive block prefixes + segment totals.
+//   4. ts_gather_kernel  — same grid as the scan: the block's packets are staged in LDS by
+//                          LDS-DMA, packed in-wave scans + the block prefix give every packet
+//                          its ES destination, and 16-lane groups copy four payloads per wave
+//                          iteration with dword-aligned stores (v_alignbyte funnel for the
+//                          unaligned LDS source).
 #include "common.h"
 
 namespace hlsp2p {
@@ -134,6 +135,16 @@ __device__ __forceinline__ uint32_t pack_meta(int c, int ps, int len, int pes) {
 }
 
 // ---------------------------------------------------------------- 2. scan
+// inclusive wave prefix sum (wave64)
+__device__ __forceinline__ int wave_incl_scan(int v, int lane) {
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const int t = __shfl_up(v, o);
+    if (lane >= o) v += t;
+  }
+  return v;
+}
+
 __global__ __launch_bounds__(kTsThreads) void ts_scan_kernel(
     const uint8_t* __restrict__ buf, const int64_t* __restrict__ seg_off, const int64_t* __restrict__ seg_len,
     const int64_t* __restrict__ blk_prefix, int nseg, int64_t* __restrict__ info, uint32_t* __restrict__ meta,
@@ -220,34 +231,63 @@ __global__ __launch_bounds__(kTsThreads) void ts_scan_kernel(
                                   static_cast<unsigned long long>(s_err));
 }
 
-// inclusive wave prefix sum (wave64)
-__device__ __forceinline__ int wave_incl_scan(int v, int lane) {
+// ---------------------------------------------------------------- 2b. block prefix
+// One wave per segment turns the scan's block sums into exclusive per-block prefixes
+// (blk_pre) and segment totals (seg_tot, info), so a gather block reads its 12 numbers
+// instead of re-reducing all of its segment's block sums.  (A last-arriving-block variant
+// inside the scan kernel needed an agent-scope release per block: on gfx950 that writes
+// back the XCD's L2, and the scan took 5x longer.)
+__global__ __launch_bounds__(64) void ts_prefix_kernel(const int64_t* __restrict__ blk_prefix,
+                                                       const int32_t* __restrict__ blk_sums,
+                                                       int32_t* __restrict__ blk_pre, int32_t* __restrict__ seg_tot,
+                                                       int64_t* __restrict__ info, int64_t max_pes) {
+  const int seg = blockIdx.x;
+  const int lane = threadIdx.x;
+  const int64_t b0 = blk_prefix[seg];
+  const int64_t nblk = blk_prefix[seg + 1] - b0;
+  int carry[2 * kClasses] = {0, 0, 0, 0, 0, 0};
+  for (int64_t bb = 0; bb < nblk; bb += 64) {
+    const int64_t b = bb + lane;
+    int v[2 * kClasses];
 #pragma unroll
-  for (int o = 1; o < 64; o <<= 1) {
-    const int t = __shfl_up(v, o);
-    if (lane >= o) v += t;
+    for (int k = 0; k < 2 * kClasses; ++k) v[k] = b < nblk ? blk_sums[(b0 + b) * 2 * kClasses + k] : 0;
+#pragma unroll
+    for (int k = 0; k < 2 * kClasses; ++k) {
+      const int inc = wave_incl_scan(v[k], lane);
+      if (b < nblk) blk_pre[(b0 + b) * 2 * kClasses + k] = carry[k] + inc - v[k];
+      carry[k] += __shfl(inc, 63);
+    }
   }
-  return v;
+  if (lane == 0) {  // carry[] is wave-uniform
+#pragma unroll
+    for (int k = 0; k < 2 * kClasses; ++k) seg_tot[seg * 2 * kClasses + k] = carry[k];
+    int64_t* inf = info + static_cast<int64_t>(seg) * kInfo;
+    int64_t over = 0;
+    for (int k = 0; k < kClasses; ++k) {
+      inf[kBytes0 + k] = carry[2 * k];
+      inf[kPes0 + k] = carry[2 * k + 1];
+      if (carry[2 * k + 1] > max_pes) over = kPesOverflow;
+    }
+    inf[kPayloadBytes] = static_cast<int64_t>(carry[0]) + carry[2] + carry[4];
+    if (over) atomicOr(reinterpret_cast<unsigned long long*>(inf + kStatus), static_cast<unsigned long long>(over));
+  }
 }
 
 // ---------------------------------------------------------------- 3. gather
 __global__ __launch_bounds__(kTsThreads) void ts_gather_kernel(
     const uint8_t* __restrict__ buf, const int64_t* __restrict__ seg_off, const int64_t* __restrict__ seg_len,
     const int64_t* __restrict__ blk_prefix, int nseg, const uint32_t* __restrict__ meta,
-    const int64_t* __restrict__ pts_dts, const int32_t* __restrict__ blk_sums, uint8_t* __restrict__ es,
-    const int64_t* __restrict__ es_off, int64_t* __restrict__ pes, int64_t max_pes, int64_t* __restrict__ info) {
+    const int64_t* __restrict__ pts_dts, const int32_t* __restrict__ blk_pre, const int32_t* __restrict__ seg_tot,
+    uint8_t* __restrict__ es, const int64_t* __restrict__ es_off, int64_t* __restrict__ pes, int64_t max_pes,
+    int64_t* __restrict__ info) {
   // this block's 256 packets (47 KiB), rounded up to whole 16-byte-per-lane LDS-DMA waves
   constexpr int kStageVec = (kTsThreads * kPkt + 16 * kTsThreads - 1) / (16 * kTsThreads);  // 12
   __shared__ __attribute__((aligned(16))) uint32_t s_pk[kStageVec * kTsThreads * 4];
-  __shared__ int64_t s_tot[2 * kClasses];     // segment totals
-  __shared__ int64_t s_pre[2 * kClasses];     // prefix of blocks before this one
-  __shared__ int32_t s_wave[4][2 * kClasses];  // per-wave totals
-  __shared__ uint8_t s_order[4][64];           // per wave: active-packet rank -> lane
+  __shared__ uint32_t s_wave[4][3];      // per-wave packed scan totals
+  __shared__ uint8_t s_order[4][64];      // per wave: active-packet rank -> lane
   const int64_t gblk = blockIdx.x;
   const int seg = find_seg_wave(blk_prefix, nseg, gblk);
-  const int64_t b0 = blk_prefix[seg];
-  const int64_t nblk = blk_prefix[seg + 1] - b0;
-  const int64_t blk = gblk - b0;
+  const int64_t blk = gblk - blk_prefix[seg];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   // Stage the block's packets (<= 47 KiB) into LDS by LDS-DMA: 12 global_load_lds_dwordx4 per
   // wave (1 KiB each, lane-linear image), all in flight at once and drained by the barrier.
@@ -274,64 +314,55 @@ __global__ __launch_bounds__(kTsThreads) void ts_gather_kernel(
   }
   const int64_t gpk = gblk * kTsThreads + tid;
   const uint32_t m = meta[gpk];
-  if (tid < 2 * kClasses) {
-    s_tot[tid] = 0;
-    s_pre[tid] = 0;
-  }
-  __syncthreads();
-  {  // segment totals and this block's exclusive prefix (nblk is small: <= ~350 for 16 MB)
-    int64_t tot[2 * kClasses] = {0, 0, 0, 0, 0, 0}, pre[2 * kClasses] = {0, 0, 0, 0, 0, 0};
-    for (int64_t b = tid; b < nblk; b += kTsThreads) {
-      const int32_t* bs = blk_sums + (b0 + b) * 2 * kClasses;
+  // block prefix and segment totals: computed once per segment by the scan kernel's last
+  // block; uniform addresses, so these are scalar loads in flight with the stage
+  int32_t pre[2 * kClasses], tot[2 * kClasses];
 #pragma unroll
-      for (int k = 0; k < 2 * kClasses; ++k) {
-        tot[k] += bs[k];
-        if (b < blk) pre[k] += bs[k];
-      }
-    }
-#pragma unroll
-    for (int k = 0; k < 2 * kClasses; ++k) {
-      int64_t t = tot[k], p = pre[k];
-#pragma unroll
-      for (int o = 32; o > 0; o >>= 1) {
-        t += __shfl_xor(t, o);
-        p += __shfl_xor(p, o);
-      }
-      if (lane == 0) {
-        if (t) atomicAdd(reinterpret_cast<unsigned long long*>(&s_tot[k]), static_cast<unsigned long long>(t));
-        if (p) atomicAdd(reinterpret_cast<unsigned long long*>(&s_pre[k]), static_cast<unsigned long long>(p));
-      }
-    }
+  for (int k = 0; k < 2 * kClasses; ++k) {
+    pre[k] = blk_pre[gblk * 2 * kClasses + k];
+    tot[k] = seg_tot[seg * 2 * kClasses + k];
   }
   const int c = m & 3, ps = (m >> 2) & 0xff, len = (m >> 10) & 0xff, pes_flag = (m >> 18) & 1;
-  // in-block exclusive scans per class (bytes and PES starts)
-  int inc_b[kClasses], inc_p[kClasses];
+  // In-wave inclusive scans of (bytes, PES starts) per class, packed three to a word (wave
+  // totals: bytes <= 64 x 184 < 2^16, PES starts <= 64 < 2^8): 3 scans instead of 6.
+  const uint32_t lb = static_cast<uint32_t>(len), pf = static_cast<uint32_t>(pes_flag);
+  uint32_t sA = (c == 0 ? lb : 0u) | ((c == 1 ? lb : 0u) << 16);
+  uint32_t sB = (c == 2 ? lb : 0u) | ((c == 0 ? pf : 0u) << 16) | ((c == 1 ? pf : 0u) << 24);
+  uint32_t sC = c == 2 ? pf : 0u;
 #pragma unroll
-  for (int k = 0; k < kClasses; ++k) {
-    inc_b[k] = wave_incl_scan(c == k ? len : 0, lane);
-    inc_p[k] = wave_incl_scan(c == k ? pes_flag : 0, lane);
+  for (int o = 1; o < 64; o <<= 1) {
+    const uint32_t tA = __shfl_up(sA, o), tB = __shfl_up(sB, o), tC = __shfl_up(sC, o);
+    if (lane >= o) {
+      sA += tA;
+      sB += tB;
+      sC += tC;
+    }
   }
   if (lane == 63) {
-#pragma unroll
-    for (int k = 0; k < kClasses; ++k) {
-      s_wave[wave][2 * k] = inc_b[k];
-      s_wave[wave][2 * k + 1] = inc_p[k];
-    }
+    s_wave[wave][0] = sA;
+    s_wave[wave][1] = sB;
+    s_wave[wave][2] = sC;
   }
   __syncthreads();
   int64_t dst_b = 0, pes_idx = 0;
   if (c < 3) {
-    int64_t wb = 0, wp = 0;
+    uint32_t wA = 0, wB = 0, wC = 0;  // earlier waves' packed totals (no field overflows: <= 256 packets)
     for (int w = 0; w < wave; ++w) {
-      wb += s_wave[w][2 * c];
-      wp += s_wave[w][2 * c + 1];
+      wA += s_wave[w][0];
+      wB += s_wave[w][1];
+      wC += s_wave[w][2];
     }
-    const int64_t class_base = (c >= 1 ? s_tot[0] : 0) + (c >= 2 ? s_tot[2] : 0);
-    const int64_t es_in_class = s_pre[2 * c] + wb + inc_b[c] - len;  // exclusive
+    sA += wA;
+    sB += wB;
+    sC += wC;
+    const uint32_t inc_b = c == 0 ? (sA & 0xffff) : c == 1 ? (sA >> 16) : (sB & 0xffff);
+    const uint32_t inc_p = c == 0 ? ((sB >> 16) & 0xff) : c == 1 ? (sB >> 24) : sC;
+    const int64_t class_base = (c >= 1 ? tot[0] : 0) + (c >= 2 ? tot[2] : 0);
+    const int64_t es_in_class = static_cast<int64_t>(pre[2 * c]) + inc_b - len;  // exclusive
     dst_b = class_base + es_in_class;
-    pes_idx = s_pre[2 * c + 1] + wp + inc_p[c] - pes_flag;
+    pes_idx = static_cast<int64_t>(pre[2 * c + 1]) + inc_p - pes_flag;
     if (pes_flag) {
-      const int64_t tot_pes = s_tot[2 * c + 1];
+      const int64_t tot_pes = tot[2 * c + 1];
       int64_t* infc = info + static_cast<int64_t>(seg) * kInfo;
       if (pes_idx == 0) infc[kFirstPts + c] = pts_dts[2 * gpk];
       if (pes_idx == tot_pes - 1) infc[kLastPts + c] = pts_dts[2 * gpk];
@@ -389,24 +420,17 @@ __global__ __launch_bounds__(kTsThreads) void ts_gather_kernel(
     }
     if (sub < tail) d[head + 4 * body + sub] = s_bytes[s + head + 4 * body + sub];
   }
-  if (blk == 0 && tid == 0) {
-    int64_t* inf = info + static_cast<int64_t>(seg) * kInfo;
-    int64_t over = 0;
-    for (int k = 0; k < kClasses; ++k) {
-      inf[kBytes0 + k] = s_tot[2 * k];
-      inf[kPes0 + k] = s_tot[2 * k + 1];
-      if (s_tot[2 * k + 1] > max_pes) over = kPesOverflow;
-    }
-    inf[kPayloadBytes] = s_tot[0] + s_tot[2] + s_tot[4];
-    if (over) atomicOr(reinterpret_cast<unsigned long long*>(inf + kStatus), static_cast<unsigned long long>(over));
-  }
 }
 
 hipError_t launch_ts_demux(const uint8_t* buf, const int64_t* seg_off, const int64_t* seg_len,
                            const int64_t* blk_prefix, int nseg, int64_t total_blocks, uint32_t* meta,
-                           int64_t* pts_dts, int32_t* blk_sums, uint8_t* es, const int64_t* es_off, int64_t* pes,
+                           int64_t* pts_dts, int32_t* aux, uint8_t* es, const int64_t* es_off, int64_t* pes,
                            int64_t max_pes, int64_t* info, hipStream_t stream) {
   if (nseg <= 0) return hipSuccess;
+  // aux (int32): [blk_sums: blocks x 6 | blk_pre: blocks x 6 | seg_tot: nseg x 6 | spare: nseg]
+  int32_t* blk_sums = aux;
+  int32_t* blk_pre = blk_sums + total_blocks * 2 * kClasses;
+  int32_t* seg_tot = blk_pre + total_blocks * 2 * kClasses;
   hipLaunchKernelGGL(ts_psi_kernel, dim3(nseg), dim3(64), 0, stream, buf, seg_off, seg_len, info, pes, max_pes);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess || total_blocks <= 0) return e;
@@ -414,8 +438,13 @@ hipError_t launch_ts_demux(const uint8_t* buf, const int64_t* seg_off, const int
                      seg_off, seg_len, blk_prefix, nseg, info, meta, pts_dts, blk_sums);
   e = hipGetLastError();
   if (e != hipSuccess) return e;
+  hipLaunchKernelGGL(ts_prefix_kernel, dim3(nseg), dim3(64), 0, stream, blk_prefix, blk_sums, blk_pre, seg_tot, info,
+                     max_pes);
+  e = hipGetLastError();
+  if (e != hipSuccess) return e;
   hipLaunchKernelGGL(ts_gather_kernel, dim3(static_cast<unsigned>(total_blocks)), dim3(kTsThreads), 0, stream, buf,
-                     seg_off, seg_len, blk_prefix, nseg, meta, pts_dts, blk_sums, es, es_off, pes, max_pes, info);
+                     seg_off, seg_len, blk_prefix, nseg, meta, pts_dts, blk_pre, seg_tot, es, es_off, pes, max_pes,
+                     info);
   return hipGetLastError();
 }
 

@@ -96,7 +96,7 @@ def demux_batch(buf: torch.Tensor, offs: Sequence[int], lens: Union[Sequence[int
     nb = max(1, total_blocks)
     meta = torch.empty(nb * 256, dtype=torch.int32, device=dev)
     pts_dts = torch.empty(nb * 256 * 2, dtype=torch.int64, device=dev)
-    blk_sums = torch.empty(nb * 6, dtype=torch.int32, device=dev)
+    blk_sums = torch.empty(nb * 12 + B * 7, dtype=torch.int32, device=dev)  # sums|prefixes|totals|counters
     info = torch.empty((B, INFO_WORDS), dtype=torch.int64, device=dev)
     pes = torch.empty((B, 3, max_pes, 3), dtype=torch.int64, device=dev)
     _dev().ts_demux(buf, d["o"], n_dev, d["bp"], total_blocks, meta, pts_dts, blk_sums, es, d["eo"], pes, max_pes, info)
