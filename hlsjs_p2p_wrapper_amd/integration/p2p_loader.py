@@ -104,11 +104,12 @@ def p2p_loader_generator(hlsjsWrapper: Any) -> type:
             self.loadInternal()
 
         def loadSuccess(self, segmentData: Any) -> None:
-            if self.stats.aborted:  # late callback after abort
+            stats = self.stats  # a JsObject: item access here skips its __getattr__ hook
+            if stats.get("aborted"):  # late callback after abort
                 return
             event = JsObject(currentTarget=JsObject(response=segmentData))
-            self.stats.tload = self.loop.now()
-            self.onSuccess(event, self.stats)
+            stats["tload"] = self.loop.now()
+            self.onSuccess(event, stats)
             self.reset()
 
         # errors from the peer agent are always HTTP-like: it ultimately falls through to the CDN
@@ -139,33 +140,36 @@ def p2p_loader_generator(hlsjsWrapper: Any) -> type:
             segmentView = SegmentView(sn=self.frag.sn, trackView=trackView, time=self.frag.start)
             reqInfo = JsObject(url=self.url, headers=headers, withCredentials=withCredentials)
             callbacks = JsObject(onSuccess=self.loadSuccess, onError=self.loadError, onProgress=self.loadProgress)
-            self.stats.tfirst = None
-            self.stats.loaded = 0
+            stats = self.stats
+            stats["tfirst"] = None
+            stats["loaded"] = 0
             self.requestTimeout = self.loop.set_timeout(self.loadTimeout, self.timeout)
             self.peerAgentLoader = hlsjsWrapper.peerAgentModule.getSegment(reqInfo, callbacks, segmentView)
 
         def loadProgress(self, event: Any) -> None:
+            get = event.get if isinstance(event, dict) else (lambda k: getattr(event, k, None))
             loaded = 0
-            cdn = _attr(event, "cdnDownloaded")
-            p2p = _attr(event, "p2pDownloaded")
+            cdn = get("cdnDownloaded")
+            p2p = get("p2pDownloaded")
             if cdn:
                 loaded += cdn
             if p2p:
                 loaded += p2p
-            self.stats.loaded = loaded
-            if self.stats.tfirst is None:
+            stats = self.stats
+            stats["loaded"] = loaded
+            if stats.get("tfirst") is None:
                 now = self.loop.now()
-                p2p_d = _attr(event, "p2pDuration")
-                cdn_d = _attr(event, "cdnDuration")
+                p2p_d = get("p2pDuration")
+                cdn_d = get("cdnDuration")
                 # a P2P hit reports once, immediately: move trequest back by the transfer time
                 # so the ABR estimate reflects the peer rate, with a synthetic RTT of at most 10 ms
                 if _is_number(p2p_d) and _is_number(cdn_d) and (p2p_d + cdn_d > 0) and (p2p or 0) > 0:
                     srTime = p2p_d + cdn_d
-                    self.stats.trequest = now - srTime
-                    self.stats.tfirst = self.stats.trequest + min(_js_round(srTime / 2), 10)
+                    stats["trequest"] = now - srTime
+                    stats["tfirst"] = stats["trequest"] + min(_js_round(srTime / 2), 10)
                 else:
-                    self.stats.tfirst = now
-            self.onProgress(event, self.stats)
+                    stats["tfirst"] = now
+            self.onProgress(event, stats)
 
         def loadTimeout(self) -> None:
             self.onTimeout(None, self.stats)

@@ -58,6 +58,7 @@ class EventLoop:
         self._ready: List[Tuple[Callable[..., Any], tuple]] = []
         self._seq = itertools.count()
         self._idle_hooks: List[Callable[[], bool]] = []
+        self._compact_at = 4096
 
     # ------------------------------------------------------------------ clock
     def now(self) -> float:
@@ -78,7 +79,15 @@ class EventLoop:
     def set_timeout(self, fn: Callable[..., Any], delay_ms: float = 0.0, *args: Any) -> TimerHandle:
         delay = 0.0 if delay_ms is None else max(0.0, float(delay_ms))
         h = TimerHandle(self.now() + delay, next(self._seq), fn, args)
-        heapq.heappush(self._heap, h)
+        heap = self._heap
+        if len(heap) >= self._compact_at:
+            # cancelled timers are dropped lazily when they reach the top; a long-running
+            # peer cancels one fragment-timeout timer per fragment (tens of thousands per
+            # second), so sweep them out whenever the heap doubles
+            heap[:] = [t for t in heap if not t.cancelled]
+            heapq.heapify(heap)
+            self._compact_at = max(4096, 2 * len(heap))
+        heapq.heappush(heap, h)
         return h
 
     setTimeout = set_timeout

@@ -94,17 +94,19 @@ class AbrController:
         self.fragCurrent = None
 
     def onFragLoading(self, data: Any) -> None:
-        frag = _get(data, "frag")
-        self.fragCurrent = frag
+        self.fragCurrent = data["frag"] if type(data) is dict else _get(data, "frag")
 
     def onFragLoaded(self, data: Any) -> None:
-        stats = _get(data, "stats")
-        frag = _get(data, "frag")
+        if type(data) is dict:  # what Hls.trigger passes: skip the generic accessor
+            stats, frag = data.get("stats"), data.get("frag")
+        else:
+            stats, frag = _get(data, "stats"), _get(data, "frag")
+        sget = stats.get if isinstance(stats, dict) else (lambda k, d=None: _get(stats, k, d))
         # only the first load of a fragment is a fair bandwidth sample (a reload may be
         # served from a cache and look infinitely fast)
-        if _get(stats, "aborted") is None and _get(frag, "loadCounter", 1) == 1:
-            ms = self.loop.now() - _get(stats, "trequest")
-            loaded = _get(stats, "loaded") or 0
+        if sget("aborted") is None and _get(frag, "loadCounter", 1) == 1:
+            ms = self.loop.now() - sget("trequest")
+            loaded = sget("loaded") or 0
             self.lastfetchduration = ms / 1000.0
             self.lastbw = (loaded * 8) / max(self.lastfetchduration, 1e-9)
             self.bwEstimator.sample(ms, loaded)

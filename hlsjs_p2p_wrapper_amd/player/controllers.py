@@ -332,8 +332,16 @@ class FragmentLoader:
                     cfg.fragLoadingRetryDelay, lambda e, s: self._progress(frag, e, s), frag)
 
     def _success(self, frag: Fragment, event: Any, stats: Any) -> None:
-        payload = event.currentTarget.response if hasattr(event, "currentTarget") else event["currentTarget"]["response"]
-        stats.length = _byte_length(payload)
+        if isinstance(event, dict):  # JsObject / plain dict event
+            ct = event["currentTarget"]
+            payload = ct["response"] if isinstance(ct, dict) else ct.response
+        else:
+            payload = event.currentTarget.response
+        length = _byte_length(payload)
+        if isinstance(stats, dict):
+            stats["length"] = length
+        else:
+            stats.length = length
         self.loaders.pop(id(frag), None)
         frag.loader = None
         self.hls.trigger(Events.FRAG_LOADED, {"payload": payload, "frag": frag, "stats": stats})
@@ -353,8 +361,9 @@ class FragmentLoader:
                                         "fatal": False, "frag": frag})
 
     def _progress(self, frag: Fragment, event: Any, stats: Any) -> None:
-        frag.loaded = stats.loaded
-        self.hls.trigger(Events.FRAG_LOAD_PROGRESS, {"frag": frag, "stats": stats})
+        frag.loaded = stats["loaded"] if isinstance(stats, dict) else stats.loaded
+        if self.hls.listening(Events.FRAG_LOAD_PROGRESS):
+            self.hls.trigger(Events.FRAG_LOAD_PROGRESS, {"frag": frag, "stats": stats})
 
 
 def _byte_length(payload: Any) -> int:
@@ -533,8 +542,10 @@ class StreamController:
         max_inflight = max(1, int(cfg.get("maxFragLoadsInFlight", 1) or 1))
         nxt = buf_end
         for f in self.inflight.values():
-            if f.end > nxt and f.start <= nxt + 0.5:
-                nxt = f.end
+            fs = f.start
+            fe = fs + f.duration  # f.end, without the property call (runs per in-flight fragment per tick)
+            if fe > nxt and fs <= nxt + 0.5:
+                nxt = fe
         while len(self.inflight) < max_inflight and nxt - pos < max_buf:
             frag = self._frag_at(details, nxt)
             if frag is None:
@@ -598,7 +609,10 @@ class StreamController:
             hls.trigger(Events.FRAG_PARSING_INIT_SEGMENT, {"frag": frag, "tracks": {
                 "video": {"pid": info["video_pid"], "type": info["video_type"]},
                 "audio": {"pid": info["audio_pid"], "type": info["audio_type"]}}})
-        if r["id3"].numel():
+        # events nobody listens to are not built (no observable difference: hls.trigger with
+        # no listener does nothing); this runs once per buffered fragment
+        listening = hls.listening
+        if listening(Events.FRAG_PARSING_METADATA) and r["id3"].numel():
             hls.trigger(Events.FRAG_PARSING_METADATA, {"frag": frag, "samples": r["id3"]})
         vfirst, vlast, nv = info["video_first_pts"], info["video_last_pts"], info["n_video_pes"]
         if vfirst >= 0 and vlast >= vfirst and nv > 1:
@@ -608,30 +622,42 @@ class StreamController:
             dur = frag.duration
         start = frag.start
         end = start + dur
-        hls.trigger(Events.FRAG_PARSING_DATA, {"frag": frag, "type": "video", "startPTS": start, "endPTS": end,
-                                               "data1": r["video"], "nb": nv, "pts": (vfirst, vlast)})
-        hls.trigger(Events.FRAG_PARSING_DATA, {"frag": frag, "type": "audio", "startPTS": start, "endPTS": end,
-                                               "data1": r["audio"], "nb": info["n_audio_pes"],
-                                               "pts": (info["audio_first_pts"], info["audio_last_pts"])})
-        hls.trigger(Events.FRAG_PARSED, {"frag": frag})
+        if listening(Events.FRAG_PARSING_DATA):
+            hls.trigger(Events.FRAG_PARSING_DATA, {"frag": frag, "type": "video", "startPTS": start, "endPTS": end,
+                                                   "data1": r["video"], "nb": nv, "pts": (vfirst, vlast)})
+            hls.trigger(Events.FRAG_PARSING_DATA, {"frag": frag, "type": "audio", "startPTS": start, "endPTS": end,
+                                                   "data1": r["audio"], "nb": info["n_audio_pes"],
+                                                   "pts": (info["audio_first_pts"], info["audio_last_pts"])})
+        if listening(Events.FRAG_PARSED):
+            hls.trigger(Events.FRAG_PARSED, {"frag": frag})
         media = hls.media
         nbytes = int(r["video"].numel() + r["audio"].numel())
-        hls.trigger(Events.BUFFER_APPENDING, {"type": "video", "parent": "main", "bytes": nbytes})
+        if listening(Events.BUFFER_APPENDING):
+            hls.trigger(Events.BUFFER_APPENDING, {"type": "video", "parent": "main", "bytes": nbytes})
         if media is not None:
             retain = (r["video"], r["audio"]) if hls.config.get("retainMediaData") else None
             if retain is not None:
                 media.retain = True
             media.append(start, end, nbytes, retain)
         now = self.loop.now()
-        stats.tbuffered = now
-        tfirst = stats.tfirst if stats.tfirst is not None else stats.trequest
+        if isinstance(stats, dict):  # JsObject stats (every built-in loader): plain item access
+            stats["tbuffered"] = now
+            tfirst = stats.get("tfirst")
+            if tfirst is None:
+                tfirst = stats.get("trequest")
+            length = stats.get("length") or 0
+        else:
+            stats.tbuffered = now
+            tfirst = stats.tfirst if stats.tfirst is not None else stats.trequest
+            length = stats.length or 0
         dt = max(now - tfirst, 1e-3)
-        self.fragLastKbps = round(8 * (stats.length or 0) / dt)
+        self.fragLastKbps = round(8 * length / dt)
         self.inflight.pop(key, None)
         self.fragPrevious = frag
         self.fragments_buffered += 1
-        self.bytes_buffered += int(stats.length or 0)
-        hls.trigger(Events.BUFFER_APPENDED, {"parent": "main", "pending": 0})
+        self.bytes_buffered += int(length)
+        if listening(Events.BUFFER_APPENDED):
+            hls.trigger(Events.BUFFER_APPENDED, {"parent": "main", "pending": 0})
         hls.trigger(Events.FRAG_BUFFERED, {"stats": stats, "frag": frag})
         self._kick()
 

@@ -86,6 +86,10 @@ class Hls:
             data = {}
         self._observer.trigger(event, data)
 
+    def listening(self, event: str) -> bool:
+        """True when ``event`` has a listener (hot paths skip building unheard payloads)."""
+        return bool(self._observer._listeners.get(event))
+
     emit = trigger
 
     def _log_error(self, event: str, data: Any) -> None:

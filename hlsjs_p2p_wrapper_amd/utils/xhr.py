@@ -52,6 +52,8 @@ def extractInfoFromXhrSetup(xhrSetup: Optional[Callable[..., Any]], url: Any = N
     ``headersBase`` is extended in place, as in the reference (``utils.js:28``).
     """
     headers: Dict[str, str] = headersBase if headersBase is not None else {}
+    if not xhrSetup:  # nothing to run: skip building the sandbox (once per fragment request)
+        return {"headers": headers, "withCredentials": False}
 
     def _set_request_header(header: str, value: Any) -> None:
         headers[header] = value

@@ -167,3 +167,21 @@ def test_stream_controller_frag_last_kbps():
                                "video": z, "audio": z, "id3": z, "plain_bytes": 0})
     assert sc.fragLastKbps == pytest.approx(1024, abs=8)
     assert sc.stats is None or True
+
+
+def test_event_loop_sweeps_cancelled_timers():
+    """A long-running peer cancels one fragment-timeout timer per fragment: the timer heap
+    must stay bounded by the live timers, and live timers must still fire in order."""
+    from hlsjs_p2p_wrapper_amd.net.event_loop import EventLoop
+
+    loop = EventLoop("virtual")
+    fired = []
+    for i in range(50_000):
+        h = loop.set_timeout(lambda: None, 60_000)
+        loop.clear_timeout(h)
+    for i in range(3):
+        loop.set_timeout(fired.append, 10 * (3 - i), i)
+    assert len(loop._heap) < 2 * 4096 + 3
+    loop.advance(100)
+    loop.run_once(block=False)
+    assert fired == [2, 1, 0]

@@ -1,10 +1,9 @@
-# Host-overhead analysis on the GPU box: cProfile of the timed steps (1080p and the tiny
-# "hostcost" config where per-segment Python cost dominates).
+# Host-path profile on one MI355X: the 1080p bench with the Cython-compiled hot path and in
+# pure-Python mode under cProfile (per-function host cost per segment), plus the
+# 30 KB-segment host-ceiling probe.
 set -e
-R=$GRAFT_REPO_ROOT
-cd $R
+cd $GRAFT_REPO_ROOT
 mkdir -p gpurun_out/host
-HLSP2P_PROFILE=gpurun_out/host/p1080 timeout -k 10 300 python bench.py --steps 20 --warmup 6 --verbose > gpurun_out/host/b1080.log 2>&1
-HLSP2P_PROFILE=gpurun_out/host/phc timeout -k 10 300 python bench.py --steps 20 --warmup 6 --verbose --config hostcost > gpurun_out/host/bhc.log 2>&1
-timeout -k 10 300 python bench.py --steps 20 --warmup 6 --verbose > gpurun_out/host/b1080_noprof.log 2>&1
-timeout -k 10 300 python bench.py --steps 20 --warmup 6 --verbose --config hostcost > gpurun_out/host/bhc_noprof.log 2>&1
+timeout -k 10 300 python bench.py --steps 30 --warmup 6 --verbose > gpurun_out/host/bench_1080p.log 2>&1
+timeout -k 10 300 python bench.py --config hostcost --steps 30 --warmup 6 --verbose > gpurun_out/host/bench_hostcost.log 2>&1
+HLSJS_P2P_PURE=1 HLSP2P_PROFILE=gpurun_out/host/cprofile_pure timeout -k 10 300 python bench.py --config hostcost --steps 30 --warmup 6 --verbose > gpurun_out/host/bench_hostcost_pure_prof.log 2>&1
