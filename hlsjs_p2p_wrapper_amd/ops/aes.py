@@ -20,7 +20,6 @@ from ._native import device as _dev
 from ._native import runtime as _rt
 from .desc import pack_to_device
 
-CHUNK_BLOCKS = 256  # 16-B blocks per wave iteration in kernels/aes_cbc.hip (64 lanes x kBlk)
 _key_cache: Dict[bytes, np.ndarray] = {}
 _tables: Dict[str, tuple] = {}
 _lock = threading.Lock()
@@ -79,8 +78,9 @@ def cbc_decrypt_batch(src: torch.Tensor, src_offs: Sequence[int], nbytes: Sequen
         return torch.from_numpy(out_len)
     blk_prefix = np.zeros(B + 1, dtype=np.int64)
     np.cumsum(nb // 16, out=blk_prefix[1:])
-    # work unit: one wave-chunk of CHUNK_BLOCKS consecutive blocks of one segment
-    units = (nb // 16 + CHUNK_BLOCKS - 1) // CHUNK_BLOCKS
+    # work unit: one wave-chunk of consecutive blocks of one segment
+    chunk = _dev().aes_chunk_blocks()  # 64 lanes x the kernel's chains per lane
+    units = (nb // 16 + chunk - 1) // chunk
     unit_prefix = np.zeros(B + 1, dtype=np.int64)
     np.cumsum(units, out=unit_prefix[1:])
     drk_le = drk.byteswap()  # state words are used as loaded (little-endian) on device

@@ -219,6 +219,9 @@ __global__ __launch_bounds__(kAesThreads, 1) void aes128_cbc_decrypt_kernel(
 #undef ROUND_READS
 #undef ROUND_XORS
 
+// 16-byte blocks per wave iteration (the host sizes its chunk index space with this)
+int aes_chunk_blocks() { return 64 * kBlk; }
+
 hipError_t launch_aes128_cbc_decrypt(const uint8_t* src, uint8_t* dst, const int64_t* src_off, const int64_t* dst_off,
                                      const int64_t* blk_prefix, const int64_t* chunk_prefix, const uint32_t* drk,
                                      const uint32_t* ivw, const uint32_t* tdl, const uint8_t* isb, int64_t* out_len,

@@ -7,6 +7,7 @@
 
 namespace hlsp2p {
 namespace dev {
+int aes_chunk_blocks();
 hipError_t launch_aes128_cbc_decrypt(const uint8_t*, uint8_t*, const int64_t*, const int64_t*, const int64_t*,
                                      const int64_t*, const uint32_t*, const uint32_t*, const uint32_t*,
                                      const uint8_t*, int64_t*, int, int64_t, int, hipStream_t);
@@ -257,6 +258,7 @@ int64_t h2d_batch(Tensor dst, pybind11::array_t<int64_t> dst_off, pybind11::arra
 PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.doc() = "hlsjs-p2p-wrapper-amd CDNA4 (gfx950) kernels";
   m.def("aes128_cbc_decrypt", &aes128_cbc_decrypt);
+  m.def("aes_chunk_blocks", &D::aes_chunk_blocks);
   m.def("crc32_batch", &crc32_batch);
   m.def("ts_demux", &ts_demux);
   m.def("range_select", &range_select);
