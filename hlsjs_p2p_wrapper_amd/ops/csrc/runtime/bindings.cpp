@@ -17,6 +17,7 @@
 #include "aes_host.hpp"
 #include "crc_host.hpp"
 #include "planner.hpp"
+#include "shm_control.hpp"
 #include "store.hpp"
 #include "ts.hpp"
 
@@ -385,6 +386,41 @@ PYBIND11_MODULE(_runtime, m) {
     }
     return out;
   });
+  // ------------------------------------------------------------------ intra-node control plane
+  py::class_<ShmControl>(m, "ShmControl")
+      .def(py::init<const std::string&, int, int, int64_t, bool>(), py::arg("name"), py::arg("rank"),
+           py::arg("world"), py::arg("slot_words"), py::arg("create"))
+      .def("unlink", &ShmControl::unlink)
+      .def_property_readonly("slot_words", &ShmControl::slot_words)
+      .def_property_readonly("generation", &ShmControl::generation)
+      // all-gather of int64 vectors; None when some rank's message exceeded slot_words
+      // (every rank sees the same lengths, so all of them take the caller's fallback)
+      .def("allgather",
+           [](ShmControl& s, Arr<int64_t> msg, double timeout_s) -> py::object {
+             const int64_t n = msg.size();
+             {
+               py::gil_scoped_release nogil;
+               s.exchange(msg.data(), n, timeout_s);
+             }
+             std::vector<int64_t> lens(s.world());
+             for (int r = 0; r < s.world(); ++r) {
+               lens[r] = s.length(r);
+               if (lens[r] > s.slot_words()) return py::none();
+             }
+             py::list out;
+             for (int r = 0; r < s.world(); ++r) {
+               Arr<int64_t> a(static_cast<py::ssize_t>(lens[r]));
+               s.read(r, a.mutable_data());
+               out.append(a);
+             }
+             return std::move(out);
+           },
+           py::arg("msg"), py::arg("timeout_s") = 300.0)
+      .def("barrier", [](ShmControl& s, double timeout_s) {
+        py::gil_scoped_release nogil;
+        s.barrier(timeout_s);
+      }, py::arg("timeout_s") = 300.0);
+
   m.attr("FLAG_ONLINE") = int64_t(kOnline);
   m.attr("FLAG_UPLOAD") = int64_t(kUploadOn);
   m.attr("FLAG_DOWNLOAD") = int64_t(kDownloadOn);

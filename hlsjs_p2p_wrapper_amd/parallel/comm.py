@@ -16,14 +16,19 @@ Backends:
 * :class:`ThreadHub` / :class:`ThreadComm` — N peers as N threads of one process sharing
   queues and a barrier (the CPU "fake swarm" of SURVEY §4.3); tensors may live on the
   CPU or all on one GPU (then a transfer is an HBM->HBM copy).
-* :class:`DistComm` — ``torch.distributed``: a **gloo** group carries the control plane
-  on CPU tensors (no GPU sync on the metadata path) and the default group — **nccl, i.e.
-  RCCL over xGMI** on MI355X, gloo in CPU tests — carries segment bytes with
-  ``batch_isend_irecv`` (coalesced: one RCCL group call on the world communicator per
-  round, one contiguous buffer per peer pair).
+* :class:`DistComm` — ``torch.distributed``: the control plane runs on the host, never
+  on a GPU stream — through the native shared-memory all-gather (``runtime/shm_control``)
+  when every rank is on one host (a node of 8 MI355X: the benchmark's case), over a
+  **gloo** group otherwise — and the default group — **nccl, i.e. RCCL over xGMI** on
+  MI355X, gloo in CPU tests — carries segment bytes with ``batch_isend_irecv``
+  (coalesced: one RCCL group call on the world communicator per round, one contiguous
+  buffer per peer pair).  ``HLSP2P_CONTROL=gloo`` forces the gloo control plane.
 """
 from __future__ import annotations
 
+import os
+import secrets
+import socket
 import threading
 from typing import List, Optional, Sequence, Tuple
 
@@ -142,6 +147,9 @@ class DistComm(SwarmComm):
         self.data_group = data_group
         self.data_backend = backend
         self._cap = 64  # int64 words per rank in the one-shot control all-gather
+        self.control_timeout_s = float(os.environ.get("HLSP2P_CONTROL_TIMEOUT", "600"))
+        self._shm = self._open_shm_control() if self.world_size > 1 else None
+        self.control_transport = "shm" if self._shm is not None else "gloo"
         if backend == "nccl" and torch.cuda.is_available():
             # batch_isend_irecv runs on the group's full communicator; when that is created
             # lazily every rank must take part in its first use.  Node construction is
@@ -150,7 +158,58 @@ class DistComm(SwarmComm):
             dist.all_reduce(t, group=data_group)
             torch.cuda.synchronize()
 
+    SHM_SLOT_WORDS = 16384  # int64 words per rank and round (128 KiB); larger -> gloo
+
+    def _open_shm_control(self):
+        """Shared-memory control plane when every rank runs on this host (collective).
+
+        Rank 0 creates the mapping under a random name, the others attach, and rank 0
+        unlinks the name once all are attached (nothing is left in /dev/shm, even after a
+        crash).  Any failure on any rank -> every rank stays on gloo."""
+        if os.environ.get("HLSP2P_CONTROL", "auto") == "gloo":
+            return None
+        dist, g = self.dist, self.control_group
+        try:
+            with open("/proc/sys/kernel/random/boot_id") as f:
+                boot = f.read().strip()
+        except OSError:
+            boot = ""
+        hosts: List[object] = [None] * self.world_size
+        dist.all_gather_object(hosts, (socket.gethostname(), boot), group=g)
+        if any(h != hosts[0] for h in hosts):
+            return None
+        from ..ops._native import runtime as _rt
+
+        rt = _rt()
+        name = [f"/hlsp2p_{os.getpid()}_{secrets.token_hex(6)}" if self.rank == 0 else None]
+        dist.broadcast_object_list(name, src=0, group=g)
+        shm, ok = None, True
+        if self.rank == 0:
+            try:
+                shm = rt.ShmControl(name[0], 0, self.world_size, self.SHM_SLOT_WORDS, True)
+            except Exception:  # noqa: BLE001 - any failure: stay on gloo
+                ok = False
+        flags: List[object] = [None] * self.world_size
+        dist.all_gather_object(flags, ok, group=g)
+        if self.rank != 0 and all(flags):
+            try:
+                shm = rt.ShmControl(name[0], self.rank, self.world_size, self.SHM_SLOT_WORDS, False)
+            except Exception:  # noqa: BLE001
+                ok = False
+        dist.all_gather_object(flags, ok, group=g)
+        if shm is not None and self.rank == 0:
+            shm.unlink()
+        return shm if all(flags) else None
+
     def allgather_control(self, msg: np.ndarray) -> List[np.ndarray]:
+        if self._shm is not None:
+            out = self._shm.allgather(np.ascontiguousarray(msg, dtype=np.int64).reshape(-1), self.control_timeout_s)
+            if out is not None:
+                return out
+            # some rank's message exceeded a slot: every rank saw that and falls back here
+        return self._allgather_gloo(msg)
+
+    def _allgather_gloo(self, msg: np.ndarray) -> List[np.ndarray]:
         """Variable-length all-gather in ONE collective on the common path: each rank sends
         ``[len, payload...]`` padded to a shared capacity.  Only when some rank's message
         exceeds it does a second all-gather move the full padded messages; the capacity
@@ -211,9 +270,14 @@ class DistComm(SwarmComm):
             t.view(-1).copy_(h, non_blocking=False)
 
     def allreduce_sum(self, values: np.ndarray) -> np.ndarray:
+        if self._shm is not None:
+            return SwarmComm.allreduce_sum(self, values)
         t = torch.from_numpy(np.asarray(values, dtype=np.int64).copy())
         self.dist.all_reduce(t, group=self.control_group)
         return t.numpy()
 
     def barrier(self) -> None:
+        if self._shm is not None:
+            self._shm.barrier(self.control_timeout_s)
+            return
         self.dist.barrier(group=self.control_group)
