@@ -113,7 +113,8 @@ class RoundHandle:
     wants: List[_Want] = field(default_factory=list)
     by_id: Dict[int, _Want] = field(default_factory=dict)
     cdn_entries: List[Tuple[_Want, int, int, int]] = field(default_factory=list)
-    recv_entries: List[Tuple[np.ndarray, int, int]] = field(default_factory=list)
+    # received segments, plain ints: (want_id, src rank, entry id, arena offset, length)
+    recv_entries: List[Tuple[int, int, int, int, int]] = field(default_factory=list)
     send_pins: Optional[np.ndarray] = None
     hold: List[np.ndarray] = field(default_factory=list)  # in-flight entries pinned until delivered
     sent_bytes: int = 0
@@ -463,16 +464,16 @@ class SwarmNode:
             h.cdn_ms = h.ev_cdn[0].elapsed_time(h.ev_cdn[1])
         if h.ev_p2p is not None:
             h.p2p_ms = h.ev_p2p[0].elapsed_time(h.ev_p2p[1])
-        ok = None
-        if h.ok_host is not None:
-            ok = h.ok_host.numpy()
-        good, bad = [], []
-        for i, ent in enumerate(h.recv_entries):
-            (good if ok is None or ok[i] else bad).append(ent)
+        okl = h.ok_host.numpy().tolist() if h.ok_host is not None else None
+        if okl is None or all(okl):
+            good, bad = h.recv_entries, []
+        else:
+            good = [e for e, k in zip(h.recv_entries, okl) if k]
+            bad = [e for e, k in zip(h.recv_entries, okl) if not k]
         if good:
-            self.store.commit(np.asarray([r[-1] for r, _, _ in good], dtype=np.int64))
+            self.store.commit(np.asarray([e[2] for e in good], dtype=np.int64))
         if bad:
-            self.store.drop(np.asarray([r[-1] for r, _, _ in bad], dtype=np.int64))
+            self.store.drop(np.asarray([e[2] for e in bad], dtype=np.int64))
             self.stats["crc_failures"] += len(bad)
         if h.send_pins is not None:
             self.store.unpin(h.send_pins)
@@ -488,35 +489,38 @@ class SwarmNode:
                 completions.append(_Completion(req, arena[off:off + n], "cdn", n, max(h.cdn_ms, h.shaped_ms), 0.0,
                                                eid, h.shaped_ms))
         link_q: Dict[int, int] = {}  # slow-link fault injection: bytes queued per source link
-        for row, off, n in good:
-            w = h.by_id.get(int(row[7]))
+        link_kbps = self.link_kbps
+        wants_map = self._wants
+        for want_id, src, eid, off, n in good:
+            w = h.by_id.get(want_id)
             if w is None:
                 continue
-            if self._wants.get(w.key) is w:
-                del self._wants[w.key]
+            if wants_map.get(w.key) is w:
+                del wants_map[w.key]
             if w.prefetch and not w.waiters:
                 self._prefetched[w.key] = "p2p"
-            src = int(row[5])
             p2p_ms, delay = h.p2p_ms, 0.0
-            kbps = self.link_kbps.get(src)
+            kbps = link_kbps.get(src) if link_kbps else None
             if kbps:
                 link_q[src] = link_q.get(src, 0) + n
                 delay = link_q[src] * 8.0 / kbps  # kbit/s == bit/ms
                 p2p_ms = max(p2p_ms, delay)
             for req in w.waiters:
-                completions.append(_Completion(req, arena[off:off + n], "p2p", n, 0.0, p2p_ms, int(row[-1]),
-                                               delay, peer=src))
-        for row, off, n in bad:
-            w = h.by_id.get(int(row[7]))
+                completions.append(_Completion(req, arena[off:off + n], "p2p", n, 0.0, p2p_ms, eid, delay, peer=src))
+        for e in bad:
+            w = h.by_id.get(e[0])
             if w is not None:
                 w.force_cdn = True  # corrupted peer copy: go to the CDN next round
                 w.attempts += 1
                 w.round = -1
+        served = None
         for w in h.wants:  # planned but not served (e.g. a CDN error already reported)
-            if w.round == h.round and self._wants.get(w.key) is w and not any(
-                    e[0] is w for e in h.cdn_entries) and not any(
-                    h.by_id.get(int(r[7])) is w for r, _, _ in h.recv_entries):
-                w.round = -1
+            if w.round == h.round and wants_map.get(w.key) is w:
+                if served is None:
+                    served = {id(e[0]) for e in h.cdn_entries}
+                    served.update(id(h.by_id.get(e[0])) for e in h.recv_entries)
+                if id(w) not in served:
+                    w.round = -1
         t2 = time.perf_counter()
         self.timer.add("commit", t2 - t1)
         self._deliver(completions)  # delivered entries stay pinned PIN_DELAY_ROUNDS launches
@@ -674,8 +678,8 @@ class SwarmNode:
             tr = torch.empty(len(rows), dtype=torch.int32, device=dev)
             recvs.append((int(src), tr))
             trailers.append(tr)
-            for r, eid, o, n in zip(rows, ids.tolist(), offs.tolist(), lens.tolist()):
-                h.recv_entries.append((np.append(r, eid), o, n))
+            h.recv_entries.extend(zip(rows[:, 7].tolist(), [int(src)] * len(rows), ids.tolist(), offs.tolist(),
+                                      lens.tolist()))
         t = time.perf_counter()
         if self.is_cuda:
             start = torch.cuda.Event(enable_timing=True)
@@ -691,15 +695,14 @@ class SwarmNode:
             return
         if self.corrupt_next_recv > 0:  # fault injection: transport corruption
             self.corrupt_next_recv -= 1
-            _, o, n = h.recv_entries[0]
+            o, n = h.recv_entries[0][3:5]
             if n:
                 self.arena[o + n // 2] ^= 0x5A
         expect = torch.cat(trailers)
-        ids_t = torch.from_numpy(np.asarray([r[-1] for r, _, _ in h.recv_entries], dtype=np.int64)).to(
-            dev, non_blocking=True)
+        ents = h.recv_entries
+        ids_t = torch.from_numpy(np.asarray([e[2] for e in ents], dtype=np.int64)).to(dev, non_blocking=True)
         self.crc_dev[ids_t] = expect
-        _, ok = _crc.crc32_batch(self.arena, [o for _, o, _ in h.recv_entries],
-                                 [n for _, _, n in h.recv_entries], expect_dev=expect)
+        _, ok = _crc.crc32_batch(self.arena, [e[3] for e in ents], [e[4] for e in ents], expect_dev=expect)
         if self.is_cuda:
             h.ok_host = torch.empty(ok.numel(), dtype=torch.uint8, pin_memory=True)
             h.ok_host.copy_(ok, non_blocking=True)

@@ -89,6 +89,7 @@ class SyntheticHlsOrigin:
         self.with_id3 = with_id3
         self.start_sn = start_sn
         self.live_speed = live_speed
+        self._paths: Dict[str, Tuple[int, int]] = {}  # segment path -> (level, sn)
         if pool_size is None:
             pool_size = num_segments if (num_segments is not None and not live) else 16
         self.pool_size = max(1, int(pool_size))
@@ -232,10 +233,16 @@ class SyntheticHlsOrigin:
 
     def resource(self, path: str) -> Tuple[torch.Tensor, int, int, int]:
         """(pinned tensor, offset, length, crc) of a segment, for zero-copy device fetches."""
-        m = self._SEG.search(path)
-        if not m:
-            raise HttpError(404, path)
-        level, sn = int(m.group(1)), int(m.group(2))
+        ls = self._paths.get(path)
+        if ls is None:  # parse once per path (each is resolved at request and at fetch time)
+            m = self._SEG.search(path)
+            if not m:
+                raise HttpError(404, path)
+            ls = (int(m.group(1)), int(m.group(2)))
+            if len(self._paths) > 65536:
+                self._paths.clear()
+            self._paths[path] = ls
+        level, sn = ls
         if level >= len(self.pools):
             raise HttpError(404, path)
         if sn < self.first_sn() - (self.window if self.live else 0) or sn > self.live_edge() or sn < self.start_sn:

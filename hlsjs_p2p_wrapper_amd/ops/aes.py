@@ -70,7 +70,11 @@ def cbc_decrypt_batch(src: torch.Tensor, src_offs: Sequence[int], nbytes: Sequen
         raise ValueError("segment offsets must be 16-byte aligned")
     if np.any(so + nb > src.numel()) or np.any(do + nb > dst.numel()):
         raise ValueError("segment range out of bounds")
-    drk = np.stack([round_keys(bytes(k)) for k in keys]).astype(np.uint32)
+    k0 = keys[0]
+    if all(k is k0 or k == k0 for k in keys):  # one key per stream: expand / stack once
+        drk = np.broadcast_to(round_keys(bytes(k0)).astype(np.uint32), (B, 44))
+    else:
+        drk = np.stack([round_keys(bytes(k)) for k in keys]).astype(np.uint32)
     iv = np.frombuffer(b"".join(bytes(v) for v in ivs), dtype=np.uint8).reshape(B, 16)
     if src.device.type == "cpu":
         out_len = np.zeros(B, dtype=np.int64)

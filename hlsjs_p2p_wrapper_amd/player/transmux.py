@@ -40,7 +40,7 @@ class TransmuxJob:
 
 def _as_tensor(payload: Any) -> torch.Tensor:
     if isinstance(payload, torch.Tensor):
-        return payload.reshape(-1)
+        return payload if payload.dim() == 1 else payload.reshape(-1)  # arena slices are 1-D already
     if isinstance(payload, np.ndarray):
         return torch.from_numpy(np.ascontiguousarray(payload.reshape(-1)).view(np.uint8))
     if isinstance(payload, (bytes, bytearray, memoryview)):
