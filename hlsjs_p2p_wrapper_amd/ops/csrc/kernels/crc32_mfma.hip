@@ -9,8 +9,10 @@
 //     v_mfma_i32_32x32x32_i8, 64 k-steps per 256-byte group (k = 2048 data bits)
 //
 // Layout choice (so no LDS transpose of the data is needed): lane l = (row r = l & 31,
-// half h = l >> 5) owns bytes [128h, 128h + 128) of group r and loads them as 8
-// dwordx4 chunks.  k-step s = 8q + jb feeds chunk q's 16 RAW bytes masked to bit jb
+// half h = l >> 5) owns the 16-byte chunks [32q + 16h, +16), q < 8, of group r, loaded as 8
+// dwordx4 (the row's two lanes read 32 contiguous bytes per instruction; a 128h-split
+// layout read two 16-byte pieces 128 B apart: 64 line pieces per wave-load instead of 32).
+// k-step s = 8q + jb feeds chunk q's 16 RAW bytes masked to bit jb
 // (one v_and per dword: values 2^jb, -128 as i8 for jb = 7) — no bit expansion.  The B
 // fragment of the same 16 k's is W scaled by 2^(7-jb) (-128 for jb = 0), so every nonzero
 // product is +-128 and the accumulator is 128 x (the GF(2) sum): the residue bit is bit 7.
@@ -81,15 +83,17 @@ __global__ __launch_bounds__(kCrcThreads) void crc32_group_residue_kernel(
   int64_t roff = res_off[seg];
   uint4 n0, n1, n2, n3, n4, n5, n6, n7;  // the next tile's chunks
   auto load_tile = [&](int64_t tile) {
-    const int64_t my = tile * kTileBytes + r * 256 + h * 128;  // byte offset of this lane's 128 B
+    // chunk q of lane (r, h) = bytes [32q + 16h, +16) of group r: the two lanes of a row read
+    // 32 contiguous bytes per instruction (32 line pieces per wave-load instead of 64)
+    const int64_t my = tile * kTileBytes + r * 256 + h * 16;
     if ((tile + 1) * kTileBytes <= len) {  // wave-uniform: only a segment's last tile is partial
       const uint4* p = reinterpret_cast<const uint4*>(buf + base + my);
-      n0 = p[0]; n1 = p[1]; n2 = p[2]; n3 = p[3]; n4 = p[4]; n5 = p[5]; n6 = p[6]; n7 = p[7];
+      n0 = p[0]; n1 = p[2]; n2 = p[4]; n3 = p[6]; n4 = p[8]; n5 = p[10]; n6 = p[12]; n7 = p[14];
     } else {
-      n0 = load_tail(buf, base, my, len);       n1 = load_tail(buf, base, my + 16, len);
-      n2 = load_tail(buf, base, my + 32, len);  n3 = load_tail(buf, base, my + 48, len);
-      n4 = load_tail(buf, base, my + 64, len);  n5 = load_tail(buf, base, my + 80, len);
-      n6 = load_tail(buf, base, my + 96, len);  n7 = load_tail(buf, base, my + 112, len);
+      n0 = load_tail(buf, base, my, len);        n1 = load_tail(buf, base, my + 32, len);
+      n2 = load_tail(buf, base, my + 64, len);   n3 = load_tail(buf, base, my + 96, len);
+      n4 = load_tail(buf, base, my + 128, len);  n5 = load_tail(buf, base, my + 160, len);
+      n6 = load_tail(buf, base, my + 192, len);  n7 = load_tail(buf, base, my + 224, len);
     }
   };
   load_tile(t_begin - tstart);

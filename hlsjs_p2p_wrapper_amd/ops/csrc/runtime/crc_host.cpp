@@ -122,7 +122,7 @@ std::vector<int8_t> mfma_group_weights() {
     }
   }
   // Fragment order: lane l (col = l & 31 = CRC bit column, h = l >> 5) at step s = 8q + jb
-  // holds B[k][col] for its 16 k's; k(s, h, e) <-> group byte 128h + 16q + e, bit jb.
+  // holds B[k][col] for its 16 k's; k(s, h, e) <-> group byte 32q + 16h + e, bit jb.
   // The kernel feeds RAW data bytes masked to bit jb (value 2^jb; -128 as i8 for jb = 7),
   // so B is scaled by 2^(7-jb) (-128 for jb = 0): every nonzero product is +-128 and the
   // accumulator is 128 x (the GF(2) sum) -> the residue bit is bit 7 of the accumulator.
@@ -133,7 +133,7 @@ std::vector<int8_t> mfma_group_weights() {
     for (int lane = 0; lane < 64; ++lane) {
       int col = lane & 31, h = lane >> 5;
       for (int e = 0; e < 16; ++e) {
-        int byte = 128 * h + 16 * q + e;
+        int byte = 32 * q + 16 * h + e;
         w[(s * 64 + lane) * 16 + e] = static_cast<int8_t>(((v[byte][jb] >> col) & 1u) ? scale : 0);
       }
     }

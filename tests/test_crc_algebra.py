@@ -17,7 +17,7 @@ def _emulate(data: bytes, w: np.ndarray, tab: np.ndarray) -> int:
     buf = np.zeros(G * 256, np.uint8)
     buf[:n] = np.frombuffer(data, np.uint8)
     # W fragments [s][lane][e] in the kernel's order: s = 8q + jb, element e = byte
-    # 128h + 16q + e of the group masked to bit jb (i8 value 2^jb, -128 for jb = 7)
+    # 32q + 16h + e of the group masked to bit jb (i8 value 2^jb, -128 for jb = 7)
     wf = w.reshape(64, 64, 16).astype(np.int64)
     residues = []
     for g in range(G):
@@ -26,7 +26,7 @@ def _emulate(data: bytes, w: np.ndarray, tab: np.ndarray) -> int:
         for s in range(64):
             q, jb = s >> 3, s & 7
             for h in range(2):
-                chunk = grp[128 * h + 16 * q:128 * h + 16 * q + 16].astype(np.int64) & (1 << jb)
+                chunk = grp[32 * q + 16 * h:32 * q + 16 * h + 16].astype(np.int64) & (1 << jb)
                 a = np.where(chunk >= 128, chunk - 256, chunk)  # signed i8
                 for col in range(32):
                     acc[col] += int((a * wf[s, col + 32 * h, :]).sum())
