@@ -30,6 +30,7 @@ from __future__ import annotations
 
 import contextlib
 import logging
+import os
 import threading
 import time
 import zlib
@@ -151,9 +152,16 @@ class SwarmNode:
         self.directory = self.rt.Directory()
         self.arena = torch.empty(self.cache_bytes + SLACK, dtype=torch.uint8, device=self.device)
         self.crc_dev = torch.zeros(1024, dtype=torch.int32, device=self.device)  # CRC per entry id
-        # all node device work (CDN H2D, ingest CRC, RCCL, verify CRC) runs on its own stream:
-        # consumers (decrypt/demux of the previous round) on the default stream overlap it
+        # all node device work (ingest CRC, RCCL, verify CRC) runs on its own stream: consumers
+        # (decrypt/demux of the previous round) on the default stream overlap it.  The CDN
+        # H2D DMAs get a copy stream of their own, so round t+1's DMA queues directly behind
+        # round t's instead of behind round t's ingest CRC: the PCIe link never idles between
+        # rounds (the node stream waits for each round's DMA with an event).  Reuse of arena
+        # space is ordered by the store's pins, not by stream order: reserved and in-flight
+        # entries stay pinned until complete_round, delivered ones PIN_DELAY_ROUNDS launches.
         self.stream = torch.cuda.Stream(self.device) if self.is_cuda else None
+        self.copy_stream = (torch.cuda.Stream(self.device) if self.is_cuda and
+                            os.environ.get("HLSP2P_COPY_STREAM", "1") != "0" else None)
         self.online = True
         self.upload_on = True
         self.download_on = True
@@ -603,9 +611,13 @@ class SwarmNode:
         if self.is_cuda:
             start = torch.cuda.Event(enable_timing=True)
             end = torch.cuda.Event(enable_timing=True)
-            start.record()
-            h.dmas = _h2d_batch(self.arena, offs, sources)
-            end.record()
+            cs = self.copy_stream
+            with (torch.cuda.stream(cs) if cs is not None else contextlib.nullcontext()):
+                start.record()
+                h.dmas = _h2d_batch(self.arena, offs, sources)
+                end.record()
+            if cs is not None:
+                self.stream.wait_event(end)  # ingest CRC / forwarding sends read the DMA'd bytes
             h.ev_cdn = (start, end)
         else:
             t = time.perf_counter()
