@@ -66,6 +66,10 @@ def parse():
                         "tensors through host memory: multi-rank rehearsal on a single GPU)")
     p.add_argument("--sync-steps", action="store_true",
                    help="no software pipelining: each step = load, round, transmux, synchronously")
+    p.add_argument("--churn", type=int, default=0, metavar="N",
+                   help="swarm churn (BASELINE config 3): every N steps the next rank goes offline for N "
+                        "steps (masked in the control plane: it neither serves nor receives P2P), then "
+                        "one all-online period; 0 = off")
     p.add_argument("--no-gc-tune", action="store_true", help="keep Python's default GC settings")
     p.add_argument("--verbose", action="store_true")
     return p.parse_args()
@@ -162,9 +166,19 @@ def main() -> int:
     #   launch transmux batch t (decrypt + demux on the default stream, overlaps round t+1)
     #   complete transmux batch t-1 -> FRAG_BUFFERED -> slots free -> player issues loads
     pipe.auto_flush = args.sync_steps
-    state = {"h": None, "b": None}
+    state = {"h": None, "b": None, "step": 0, "offline_steps": 0}
+
+    def churn():
+        # rotation: rank k is offline during the k-th N-step period of every (world + 1) periods
+        if args.churn > 0 and world > 1:
+            online = (state["step"] // args.churn) % (world + 1) != rank
+            if online != node.online:
+                node.set_online(online)
+            state["offline_steps"] += 0 if online else 1
+        state["step"] += 1
 
     def step():
+        churn()
         t0 = time.perf_counter()
         if args.sync_steps:
             sc.tick()
@@ -259,7 +273,7 @@ def main() -> int:
         "config": {"model": desc, "global_batch": K * world, "seq_len": seg_bytes,
                    "parallelism": f"swarm{world}" + (f"-{'rccl' if dist.get_backend() == 'nccl' else 'gloo'}"
                                                      if world > 1 else ""),
-                   "inflight_per_gpu": K, "encrypted": encrypted, "segment_s": seg_dur,
+                   "inflight_per_gpu": K, "encrypted": encrypted, "segment_s": seg_dur, "churn_steps": args.churn,
                    "device": "MI355X" if use_gpu else "cpu"},
     }
     if args.verbose:

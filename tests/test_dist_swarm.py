@@ -70,6 +70,33 @@ def test_two_process_gloo_swarm():
     assert out[0][3] == pytest.approx(0.5)
 
 
+def _bench_cpu(port: int, *extra: str) -> dict:
+    import json
+    import subprocess
+    import sys
+    from pathlib import Path
+
+    repo = Path(__file__).resolve().parents[1]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2", "--master-addr",
+           "127.0.0.1", "--master-port", str(port), str(repo / "bench.py"), "--cpu", "--gpus", "2", "--config",
+           "abr5", "--steps", "8", "--warmup", "2", "--inflight", "8", "--pool", "8", "--cache-gb", "0.5", *extra]
+    p = subprocess.run(cmd, cwd=repo, env=dict(os.environ, PYTHONPATH=str(repo)), capture_output=True, text=True,
+                       timeout=300)
+    assert p.returncode == 0, p.stderr[-4000:]
+    return json.loads([ln for ln in p.stdout.splitlines() if ln.startswith("{")][-1])
+
+
+def test_bench_two_ranks_abr_ladder_with_churn():
+    # BASELINE config 3 through the driver's launch path (torchrun + bench.py), gloo on CPU:
+    # with churn, a rank masked offline fetches everything from the CDN, so the swarm
+    # offload ratio drops below the churn-free run's; nothing errors either way
+    calm = _bench_cpu(_free_port())
+    churn = _bench_cpu(_free_port(), "--churn", "2")
+    assert calm["errors"] == 0 and churn["errors"] == 0
+    assert calm["n_gpus"] == 2 and churn["config"]["churn_steps"] == 2
+    assert 0 < churn["offload_ratio"] < calm["offload_ratio"]
+
+
 def _peer4(rank: int, world: int, port: int, q) -> None:
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world))
     import torch.distributed as dist
