@@ -66,6 +66,9 @@ def parse():
                         "tensors through host memory: multi-rank rehearsal on a single GPU)")
     p.add_argument("--sync-steps", action="store_true",
                    help="no software pipelining: each step = load, round, transmux, synchronously")
+    p.add_argument("--lag", type=int, default=2,
+                   help="swarm rounds in flight on the device before the host completes the oldest "
+                        "(2: the next round's CDN DMA is always queued behind the current one)")
     p.add_argument("--churn", type=int, default=0, metavar="N",
                    help="swarm churn (BASELINE config 3): every N steps the next rank goes offline for N "
                         "steps (masked in the control plane: it neither serves nor receives P2P), then "
@@ -120,7 +123,7 @@ def main() -> int:
                                "cacheBytes": int(args.cache_gb * (1 << 30)), "autoTick": False,
                                "cdnDedup": not args.no_dedup, "maxWantsPerRound": K}}
     node = node_for_config(p2p_config)
-    depth = 1 if args.sync_steps else 3  # rounds a fragment spends in flight (see step())
+    depth = 1 if args.sync_steps else args.lag + 2  # rounds a fragment spends in flight (see step())
     hls_config = {"maxFragLoadsInFlight": K * depth, "maxBufferLength": 1e9, "maxMaxBufferLength": 1e9,
                   "startPosition": 0, "fragLoadingTimeOut": 600_000, "tickInterval": 1e9}
     if preset != "abr5":
@@ -160,13 +163,16 @@ def main() -> int:
 
     bt = PhaseTimer()
 
-    # Software pipeline over steps (steady state, 3 rounds in flight per peer):
-    #   launch round t+1 (collective; device: H2D / RCCL / CRC on the node stream)
+    # Software pipeline over steps (steady state, --lag + 2 rounds of fragments per peer):
+    #   launch round t+lag (collective; device: H2D on the copy stream, RCCL / CRC on the node
+    #     stream), so the DMA engine always has the next round queued behind the current one
     #   complete round t  -> onSuccess -> FRAG_LOADED -> transmux submit
-    #   launch transmux batch t (decrypt + demux on the default stream, overlaps round t+1)
+    #   launch transmux batch t (decrypt + demux on the default stream, overlaps the rounds in flight)
     #   complete transmux batch t-1 -> FRAG_BUFFERED -> slots free -> player issues loads
     pipe.auto_flush = args.sync_steps
-    state = {"h": None, "b": None, "step": 0, "offline_steps": 0}
+    import collections
+
+    state = {"hs": collections.deque(), "b": None, "step": 0, "offline_steps": 0}
 
     def churn():
         # rotation: rank k is offline during the k-th N-step period of every (world + 1) periods
@@ -190,10 +196,10 @@ def main() -> int:
             pipe.flush()
             drain_ready()
         else:
-            h = node.launch_round()
+            state["hs"].append(node.launch_round())
             t1 = time.perf_counter()
-            if state["h"] is not None:
-                node.complete_round(state["h"])
+            if len(state["hs"]) > args.lag:
+                node.complete_round(state["hs"].popleft())
             drain_ready()
             t2 = time.perf_counter()
             b = pipe.launch()
@@ -211,7 +217,7 @@ def main() -> int:
             bt.add("c3_drain", t25 - t22)
             sc.tick()
             drain_ready()
-            state["h"], state["b"] = h, b
+            state["b"] = b
             bt.add("d_player_loads", time.perf_counter() - t25)
         t3 = time.perf_counter()
         bt.add("a_launch_or_tick", t1 - t0)

@@ -423,12 +423,12 @@ class SwarmNode:
         recv_rows = plan[(plan[:, 6] == me) & (plan[:, 5] >= 0)]
         h.n_send = len(send_rows)
         # ---------------- 2. pin what we send from cache (seeded rows come from the CDN phase)
-        cached_send = send_rows[send_rows[:, 8] == 0]
-        send_ids: Dict[Tuple[int, int, int, int], int] = {}
-        if len(cached_send):
-            ids = self.store.lookup(np.ascontiguousarray(cached_send[:, :4]), False)
-            for row, eid in zip(cached_send.tolist(), ids.tolist()):
-                send_ids[tuple(row[:4])] = eid
+        # send_eids[i]: store entry of send row i (-1: missing), aligned with send_rows
+        send_eids = np.full(len(send_rows), -1, dtype=np.int64)
+        cached = send_rows[:, 8] == 0
+        if cached.any():
+            ids = self.store.lookup(np.ascontiguousarray(send_rows[cached, :4]), False)
+            send_eids[cached] = ids
             valid = ids[ids >= 0]
             if len(valid):
                 self.store.pin(valid)
@@ -439,15 +439,17 @@ class SwarmNode:
             # ---------------- 3. CDN phase (pinned host -> HBM, DMA engines)
             if len(cdn_rows):
                 self._cdn_phase(h, cdn_rows)
-                for w, eid, off, n in h.cdn_entries:
-                    send_ids.setdefault(w.key, eid)
+                seeded = np.flatnonzero(~cached)
+                if len(seeded) and h.cdn_entries:  # forwarded in this same round
+                    fetched = {w.key: eid for w, eid, _, _ in h.cdn_entries}
+                    send_eids[seeded] = [fetched.get(k, -1) for k in map(tuple, send_rows[seeded, :4].tolist())]
             t_p2p0 = time.perf_counter()
             self.timer.add("cdn_enqueue", t_p2p0 - t_cdn0)
             # ---------------- 4. P2P phase: entered by EVERY rank when the (identical) plan
             # has any transfer, so a collective transport (the in-process hub) stays in step;
             # RCCL point-to-point with no local ops posts nothing
             if bool((plan[:, 5] >= 0).any()):
-                self._p2p_phase(h, send_rows, recv_rows, send_ids)
+                self._p2p_phase(h, send_rows, recv_rows, send_eids)
             h.sent_bytes = int(send_rows[:, 4].sum()) if len(send_rows) else 0
             if self.is_cuda:
                 h.done = torch.cuda.Event()
@@ -637,61 +639,72 @@ class SwarmNode:
         self.stats["cdn_segments"] += len(wants)
         h.cdn_entries = [(w, eid, o, n) for w, eid, o, n in zip(wants, ids.tolist(), offs.tolist(), lens.tolist())]
 
-    def _p2p_phase(self, h: RoundHandle, send_rows: np.ndarray, recv_rows: np.ndarray, send_ids: Dict) -> None:
+    def _p2p_phase(self, h: RoundHandle, send_rows: np.ndarray, recv_rows: np.ndarray,
+                   send_eids: np.ndarray) -> None:
+        """Post this round's transfers.  Plan rows arrive sorted by (src, dst, key), so each
+        peer's rows are one contiguous run.  Bookkeeping is batched over ALL peers: one
+        gather of the send CRC trailers, one trailer buffer for every receive, one H2D of the
+        received entry ids (per-peer tensor ops cost ~30 us of host time each at 7 peers)."""
         sends: List[Tuple[int, torch.Tensor]] = []
         recvs: List[Tuple[int, torch.Tensor]] = []
         dev = self.device
+        t_prep = time.perf_counter()
         # --- sends: one contiguous buffer (+ CRC trailer) per destination
-        for dst in (np.unique(send_rows[:, 6]).tolist() if len(send_rows) else []):
-            rows = send_rows[send_rows[:, 6] == dst]
-            ids = np.asarray([send_ids.get(tuple(r[:4]), -1) for r in rows.tolist()], dtype=np.int64)
-            present = ids >= 0
-            sizes = rows[:, 4]
-            contiguous = False
-            if present.all():
-                ent = self.store.entries(ids)
-                offs, lens = ent[:, 0], ent[:, 1]
-                contiguous = bool(np.all(offs[1:] == offs[:-1] + (lens[:-1] + ALIGN - 1) // ALIGN * ALIGN)
-                                  and np.all(lens == sizes))
-            if contiguous:
-                total = int(offs[-1] + lens[-1] - offs[0])
-                buf = self.arena[int(offs[0]):int(offs[0]) + total]
-                trailer = self.crc_dev[torch.from_numpy(ids).to(dev, non_blocking=True)]
-            else:
-                layout = np.zeros(len(rows), dtype=np.int64)
-                if len(rows) > 1:
-                    layout[1:] = np.cumsum((sizes[:-1] + ALIGN - 1) // ALIGN * ALIGN)
-                total = int(layout[-1] + sizes[-1])
-                buf = torch.zeros(total, dtype=torch.uint8, device=dev)
-                trailer = torch.full((len(rows),), -1, dtype=torch.int32, device=dev)  # missing: bad CRC
-                if present.any():
-                    ent = self.store.entries(ids[present])
-                    n_copy = np.minimum(ent[:, 1], sizes[present])
-                    _seg.copy_segments(self.arena, buf, ent[:, 0], layout[present], n_copy)
-                    pidx = torch.from_numpy(np.nonzero(present)[0]).to(dev)
-                    trailer[pidx] = self.crc_dev[torch.from_numpy(ids[present]).to(dev)]
-            sends.append((int(dst), buf))
-            sends.append((int(dst), trailer.contiguous()))
-        # --- recvs: reserve one contiguous run per source
-        trailers = []
-        for src in (np.unique(recv_rows[:, 5]).tolist() if len(recv_rows) else []):
-            rows = recv_rows[recv_rows[:, 5] == src]
-            keys = np.ascontiguousarray(rows[:, :4])
-            lens = np.ascontiguousarray(rows[:, 4])
+        if len(send_rows):
+            present_all = send_eids >= 0
+            trailer_all = self.crc_dev[torch.from_numpy(np.where(present_all, send_eids, 0)).to(dev, non_blocking=True)]
+            if not present_all.all():  # missing entry: a bad CRC, the receiver re-fetches from the CDN
+                trailer_all[torch.from_numpy(np.flatnonzero(~present_all)).to(dev)] = -1
+            for dst, a, b in _runs(send_rows[:, 6]):
+                ids = send_eids[a:b]
+                present = present_all[a:b]
+                sizes = send_rows[a:b, 4]
+                contiguous = False
+                if present.all():
+                    ent = self.store.entries(ids)
+                    offs, lens = ent[:, 0], ent[:, 1]
+                    contiguous = bool(np.all(offs[1:] == offs[:-1] + (lens[:-1] + ALIGN - 1) // ALIGN * ALIGN)
+                                      and np.all(lens == sizes))
+                if contiguous:
+                    total = int(offs[-1] + lens[-1] - offs[0])
+                    buf = self.arena[int(offs[0]):int(offs[0]) + total]
+                else:
+                    layout = np.zeros(b - a, dtype=np.int64)
+                    if b - a > 1:
+                        layout[1:] = np.cumsum((sizes[:-1] + ALIGN - 1) // ALIGN * ALIGN)
+                    total = int(layout[-1] + sizes[-1])
+                    buf = torch.zeros(total, dtype=torch.uint8, device=dev)
+                    if present.any():
+                        ent = self.store.entries(ids[present])
+                        n_copy = np.minimum(ent[:, 1], sizes[present])
+                        _seg.copy_segments(self.arena, buf, ent[:, 0], layout[present], n_copy)
+                sends.append((dst, buf))
+                sends.append((dst, trailer_all[a:b]))
+        # --- recvs: reserve one contiguous run per source; one trailer buffer for all of them
+        trailers = torch.empty(len(recv_rows), dtype=torch.int32, device=dev) if len(recv_rows) else None
+        rid, roff, rlen, rsrc = [], [], [], []
+        for src, a, b in _runs(recv_rows[:, 5]):
+            keys = np.ascontiguousarray(recv_rows[a:b, :4])
+            lens = np.ascontiguousarray(recv_rows[a:b, 4])
             res = self.store.reserve_run(keys, lens, self.round)
             if res is None:  # _admit guarantees room
                 raise RuntimeError("segment cache cannot make room for peer data")
             base, ids, offs = res
             self.store.pin(ids)
             h.hold.append(ids)
-            self._grow_crc(int(ids.max()) + 1)
             total = int(offs[-1] + lens[-1] - offs[0])
-            recvs.append((int(src), self.arena[int(base):int(base) + total]))
-            tr = torch.empty(len(rows), dtype=torch.int32, device=dev)
-            recvs.append((int(src), tr))
-            trailers.append(tr)
-            h.recv_entries.extend(zip(rows[:, 7].tolist(), [int(src)] * len(rows), ids.tolist(), offs.tolist(),
-                                      lens.tolist()))
+            recvs.append((src, self.arena[int(base):int(base) + total]))
+            recvs.append((src, trailers[a:b]))
+            rid.append(ids)
+            roff.append(offs)
+            rlen.append(lens)
+            rsrc.append(np.full(b - a, src, dtype=np.int64))
+        if rid:
+            rid_a = np.concatenate(rid)
+            self._grow_crc(int(rid_a.max()) + 1)
+            h.recv_entries = list(zip(recv_rows[:, 7].tolist(), np.concatenate(rsrc).tolist(), rid_a.tolist(),
+                                      np.concatenate(roff).tolist(), np.concatenate(rlen).tolist()))
+        self.timer.add("p2p_prep", time.perf_counter() - t_prep)
         t = time.perf_counter()
         if self.is_cuda:
             start = torch.cuda.Event(enable_timing=True)
@@ -710,11 +723,10 @@ class SwarmNode:
             o, n = h.recv_entries[0][3:5]
             if n:
                 self.arena[o + n // 2] ^= 0x5A
-        expect = torch.cat(trailers)
-        ents = h.recv_entries
-        ids_t = torch.from_numpy(np.asarray([e[2] for e in ents], dtype=np.int64)).to(dev, non_blocking=True)
+        expect = trailers
+        ids_t = torch.from_numpy(rid_a).to(dev, non_blocking=True)
         self.crc_dev[ids_t] = expect
-        _, ok = _crc.crc32_batch(self.arena, [e[3] for e in ents], [e[4] for e in ents], expect_dev=expect)
+        _, ok = _crc.crc32_batch(self.arena, np.concatenate(roff), np.concatenate(rlen), expect_dev=expect)
         if self.is_cuda:
             h.ok_host = torch.empty(ok.numel(), dtype=torch.uint8, pin_memory=True)
             h.ok_host.copy_(ok, non_blocking=True)
@@ -823,6 +835,17 @@ class SwarmNode:
     def swarm_offload_ratio(self) -> float:
         c, p = self.swarm_stats["cdn"], self.swarm_stats["p2p"]
         return p / (p + c) if (p + c) else 0.0
+
+
+def _runs(col: np.ndarray) -> List[Tuple[int, int, int]]:
+    """(value, start, end) of each run of equal values in a sorted column."""
+    n = len(col)
+    if n == 0:
+        return []
+    cuts = np.flatnonzero(col[1:] != col[:-1]) + 1
+    starts = [0] + cuts.tolist()
+    ends = cuts.tolist() + [n]
+    return list(zip(col[starts].tolist(), starts, ends))
 
 
 def _h2d_batch(arena: torch.Tensor, dst_offs: np.ndarray, sources: List[Tuple[torch.Tensor, int, int, bool]]) -> None:
