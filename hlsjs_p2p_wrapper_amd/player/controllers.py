@@ -591,7 +591,7 @@ class StreamController:
         pipeline_for(dev, self.loop).submit(
             TransmuxJob(payload, key, iv, lambda r: self._on_parsed(frag, stats, r), frag))
 
-    def _on_parsed(self, frag: Fragment, stats: Any, r: Dict[str, Any]) -> None:
+    def _on_parsed(self, frag: Fragment, stats: Any, r: Any) -> None:  # r: dict-like transmux result
         hls = self.hls
         key = (frag.level, frag.sn)
         if self.inflight.get(key) is not frag:
@@ -631,7 +631,8 @@ class StreamController:
         if listening(Events.FRAG_PARSED):
             hls.trigger(Events.FRAG_PARSED, {"frag": frag})
         media = hls.media
-        nbytes = int(r["video"].numel() + r["audio"].numel())
+        vb, ab = info.get("video_bytes"), info.get("audio_bytes")  # the ES views stay unbuilt
+        nbytes = int(vb + ab) if vb is not None and ab is not None else int(r["video"].numel() + r["audio"].numel())
         if listening(Events.BUFFER_APPENDING):
             hls.trigger(Events.BUFFER_APPENDING, {"type": "video", "parent": "main", "bytes": nbytes})
         if media is not None:

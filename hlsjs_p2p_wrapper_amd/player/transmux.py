@@ -202,31 +202,13 @@ class MediaPipeline:
             hinfo = hinfo.numpy() if isinstance(hinfo, torch.Tensor) else hinfo
             plain_lens = hlens.numpy() if isinstance(hlens, torch.Tensor) else hlens
             rows = hinfo.tolist()
-            # ES views of the whole group in ONE split (video | audio | id3 | pad per
-            # segment) instead of three ATen slicing calls per fragment
-            cuts, first, pos = [], [], 0
-            for k in range(len(idx)):
-                row, base = rows[k], es_offs[k]
-                if base > pos:
-                    cuts.append(base - pos)  # alignment gap before this segment's ES
-                first.append(len(cuts))
-                cuts += [row[_VB], row[_AB], row[_IB]]
-                pos = base + row[_VB] + row[_AB] + row[_IB]
-            cuts.append(res.es.numel() - pos)
-            views = torch.split(res.es, cuts)
+            es = res.es
             for k, i in enumerate(idx):
                 row = rows[k]
-                video, audio, id3 = views[first[k]], views[first[k] + 1], views[first[k] + 2]
-                r = {
-                    "status": row[0],
-                    "info": InfoRow(row),
-                    "plain_bytes": int(plain_lens[k]),
-                    "video": video,
-                    "audio": audio,
-                    "id3": id3,
-                    "demux": res,
-                    "index": k,
-                }
+                # ES views (video | audio | id3 at es_offs[k]) are built on first access: the
+                # buffer path only needs their byte counts, which the info row holds
+                r = _Result(status=row[0], info=InfoRow(row), plain_bytes=int(plain_lens[k]), demux=res, index=k)
+                r._es = (es, es_offs[k], row[_VB], row[_AB], row[_IB])
                 if plain_lens[k] < 0:
                     r["error"] = ValueError("decryption failed (bad PKCS#7 padding)")
                 results[i] = r
@@ -235,6 +217,24 @@ class MediaPipeline:
 
 
 _VB, _AB, _IB = _ts.INFO["video_bytes"], _ts.INFO["audio_bytes"], _ts.INFO["id3_bytes"]
+
+
+class _Result(dict):
+    """One fragment's transmux result: ``status``, ``info``, ``plain_bytes``, ``demux``,
+    ``index`` (and ``error``) stored; ``video`` / ``audio`` / ``id3`` ES views of the batch's
+    ES buffer made on first access."""
+
+    __slots__ = ("_es",)
+
+    def __missing__(self, key):
+        if key not in ("video", "audio", "id3"):
+            raise KeyError(key)
+        es, base, vb, ab, ib = self._es
+        v = es.narrow(0, base, vb)
+        a = es.narrow(0, base + vb, ab)
+        i = es.narrow(0, base + vb + ab, ib)
+        self["video"], self["audio"], self["id3"] = v, a, i
+        return self[key]
 
 
 class InfoRow:
