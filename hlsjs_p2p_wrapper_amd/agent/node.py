@@ -134,6 +134,21 @@ class RoundHandle:
     completed: bool = False
 
 
+class _EventPool:
+    """Recycled HIP events (a fresh torch.cuda.Event costs ~5 us of host time; a round uses
+    five).  An event goes back to the pool only after the host has waited on its round."""
+
+    def __init__(self) -> None:
+        self._free: Dict[bool, List[Any]] = {True: [], False: []}
+
+    def get(self, timing: bool = False):
+        free = self._free[timing]
+        return free.pop() if free else torch.cuda.Event(enable_timing=timing)
+
+    def put(self, timing: bool, *events) -> None:
+        self._free[timing].extend(e for e in events if e is not None)
+
+
 class SwarmNode:
     def __init__(self, comm: Optional[SwarmComm] = None, device: Any = "auto", cache_bytes: int = 1 << 30,
                  loop=None, cdn_dedup: bool = True, round_interval_ms: Optional[float] = None,
@@ -162,6 +177,7 @@ class SwarmNode:
         self.stream = torch.cuda.Stream(self.device) if self.is_cuda else None
         self.copy_stream = (torch.cuda.Stream(self.device) if self.is_cuda and
                             os.environ.get("HLSP2P_COPY_STREAM", "1") != "0" else None)
+        self._events = _EventPool()
         self.online = True
         self.upload_on = True
         self.download_on = True
@@ -452,7 +468,7 @@ class SwarmNode:
                 self._p2p_phase(h, send_rows, recv_rows, send_eids)
             h.sent_bytes = int(send_rows[:, 4].sum()) if len(send_rows) else 0
             if self.is_cuda:
-                h.done = torch.cuda.Event()
+                h.done = self._events.get()
                 h.done.record()
         self.timer.add("p2p_enqueue", time.perf_counter() - t_p2p0)
         return h
@@ -472,8 +488,13 @@ class SwarmNode:
         self.timer.add("wait_device", t1 - t0)
         if h.ev_cdn is not None:
             h.cdn_ms = h.ev_cdn[0].elapsed_time(h.ev_cdn[1])
+            self._events.put(True, *h.ev_cdn)
         if h.ev_p2p is not None:
             h.p2p_ms = h.ev_p2p[0].elapsed_time(h.ev_p2p[1])
+            self._events.put(True, *h.ev_p2p)
+        if h.done is not None:
+            self._events.put(False, h.done)
+            h.done = None
         okl = h.ok_host.numpy().tolist() if h.ok_host is not None else None
         if okl is None or all(okl):
             good, bad = h.recv_entries, []
@@ -611,8 +632,8 @@ class SwarmNode:
         h.hold.append(ids)
         self._grow_crc(int(ids.max()) + 1)
         if self.is_cuda:
-            start = torch.cuda.Event(enable_timing=True)
-            end = torch.cuda.Event(enable_timing=True)
+            start = self._events.get(True)
+            end = self._events.get(True)
             cs = self.copy_stream
             with (torch.cuda.stream(cs) if cs is not None else contextlib.nullcontext()):
                 start.record()
@@ -707,8 +728,8 @@ class SwarmNode:
         self.timer.add("p2p_prep", time.perf_counter() - t_prep)
         t = time.perf_counter()
         if self.is_cuda:
-            start = torch.cuda.Event(enable_timing=True)
-            end = torch.cuda.Event(enable_timing=True)
+            start = self._events.get(True)
+            end = self._events.get(True)
             start.record()
         self.comm.exchange(sends, recvs)
         if self.is_cuda:

@@ -28,6 +28,11 @@ def pack_to_device(arrays: Dict[str, np.ndarray], device: torch.device) -> Dict[
     """Copy ``arrays`` to ``device`` in one transfer; returns typed device views.
 
     ``uint32`` arrays come back as ``int32`` views (same bits)."""
+    if device.type == "cuda":  # native: one memcpy per array into the pinned block, one H2D
+        from ._native import device as _dev
+
+        idx = device.index if device.index is not None else torch.cuda.current_device()
+        return dict(zip(arrays.keys(), _dev().pack_h2d(list(arrays.values()), idx)))
     layout: List[Tuple[str, int, np.ndarray]] = []
     off = 0
     for name, a in arrays.items():
