@@ -137,3 +137,29 @@ def test_copy_segments(cuda):
     segment.copy_segments(src, dst, so, do, n)
     for a, b, c in zip(so, do, n):
         assert torch.equal(dst[b:b + c], src[a:a + c])
+
+
+def test_pack_to_device_native_dtypes_and_layout(cuda):
+    # the native descriptor packer (one pinned block, one H2D): every dtype the launchers
+    # use, uint32 as int32 bits, non-contiguous input, odd sizes (16-byte sub-array padding)
+    from hlsjs_p2p_wrapper_amd.ops.desc import pack_to_device
+
+    rng = np.random.default_rng(5)
+    arrays = {
+        "i64": rng.integers(-2**40, 2**40, 7, dtype=np.int64),
+        "u32": rng.integers(0, 2**32, 13, dtype=np.uint32),
+        "i32": rng.integers(-2**31, 2**31, 3, dtype=np.int32),
+        "u8": rng.integers(0, 256, (5, 16), dtype=np.uint8),
+        "f64": rng.random(9),
+        "strided": np.arange(40, dtype=np.int64)[::3],
+        "empty": np.zeros(0, dtype=np.int64),
+    }
+    out = pack_to_device(arrays, cuda)
+    assert list(out) == list(arrays)
+    for name, a in arrays.items():
+        t = out[name]
+        assert t.device.type == "cuda" and t.numel() == a.size
+        ref = a.reshape(-1).view(np.int32) if a.dtype == np.uint32 else a.reshape(-1)
+        assert np.array_equal(t.cpu().numpy(), ref), name
+        if t.numel():
+            assert t.data_ptr() % 16 == 0
