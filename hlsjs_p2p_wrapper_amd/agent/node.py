@@ -469,7 +469,7 @@ class SwarmNode:
             h.sent_bytes = int(send_rows[:, 4].sum()) if len(send_rows) else 0
             if self.is_cuda:
                 h.done = self._events.get()
-                h.done.record()
+                h.done.record(self.stream)  # explicit stream: skips torch's current_stream() lookup
         self.timer.add("p2p_enqueue", time.perf_counter() - t_p2p0)
         return h
 
@@ -636,9 +636,9 @@ class SwarmNode:
             end = self._events.get(True)
             cs = self.copy_stream
             with (torch.cuda.stream(cs) if cs is not None else contextlib.nullcontext()):
-                start.record()
+                start.record(cs if cs is not None else self.stream)
                 h.dmas = _h2d_batch(self.arena, offs, sources)
-                end.record()
+                end.record(cs if cs is not None else self.stream)
             if cs is not None:
                 self.stream.wait_event(end)  # ingest CRC / forwarding sends read the DMA'd bytes
             h.ev_cdn = (start, end)
@@ -650,8 +650,7 @@ class SwarmNode:
         for (_, _, n, corrupt), doff in zip(sources, offs.tolist()):
             if corrupt and n:
                 self.arena[doff + n // 2] ^= 0xFF
-        crc, _ = _crc.crc32_batch(self.arena, offs.tolist(), lens.tolist())
-        self.crc_dev[torch.from_numpy(ids).to(self.device, non_blocking=True)] = crc
+        _crc.crc32_batch(self.arena, offs, lens, scatter_to=self.crc_dev, scatter_idx=ids)  # ingest CRCs
         self.store.commit(ids)  # announced next round; peers' reads are stream-ordered after the H2D
         # CDN bandwidth shaping (xhr-shaper analog): completions are deferred by the modelled
         # transfer time of this round's CDN bytes
@@ -730,10 +729,10 @@ class SwarmNode:
         if self.is_cuda:
             start = self._events.get(True)
             end = self._events.get(True)
-            start.record()
+            start.record(self.stream)  # launch_round runs this phase on the node stream
         self.comm.exchange(sends, recvs)
         if self.is_cuda:
-            end.record()
+            end.record(self.stream)
             h.ev_p2p = (start, end)
         else:
             h.p2p_ms = (time.perf_counter() - t) * 1e3

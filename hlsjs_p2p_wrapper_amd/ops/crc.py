@@ -38,11 +38,15 @@ def _device_consts(device: torch.device):
 
 def crc32_batch(buf: torch.Tensor, offs: Sequence[int], lens: Sequence[int],
                 expect: Optional[Sequence[int]] = None,
-                expect_dev: Optional[torch.Tensor] = None) -> Tuple[torch.Tensor, Optional[torch.Tensor]]:
+                expect_dev: Optional[torch.Tensor] = None, scatter_to: Optional[torch.Tensor] = None,
+                scatter_idx: Optional[Sequence[int]] = None) -> Tuple[torch.Tensor, Optional[torch.Tensor]]:
     """CRC-32 of ``buf[offs[i]:offs[i]+lens[i]]``.
 
     Returns ``(crc int32[B], ok uint8[B] | None)`` on ``buf.device``; ``ok`` is produced
     when expected values are given (host list ``expect`` or device tensor ``expect_dev``).
+    With ``scatter_to`` (int32 table on ``buf.device``) the CRCs are also written to
+    ``scatter_to[scatter_idx[i]]`` -- on the device by the combine kernel, whose index
+    array rides the same descriptor H2D (no separate index copy / index_put launch).
     """
     B = len(offs)
     o = np.asarray(offs, dtype=np.int64)
@@ -52,6 +56,11 @@ def crc32_batch(buf: torch.Tensor, offs: Sequence[int], lens: Sequence[int],
         return z, (torch.empty(0, dtype=torch.uint8, device=buf.device) if (expect is not None or expect_dev is not None) else None)
     if np.any(o < 0) or np.any(n < 0) or np.any(o + n > buf.numel()):
         raise ValueError("crc32_batch: range out of bounds")
+    sidx = None
+    if scatter_to is not None:
+        sidx = np.asarray(scatter_idx, dtype=np.int64).reshape(-1)
+        if sidx.size != B or np.any(sidx < 0) or np.any(sidx >= scatter_to.numel()):
+            raise ValueError("crc32_batch: scatter index out of range")
     if buf.device.type == "cpu":
         crc = _rt().crc32_batch(buf.numpy(), o, n).view(np.int32)
         crc_t = torch.from_numpy(crc.copy())
@@ -61,6 +70,8 @@ def crc32_batch(buf: torch.Tensor, offs: Sequence[int], lens: Sequence[int],
         elif expect is not None:
             exp = np.asarray(expect, dtype=np.uint32).view(np.int32)
             ok = torch.from_numpy((crc == exp).astype(np.uint8))
+        if sidx is not None:
+            scatter_to[torch.from_numpy(sidx)] = crc_t
         return crc_t, ok
     if np.any(o % 16):
         raise ValueError("crc32_batch: offsets must be 16-byte aligned on device")
@@ -74,6 +85,8 @@ def crc32_batch(buf: torch.Tensor, offs: Sequence[int], lens: Sequence[int],
     arrays = {"o": o, "n": n, "tp": tile_prefix, "ro": res_off}
     if expect is not None and expect_dev is None:
         arrays["ex"] = np.asarray(expect, dtype=np.uint32)
+    if sidx is not None:
+        arrays["si"] = sidx
     d = pack_to_device(arrays, buf.device)
     w, tables = _device_consts(buf.device)
     residues = torch.empty(max(1, int(groups.sum())), dtype=torch.int32, device=buf.device)
@@ -81,7 +94,7 @@ def crc32_batch(buf: torch.Tensor, offs: Sequence[int], lens: Sequence[int],
     exp_t = expect_dev if expect_dev is not None else d.get("ex")
     ok = torch.empty(B, dtype=torch.uint8, device=buf.device) if exp_t is not None else None
     _dev().crc32_batch(buf, d["o"], d["n"], d["tp"], d["ro"], w, tables, residues, crc, exp_t, ok,
-                       int(tile_prefix[-1]))
+                       int(tile_prefix[-1]), d.get("si"), scatter_to)
     return crc, ok
 
 

@@ -15,8 +15,8 @@ hipError_t launch_aes128_cbc_decrypt(const uint8_t*, uint8_t*, const int64_t*, c
                                      const int64_t*, const uint32_t*, const uint32_t*, const uint32_t*,
                                      const uint8_t*, int64_t*, int, int64_t, int, hipStream_t);
 hipError_t launch_crc32_batch(const uint8_t*, const int64_t*, const int64_t*, const int64_t*, const int64_t*,
-                              const void*, const uint32_t*, uint32_t*, uint32_t*, const uint32_t*, uint8_t*, int,
-                              int64_t, int, hipStream_t);
+                              const void*, const uint32_t*, uint32_t*, uint32_t*, const uint32_t*, uint8_t*,
+                              const int64_t*, uint32_t*, int64_t, int, int64_t, int, hipStream_t);
 hipError_t launch_ts_demux(const uint8_t*, const int64_t*, const int64_t*, const int64_t*, int, int64_t, uint32_t*,
                            int64_t*, int32_t*, uint8_t*, const int64_t*, int64_t*, int64_t, int64_t*, hipStream_t);
 hipError_t launch_range_select(const double*, const int64_t*, const int64_t*, const double*, const double*, int64_t*,
@@ -96,7 +96,8 @@ void aes128_cbc_decrypt(Tensor src, Tensor dst, Tensor src_off, Tensor dst_off, 
 
 void crc32_batch(Tensor buf, Tensor seg_off, Tensor seg_len, Tensor tile_prefix, Tensor res_off, Tensor wfrag,
                  Tensor tables, Tensor residues, Tensor crc_out, c10::optional<Tensor> expect,
-                 c10::optional<Tensor> ok_out, int64_t total_tiles) {
+                 c10::optional<Tensor> ok_out, int64_t total_tiles, c10::optional<Tensor> scatter_idx,
+                 c10::optional<Tensor> scatter_out) {
   const int64_t B = seg_off.numel();
   check(buf, "buf", torch::kUInt8);
   check(seg_off, "seg_off", torch::kInt64);
@@ -118,10 +119,21 @@ void crc32_batch(Tensor buf, Tensor seg_off, Tensor seg_len, Tensor tile_prefix,
     check(*ok_out, "ok_out", torch::kUInt8, B);
     okp = mptr<uint8_t>(*ok_out);
   }
+  const int64_t* sidx = nullptr;
+  uint32_t* sout = nullptr;
+  int64_t sn = 0;
+  TORCH_CHECK(scatter_idx.has_value() == scatter_out.has_value(), "scatter_idx and scatter_out go together");
+  if (scatter_out.has_value()) {
+    check(*scatter_idx, "scatter_idx", torch::kInt64, B);
+    check(*scatter_out, "scatter_out", torch::kInt32);
+    sidx = cptr<int64_t>(*scatter_idx);
+    sout = mptr<uint32_t>(*scatter_out);
+    sn = scatter_out->numel();
+  }
   ok(D::launch_crc32_batch(cptr<uint8_t>(buf), cptr<int64_t>(seg_off), cptr<int64_t>(seg_len),
                            cptr<int64_t>(tile_prefix), cptr<int64_t>(res_off), wfrag.data_ptr(),
                            cptr<uint32_t>(tables), mptr<uint32_t>(residues), mptr<uint32_t>(crc_out), ex, okp,
-                           static_cast<int>(B), total_tiles, num_cus(buf), stream()),
+                           sidx, sout, sn, static_cast<int>(B), total_tiles, num_cus(buf), stream()),
      "crc32_batch");
 }
 
@@ -308,7 +320,11 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.doc() = "hlsjs-p2p-wrapper-amd CDNA4 (gfx950) kernels";
   m.def("aes128_cbc_decrypt", &aes128_cbc_decrypt);
   m.def("aes_chunk_blocks", &D::aes_chunk_blocks);
-  m.def("crc32_batch", &crc32_batch);
+  namespace py = pybind11;
+  m.def("crc32_batch", &crc32_batch, py::arg("buf"), py::arg("seg_off"), py::arg("seg_len"), py::arg("tile_prefix"),
+        py::arg("res_off"), py::arg("wfrag"), py::arg("tables"), py::arg("residues"), py::arg("crc_out"),
+        py::arg("expect"), py::arg("ok_out"), py::arg("total_tiles"), py::arg("scatter_idx") = py::none(),
+        py::arg("scatter_out") = py::none());
   m.def("ts_demux", &ts_demux);
   m.def("range_select", &range_select);
   m.def("key_hash", &key_hash);

@@ -164,7 +164,8 @@ constexpr uint32_t kInitFold = 0xf2697aa7u;
 __global__ __launch_bounds__(kCombineThreads) void crc32_combine_kernel(
     const uint32_t* __restrict__ residues, const int64_t* __restrict__ res_off, const int64_t* __restrict__ seg_len,
     const uint32_t* __restrict__ tables, uint32_t* __restrict__ crc_out, const uint32_t* __restrict__ expect,
-    uint8_t* __restrict__ ok_out) {
+    uint8_t* __restrict__ ok_out, const int64_t* __restrict__ scatter_idx, uint32_t* __restrict__ scatter_out,
+    int64_t scatter_n) {
   __shared__ __attribute__((aligned(16))) uint32_t s_tab[kCombineLdsTables * kSlice];  // 60 KiB
   __shared__ __attribute__((aligned(16))) uint32_t s_q[kNumQ * kSlice];                // 32 KiB
   __shared__ uint32_t s_acc[kCombineThreads];
@@ -234,13 +235,20 @@ __global__ __launch_bounds__(kCombineThreads) void crc32_combine_kernel(
     const uint32_t crc = raw ^ init ^ 0xFFFFFFFFu;
     crc_out[seg] = crc;
     if (ok_out) ok_out[seg] = (expect && expect[seg] == crc) ? 1 : 0;
+    // optional scatter into a per-entry CRC table (the cache's ingest CRCs): saves the
+    // caller an index H2D plus an index_put launch per round; out-of-range ids are dropped
+    if (scatter_out) {
+      const int64_t d = scatter_idx[seg];
+      if (d >= 0 && d < scatter_n) scatter_out[d] = crc;
+    }
   }
 }
 
 hipError_t launch_crc32_batch(const uint8_t* buf, const int64_t* seg_off, const int64_t* seg_len,
                               const int64_t* tile_prefix, const int64_t* res_off, const void* wfrag,
                               const uint32_t* tables, uint32_t* residues, uint32_t* crc_out, const uint32_t* expect,
-                              uint8_t* ok_out, int nseg, int64_t total_tiles, int num_cu, hipStream_t stream) {
+                              uint8_t* ok_out, const int64_t* scatter_idx, uint32_t* scatter_out, int64_t scatter_n,
+                              int nseg, int64_t total_tiles, int num_cu, hipStream_t stream) {
   if (nseg <= 0) return hipSuccess;
   if (total_tiles > 0) {
     const int64_t waves_max = static_cast<int64_t>(num_cu) * 2 * (kCrcThreads / 64);
@@ -255,7 +263,7 @@ hipError_t launch_crc32_batch(const uint8_t* buf, const int64_t* seg_off, const 
     if (e != hipSuccess) return e;
   }
   hipLaunchKernelGGL(crc32_combine_kernel, dim3(static_cast<unsigned>(nseg)), dim3(kCombineThreads), 0, stream,
-                     residues, res_off, seg_len, tables, crc_out, expect, ok_out);
+                     residues, res_off, seg_len, tables, crc_out, expect, ok_out, scatter_idx, scatter_out, scatter_n);
   return hipGetLastError();
 }
 

@@ -40,6 +40,27 @@ def test_crc32_mfma_matches_zlib(cuda):
     _ = rng
 
 
+@pytest.mark.parametrize("dev", ["cpu", "cuda"])
+def test_crc32_scatter_into_entry_table(dev, request):
+    # the ingest path writes each CRC to table[entry id] inside the combine kernel; slots not
+    # named keep their value, and an out-of-range id is refused on the host before any launch
+    device = request.getfixturevalue("cuda") if dev == "cuda" else torch.device("cpu")
+    lens = [0, 3, 256, 70001, 4096]
+    offs = [i * 81920 for i in range(len(lens))]
+    buf = _rand(offs[-1] + 81920, 11)
+    t = torch.from_numpy(buf).to(device)
+    table = torch.full((40,), 7, dtype=torch.int32, device=device)
+    ids = [31, 2, 17, 0, 39]
+    crc_t, _ = crc.crc32_batch(t, offs, lens, scatter_to=table, scatter_idx=ids)
+    expect = np.array([zlib.crc32(buf[o:o + n].tobytes()) for o, n in zip(offs, lens)], dtype=np.uint32)
+    ref = np.full(40, 7, dtype=np.int32)
+    ref[ids] = expect.view(np.int32)
+    assert np.array_equal(table.cpu().numpy(), ref)
+    assert np.array_equal(crc_t.cpu().numpy(), expect.view(np.int32))
+    with pytest.raises(ValueError):
+        crc.crc32_batch(t, offs[:1], lens[:1], scatter_to=table, scatter_idx=[40])
+
+
 def test_aes_cbc_decrypt_matches_host(cuda):
     B = 9
     keys = [bytes(np.random.default_rng(100 + i).integers(0, 256, 16, dtype=np.uint8)) for i in range(B)]
