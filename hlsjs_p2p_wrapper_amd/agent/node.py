@@ -206,6 +206,7 @@ class SwarmNode:
         # per-request trace records {key, trequest, tfirst, tload, source, bytes, peer, round}
         # (SURVEY §5.1); None = off (p2pConfig["gpuSwarm"]["trace"] or enable_trace())
         self.trace: Optional[TraceLog] = None
+        self.metrics_server: Any = None  # utils.metrics.MetricsServer (gpuSwarm.metricsPort)
         self._lock = threading.RLock()
         if self.world > 1 and auto_tick:
             self._timer = self.loop.set_interval(self._timer_tick, round_interval_ms or 10.0)
@@ -851,6 +852,9 @@ class SwarmNode:
                 if self.tick():
                     break
         self.closed = True
+        if self.metrics_server is not None:
+            self.metrics_server.close()
+            self.metrics_server = None
 
     def swarm_offload_ratio(self) -> float:
         c, p = self.swarm_stats["cdn"], self.swarm_stats["p2p"]
@@ -909,8 +913,9 @@ def node_for_config(p2p_config: Any) -> SwarmNode:
     ``gpuSwarm`` keys: ``backend`` ("auto" | "local" | "dist" | "thread"), ``hub`` and
     ``rank`` (thread backend), ``device``, ``cacheBytes``, ``cdnDedup``,
     ``roundIntervalMs``, ``autoTick``, ``maxWantsPerRound``, ``trace``, ``linkKbps``
-    (``{peer: kbit/s}`` slow-link fault injection); the agent reads ``prefetchSeconds`` /
-    ``prefetchMaxSegments``.
+    (``{peer: kbit/s}`` slow-link fault injection), ``metricsPort`` (serve Prometheus
+    ``GET /metrics`` on port + rank, 0 = ephemeral; ``metricsHost`` defaults to
+    127.0.0.1); the agent reads ``prefetchSeconds`` / ``prefetchMaxSegments``.
     """
     node = current_node()
     if node is not None and not node.closed:
@@ -941,5 +946,11 @@ def node_for_config(p2p_config: Any) -> SwarmNode:
         node.enable_trace()
     for peer, kbps in (cfg.get("linkKbps") or {}).items():
         node.set_link_bandwidth(int(peer), kbps)
+    if cfg.get("metricsPort") is not None:
+        from ..utils.metrics import MetricsServer
+
+        port = int(cfg["metricsPort"])
+        node.metrics_server = MetricsServer(node, port=port + node.rank if port else 0,
+                                            host=str(cfg.get("metricsHost", "127.0.0.1")))
     set_current_node(node)
     return node

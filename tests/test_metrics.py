@@ -1,0 +1,129 @@
+"""Metrics export: the reference ``stats`` counters, swarm offload ratio, HBM
+cache occupancy, phase timings and request-latency quantiles in the Prometheus text format,
+checked against a 2-peer in-process swarm (CPU, ThreadHub)."""
+import re
+import urllib.request
+
+import pytest
+
+from hlsjs_p2p_wrapper_amd.net.origin import Rendition, SyntheticHlsOrigin
+from hlsjs_p2p_wrapper_amd.utils.metrics import MetricsServer, agent_metrics, node_metrics, render
+
+from test_swarm import fresh, run_swarm  # noqa: F401 - fixture re-export
+
+_LV = r'"(?:[^"\\]|\\.)*"'  # a label value with escapes
+_SAMPLE = re.compile(r'^([a-zA-Z_:][a-zA-Z0-9_:]*)(\{([a-z_]+=' + _LV + r'(,[a-z_]+=' + _LV + r')*)\})? (-?[0-9.e+-]+|NaN)$')
+
+
+def parse(text):
+    """``{name: [(labels, value)]}``; asserts every line is valid exposition syntax and
+    that each family has exactly one HELP and one TYPE line, before its samples."""
+    fams, seen_help, seen_type = {}, set(), set()
+    for line in text.strip().split("\n"):
+        if line.startswith("# HELP "):
+            name = line.split()[2]
+            assert name not in seen_help, f"duplicate HELP for {name}"
+            seen_help.add(name)
+        elif line.startswith("# TYPE "):
+            _, _, name, kind = line.split()
+            assert kind in ("counter", "gauge", "summary"), line
+            assert name not in seen_type, f"duplicate TYPE for {name}"
+            seen_type.add(name)
+        else:
+            m = _SAMPLE.match(line)
+            assert m, f"bad sample line {line!r}"
+            name = m.group(1)
+            assert name in seen_type, f"sample before TYPE: {line!r}"
+            labels = dict(re.findall(r'([a-z_]+)="((?:[^"\\]|\\.)*)"', m.group(3) or ""))
+            fams.setdefault(name, []).append((labels, float(m.group(5))))
+    return fams
+
+
+def value(fams, name, **labels):
+    hits = [v for lab, v in fams[name] if all(lab.get(k) == str(x) for k, x in labels.items())]
+    assert len(hits) == 1, (name, labels, fams.get(name))
+    return hits[0]
+
+
+@pytest.fixture
+def vod():
+    return SyntheticHlsOrigin("http://cdn.metrics/vod/", renditions=[Rendition(1_000_000, 640, 360)],
+                              num_segments=10, encrypted=True)
+
+
+def test_render_format_and_merge():
+    fams = [("x_total", "counter", "h", [({"a": 'q"\\'}, 3.0)]), ("x_total", "counter", "h", [({"a": "b"}, 1.5)]),
+            ("y", "gauge", "g", [({}, 0.25)])]
+    text = render(fams)
+    parsed = parse(text)
+    assert parsed["x_total"] == [({"a": 'q\\"\\\\'}, 3.0), ({"a": "b"}, 1.5)]
+    assert "y 0.25\n" in text and "x_total{a=\"b\"} 1.5" in text
+
+
+def test_swarm_metrics_match_stats(vod):
+    nodes, wrappers = {}, {}
+
+    def before(r, node, w):
+        node.enable_trace()
+        nodes[r], wrappers[r] = node, w
+
+    out = run_swarm(2, vod, before=before)
+    seg_total = sum(vod.pools[0].lengths)
+    texts = {r: render(node_metrics(nodes[r]) + [f for a in nodes[r]._agents for f in agent_metrics(a)])
+             for r in nodes}
+    per = {r: parse(t) for r, t in texts.items()}
+    cdn = sum(value(per[r], "hlsp2p_cdn_bytes_total", rank=r) for r in per)
+    p2p = sum(value(per[r], "hlsp2p_p2p_bytes_total", rank=r) for r in per)
+    assert cdn == seg_total and p2p == seg_total  # each segment: one CDN fetch, one peer transfer
+    for r, f in per.items():
+        st = nodes[r].stats
+        assert value(f, "hlsp2p_upload_bytes_total", rank=r) == st["upload"]
+        assert value(f, "hlsp2p_rounds_total", rank=r) == st["rounds"] > 0
+        assert value(f, "hlsp2p_crc_failures_total", rank=r) == 0
+        assert value(f, "hlsp2p_swarm_offload_ratio", rank=r) == pytest.approx(out[r]["offload"]) == pytest.approx(0.5)
+        assert value(f, "hlsp2p_world_size", rank=r) == 2
+        assert value(f, "hlsp2p_cache_capacity_bytes", rank=r) == 128 << 20
+        assert 0 < value(f, "hlsp2p_cache_used_bytes", rank=r) <= 128 << 20
+        assert value(f, "hlsp2p_cache_entries", rank=r) >= 1
+        assert sum(v for _, v in f["hlsp2p_phase_calls_total"]) > 0
+        srcs = {lab["source"] for lab, _ in f["hlsp2p_request_latency_seconds"]}
+        assert srcs and srcs <= {"cdn", "p2p", "cache"}
+        for lab, v in f["hlsp2p_request_latency_seconds"]:
+            assert v >= 0
+        # the reference stats object, exported per agent
+        assert value(f, "hlsp2p_agent_bytes_total", source="cdn") == out[r]["stats"]["cdn"]
+        assert value(f, "hlsp2p_agent_bytes_total", source="p2p") == out[r]["stats"]["p2p"]
+
+
+def test_metrics_server_scrape(vod):
+    nodes = {}
+    run_swarm(2, vod, before=lambda r, node, w: nodes.setdefault(r, node))
+    srv = MetricsServer(nodes[0], port=0, agents=[])
+    try:
+        with urllib.request.urlopen(f"http://127.0.0.1:{srv.port}/metrics", timeout=10) as resp:
+            assert resp.status == 200
+            assert resp.headers["Content-Type"].startswith("text/plain; version=0.0.4")
+            fams = parse(resp.read().decode())
+        assert value(fams, "hlsp2p_rounds_total", rank=0) == nodes[0].stats["rounds"]
+        with pytest.raises(urllib.error.HTTPError) as ei:
+            urllib.request.urlopen(f"http://127.0.0.1:{srv.port}/nope", timeout=10)
+        assert ei.value.code == 404
+    finally:
+        srv.close()
+
+
+def test_metrics_port_from_p2p_config(vod):
+    """``p2pConfig.gpuSwarm.metricsPort`` starts the endpoint with the node and ``close()``
+    stops it."""
+    scraped, nodes = {}, {}
+
+    def before(r, node, w):
+        nodes[r] = node
+        assert node.metrics_server is not None
+        with urllib.request.urlopen(f"http://127.0.0.1:{node.metrics_server.port}/metrics", timeout=10) as resp:
+            scraped[r] = parse(resp.read().decode())
+
+    run_swarm(2, vod, before=before, cfg_extra={"metricsPort": 0})
+    for r in (0, 1):
+        assert value(scraped[r], "hlsp2p_world_size", rank=r) == 2
+        assert nodes[r].closed and nodes[r].metrics_server is None
