@@ -74,6 +74,8 @@ def parse():
                         "steps (masked in the control plane: it neither serves nor receives P2P), then "
                         "one all-online period; 0 = off")
     p.add_argument("--no-gc-tune", action="store_true", help="keep Python's default GC settings")
+    p.add_argument("--metrics-port", type=int, default=None,
+                   help="serve Prometheus GET /metrics on port + rank while the bench runs (idle unless scraped)")
     p.add_argument("--verbose", action="store_true")
     return p.parse_args()
 
@@ -122,6 +124,8 @@ def main() -> int:
                   "gpuSwarm": {"backend": "dist" if world > 1 else "local", "device": str(device),
                                "cacheBytes": int(args.cache_gb * (1 << 30)), "autoTick": False,
                                "cdnDedup": not args.no_dedup, "maxWantsPerRound": K}}
+    if args.metrics_port is not None:
+        p2p_config["gpuSwarm"]["metricsPort"] = args.metrics_port
     node = node_for_config(p2p_config)
     depth = 1 if args.sync_steps else args.lag + 2  # rounds a fragment spends in flight (see step())
     hls_config = {"maxFragLoadsInFlight": K * depth, "maxBufferLength": 1e9, "maxMaxBufferLength": 1e9,
