@@ -127,3 +127,47 @@ def test_metrics_port_from_p2p_config(vod):
     for r in (0, 1):
         assert value(scraped[r], "hlsp2p_world_size", rank=r) == 2
         assert nodes[r].closed and nodes[r].metrics_server is None
+
+
+@pytest.mark.gpu
+def test_metrics_on_gpu_node():
+    """A 1-rank node on the MI355X (HBM arena, native kernels): scrape after a 4-segment AES
+    playback; the counters match the node and the arena is reported as device memory."""
+    import torch
+
+    from hlsjs_p2p_wrapper_amd import Hls
+    from hlsjs_p2p_wrapper_amd.agent import current_node, set_current_node
+    from hlsjs_p2p_wrapper_amd.net import clear_origins, new_event_loop
+    from hlsjs_p2p_wrapper_amd.ops import _native
+    from hlsjs_p2p_wrapper_amd.player import MediaElement
+
+    _native.device()  # the gfx950 kernels must load
+    clear_origins()
+    set_current_node(None)
+    loop = new_event_loop("virtual")
+    origin = SyntheticHlsOrigin("http://cdn.gpumetrics/vod/", renditions=[Rendition(2_000_000, 1280, 720)],
+                                num_segments=4, encrypted=True, pin_memory=True)
+    p2p = {"streamrootKey": "m", "gpuSwarm": {"device": "cuda:0", "cacheBytes": 64 << 20, "metricsPort": 0,
+                                              "trace": True}}
+    hls = Hls({"transmuxDevice": "cuda:0"}, p2p)
+    media = MediaElement()
+    buffered = []
+    hls.on(Hls.Events.FRAG_BUFFERED, lambda e, d: buffered.append(d["frag"].sn))
+    hls.loadSource(origin.master_url())
+    hls.attachMedia(media)
+    hls.on(Hls.Events.MANIFEST_PARSED, lambda e, d: media.play())
+    assert loop.run_until(lambda: len(buffered) == 4, timeout_ms=120_000), buffered
+    torch.cuda.synchronize()
+    node = current_node()
+    assert node.arena.is_cuda
+    with urllib.request.urlopen(f"http://127.0.0.1:{node.metrics_server.port}/metrics", timeout=10) as resp:
+        fams = parse(resp.read().decode())
+    assert value(fams, "hlsp2p_cdn_bytes_total", rank=0) == node.stats["cdn"] == sum(origin.pools[0].lengths)
+    assert value(fams, "hlsp2p_cdn_segments_total", rank=0) == 4
+    assert value(fams, "hlsp2p_cache_used_bytes", rank=0) >= node.stats["cdn"]
+    assert {lab["source"] for lab, _ in fams["hlsp2p_request_latency_seconds"]} == {"cdn"}
+    hls.destroy()
+    node.close()
+    assert node.metrics_server is None
+    clear_origins()
+    set_current_node(None)
