@@ -847,14 +847,16 @@ class SwarmNode:
         if self._timer is not None:
             self._timer.cancel()
             self._timer = None
-        if self.world > 1:
-            for _ in range(timeout_rounds):
-                if self.tick():
-                    break
-        self.closed = True
-        if self.metrics_server is not None:
-            self.metrics_server.close()
-            self.metrics_server = None
+        try:
+            if self.world > 1:
+                for _ in range(timeout_rounds):
+                    if self.tick():
+                        break
+        finally:
+            self.closed = True
+            if self.metrics_server is not None:
+                srv, self.metrics_server = self.metrics_server, None
+                srv.close()
 
     def swarm_offload_ratio(self) -> float:
         c, p = self.swarm_stats["cdn"], self.swarm_stats["p2p"]
@@ -947,10 +949,27 @@ def node_for_config(p2p_config: Any) -> SwarmNode:
     for peer, kbps in (cfg.get("linkKbps") or {}).items():
         node.set_link_bandwidth(int(peer), kbps)
     if cfg.get("metricsPort") is not None:
-        from ..utils.metrics import MetricsServer
-
-        port = int(cfg["metricsPort"])
-        node.metrics_server = MetricsServer(node, port=port + node.rank if port else 0,
-                                            host=str(cfg.get("metricsHost", "127.0.0.1")))
+        node.metrics_server = _start_metrics(node, cfg, backend)
     set_current_node(node)
     return node
+
+
+def _start_metrics(node: SwarmNode, cfg: dict, backend: str) -> Any:
+    """Serve ``GET /metrics`` for ``node`` on ``metricsPort`` + the node-local rank.
+
+    The endpoint is optional observability: a bind failure (port taken, two jobs on one
+    host) logs a warning and the rank keeps serving without it — it must never take a
+    rank out of the collective rounds its peers are already waiting in.  The offset is
+    ``LOCAL_RANK`` under torchrun (ports stay within [port, port + ranks per host) on
+    every host of a multi-host job), the in-process rank otherwise."""
+    from ..utils.metrics import MetricsServer
+
+    port = int(cfg["metricsPort"])
+    if port:
+        local = os.environ.get("LOCAL_RANK") if backend == "dist" else None
+        port += int(local) if local is not None else node.rank
+    try:
+        return MetricsServer(node, port=port, host=str(cfg.get("metricsHost", "127.0.0.1")))
+    except OSError as e:
+        log.warning("metrics endpoint disabled on rank %d: cannot bind port %d (%s)", node.rank, port, e)
+        return None

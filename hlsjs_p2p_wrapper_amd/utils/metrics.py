@@ -69,8 +69,10 @@ def render(families: Iterable[Family]) -> str:
         out.append(f"# HELP {name} {help_}")
         out.append(f"# TYPE {name} {kind}")
         for labels, value in samples:
-            lab = ",".join(f'{k}="{_esc(str(v))}"' for k, v in labels.items())
-            out.append(f"{name}{{{lab}}} {_fmt(value)}" if lab else f"{name} {_fmt(value)}")
+            # a summary's _sum / _count series ride in the family with a "__suffix" pseudo-label
+            suffix = labels.get("__suffix", "")
+            lab = ",".join(f'{k}="{_esc(str(v))}"' for k, v in labels.items() if k != "__suffix")
+            out.append(f"{name}{suffix}{{{lab}}} {_fmt(value)}" if lab else f"{name}{suffix} {_fmt(value)}")
     return "\n".join(out) + "\n"
 
 
@@ -105,25 +107,38 @@ def node_metrics(node: Any, quantiles: Sequence[float] = (0.5, 0.9, 0.99)) -> Li
     fams.append((PREFIX + "cache_evictions_total", "counter", "Segments evicted from the HBM cache.",
                  [(dict(base), float(store.evictions))]))
     timer = node.timer
+    totals, counts = dict(timer.total), dict(timer.count)  # C-level copies: the round loop keeps adding
     fams.append((PREFIX + "phase_seconds_total", "counter", "Host wall time per round phase.",
-                 [(dict(base, phase=k), float(v)) for k, v in sorted(timer.total.items())]))
+                 [(dict(base, phase=k), float(v)) for k, v in sorted(totals.items())]))
     fams.append((PREFIX + "phase_calls_total", "counter", "Round phase executions.",
-                 [(dict(base, phase=k), float(v)) for k, v in sorted(timer.count.items())]))
+                 [(dict(base, phase=k), float(v)) for k, v in sorted(counts.items())]))
     trace = getattr(node, "trace", None)
     if trace is not None and len(trace):
+        # one snapshot, grouped by source in one pass, each group sorted once
         samples: List[Sample] = []
-        for src in sorted(trace.by_source()):
-            for q in quantiles:
-                samples.append((dict(base, source=src, quantile=str(q)), trace.latency_ms(q, src) / 1e3))
+        for src, (n, sum_ms, qs) in sorted(trace.latency_summary(quantiles).items()):
+            for q, ms in qs:
+                samples.append((dict(base, source=src, quantile=str(q)), ms / 1e3))
+            samples.append(({**base, "source": src, "__suffix": "_sum"}, sum_ms / 1e3))
+            samples.append(({**base, "source": src, "__suffix": "_count"}, float(n)))
         fams.append((PREFIX + "request_latency_seconds", "summary",
-                     "Request latency (submit -> delivered) by source, from the trace log.", samples))
+                     "Request latency (submit -> delivered) by source over the retained trace log (the "
+                     "last gpuSwarm.trace records, lifetime rather than a time window); the unit follows "
+                     "the event-loop clock (virtual time under the virtual loop).", samples))
     return fams
 
 
-def agent_metrics(agent: Any) -> List[Family]:
-    """The reference ``stats`` object (``{cdn, p2p, upload, peers}``) of one peer agent."""
+def agent_metrics(agent: Any, index: int = 0, rank: Optional[int] = None) -> List[Family]:
+    """The reference ``stats`` object (``{cdn, p2p, upload, peers}``) of one peer agent.
+
+    Labelled by ``rank`` and ``agent`` (the attach index on its node) besides ``content``:
+    two players on one node watching the same stream would otherwise emit identical label
+    sets (``contentId`` defaults to ``contentUrl``)."""
     s = agent.stats
-    lab = {"content": str(getattr(agent, "contentId", "") or "")}
+    if rank is None:
+        node = getattr(agent, "node", None)
+        rank = getattr(node, "rank", 0) if node is not None else 0
+    lab = {"rank": str(rank), "agent": str(index), "content": str(getattr(agent, "contentId", "") or "")}
     return [
         (PREFIX + "agent_bytes_total", "counter", "Per-session bytes (wrapper.stats).",
          [(dict(lab, source=k), float(s[k])) for k in ("cdn", "p2p", "upload")]),
@@ -166,8 +181,8 @@ class MetricsServer:
     def text(self) -> str:
         fams = node_metrics(self.node)
         agents = self.agents if self.agents is not None else getattr(self.node, "_agents", [])
-        for a in list(agents):
-            fams.extend(agent_metrics(a))
+        for i, a in enumerate(list(agents)):
+            fams.extend(agent_metrics(a, i, getattr(self.node, "rank", 0)))
         return render(fams)
 
     def close(self) -> None:

@@ -10,10 +10,10 @@
 from __future__ import annotations
 
 import time
-from collections import defaultdict, deque
+from collections import defaultdict, deque, namedtuple
 from contextlib import contextmanager
 from dataclasses import dataclass
-from typing import Deque, Dict, Iterator, Optional, Tuple
+from typing import Deque, Dict, Iterator, List, Optional, Sequence, Tuple
 
 
 class PhaseTimer:
@@ -67,6 +67,10 @@ class RequestTrace:
     round: int
 
 
+# count, sum of latencies (ms), [(quantile, latency ms)]
+LatencySummary = namedtuple("LatencySummary", ["count", "sum_ms", "quantiles_ms"])
+
+
 class TraceLog:
     def __init__(self, maxlen: int = 100_000) -> None:
         self.records: Deque[RequestTrace] = deque(maxlen=maxlen)
@@ -80,17 +84,35 @@ class TraceLog:
     def by_source(self) -> Dict[str, Tuple[int, int]]:
         """``{source: (requests, bytes)}``."""
         out: Dict[str, Tuple[int, int]] = {}
-        for r in self.records:
+        for r in list(self.records):
             n, b = out.get(r.source, (0, 0))
             out[r.source] = (n + 1, b + r.bytes)
         return out
 
     def latency_ms(self, q: float = 0.5, source: Optional[str] = None) -> float:
         """``q``-quantile of ``tload - trequest``."""
-        xs = sorted(r.tload - r.trequest for r in self.records if source is None or r.source == source)
+        xs = sorted(r.tload - r.trequest for r in list(self.records) if source is None or r.source == source)
         if not xs:
             return 0.0
         return xs[min(len(xs) - 1, int(q * len(xs)))]
+
+    def latency_summary(self, quantiles: Sequence[float] = (0.5, 0.9, 0.99)) -> Dict[str, Tuple[int, float, List[Tuple[float, float]]]]:
+        """Per-source latency summary of the whole retained log in ONE pass.
+
+        Safe to call from another thread while the round loop appends: ``list(deque)`` is a
+        single C-level copy under the GIL, so the snapshot never sees a mutation mid-loop.
+        Each source's latencies are sorted once and every quantile is read from that sort.
+        Values are event-loop milliseconds (virtual time under the ``virtual`` loop) over
+        the retained records (the last ``maxlen`` requests), not a sliding time window."""
+        groups: Dict[str, List[float]] = {}
+        for r in list(self.records):
+            groups.setdefault(r.source, []).append(r.tload - r.trequest)
+        out: Dict[str, Tuple[int, float, List[Tuple[float, float]]]] = {}
+        for src, xs in groups.items():
+            xs.sort()
+            n = len(xs)
+            out[src] = LatencySummary(n, float(sum(xs)), [(q, xs[min(n - 1, int(q * n))]) for q in quantiles])
+        return out
 
     def to_dicts(self):
         return [{"key": list(r.key), "trequest": r.trequest, "tfirst": r.tfirst, "tload": r.tload,

@@ -18,7 +18,7 @@ _SAMPLE = re.compile(r'^([a-zA-Z_:][a-zA-Z0-9_:]*)(\{([a-z_]+=' + _LV + r'(,[a-z
 def parse(text):
     """``{name: [(labels, value)]}``; asserts every line is valid exposition syntax and
     that each family has exactly one HELP and one TYPE line, before its samples."""
-    fams, seen_help, seen_type = {}, set(), set()
+    fams, seen_help, seen_type, summaries = {}, set(), set(), set()
     for line in text.strip().split("\n"):
         if line.startswith("# HELP "):
             name = line.split()[2]
@@ -27,13 +27,16 @@ def parse(text):
         elif line.startswith("# TYPE "):
             _, _, name, kind = line.split()
             assert kind in ("counter", "gauge", "summary"), line
+            if kind == "summary":
+                summaries.add(name)
             assert name not in seen_type, f"duplicate TYPE for {name}"
             seen_type.add(name)
         else:
             m = _SAMPLE.match(line)
             assert m, f"bad sample line {line!r}"
             name = m.group(1)
-            assert name in seen_type, f"sample before TYPE: {line!r}"
+            base = name[:-4] if name.endswith("_sum") else name[:-6] if name.endswith("_count") else None
+            assert name in seen_type or (base in seen_type and base in summaries), f"sample before TYPE: {line!r}"
             labels = dict(re.findall(r'([a-z_]+)="((?:[^"\\]|\\.)*)"', m.group(3) or ""))
             fams.setdefault(name, []).append((labels, float(m.group(5))))
     return fams
@@ -90,9 +93,84 @@ def test_swarm_metrics_match_stats(vod):
         assert srcs and srcs <= {"cdn", "p2p", "cache"}
         for lab, v in f["hlsp2p_request_latency_seconds"]:
             assert v >= 0
-        # the reference stats object, exported per agent
-        assert value(f, "hlsp2p_agent_bytes_total", source="cdn") == out[r]["stats"]["cdn"]
-        assert value(f, "hlsp2p_agent_bytes_total", source="p2p") == out[r]["stats"]["p2p"]
+        # summary _sum / _count per source, consistent with the trace log
+        summ = nodes[r].trace.latency_summary()
+        for src in srcs:
+            assert value(f, "hlsp2p_request_latency_seconds_count", source=src) == summ[src].count > 0
+            assert value(f, "hlsp2p_request_latency_seconds_sum", source=src) == pytest.approx(summ[src].sum_ms / 1e3)
+        # the reference stats object, exported per agent (labelled by rank and attach index)
+        assert value(f, "hlsp2p_agent_bytes_total", source="cdn", rank=r, agent=0) == out[r]["stats"]["cdn"]
+        assert value(f, "hlsp2p_agent_bytes_total", source="p2p", rank=r, agent=0) == out[r]["stats"]["p2p"]
+
+
+def test_agent_labels_distinguish_players_on_one_node():
+    """Two agents on one node watching the same content: distinct label sets per agent."""
+
+    class _A:
+        def __init__(self, cdn):
+            self.stats = {"cdn": cdn, "p2p": 0, "upload": 0, "peers": 1}
+            self.contentId = "http://same/stream.m3u8"
+
+    fams = parse(render(agent_metrics(_A(1), 0, rank=3) + agent_metrics(_A(2), 1, rank=3)))
+    assert value(fams, "hlsp2p_agent_bytes_total", source="cdn", agent=0, rank=3) == 1
+    assert value(fams, "hlsp2p_agent_bytes_total", source="cdn", agent=1, rank=3) == 2
+    labs = [tuple(sorted(lab.items())) for lab, _ in fams["hlsp2p_agent_peers"]]
+    assert len(set(labs)) == 2
+
+
+def test_scrape_while_rounds_run(vod, monkeypatch):
+    """The endpoint is scraped from its own thread while the swarm keeps running rounds
+    (and appending trace records): every scrape parses, none raises."""
+    import threading
+
+    scrapes, errors, stop = [], [], threading.Event()
+
+    def scraper(node):
+        while not stop.is_set():
+            try:
+                scrapes.append(parse(render(node_metrics(node))))
+            except Exception as e:  # noqa: BLE001
+                errors.append(e)
+                return
+            stop.wait(0.002)  # a scrape every few ms: far more often than any real scraper
+
+    ths = []
+
+    def before(r, node, w):
+        node.enable_trace()
+        if r == 0:
+            t = threading.Thread(target=scraper, args=(node,), daemon=True)
+            t.start()
+            ths.append(t)
+
+    try:
+        run_swarm(2, vod, before=before)
+    finally:
+        stop.set()
+        for t in ths:
+            t.join(10)
+    assert not errors, errors
+    assert len(scrapes) >= 2
+    assert any("hlsp2p_request_latency_seconds" in f for f in scrapes)
+
+
+def test_metrics_port_taken_does_not_fail_the_node(vod):
+    """A taken metricsPort logs a warning and the node runs on without the endpoint."""
+    import socket
+
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    s.listen(1)
+    taken = s.getsockname()[1]
+    nodes = {}
+    try:
+        # rank r binds taken + r: rank 0 collides, rank 1 (taken + 1) is most likely free
+        out = run_swarm(2, vod, before=lambda r, node, w: nodes.setdefault(r, node),
+                        cfg_extra={"metricsPort": taken})
+    finally:
+        s.close()
+    assert all(o["ok"] for o in out.values())
+    assert nodes[0].closed and nodes[0].metrics_server is None
 
 
 def test_metrics_server_scrape(vod):
@@ -150,24 +228,29 @@ def test_metrics_on_gpu_node():
     p2p = {"streamrootKey": "m", "gpuSwarm": {"device": "cuda:0", "cacheBytes": 64 << 20, "metricsPort": 0,
                                               "trace": True}}
     hls = Hls({"transmuxDevice": "cuda:0"}, p2p)
-    media = MediaElement()
-    buffered = []
-    hls.on(Hls.Events.FRAG_BUFFERED, lambda e, d: buffered.append(d["frag"].sn))
-    hls.loadSource(origin.master_url())
-    hls.attachMedia(media)
-    hls.on(Hls.Events.MANIFEST_PARSED, lambda e, d: media.play())
-    assert loop.run_until(lambda: len(buffered) == 4, timeout_ms=120_000), buffered
-    torch.cuda.synchronize()
     node = current_node()
-    assert node.arena.is_cuda
-    with urllib.request.urlopen(f"http://127.0.0.1:{node.metrics_server.port}/metrics", timeout=10) as resp:
-        fams = parse(resp.read().decode())
-    assert value(fams, "hlsp2p_cdn_bytes_total", rank=0) == node.stats["cdn"] == sum(origin.pools[0].lengths)
-    assert value(fams, "hlsp2p_cdn_segments_total", rank=0) == 4
-    assert value(fams, "hlsp2p_cache_used_bytes", rank=0) >= node.stats["cdn"]
-    assert {lab["source"] for lab, _ in fams["hlsp2p_request_latency_seconds"]} == {"cdn"}
-    hls.destroy()
-    node.close()
-    assert node.metrics_server is None
-    clear_origins()
-    set_current_node(None)
+    try:
+        media = MediaElement()
+        buffered = []
+        hls.on(Hls.Events.FRAG_BUFFERED, lambda e, d: buffered.append(d["frag"].sn))
+        hls.loadSource(origin.master_url())
+        hls.attachMedia(media)
+        hls.on(Hls.Events.MANIFEST_PARSED, lambda e, d: media.play())
+        assert loop.run_until(lambda: len(buffered) == 4, timeout_ms=120_000), buffered
+        torch.cuda.synchronize()
+        node = current_node()
+        assert node.arena.is_cuda
+        with urllib.request.urlopen(f"http://127.0.0.1:{node.metrics_server.port}/metrics", timeout=10) as resp:
+            fams = parse(resp.read().decode())
+        assert value(fams, "hlsp2p_cdn_bytes_total", rank=0) == node.stats["cdn"] == sum(origin.pools[0].lengths)
+        assert value(fams, "hlsp2p_cdn_segments_total", rank=0) == 4
+        assert value(fams, "hlsp2p_cache_used_bytes", rank=0) >= node.stats["cdn"]
+        assert {lab["source"] for lab, _ in fams["hlsp2p_request_latency_seconds"]} == {"cdn"}
+        assert value(fams, "hlsp2p_request_latency_seconds_count", source="cdn") == 4
+    finally:
+        hls.destroy()
+        if node is not None:
+            node.close()
+            assert node.metrics_server is None
+        clear_origins()
+        set_current_node(None)
