@@ -47,6 +47,8 @@ CONFIGS = {
     # diagnostic only: ~30 KB segments, so per-segment host (Python) cost dominates
     "hostcost": ("tiny", True, 4.0, "60 kb/s HLS (AES-128) - host-overhead probe"),
     "hostcost-abr": ("tiny-abr", True, 4.0, "5 x 20-100 kb/s ABR ladder (AES-128) - host-overhead probe"),
+    # diagnostic only: ~4 KB segments, for the CPU host-cost harness (device ops ~free)
+    "hostcost-micro": ("micro", True, 4.0, "8 kb/s HLS (AES-128) - host-overhead probe, CPU harness"),
 }
 
 
@@ -110,6 +112,7 @@ def main() -> int:
     preset, encrypted, seg_dur, desc = CONFIGS[args.config]
     rends = {"1080p": PRESET_1080P_6M, "4k": PRESET_4K_25M, "abr5": PRESET_ABR5,
              "tiny": [Rendition(60_000, 320, 180, name="180p")],
+             "micro": [Rendition(8_000, 160, 90, name="90p")],
              "tiny-abr": [Rendition(20_000 * (i + 1), 160 * (i + 1), 90 * (i + 1), name=f"t{i}") for i in range(5)]}[preset]
     K = args.inflight
     total_steps = args.warmup + args.steps

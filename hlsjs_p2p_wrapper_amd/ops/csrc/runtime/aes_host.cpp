@@ -2,6 +2,10 @@
 
 #include <cstring>
 
+#if defined(__x86_64__)
+#include <immintrin.h>
+#endif
+
 namespace hlsp2p {
 namespace aes {
 namespace {
@@ -169,17 +173,78 @@ size_t cbc_encrypt_pkcs7(const uint8_t key[16], const uint8_t iv[16], const uint
   return total;
 }
 
+bool have_aesni() {
+#if defined(__x86_64__)
+  static const bool ok = __builtin_cpu_supports("aes") && __builtin_cpu_supports("sse4.1");
+  return ok;
+#else
+  return false;
+#endif
+}
+
+#if defined(__x86_64__)
+namespace {
+// AESDEC is one round of the equivalent inverse cipher, so the drk schedule (four
+// big-endian column words per round) maps onto it byte for byte.
+__attribute__((target("aes,sse4.1"))) void cbc_decrypt_aesni(const uint32_t drk[44], const uint8_t iv[16],
+                                                              const uint8_t* in, size_t n, uint8_t* out) {
+  __m128i k[11];
+  for (int r = 0; r < 11; ++r) {
+    uint8_t b[16];
+    for (int c = 0; c < 4; ++c) store_be(b + 4 * c, drk[4 * r + c]);
+    k[r] = _mm_loadu_si128(reinterpret_cast<const __m128i*>(b));
+  }
+  __m128i prev = _mm_loadu_si128(reinterpret_cast<const __m128i*>(iv));
+  const size_t nb = n / 16;
+  size_t i = 0;
+  for (; i + 8 <= nb; i += 8) {  // eight independent blocks in flight
+    __m128i c[8], s[8];
+    for (int j = 0; j < 8; ++j) {
+      c[j] = _mm_loadu_si128(reinterpret_cast<const __m128i*>(in + 16 * (i + j)));
+      s[j] = _mm_xor_si128(c[j], k[0]);
+    }
+    for (int r = 1; r < 10; ++r)
+      for (int j = 0; j < 8; ++j) s[j] = _mm_aesdec_si128(s[j], k[r]);
+    for (int j = 0; j < 8; ++j) s[j] = _mm_aesdeclast_si128(s[j], k[10]);
+    _mm_storeu_si128(reinterpret_cast<__m128i*>(out + 16 * i), _mm_xor_si128(s[0], prev));
+    for (int j = 1; j < 8; ++j)
+      _mm_storeu_si128(reinterpret_cast<__m128i*>(out + 16 * (i + j)), _mm_xor_si128(s[j], c[j - 1]));
+    prev = c[7];
+  }
+  for (; i < nb; ++i) {
+    __m128i c = _mm_loadu_si128(reinterpret_cast<const __m128i*>(in + 16 * i));
+    __m128i s = _mm_xor_si128(c, k[0]);
+    for (int r = 1; r < 10; ++r) s = _mm_aesdec_si128(s, k[r]);
+    s = _mm_aesdeclast_si128(s, k[10]);
+    _mm_storeu_si128(reinterpret_cast<__m128i*>(out + 16 * i), _mm_xor_si128(s, prev));
+    prev = c;
+  }
+}
+}  // namespace
+#endif
+
+void cbc_decrypt_raw(const uint32_t drk[44], const uint8_t iv[16], const uint8_t* in, size_t n, uint8_t* out) {
+#if defined(__x86_64__)
+  if (have_aesni()) {
+    cbc_decrypt_aesni(drk, iv, in, n, out);
+    return;
+  }
+#endif
+  uint8_t prev[16], cur[16], tmp[16];
+  std::memcpy(prev, iv, 16);
+  for (size_t off = 0; off + 16 <= n; off += 16) {
+    std::memcpy(cur, in + off, 16);  // in-place safe
+    decrypt_block(drk, cur, tmp);
+    for (int i = 0; i < 16; ++i) out[off + i] = tmp[i] ^ prev[i];
+    std::memcpy(prev, cur, 16);
+  }
+}
+
 int64_t cbc_decrypt_pkcs7(const uint8_t key[16], const uint8_t iv[16], const uint8_t* in, size_t n, uint8_t* out) {
   if (n == 0 || n % 16 != 0) return -1;
   uint32_t drk[44];
   expand_key_dec(key, drk);
-  const uint8_t* prev = iv;
-  for (size_t off = 0; off < n; off += 16) {
-    uint8_t tmp[16];
-    decrypt_block(drk, in + off, tmp);
-    for (int i = 0; i < 16; ++i) out[off + i] = tmp[i] ^ prev[i];
-    prev = in + off;
-  }
+  cbc_decrypt_raw(drk, iv, in, n, out);
   uint8_t pad = out[n - 1];
   if (pad == 0 || pad > 16) return -1;
   for (size_t i = n - pad; i < n; ++i)

@@ -39,6 +39,12 @@ void decrypt_block(const uint32_t drk[44], const uint8_t in[16], uint8_t out[16]
 // CBC encrypt with PKCS#7 padding.  `out` must hold n + 16 bytes.  Returns output size.
 size_t cbc_encrypt_pkcs7(const uint8_t key[16], const uint8_t iv[16], const uint8_t* in, size_t n,
                          uint8_t* out);
+// CBC decrypt of n bytes (multiple of 16, no unpadding) with equivalent-inverse-cipher
+// round keys.  Uses the x86 AES instructions when the CPU has them (CBC decryption is
+// block-parallel: eight blocks in flight), the T-table cipher otherwise.
+void cbc_decrypt_raw(const uint32_t drk[44], const uint8_t iv[16], const uint8_t* in, size_t n, uint8_t* out);
+bool have_aesni();
+
 // CBC decrypt + PKCS#7 unpad.  `n` must be a multiple of 16.  Returns plaintext size, or
 // -1 on a bad size / padding.
 int64_t cbc_decrypt_pkcs7(const uint8_t key[16], const uint8_t iv[16], const uint8_t* in, size_t n,

@@ -38,9 +38,11 @@ T* mut_ptr(py::array& a, const char* name) {
 }
 
 template <typename F>
-void parallel_for(int64_t n, F&& f) {
+void parallel_for(int64_t n, F&& f, int64_t work_bytes = -1) {
   unsigned hw = std::max(1u, std::thread::hardware_concurrency());
   int64_t nt = std::min<int64_t>(n, std::min<unsigned>(hw, 16u));
+  // a thread spawn costs ~10-20 us: small batches (host-path probes, unit tests) run inline
+  if (work_bytes >= 0) nt = std::min<int64_t>(nt, std::max<int64_t>(1, work_bytes >> 20));
   if (nt <= 1) {
     for (int64_t i = 0; i < n; ++i) f(i);
     return;
@@ -149,19 +151,12 @@ PYBIND11_MODULE(_runtime, m) {
     for (int64_t b = 0; b < B; ++b)
       if (nb[b] < 0 || nb[b] % 16 || so[b] < 0 || so[b] + nb[b] > src_n || dof[b] < 0 || dof[b] + nb[b] > dst_n)
         throw std::invalid_argument("cbc_decrypt_batch: segment out of bounds or not a multiple of 16");
+    int64_t total = 0;
+    for (int64_t b = 0; b < B; ++b) total += nb[b];
     py::gil_scoped_release nogil;
     parallel_for(B, [&](int64_t b) {
-      const uint8_t* in = s + so[b];
       uint8_t* out = d + dof[b];
-      const uint32_t* rk = k + 44 * b;
-      uint8_t prev[16], cur[16], tmp[16];
-      std::memcpy(prev, ivp + 16 * b, 16);
-      for (int64_t off = 0; off < nb[b]; off += 16) {
-        std::memcpy(cur, in + off, 16);
-        aes::decrypt_block(rk, cur, tmp);
-        for (int i = 0; i < 16; ++i) out[off + i] = tmp[i] ^ prev[i];
-        std::memcpy(prev, cur, 16);
-      }
+      aes::cbc_decrypt_raw(k + 44 * b, ivp + 16 * b, s + so[b], static_cast<size_t>(nb[b]), out);
       int64_t len = -1;
       if (nb[b] >= 16) {
         uint8_t pad = out[nb[b] - 1];
@@ -172,7 +167,7 @@ PYBIND11_MODULE(_runtime, m) {
         }
       }
       ol[b] = len;
-    });
+    }, total);
   });
 
   // ------------------------------------------------------------------ CRC
@@ -188,8 +183,10 @@ PYBIND11_MODULE(_runtime, m) {
     const int64_t* ln = len.data();
     for (int64_t b = 0; b < B; ++b)
       if (of[b] < 0 || ln[b] < 0 || of[b] + ln[b] > buf.size()) throw std::invalid_argument("crc32_batch: out of bounds");
+    int64_t total = 0;
+    for (int64_t b = 0; b < B; ++b) total += ln[b];
     py::gil_scoped_release nogil;
-    parallel_for(B, [&](int64_t b) { o[b] = crc::crc32(p + of[b], static_cast<size_t>(ln[b])); });
+    parallel_for(B, [&](int64_t b) { o[b] = crc::crc32(p + of[b], static_cast<size_t>(ln[b])); }, total);
     return out;
   });
   m.def("crc_mfma_weights", [] {
@@ -248,11 +245,13 @@ PYBIND11_MODULE(_runtime, m) {
     const int64_t* o = off.data();
     const int64_t* l = len.data();
     const int64_t* eo = es_off.data();
+    int64_t total = 0;
+    for (int64_t b = 0; b < B; ++b) total += l[b];
     py::gil_scoped_release nogil;
     parallel_for(B, [&](int64_t b) {
       ts::demux_segment(p + o[b], l[b], e + eo[b], pp + b * ts::kClasses * max_pes * 3, max_pes,
                         ip + b * ts::kInfoWords);
-    });
+    }, total);
   });
   m.def("mpeg_crc32", [](Arr<uint8_t> data) { return ts::mpeg_crc32(data.data(), static_cast<size_t>(data.size())); });
   m.attr("TS_INFO_WORDS") = ts::kInfoWords;
