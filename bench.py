@@ -311,6 +311,7 @@ def main() -> int:
         print(json.dumps(result), flush=True)
     if world > 1:
         node.comm.barrier()
+        node.comm.close()  # the native RCCL communicator (collective, every rank is here)
         dist.destroy_process_group()
     return 0
 

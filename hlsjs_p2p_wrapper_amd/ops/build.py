@@ -119,9 +119,10 @@ def build_device(force: bool = False, verbose: bool = False) -> Path:
     hipcc = shutil.which("hipcc") or "/opt/rocm/bin/hipcc"
     kern = sorted(KERNEL_SRC.glob("*.hip"))
     hdrs = sorted(KERNEL_SRC.glob("*.h")) + sorted(KERNEL_SRC.glob("*.hpp"))
-    binding = KERNEL_SRC / "bindings.cpp"
+    # host-only translation units: bindings.cpp (torch ops) and rccl_comm.cpp (RCCL data plane)
+    host_srcs = sorted(KERNEL_SRC.glob("*.cpp"))
     out = device_path()
-    if not force and not _stale(out, kern + hdrs + [binding]):
+    if not force and not _stale(out, kern + hdrs + host_srcs):
         return out
     objdir = BUILD / "device"
     objdir.mkdir(parents=True, exist_ok=True)
@@ -138,21 +139,23 @@ def build_device(force: bool = False, verbose: bool = False) -> Path:
             _run([hipcc, *kflags, "-c", str(src), "-o", str(obj)])
         return obj
 
-    def compile_binding() -> Path:
-        obj = objdir / "bindings.o"
-        if force or _stale(obj, [binding] + hdrs):
+    def compile_host(src: Path) -> Path:
+        obj = objdir / (src.stem + ".o")
+        if force or _stale(obj, [src] + hdrs):
             # host-only translation unit: plain clang++ from the ROCm toolchain via hipcc
-            _run([hipcc, *bflags, "-x", "c++", "-c", str(binding), "-o", str(obj)])
+            _run([hipcc, *bflags, "-x", "c++", "-c", str(src), "-o", str(obj)])
         return obj
 
     with cf.ThreadPoolExecutor(max_workers=_jobs()) as ex:
-        futs = [ex.submit(compile_kernel, s) for s in kern] + [ex.submit(compile_binding)]
+        futs = [ex.submit(compile_kernel, s) for s in kern] + [ex.submit(compile_host, s) for s in host_srcs]
         objs = [f.result() for f in futs]
     tmp = out.with_suffix(out.suffix + ".tmp")
     link = [hipcc, "-shared", "-fPIC", f"--offload-arch={ARCH}", *map(str, objs), "-o", str(tmp)]
     for d in libdirs:
         link += [f"-L{d}", f"-Wl,-rpath,{d}"]
-    link += ["-lc10", "-lc10_hip", "-ltorch", "-ltorch_cpu", "-ltorch_hip", "-ltorch_python", "-lamdhip64"]
+    # -lrccl resolves to the librccl PyTorch ships (torch/lib comes first on the search path
+    # and in the rpath): one RCCL runtime per process
+    link += ["-lc10", "-lc10_hip", "-ltorch", "-ltorch_cpu", "-ltorch_hip", "-ltorch_python", "-lamdhip64", "-lrccl"]
     _run(link)
     os.replace(tmp, out)
     if verbose:

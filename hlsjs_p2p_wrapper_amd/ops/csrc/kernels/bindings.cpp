@@ -316,6 +316,8 @@ std::vector<Tensor> pack_h2d(const std::vector<pybind11::array>& arrays, int64_t
 
 }  // namespace
 
+void register_rccl(pybind11::module& m);  // rccl_comm.cpp: native RCCL data plane
+
 PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.doc() = "hlsjs-p2p-wrapper-amd CDNA4 (gfx950) kernels";
   m.def("aes128_cbc_decrypt", &aes128_cbc_decrypt);
@@ -334,5 +336,6 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("device_cus", &device_cus);
   m.def("h2d_batch", &h2d_batch);
   m.def("pack_h2d", &pack_h2d);
+  register_rccl(m);
   m.attr("ARCH") = "gfx950";
 }

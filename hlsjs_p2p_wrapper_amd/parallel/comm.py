@@ -19,13 +19,16 @@ Backends:
 * :class:`DistComm` — ``torch.distributed``: the control plane runs on the host, never
   on a GPU stream — through the native shared-memory all-gather (``runtime/shm_control``)
   when every rank is on one host (a node of 8 MI355X: the benchmark's case), over a
-  **gloo** group otherwise — and the default group — **nccl, i.e. RCCL over xGMI** on
-  MI355X, gloo in CPU tests — carries segment bytes with ``batch_isend_irecv``
-  (coalesced: one RCCL group call on the world communicator per round, one contiguous
-  buffer per peer pair).  ``HLSP2P_CONTROL=gloo`` forces the gloo control plane.
+  **gloo** group otherwise.  Segment bytes move over **RCCL on xGMI** when the default
+  group is nccl: by default through the native data plane (``kernels/rccl_comm.cpp``: the
+  node's own RCCL communicator, one ``ncclGroupStart / ncclSend* / ncclRecv* /
+  ncclGroupEnd`` call per round enqueued on the node stream, one contiguous buffer per peer
+  pair), or with ``HLSP2P_NATIVE_RCCL=0`` through torch's ``batch_isend_irecv``; gloo in
+  CPU tests.  ``HLSP2P_CONTROL=gloo`` forces the gloo control plane.
 """
 from __future__ import annotations
 
+import atexit
 import os
 import secrets
 import socket
@@ -150,6 +153,7 @@ class DistComm(SwarmComm):
         self.control_timeout_s = float(os.environ.get("HLSP2P_CONTROL_TIMEOUT", "600"))
         self._shm = self._open_shm_control() if self.world_size > 1 else None
         self.control_transport = "shm" if self._shm is not None else "gloo"
+        self._rccl = None
         if backend == "nccl" and torch.cuda.is_available():
             # batch_isend_irecv runs on the group's full communicator; when that is created
             # lazily every rank must take part in its first use.  Node construction is
@@ -157,6 +161,35 @@ class DistComm(SwarmComm):
             t = torch.zeros(1, dtype=torch.int64, device=torch.device("cuda", torch.cuda.current_device()))
             dist.all_reduce(t, group=data_group)
             torch.cuda.synchronize()
+            if os.environ.get("HLSP2P_NATIVE_RCCL", "1") != "0":
+                self._rccl = self._open_native_rccl()
+        self.data_transport = ("rccl-native" if self._rccl is not None else
+                               "rccl-torch" if backend == "nccl" else backend)
+
+    def _open_native_rccl(self):
+        """The node's own RCCL communicator (collective).  Every rank first reports whether
+        the native module and RCCL are usable; only if all are does any rank enter
+        ``ncclCommInitRank`` (a rank that cannot join would leave the others blocked in it).
+        Otherwise every rank stays on torch's ``batch_isend_irecv``."""
+        dist, g = self.dist, self.control_group
+        dev = None
+        ok = True
+        try:
+            from ..ops._native import device as _dev
+
+            dev = _dev()
+            dev.rccl_version()
+        except Exception:  # noqa: BLE001 - no native module / RCCL: torch's path
+            ok = False
+        uid = [dev.rccl_unique_id() if (ok and self.rank == 0) else None]
+        flags: List[object] = [None] * self.world_size
+        dist.all_gather_object(flags, ok, group=g)
+        if not all(flags):
+            return None
+        dist.broadcast_object_list(uid, src=0, group=g)
+        comm = dev.RcclComm(uid[0], self.world_size, self.rank, torch.cuda.current_device())
+        atexit.register(comm.abort)  # no-op once closed
+        return comm
 
     SHM_SLOT_WORDS = 16384  # int64 words per rank and round (128 KiB); larger -> gloo
 
@@ -236,6 +269,9 @@ class DistComm(SwarmComm):
 
     def exchange(self, sends, recvs) -> None:
         dist = self.dist
+        if self._rccl is not None:
+            self._exchange_native(sends, recvs)
+            return
         if self.data_backend == "gloo" and any(t.is_cuda for _, t in list(sends) + list(recvs)):
             self._exchange_staged(sends, recvs)
             return
@@ -249,6 +285,27 @@ class DistComm(SwarmComm):
         reqs = dist.batch_isend_irecv(ops)
         for r in reqs:
             r.wait()
+
+    def _exchange_native(self, sends, recvs) -> None:
+        """One RCCL group call on the current stream (the swarm node's stream)."""
+        if not sends and not recvs:
+            return
+        ns, nr = len(sends), len(recvs)
+        ptr = np.empty(ns + nr, dtype=np.int64)
+        nbytes = np.empty(ns + nr, dtype=np.int64)
+        peer = np.empty(ns + nr, dtype=np.int64)
+        for i, (p, t) in enumerate(list(sends) + list(recvs)):
+            if not (t.is_cuda and t.is_contiguous()):
+                raise ValueError("native RCCL exchange needs contiguous GPU tensors")
+            ptr[i] = t.data_ptr()
+            nbytes[i] = t.numel() * t.element_size()
+            peer[i] = p
+        stream = torch.cuda.current_stream().cuda_stream
+        self._rccl.exchange(ptr[:ns], nbytes[:ns], peer[:ns], ptr[ns:], nbytes[ns:], peer[ns:], stream)
+
+    def close(self) -> None:
+        if self._rccl is not None:
+            self._rccl.close()
 
     def _exchange_staged(self, sends, recvs) -> None:
         """gloo data plane with GPU tensors (several ranks sharing one GPU, e.g. rehearsing

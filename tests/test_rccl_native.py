@@ -1,0 +1,112 @@
+"""Native RCCL data plane (``kernels/rccl_comm.cpp``).
+
+The pool's GPU box has one MI355X and RCCL refuses two ranks on one device, so the GPU
+tests use a one-rank communicator: a rank sending to and receiving from itself runs the
+same ncclGroupStart / ncclSend / ncclRecv / ncclGroupEnd path, on the caller's stream, as
+a round between peers.  The multi-GPU run is the driver's 1/2/4/8-GPU bench."""
+import os
+import socket
+import subprocess
+import sys
+from pathlib import Path
+
+import numpy as np
+import pytest
+import torch
+
+REPO = Path(__file__).resolve().parents[1]
+
+
+def test_unique_id_and_version_without_gpu():
+    from hlsjs_p2p_wrapper_amd.ops._native import device
+
+    dev = device()
+    uid = dev.rccl_unique_id()
+    assert isinstance(uid, bytes) and len(uid) == 128
+    assert int(dev.rccl_version()) >= 21800
+    with pytest.raises(ValueError):
+        dev.RcclComm(b"short", 1, 0, 0)
+
+
+def test_gloo_world_keeps_torch_data_plane():
+    """A gloo default group never opens the native plane (CPU tests, rehearsals)."""
+    code = (
+        "import torch.distributed as dist\n"
+        "from hlsjs_p2p_wrapper_amd.parallel.comm import DistComm\n"
+        "dist.init_process_group('gloo', init_method='tcp://127.0.0.1:%d', world_size=1, rank=0)\n"
+        "c = DistComm()\n"
+        "print('RESULT', c.data_transport, c._rccl is None)\n"
+        "dist.destroy_process_group()\n" % _free_port())
+    p = subprocess.run([sys.executable, "-c", code], cwd=REPO, capture_output=True, text=True, timeout=120,
+                       env=dict(os.environ, PYTHONPATH=str(REPO)))
+    assert p.returncode == 0, p.stderr[-2000:]
+    assert [ln.split()[1:] for ln in p.stdout.splitlines() if ln.startswith("RESULT")] == [["gloo", "True"]]
+
+
+def _free_port() -> int:
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+@pytest.mark.gpu
+def test_native_rccl_self_exchange_on_stream(cuda):
+    from hlsjs_p2p_wrapper_amd.ops._native import device
+
+    dev = device()
+    comm = dev.RcclComm(dev.rccl_unique_id(), 1, 0, torch.cuda.current_device())
+    try:
+        g = torch.Generator(device="cpu").manual_seed(3)
+        seg = torch.randint(0, 256, (3_000_017,), dtype=torch.uint8, generator=g).to(cuda)
+        trailer = torch.arange(1, 65, dtype=torch.int32, device=cuda) * 0x01010101
+        out_seg = torch.zeros_like(seg)
+        out_tr = torch.zeros_like(trailer)
+        s = torch.cuda.Stream()
+        s.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(s):
+            comm.exchange(np.array([seg.data_ptr(), trailer.data_ptr()]), np.array([seg.numel(), 4 * trailer.numel()]),
+                          np.array([0, 0]), np.array([out_seg.data_ptr(), out_tr.data_ptr()]),
+                          np.array([out_seg.numel(), 4 * out_tr.numel()]), np.array([0, 0]), s.cuda_stream)
+            done = torch.cuda.Event()
+            done.record(s)
+        done.synchronize()
+        assert torch.equal(out_seg, seg) and torch.equal(out_tr, trailer)
+        assert comm.rounds == 1 and comm.async_error() == ""
+        with pytest.raises(ValueError):  # peer out of range for a world of one
+            comm.exchange(np.array([seg.data_ptr()]), np.array([16]), np.array([1]), np.zeros(0, np.int64),
+                          np.zeros(0, np.int64), np.zeros(0, np.int64), s.cuda_stream)
+    finally:
+        comm.close()
+    assert comm.closed
+
+
+@pytest.mark.gpu
+def test_distcomm_uses_native_rccl_in_an_nccl_group(cuda):
+    """DistComm over a one-rank nccl group opens the native plane and moves a round's
+    (segment buffer, CRC trailer) pair through it on the node-style side stream."""
+    code = f"""
+import torch, torch.distributed as dist
+from hlsjs_p2p_wrapper_amd.parallel.comm import DistComm
+dev = torch.device('cuda', 0)
+torch.cuda.set_device(dev)
+dist.init_process_group('nccl', init_method='tcp://127.0.0.1:{_free_port()}', world_size=1, rank=0, device_id=dev)
+c = DistComm()
+assert c.data_transport == 'rccl-native', c.data_transport
+buf = torch.arange(1 << 20, dtype=torch.int32, device=dev).view(torch.uint8)
+tr = torch.tensor([7, 8, 9], dtype=torch.int32, device=dev)
+rb, rt = torch.empty_like(buf), torch.empty_like(tr)
+s = torch.cuda.Stream(dev)
+s.wait_stream(torch.cuda.current_stream())
+with torch.cuda.stream(s):
+    c.exchange([(0, buf), (0, tr)], [(0, rb), (0, rt)])
+torch.cuda.synchronize()
+assert torch.equal(rb, buf) and torch.equal(rt, tr)
+c.close()
+dist.destroy_process_group()
+print('NATIVE_OK')
+"""
+    p = subprocess.run([sys.executable, "-c", code], cwd=REPO, capture_output=True, text=True, timeout=180,
+                       env=dict(os.environ, PYTHONPATH=str(REPO)))
+    assert p.returncode == 0 and "NATIVE_OK" in p.stdout, (p.stdout[-2000:], p.stderr[-4000:])
