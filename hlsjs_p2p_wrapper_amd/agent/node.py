@@ -61,20 +61,32 @@ def swarm_id_for(content_id: str) -> int:
     return zlib.crc32(content_id.encode()) & 0x7FFFFFFF
 
 
-@dataclass(eq=False)
+_M32 = 0xFFFFFFFF
+
+
 class Request:
-    node: "SwarmNode"
-    key: Tuple[int, int, int, int]
-    url: str
-    headers: Dict[str, str]
-    callbacks: Any
-    agent: Any = None
-    aborted: bool = False
-    done: bool = False
-    t_submit: float = 0.0
+    """One ``getSegment`` request: the loader handle (``abort()``) and its delivery state."""
+
+    __slots__ = ("node", "key", "url", "headers", "callbacks", "agent", "aborted", "done", "t_submit")
+
+    def __init__(self, node: "SwarmNode", key: Tuple[int, int, int, int], url: str, headers: Dict[str, str],
+                 callbacks: Any, agent: Any = None, aborted: bool = False, done: bool = False,
+                 t_submit: float = 0.0) -> None:
+        self.node = node
+        self.key = key
+        self.url = url
+        self.headers = headers
+        self.callbacks = callbacks
+        self.agent = agent
+        self.aborted = aborted
+        self.done = done
+        self.t_submit = t_submit
 
     def abort(self) -> None:
         self.aborted = True
+
+    def __repr__(self) -> str:
+        return f"Request(key={self.key}, url={self.url!r}, aborted={self.aborted}, done={self.done})"
 
 
 @dataclass(eq=False)
@@ -237,8 +249,9 @@ class SwarmNode:
     # ------------------------------------------------------------------ requests
     def request(self, key: Tuple[int, int, int, int], url: str, headers: Optional[Dict[str, str]],
                 callbacks: Any, agent: Any = None) -> Request:
-        req = Request(self, tuple(int(k) & 0xFFFFFFFF for k in key), url, dict(headers or {}), callbacks, agent,
-                      t_submit=self.loop.now())
+        k0, k1, k2, k3 = key
+        req = Request(self, (int(k0) & _M32, int(k1) & _M32, int(k2) & _M32, int(k3) & _M32), url,
+                      dict(headers) if headers else {}, callbacks, agent, False, False, self.loop.now())
         eid = self.store.lookup1(*req.key)
         if eid >= 0:  # local cache hit
             self.store.pin(np.array([eid], dtype=np.int64))
@@ -744,10 +757,11 @@ class SwarmNode:
             o, n = h.recv_entries[0][3:5]
             if n:
                 self.arena[o + n // 2] ^= 0x5A
-        expect = trailers
-        ids_t = torch.from_numpy(rid_a).to(dev, non_blocking=True)
-        self.crc_dev[ids_t] = expect
-        _, ok = _crc.crc32_batch(self.arena, np.concatenate(roff), np.concatenate(rlen), expect_dev=expect)
+        # verify against the senders' trailers; the combine kernel also scatters the computed
+        # CRCs into the per-entry table (ids ride the descriptor H2D): a mismatching entry is
+        # dropped in complete_round, so the table only ever serves verified values
+        _, ok = _crc.crc32_batch(self.arena, np.concatenate(roff), np.concatenate(rlen), expect_dev=trailers,
+                                 scatter_to=self.crc_dev, scatter_idx=rid_a)
         if self.is_cuda:
             h.ok_host = torch.empty(ok.numel(), dtype=torch.uint8, pin_memory=True)
             h.ok_host.copy_(ok, non_blocking=True)

@@ -61,6 +61,10 @@ class Shaper:
 
 _registry: Dict[str, Any] = {}
 _reg_lock = threading.Lock()
+# url -> (origin, path): every fragment URL is resolved at request (size) and again at
+# fetch time; the longest-prefix scan is done once per URL.  Cleared on any registry change.
+_resolved: Dict[str, Tuple[Any, str]] = {}
+_RESOLVED_MAX = 1 << 16
 
 
 def register_origin(base_url: str, origin: Any) -> None:
@@ -68,6 +72,7 @@ def register_origin(base_url: str, origin: Any) -> None:
         base_url += "/"
     with _reg_lock:
         _registry[base_url] = origin
+        _resolved.clear()
 
 
 def unregister_origin(base_url: str) -> None:
@@ -75,21 +80,30 @@ def unregister_origin(base_url: str) -> None:
         base_url += "/"
     with _reg_lock:
         _registry.pop(base_url, None)
+        _resolved.clear()
 
 
 def clear_origins() -> None:
     with _reg_lock:
         _registry.clear()
+        _resolved.clear()
 
 
 def resolve(url: str) -> Tuple[Any, str]:
+    hit = _resolved.get(url)
+    if hit is not None:
+        return hit
     best = None
     for base, origin in list(_registry.items()):
         if url.startswith(base) and (best is None or len(base) > len(best[0])):
             best = (base, origin)
     if best is None:
         raise HttpError(0, url, f"no origin serves {url}")  # status 0 = network error
-    return best[1], url[len(best[0]):]
+    hit = (best[1], url[len(best[0]):])
+    if len(_resolved) >= _RESOLVED_MAX:
+        _resolved.clear()
+    _resolved[url] = hit
+    return hit
 
 
 _RANGE = re.compile(r"bytes=(\d+)-(\d*)")

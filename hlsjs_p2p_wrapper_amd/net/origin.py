@@ -209,6 +209,8 @@ class SyntheticHlsOrigin:
             self._corrupt.clear()
 
     def _check_fail(self, path: str) -> None:
+        if not self._failures:  # the common case, per request: no lock
+            return
         with self._lock:
             for i, (rx, status, times) in enumerate(self._failures):
                 if rx.search(path):
@@ -219,6 +221,8 @@ class SyntheticHlsOrigin:
                     raise HttpError(status, path)
 
     def should_corrupt(self, path: str) -> bool:
+        if not self._corrupt:
+            return False
         with self._lock:
             for i, (rx, times) in enumerate(self._corrupt):
                 if rx.search(path) and times != 0:

@@ -6,5 +6,5 @@ cd $R
 export PYTHONPATH=$R
 O=gpurun_out/sample
 mkdir -p $O
-HLSJS_P2P_PURE=1 timeout -k 10 300 python tools/sample_prof.py --config ${CONFIG:-hostcost} --steps 1500 --warmup 10 --verbose > $O/pure.out 2> $O/pure.txt
+SAMPLE_TOP=400 HLSJS_P2P_PURE=1 timeout -k 10 300 python tools/sample_prof.py --config ${CONFIG:-hostcost} --steps 1500 --warmup 10 --verbose > $O/pure.out 2> $O/pure.txt
 timeout -k 10 300 python bench.py --config ${CONFIG:-hostcost} --steps 100 --warmup 10 --verbose > $O/compiled.out 2> $O/compiled.txt

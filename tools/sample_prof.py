@@ -55,7 +55,7 @@ def main():
     short = lambda p: p.split("hlsjs_p2p_wrapper_amd/")[-1].split("site-packages/")[-1]
     print(f"# {n} samples", file=sys.stderr)
     print("# self time by line", file=sys.stderr)
-    for (fn, ln, name), c in self_lines.most_common(60):
+    for (fn, ln, name), c in self_lines.most_common(int(os.environ.get("SAMPLE_TOP", "60"))):
         print(f"{100.0 * c / n:6.2f}%  {short(fn)}:{ln} {name}", file=sys.stderr)
     print("# inclusive time by function", file=sys.stderr)
     for (fn, ln, name), c in incl_funcs.most_common(70):
