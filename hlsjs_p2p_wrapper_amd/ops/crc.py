@@ -9,6 +9,7 @@ shift-operator combine).  CPU path: slice-by-8 host oracle (== ``zlib.crc32``).
 """
 from __future__ import annotations
 
+import os
 import threading
 from typing import Dict, Optional, Sequence, Tuple
 
@@ -19,16 +20,24 @@ from ._native import device as _dev
 from ._native import runtime as _rt
 from .desc import pack_to_device
 
-_consts: Dict[str, tuple] = {}
+_consts: Dict[tuple, tuple] = {}
 _lock = threading.Lock()
 
 
-def _device_consts(device: torch.device):
-    k = str(device)
+# matrix-core path of the residue kernel: "fp4" (f8f6f4 MFMA, e2m1 operands, 32 MFMAs per
+# 8 KB tile) or "i8" (v_mfma_i32_32x32x32_i8, 64 per tile); the B-fragment dtype selects it
+MFMA_VARIANT = os.environ.get("HLSP2P_CRC_MFMA", "fp4")
+
+
+def _device_consts(device: torch.device, variant: str):
+    k = (str(device), variant)
     c = _consts.get(k)
     if c is None:
+        if variant not in ("fp4", "i8"):
+            raise ValueError(f"unknown CRC MFMA variant {variant!r}")
         rt = _rt()
-        w = torch.from_numpy(rt.crc_mfma_weights()).to(device)
+        frags = rt.crc_mfma_weights_fp4() if variant == "fp4" else rt.crc_mfma_weights()
+        w = torch.from_numpy(frags).to(device)
         t = torch.from_numpy(rt.crc_shift_tables().view(np.int32)).to(device)
         c = (w, t)
         with _lock:
@@ -39,7 +48,8 @@ def _device_consts(device: torch.device):
 def crc32_batch(buf: torch.Tensor, offs: Sequence[int], lens: Sequence[int],
                 expect: Optional[Sequence[int]] = None,
                 expect_dev: Optional[torch.Tensor] = None, scatter_to: Optional[torch.Tensor] = None,
-                scatter_idx: Optional[Sequence[int]] = None) -> Tuple[torch.Tensor, Optional[torch.Tensor]]:
+                scatter_idx: Optional[Sequence[int]] = None,
+                variant: Optional[str] = None) -> Tuple[torch.Tensor, Optional[torch.Tensor]]:
     """CRC-32 of ``buf[offs[i]:offs[i]+lens[i]]``.
 
     Returns ``(crc int32[B], ok uint8[B] | None)`` on ``buf.device``; ``ok`` is produced
@@ -47,6 +57,7 @@ def crc32_batch(buf: torch.Tensor, offs: Sequence[int], lens: Sequence[int],
     With ``scatter_to`` (int32 table on ``buf.device``) the CRCs are also written to
     ``scatter_to[scatter_idx[i]]`` -- on the device by the combine kernel, whose index
     array rides the same descriptor H2D (no separate index copy / index_put launch).
+    ``variant`` picks the residue kernel's matrix-core path (default :data:`MFMA_VARIANT`).
     """
     B = len(offs)
     o = np.asarray(offs, dtype=np.int64)
@@ -88,7 +99,7 @@ def crc32_batch(buf: torch.Tensor, offs: Sequence[int], lens: Sequence[int],
     if sidx is not None:
         arrays["si"] = sidx
     d = pack_to_device(arrays, buf.device)
-    w, tables = _device_consts(buf.device)
+    w, tables = _device_consts(buf.device, variant or MFMA_VARIANT)
     residues = torch.empty(max(1, int(groups.sum())), dtype=torch.int32, device=buf.device)
     crc = torch.empty(B, dtype=torch.int32, device=buf.device)
     exp_t = expect_dev if expect_dev is not None else d.get("ex")

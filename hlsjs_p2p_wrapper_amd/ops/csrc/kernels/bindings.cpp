@@ -16,7 +16,7 @@ hipError_t launch_aes128_cbc_decrypt(const uint8_t*, uint8_t*, const int64_t*, c
                                      const uint8_t*, int64_t*, int, int64_t, int, hipStream_t);
 hipError_t launch_crc32_batch(const uint8_t*, const int64_t*, const int64_t*, const int64_t*, const int64_t*,
                               const void*, const uint32_t*, uint32_t*, uint32_t*, const uint32_t*, uint8_t*,
-                              const int64_t*, uint32_t*, int64_t, int, int64_t, int, hipStream_t);
+                              const int64_t*, uint32_t*, int64_t, int, int64_t, int, bool, hipStream_t);
 hipError_t launch_ts_demux(const uint8_t*, const int64_t*, const int64_t*, const int64_t*, int, int64_t, uint32_t*,
                            int64_t*, int32_t*, uint8_t*, const int64_t*, int64_t*, int64_t, int64_t*, hipStream_t);
 hipError_t launch_range_select(const double*, const int64_t*, const int64_t*, const double*, const double*, int64_t*,
@@ -104,7 +104,10 @@ void crc32_batch(Tensor buf, Tensor seg_off, Tensor seg_len, Tensor tile_prefix,
   check(seg_len, "seg_len", torch::kInt64, B);
   check(tile_prefix, "tile_prefix", torch::kInt64, B + 1);
   check(res_off, "res_off", torch::kInt64, B);
-  check(wfrag, "wfrag", torch::kInt8, 64 * 64 * 16);
+  // B fragments pick the matrix-core path: int8 [64 steps][64 lanes][16] for the i8 MFMA,
+  // uint8 [32][64][16] of packed e2m1 nibbles for the FP4 f8f6f4 MFMA
+  const bool fp4 = wfrag.scalar_type() == torch::kUInt8;
+  check(wfrag, "wfrag", fp4 ? torch::kUInt8 : torch::kInt8, fp4 ? 32 * 64 * 16 : 64 * 64 * 16);
   check(tables, "tables", torch::kInt32, 48 * 1024);
   check(residues, "residues", torch::kInt32);
   check(crc_out, "crc_out", torch::kInt32, B);
@@ -133,7 +136,7 @@ void crc32_batch(Tensor buf, Tensor seg_off, Tensor seg_len, Tensor tile_prefix,
   ok(D::launch_crc32_batch(cptr<uint8_t>(buf), cptr<int64_t>(seg_off), cptr<int64_t>(seg_len),
                            cptr<int64_t>(tile_prefix), cptr<int64_t>(res_off), wfrag.data_ptr(),
                            cptr<uint32_t>(tables), mptr<uint32_t>(residues), mptr<uint32_t>(crc_out), ex, okp,
-                           sidx, sout, sn, static_cast<int>(B), total_tiles, num_cus(buf), stream()),
+                           sidx, sout, sn, static_cast<int>(B), total_tiles, num_cus(buf), fp4, stream()),
      "crc32_batch");
 }
 

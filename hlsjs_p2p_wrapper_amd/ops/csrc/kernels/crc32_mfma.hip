@@ -147,6 +147,96 @@ __global__ __launch_bounds__(kCrcThreads) void crc32_group_residue_kernel(
   }
 }
 
+// FP4 variant on the block-scaled f8f6f4 matrix cores (v_mfma_scale_f32_32x32x64_f8f6f4,
+// e2m1 A and B, unit scales).  An FP4 MFMA takes the cycles of the i8 32x32x32 one but
+// covers 64 k, so a tile needs 32 MFMAs instead of 64; each consumes ONE data dword per lane
+// (vs 16 bytes masked to one bit), fed as 4 operand dwords -- bits 0/1/2/3 of every nibble:
+// d & 0x11111111 (= 0.5), d & 0x22222222 (= 1.0), d & 0x44444444 (= 2.0),
+// (d >> 1) & 0x44444444 (= 2.0) -- with B pre-scaled by the inverse on the host
+// (crc_host.cpp: mfma_group_weights_fp4), so every nonzero product is exactly 1.0 and the
+// f32 accumulator is an exact count (<= 2048): its parity is the GF(2) residue bit.
+// Step s = 4q + w uses dword w of the lane's 16-byte chunk q (same loads as the i8 path).
+typedef int v8i __attribute__((ext_vector_type(8)));
+typedef float v16f __attribute__((ext_vector_type(16)));
+
+__global__ __launch_bounds__(kCrcThreads) void crc32_group_residue_fp4_kernel(
+    const uint8_t* __restrict__ buf, const int64_t* __restrict__ seg_off, const int64_t* __restrict__ seg_len,
+    const int64_t* __restrict__ tile_prefix, const int64_t* __restrict__ res_off, const v4i* __restrict__ wfrag,
+    uint32_t* __restrict__ residues, int nseg, int64_t total_tiles, int64_t tiles_per_wave) {
+  __shared__ v4i s_w[32 * 64];  // 32 KiB: [step][lane] fragments
+  const int tid = threadIdx.x;
+  lds_fill<32 * 64 / kCrcThreads>(s_w, wfrag, 32 * 64, tid, kCrcThreads);
+  __syncthreads();
+
+  const int lane = tid & 63;
+  const int wave = tid >> 6;
+  const int r = lane & 31, h = lane >> 5;
+  const int64_t gwave = static_cast<int64_t>(blockIdx.x) * (kCrcThreads / 64) + wave;
+  const int64_t t_begin = gwave * tiles_per_wave;
+  const int64_t t_end = t_begin + tiles_per_wave < total_tiles ? t_begin + tiles_per_wave : total_tiles;
+  if (t_begin >= t_end) return;
+  int seg = find_seg_wave(tile_prefix, nseg, t_begin);
+  int64_t base = seg_off[seg], len = seg_len[seg], tstart = tile_prefix[seg], tend = tile_prefix[seg + 1];
+  int64_t roff = res_off[seg];
+  uint4 n0, n1, n2, n3, n4, n5, n6, n7;  // the next tile's chunks
+  auto load_tile = [&](int64_t tile) {
+    const int64_t my = tile * kTileBytes + r * 256 + h * 16;
+    if ((tile + 1) * kTileBytes <= len) {
+      const uint4* p = reinterpret_cast<const uint4*>(buf + base + my);
+      n0 = p[0]; n1 = p[2]; n2 = p[4]; n3 = p[6]; n4 = p[8]; n5 = p[10]; n6 = p[12]; n7 = p[14];
+    } else {
+      n0 = load_tail(buf, base, my, len);        n1 = load_tail(buf, base, my + 32, len);
+      n2 = load_tail(buf, base, my + 64, len);   n3 = load_tail(buf, base, my + 96, len);
+      n4 = load_tail(buf, base, my + 128, len);  n5 = load_tail(buf, base, my + 160, len);
+      n6 = load_tail(buf, base, my + 192, len);  n7 = load_tail(buf, base, my + 224, len);
+    }
+  };
+  load_tile(t_begin - tstart);
+  for (int64_t t = t_begin; t < t_end; ++t) {
+    uint4 c0 = n0, c1 = n1, c2 = n2, c3 = n3, c4 = n4, c5 = n5, c6 = n6, c7 = n7;
+    const int64_t tile = t - tstart;
+    const int64_t c_len = len, c_roff = roff;
+    if (t + 1 < t_end) {
+      if (t + 1 >= tend) {
+        seg = advance_seg(tile_prefix, seg, t + 1);
+        base = seg_off[seg];
+        len = seg_len[seg];
+        tstart = tile_prefix[seg];
+        tend = tile_prefix[seg + 1];
+        roff = res_off[seg];
+      }
+      load_tile(t + 1 - tstart);
+    }
+    v16f acc = {};
+#pragma unroll 1
+    for (int q = 0; q < 8; ++q) {
+      const uint32_t dw[4] = {c0.x, c0.y, c0.z, c0.w};
+#pragma unroll
+      for (int w = 0; w < 4; ++w) {
+        const uint32_t d = dw[w];
+        const v8i a = {static_cast<int>(d & 0x11111111u), static_cast<int>(d & 0x22222222u),
+                       static_cast<int>(d & 0x44444444u), static_cast<int>((d >> 1) & 0x44444444u), 0, 0, 0, 0};
+        const v4i b4 = s_w[(4 * q + w) * 64 + lane];
+        const v8i b = {b4.x, b4.y, b4.z, b4.w, 0, 0, 0, 0};
+        // cbsz = blgp = 4: e2m1 A and B; scale exponents 0 select the unscaled form
+        acc = __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(a, b, acc, 4, 4, 0, 0, 0, 0);
+      }
+      c0 = c1; c1 = c2; c2 = c3; c3 = c4; c4 = c5; c5 = c6; c6 = c7;
+    }
+    const int64_t groups = (c_len + 255) >> 8;
+    const int64_t g0 = tile * 32;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+      const uint64_t m = __ballot(static_cast<int>(acc[i]) & 1);  // exact count: parity = GF(2) sum
+      const int row = (i & 3) + 8 * (i >> 2);
+      if (lane == 0) {
+        if (g0 + row < groups) residues[c_roff + g0 + row] = static_cast<uint32_t>(m);
+        if (g0 + row + 4 < groups) residues[c_roff + g0 + row + 4] = static_cast<uint32_t>(m >> 32);
+      }
+    }
+  }
+}
+
 __device__ __forceinline__ uint32_t apply_tab(const uint32_t* __restrict__ t, uint32_t v) {
   return t[v & 0xff] ^ t[256 + ((v >> 8) & 0xff)] ^ t[512 + ((v >> 16) & 0xff)] ^ t[768 + (v >> 24)];
 }
@@ -248,7 +338,7 @@ hipError_t launch_crc32_batch(const uint8_t* buf, const int64_t* seg_off, const 
                               const int64_t* tile_prefix, const int64_t* res_off, const void* wfrag,
                               const uint32_t* tables, uint32_t* residues, uint32_t* crc_out, const uint32_t* expect,
                               uint8_t* ok_out, const int64_t* scatter_idx, uint32_t* scatter_out, int64_t scatter_n,
-                              int nseg, int64_t total_tiles, int num_cu, hipStream_t stream) {
+                              int nseg, int64_t total_tiles, int num_cu, bool fp4, hipStream_t stream) {
   if (nseg <= 0) return hipSuccess;
   if (total_tiles > 0) {
     const int64_t waves_max = static_cast<int64_t>(num_cu) * 2 * (kCrcThreads / 64);
@@ -256,9 +346,14 @@ hipError_t launch_crc32_batch(const uint8_t* buf, const int64_t* seg_off, const 
     if (tiles_per_wave < 1) tiles_per_wave = 1;
     const int64_t waves = (total_tiles + tiles_per_wave - 1) / tiles_per_wave;
     const int64_t grid = (waves + (kCrcThreads / 64) - 1) / (kCrcThreads / 64);
-    hipLaunchKernelGGL(crc32_group_residue_kernel, dim3(static_cast<unsigned>(grid)), dim3(kCrcThreads), 0, stream,
-                       buf, seg_off, seg_len, tile_prefix, res_off, reinterpret_cast<const v4i*>(wfrag), residues,
-                       nseg, total_tiles, tiles_per_wave);
+    if (fp4)
+      hipLaunchKernelGGL(crc32_group_residue_fp4_kernel, dim3(static_cast<unsigned>(grid)), dim3(kCrcThreads), 0,
+                         stream, buf, seg_off, seg_len, tile_prefix, res_off, reinterpret_cast<const v4i*>(wfrag),
+                         residues, nseg, total_tiles, tiles_per_wave);
+    else
+      hipLaunchKernelGGL(crc32_group_residue_kernel, dim3(static_cast<unsigned>(grid)), dim3(kCrcThreads), 0, stream,
+                         buf, seg_off, seg_len, tile_prefix, res_off, reinterpret_cast<const v4i*>(wfrag), residues,
+                         nseg, total_tiles, tiles_per_wave);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
   }

@@ -195,6 +195,12 @@ PYBIND11_MODULE(_runtime, m) {
     std::memcpy(a.mutable_data(), w.data(), w.size());
     return a;
   });
+  m.def("crc_mfma_weights_fp4", [] {
+    auto w = crc::mfma_group_weights_fp4();
+    Arr<uint8_t> a(static_cast<py::ssize_t>(w.size()));
+    std::memcpy(a.mutable_data(), w.data(), w.size());
+    return a;
+  });
   m.def("crc_shift_tables", [] {
     auto t = crc::shift_tables();
     Arr<uint32_t> a(static_cast<py::ssize_t>(t.size()));

@@ -141,6 +141,53 @@ std::vector<int8_t> mfma_group_weights() {
   return w;
 }
 
+namespace {
+// v[byte][bit]: raw CRC (zero init) of a 256-byte group with only that bit set
+struct GroupBitCrc {
+  uint32_t v[kGroupBytes][8];
+  GroupBitCrc() {
+    const ByteTable& T = table();
+    for (int bit = 0; bit < 8; ++bit) {
+      uint32_t r = T.t[0][1u << bit];
+      for (int b = kGroupBytes - 1; b >= 0; --b) {
+        v[b][bit] = r;
+        r = (r >> 8) ^ T.t[0][r & 0xff];
+      }
+    }
+  }
+};
+}  // namespace
+
+std::vector<uint8_t> mfma_group_weights_fp4() {
+  static const GroupBitCrc g;
+  // Step s = 4q + w consumes data dword w of the lane's 16-byte chunk q, i.e. group bytes
+  // [32q + 16h + 4w, +4) for lane half h.  The kernel feeds that dword d as 4 fp4 operand
+  // dwords: A_v = d & 0x11111111 (bit 0 of each nibble = e2m1 0.5), d & 0x22222222 (bit 1 =
+  // 1.0), d & 0x44444444 (bit 2 = 2.0) and (d >> 1) & 0x44444444 (bit 3 = 2.0): element
+  // j = 8v + e (nibble e of operand dword v) carries data bit 4e + v of d.  B holds the
+  // weight bit of the same k scaled by the inverse (2.0, 1.0, 0.5, 0.5), so every nonzero
+  // product is exactly 1.0 and the f32 accumulator counts set terms: its parity is the
+  // GF(2) sum.  A and B share the element -> k assignment, so the MFMA's internal k order
+  // does not matter.
+  static const uint8_t kOne[4] = {0x4, 0x2, 0x1, 0x1};  // e2m1: 2.0, 1.0, 0.5, 0.5
+  std::vector<uint8_t> w(32 * 64 * 16, 0);
+  for (int s = 0; s < 32; ++s) {
+    const int q = s >> 2, wd = s & 3;
+    for (int lane = 0; lane < 64; ++lane) {
+      const int col = lane & 31, h = lane >> 5;
+      uint8_t* frag = &w[(size_t(s) * 64 + lane) * 16];
+      for (int v = 0; v < 4; ++v)
+        for (int e = 0; e < 8; ++e) {
+          const int bit = 4 * e + v;  // bit of the data dword
+          const int byte = 32 * q + 16 * h + 4 * wd + (bit >> 3);
+          if (!((g.v[byte][bit & 7] >> col) & 1u)) continue;
+          frag[4 * v + (e >> 1)] |= static_cast<uint8_t>(kOne[v] << (4 * (e & 1)));
+        }
+    }
+  }
+  return w;
+}
+
 std::vector<uint32_t> shift_tables() {
   std::vector<uint32_t> out(size_t(kNumP + kNumQ) * kSliceWords);
   Mat a8 = zero_byte_op();

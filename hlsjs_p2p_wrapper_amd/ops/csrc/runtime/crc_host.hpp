@@ -41,6 +41,9 @@ void slice_table(const Mat& m, uint32_t* out /* kSliceWords */);
 
 // MFMA B-fragment weight table: [step s=0..63][lane=0..63][16 int8] = 65536 bytes.
 std::vector<int8_t> mfma_group_weights();
+// FP4 (e2m1) variant for v_mfma_scale_f32_32x32x64_f8f6f4: [step s=0..31][lane][16 bytes of
+// packed nibbles] = 32768 bytes (see crc32_mfma.hip for the operand scheme).
+std::vector<uint8_t> mfma_group_weights_fp4();
 // Byte-slice tables: P_0..P_39 then Q_0..Q_7, each kSliceWords u32.
 std::vector<uint32_t> shift_tables();
 

@@ -63,3 +63,36 @@ def test_host_crc_matches_zlib(rt):
     for n in (0, 1, 7, 8, 9, 1000, 65537):
         d = rng.integers(0, 256, n, dtype=np.uint8)
         assert rt.crc32(d) == zlib.crc32(d.tobytes())
+
+
+_E2M1 = np.array([0, 0.5, 1, 1.5, 2, 3, 4, 6, -0.0, -0.5, -1, -1.5, -2, -3, -4, -6])
+
+
+def _fp4_elements(words) -> np.ndarray:
+    """32 e2m1 values of a 4-dword operand fragment, element j = 8v + e = nibble e of dword v."""
+    w = np.asarray(words, dtype=np.uint64).reshape(4, 1)
+    nib = (w >> (4 * np.arange(8, dtype=np.uint64))) & 0xF
+    return _E2M1[nib.reshape(-1).astype(np.int64)]
+
+
+def test_fp4_mfma_crc_formulation_matches_zlib(rt):
+    """The f8f6f4 path: each step feeds one data dword per lane as four e2m1 operand dwords
+    (nibble bits 0/1/2/3 = 0.5/1.0/2.0/2.0) against host B fragments scaled by the inverse;
+    the f32 accumulator must be an exact count whose parity is the group's raw CRC bit."""
+    w = rt.crc_mfma_weights_fp4().reshape(32, 64, 16)
+    b = np.stack([[_fp4_elements(np.frombuffer(w[s, lane].tobytes(), dtype=np.uint32)) for lane in range(64)]
+                  for s in range(32)])  # [s][lane][32]
+    rng = np.random.default_rng(11)
+    groups = rng.integers(0, 256, size=(6, 256), dtype=np.uint8)
+    groups[0] = 0xFF  # every nibble bit set: the largest counts
+    for grp in groups:
+        acc = np.zeros(32)
+        for s in range(32):
+            q, wd = s >> 2, s & 3
+            for h in range(2):
+                d = int(np.frombuffer(grp[32 * q + 16 * h + 4 * wd:][:4].tobytes(), dtype=np.uint32)[0])
+                a = _fp4_elements([d & 0x11111111, d & 0x22222222, d & 0x44444444, (d >> 1) & 0x44444444])
+                acc += b[s, 32 * h:32 * h + 32] @ a
+        assert np.all(acc == np.round(acc)) and acc.max() <= 2048  # exact in f32
+        par = sum((int(acc[c]) & 1) << c for c in range(32))
+        assert par == (~zlib.crc32(grp.tobytes(), 0xFFFFFFFF)) & 0xFFFFFFFF  # zero-init register

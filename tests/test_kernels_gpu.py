@@ -15,7 +15,8 @@ def _rand(n, seed):
     return np.random.default_rng(seed).integers(0, 256, size=n, dtype=np.uint8)
 
 
-def test_crc32_mfma_matches_zlib(cuda):
+@pytest.mark.parametrize("variant", ["fp4", "i8"])
+def test_crc32_mfma_matches_zlib(cuda, variant):
     rng = np.random.default_rng(0)
     lens = [0, 1, 15, 16, 255, 256, 257, 4096, 8191, 8192, 8193, 100003, 3_000_064, 1 << 20, 5_000_011]
     offs, blob = [], []
@@ -29,13 +30,13 @@ def test_crc32_mfma_matches_zlib(cuda):
     buf = np.concatenate(blob)
     t = torch.from_numpy(buf).to(cuda)
     expect = [zlib.crc32(buf[o:o + n].tobytes()) for o, n in zip(offs, lens)]
-    got, ok = crc.crc32_batch(t, offs, lens, expect=expect)
+    got, ok = crc.crc32_batch(t, offs, lens, expect=expect, variant=variant)
     got = got.cpu().numpy().view(np.uint32)
     assert [int(x) for x in got] == expect
     assert ok.cpu().numpy().tolist() == [1] * len(lens)
     # corrupt one byte -> mismatch detected
     t[offs[7] + 3] ^= 0x40
-    _, ok2 = crc.crc32_batch(t, offs, lens, expect=expect)
+    _, ok2 = crc.crc32_batch(t, offs, lens, expect=expect, variant=variant)
     assert ok2.cpu().numpy().tolist()[7] == 0
     _ = rng
 
