@@ -304,8 +304,13 @@ class DistComm(SwarmComm):
         self._rccl.exchange(ptr[:ns], nbytes[:ns], peer[:ns], ptr[ns:], nbytes[ns:], peer[ns:], stream)
 
     def close(self) -> None:
+        """Release the native RCCL communicator.  Callers close after their last round has
+        completed on the device, so this aborts (returns without waiting on peers) rather
+        than runs ncclCommDestroy's finalize, which a rank that already left could hang."""
         if self._rccl is not None:
-            self._rccl.close()
+            if torch.cuda.is_available():
+                torch.cuda.synchronize()
+            self._rccl.abort()
 
     def _exchange_staged(self, sends, recvs) -> None:
         """gloo data plane with GPU tensors (several ranks sharing one GPU, e.g. rehearsing

@@ -70,16 +70,17 @@ def test_two_process_gloo_swarm():
     assert out[0][3] == pytest.approx(0.5)
 
 
-def _bench_cpu(port: int, *extra: str) -> dict:
+def _bench_cpu(port: int, *extra: str, nproc: int = 2, config: str = "abr5") -> dict:
     import json
     import subprocess
     import sys
     from pathlib import Path
 
     repo = Path(__file__).resolve().parents[1]
-    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2", "--master-addr",
-           "127.0.0.1", "--master-port", str(port), str(repo / "bench.py"), "--cpu", "--gpus", "2", "--config",
-           "abr5", "--steps", "8", "--warmup", "2", "--inflight", "8", "--pool", "8", "--cache-gb", "0.5", *extra]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", str(nproc),
+           "--master-addr", "127.0.0.1", "--master-port", str(port), str(repo / "bench.py"), "--cpu", "--gpus",
+           str(nproc), "--config", config, "--steps", "8", "--warmup", "2", "--inflight", "8", "--pool", "8",
+           "--cache-gb", "0.5", *extra]
     p = subprocess.run(cmd, cwd=repo, env=dict(os.environ, PYTHONPATH=str(repo)), capture_output=True, text=True,
                        timeout=300)
     assert p.returncode == 0, p.stderr[-4000:]
@@ -95,6 +96,17 @@ def test_bench_two_ranks_abr_ladder_with_churn():
     assert calm["errors"] == 0 and churn["errors"] == 0
     assert calm["n_gpus"] == 2 and churn["config"]["churn_steps"] == 2
     assert 0 < churn["offload_ratio"] < calm["offload_ratio"]
+
+
+def test_bench_eight_ranks_driver_shape():
+    """The driver's N=8 launch (torchrun, 8 ranks, one bench.py each) rehearsed on CPU with
+    gloo: shared-memory control plane across 8 processes, every segment fetched from the
+    CDN once and forwarded to the 7 other peers (offload 7/8), no errors."""
+    res = _bench_cpu(_free_port(), nproc=8, config="hostcost-micro")
+    assert res["n_gpus"] == 8 and res["errors"] == 0
+    assert res["config"]["global_batch"] == 64 and res["config"]["parallelism"] == "swarm8-gloo"
+    assert res["offload_ratio"] == pytest.approx(7 / 8, abs=1e-3)
+    assert res["value"] > 0
 
 
 def _peer4(rank: int, world: int, port: int, q) -> None:
