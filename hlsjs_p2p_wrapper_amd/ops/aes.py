@@ -21,6 +21,7 @@ from ._native import runtime as _rt
 from .desc import pack_to_device
 
 _key_cache: Dict[bytes, np.ndarray] = {}
+_key_cache_le: Dict[bytes, np.ndarray] = {}
 _tables: Dict[str, tuple] = {}
 _lock = threading.Lock()
 
@@ -39,6 +40,22 @@ def round_keys(key: bytes) -> np.ndarray:
         with _lock:
             _key_cache[key] = rk
     return rk
+
+
+def round_keys_le(key: bytes) -> np.ndarray:
+    """Round keys as the kernel consumes them: uint32[44] byte-swapped to little-endian
+    column words (state words are used as loaded)."""
+    rk = _key_cache_le.get(key)
+    if rk is None:
+        rk = np.ascontiguousarray(round_keys(bytes(key)).astype(np.uint32).byteswap())
+        with _lock:
+            _key_cache_le[key] = rk
+    return rk
+
+
+def device_tables(device: torch.device):
+    """(TdL int32[256], InvSbox uint8[256]) on ``device`` (cached)."""
+    return _device_tables(device)
 
 
 def _device_tables(device: torch.device):

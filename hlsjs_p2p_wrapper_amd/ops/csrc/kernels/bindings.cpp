@@ -319,7 +319,8 @@ std::vector<Tensor> pack_h2d(const std::vector<pybind11::array>& arrays, int64_t
 
 }  // namespace
 
-void register_rccl(pybind11::module& m);  // rccl_comm.cpp: native RCCL data plane
+void register_rccl(pybind11::module& m);      // rccl_comm.cpp: native RCCL data plane
+void register_transmux(pybind11::module& m);  // transmux.cpp: one native call per transmux batch
 
 PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.doc() = "hlsjs-p2p-wrapper-amd CDNA4 (gfx950) kernels";
@@ -340,5 +341,6 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("h2d_batch", &h2d_batch);
   m.def("pack_h2d", &pack_h2d);
   register_rccl(m);
+  register_transmux(m);
   m.attr("ARCH") = "gfx950";
 }

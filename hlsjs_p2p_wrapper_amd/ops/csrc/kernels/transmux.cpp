@@ -1,0 +1,263 @@
+// One native call per transmux batch (player/transmux.py, SURVEY §2.2 K10 + K11): the
+// per-segment descriptor math of AES-128-CBC decrypt and MPEG-TS demux, ONE pinned staging
+// block + ONE H2D for every descriptor of the batch, the decrypt launch, the demux launch
+// sequence per group (encrypted segments demux from the decrypt buffer with their plaintext
+// lengths read on device; clear ones in place), and the async D2H of the small per-segment
+// info rows and plaintext lengths into one pinned block.
+//
+// The same steps in Python (ops/aes.py + ops/tsdemux.py: numpy prefix sums, two descriptor
+// packs, argument checks, six pybind launches, two pinned allocations) cost ~0.2 ms of host
+// time per 64-segment batch -- the host path bounds the per-GPU segment rate once peers
+// share the CDN work (N > 1); here it is tens of microseconds.
+#include <c10/hip/HIPStream.h>
+#include <hip/hip_runtime_api.h>
+#include <torch/extension.h>
+#include <pybind11/numpy.h>
+#include <pybind11/stl.h>
+
+#include <algorithm>
+#include <cstring>
+#include <vector>
+
+namespace hlsp2p {
+namespace dev {
+int aes_chunk_blocks();
+hipError_t launch_aes128_cbc_decrypt(const uint8_t*, uint8_t*, const int64_t*, const int64_t*, const int64_t*,
+                                     const int64_t*, const uint32_t*, const uint32_t*, const uint32_t*,
+                                     const uint8_t*, int64_t*, int, int64_t, int, hipStream_t);
+hipError_t launch_ts_demux(const uint8_t*, const int64_t*, const int64_t*, const int64_t*, int, int64_t, uint32_t*,
+                           int64_t*, int32_t*, uint8_t*, const int64_t*, int64_t*, int64_t, int64_t*, hipStream_t);
+}  // namespace dev
+}  // namespace hlsp2p
+
+namespace {
+
+namespace py = pybind11;
+using torch::Tensor;
+using I64 = py::array_t<int64_t, py::array::c_style | py::array::forcecast>;
+
+constexpr int64_t kAlign = 256;   // segment start alignment in the decrypt / ES buffers
+constexpr int64_t kPacket = 188;  // MPEG-TS packet
+constexpr int64_t kInfo = 24;     // int64 words per segment info row (ops/tsdemux.py INFO_WORDS)
+
+int64_t align_up(int64_t n) { return (n + kAlign - 1) / kAlign * kAlign; }
+
+// Host staging of many small arrays, 16-byte aligned, copied to the device in one H2D.
+class Desc {
+ public:
+  int64_t add(const void* p, int64_t nbytes) {
+    const int64_t off = static_cast<int64_t>(buf_.size());
+    buf_.resize(off + ((nbytes + 15) & ~int64_t(15)), 0);
+    if (nbytes) std::memcpy(buf_.data() + off, p, static_cast<size_t>(nbytes));
+    return off;
+  }
+  template <typename T>
+  int64_t add(const std::vector<T>& v) { return add(v.data(), static_cast<int64_t>(v.size() * sizeof(T))); }
+  // pinned block from the caching host allocator (recorded on the copy's stream, so reuse
+  // waits for the copy), one non-blocking H2D on the current stream
+  Tensor upload(int device) {
+    const int64_t n = std::max<int64_t>(16, static_cast<int64_t>(buf_.size()));
+    Tensor host = torch::empty({n}, torch::TensorOptions().dtype(torch::kUInt8).pinned_memory(true));
+    std::memcpy(host.data_ptr<uint8_t>(), buf_.data(), buf_.size());
+    Tensor d = torch::empty({n}, torch::TensorOptions().dtype(torch::kUInt8).device(torch::kCUDA, device));
+    d.copy_(host, /*non_blocking=*/true);
+    dev_ = d;
+    return d;
+  }
+  template <typename T>
+  T* at(int64_t off) const { return reinterpret_cast<T*>(static_cast<uint8_t*>(dev_.data_ptr()) + off); }
+
+ private:
+  std::vector<uint8_t> buf_;
+  Tensor dev_;
+};
+
+struct DemuxPlan {
+  std::vector<int64_t> idx, off, len, cap, es_off, blk_prefix;
+  int64_t es_bytes = 0, total_blocks = 0;
+  int64_t d_off = -1, d_len = -1, d_bp = -1, d_eo = -1;
+};
+
+void plan_demux(DemuxPlan& p) {
+  const size_t B = p.idx.size();
+  p.es_off.resize(B);
+  p.blk_prefix.assign(B + 1, 0);
+  int64_t pos = 0;
+  for (size_t i = 0; i < B; ++i) {
+    p.es_off[i] = pos;
+    pos += align_up(p.cap[i]);
+    const int64_t blocks = ((p.cap[i] + kPacket - 1) / kPacket + 255) / 256;
+    p.blk_prefix[i + 1] = p.blk_prefix[i] + blocks;
+  }
+  p.es_bytes = pos + kAlign;
+  p.total_blocks = p.blk_prefix[B];
+}
+
+int cus(int device) {
+  static int cached[64] = {0};
+  if (device >= 0 && device < 64 && cached[device]) return cached[device];
+  int n = 0;
+  hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, device);
+  if (n <= 0) n = 256;
+  if (device >= 0 && device < 64) cached[device] = n;
+  return n;
+}
+
+void hip_ok(hipError_t e, const char* what) { TORCH_CHECK(e == hipSuccess, what, " failed: ", hipGetErrorString(e)); }
+
+// src: uint8 device buffer holding every payload at src_off[i] (16-byte aligned) with
+// nbytes[i] bytes; enc[i] != 0 -> AES-128-CBC with round keys drk[i] (44 little-endian
+// words, equivalent inverse cipher) and IV iv[i]; encrypted sizes must be positive
+// multiples of 16 (the caller rejects others).  Returns, per group (encrypted, then clear):
+// (indices into the batch, info [B,24] device, pes device, es buffer, es offsets,
+// info rows in pinned host memory, plaintext lengths in pinned host memory (enc) or a
+// host array (clear)); plus the decrypt buffer to keep alive until the batch completes.
+py::tuple transmux_launch(Tensor src, I64 src_off, I64 nbytes, py::array_t<uint8_t, py::array::c_style> enc,
+                          py::array_t<uint32_t, py::array::c_style | py::array::forcecast> drk,
+                          py::array_t<uint8_t, py::array::c_style | py::array::forcecast> iv, Tensor td0, Tensor isb,
+                          int64_t max_pes) {
+  TORCH_CHECK(src.is_cuda() && src.is_contiguous() && src.scalar_type() == torch::kUInt8, "src: contiguous GPU uint8");
+  TORCH_CHECK((reinterpret_cast<uintptr_t>(src.data_ptr()) & 15) == 0, "src must be 16-byte aligned");
+  const int64_t B = src_off.size();
+  TORCH_CHECK(nbytes.size() == B && enc.size() == B, "transmux_launch: argument sizes differ");
+  TORCH_CHECK(drk.ndim() == 2 && drk.shape(0) == B && drk.shape(1) == 44, "drk must be [B, 44]");
+  TORCH_CHECK(iv.ndim() == 2 && iv.shape(0) == B && iv.shape(1) == 16, "iv must be [B, 16]");
+  TORCH_CHECK(td0.is_cuda() && td0.numel() >= 256 && isb.is_cuda() && isb.numel() >= 256, "AES tables");
+  TORCH_CHECK(max_pes > 0, "max_pes must be positive");
+  const int64_t* so = src_off.data();
+  const int64_t* nb = nbytes.data();
+  const uint8_t* en = enc.data();
+  const int64_t cap_src = src.numel();
+  const int device = src.get_device();
+  for (int64_t i = 0; i < B; ++i) {
+    TORCH_CHECK(so[i] >= 0 && nb[i] >= 0 && so[i] + nb[i] <= cap_src, "payload out of bounds");
+    TORCH_CHECK(so[i] % 16 == 0, "payload offsets must be 16-byte aligned");
+    if (en[i]) TORCH_CHECK(nb[i] >= 16 && nb[i] % 16 == 0, "encrypted payload is not a positive multiple of 16");
+  }
+  const auto dev_opts = torch::TensorOptions().device(torch::kCUDA, device);
+  hipStream_t st = c10::hip::getCurrentHIPStream(device).stream();
+
+  // ---- plans: AES over the encrypted segments, demux per group
+  std::vector<int64_t> a_so, a_do, a_bp{0}, a_cp{0};
+  std::vector<uint32_t> a_drk;
+  std::vector<uint8_t> a_iv;
+  DemuxPlan pe, pc;
+  const int64_t chunk = hlsp2p::dev::aes_chunk_blocks();
+  int64_t dec_pos = 0;
+  for (int64_t i = 0; i < B; ++i) {
+    if (en[i]) {
+      a_so.push_back(so[i]);
+      a_do.push_back(dec_pos);
+      pe.idx.push_back(i);
+      pe.off.push_back(dec_pos);
+      pe.cap.push_back(nb[i]);
+      dec_pos += align_up(nb[i]);
+      const int64_t blocks = nb[i] / 16;
+      a_bp.push_back(a_bp.back() + blocks);
+      a_cp.push_back(a_cp.back() + (blocks + chunk - 1) / chunk);
+      a_drk.insert(a_drk.end(), drk.data(i, 0), drk.data(i, 0) + 44);
+      a_iv.insert(a_iv.end(), iv.data(i, 0), iv.data(i, 0) + 16);
+    } else {
+      pc.idx.push_back(i);
+      pc.off.push_back(so[i]);
+      pc.cap.push_back(nb[i]);
+      pc.len.push_back(nb[i]);
+    }
+  }
+  const int64_t ne = static_cast<int64_t>(pe.idx.size()), nc = static_cast<int64_t>(pc.idx.size());
+  plan_demux(pe);
+  plan_demux(pc);
+
+  // ---- every descriptor of the batch in one staging block, one H2D
+  Desc desc;
+  int64_t d_so = -1, d_do = -1, d_bp = -1, d_cp = -1, d_drk = -1, d_iv = -1;
+  if (ne) {
+    d_so = desc.add(a_so);
+    d_do = desc.add(a_do);
+    d_bp = desc.add(a_bp);
+    d_cp = desc.add(a_cp);
+    d_drk = desc.add(a_drk);
+    d_iv = desc.add(a_iv);
+    pe.d_off = desc.add(pe.off);
+    pe.d_bp = desc.add(pe.blk_prefix);
+    pe.d_eo = desc.add(pe.es_off);
+  }
+  if (nc) {
+    pc.d_off = desc.add(pc.off);
+    pc.d_len = desc.add(pc.len);
+    pc.d_bp = desc.add(pc.blk_prefix);
+    pc.d_eo = desc.add(pc.es_off);
+  }
+  desc.upload(device);
+
+  // ---- host results block: info rows (enc group, then clear group) | enc plaintext lengths
+  Tensor host = torch::empty({(ne + nc) * kInfo + ne + 1}, torch::TensorOptions().dtype(torch::kInt64).pinned_memory(true));
+  int64_t* hp = host.data_ptr<int64_t>();
+  Tensor dec, out_len;
+  if (ne) {
+    dec = torch::empty({dec_pos + kAlign}, dev_opts.dtype(torch::kUInt8));
+    out_len = torch::empty({ne}, dev_opts.dtype(torch::kInt64));
+    hip_ok(hlsp2p::dev::launch_aes128_cbc_decrypt(
+               static_cast<const uint8_t*>(src.data_ptr()), static_cast<uint8_t*>(dec.data_ptr()),
+               desc.at<int64_t>(d_so), desc.at<int64_t>(d_do), desc.at<int64_t>(d_bp), desc.at<int64_t>(d_cp),
+               desc.at<uint32_t>(d_drk), desc.at<uint32_t>(d_iv), static_cast<const uint32_t*>(td0.data_ptr()),
+               static_cast<const uint8_t*>(isb.data_ptr()), out_len.data_ptr<int64_t>(), static_cast<int>(ne),
+               a_cp.back(), cus(device), st),
+           "aes128_cbc_decrypt");
+  }
+
+  py::list groups;
+  int64_t row0 = 0;
+  for (int g = 0; g < 2; ++g) {
+    DemuxPlan& p = g == 0 ? pe : pc;
+    const int64_t n = static_cast<int64_t>(p.idx.size());
+    if (!n) continue;
+    const uint8_t* buf = g == 0 ? static_cast<const uint8_t*>(dec.data_ptr())
+                                : static_cast<const uint8_t*>(src.data_ptr());
+    const int64_t* lens = g == 0 ? out_len.data_ptr<int64_t>() : desc.at<int64_t>(p.d_len);
+    const int64_t nb_blocks = std::max<int64_t>(1, p.total_blocks);
+    Tensor es = torch::empty({p.es_bytes}, dev_opts.dtype(torch::kUInt8));
+    Tensor meta = torch::empty({nb_blocks * 256}, dev_opts.dtype(torch::kInt32));
+    Tensor pts = torch::empty({nb_blocks * 256 * 2}, dev_opts.dtype(torch::kInt64));
+    Tensor aux = torch::empty({nb_blocks * 12 + n * 7}, dev_opts.dtype(torch::kInt32));
+    Tensor info = torch::empty({n, kInfo}, dev_opts.dtype(torch::kInt64));
+    Tensor pes = torch::empty({n, 3, max_pes, 3}, dev_opts.dtype(torch::kInt64));
+    hip_ok(hlsp2p::dev::launch_ts_demux(buf, desc.at<int64_t>(p.d_off), lens, desc.at<int64_t>(p.d_bp),
+                                        static_cast<int>(n), p.total_blocks,
+                                        reinterpret_cast<uint32_t*>(meta.data_ptr<int32_t>()),
+                                        pts.data_ptr<int64_t>(), aux.data_ptr<int32_t>(), es.data_ptr<uint8_t>(),
+                                        desc.at<int64_t>(p.d_eo), pes.data_ptr<int64_t>(), max_pes,
+                                        info.data_ptr<int64_t>(), st),
+           "ts_demux");
+    hip_ok(hipMemcpyAsync(hp + row0 * kInfo, info.data_ptr<int64_t>(), static_cast<size_t>(n * kInfo * 8),
+                          hipMemcpyDeviceToHost, st),
+           "info D2H");
+    Tensor hinfo = host.narrow(0, row0 * kInfo, n * kInfo).view({n, kInfo});
+    py::object hlens;
+    if (g == 0) {
+      hip_ok(hipMemcpyAsync(hp + (ne + nc) * kInfo, out_len.data_ptr<int64_t>(), static_cast<size_t>(ne * 8),
+                            hipMemcpyDeviceToHost, st),
+             "lengths D2H");
+      hlens = py::cast(host.narrow(0, (ne + nc) * kInfo, ne));
+    } else {
+      I64 l(static_cast<py::ssize_t>(n));
+      std::memcpy(l.mutable_data(), p.len.data(), static_cast<size_t>(n * 8));
+      hlens = l;
+    }
+    I64 idx(static_cast<py::ssize_t>(n)), eo(static_cast<py::ssize_t>(n));
+    std::memcpy(idx.mutable_data(), p.idx.data(), static_cast<size_t>(n * 8));
+    std::memcpy(eo.mutable_data(), p.es_off.data(), static_cast<size_t>(n * 8));
+    groups.append(py::make_tuple(idx, info, pes, es, eo, hinfo, hlens));
+    row0 += n;
+  }
+  // `host` is written by D2H copies on `st`: the caller keeps it (and `dec`) alive until it
+  // has waited on an event recorded after this call, so the block is never recycled early
+  return py::make_tuple(groups, dec.defined() ? py::cast(dec) : py::none(), host);
+}
+
+}  // namespace
+
+void register_transmux(py::module& m) {
+  m.def("transmux_launch", &transmux_launch, py::arg("src"), py::arg("src_off"), py::arg("nbytes"), py::arg("enc"),
+        py::arg("drk"), py::arg("iv"), py::arg("td0"), py::arg("isb"), py::arg("max_pes"));
+}

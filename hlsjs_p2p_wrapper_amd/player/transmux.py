@@ -24,6 +24,7 @@ import torch
 from ..net.event_loop import get_event_loop
 from ..ops import aes as _aes
 from ..ops import tsdemux as _ts
+from ..ops._native import device as _native_device
 from ..utils.trace import PhaseTimer
 
 ALIGN = 256
@@ -145,7 +146,10 @@ class MediaPipeline:
             bad = [i for i in enc if sizes[i] == 0 or sizes[i] % 16]
             for i in bad:
                 results[i] = {"error": ValueError("encrypted payload is not a multiple of 16 bytes"), "status": -1}
-            enc = [i for i in enc if i not in bad]
+            if bad:
+                enc = [i for i in enc if i not in bad]
+        if dev.type == "cuda":
+            return self._launch_native(jobs, src, src_offs, sizes, enc, clear, results, t1)
         if enc:
             dec_offs, pos = [], 0
             for i in enc:
@@ -190,6 +194,43 @@ class MediaPipeline:
             ev.record()
         tm.add("demux_launch", time.perf_counter() - t2)
         return _Batch(jobs, infos=infos, host=host, event=ev, results=results)
+
+    def _launch_native(self, jobs, src, src_offs, sizes, enc, clear, results, t1) -> "_Batch":
+        """GPU batch in ONE native call (``kernels/transmux.cpp``): descriptor math, one
+        staging H2D, AES-CBC decrypt, demux per group, D2H of the info rows."""
+        tm = self.timer
+        idx = enc + clear
+        n = len(idx)
+        if n == 0:  # every job was rejected above
+            return _Batch(jobs, infos=[], host=[], event=None, results=results)
+        offs = np.fromiter((src_offs[i] for i in idx), dtype=np.int64, count=n)
+        nb = np.fromiter((sizes[i] for i in idx), dtype=np.int64, count=n)
+        flags = np.zeros(n, dtype=np.uint8)
+        flags[:len(enc)] = 1
+        drk = np.zeros((n, 44), dtype=np.uint32)
+        iv = np.zeros((n, 16), dtype=np.uint8)
+        if enc:
+            k0 = jobs[enc[0]].key
+            if all(jobs[i].key is k0 or jobs[i].key == k0 for i in enc):  # one key per stream
+                drk[:len(enc)] = _aes.round_keys_le(bytes(k0))
+            else:
+                for r, i in enumerate(enc):
+                    drk[r] = _aes.round_keys_le(bytes(jobs[i].key))
+            iv[:len(enc)] = np.frombuffer(b"".join(bytes(jobs[i].iv) for i in enc), dtype=np.uint8).reshape(-1, 16)
+        td0, isb = _aes.device_tables(self.device)
+        t2 = time.perf_counter()
+        tm.add("decrypt_launch", t2 - t1)
+        groups, dec, host_block = _native_device().transmux_launch(src, offs, nb, flags, drk, iv, td0, isb,
+                                                                   _ts.DEFAULT_MAX_PES)
+        infos, host = [], []
+        for gidx, info, pes, es, es_offs, hinfo, hlens in groups:
+            batch_idx = [idx[k] for k in gidx.tolist()]
+            infos.append((batch_idx, _ts.DemuxResult(info, pes, es, es_offs), es_offs, hlens))
+            host.append((hinfo, hlens))
+        ev = self._free_events.pop() if self._free_events else torch.cuda.Event()
+        ev.record()
+        tm.add("demux_launch", time.perf_counter() - t2)
+        return _Batch(jobs, infos=infos, host=host, event=ev, results=results, keep=(dec, host_block))
 
     def _complete(self, b: "_Batch") -> List[Dict[str, Any]]:
         tm = self.timer
@@ -287,6 +328,7 @@ class _Batch:
     event: Any = None
     results: Any = None
     error: Optional[BaseException] = None
+    keep: Any = None  # device/pinned buffers the batch's in-flight work uses
 
 
 _local = threading.local()
