@@ -524,19 +524,20 @@ class SwarmNode:
             self.store.unpin(h.send_pins)
         self.stats["upload"] += h.sent_bytes
         completions: List[_Completion] = []
-        arena = self.arena
-        for w, eid, off, n in h.cdn_entries:
+        cdn_views = self._views([e[2] for e in h.cdn_entries], [e[3] for e in h.cdn_entries])
+        cdn_ms = max(h.cdn_ms, h.shaped_ms)
+        for (w, eid, off, n), view in zip(h.cdn_entries, cdn_views):
             if self._wants.get(w.key) is w:
                 del self._wants[w.key]
             if w.prefetch and not w.waiters:
                 self._prefetched[w.key] = "cdn"
             for req in w.waiters:
-                completions.append(_Completion(req, arena[off:off + n], "cdn", n, max(h.cdn_ms, h.shaped_ms), 0.0,
-                                               eid, h.shaped_ms))
+                completions.append(_Completion(req, view, "cdn", n, cdn_ms, 0.0, eid, h.shaped_ms))
         link_q: Dict[int, int] = {}  # slow-link fault injection: bytes queued per source link
         link_kbps = self.link_kbps
         wants_map = self._wants
-        for want_id, src, eid, off, n in good:
+        p2p_views = self._views([e[3] for e in good], [e[4] for e in good])
+        for (want_id, src, eid, off, n), view in zip(good, p2p_views):
             w = h.by_id.get(want_id)
             if w is None:
                 continue
@@ -551,7 +552,7 @@ class SwarmNode:
                 delay = link_q[src] * 8.0 / kbps  # kbit/s == bit/ms
                 p2p_ms = max(p2p_ms, delay)
             for req in w.waiters:
-                completions.append(_Completion(req, arena[off:off + n], "p2p", n, 0.0, p2p_ms, eid, delay, peer=src))
+                completions.append(_Completion(req, view, "p2p", n, 0.0, p2p_ms, eid, delay, peer=src))
         for e in bad:
             w = h.by_id.get(e[0])
             if w is not None:
@@ -580,6 +581,18 @@ class SwarmNode:
                            "ms": (time.perf_counter() - h.t0) * 1e3}
         if any(w.round < 0 for w in self._wants.values()):
             self._schedule()
+
+    def _views(self, offs: List[int], lens: List[int]) -> List[torch.Tensor]:
+        """Zero-copy uint8 views of the arena for a round's deliveries (one native call on
+        the GPU; a Python slice costs ~1.5 us per view)."""
+        if not offs:
+            return []
+        if self.is_cuda:
+            from ..ops._native import device as _dev
+
+            return _dev().arena_views(self.arena, np.asarray(offs, dtype=np.int64), np.asarray(lens, dtype=np.int64))
+        arena = self.arena
+        return [arena[o:o + n] for o, n in zip(offs, lens)]
 
     # ------------------------------------------------------------------ phases
     def _admit(self, wants: List[_Want]) -> List[_Want]:

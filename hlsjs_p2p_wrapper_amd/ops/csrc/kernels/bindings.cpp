@@ -321,6 +321,7 @@ std::vector<Tensor> pack_h2d(const std::vector<pybind11::array>& arrays, int64_t
 
 void register_rccl(pybind11::module& m);      // rccl_comm.cpp: native RCCL data plane
 void register_transmux(pybind11::module& m);  // transmux.cpp: one native call per transmux batch
+void register_ingest(pybind11::module& m);    // ingest.cpp: CRC launch + arena views for the node
 
 PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.doc() = "hlsjs-p2p-wrapper-amd CDNA4 (gfx950) kernels";
@@ -342,5 +343,6 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("pack_h2d", &pack_h2d);
   register_rccl(m);
   register_transmux(m);
+  register_ingest(m);
   m.attr("ARCH") = "gfx950";
 }

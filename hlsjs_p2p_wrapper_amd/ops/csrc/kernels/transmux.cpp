@@ -116,23 +116,23 @@ py::tuple transmux_launch(Tensor src, I64 src_off, I64 nbytes, py::array_t<uint8
                           py::array_t<uint32_t, py::array::c_style | py::array::forcecast> drk,
                           py::array_t<uint8_t, py::array::c_style | py::array::forcecast> iv, Tensor td0, Tensor isb,
                           int64_t max_pes) {
-  TORCH_CHECK(src.is_cuda() && src.is_contiguous() && src.scalar_type() == torch::kUInt8, "src: contiguous GPU uint8");
-  TORCH_CHECK((reinterpret_cast<uintptr_t>(src.data_ptr()) & 15) == 0, "src must be 16-byte aligned");
+  TORCH_CHECK_VALUE(src.is_cuda() && src.is_contiguous() && src.scalar_type() == torch::kUInt8, "src: contiguous GPU uint8");
+  TORCH_CHECK_VALUE((reinterpret_cast<uintptr_t>(src.data_ptr()) & 15) == 0, "src must be 16-byte aligned");
   const int64_t B = src_off.size();
-  TORCH_CHECK(nbytes.size() == B && enc.size() == B, "transmux_launch: argument sizes differ");
-  TORCH_CHECK(drk.ndim() == 2 && drk.shape(0) == B && drk.shape(1) == 44, "drk must be [B, 44]");
-  TORCH_CHECK(iv.ndim() == 2 && iv.shape(0) == B && iv.shape(1) == 16, "iv must be [B, 16]");
-  TORCH_CHECK(td0.is_cuda() && td0.numel() >= 256 && isb.is_cuda() && isb.numel() >= 256, "AES tables");
-  TORCH_CHECK(max_pes > 0, "max_pes must be positive");
+  TORCH_CHECK_VALUE(nbytes.size() == B && enc.size() == B, "transmux_launch: argument sizes differ");
+  TORCH_CHECK_VALUE(drk.ndim() == 2 && drk.shape(0) == B && drk.shape(1) == 44, "drk must be [B, 44]");
+  TORCH_CHECK_VALUE(iv.ndim() == 2 && iv.shape(0) == B && iv.shape(1) == 16, "iv must be [B, 16]");
+  TORCH_CHECK_VALUE(td0.is_cuda() && td0.numel() >= 256 && isb.is_cuda() && isb.numel() >= 256, "AES tables");
+  TORCH_CHECK_VALUE(max_pes > 0, "max_pes must be positive");
   const int64_t* so = src_off.data();
   const int64_t* nb = nbytes.data();
   const uint8_t* en = enc.data();
   const int64_t cap_src = src.numel();
   const int device = src.get_device();
   for (int64_t i = 0; i < B; ++i) {
-    TORCH_CHECK(so[i] >= 0 && nb[i] >= 0 && so[i] + nb[i] <= cap_src, "payload out of bounds");
-    TORCH_CHECK(so[i] % 16 == 0, "payload offsets must be 16-byte aligned");
-    if (en[i]) TORCH_CHECK(nb[i] >= 16 && nb[i] % 16 == 0, "encrypted payload is not a positive multiple of 16");
+    TORCH_CHECK_VALUE(so[i] >= 0 && nb[i] >= 0 && so[i] + nb[i] <= cap_src, "payload out of bounds");
+    TORCH_CHECK_VALUE(so[i] % 16 == 0, "payload offsets must be 16-byte aligned");
+    if (en[i]) TORCH_CHECK_VALUE(nb[i] >= 16 && nb[i] % 16 == 0, "encrypted payload is not a positive multiple of 16");
   }
   const auto dev_opts = torch::TensorOptions().device(torch::kCUDA, device);
   hipStream_t st = c10::hip::getCurrentHIPStream(device).stream();

@@ -185,3 +185,36 @@ def test_pack_to_device_native_dtypes_and_layout(cuda):
         assert np.array_equal(t.cpu().numpy(), ref), name
         if t.numel():
             assert t.data_ptr() % 16 == 0
+
+
+def test_native_crc_launch_matches_python_assembly(cuda):
+    """crc32_launch (one native call) == the Python-assembled launch, incl. verify + scatter."""
+    lens = [0, 17, 4096, 8193, 3_000_064, 250_000]
+    offs, pos = [], 0
+    for n in lens:
+        offs.append(pos)
+        pos += (n + 255) // 256 * 256 + 256
+    buf = torch.from_numpy(_rand(pos, 5)).to(cuda)
+    o, n = np.asarray(offs, np.int64), np.asarray(lens, np.int64)
+    expect = [zlib.crc32(buf[a:a + b].cpu().numpy().tobytes()) for a, b in zip(offs, lens)]
+    exp_dev = torch.from_numpy(np.asarray(expect, np.uint32).view(np.int32).copy()).to(cuda)
+    exp_dev[2] ^= 1  # one mismatch
+    ids = np.array([9, 3, 7, 0, 5, 11], np.int64)
+    t_native = torch.zeros(16, dtype=torch.int32, device=cuda)
+    t_py = torch.zeros(16, dtype=torch.int32, device=cuda)
+    c1, ok1 = crc.crc32_batch(buf, offs, lens, expect_dev=exp_dev, scatter_to=t_native, scatter_idx=ids)
+    c2, ok2 = crc._crc32_batch_py(buf, o, n, None, exp_dev, t_py, ids)
+    assert torch.equal(c1, c2) and torch.equal(ok1, ok2) and torch.equal(t_native, t_py)
+    assert [int(x) for x in c1.cpu().numpy().view(np.uint32)] == expect
+    assert ok1.cpu().tolist() == [1, 1, 0, 1, 1, 1]
+
+
+def test_arena_views_share_storage(cuda):
+    from hlsjs_p2p_wrapper_amd.ops._native import device
+
+    arena = torch.arange(4096, dtype=torch.int32, device=cuda).view(torch.uint8)
+    views = device().arena_views(arena, np.array([0, 256, 1000], np.int64), np.array([16, 0, 3000], np.int64))
+    assert [v.numel() for v in views] == [16, 0, 3000]
+    assert views[2].data_ptr() == arena.data_ptr() + 1000 and torch.equal(views[2], arena[1000:4000])
+    with pytest.raises(ValueError):
+        device().arena_views(arena, np.array([16000], np.int64), np.array([1000], np.int64))
