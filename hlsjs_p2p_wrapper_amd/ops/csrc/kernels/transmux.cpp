@@ -192,7 +192,6 @@ py::tuple transmux_launch(Tensor src, I64 src_off, I64 nbytes, py::array_t<uint8
 
   // ---- host results block: info rows (enc group, then clear group) | enc plaintext lengths
   Tensor host = torch::empty({(ne + nc) * kInfo + ne + 1}, torch::TensorOptions().dtype(torch::kInt64).pinned_memory(true));
-  int64_t* hp = host.data_ptr<int64_t>();
   Tensor dec, out_len;
   if (ne) {
     dec = torch::empty({dec_pos + kAlign}, dev_opts.dtype(torch::kUInt8));
@@ -229,16 +228,16 @@ py::tuple transmux_launch(Tensor src, I64 src_off, I64 nbytes, py::array_t<uint8
                                         desc.at<int64_t>(p.d_eo), pes.data_ptr<int64_t>(), max_pes,
                                         info.data_ptr<int64_t>(), st),
            "ts_demux");
-    hip_ok(hipMemcpyAsync(hp + row0 * kInfo, info.data_ptr<int64_t>(), static_cast<size_t>(n * kInfo * 8),
-                          hipMemcpyDeviceToHost, st),
-           "info D2H");
+    // D2H through torch's copy so the caching host allocator records the use of the pinned
+    // block on `st` (it is not handed out again before the copy has run, even if the batch
+    // is dropped uncompleted)
     Tensor hinfo = host.narrow(0, row0 * kInfo, n * kInfo).view({n, kInfo});
+    hinfo.copy_(info, /*non_blocking=*/true);
     py::object hlens;
     if (g == 0) {
-      hip_ok(hipMemcpyAsync(hp + (ne + nc) * kInfo, out_len.data_ptr<int64_t>(), static_cast<size_t>(ne * 8),
-                            hipMemcpyDeviceToHost, st),
-             "lengths D2H");
-      hlens = py::cast(host.narrow(0, (ne + nc) * kInfo, ne));
+      Tensor hl = host.narrow(0, (ne + nc) * kInfo, ne);
+      hl.copy_(out_len, /*non_blocking=*/true);
+      hlens = py::cast(hl);
     } else {
       I64 l(static_cast<py::ssize_t>(n));
       std::memcpy(l.mutable_data(), p.len.data(), static_cast<size_t>(n * 8));
@@ -250,8 +249,6 @@ py::tuple transmux_launch(Tensor src, I64 src_off, I64 nbytes, py::array_t<uint8
     groups.append(py::make_tuple(idx, info, pes, es, eo, hinfo, hlens));
     row0 += n;
   }
-  // `host` is written by D2H copies on `st`: the caller keeps it (and `dec`) alive until it
-  // has waited on an event recorded after this call, so the block is never recycled early
   return py::make_tuple(groups, dec.defined() ? py::cast(dec) : py::none(), host);
 }
 
