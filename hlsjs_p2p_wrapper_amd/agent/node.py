@@ -689,68 +689,52 @@ class SwarmNode:
     def _p2p_phase(self, h: RoundHandle, send_rows: np.ndarray, recv_rows: np.ndarray,
                    send_eids: np.ndarray) -> None:
         """Post this round's transfers.  Plan rows arrive sorted by (src, dst, key), so each
-        peer's rows are one contiguous run.  Bookkeeping is batched over ALL peers: one
-        gather of the send CRC trailers, one trailer buffer for every receive, one H2D of the
-        received entry ids (per-peer tensor ops cost ~30 us of host time each at 7 peers)."""
+        peer's rows are one contiguous run.  Bookkeeping is batched over ALL peers: the
+        per-peer layout and ring reservations in one native call, one gather of the send CRC
+        trailers, one trailer buffer for every receive, the arena views in one call, and the
+        received entry ids riding the verify CRC's descriptor block (per-peer Python and
+        tensor ops cost ~50 us of host time per peer per round)."""
         sends: List[Tuple[int, torch.Tensor]] = []
         recvs: List[Tuple[int, torch.Tensor]] = []
         dev = self.device
         t_prep = time.perf_counter()
-        # --- sends: one contiguous buffer (+ CRC trailer) per destination
+        # per-peer layout in ONE native call: contiguous send spans (or gather lists),
+        # one pinned ring reservation per source (SegmentStore.p2p_layout)
+        srun, gath, rrun, rid_a, roff_a = self.store.p2p_layout(
+            np.ascontiguousarray(send_rows), np.ascontiguousarray(send_eids, dtype=np.int64),
+            np.ascontiguousarray(recv_rows), self.round)
+        # --- sends: one buffer (+ CRC trailer slice) per destination
         if len(send_rows):
             present_all = send_eids >= 0
-            trailer_all = self.crc_dev[torch.from_numpy(np.where(present_all, send_eids, 0)).to(dev, non_blocking=True)]
+            idx = _dev_index(np.where(present_all, send_eids, 0), dev)
+            trailer_all = torch.index_select(self.crc_dev, 0, idx)
             if not present_all.all():  # missing entry: a bad CRC, the receiver re-fetches from the CDN
                 trailer_all[torch.from_numpy(np.flatnonzero(~present_all)).to(dev)] = -1
-            for dst, a, b in _runs(send_rows[:, 6]):
-                ids = send_eids[a:b]
-                present = present_all[a:b]
-                sizes = send_rows[a:b, 4]
-                contiguous = False
-                if present.all():
-                    ent = self.store.entries(ids)
-                    offs, lens = ent[:, 0], ent[:, 1]
-                    contiguous = bool(np.all(offs[1:] == offs[:-1] + (lens[:-1] + ALIGN - 1) // ALIGN * ALIGN)
-                                      and np.all(lens == sizes))
-                if contiguous:
-                    total = int(offs[-1] + lens[-1] - offs[0])
-                    buf = self.arena[int(offs[0]):int(offs[0]) + total]
-                else:
-                    layout = np.zeros(b - a, dtype=np.int64)
-                    if b - a > 1:
-                        layout[1:] = np.cumsum((sizes[:-1] + ALIGN - 1) // ALIGN * ALIGN)
-                    total = int(layout[-1] + sizes[-1])
+            spans = self._views(srun[:, 4].tolist(), srun[:, 5].tolist()) if len(srun) and (srun[:, 3] == 0).all() \
+                else None
+            for k, (dst, a, b, mode, off, total) in enumerate(srun.tolist()):
+                if mode == 0:
+                    buf = spans[k] if spans is not None else self.arena[off:off + total]
+                else:  # entries not back to back in the arena: gather into a staging buffer
                     buf = torch.zeros(total, dtype=torch.uint8, device=dev)
-                    if present.any():
-                        ent = self.store.entries(ids[present])
-                        n_copy = np.minimum(ent[:, 1], sizes[present])
-                        _seg.copy_segments(self.arena, buf, ent[:, 0], layout[present], n_copy)
+                    g = gath[gath[:, 0] == k]
+                    if len(g):
+                        _seg.copy_segments(self.arena, buf, g[:, 1], g[:, 2], g[:, 3])
                 sends.append((dst, buf))
                 sends.append((dst, trailer_all[a:b]))
-        # --- recvs: reserve one contiguous run per source; one trailer buffer for all of them
-        trailers = torch.empty(len(recv_rows), dtype=torch.int32, device=dev) if len(recv_rows) else None
-        rid, roff, rlen, rsrc = [], [], [], []
-        for src, a, b in _runs(recv_rows[:, 5]):
-            keys = np.ascontiguousarray(recv_rows[a:b, :4])
-            lens = np.ascontiguousarray(recv_rows[a:b, 4])
-            res = self.store.reserve_run(keys, lens, self.round)
-            if res is None:  # _admit guarantees room
-                raise RuntimeError("segment cache cannot make room for peer data")
-            base, ids, offs = res
-            self.store.pin(ids)
-            h.hold.append(ids)
-            total = int(offs[-1] + lens[-1] - offs[0])
-            recvs.append((src, self.arena[int(base):int(base) + total]))
-            recvs.append((src, trailers[a:b]))
-            rid.append(ids)
-            roff.append(offs)
-            rlen.append(lens)
-            rsrc.append(np.full(b - a, src, dtype=np.int64))
-        if rid:
-            rid_a = np.concatenate(rid)
+        # --- recvs: the reserved runs; one trailer buffer for all of them
+        if len(rrun):
+            trailers = torch.empty(len(recv_rows), dtype=torch.int32, device=dev)
+            views = self._views(rrun[:, 3].tolist(), rrun[:, 4].tolist())
+            for (src, a, b, _, _), view in zip(rrun.tolist(), views):
+                recvs.append((src, view))
+                recvs.append((src, trailers[a:b]))
+            h.hold.append(rid_a)  # pinned by p2p_layout until complete_round
             self._grow_crc(int(rid_a.max()) + 1)
-            h.recv_entries = list(zip(recv_rows[:, 7].tolist(), np.concatenate(rsrc).tolist(), rid_a.tolist(),
-                                      np.concatenate(roff).tolist(), np.concatenate(rlen).tolist()))
+            rlen = recv_rows[:, 4]
+            rsrc = recv_rows[:, 5]
+            h.recv_entries = list(zip(recv_rows[:, 7].tolist(), rsrc.tolist(), rid_a.tolist(), roff_a.tolist(),
+                                      rlen.tolist()))
         self.timer.add("p2p_prep", time.perf_counter() - t_prep)
         t = time.perf_counter()
         if self.is_cuda:
@@ -773,7 +757,7 @@ class SwarmNode:
         # verify against the senders' trailers; the combine kernel also scatters the computed
         # CRCs into the per-entry table (ids ride the descriptor H2D): a mismatching entry is
         # dropped in complete_round, so the table only ever serves verified values
-        _, ok = _crc.crc32_batch(self.arena, np.concatenate(roff), np.concatenate(rlen), expect_dev=trailers,
+        _, ok = _crc.crc32_batch(self.arena, roff_a, recv_rows[:, 4], expect_dev=trailers,
                                  scatter_to=self.crc_dev, scatter_idx=rid_a)
         if self.is_cuda:
             h.ok_host = torch.empty(ok.numel(), dtype=torch.uint8, pin_memory=True)
@@ -899,6 +883,15 @@ def _runs(col: np.ndarray) -> List[Tuple[int, int, int]]:
     starts = [0] + cuts.tolist()
     ends = cuts.tolist() + [n]
     return list(zip(col[starts].tolist(), starts, ends))
+
+
+def _dev_index(idx: np.ndarray, dev: torch.device) -> torch.Tensor:
+    """int64 index array on ``dev`` (pinned staging + one async H2D on GPUs)."""
+    if dev.type == "cuda":
+        from ..ops.desc import pack_to_device
+
+        return pack_to_device({"i": np.ascontiguousarray(idx, dtype=np.int64)}, dev)["i"]
+    return torch.from_numpy(np.ascontiguousarray(idx, dtype=np.int64))
 
 
 def _h2d_batch(arena: torch.Tensor, dst_offs: np.ndarray, sources: List[Tuple[torch.Tensor, int, int, bool]]) -> None:

@@ -133,17 +133,19 @@ __global__ __launch_bounds__(kCrcThreads) void crc32_group_residue_kernel(
       }
       c0 = c1; c1 = c2; c2 = c3; c3 = c4; c4 = c5; c5 = c6; c6 = c7;
     }
-    const int64_t groups = (c_len + 255) >> 8;
-    const int64_t g0 = tile * 32;
+    // lane `row` takes its group's residue from the 16 ballots; one masked store (see the
+    // fp4 kernel)
+    uint32_t res = 0;
 #pragma unroll
     for (int i = 0; i < 16; ++i) {
       const uint64_t m = __ballot(acc[i] & 0x80);  // 128 x GF(2) sum: parity is bit 7
       const int row = (i & 3) + 8 * (i >> 2);
-      if (lane == 0) {
-        if (g0 + row < groups) residues[c_roff + g0 + row] = static_cast<uint32_t>(m);
-        if (g0 + row + 4 < groups) residues[c_roff + g0 + row + 4] = static_cast<uint32_t>(m >> 32);
-      }
+      res = lane == row ? static_cast<uint32_t>(m) : res;
+      res = lane == row + 4 ? static_cast<uint32_t>(m >> 32) : res;
     }
+    const int64_t groups = (c_len + 255) >> 8;
+    const int64_t g = tile * 32 + lane;
+    if (lane < 32 && g < groups) residues[c_roff + g] = res;
   }
 }
 

@@ -305,6 +305,93 @@ PYBIND11_MODULE(_runtime, m) {
         if (base < 0) return py::none();
         return py::make_tuple(base, ids, offs);
       })
+      .def("p2p_layout", [](SegmentStore& s, Arr<int64_t> send_rows, Arr<int64_t> send_eids, Arr<int64_t> recv_rows,
+                            int64_t tick) {
+        // One round's P2P buffers (node.py:_p2p_phase), in one call.  Plan rows (sorted by
+        // (src, dst, key)): [key x4, len, src, dst, want_id, seeded].
+        //  sends, per destination run: (dst, row_a, row_b, mode, offset, total) -- mode 0:
+        //    the run's entries lie back to back in the arena (aligned), send arena[offset,
+        //    offset + total) as is; mode 1: gather into a staging buffer of `total` bytes,
+        //    copies listed in `gathers` (run, arena offset, buffer offset, length).
+        //  recvs, per source run: (src, row_a, row_b, base, total) -- one contiguous ring
+        //    reservation, entries pinned; rid / roff: entry id / offset per recv row.
+        const int64_t ns = send_eids.size();
+        const int64_t nr = recv_rows.ndim() == 2 ? recv_rows.shape(0) : 0;
+        if (ns && (send_rows.ndim() != 2 || send_rows.shape(0) != ns || send_rows.shape(1) < 9))
+          throw std::invalid_argument("send_rows must be int64[n, >=9] aligned with send_eids");
+        if (nr && recv_rows.shape(1) < 9) throw std::invalid_argument("recv_rows must be int64[n, >=9]");
+        const int64_t sc = ns ? send_rows.shape(1) : 9, rc = nr ? recv_rows.shape(1) : 9;
+        const int64_t* sr = send_rows.data();
+        const int64_t* se = send_eids.data();
+        const int64_t* rr = recv_rows.data();
+        std::vector<int64_t> srun, gath;
+        for (int64_t a = 0; a < ns;) {
+          const int64_t dst = sr[a * sc + 6];
+          int64_t b = a + 1;
+          while (b < ns && sr[b * sc + 6] == dst) ++b;
+          bool contiguous = true;
+          int64_t total = 0;
+          for (int64_t i = a; i < b && contiguous; ++i) {
+            const int64_t id = se[i];
+            if (id < 0 || id >= s.max_entries()) { contiguous = false; break; }
+            const Entry& e = s.entry(id);
+            if (e.length != sr[i * sc + 4]) contiguous = false;
+            if (i > a) {
+              const Entry& p = s.entry(se[i - 1]);
+              if (e.offset != p.offset + s.aligned(p.length)) contiguous = false;
+            }
+          }
+          if (contiguous) {
+            const Entry& f = s.entry(se[a]);
+            const Entry& l = s.entry(se[b - 1]);
+            total = l.offset + l.length - f.offset;
+            srun.insert(srun.end(), {dst, a, b, 0, f.offset, total});
+          } else {
+            const int64_t run = static_cast<int64_t>(srun.size() / 6);
+            int64_t pos = 0;
+            for (int64_t i = a; i < b; ++i) {
+              const int64_t len = sr[i * sc + 4];
+              const int64_t id = se[i];
+              if (id >= 0 && id < s.max_entries()) {
+                const Entry& e = s.entry(id);
+                gath.insert(gath.end(), {run, e.offset, pos, std::min(e.length, len)});
+              }
+              total = pos + len;
+              pos += s.aligned(len);
+            }
+            srun.insert(srun.end(), {dst, a, b, 1, -1, total});
+          }
+          a = b;
+        }
+        std::vector<int64_t> rrun;
+        Arr<int64_t> rid(nr), roff(nr);
+        for (int64_t a = 0; a < nr;) {
+          const int64_t src = rr[a * rc + 5];
+          int64_t b = a + 1;
+          while (b < nr && rr[b * rc + 5] == src) ++b;
+          const int64_t n = b - a;
+          std::vector<SegKey> keys(n);
+          std::vector<int64_t> lens(n);
+          for (int64_t i = 0; i < n; ++i) {
+            keys[i] = key_from(rr + (a + i) * rc);
+            lens[i] = rr[(a + i) * rc + 4];
+          }
+          const int64_t base = s.reserve_run(keys.data(), lens.data(), n, tick, rid.mutable_data() + a,
+                                             roff.mutable_data() + a);
+          if (base < 0) throw std::runtime_error("segment cache cannot make room for peer data");
+          for (int64_t i = a; i < b; ++i) s.pin(rid.data()[i]);
+          const int64_t total = roff.data()[b - 1] + lens[n - 1] - roff.data()[a];
+          rrun.insert(rrun.end(), {src, a, b, roff.data()[a], total});
+          a = b;
+        }
+        auto as2d = [](const std::vector<int64_t>& v, int64_t cols) {
+          const int64_t rows = static_cast<int64_t>(v.size()) / cols;
+          Arr<int64_t> out({rows, cols});
+          if (rows) std::memcpy(out.mutable_data(), v.data(), v.size() * sizeof(int64_t));
+          return out;
+        };
+        return py::make_tuple(as2d(srun, 6), as2d(gath, 4), as2d(rrun, 5), rid, roff);
+      })
       .def("fits", &SegmentStore::fits)
       .def("resident", [](const SegmentStore& s) {
         // -> (ids int64[n], keys int64[n,4]) of resident entries, oldest first

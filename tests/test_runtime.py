@@ -25,6 +25,38 @@ def test_store_reserve_commit_lookup_delta(rt):
     assert len(add) == 0 and rm[:, 3].tolist() == [1]
 
 
+def _plan_rows(ks, lens, src, dst, seeded=0):
+    rows = np.zeros((len(ks), 9), dtype=np.int64)
+    rows[:, :4] = ks
+    rows[:, 4] = lens
+    rows[:, 5] = src
+    rows[:, 6] = dst
+    rows[:, 7] = np.arange(len(ks)) + 100
+    rows[:, 8] = seeded
+    return rows
+
+
+def test_store_p2p_layout_sends_and_recv_reservations(rt):
+    """One native call lays out a round's P2P buffers (node.py:_p2p_phase): a destination
+    whose entries lie back to back sends its arena span as is; one that does not (or misses
+    an entry) gets a gather list; each source gets one pinned contiguous reservation."""
+    st = rt.SegmentStore(1 << 20, 256)
+    _, ids, offs = st.reserve_run(keys(1, 2, 3, 4), np.array([1000, 300, 256, 700]), 0)
+    st.commit(ids)
+    send = np.concatenate([_plan_rows(keys(1, 2), [1000, 300], 0, 1),     # back to back -> span
+                           _plan_rows(keys(1, 3, 9), [1000, 256, 50], 0, 2)])  # gap + missing -> gather
+    eids = np.array([ids[0], ids[1], ids[0], ids[2], -1], dtype=np.int64)
+    recv = np.concatenate([_plan_rows(keys(20, 21), [400, 500], 1, 0), _plan_rows(keys(30), [90], 3, 0)])
+    srun, gath, rrun, rid, roff = st.p2p_layout(send, eids, recv, 5)
+    assert srun.tolist() == [[1, 0, 2, 0, 0, 1024 + 300], [2, 2, 5, 1, -1, 1024 + 256 + 50]]
+    assert gath.tolist() == [[1, offs[0], 0, 1000], [1, offs[2], 1024, 256]]
+    assert rrun[:, 0].tolist() == [1, 3] and rrun[:, 1:3].tolist() == [[0, 2], [2, 3]]
+    assert roff[1] == roff[0] + 512 and rrun[0, 3] == roff[0] and rrun[0, 4] == 512 + 500
+    ent = st.entries(rid)
+    assert ent[:, 3].tolist() == [1, 1, 1]  # pinned until the round completes
+    assert st.lookup(keys(20, 21, 30), True).tolist() == rid.tolist()  # pending reservations
+
+
 def test_store_ring_fifo_eviction_and_pins(rt):
     st = rt.SegmentStore(4096, 256)
     _, a, _ = st.reserve_run(keys(1, 2), np.array([1024, 1024]), 0)
