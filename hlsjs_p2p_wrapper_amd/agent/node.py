@@ -347,19 +347,6 @@ class SwarmNode:
         return np.concatenate([hdr, w.reshape(-1), adds.reshape(-1).astype(np.int64),
                                rms.reshape(-1).astype(np.int64)])
 
-    @staticmethod
-    def _decode(msg: np.ndarray):
-        if msg.size < HDR or msg[0] != MAGIC:
-            raise RuntimeError("bad swarm control message")
-        nw, na, nr = int(msg[2]), int(msg[3]), int(msg[4])
-        p = HDR
-        w = msg[p:p + 6 * nw].reshape(nw, 6)
-        p += 6 * nw
-        a = msg[p:p + 5 * na].reshape(na, 5)
-        p += 5 * na
-        r = msg[p:p + 4 * nr].reshape(nr, 4)
-        return msg[:HDR], w, a, r
-
     def _grow_crc(self, n: int) -> None:
         if n > self.crc_dev.numel():
             new = torch.zeros(max(n, 2 * self.crc_dev.numel()), dtype=torch.int32, device=self.device)
@@ -414,33 +401,16 @@ class SwarmNode:
         wants = self._admit(wants)
         adds, rms = self.store.take_delta()
         parts = self.comm.allgather_control(self._encode(wants, adds, rms))
-        all_leaving = True
-        flags = np.zeros(self.world, dtype=np.int64)
-        want_rows = []
-        swarm_tot = np.zeros(3, dtype=np.int64)
-        for r, part in enumerate(parts):
-            hdr, w, a, rm = self._decode(part)
-            flags[r] = hdr[1]
-            all_leaving = all_leaving and bool(hdr[5])
-            swarm_tot += hdr[7:10]
-            if len(a) or len(rm):
-                self.directory.apply(r, np.ascontiguousarray(a), np.ascontiguousarray(rm))
-            if len(w):
-                rows = np.empty((len(w), 8), dtype=np.int64)
-                rows[:, :5] = w[:, :5]
-                rows[:, 5] = w[:, 5] & ((1 << 62) - 1)
-                rows[:, 6] = r
-                rows[:, 7] = (w[:, 5] >> 62) & 1
-                want_rows.append(rows)
+        # every rank's deltas into the directory + the round's want rows, in one native call
+        all_wants, flags, all_leaving, swarm_tot = rt.ingest_control(self.directory, parts, MAGIC, HDR)
         self.peer_online = (flags & rt.FLAG_ONLINE) != 0
         self.swarm_stats = {"cdn": int(swarm_tot[0]), "p2p": int(swarm_tot[1]), "upload": int(swarm_tot[2])}
         h = RoundHandle(self.round, all_leaving, t0=t0)
         t_ctrl = time.perf_counter()
         self.timer.add("control", t_ctrl - t0)
-        if not want_rows:
+        if not len(all_wants):
             return h
         h.empty = False
-        all_wants = np.ascontiguousarray(np.concatenate(want_rows))
         plan = rt.plan_round(self.directory, all_wants, flags, self.world)
         me = self.rank
         h.wants = wants

@@ -452,6 +452,50 @@ PYBIND11_MODULE(_runtime, m) {
         const DirEntry* e = d.find(SegKey{swarm, level, url_id, sn});
         return e ? e->holders : uint64_t(0);
       });
+  // One round's gathered control messages (agent/node.py:_encode layout: header[hdr_words] =
+  // magic, flags, #wants, #adds, #removes, leaving, round, cdn, p2p, upload, ...; then wants
+  // [key4, size, want_id | force_cdn << 62], adds [key4, len], removes [key4]) in one call:
+  // applies every rank's cache delta to the directory and returns (want rows int64[n, 8] for
+  // plan_round, per-rank flags, all-leaving, swarm byte totals [cdn, p2p, upload]).
+  m.def("ingest_control", [](Directory& d, const std::vector<Arr<int64_t>>& parts, int64_t magic,
+                             int64_t hdr_words) {
+    const int world = static_cast<int>(parts.size());
+    Arr<int64_t> flags(world);
+    int64_t tot[3] = {0, 0, 0};
+    bool all_leaving = true;
+    std::vector<int64_t> rows;
+    for (int r = 0; r < world; ++r) {
+      const Arr<int64_t>& m = parts[r];
+      const int64_t* p = m.data();
+      const int64_t size = m.size();
+      if (size < hdr_words || p[0] != magic) throw std::runtime_error("bad swarm control message");
+      const int64_t nw = p[2], na = p[3], nr = p[4];
+      if (nw < 0 || na < 0 || nr < 0 || hdr_words + 6 * nw + 5 * na + 4 * nr > size)
+        throw std::runtime_error("truncated swarm control message");
+      flags.mutable_data()[r] = p[1];
+      all_leaving = all_leaving && p[5] != 0;
+      tot[0] += p[7];
+      tot[1] += p[8];
+      tot[2] += p[9];
+      const int64_t* w = p + hdr_words;
+      const int64_t* a = w + 6 * nw;
+      const int64_t* rm = a + 5 * na;
+      for (int64_t i = 0; i < na; ++i) d.apply_add(r, key_from(a + 5 * i), a[5 * i + 4]);
+      for (int64_t i = 0; i < nr; ++i) d.apply_remove(r, key_from(rm + 4 * i));
+      for (int64_t i = 0; i < nw; ++i) {
+        const int64_t* x = w + 6 * i;
+        const int64_t id = x[5] & ((int64_t(1) << 62) - 1);
+        const int64_t force = (x[5] >> 62) & 1;
+        rows.insert(rows.end(), {x[0], x[1], x[2], x[3], x[4], id, r, force});
+      }
+    }
+    const int64_t n = static_cast<int64_t>(rows.size() / 8);
+    Arr<int64_t> out({n, int64_t(8)});
+    if (n) std::memcpy(out.mutable_data(), rows.data(), rows.size() * sizeof(int64_t));
+    Arr<int64_t> totals(3);
+    std::memcpy(totals.mutable_data(), tot, sizeof(tot));
+    return py::make_tuple(out, flags, all_leaving, totals);
+  });
   // wants: int64[n, 8] = (key4, size, want_id, rank, want_flags); flags int64[world]
   // -> int64[m, 10] = (key4, size, src, dst, want_id, seeded, reserved)
   m.def("plan_round", [](const Directory& d, Arr<int64_t> wants, Arr<int64_t> flags, int world) {
