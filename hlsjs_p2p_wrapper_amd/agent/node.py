@@ -29,6 +29,7 @@ zero-copy ``uint8`` view of the arena, or ``onError(HttpError)``
 from __future__ import annotations
 
 import contextlib
+import itertools
 import logging
 import os
 import threading
@@ -101,6 +102,10 @@ class _Want:
     attempts: int = 0
     round: int = -1  # round it is in flight in (-1: waiting)
     prefetch: bool = False  # issued by an agent's prefetch planner (may have no waiters)
+    row: tuple = ()  # control-message encoding (key x4, size, want_id | force_cdn << 62)
+
+    def encode(self) -> None:
+        self.row = (*self.key, self.size, self.want_id | ((1 if self.force_cdn else 0) << 62))
 
 
 class _Completion:
@@ -266,6 +271,7 @@ class SwarmNode:
                 self.loop.call_soon(self._fail, req, e)
                 return req
             w = _Want(req.key, url, req.headers, int(size), self._next_want_id)
+            w.encode()
             self._next_want_id += 1
             self._wants[req.key] = w
         w.waiters.append(req)
@@ -284,6 +290,7 @@ class SwarmNode:
         except http.HttpError:
             return False
         w = _Want(key, url, dict(headers or {}), int(size), self._next_want_id, prefetch=True)
+        w.encode()
         self._next_want_id += 1
         self._wants[key] = w
         self.stats["prefetched"] += 1
@@ -340,8 +347,9 @@ class SwarmNode:
         hdr[8] = self.stats["p2p"]
         hdr[9] = self.stats["upload"]
         if wants:
-            w = np.array([(*x.key, x.size, x.want_id | ((1 if x.force_cdn else 0) << 62)) for x in wants],
-                         dtype=np.int64)
+            # rows pre-encoded at want creation: one flat fromiter (~3x faster than np.array of tuples)
+            w = np.fromiter(itertools.chain.from_iterable([x.row for x in wants]), dtype=np.int64,
+                            count=6 * len(wants))
         else:
             w = np.zeros((0, 6), dtype=np.int64)
         return np.concatenate([hdr, w.reshape(-1), adds.reshape(-1).astype(np.int64),
@@ -527,6 +535,7 @@ class SwarmNode:
             w = h.by_id.get(e[0])
             if w is not None:
                 w.force_cdn = True  # corrupted peer copy: go to the CDN next round
+                w.encode()
                 w.attempts += 1
                 w.round = -1
         served = None
