@@ -40,7 +40,11 @@ _PROF_C3 = _PROF is not None and os.environ.get("HLSP2P_PROFILE_SECTION") == "c3
 
 CONFIGS = {
     # name: (renditions preset, encrypted, segment seconds, description)
-    "1080p6m": ("1080p", True, 4.0, "1080p 6 Mb/s HLS live (AES-128, 4 s TS segments, 8 peers)"),
+    # the swarm drains a live channel's DVR window as fast as it can (a throughput bench: at
+    # real-time live pace every peer would take 1 segment per 4 s); the window is served as a
+    # complete playlist, so no mid-run playlist reloads (live mode, sliding windows and
+    # live-window eviction are covered by tests/test_swarm.py)
+    "1080p6m": ("1080p", True, 4.0, "1080p 6 Mb/s HLS live-channel DVR catch-up (AES-128, 4 s TS segments, 8 peers)"),
     "1080p6m-clear": ("1080p", False, 4.0, "1080p 6 Mb/s HLS (clear, 4 s TS segments)"),
     "abr5": ("abr5", True, 4.0, "5-rendition ABR ladder (AES-128, 4 s TS)"),
     "4k25m": ("4k", True, 4.0, "4K 25 Mb/s HLS (AES-128, 4 s TS segments)"),

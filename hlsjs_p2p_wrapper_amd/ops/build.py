@@ -171,6 +171,7 @@ def build_device(force: bool = False, verbose: bool = False) -> Path:
 ACCEL_MODULES = [
     "utils/events.py", "utils/xhr.py", "net/event_loop.py", "net/http.py", "net/origin.py",
     "player/controllers.py", "player/abr.py", "player/media.py", "player/transmux.py", "player/level.py",
+    "player/playlist.py",
     "integration/p2p_loader.py", "agent/node.py", "agent/peer_agent.py",
     "models/segment_view.py", "models/track_view.py",
     "player/hls.py", "player/config.py", "utils/trace.py", "integration/player_interface.py",
