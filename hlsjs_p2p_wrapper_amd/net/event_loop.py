@@ -41,9 +41,6 @@ class TimerHandle:
     def cancel(self) -> None:
         self.cancelled = True
 
-    def __lt__(self, other: "TimerHandle") -> bool:  # heap order
-        return (self.when, self.seq) < (other.when, other.seq)
-
 
 class EventLoop:
     """Timer queue with a real or virtual millisecond clock."""
@@ -54,7 +51,9 @@ class EventLoop:
         self.clock = clock
         self._t0 = time.perf_counter()
         self._vnow = 0.0
-        self._heap: List[TimerHandle] = []
+        # heap of (when, seq, handle): tuple order compares in C (a handle __lt__ cost a
+        # Python call per comparison, ~12 per push on a few thousand pending timers)
+        self._heap: List[Tuple[float, int, TimerHandle]] = []
         self._ready: List[Tuple[Callable[..., Any], tuple]] = []
         self._seq = itertools.count()
         self._idle_hooks: List[Callable[[], bool]] = []
@@ -84,10 +83,10 @@ class EventLoop:
             # cancelled timers are dropped lazily when they reach the top; a long-running
             # peer cancels one fragment-timeout timer per fragment (tens of thousands per
             # second), so sweep them out whenever the heap doubles
-            heap[:] = [t for t in heap if not t.cancelled]
+            heap[:] = [e for e in heap if not e[2].cancelled]
             heapq.heapify(heap)
             self._compact_at = max(4096, 2 * len(heap))
-        heapq.heappush(heap, h)
+        heapq.heappush(heap, (h.when, h.seq, h))
         return h
 
     setTimeout = set_timeout
@@ -95,7 +94,7 @@ class EventLoop:
     def set_interval(self, fn: Callable[..., Any], interval_ms: float, *args: Any) -> TimerHandle:
         interval = max(0.0, float(interval_ms))
         h = TimerHandle(self.now() + interval, next(self._seq), fn, args, interval)
-        heapq.heappush(self._heap, h)
+        heapq.heappush(self._heap, (h.when, h.seq, h))
         return h
 
     setInterval = set_interval
@@ -126,11 +125,11 @@ class EventLoop:
     def _pop_due(self, now: float) -> Optional[TimerHandle]:
         heap = self._heap
         while heap:
-            h = heap[0]
+            when, _, h = heap[0]
             if h.cancelled:
                 heapq.heappop(heap)
                 continue
-            if h.when <= now:
+            if when <= now:
                 heapq.heappop(heap)
                 return h
             return None
@@ -138,15 +137,15 @@ class EventLoop:
 
     def _next_deadline(self) -> Optional[float]:
         heap = self._heap
-        while heap and heap[0].cancelled:
+        while heap and heap[0][2].cancelled:
             heapq.heappop(heap)
-        return heap[0].when if heap else None
+        return heap[0][0] if heap else None
 
     def _fire(self, h: TimerHandle) -> None:
         if h.interval is not None and not h.cancelled:
             h.when = max(h.when + h.interval, self.now()) if self.clock == "real" else h.when + h.interval
             h.seq = next(self._seq)
-            heapq.heappush(self._heap, h)
+            heapq.heappush(self._heap, (h.when, h.seq, h))
         h.fn(*h.args)
 
     def run_once(self, block: bool = True, max_wait_ms: float = 50.0) -> bool:
@@ -204,7 +203,7 @@ class EventLoop:
         self.run_until(lambda: self.now() >= end, timeout_ms=duration_ms + 1.0)
 
     def pending(self) -> int:
-        return len(self._ready) + sum(1 for h in self._heap if not h.cancelled)
+        return len(self._ready) + sum(1 for e in self._heap if not e[2].cancelled)
 
 
 _local = threading.local()
