@@ -117,7 +117,8 @@ def main() -> int:
     rends = {"1080p": PRESET_1080P_6M, "4k": PRESET_4K_25M, "abr5": PRESET_ABR5,
              "tiny": [Rendition(60_000, 320, 180, name="180p")],
              "micro": [Rendition(8_000, 160, 90, name="90p")],
-             "tiny-abr": [Rendition(20_000 * (i + 1), 160 * (i + 1), 90 * (i + 1), name=f"t{i}") for i in range(5)]}[preset]
+             "tiny-abr": [Rendition(20_000 * (i + 1), 160 * (i + 1), 90 * (i + 1), name=f"t{i}")
+                          for i in range(5)]}[preset]
     K = args.inflight
     total_steps = args.warmup + args.steps
     n_segments = (total_steps + 4) * K

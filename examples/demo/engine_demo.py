@@ -40,8 +40,8 @@ def main():
             shown[0] = t
             ahead = media._buffer_ahead(media.currentTime)
             bw = hls.abrController.bwEstimator.getEstimate() / 1e6
-            print(f"t={media.currentTime:5.1f}s level={hls.currentLevel} buffered={ahead:5.1f}s bw={bw:7.2f} Mb/s",
-                  flush=True)
+            print(f"t={media.currentTime:5.1f}s level={hls.currentLevel} buffered={ahead:5.1f}s "
+                  f"bw={bw:7.2f} Mb/s", flush=True)
         return media.currentTime >= args.seconds
 
     ok = loop.run_until(status, timeout_ms=600_000)

@@ -11,7 +11,8 @@ This is the engine behind the peer agent's ``getSegment`` (the closed-source
   the control plane, identical deterministic planning everywhere (native
   ``plan_round``), a CDN phase (pinned-host -> HBM ``hipMemcpyAsync`` batch on a side
   stream, the DMA engines) with ingest CRC on the MFMA CRC kernel, and a P2P phase: ONE
-  contiguous buffer per peer pair over RCCL (``batch_isend_irecv``), the sender's CRCs as
+  contiguous buffer per peer pair over RCCL (one native ncclGroupStart/Send/Recv group on the
+  node's stream, ``kernels/rccl_comm.cpp``), the sender's CRCs as
   a trailer, verified on device by the receiver.
 * **Asynchronous rounds**: :meth:`launch_round` (collective) only *enqueues* device work
   and records an event; :meth:`complete_round` (local) waits for it, commits/drops and
@@ -167,6 +168,8 @@ class _EventPool:
 
 
 class SwarmNode:
+    """One swarm peer (one GPU per process): HBM segment cache, collective exchange rounds,
+    the request queue the peer agents feed."""
     def __init__(self, comm: Optional[SwarmComm] = None, device: Any = "auto", cache_bytes: int = 1 << 30,
                  loop=None, cdn_dedup: bool = True, round_interval_ms: Optional[float] = None,
                  auto_tick: bool = True, max_wants_per_round: Optional[int] = None) -> None:
@@ -230,9 +233,11 @@ class SwarmNode:
 
     # ------------------------------------------------------------------ agents
     def attach(self, agent: Any) -> None:
+        """Register a peer agent (its requests, stats and metrics)."""
         self._agents.append(agent)
 
     def detach(self, agent: Any) -> None:
+        """Unregister an agent and fail its pending requests."""
         if agent in self._agents:
             self._agents.remove(agent)
         for w in list(self._wants.values()):
@@ -240,6 +245,7 @@ class SwarmNode:
 
     @property
     def flags(self) -> int:
+        """Control-message flag bits: online / download / upload state."""
         f = 0
         if self.online:
             f |= self.rt.FLAG_ONLINE
@@ -254,6 +260,8 @@ class SwarmNode:
     # ------------------------------------------------------------------ requests
     def request(self, key: Tuple[int, int, int, int], url: str, headers: Optional[Dict[str, str]],
                 callbacks: Any, agent: Any = None) -> Request:
+        """Queue a fragment request for key ``(swarm, level, urlId, sn)``; served from the cache,
+        a peer or the CDN in the next round."""
         k0, k1, k2, k3 = key
         req = Request(self, (int(k0) & _M32, int(k1) & _M32, int(k2) & _M32, int(k3) & _M32), url,
                       dict(headers) if headers else {}, callbacks, agent, False, False, self.loop.now())
@@ -803,6 +811,7 @@ class SwarmNode:
 
     # ------------------------------------------------------------------ lifecycle
     def enable_trace(self, maxlen: int = 100_000) -> TraceLog:
+        """Start (or return) the round / request trace log."""
         if self.trace is None:
             self.trace = TraceLog(maxlen)
         return self.trace
@@ -829,6 +838,7 @@ class SwarmNode:
             self.link_kbps.pop(int(peer), None)
 
     def set_online(self, online: bool) -> None:
+        """Announce online / offline to the swarm from the next round (churn)."""
         self.online = bool(online)
 
     def close(self, timeout_rounds: int = 100000) -> None:
@@ -849,6 +859,7 @@ class SwarmNode:
                 srv.close()
 
     def swarm_offload_ratio(self) -> float:
+        """P2P bytes / (P2P + CDN bytes) over the whole swarm."""
         c, p = self.swarm_stats["cdn"], self.swarm_stats["p2p"]
         return p / (p + c) if (p + c) else 0.0
 

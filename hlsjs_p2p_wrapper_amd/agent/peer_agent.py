@@ -26,6 +26,9 @@ log = logging.getLogger("hlsjs_p2p_wrapper_amd.agent")
 
 
 class PeerAgent:
+    """Per-session P2P agent: serves the loader's fragment requests from the swarm node
+    (HBM cache, peers, CDN), follows the playhead for prefetch and live-window eviction, and
+    keeps the session's ``stats``."""
     StreamTypes = JsObject(HLS="hls", DASH="dash", SMOOTH="smooth")
 
     def __init__(self, playerInterface: Any, contentUrl: str, mediaMap: Any, p2pConfig: Dict[str, Any],
@@ -68,6 +71,8 @@ class PeerAgent:
 
     # ------------------------------------------------------------------ contract
     def getSegment(self, reqInfo: Any, callbacks: Any, segmentView: Any):
+        """Queue a fragment request on the node; ``callbacks`` get ``onProgress`` then
+        ``onSuccess(data)`` / ``onError(err)``.  Returns the request handle (``abort()``)."""
         if self.disposed:
             raise RuntimeError("PeerAgent is disposed")
         url = _get(reqInfo, "url")
@@ -80,6 +85,7 @@ class PeerAgent:
     get_segment = getSegment
 
     def setMediaElement(self, media: Any) -> None:
+        """The media element whose playhead drives prefetch and eviction."""
         self.media = media
 
     def before_round(self) -> None:
@@ -146,6 +152,7 @@ class PeerAgent:
                                headers)
 
     def dispose(self) -> None:
+        """End the session: detach from the node and the player bridge (idempotent)."""
         if self.disposed:
             return
         self.disposed = True
@@ -155,6 +162,7 @@ class PeerAgent:
 
     @property
     def stats(self) -> JsObject:
+        """``{cdn, p2p, upload, peers}``: bytes by source for this session, peers online."""
         node = self.node
         peers = int(node.peer_online.sum()) - 1 if node.online else 0
         return JsObject(cdn=self._stats["cdn"], p2p=self._stats["p2p"],
@@ -162,6 +170,7 @@ class PeerAgent:
 
     @property
     def p2pDownloadOn(self) -> bool:
+        """Read / write: fetch fragments from peers."""
         return self.node.download_on
 
     @p2pDownloadOn.setter
@@ -170,6 +179,7 @@ class PeerAgent:
 
     @property
     def p2pUploadOn(self) -> bool:
+        """Read / write: serve cached fragments to peers."""
         return self.node.upload_on
 
     @p2pUploadOn.setter

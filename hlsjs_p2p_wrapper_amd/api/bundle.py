@@ -22,6 +22,9 @@ _UA = _ua.current_user_agent()  # parsed once at import, like the reference's mo
 
 
 class Hls(_Engine, metaclass=StaticMirrorMeta):
+    """Media-engine constructor with P2P built in: ``Hls(hlsjsConfig, p2pConfig)`` returns an engine
+    whose fragment loader is the P2P loader; engine statics are mirrored read-only."""
+
     def __new__(cls, hlsjsConfig: Optional[Dict[str, Any]] = None, p2pConfig: Optional[Dict[str, Any]] = None):
         return HlsjsP2PWrapper(_Engine).createPlayer(hlsjsConfig, p2pConfig)
 
@@ -33,11 +36,13 @@ inheritStaticPropertiesReadOnly(Hls, _Engine)
 
 
 def _is_supported() -> bool:
+    """Engine supported, and the user agent is neither Safari nor a mobile / tablet / console."""
     res = _UA if _ua._override is None else _ua.current_user_agent()
     return _Engine.isSupported() and not _ua.is_safari(res) and not _ua.is_mobile(res)
 
 
 def _get_browser_name() -> Optional[str]:
+    """Browser name parsed from the user agent (``None`` when unknown)."""
     res = _UA if _ua._override is None else _ua.current_user_agent()
     return res.browser.get("name")
 

@@ -23,6 +23,10 @@ class _Version:
 
 
 class HlsjsP2PWrapper:
+    """Wrapper around a media-engine constructor: ``createPlayer(hlsjsConfig, p2pConfig)`` builds an
+    engine with a P2P session attached once its manifest starts loading; ``P2PLoader`` is the
+    fragment-loader class for engines built by hand."""
+
     version = _Version()
 
     def __init__(self, hlsjsConstructor: Any = None, peerAgentConstructor: Any = PeerAgent) -> None:
@@ -34,6 +38,7 @@ class HlsjsP2PWrapper:
 
     @property
     def stats(self):
+        """The session's ``{cdn, p2p, upload, peers}`` byte / peer counters (raises before a session)."""
         agent = self._wrapper.peerAgentModule
         if agent is None:
             raise TypeError("Cannot read property 'stats' of undefined (no P2P session)")
@@ -41,6 +46,7 @@ class HlsjsP2PWrapper:
 
     @property
     def p2pDownloadOn(self) -> bool:
+        """Read / write: fetch fragments from peers (``False`` = CDN only)."""
         return self._require().p2pDownloadOn
 
     @p2pDownloadOn.setter
@@ -49,6 +55,7 @@ class HlsjsP2PWrapper:
 
     @property
     def p2pUploadOn(self) -> bool:
+        """Read / write: serve cached fragments to peers."""
         return self._require().p2pUploadOn
 
     @p2pUploadOn.setter
@@ -62,5 +69,5 @@ class HlsjsP2PWrapper:
         return agent
 
     # python conveniences
-    create_player = property(lambda self: self.createPlayer)
-    create_sr_module = property(lambda self: self.createSRModule)
+    create_player = property(lambda self: self.createPlayer, doc="snake_case alias of ``createPlayer``")
+    create_sr_module = property(lambda self: self.createSRModule, doc="snake_case alias of ``createSRModule``")

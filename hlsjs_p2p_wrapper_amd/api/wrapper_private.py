@@ -37,6 +37,9 @@ def _defaults(target: Dict[str, Any], source: Dict[str, Any]) -> Dict[str, Any]:
 
 
 class HlsjsP2PWrapperPrivate:
+    """Session orchestrator: one media engine and one peer agent at a time, both constructors
+    injected."""
+
     def __init__(self, hlsjsConstructor: Any = None, peerAgentModuleConstructor: Any = None) -> None:
         if not peerAgentModuleConstructor:
             raise Exception("Constructor needs DI of PeerAgent")
@@ -47,6 +50,7 @@ class HlsjsP2PWrapperPrivate:
 
     # ------------------------------------------------------------------ engines
     def createMediaEngine(self, hlsjsConfig: Optional[Dict[str, Any]] = None, p2pConfig: Any = None):
+        """New engine (P2P loader config merged in); the session starts on its ``MANIFEST_LOADING``."""
         Hlsjs = self.Hlsjs
         mediaEngine = self.newMediaEngine(hlsjsConfig if hlsjsConfig is not None else {})
 
@@ -58,6 +62,7 @@ class HlsjsP2PWrapperPrivate:
         return mediaEngine
 
     def createPlayer(self, hlsjsConfig: Optional[Dict[str, Any]] = None, p2pConfig: Any = None):
+        """Public name of ``createMediaEngine``."""
         return self.createMediaEngine(hlsjsConfig, p2pConfig)
 
     def createSRModule(self, p2pConfig: Dict[str, Any], mediaEngine: Any, hlsEventsEnum: Any,
@@ -68,9 +73,11 @@ class HlsjsP2PWrapperPrivate:
 
     @property
     def P2PLoader(self) -> type:
+        """A fresh fragment-loader class bound to this wrapper (new class on every access)."""
         return p2p_loader_generator(self)
 
     def getConfig(self) -> Dict[str, Any]:
+        """Engine defaults the wrapper needs: ``fLoader`` (P2P), no byte cap, 30 s buffer / live sync."""
         # fLoader, never `loader`: playlists and keys must not go through the P2P loader
         return {
             "fLoader": p2p_loader_generator(self),
@@ -81,9 +88,11 @@ class HlsjsP2PWrapperPrivate:
 
     # ------------------------------------------------------------------ session
     def onDispose(self) -> None:
+        """Engine destroyed: end the session."""
         self.stopSession()
 
     def stopSession(self) -> None:
+        """Dispose the peer agent, if any (idempotent)."""
         if not self.peerAgentModule:
             return
         self.peerAgentModule.dispose()
@@ -91,6 +100,7 @@ class HlsjsP2PWrapperPrivate:
 
     def startSession(self, hlsjs: Any, hlsjsConfig: Optional[Dict[str, Any]], p2pConfig: Any,
                      contentUrl: Optional[str]):
+        """Attach a peer agent to ``hlsjs`` (or to a new engine); ``p2pConfig`` must be a dict."""
         Hlsjs = self.Hlsjs
         if not truthy(p2pConfig) or not isinstance(p2pConfig, dict):  # JS: {} is a valid object
             raise Exception("p2pConfig must be a valid config object")
@@ -99,6 +109,8 @@ class HlsjsP2PWrapperPrivate:
         return mediaEngine
 
     def newMediaEngine(self, hlsjsConfig: Optional[Dict[str, Any]] = None):
+        """Engine built with ``getConfig()`` defaults filled into ``hlsjsConfig`` (a user ``fLoader`` is
+        an error; ``liveSyncDurationCount`` suppresses the ``liveSyncDuration`` default)."""
         if hlsjsConfig is None:
             hlsjsConfig = {}
         Hlsjs = self.Hlsjs
@@ -113,6 +125,7 @@ class HlsjsP2PWrapperPrivate:
         return Hlsjs(_defaults(hlsjsConfig, newDefaultConf))
 
     def hasSession(self) -> bool:
+        """A peer agent is attached."""
         return bool(self.peerAgentModule)
 
     def _setMediaElement(self, hlsjs: Any, hlsEventsEnum: Any) -> None:
@@ -127,6 +140,8 @@ class HlsjsP2PWrapperPrivate:
 
     def createPeerAgent(self, p2pConfig: Dict[str, Any], hlsjs: Any, hlsEventsEnum: Any,
                         url: Optional[str] = None) -> None:
+        """Build player bridge + media map + peer agent for ``hlsjs`` (one session at a time; the
+        content URL is ``url`` or the engine's ``url``)."""
         self.hls = hlsjs
         StreamrootPeerAgentModule = self.StreamrootPeerAgentModule
         streamType = StreamrootPeerAgentModule.StreamTypes.HLS
@@ -147,6 +162,7 @@ class HlsjsP2PWrapperPrivate:
 
     @staticmethod
     def onMediaEngineError(event: str, data: Any) -> None:
+        """Log engine errors (fatal -> error, otherwise warning)."""
         fatal = data.get("fatal") if isinstance(data, dict) else getattr(data, "fatal", False)
         typ = data.get("type") if isinstance(data, dict) else getattr(data, "type", None)
         details = data.get("details") if isinstance(data, dict) else getattr(data, "details", None)

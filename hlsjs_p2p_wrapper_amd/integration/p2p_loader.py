@@ -52,7 +52,8 @@ def p2p_loader_generator(hlsjsWrapper: Any) -> type:
             self.loop = get_event_loop()
             self.xhrSetup = None
             if config:
-                self.xhrSetup = config.get("xhrSetup") if isinstance(config, dict) else getattr(config, "xhrSetup", None)
+                self.xhrSetup = (config.get("xhrSetup") if isinstance(config, dict)
+                                 else getattr(config, "xhrSetup", None))
             self.stats = JsObject()
             self.byteRange = None
             self.requestTimeout = None

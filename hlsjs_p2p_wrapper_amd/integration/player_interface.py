@@ -22,6 +22,9 @@ from ..utils.events import EventEmitter
 
 
 class PlayerInterface(EventEmitter):
+    """Player bridge given to the peer agent: live / buffer queries on the engine, and
+    ``onTrackChange`` events re-emitted from the engine's level switches."""
+
     __slots__ = ("hls", "onDispose")
 
     def __init__(self, hls: Any, Events: Any, onDispose: Callable[[], Any], *_legacy: Any) -> None:
@@ -43,6 +46,7 @@ class PlayerInterface(EventEmitter):
         self.hls.on(destroying, on_destroying)
 
     def isLive(self) -> bool:
+        """``details.live`` of the first parsed level; raises before any playlist is parsed."""
         levels = self.hls.levels
         if levels is None:  # (an empty JS array is truthy: only "undefined" means unparsed)
             raise Exception("Called isLive before the master playlist was parsed")
@@ -53,6 +57,7 @@ class PlayerInterface(EventEmitter):
         raise Exception("Called isLive before any levelplaylist was parsed")
 
     def getBufferLevelMax(self) -> float:
+        """Target buffer in seconds: ``liveSyncDuration`` if set, else ``maxBufferLength``."""
         cfg = self.hls.config
         if _attr(cfg, "liveSyncDuration"):
             conf_param = "liveSyncDuration"
@@ -66,15 +71,18 @@ class PlayerInterface(EventEmitter):
         return max_level
 
     def setBufferMarginLive(self, bufferLevel: float) -> None:
+        """Set the engine's buffer target to ``bufferLevel`` seconds (and lift the byte cap)."""
         cfg = self.hls.config
         _set(cfg, "maxBufferSize", 0)
         _set(cfg, "maxBufferLength", bufferLevel)
 
     def addEventListener(self, eventName: str, listener: Callable) -> None:
+        """Subscribe to ``'onTrackChange'``; other names are ignored."""
         if eventName == "onTrackChange":
             self.on(eventName, listener)
 
     def removeEventListener(self, eventName: str, listener: Callable) -> None:
+        """Unsubscribe from ``'onTrackChange'``; other names are ignored."""
         if eventName == "onTrackChange":
             self.remove_listener(eventName, listener)
 

@@ -42,11 +42,13 @@ class _StartIndex:
 
 
 class MediaMap:
+    """Segment/track queries over the engine's parsed playlists, for the peer agent."""
     def __init__(self, hls: Any) -> None:
         self.hls = hls
         self._idx: dict = {}
 
     def getSegmentTime(self, segmentView: SegmentView) -> Any:
+        """Start time of the segment (raises when the view carries none)."""
         if segmentView.time is None:
             raise Exception("getSegmentTime: segmentView.time is undefined")
         return segmentView.time
@@ -60,6 +62,8 @@ class MediaMap:
         return levels[index]
 
     def getSegmentList(self, trackView: TrackView, beginTime: float, duration: float) -> List[SegmentView]:
+        """SegmentViews of ``trackView`` whose start lies in ``[beginTime, beginTime + duration]``
+        (playlist order; ``[]`` while the level is unparsed, raises for a missing level)."""
         level = self._level(trackView.level)
         if not level:
             raise Exception("getSegmentList: level doesn't exist")
@@ -145,6 +149,7 @@ class MediaMap:
         return None
 
     def getTrackList(self) -> List[TrackView]:
+        """Every ``(level, urlId)`` track, redundant URLs included."""
         levels = self.hls.levels
         if not levels:
             return []
@@ -155,6 +160,7 @@ class MediaMap:
         return tracks
 
     def getSegmentDuration(self, segmentView: SegmentView) -> Any:
+        """Duration of the track's segments (the first fragment's)."""
         level = self._level(segmentView.trackView.level)
         for fragment in level.details.fragments:
             return fragment.duration

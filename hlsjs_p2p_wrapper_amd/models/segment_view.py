@@ -27,6 +27,8 @@ def _field(obj: Any, name: str) -> Any:
 
 
 class SegmentView:
+    """One media segment ``(sn, trackView)`` plus its start ``time``; 12-byte binary key."""
+
     __slots__ = ("sn", "trackView", "time")
 
     def __init__(self, obj: Any = None, *, sn: Any = None, trackView: Any = None,
@@ -49,14 +51,17 @@ class SegmentView:
         return SegmentView(trackView=TrackView(level=level, urlId=url_id), sn=sn)
 
     def isEqual(self, segmentView: Optional["SegmentView"]) -> bool:
+        """Same sn and track (``time`` ignored; ``False`` for a falsy argument)."""
         if not segmentView:
             return False
         return self.sn == segmentView.sn and self.trackView.isEqual(segmentView.trackView)
 
     def isInTrack(self, trackView: Optional[TrackView]) -> bool:
+        """The segment belongs to ``trackView``."""
         return self.trackView.isEqual(trackView)
 
     def viewToString(self) -> str:
+        """``"L{level}U{urlId}S{sn}"``."""
         return f"{self.trackView.viewToString()}S{_js_str(self.sn)}"
 
     def toArrayBuffer(self) -> bytes:
@@ -64,6 +69,7 @@ class SegmentView:
         return _KEY.pack(_u32(self.trackView.level), _u32(self.trackView.urlId), _u32(self.sn))
 
     def getId(self) -> Any:
+        """The sequence number."""
         return self.sn
 
     # --- python conveniences -------------------------------------------------
@@ -79,6 +85,7 @@ class SegmentView:
         return (_u32(self.trackView.level), _u32(self.trackView.urlId), _u32(self.sn))
 
     def to_dict(self) -> dict:
+        """``{"sn", "trackView"[, "time"]}`` (JSON form; ``time`` survives the round trip)."""
         d = {"sn": self.sn, "trackView": self.trackView.to_dict()}
         if self.time is not None:
             d["time"] = self.time

@@ -25,6 +25,8 @@ def _field(obj: Any, name: str) -> Any:
 
 
 class TrackView:
+    """One rendition track ``(level, urlId)``; built from any object or dict carrying both."""
+
     __slots__ = ("level", "urlId")
 
     def __init__(self, obj: Any = None, *, level: Any = None, urlId: Any = None) -> None:
@@ -36,15 +38,18 @@ class TrackView:
 
     # --- reference API -------------------------------------------------------
     def viewToString(self) -> str:
+        """``"L{level}U{urlId}"``."""
         return f"L{_js_str(self.level)}U{_js_str(self.urlId)}"
 
     def isEqual(self, trackView: Optional["TrackView"]) -> bool:
+        """Same level and urlId (``False`` for a falsy argument)."""
         if not trackView:
             return False
         return trackView.level == self.level and trackView.urlId == self.urlId
 
     @property
     def type(self) -> str:
+        """Always ``"video"``."""
         return "video"
 
     # --- python conveniences -------------------------------------------------
@@ -53,12 +58,15 @@ class TrackView:
 
     @property
     def url_id(self) -> Any:
+        """snake_case alias of ``urlId``."""
         return self.urlId
 
     def key(self) -> Tuple[Any, Any]:
+        """``(level, urlId)``."""
         return (self.level, self.urlId)
 
     def to_dict(self) -> dict:
+        """``{"level", "urlId"}`` (JSON form)."""
         return {"level": self.level, "urlId": self.urlId}
 
     toJSON = to_dict

@@ -64,7 +64,8 @@ def crc32_batch(buf: torch.Tensor, offs: Sequence[int], lens: Sequence[int],
     n = np.asarray(lens, dtype=np.int64)
     if B == 0:
         z = torch.empty(0, dtype=torch.int32, device=buf.device)
-        return z, (torch.empty(0, dtype=torch.uint8, device=buf.device) if (expect is not None or expect_dev is not None) else None)
+        want_ok = expect is not None or expect_dev is not None
+        return z, (torch.empty(0, dtype=torch.uint8, device=buf.device) if want_ok else None)
     sidx = None if scatter_to is None else np.asarray(scatter_idx, dtype=np.int64).reshape(-1)
     if buf.device.type == "cpu":
         if np.any(o < 0) or np.any(n < 0) or np.any(o + n > buf.numel()):
@@ -121,7 +122,10 @@ def crc32(data) -> int:
     """Host CRC-32 of bytes / numpy / CPU tensor (== zlib.crc32)."""
     if isinstance(data, torch.Tensor):
         data = data.detach().cpu().numpy()
-    arr = np.frombuffer(data, dtype=np.uint8) if isinstance(data, (bytes, bytearray, memoryview)) else np.asarray(data, dtype=np.uint8)
+    if isinstance(data, (bytes, bytearray, memoryview)):
+        arr = np.frombuffer(data, dtype=np.uint8)
+    else:
+        arr = np.asarray(data, dtype=np.uint8)
     return int(_rt().crc32(np.ascontiguousarray(arr)))
 
 

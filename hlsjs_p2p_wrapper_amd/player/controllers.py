@@ -51,7 +51,8 @@ class PlaylistLoader:
         loader = _loader_class(cfg, "pLoader")(cfg)
         self.loaders[kind] = loader
         if kind == "manifest":
-            timeout, retry, delay = cfg.manifestLoadingTimeOut, cfg.manifestLoadingMaxRetry, cfg.manifestLoadingRetryDelay
+            timeout = cfg.manifestLoadingTimeOut
+            retry, delay = cfg.manifestLoadingMaxRetry, cfg.manifestLoadingRetryDelay
         else:
             timeout, retry, delay = cfg.levelLoadingTimeOut, cfg.levelLoadingMaxRetry, cfg.levelLoadingRetryDelay
         loader.load(url, "text", lambda e, s: self._success(kind, url, ctx, e, s),
@@ -598,7 +599,8 @@ class StreamController:
             return
         if r.get("error") is not None or r.get("status", 0) & 0b111111:
             self.inflight.pop(key, None)
-            details = ErrorDetails.FRAG_DECRYPT_ERROR if r.get("plain_bytes", 0) < 0 else ErrorDetails.FRAG_PARSING_ERROR
+            details = (ErrorDetails.FRAG_DECRYPT_ERROR if r.get("plain_bytes", 0) < 0
+                       else ErrorDetails.FRAG_PARSING_ERROR)
             hls.trigger(Events.ERROR, {"type": ErrorTypes.MEDIA_ERROR, "details": details, "fatal": False,
                                        "frag": frag, "reason": str(r.get("error") or r.get("status"))})
             self._kick()

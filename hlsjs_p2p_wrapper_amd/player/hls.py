@@ -33,6 +33,8 @@ class _DefaultConfigDescriptor:
 
 
 class Hls:
+    """hls.js-compatible media engine: playlist / key / fragment loaders, level and ABR
+    controllers, transmux to the media element; events through ``on`` / ``trigger``."""
     Events = Events
     ErrorTypes = ErrorTypes
     ErrorDetails = ErrorDetails
@@ -73,15 +75,19 @@ class Hls:
 
     # ------------------------------------------------------------------ events
     def on(self, event: str, listener: Callable[[str, Any], Any]) -> None:
+        """Subscribe ``listener(event, data)``."""
         self._observer.on(event, listener)
 
     def once(self, event: str, listener: Callable[[str, Any], Any]) -> None:
+        """Subscribe for one delivery."""
         self._observer.once(event, listener)
 
     def off(self, event: str, listener: Callable[[str, Any], Any]) -> None:
+        """Unsubscribe."""
         self._observer.off(event, listener)
 
     def trigger(self, event: str, data: Any = None) -> None:
+        """Emit ``event`` with ``data`` (``{}`` when omitted)."""
         if data is None:
             data = {}
         self._observer.trigger(event, data)
@@ -98,15 +104,18 @@ class Hls:
 
     # ------------------------------------------------------------------ lifecycle
     def loadSource(self, url: str) -> None:
+        """Set ``url`` and start loading the master playlist (``MANIFEST_LOADING``)."""
         self.url = url
         self.trigger(Events.MANIFEST_LOADING, {"url": url})
 
     def attachMedia(self, media: Any) -> None:
+        """Bind a media element (``MEDIA_ATTACHING`` / ``MEDIA_ATTACHED``)."""
         self.media = media
         self.trigger(Events.MEDIA_ATTACHING, {"media": media})
         self.trigger(Events.MEDIA_ATTACHED, {"media": media})
 
     def detachMedia(self) -> None:
+        """Unbind the media element (``MEDIA_DETACHING`` / ``MEDIA_DETACHED``)."""
         if self.media is None:
             return
         self.trigger(Events.MEDIA_DETACHING, {})
@@ -117,12 +126,15 @@ class Hls:
         self.trigger(Events.MEDIA_DETACHED, {})
 
     def startLoad(self, startPosition: float = -1) -> None:
+        """Start fragment loading at ``startPosition`` (-1: default position)."""
         self.streamController.startLoad(startPosition)
 
     def stopLoad(self) -> None:
+        """Stop fragment loading."""
         self.streamController.stopLoad()
 
     def destroy(self) -> None:
+        """``DESTROYING``, then stop every loader and drop listeners (idempotent)."""
         if self._destroyed:
             return
         self.trigger(Events.DESTROYING, {})
@@ -140,10 +152,12 @@ class Hls:
     # ------------------------------------------------------------------ levels
     @property
     def levels(self):
+        """Parsed variant levels (``None`` before the master playlist)."""
         return self.levelController.levels
 
     @property
     def currentLevel(self) -> int:
+        """Level of the last loaded fragment; setting it switches immediately."""
         frag = self.streamController.fragPrevious
         return frag.level if frag is not None else self.levelController.level
 
@@ -153,6 +167,7 @@ class Hls:
 
     @property
     def loadLevel(self) -> int:
+        """Level being loaded; setting it forces a manual level."""
         return self.levelController.level
 
     @loadLevel.setter
@@ -161,6 +176,7 @@ class Hls:
 
     @property
     def nextLevel(self) -> int:
+        """Level of the next fragment; setting it switches at the next fragment."""
         return self.nextLoadLevel
 
     @nextLevel.setter
@@ -169,14 +185,17 @@ class Hls:
 
     @property
     def manualLevel(self) -> int:
+        """Forced level, -1 in auto mode."""
         return self.levelController.manualLevel
 
     @property
     def autoLevelEnabled(self) -> bool:
+        """ABR chooses the level."""
         return self.levelController.manualLevel == -1
 
     @property
     def nextLoadLevel(self) -> int:
+        """Level the next fragment load will use (manual, else the ABR choice)."""
         if self.levelController.manualLevel != -1:
             return self.levelController.manualLevel
         return self.abrController.nextAutoLevel
@@ -187,10 +206,12 @@ class Hls:
 
     @property
     def startLevel(self) -> int:
+        """First level loaded."""
         return self.levelController.firstLevel
 
     @property
     def bandwidthEstimate(self) -> float:
+        """ABR bandwidth estimate, bits/s."""
         return self.abrController.bwEstimator.getEstimate()
 
     # ------------------------------------------------------------------ transmux placement

@@ -48,6 +48,7 @@ class TimeRanges:
 
 
 class MediaElement(EventEmitter):
+    """``<video>`` + SourceBuffer model: playhead clock, buffered ranges, media events."""
     TICK_MS = 250.0
     GAP_TOLERANCE = 0.1  # seconds: adjacent appends closer than this merge
 
@@ -76,13 +77,16 @@ class MediaElement(EventEmitter):
 
     # ---------------------------------------------------------------- DOM-ish API
     def addEventListener(self, name: str, fn: Callable) -> None:
+        """Subscribe to a media event (``timeupdate``, ``seeked``, ...)."""
         self.on(name, fn)
 
     def removeEventListener(self, name: str, fn: Callable) -> None:
+        """Unsubscribe."""
         self.remove_listener(name, fn)
 
     @property
     def currentTime(self) -> float:
+        """Playhead position in seconds (settable: seeks)."""
         return self._time
 
     @currentTime.setter
@@ -95,13 +99,16 @@ class MediaElement(EventEmitter):
 
     @property
     def buffered(self) -> TimeRanges:
+        """Buffered ranges as TimeRanges."""
         return TimeRanges(self._ranges)
 
     @property
     def readyState(self) -> int:
+        """4 with > 0.5 s buffered ahead, 1 with any buffer, else 0."""
         return 4 if self._buffer_ahead(self._time) > 0.5 else (1 if self._ranges else 0)
 
     def play(self) -> None:
+        """Start the playback clock (``play``)."""
         if not self.paused:
             return
         self.paused = False
@@ -110,11 +117,13 @@ class MediaElement(EventEmitter):
         self.emit("play")
 
     def pause(self) -> None:
+        """Stop the playback clock."""
         self.paused = True
         self.emit("pause")
 
     # ---------------------------------------------------------------- SourceBuffer side
     def append(self, start: float, end: float, nbytes: int = 0, data: Any = None) -> None:
+        """SourceBuffer append of media ``[start, end)`` (``nbytes`` counted, ranges merged)."""
         if end <= start:
             return
         self.bytes_appended += int(nbytes)
@@ -136,6 +145,7 @@ class MediaElement(EventEmitter):
         self._check_seeked()
 
     def remove(self, start: float, end: float) -> None:
+        """Drop buffered media in ``[start, end)``."""
         out = []
         for s, e in self._ranges:
             if e <= start or s >= end:
@@ -150,6 +160,7 @@ class MediaElement(EventEmitter):
             self.retained = [r for r in self.retained if r[1] <= start or r[0] >= end]
 
     def flush(self) -> None:
+        """Drop all buffered media."""
         self._ranges = []
         self.retained = []
 
@@ -217,6 +228,7 @@ class MediaElement(EventEmitter):
                 self._drain()
 
     def stop(self) -> None:
+        """Cancel the playback timer."""
         if self._timer is not None:
             self._timer.cancel()
             self._timer = None

@@ -179,6 +179,7 @@ class MetricsServer:
         self._thread.start()
 
     def text(self) -> str:
+        """Current exposition text (node families, then one set per agent)."""
         fams = node_metrics(self.node)
         agents = self.agents if self.agents is not None else getattr(self.node, "_agents", [])
         for i, a in enumerate(list(agents)):
@@ -186,6 +187,7 @@ class MetricsServer:
         return render(fams)
 
     def close(self) -> None:
+        """Stop serving and release the port."""
         self._srv.shutdown()
         self._srv.server_close()
         self._thread.join(timeout=5)

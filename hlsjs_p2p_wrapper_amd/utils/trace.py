@@ -96,7 +96,8 @@ class TraceLog:
             return 0.0
         return xs[min(len(xs) - 1, int(q * len(xs)))]
 
-    def latency_summary(self, quantiles: Sequence[float] = (0.5, 0.9, 0.99)) -> Dict[str, Tuple[int, float, List[Tuple[float, float]]]]:
+    def latency_summary(self, quantiles: Sequence[float] = (0.5, 0.9, 0.99)
+                        ) -> Dict[str, Tuple[int, float, List[Tuple[float, float]]]]:
         """Per-source latency summary of the whole retained log in ONE pass.
 
         Safe to call from another thread while the round loop appends: ``list(deque)`` is a

@@ -12,7 +12,8 @@ from hlsjs_p2p_wrapper_amd.utils.metrics import MetricsServer, agent_metrics, no
 from test_swarm import fresh, run_swarm  # noqa: F401 - fixture re-export
 
 _LV = r'"(?:[^"\\]|\\.)*"'  # a label value with escapes
-_SAMPLE = re.compile(r'^([a-zA-Z_:][a-zA-Z0-9_:]*)(\{([a-z_]+=' + _LV + r'(,[a-z_]+=' + _LV + r')*)\})? (-?[0-9.e+-]+|NaN)$')
+_SAMPLE = re.compile(r'^([a-zA-Z_:][a-zA-Z0-9_:]*)(\{([a-z_]+=' + _LV + r'(,[a-z_]+=' + _LV + r')*)\})?'
+                     r' (-?[0-9.e+-]+|NaN)$')
 
 
 def parse(text):

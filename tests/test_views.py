@@ -50,8 +50,9 @@ def test_segmentview_to_array_buffer_type_and_roundtrip():
 
 def test_segmentview_binary_key_matches_packed_tensor_rows():
     keys = segment.pack_keys([1, 5], [1, 0], [25, 1560], swarm=9)
-    assert segment.wire_keys(keys) == (SegmentView({"sn": 25, "trackView": {"level": 1, "urlId": 1}}).toArrayBuffer()
-                                       + SegmentView({"sn": 1560, "trackView": {"level": 5, "urlId": 0}}).toArrayBuffer())
+    a = SegmentView({"sn": 25, "trackView": {"level": 1, "urlId": 1}})
+    b = SegmentView({"sn": 1560, "trackView": {"level": 5, "urlId": 0}})
+    assert segment.wire_keys(keys) == a.toArrayBuffer() + b.toArrayBuffer()
 
 
 def test_segmentview_is_in_track():
