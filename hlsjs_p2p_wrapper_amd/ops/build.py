@@ -219,7 +219,10 @@ def build_accel(force: bool = False, verbose: bool = False) -> List[Path]:
     # one cythonize call (the Cython compiler is not thread-safe), C files next to the
     # sources, moved into build/ right after
     cythonize([str(src) for _, src, _, _ in todo], language_level=3, quiet=True, force=True,
-              compiler_directives={"binding": True})
+              compiler_directives={"binding": True,
+                                   # HLSP2P_CYTHON_PROFILE=1: cProfile sees the compiled functions
+                                   # (diagnostic builds only: the hooks cost ~2x per call)
+                                   "profile": os.environ.get("HLSP2P_CYTHON_PROFILE") == "1"})
     c_files = {}
     for rel, src, _, _ in todo:
         c_file = objdir / (rel[:-3].replace("/", "__") + ".c")
