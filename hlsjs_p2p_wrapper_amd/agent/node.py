@@ -91,19 +91,30 @@ class Request:
         return f"Request(key={self.key}, url={self.url!r}, aborted={self.aborted}, done={self.done})"
 
 
-@dataclass(eq=False)
 class _Want:
-    key: Tuple[int, int, int, int]
-    url: str
-    headers: Dict[str, str]
-    size: int
-    want_id: int
-    waiters: List[Request] = field(default_factory=list)
-    force_cdn: bool = False
-    attempts: int = 0
-    round: int = -1  # round it is in flight in (-1: waiting)
-    prefetch: bool = False  # issued by an agent's prefetch planner (may have no waiters)
-    row: tuple = ()  # control-message encoding (key x4, size, want_id | force_cdn << 62)
+    """One wanted segment of this rank (all requests for one key share it).  Slotted plain
+    class: one per request, and a dataclass ``__init__`` is interpreted code even here."""
+
+    __slots__ = ("key", "url", "headers", "size", "want_id", "waiters", "force_cdn", "attempts", "round",
+                 "prefetch", "row")
+
+    def __init__(self, key: Tuple[int, int, int, int], url: str, headers: Dict[str, str], size: int,
+                 want_id: int, waiters: Optional[List[Request]] = None, force_cdn: bool = False,
+                 attempts: int = 0, round: int = -1, prefetch: bool = False) -> None:
+        self.key = key
+        self.url = url
+        self.headers = headers
+        self.size = size
+        self.want_id = want_id
+        self.waiters = [] if waiters is None else waiters
+        self.force_cdn = force_cdn
+        self.attempts = attempts
+        self.round = round  # round it is in flight in (-1: waiting)
+        self.prefetch = prefetch  # issued by an agent's prefetch planner (may have no waiters)
+        self.row = ()  # control-message encoding (key x4, size, want_id | force_cdn << 62)
+
+    def __repr__(self) -> str:
+        return f"_Want(key={self.key}, size={self.size}, want_id={self.want_id}, round={self.round})"
 
     def encode(self) -> None:
         self.row = (*self.key, self.size, self.want_id | ((1 if self.force_cdn else 0) << 62))

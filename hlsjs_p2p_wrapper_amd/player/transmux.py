@@ -30,13 +30,24 @@ from ..utils.trace import PhaseTimer
 ALIGN = 256
 
 
-@dataclass
 class TransmuxJob:
-    payload: Any                       # torch uint8 tensor (any device) / numpy / bytes
-    key: Optional[bytes]               # AES-128 key or None
-    iv: Optional[bytes]
-    callback: Callable[[Dict[str, Any]], None]
-    frag: Any = None
+    """One fragment to transmux: ``payload`` (torch uint8 tensor on any device / numpy /
+    bytes), the AES-128 ``key`` and ``iv`` (``None``: clear), ``callback(result)``.  A plain
+    slotted class: one is built per fragment, and a dataclass ``__init__`` stays interpreted
+    code inside the compiled module."""
+
+    __slots__ = ("payload", "key", "iv", "callback", "frag")
+
+    def __init__(self, payload: Any, key: Optional[bytes], iv: Optional[bytes],
+                 callback: Callable[[Dict[str, Any]], None], frag: Any = None) -> None:
+        self.payload = payload
+        self.key = key
+        self.iv = iv
+        self.callback = callback
+        self.frag = frag
+
+    def __repr__(self) -> str:
+        return f"TransmuxJob(key={'set' if self.key else None}, frag={self.frag!r})"
 
 
 def _as_tensor(payload: Any) -> torch.Tensor:
