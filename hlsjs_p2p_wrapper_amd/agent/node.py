@@ -96,7 +96,7 @@ class _Want:
     class: one per request, and a dataclass ``__init__`` is interpreted code even here."""
 
     __slots__ = ("key", "url", "headers", "size", "want_id", "waiters", "force_cdn", "attempts", "round",
-                 "prefetch", "row")
+                 "prefetch", "row", "net", "staged", "staging")
 
     def __init__(self, key: Tuple[int, int, int, int], url: str, headers: Dict[str, str], size: int,
                  want_id: int, waiters: Optional[List[Request]] = None, force_cdn: bool = False,
@@ -111,13 +111,20 @@ class _Want:
         self.attempts = attempts
         self.round = round  # round it is in flight in (-1: waiting)
         self.prefetch = prefetch  # issued by an agent's prefetch planner (may have no waiters)
-        self.row = ()  # control-message encoding (key x4, size, want_id | force_cdn << 62)
+        self.row = ()  # control-message encoding (key x4, size, want_id | force_cdn << 62 | ...)
+        # network origin (net/network.py): (origin, path, range); the body must be staged in
+        # host memory (staged) before a round may fetch it; staging: download in progress
+        self.net = None
+        self.staged = True
+        self.staging = False
 
     def __repr__(self) -> str:
         return f"_Want(key={self.key}, size={self.size}, want_id={self.want_id}, round={self.round})"
 
     def encode(self) -> None:
-        self.row = (*self.key, self.size, self.want_id | ((1 if self.force_cdn else 0) << 62))
+        self.row = (*self.key, self.size,
+                    self.want_id | ((1 if self.force_cdn else 0) << 62) | ((0 if self.staged else 1) << 61)
+                    | ((1 if self.staging else 0) << 60))
 
 
 class _Completion:
@@ -147,6 +154,7 @@ class RoundHandle:
     recv_entries: List[Tuple[int, int, int, int, int]] = field(default_factory=list)
     send_pins: Optional[np.ndarray] = None
     hold: List[np.ndarray] = field(default_factory=list)  # in-flight entries pinned until delivered
+    release: List[Any] = field(default_factory=list)  # network-origin wants whose staged copy this round DMAs
     sent_bytes: int = 0
     ev_cdn: Any = None
     dmas: int = 0
@@ -226,6 +234,7 @@ class SwarmNode:
         self._pins: List[Tuple[int, np.ndarray]] = []  # (release at launch #, entry ids)
         self._agents: List[Any] = []
         self._prefetched: Dict[Tuple[int, int, int, int], str] = {}  # key -> "cdn" | "p2p"
+        self._net_wants = False  # some want came from a network origin (plans may carry STAGE rows)
         self.peer_online = np.ones(self.world, dtype=bool)
         self.stats = {"cdn": 0, "p2p": 0, "upload": 0, "cache": 0, "rounds": 0, "crc_failures": 0,
                       "segments": 0, "cdn_segments": 0, "p2p_segments": 0, "prefetched": 0}
@@ -285,17 +294,71 @@ class SwarmNode:
         w = self._wants.get(req.key)
         if w is None:
             try:
-                size = http.head(url, req.headers)
+                w = self._new_want(req.key, url, req.headers)
             except http.HttpError as e:
                 self.loop.call_soon(self._fail, req, e)
                 return req
-            w = _Want(req.key, url, req.headers, int(size), self._next_want_id)
-            w.encode()
-            self._next_want_id += 1
             self._wants[req.key] = w
         w.waiters.append(req)
         self._schedule()
         return req
+
+    def _new_want(self, key, url: str, headers: Dict[str, str], prefetch: bool = False) -> _Want:
+        """A want for ``url``: its size from the origin, or, for a network origin whose body is
+        not staged yet, size 0 and ``staged=False`` (the planner then has it staged first)."""
+        origin, path = http.resolve(url)
+        rng = http.parse_range(headers) if headers else None
+        net = None
+        if getattr(origin, "staged_fetch", False):
+            size = origin.staged_size(path, rng)
+            net = (origin, path, rng)
+        else:
+            size = origin.size(path, url, rng)
+        w = _Want(key, url, headers, int(size or 0), self._next_want_id, prefetch=prefetch)
+        if net is not None:
+            w.net = net
+            w.staged = size is not None
+            self._net_wants = True
+        w.encode()
+        self._next_want_id += 1
+        return w
+
+    def _stage(self, w: _Want) -> None:
+        """Plan said: download ``w``'s body from its network origin into host memory.  The
+        completion comes back to this loop; the want is planned again once staged."""
+        if w.staging or w.staged or w.net is None:
+            return
+        origin, path, rng = w.net
+        w.staging = True
+        w.encode()  # published as downloading: the planner stages it nowhere else meanwhile
+        loop = self.loop
+        loop.hold()
+
+        def done(n, err):  # worker thread
+            try:
+                loop.call_soon_threadsafe(self._on_staged, w, n, err)
+            finally:
+                loop.release()
+
+        origin.stage(path, w.url, rng, w.headers, done)
+
+    def _on_staged(self, w: _Want, n, err) -> None:
+        w.staging = False
+        w.encode()
+        if err is not None:
+            if self._wants.get(w.key) is w:
+                del self._wants[w.key]
+            for req in w.waiters:
+                self._fail(req, err)
+            return
+        w.size = int(n)
+        w.staged = True
+        w.encode()
+        if self._wants.get(w.key) is w:
+            self._schedule()
+        else:  # nobody waits any more (aborted / served meanwhile): drop the host copy
+            origin, path, rng = w.net
+            origin.release(path, rng)
 
     def prefetch(self, key: Tuple[int, int, int, int], url: str, headers: Optional[Dict[str, str]] = None) -> bool:
         """Fill the cache with a segment no player asked for yet (agent prefetch planning,
@@ -305,12 +368,9 @@ class SwarmNode:
         if key in self._wants or self.store.lookup1(*key) >= 0:
             return False
         try:
-            size = http.head(url, dict(headers or {}))
+            w = self._new_want(key, url, dict(headers or {}), prefetch=True)
         except http.HttpError:
             return False
-        w = _Want(key, url, dict(headers or {}), int(size), self._next_want_id, prefetch=True)
-        w.encode()
-        self._next_want_id += 1
         self._wants[key] = w
         self.stats["prefetched"] += 1
         self._schedule()
@@ -446,6 +506,11 @@ class SwarmNode:
             w.round = self.round
         h.n_wants = len(all_wants)
         cdn_rows = plan[(plan[:, 5] == -1) & (plan[:, 6] == me)]
+        if self._net_wants:  # network-origin wants this rank must download first (STAGE rows)
+            for wid in plan[(plan[:, 5] == -2) & (plan[:, 6] == me), 7].tolist():
+                w = h.by_id.get(wid)
+                if w is not None:
+                    self._stage(w)
         send_rows = plan[plan[:, 5] == me]
         recv_rows = plan[(plan[:, 6] == me) & (plan[:, 5] >= 0)]
         h.n_send = len(send_rows)
@@ -519,6 +584,9 @@ class SwarmNode:
             self.stats["crc_failures"] += len(bad)
         if h.send_pins is not None:
             self.store.unpin(h.send_pins)
+        for w in h.release:  # the round's DMAs are done: drop the staged host copies
+            origin, path, rng = w.net
+            origin.release(path, rng)
         self.stats["upload"] += h.sent_bytes
         completions: List[_Completion] = []
         cdn_views = self._views([e[2] for e in h.cdn_entries], [e[3] for e in h.cdn_entries])
@@ -540,6 +608,8 @@ class SwarmNode:
                 continue
             if wants_map.get(w.key) is w:
                 del wants_map[w.key]
+            if w.net is not None and w.staged:  # staged here, but a peer's copy came first
+                w.net[0].release(w.net[1], w.net[2])
             if w.prefetch and not w.waiters:
                 self._prefetched[w.key] = "p2p"
             p2p_ms, delay = h.p2p_ms, 0.0
@@ -577,8 +647,8 @@ class SwarmNode:
         self.last_round = {"wants": h.n_wants, "cdn": len(h.cdn_entries), "send": h.n_send,
                            "recv": len(h.recv_entries), "cdn_ms": h.cdn_ms, "dmas": h.dmas, "p2p_ms": h.p2p_ms,
                            "ms": (time.perf_counter() - h.t0) * 1e3}
-        if any(w.round < 0 for w in self._wants.values()):
-            self._schedule()
+        if any(w.round < 0 and not w.staging for w in self._wants.values()):
+            self._schedule()  # (a want being downloaded is rescheduled when it lands)
 
     def _views(self, offs: List[int], lens: List[int]) -> List[torch.Tensor]:
         """Zero-copy uint8 views of the arena for a round's deliveries (one native call on
@@ -629,14 +699,20 @@ class SwarmNode:
             if w is None:
                 continue
             try:
-                origin, path = http.resolve(w.url)
-                data, off, n, _ = origin.resource(path)
-                rng = http.parse_range(w.headers) if w.headers else None
-                if rng is not None:
-                    s, e = rng
-                    e = n - 1 if e is None else min(e, n - 1)
-                    off, n = off + s, max(0, e - s + 1)
-                corrupt = origin.should_corrupt(path)
+                if w.net is not None:  # network origin: the staged (already ranged) host copy
+                    origin, path, rng = w.net
+                    data, off, n, _ = origin.resource_range(path, rng)
+                    corrupt = False
+                    h.release.append(w)
+                else:
+                    origin, path = http.resolve(w.url)
+                    data, off, n, _ = origin.resource(path)
+                    rng = http.parse_range(w.headers) if w.headers else None
+                    if rng is not None:
+                        s, e = rng
+                        e = n - 1 if e is None else min(e, n - 1)
+                        off, n = off + s, max(0, e - s + 1)
+                    corrupt = origin.should_corrupt(path)
             except http.HttpError as e:
                 if self._wants.get(w.key) is w:
                     del self._wants[w.key]
@@ -938,8 +1014,11 @@ def node_for_config(p2p_config: Any) -> SwarmNode:
     ``roundIntervalMs``, ``autoTick``, ``maxWantsPerRound``, ``trace``, ``linkKbps``
     (``{peer: kbit/s}`` slow-link fault injection), ``metricsPort`` (serve Prometheus
     ``GET /metrics`` on port + rank, 0 = ephemeral; ``metricsHost`` defaults to
-    127.0.0.1); the agent reads ``prefetchSeconds`` / ``prefetchMaxSegments``.
+    127.0.0.1), ``network`` (``True`` or ``HttpOrigin`` options: fetch ``http(s)://`` URLs
+    no in-process origin serves from the real CDN, :mod:`..net.network`); the agent reads
+    ``prefetchSeconds`` / ``prefetchMaxSegments``.
     """
+    apply_network_config(p2p_config)
     node = current_node()
     if node is not None and not node.closed:
         return node
@@ -973,6 +1052,15 @@ def node_for_config(p2p_config: Any) -> SwarmNode:
         node.metrics_server = _start_metrics(node, cfg, backend)
     set_current_node(node)
     return node
+
+
+def apply_network_config(p2p_config: Any) -> None:
+    """``p2pConfig.gpuSwarm.network``: ``True`` / a dict of :class:`~..net.network.HttpOrigin`
+    options turns on real-CDN resolution for ``http(s)://`` URLs (``http.enable_network``)."""
+    gs = p2p_config.get("gpuSwarm") if isinstance(p2p_config, dict) else None
+    net = gs.get("network") if isinstance(gs, dict) else None
+    if net and not http.network_enabled():
+        http.enable_network(True, **(net if isinstance(net, dict) else {}))
 
 
 def _start_metrics(node: SwarmNode, cfg: dict, backend: str) -> Any:

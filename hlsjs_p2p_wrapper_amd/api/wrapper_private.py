@@ -19,6 +19,7 @@ from __future__ import annotations
 import logging
 from typing import Any, Dict, Optional
 
+from ..agent.node import apply_network_config
 from ..integration.p2p_loader import p2p_loader_generator
 from ..integration.player_interface import PlayerInterface
 from ..models.media_map import MediaMap
@@ -52,6 +53,7 @@ class HlsjsP2PWrapperPrivate:
     def createMediaEngine(self, hlsjsConfig: Optional[Dict[str, Any]] = None, p2pConfig: Any = None):
         """New engine (P2P loader config merged in); the session starts on its ``MANIFEST_LOADING``."""
         Hlsjs = self.Hlsjs
+        apply_network_config(p2pConfig)  # the manifest may come from the real CDN: before loadSource
         mediaEngine = self.newMediaEngine(hlsjsConfig if hlsjsConfig is not None else {})
 
         def on_manifest_loading(event: str, data: Any) -> None:

@@ -15,10 +15,15 @@ Two clocks:
   playlist refreshes) in milliseconds, deterministically.
 
 One loop per thread (``get_event_loop()``), mirroring the one-timer-queue-per-tab model;
-the in-process multi-peer swarm test runs one peer per thread.
+the in-process multi-peer swarm test runs one peer per thread.  Work done on other threads
+(network fetches, :mod:`.network`) comes back through :meth:`EventLoop.call_soon_threadsafe`;
+while such work is outstanding (:meth:`EventLoop.hold` / :meth:`EventLoop.release`) an idle
+loop waits for it instead of sleeping to its next timer, and a virtual clock does not jump
+past it.
 """
 from __future__ import annotations
 
+import collections
 import heapq
 import itertools
 import threading
@@ -58,6 +63,12 @@ class EventLoop:
         self._seq = itertools.count()
         self._idle_hooks: List[Callable[[], bool]] = []
         self._compact_at = 4096
+        # callbacks posted from other threads (deque append / popleft are atomic) and the
+        # event that wakes an idle loop for them; _external counts outstanding foreign work
+        self._threadsafe: collections.deque = collections.deque()
+        self._wake = threading.Event()
+        self._external = 0
+        self._ext_lock = threading.Lock()
 
     # ------------------------------------------------------------------ clock
     def now(self) -> float:
@@ -111,6 +122,28 @@ class EventLoop:
     def call_soon(self, fn: Callable[..., Any], *args: Any) -> None:
         self._ready.append((fn, args))
 
+    def call_soon_threadsafe(self, fn: Callable[..., Any], *args: Any) -> None:
+        """Schedule ``fn(*args)`` on this loop from any thread (wakes an idle loop)."""
+        self._threadsafe.append((fn, args))
+        self._wake.set()
+
+    def hold(self) -> None:
+        """Another thread is doing work whose result comes back through
+        :meth:`call_soon_threadsafe`: an idle loop waits for it (and a virtual clock does not
+        skip ahead of it).  Pair with :meth:`release`, called on any thread."""
+        with self._ext_lock:
+            self._external += 1
+
+    def release(self) -> None:
+        with self._ext_lock:
+            self._external = max(0, self._external - 1)
+        self._wake.set()
+
+    def _take_threadsafe(self) -> None:
+        q = self._threadsafe
+        while q:
+            self._ready.append(q.popleft())
+
     def add_idle_hook(self, hook: Callable[[], bool]) -> None:
         """``hook()`` runs when the loop would otherwise sleep; returns True if it did work."""
         self._idle_hooks.append(hook)
@@ -151,6 +184,8 @@ class EventLoop:
     def run_once(self, block: bool = True, max_wait_ms: float = 50.0) -> bool:
         """Run ready callbacks and due timers.  Returns False when nothing is left."""
         did = False
+        if self._threadsafe:
+            self._take_threadsafe()
         if self._ready:
             ready, self._ready = self._ready, []
             for fn, args in ready:
@@ -172,15 +207,24 @@ class EventLoop:
         if did:
             return True
         deadline = self._next_deadline()
+        if self._external:  # foreign work outstanding: wait for it (or the next timer)
+            if not block:
+                return True
+            wait = max_wait_ms if deadline is None or self.clock == "virtual" else \
+                min(max(0.0, deadline - self.now()), max_wait_ms)
+            self._wake.wait(wait / 1000.0)
+            self._wake.clear()
+            return True
         if deadline is None:
-            return bool(self._ready)
+            return bool(self._ready) or bool(self._threadsafe)
         if self.clock == "virtual":
             self._vnow = max(self._vnow, deadline)
             return True
         if block:
             wait = min(max(0.0, deadline - self.now()), max_wait_ms) / 1000.0
             if wait > 0:
-                time.sleep(wait)
+                self._wake.wait(wait)
+                self._wake.clear()
         return True
 
     def run_until(self, predicate: Callable[[], bool], timeout_ms: float = 60_000.0) -> bool:
@@ -191,7 +235,8 @@ class EventLoop:
                 return False
             if self.clock == "virtual":
                 nd = self._next_deadline()
-                if not self._ready and nd is not None and nd > end and not self._idle_hooks:
+                if not self._ready and nd is not None and nd > end and not self._idle_hooks \
+                        and not self._external and not self._threadsafe:
                     self._vnow = end
                     return predicate()
             if not self.run_once():
@@ -203,7 +248,8 @@ class EventLoop:
         self.run_until(lambda: self.now() >= end, timeout_ms=duration_ms + 1.0)
 
     def pending(self) -> int:
-        return len(self._ready) + sum(1 for e in self._heap if not e[2].cancelled)
+        return (len(self._ready) + len(self._threadsafe) + self._external
+                + sum(1 for e in self._heap if not e[2].cancelled))
 
 
 _local = threading.local()

@@ -16,7 +16,7 @@ import math
 import re
 import threading
 from dataclasses import dataclass
-from typing import Any, Dict, List, Optional, Tuple
+from typing import Any, Callable, Dict, List, Optional, Tuple
 
 
 class HttpError(Exception):
@@ -85,8 +85,47 @@ def unregister_origin(base_url: str) -> None:
 
 def clear_origins() -> None:
     with _reg_lock:
+        origins = list(_registry.values())
         _registry.clear()
         _resolved.clear()
+    for o in origins:  # network origins own worker threads and staged host buffers
+        if getattr(o, "staged_fetch", False):
+            o.close()
+
+
+_network: Optional[Dict[str, Any]] = None  # enable_network() options; None = in-process origins only
+
+
+def enable_network(on: bool = True, **options: Any) -> None:
+    """Let ``http(s)://`` URLs that no registered origin claims resolve to a real CDN: one
+    :class:`~.network.HttpOrigin` per scheme://host, created on first use with ``options``
+    (``workers``, ``timeout_s``, ``pin_memory`` ...).  ``enable_network(False)`` turns it off
+    (origins already created stay registered until :func:`clear_origins`)."""
+    global _network
+    with _reg_lock:
+        _network = dict(options) if on else None
+        _resolved.clear()
+
+
+def network_enabled() -> bool:
+    return _network is not None
+
+
+def _network_origin(url: str) -> Optional[Tuple[str, Any]]:
+    if _network is None or not (url.startswith("http://") or url.startswith("https://")):
+        return None
+    from urllib.parse import urlsplit
+
+    from .network import HttpOrigin
+
+    u = urlsplit(url)
+    base = f"{u.scheme}://{u.netloc}/"
+    with _reg_lock:
+        origin = _registry.get(base)
+        if origin is None:
+            origin = HttpOrigin(base, register=False, **_network)
+            _registry[base] = origin
+    return base, origin
 
 
 def resolve(url: str) -> Tuple[Any, str]:
@@ -97,6 +136,8 @@ def resolve(url: str) -> Tuple[Any, str]:
     for base, origin in list(_registry.items()):
         if url.startswith(base) and (best is None or len(base) > len(best[0])):
             best = (base, origin)
+    if best is None:
+        best = _network_origin(url)
     if best is None:
         raise HttpError(0, url, f"no origin serves {url}")  # status 0 = network error
     hit = (best[1], url[len(best[0]):])
@@ -128,6 +169,40 @@ def fetch(url: str, headers: Optional[Dict[str, str]] = None, with_credentials: 
     origin, path = resolve(url)
     rng = parse_range(headers)
     return origin.serve(path, url, rng, headers or {}, with_credentials)
+
+
+def fetch_async(url: str, headers: Optional[Dict[str, str]], with_credentials: bool, loop: Any,
+                on_response: Callable[[Response], Any], on_error: Callable[[HttpError], Any]) -> None:
+    """:func:`fetch` that never blocks ``loop``: an origin with ``serve_async`` (a network
+    origin) runs on its worker pool and the callback is posted back to ``loop``; in-process
+    origins answer synchronously (the callback runs before this returns, as before)."""
+    try:
+        origin, path = resolve(url)
+        rng = parse_range(headers)
+    except HttpError as e:
+        on_error(e)
+        return
+    serve_async = getattr(origin, "serve_async", None)
+    if serve_async is None:
+        try:
+            resp = origin.serve(path, url, rng, headers or {}, with_credentials)
+        except HttpError as e:
+            on_error(e)
+            return
+        on_response(resp)
+        return
+    loop.hold()
+
+    def done(resp: Optional[Response], err: Optional[HttpError]) -> None:
+        try:
+            if err is not None:
+                loop.call_soon_threadsafe(on_error, err)
+            else:
+                loop.call_soon_threadsafe(on_response, resp)
+        finally:
+            loop.release()
+
+    serve_async(path, url, rng, headers or {}, with_credentials, done)
 
 
 def head(url: str, headers: Optional[Dict[str, str]] = None) -> int:

@@ -454,7 +454,8 @@ PYBIND11_MODULE(_runtime, m) {
       });
   // One round's gathered control messages (agent/node.py:_encode layout: header[hdr_words] =
   // magic, flags, #wants, #adds, #removes, leaving, round, cdn, p2p, upload, ...; then wants
-  // [key4, size, want_id | force_cdn << 62], adds [key4, len], removes [key4]) in one call:
+  // [key4, size, want_id | force_cdn << 62 | not_staged << 61 | staging << 60], adds [key4, len], removes
+  // [key4]) in one call:
   // applies every rank's cache delta to the directory and returns (want rows int64[n, 8] for
   // plan_round, per-rank flags, all-leaving, swarm byte totals [cdn, p2p, upload]).
   m.def("ingest_control", [](Directory& d, const std::vector<Arr<int64_t>>& parts, int64_t magic,
@@ -484,9 +485,11 @@ PYBIND11_MODULE(_runtime, m) {
       for (int64_t i = 0; i < nr; ++i) d.apply_remove(r, key_from(rm + 4 * i));
       for (int64_t i = 0; i < nw; ++i) {
         const int64_t* x = w + 6 * i;
-        const int64_t id = x[5] & ((int64_t(1) << 62) - 1);
-        const int64_t force = (x[5] >> 62) & 1;
-        rows.insert(rows.end(), {x[0], x[1], x[2], x[3], x[4], id, r, force});
+        // want word: want_id | force_cdn << 62 | not_staged << 61 | staging << 60 -> WantFlag bits
+        const int64_t id = x[5] & ((int64_t(1) << 60) - 1);
+        const int64_t wflags = ((x[5] >> 62) & 1 ? kForceCdn : 0) | ((x[5] >> 61) & 1 ? kNotStaged : 0) |
+                               ((x[5] >> 60) & 1 ? kStaging : 0);
+        rows.insert(rows.end(), {x[0], x[1], x[2], x[3], x[4], id, r, wflags});
       }
     }
     const int64_t n = static_cast<int64_t>(rows.size() / 8);
@@ -497,7 +500,8 @@ PYBIND11_MODULE(_runtime, m) {
     return py::make_tuple(out, flags, all_leaving, totals);
   });
   // wants: int64[n, 8] = (key4, size, want_id, rank, want_flags); flags int64[world]
-  // -> int64[m, 10] = (key4, size, src, dst, want_id, seeded, reserved)
+  // -> int64[m, 10] = (key4, size, src, dst, want_id, seeded, reserved); src -1 = CDN fetch,
+  // -2 = stage (download from a network origin into host memory for a later round)
   m.def("plan_round", [](const Directory& d, Arr<int64_t> wants, Arr<int64_t> flags, int world) {
     const int64_t n = wants.size() / 8;
     std::vector<Want> w(n);

@@ -48,13 +48,21 @@ std::vector<Transfer> plan_round(const Directory& dir, const std::vector<Want>& 
   std::vector<int64_t> link(size_t(world) * world, 0);  // bytes src->dst this round
   std::vector<int64_t> send_total(world, 0), cdn_total(world, 0);
   std::vector<Transfer> cdn, p2p;
+  // a CDN fetch for want w, or its STAGE row when w's body is not in host memory yet
+  auto cdn_or_stage = [&](const Want& wt, const SegKey& key) {
+    if (wt.flags & kStaging) return;  // its download is running: nothing to plan yet
+    const bool staged = !(wt.flags & kNotStaged);
+    cdn.push_back({key, wt.size, staged ? kCdn : kStage, wt.rank, wt.want_id, 0});
+    if (staged) cdn_total[wt.rank] += wt.size;
+  };
   // keys no peer holds yet but several ranks want: ONE rank fetches from the CDN and
   // forwards in the same round ("seeding"); assigned after the pass (run-affine, below)
   struct SeedGroup {
     SegKey key;
     size_t i, j;
     std::vector<size_t> unserved;
-    uint64_t cands;  // wanting ranks that may upload
+    uint64_t cands;  // wanting ranks that may upload (staged ones only, when any is)
+    bool staged;     // the seeder has the body in host memory (else it only stages it)
   };
   std::vector<SeedGroup> seeds;
 
@@ -74,8 +82,7 @@ std::vector<Transfer> plan_round(const Directory& dir, const std::vector<Want>& 
       const Want& wt = wants[w];
       const int d = wt.rank;
       if (!flag(d, kOnline) || !flag(d, kDownloadOn) || (wt.flags & kForceCdn)) {
-        cdn.push_back({key, wt.size, -1, d, wt.want_id, 0});
-        cdn_total[d] += wt.size;
+        cdn_or_stage(wt, key);
         continue;
       }
       uint64_t cand = holders & ~(uint64_t(1) << d);
@@ -104,12 +111,18 @@ std::vector<Transfer> plan_round(const Directory& dir, const std::vector<Want>& 
         for (size_t w : unserved)
           if (flag(wants[w].rank, kUploadOn)) cands |= uint64_t(1) << wants[w].rank;
       if (cands) {
-        seeds.push_back({key, i, j, std::move(unserved), cands});  // seeder chosen below
-      } else {
+        // staged wanters seed; with none staged yet, one wanter is chosen to stage it
+        uint64_t ready = 0;
+        bool staging = false;
         for (size_t w : unserved) {
-          cdn.push_back({key, wants[w].size, -1, wants[w].rank, wants[w].want_id, 0});
-          cdn_total[wants[w].rank] += wants[w].size;
+          if (!(wants[w].flags & kNotStaged)) ready |= uint64_t(1) << wants[w].rank;
+          staging = staging || (wants[w].flags & kStaging);
         }
+        if ((cands & ready) || !staging)  // else a wanter is downloading it: all wait this round
+          seeds.push_back({key, i, j, std::move(unserved), (cands & ready) ? (cands & ready) : cands,
+                           (cands & ready) != 0});  // seeder chosen below
+      } else {
+        for (size_t w : unserved) cdn_or_stage(wants[w], key);
       }
     }
     i = j;
@@ -122,7 +135,9 @@ std::vector<Transfer> plan_round(const Directory& dir, const std::vector<Want>& 
     int64_t seed_bytes = 0;
     uint64_t all = 0;
     for (const auto& g : seeds) {
-      seed_bytes += wants[g.unserved[0]].size;
+      int64_t sz = 0;  // a not-yet-staged network want does not know its size (0)
+      for (size_t w : g.unserved) sz = std::max(sz, wants[w].size);
+      seed_bytes += sz;
       all |= g.cands;
     }
     int nseed = 0;
@@ -147,21 +162,30 @@ std::vector<Transfer> plan_round(const Directory& dir, const std::vector<Want>& 
         }
       }
       cur = seeder;
-      const int64_t sz = wants[g.unserved[0]].size;
+      // the seeder's want carries the size every forwarded copy has (a wanter that has not
+      // staged the body itself may not know it)
+      const Want* own = nullptr;
+      for (size_t w : g.unserved)
+        if (wants[w].rank == seeder && own == nullptr) own = &wants[w];
+      const int64_t sz = own->size;
       seeded[seeder] += sz;
+      if (!g.staged) {  // nobody has the body yet: the seeder stages it, the rest wait
+        cdn.push_back({g.key, sz, kStage, seeder, own->want_id, 0});
+        continue;
+      }
       for (size_t w : g.unserved) {
         const Want& wt = wants[w];
         if (wt.rank == seeder) {
-          cdn.push_back({g.key, wt.size, -1, seeder, wt.want_id, 0});
+          cdn.push_back({g.key, wt.size, kCdn, seeder, wt.want_id, 0});
           cdn_total[seeder] += wt.size;
         }
       }
       for (size_t w : g.unserved) {
         const Want& wt = wants[w];
         if (wt.rank == seeder) continue;
-        p2p.push_back({g.key, wt.size, seeder, wt.rank, wt.want_id, 1});
-        link[size_t(seeder) * world + wt.rank] += wt.size;
-        send_total[seeder] += wt.size;
+        p2p.push_back({g.key, sz, seeder, wt.rank, wt.want_id, 1});
+        link[size_t(seeder) * world + wt.rank] += sz;
+        send_total[seeder] += sz;
       }
     }
   }

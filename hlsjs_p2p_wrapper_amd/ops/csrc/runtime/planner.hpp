@@ -17,6 +17,13 @@
 //   3. nobody holds it: with CDN de-duplication one wanter (least CDN bytes this round,
 //      hash rotation on ties) "seeds" it from the CDN and forwards it to the other wanters
 //      in the same round; without it every wanter goes to the CDN.
+// A CDN fetch needs the body in host memory.  In-process origins always have it; a network
+// origin (net/network.py) first downloads it ("stages" it).  A want flagged kNotStaged is
+// never given a CDN row: where it would be, the planner emits a STAGE row (src = kStage) for
+// that rank instead — for a seed group only for the rank chosen as seeder, the others wait —
+// and the want is planned again once its rank reports it staged.  While some wanter is
+// still downloading (kStaging) nobody else is told to: the key's other wanters wait.  So a segment crosses the
+// network once per swarm, and the same round protocol serves both origin kinds.
 #pragma once
 #include <cstdint>
 #include <unordered_map>
@@ -35,7 +42,11 @@ struct DirEntry {
   int64_t length = 0;
 };
 
-enum WantFlag : int64_t { kForceCdn = 1 };
+// kNotStaged: the body is not in host memory yet; kStaging: this rank is downloading it now
+enum WantFlag : int64_t { kForceCdn = 1, kNotStaged = 2, kStaging = 4 };
+
+constexpr int32_t kCdn = -1;    // Transfer.src: CDN fetch (body in host memory) by dst
+constexpr int32_t kStage = -2;  // Transfer.src: dst downloads the body from its network origin
 
 struct Want {
   SegKey key;
@@ -48,7 +59,7 @@ struct Want {
 struct Transfer {  // one segment moving src -> dst
   SegKey key;
   int64_t size;
-  int32_t src;      // -1 = CDN
+  int32_t src;      // kCdn (-1) = CDN fetch, kStage (-2) = stage, else the sending rank
   int32_t dst;
   int64_t want_id;  // want id at dst
   int32_t seeded;   // 1: src fetched it from the CDN this round (forwarding)

@@ -20,7 +20,7 @@ import math
 from typing import Any, Callable, Optional
 
 from ..net.event_loop import get_event_loop
-from ..net.http import HttpError, Shaper, fetch
+from ..net.http import HttpError, Shaper, fetch_async
 from ..utils.events import JsObject
 
 log = logging.getLogger("hlsjs_p2p_wrapper_amd.loader")
@@ -51,6 +51,7 @@ class XhrLoader:
         self._request_timeout = None
         self._retry_timeout = None
         self._inflight = False
+        self._attempt = 0
         self.byteRange: Optional[str] = None
 
     # ------------------------------------------------------------------ API
@@ -103,11 +104,21 @@ class XhrLoader:
         self.stats.loaded = 0
         self._inflight = True
         self._request_timeout = self.loop.set_timeout(self._on_timeout, self.timeout)
-        try:
-            resp = fetch(self.url, headers, shim.withCredentials)
-        except HttpError as e:
-            delay = Shaper.minLatency
-            self._timers.append(self.loop.set_timeout(self._on_error, delay, e.status))
+        self._attempt += 1
+        attempt = self._attempt
+        # in-process origins answer before fetch_async returns; a network origin answers on
+        # this loop later (a stale answer of an aborted / retried attempt is dropped)
+        fetch_async(self.url, headers, shim.withCredentials, self.loop,
+                    lambda resp: self._on_response(attempt, resp), lambda e: self._on_fetch_error(attempt, e))
+
+    def _on_fetch_error(self, attempt: int, e: HttpError) -> None:
+        if attempt != self._attempt or not self._inflight:
+            return
+        delay = Shaper.minLatency
+        self._timers.append(self.loop.set_timeout(self._on_error, delay, e.status))
+
+    def _on_response(self, attempt: int, resp) -> None:
+        if attempt != self._attempt or not self._inflight:
             return
         total = resp.length
         duration = Shaper.transfer_ms(total)
