@@ -206,6 +206,7 @@ class HttpOrigin:
                 self._inflight.pop(key, None)
 
     def staged_size(self, path: str, rng: Range = None) -> Optional[int]:
+        """Length of a staged resource, ``None`` when it is not staged."""
         with self._lock:
             hit = self._staged.get((path, rng))
         return None if hit is None else hit[1]
@@ -225,14 +226,17 @@ class HttpOrigin:
 
     @property
     def staged_bytes(self) -> int:
+        """Host bytes held by staged resources."""
         with self._lock:
             return sum(n for _, n in self._staged.values())
 
     # ------------------------------------------------------------------ origin interface
     def resource(self, path: str):
+        """The staged full resource (origin interface of the in-process origins)."""
         return self.resource_range(path, None)
 
     def size(self, path: str, url: str = "", rng: Range = None) -> int:
+        """Length of a resource: the staged copy's, else a ``HEAD`` request (blocking)."""
         n = self.staged_size(path, rng)
         if n is not None:
             return n
@@ -243,6 +247,7 @@ class HttpOrigin:
         return int(resp.getheader("Content-Length") or 0)
 
     def should_corrupt(self, path: str) -> bool:
+        """Fault-injection hook of the in-process origins: never for a real CDN."""
         return False
 
     def serve(self, path: str, url: str, rng: Range, headers: Dict[str, str], with_credentials: bool) -> Response:
@@ -264,6 +269,7 @@ class HttpOrigin:
         self._pool.submit(job)
 
     def close(self) -> None:
+        """Stop the worker pool and drop every staged copy."""
         self.closed = True
         self._pool.shutdown(wait=False, cancel_futures=True)
         with self._lock:

@@ -43,6 +43,8 @@ SURFACE = [
     ("xhrSetup sandbox", "hlsjs_p2p_wrapper_amd.utils.xhr", "extractInfoFromXhrSetup"),
     ("Statics", "hlsjs_p2p_wrapper_amd.utils.statics", "inheritStaticPropertiesReadOnly"),
     ("Metrics", "hlsjs_p2p_wrapper_amd.utils.metrics", "MetricsServer"),
+    ("Network CDN", "hlsjs_p2p_wrapper_amd.net.http", "enable_network"),
+    ("Network CDN", "hlsjs_p2p_wrapper_amd.net.network", "HttpOrigin"),
     ("Checkpoint", "hlsjs_p2p_wrapper_amd.agent.checkpoint", "save_cache"),
     ("Checkpoint", "hlsjs_p2p_wrapper_amd.agent.checkpoint", "load_cache"),
 ]
