@@ -3,7 +3,8 @@
 The analog of the reference's ``example/config.js`` (p2pConfig / hlsjsConfig /
 contentUrl, WebRTC capability detection, ``example/config.js:5-17``).  In this framework a
 "peer" is a GPU (or a CPU thread in tests), so the capability check is "can this process
-join a swarm" and the stream is a synthetic HLS origin served from pinned host memory.
+join a swarm" and the stream is a synthetic HLS origin served from pinned host memory, or
+with ``--url`` a real HLS stream from its CDN (``p2pConfig.gpuSwarm.network``).
 
 Every example runs as:
 
@@ -26,6 +27,7 @@ import torch  # noqa: E402
 
 from hlsjs_p2p_wrapper_amd.agent import current_node, node_for_config, set_current_node  # noqa: E402
 from hlsjs_p2p_wrapper_amd.net import new_event_loop  # noqa: E402
+from hlsjs_p2p_wrapper_amd.net.http import enable_network  # noqa: E402
 from hlsjs_p2p_wrapper_amd.net.origin import Rendition, SyntheticHlsOrigin  # noqa: E402
 from hlsjs_p2p_wrapper_amd.player import MediaElement  # noqa: E402
 
@@ -68,6 +70,9 @@ def parse_args(description: str) -> argparse.Namespace:
     p.add_argument("--clear", action="store_true", help="unencrypted stream")
     p.add_argument("--cpu", action="store_true", help="CPU only (no GPU)")
     p.add_argument("--no-p2p", action="store_true", help="play with P2P disabled (plain engine)")
+    p.add_argument("--url", default=None,
+                   help="play this http(s):// master playlist from the real CDN (net/network.py) "
+                        "instead of the synthetic origin")
     return p.parse_args()
 
 
@@ -76,11 +81,15 @@ PlayFn = Callable[[Dict[str, Any], MediaElement, bool], Any]
 
 def _peer(play: PlayFn, args, origin, gpu_swarm: Dict[str, Any], out: Dict[int, Any], rank: int) -> None:
     set_current_node(None)
-    loop = new_event_loop("virtual")
+    # a real CDN plays on the wall clock; the synthetic origin on a virtual one (fast)
+    loop = new_event_loop("real" if args.url else "virtual")
+    if args.url:
+        gpu_swarm = dict(gpu_swarm, network=True)
+        enable_network()  # also for --no-p2p: the plain engine's loaders need the CDN too
     cfg = {
         "p2pConfig": dict(STREAMROOT_CONFIG["p2pConfig"], gpuSwarm=gpu_swarm),
         "hlsjsConfig": dict(STREAMROOT_CONFIG["hlsjsConfig"]),
-        "contentUrl": origin.master_url(),
+        "contentUrl": args.url or origin.master_url(),
     }
     p2p_enabled = has_swarm() and not args.no_p2p
     if p2p_enabled:
@@ -101,7 +110,7 @@ def main(play: PlayFn, description: str) -> Dict[int, Any]:
     args = parse_args(description)
     world = int(os.environ.get("WORLD_SIZE", "1"))
     device = "cpu" if (args.cpu or not torch.cuda.is_available()) else "cuda"
-    origin = make_origin(live=args.live, encrypted=not args.clear)
+    origin = None if args.url else make_origin(live=args.live, encrypted=not args.clear)
     out: Dict[int, Any] = {}
     if world > 1:  # torchrun: one peer per rank (one GPU each)
         import torch.distributed as dist

@@ -56,3 +56,19 @@ def test_example_torchrun_two_ranks():
     assert sorted(peers) == [0, 1]
     assert all(p["ok"] for p in peers.values())
     assert sum(p["p2p"] for p in peers.values()) > 0
+
+
+def test_example_plays_a_real_http_cdn():
+    """``--url``: the bundle example against a real HTTP server (the local CDN of
+    ``test_network_origin.py``), two in-process peers sharing the downloads."""
+    from test_network_origin import _Cdn
+
+    cdn = _Cdn(num_segments=4)
+    try:
+        peers = _run(["examples/bundle/play.py", "--peers", "2", "--cpu", "--seconds", "3",
+                      "--url", cdn.origin.master_url()])
+        assert sorted(peers) == [0, 1] and all(p["ok"] for p in peers.values())
+        assert sum(p["cdn"] for p in peers.values()) == cdn.ts_bytes()  # one download per segment
+        assert sum(p["p2p"] for p in peers.values()) > 0
+    finally:
+        cdn.close()
