@@ -479,6 +479,8 @@ class SwarmNode:
                 continue
             if not any(not r.aborted for r in w.waiters):
                 del self._wants[k]
+                if w.net is not None and w.staged:  # nobody wants it any more: drop the host copy
+                    w.net[0].release(w.net[1], w.net[2])
                 continue
             wants.append(w)
             if cap is not None and len(wants) >= cap:
@@ -686,6 +688,8 @@ class SwarmNode:
             if a > self.cache_bytes:  # can never fit: fail it
                 if self._wants.get(w.key) is w:
                     del self._wants[w.key]
+                if w.net is not None and w.staged:
+                    w.net[0].release(w.net[1], w.net[2])
                 err = http.HttpError(507, f"segment of {w.size} bytes exceeds the {self.cache_bytes}-byte cache")
                 for req in w.waiters:
                     self.loop.call_soon(self._fail, req, err)
