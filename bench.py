@@ -82,8 +82,26 @@ def parse():
     p.add_argument("--no-gc-tune", action="store_true", help="keep Python's default GC settings")
     p.add_argument("--metrics-port", type=int, default=None,
                    help="serve Prometheus GET /metrics on port + rank while the bench runs (idle unless scraped)")
+    p.add_argument("--numa", default="off", choices=["auto", "off", "remote"],
+                   help="auto: run on (and first-touch pinned buffers from) the CPUs local to the GPU; "
+                        "remote: the other socket's CPUs (diagnostic); off: leave the affinity alone")
     p.add_argument("--verbose", action="store_true")
     return p.parse_args()
+
+
+def _numa(mode: str, dev: int):
+    from hlsjs_p2p_wrapper_amd.utils.runtime import bind_to_gpu_numa, gpu_local_cpus
+
+    if mode == "off":
+        return None
+    if mode == "auto":
+        return bind_to_gpu_numa(dev)
+    node, local = gpu_local_cpus(dev)  # remote: every allowed CPU NOT local to the GPU
+    other = os.sched_getaffinity(0).difference(local)
+    if node is None or len(other) < 8:
+        return None
+    os.sched_setaffinity(0, other)
+    return f"remote-of-{node}"
 
 
 def main() -> int:
@@ -96,8 +114,10 @@ def main() -> int:
         local_dev = local_rank % torch.cuda.device_count()  # rehearsals may share one GPU
         torch.cuda.set_device(local_dev)
         device = torch.device("cuda", local_dev)
+        numa_node = _numa(args.numa, local_dev)  # before the pinned CDN buffers are allocated
     else:
         device = torch.device("cpu")
+        numa_node = None
     import torch.distributed as dist
 
     if world > 1:
@@ -294,7 +314,7 @@ def main() -> int:
                    "parallelism": f"swarm{world}" + (f"-{'rccl' if dist.get_backend() == 'nccl' else 'gloo'}"
                                                      if world > 1 else ""),
                    "inflight_per_gpu": K, "encrypted": encrypted, "segment_s": seg_dur, "churn_steps": args.churn,
-                   "device": "MI355X" if use_gpu else "cpu"},
+                   "device": "MI355X" if use_gpu else "cpu", "numa": numa_node},
     }
     if args.verbose:
         print(f"# rank {rank} pack {t_pack:.2f}s counters {counters} level {hls.currentLevel}\n"

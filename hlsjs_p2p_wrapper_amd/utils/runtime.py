@@ -8,11 +8,16 @@ everything alive into the permanent generation (``gc.freeze``) and raises the ge
 threshold, so collections only look at young objects.  The per-fragment churn (loader
 stats, event payloads, closures) is mostly freed by reference counting anyway.  GC stays
 enabled: new cycles are still collected.
+
+:func:`bind_to_gpu_numa` keeps a peer's host side on the NUMA node its GPU hangs off: the
+CPUs it runs on (the host path is one Python thread per GPU) and, through first touch, the
+pinned host buffers the CDN DMAs read, so those transfers do not cross the socket link.
 """
 from __future__ import annotations
 
 import gc
-from typing import Tuple
+import os
+from typing import List, Optional, Tuple
 
 
 def tune_gc(gen0_threshold: int = 50_000) -> Tuple[int, int, int]:
@@ -25,3 +30,50 @@ def tune_gc(gen0_threshold: int = 50_000) -> Tuple[int, int, int]:
     gc.freeze()
     gc.set_threshold(gen0_threshold, prev[1], prev[2])
     return prev
+
+
+def _parse_cpulist(text: str) -> List[int]:
+    cpus: List[int] = []
+    for part in text.strip().split(","):
+        if not part:
+            continue
+        if "-" in part:
+            a, b = part.split("-")
+            cpus.extend(range(int(a), int(b) + 1))
+        else:
+            cpus.append(int(part))
+    return cpus
+
+
+def gpu_local_cpus(device_index: int = 0) -> Tuple[Optional[int], List[int]]:
+    """``(numa_node, cpus)`` of a GPU from sysfs (its PCI function's ``numa_node`` and
+    ``local_cpulist``); ``(None, [])`` when unknown."""
+    import torch
+
+    try:
+        p = torch.cuda.get_device_properties(device_index)
+        addr = f"{getattr(p, 'pci_domain_id', 0):04x}:{p.pci_bus_id:02x}:{getattr(p, 'pci_device_id', 0):02x}.0"
+        base = f"/sys/bus/pci/devices/{addr}"
+        with open(os.path.join(base, "local_cpulist")) as f:
+            cpus = _parse_cpulist(f.read())
+        with open(os.path.join(base, "numa_node")) as f:
+            node = int(f.read().strip())
+    except (AttributeError, OSError, ValueError, RuntimeError):
+        return None, []
+    return (node if node >= 0 else None), cpus
+
+
+def bind_to_gpu_numa(device_index: int = 0, min_cpus: int = 8) -> Optional[int]:
+    """Restrict this process to the CPUs local to its GPU (and so, by first touch, its later
+    host allocations to that NUMA node).  Only narrows the current affinity, and only when
+    at least ``min_cpus`` of the GPU's CPUs are allowed; returns the node, or None when it
+    left the affinity alone.  Call it before allocating pinned buffers."""
+    node, cpus = gpu_local_cpus(device_index)
+    if node is None or not cpus:
+        return None
+    allowed = os.sched_getaffinity(0)
+    local = allowed.intersection(cpus)
+    if len(local) < min_cpus or local == allowed:
+        return node if local == allowed else None
+    os.sched_setaffinity(0, local)
+    return node
