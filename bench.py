@@ -82,7 +82,7 @@ def parse():
     p.add_argument("--no-gc-tune", action="store_true", help="keep Python's default GC settings")
     p.add_argument("--metrics-port", type=int, default=None,
                    help="serve Prometheus GET /metrics on port + rank while the bench runs (idle unless scraped)")
-    p.add_argument("--numa", default="off", choices=["auto", "off", "remote"],
+    p.add_argument("--numa", default="auto", choices=["auto", "off", "remote"],
                    help="auto: run on (and first-touch pinned buffers from) the CPUs local to the GPU; "
                         "remote: the other socket's CPUs (diagnostic); off: leave the affinity alone")
     p.add_argument("--verbose", action="store_true")
