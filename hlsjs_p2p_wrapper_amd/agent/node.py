@@ -1020,7 +1020,8 @@ def node_for_config(p2p_config: Any) -> SwarmNode:
     ``GET /metrics`` on port + rank, 0 = ephemeral; ``metricsHost`` defaults to
     127.0.0.1), ``network`` (``True`` or ``HttpOrigin`` options: fetch ``http(s)://`` URLs
     no in-process origin serves from the real CDN, :mod:`..net.network`); the agent reads
-    ``prefetchSeconds`` / ``prefetchMaxSegments``.
+    ``prefetchSeconds`` / ``prefetchMaxSegments``.  ``numaBind``: run this process on the CPUs
+    local to the node's GPU (``utils.runtime.bind_to_gpu_numa``; ``bench.py --numa auto``).
     """
     apply_network_config(p2p_config)
     node = current_node()
@@ -1048,6 +1049,10 @@ def node_for_config(p2p_config: Any) -> SwarmNode:
     node = SwarmNode(comm, device=cfg.get("device", "auto"), cache_bytes=int(cfg.get("cacheBytes", 1 << 30)),
                      cdn_dedup=bool(cfg.get("cdnDedup", True)), round_interval_ms=cfg.get("roundIntervalMs"),
                      auto_tick=bool(cfg.get("autoTick", True)), max_wants_per_round=cfg.get("maxWantsPerRound"))
+    if cfg.get("numaBind") and node.is_cuda:
+        from ..utils.runtime import bind_to_gpu_numa
+
+        bind_to_gpu_numa(node.device.index if node.device.index is not None else torch.cuda.current_device())
     if cfg.get("trace"):
         node.enable_trace()
     for peer, kbps in (cfg.get("linkKbps") or {}).items():
