@@ -137,8 +137,10 @@ def p2p_loader_generator(hlsjsWrapper: Any) -> type:
             if self.byteRange:
                 headers["Range"] = f"bytes={self.frag.byteRangeStartOffset}-{self.frag.byteRangeEndOffset - 1}"
             level = hlsjsWrapper.hls.levels[self.frag.level]
-            trackView = TrackView(level=self.frag.level, urlId=_attr(level, "urlId"))
-            segmentView = SegmentView(sn=self.frag.sn, trackView=trackView, time=self.frag.start)
+            frag = self.frag
+            # a fresh TrackView handed over: the view need not deep-copy it (segment-view.js:24)
+            segmentView = SegmentView._owning(frag.sn, TrackView(level=frag.level, urlId=_attr(level, "urlId")),
+                                              frag.start)
             reqInfo = JsObject(url=self.url, headers=headers, withCredentials=withCredentials)
             callbacks = JsObject(onSuccess=self.loadSuccess, onError=self.loadError, onProgress=self.loadProgress)
             stats = self.stats

@@ -42,6 +42,16 @@ class SegmentView:
         self.trackView = TrackView(trackView)
         self.time = time
 
+    @classmethod
+    def _owning(cls, sn: Any, trackView: TrackView, time: Any) -> "SegmentView":
+        """A view that takes ``trackView`` as is (no copy): for callers that just built that
+        TrackView and hand it over (the P2P loader, once per fragment request)."""
+        v = cls.__new__(cls)
+        v.sn = sn
+        v.trackView = trackView
+        v.time = time
+        return v
+
     # --- reference API -------------------------------------------------------
     @staticmethod
     def fromArrayBuffer(buf: Any) -> "SegmentView":

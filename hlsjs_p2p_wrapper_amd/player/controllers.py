@@ -568,9 +568,27 @@ class StreamController:
         self.inflight[(frag.level, frag.sn)] = frag
         dd = frag.decryptdata
         if dd is not None and dd.needs_key:
-            self.hls.trigger(Events.KEY_LOADING, {"frag": frag})
-        else:
-            self.hls.trigger(Events.FRAG_LOADING, {"frag": frag})
+            key = self._cached_key(dd)
+            if key is None:
+                self.hls.trigger(Events.KEY_LOADING, {"frag": frag})
+                return
+            dd.key = key  # what KeyLoader.onKeyLoading -> KEY_LOADED -> onKeyLoaded would do
+        self.hls.trigger(Events.FRAG_LOADING, {"frag": frag})
+
+    def _cached_key(self, dd) -> Optional[bytes]:
+        """The already-loaded key of ``dd`` when the KEY_LOADING / KEY_LOADED round trip would
+        only reach the engine's own handlers (the key loader and this controller): then the
+        result is the same without the two events (once per fragment of an encrypted
+        stream).  With any other listener, the events are sent as usual."""
+        obs = self.hls._observer._listeners
+        kl = obs.get(Events.KEY_LOADING)
+        kd = obs.get(Events.KEY_LOADED)
+        if kl is None or kd is None or len(kl) != 1 or len(kd) != 1:
+            return None
+        key_loader = self.hls.keyLoader
+        if kl[0] != key_loader.onKeyLoading or kd[0] != self.onKeyLoaded:
+            return None
+        return key_loader.keys.get(dd.uri)
 
     def onKeyLoaded(self, event: str, data: Any) -> None:
         frag = data["frag"]
