@@ -82,6 +82,10 @@ def parse():
     p.add_argument("--no-gc-tune", action="store_true", help="keep Python's default GC settings")
     p.add_argument("--metrics-port", type=int, default=None,
                    help="serve Prometheus GET /metrics on port + rank while the bench runs (idle unless scraped)")
+    p.add_argument("--players", type=int, default=0,
+                   help="fleet mode: this many player processes per GPU feed the node (each plays its own "
+                        "slice of the DVR window with --inflight fragments per step); 0 = the player runs in "
+                        "the node's process")
     p.add_argument("--numa", default="auto", choices=["auto", "off", "remote"],
                    help="auto: run on (and first-touch pinned buffers from) the CPUs local to the GPU; "
                         "remote: the other socket's CPUs (diagnostic); off: leave the affinity alone")
@@ -142,11 +146,13 @@ def main() -> int:
     K = args.inflight
     total_steps = args.warmup + args.steps
     n_segments = (total_steps + 4) * K
+    W = max(0, args.players)
+    origin_kwargs = dict(base_url="http://cdn.bench/live/", renditions=rends,
+                         num_segments=n_segments * max(1, W) + (16 * K if W else 0),
+                         segment_duration=seg_dur, encrypted=encrypted, pool_size=args.pool, seed=7)
     loop = new_event_loop("real")
     t_pack = time.perf_counter()
-    origin = SyntheticHlsOrigin("http://cdn.bench/live/", renditions=rends, num_segments=n_segments,
-                                segment_duration=seg_dur, encrypted=encrypted, pool_size=args.pool,
-                                pin_memory=use_gpu, seed=7)
+    origin = SyntheticHlsOrigin(**origin_kwargs, pin_memory=use_gpu)
     t_pack = time.perf_counter() - t_pack
     p2p_config = {"streamrootKey": "bench", "contentId": "bench-1080p",
                   "gpuSwarm": {"backend": "dist" if world > 1 else "local", "device": str(device),
@@ -160,6 +166,9 @@ def main() -> int:
                   "startPosition": 0, "fragLoadingTimeOut": 600_000, "tickInterval": 1e9}
     if preset != "abr5":
         hls_config["startLevel"] = 0
+    if W:
+        return _fleet(args, world, rank, device, use_gpu, node, origin, origin_kwargs, p2p_config, hls_config,
+                      n_segments, seg_dur, desc, encrypted, numa_node, dist, t_pack)
     hls = Hls(hls_config, p2p_config)
     media = MediaElement(mode="drain", loop=loop)
     counters = {"buffered": 0, "errors": 0, "level_switches": 0}
@@ -292,9 +301,178 @@ def main() -> int:
     else:
         tot, max_ns = vals, int(vals[3])
     max_s = max_ns / 1e9
+    result = _result(args, world, tot, max_s, origin, K, desc, encrypted, seg_dur, use_gpu, numa_node, dist)
+    if args.verbose:
+        print(f"# rank {rank} pack {t_pack:.2f}s counters {counters} level {hls.currentLevel}\n"
+              f"#   node stats {node.stats} last round {node.last_round}\n"
+              f"#   step ms {bt.summary_ms(args.steps)}\n"
+              f"#   node ms {node.timer.summary_ms(args.steps)}\n"
+              f"#   transmux ms {pipe.timer.summary_ms(args.steps)}", file=sys.stderr)
+    _dump_profile(rank)
+    if rank == 0:
+        print(json.dumps(result), flush=True)
+    if world > 1:
+        node.comm.barrier()
+        node.comm.close()  # the native RCCL communicator (collective, every rank is here)
+        dist.destroy_process_group()
+    return 0
+
+
+def _fleet(args, world, rank, device, use_gpu, node, origin, origin_kwargs, p2p_config, hls_config, n_segments,
+           seg_dur, desc, encrypted, numa_node, dist, t_pack):
+    """Fleet mode (``--players W``): W player processes per GPU, each playing its own slice of
+    the DVR window through the bundle ``Hls`` over a ``RemoteNode``; this process runs the
+    node (rounds, CDN DMA, RCCL, CRC) and the batched GPU transmux (``parallel/fleet.py``).
+    The timed window is K node steps; the fragments counted are those the players buffered
+    between two in-band marks sent at its edges (a mark follows every answer sent before it
+    through the same pipe)."""
+    import collections
+    import multiprocessing as mp
+
+    from hlsjs_p2p_wrapper_amd.parallel.fleet import FleetServer, player_main
+    from hlsjs_p2p_wrapper_amd.player.transmux import pipeline_for
+    from hlsjs_p2p_wrapper_amd.utils.runtime import tune_gc
+
+    W, K = args.players, args.inflight
+    ctx = mp.get_context("spawn")
+    conns, procs = [], []
+    # the players never touch the GPU: hide it from them (set only around the spawns)
+    saved = {k: os.environ.get(k) for k in ("HIP_VISIBLE_DEVICES", "CUDA_VISIBLE_DEVICES")}
+    os.environ["HIP_VISIBLE_DEVICES"] = os.environ["CUDA_VISIBLE_DEVICES"] = "-1"
+    try:
+        for w in range(W):
+            parent, child = ctx.Pipe()
+            spec = {"origin": dict(origin_kwargs, pin_memory=False),
+                    "hls_config": dict(hls_config, startPosition=w * n_segments * seg_dur),
+                    "p2p_config": {k: v for k, v in p2p_config.items() if k != "gpuSwarm"},
+                    "world": world, "rank": rank}
+            pr = ctx.Process(target=player_main, args=(child, spec), daemon=True, name=f"hlsp2p-player{w}")
+            pr.start()
+            child.close()
+            conns.append(parent)
+            procs.append(pr)
+    finally:
+        for k, v in saved.items():
+            if v is None:
+                os.environ.pop(k, None)
+            else:
+                os.environ[k] = v
+    pipe = pipeline_for(device)
+    pipe.auto_flush = False
+    server = FleetServer(node, pipe, conns)
+    state = {"hs": collections.deque(), "b": None}
+
+    def step():
+        server.poll()
+        state["hs"].append(node.launch_round())
+        if len(state["hs"]) > args.lag:
+            node.complete_round(state["hs"].popleft())
+        b = server.launch_transmux()
+        server.complete_transmux(state["b"])
+        server.send()
+        state["b"] = b
+
+    def sync():
+        if use_gpu:
+            torch.cuda.synchronize(device)
+        if world > 1:
+            node.comm.barrier()
+        if use_gpu:
+            torch.cuda.synchronize(device)
+
+    def mark(tag):
+        for c, o in zip(conns, server.open):
+            if o:
+                c.send(("mark", tag))
+
+    try:
+        # players start (import, playlists, keys): step until every one of them has requests in
+        # flight.  Collective: every rank steps until all ranks' players are up.
+        t_end = time.perf_counter() + 180
+        while True:
+            step()
+            up = np.array([int(all(len(r) > 0 or not o for r, o in zip(server._by_rid, server.open)))],
+                          dtype=np.int64)
+            if world > 1:
+                up = np.array([min(int(x[0]) for x in node.comm.allgather_control(up))], dtype=np.int64)
+            if up[0]:
+                break
+            if time.perf_counter() > t_end or not all(pr.is_alive() for pr in procs):
+                raise RuntimeError("fleet players did not start")
+            time.sleep(0.002)
+        tune_gc()
+        for _ in range(args.warmup):
+            step()
+        sync()
+        node.timer.reset()
+        s0 = dict(node.stats)
+        mark("t0")
+        t0 = time.perf_counter()
+        for _ in range(args.steps):
+            step()
+        sync()
+        elapsed = time.perf_counter() - t0
+        mark("t1")
+        s1 = dict(node.stats)
+        # keep serving until every player has acknowledged both marks (collective rounds)
+        t_end = time.perf_counter() + 120
+        while True:
+            step()
+            got = server.marks.get("t1", {})
+            ok = np.array([int(all(not o or w in got for w, o in enumerate(server.open)))], dtype=np.int64)
+            if world > 1:
+                ok = np.array([min(int(x[0]) for x in node.comm.allgather_control(ok))], dtype=np.int64)
+            if ok[0]:
+                break
+            if time.perf_counter() > t_end:
+                raise TimeoutError("fleet players did not acknowledge the window marks")
+        m0, m1 = server.marks.get("t0", {}), server.marks["t1"]
+        done = sum(m1[w]["buffered"] - m0.get(w, {"buffered": 0})["buffered"] for w in m1)
+        errors = sum(m1[w]["errors"] for w in m1)
+        d_segs = sum(s1[k] - s0[k] for k in ("cdn_segments", "p2p_segments"))
+        vals = np.array([done, s1["cdn"] - s0["cdn"], s1["p2p"] - s0["p2p"], int(elapsed * 1e9), errors, d_segs],
+                        dtype=np.int64)
+        if world > 1:
+            parts = node.comm.allgather_control(vals)
+            tot = np.sum(np.stack(parts), axis=0)
+            max_ns = max(int(x[3]) for x in parts)
+        else:
+            tot, max_ns = vals, int(vals[3])
+        result = _result(args, world, tot, max_ns / 1e9, origin, K, desc, encrypted, seg_dur, use_gpu, numa_node,
+                         dist, players=W)
+        if args.verbose:
+            print(f"# rank {rank} pack {t_pack:.2f}s players {W} marks {dict(m1)}\n"
+                  f"#   node stats {node.stats} last round {node.last_round}\n"
+                  f"#   node ms {node.timer.summary_ms(args.steps)}\n"
+                  f"#   transmux ms {pipe.timer.summary_ms(args.steps)}", file=sys.stderr)
+        if rank == 0:
+            print(json.dumps(result), flush=True)
+    finally:
+        for c, o in zip(conns, server.open):
+            if o:
+                try:
+                    c.send(("stop",))
+                except (OSError, BrokenPipeError):
+                    pass
+        for pr in procs:
+            pr.join(timeout=20)
+            if pr.is_alive():
+                pr.kill()
+                pr.join(timeout=5)
+    if world > 1:
+        node.comm.barrier()
+        node.comm.close()
+        dist.destroy_process_group()
+    return 0
+
+
+def _result(args, world, tot, max_s, origin, K, desc, encrypted, seg_dur, use_gpu, numa_node, dist, players=0):
+    """The JSON line (``tot``: [fragments buffered, cdn bytes, p2p bytes, ns, errors, segments]
+    summed over ranks; ``max_s``: the slowest rank's timed window)."""
     # bytes per delivered segment over the timed region (an ABR ladder mixes renditions)
     seg_bytes = int((tot[1] + tot[2]) // max(1, tot[5])) if tot[5] else int(np.mean(origin.pools[0].lengths))
-    result = {
+    inflight = K * max(1, players)
+    return {
         "metric": "segments/sec + P2P offload ratio, 1080p 6 Mb/s HLS at 1/2/4/8 MI355X",
         "value": round(float(tot[0]) / max_s, 2),
         "unit": "segments/s",
@@ -310,18 +488,16 @@ def main() -> int:
         "offload_ratio": round(float(tot[2]) / max(1.0, float(tot[1] + tot[2])), 4),
         "goodput_GBps": round(float(tot[1] + tot[2]) / max_s / 1e9, 3),  # bytes delivered to the players
         "errors": int(tot[4]),
-        "config": {"model": desc, "global_batch": K * world, "seq_len": seg_bytes,
+        "config": {"model": desc, "global_batch": inflight * world, "seq_len": seg_bytes,
                    "parallelism": f"swarm{world}" + (f"-{'rccl' if dist.get_backend() == 'nccl' else 'gloo'}"
                                                      if world > 1 else ""),
-                   "inflight_per_gpu": K, "encrypted": encrypted, "segment_s": seg_dur, "churn_steps": args.churn,
-                   "device": "MI355X" if use_gpu else "cpu", "numa": numa_node},
+                   "inflight_per_gpu": inflight, "players_per_gpu": max(1, players),
+                   "player_processes": players > 0, "encrypted": encrypted, "segment_s": seg_dur,
+                   "churn_steps": args.churn, "device": "MI355X" if use_gpu else "cpu", "numa": numa_node},
     }
-    if args.verbose:
-        print(f"# rank {rank} pack {t_pack:.2f}s counters {counters} level {hls.currentLevel}\n"
-              f"#   node stats {node.stats} last round {node.last_round}\n"
-              f"#   step ms {bt.summary_ms(args.steps)}\n"
-              f"#   node ms {node.timer.summary_ms(args.steps)}\n"
-              f"#   transmux ms {pipe.timer.summary_ms(args.steps)}", file=sys.stderr)
+
+
+def _dump_profile(rank: int) -> None:
     if _PROF is not None:
         import io
         import pstats
@@ -332,13 +508,6 @@ def main() -> int:
         st.sort_stats("cumtime").print_stats(60)
         with open(os.environ["HLSP2P_PROFILE"] + f".{rank}.txt", "w") as f:
             f.write(out.getvalue())
-    if rank == 0:
-        print(json.dumps(result), flush=True)
-    if world > 1:
-        node.comm.barrier()
-        node.comm.close()  # the native RCCL communicator (collective, every rank is here)
-        dist.destroy_process_group()
-    return 0
 
 
 if __name__ == "__main__":

@@ -279,9 +279,10 @@ class SwarmNode:
 
     # ------------------------------------------------------------------ requests
     def request(self, key: Tuple[int, int, int, int], url: str, headers: Optional[Dict[str, str]],
-                callbacks: Any, agent: Any = None) -> Request:
+                callbacks: Any, agent: Any = None, view: Any = None) -> Request:
         """Queue a fragment request for key ``(swarm, level, urlId, sn)``; served from the cache,
-        a peer or the CDN in the next round."""
+        a peer or the CDN in the next round.  (``view``: the agent's SegmentView, which a
+        fleet's remote node uses to find the fragment's AES key; unused here.)"""
         k0, k1, k2, k3 = key
         req = Request(self, (int(k0) & _M32, int(k1) & _M32, int(k2) & _M32, int(k3) & _M32), url,
                       dict(headers) if headers else {}, callbacks, agent, False, False, self.loop.now())
@@ -1044,6 +1045,12 @@ def node_for_config(p2p_config: Any) -> SwarmNode:
         from ..parallel.comm import DistComm
 
         comm = DistComm()
+    elif backend == "remote":  # fleet player process: the node lives in the GPU process
+        from ..parallel.fleet import RemoteNode
+
+        node = RemoteNode(cfg["conn"], world=int(cfg.get("world", 1)), rank=int(cfg.get("rank", 0)))
+        set_current_node(node)
+        return node
     else:
         raise ValueError(f"unknown gpuSwarm backend {backend!r}")
     node = SwarmNode(comm, device=cfg.get("device", "auto"), cache_bytes=int(cfg.get("cacheBytes", 1 << 30)),

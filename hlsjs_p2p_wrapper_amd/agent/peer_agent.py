@@ -79,7 +79,7 @@ class PeerAgent:
         headers = _get(reqInfo, "headers") or {}
         tv = segmentView.trackView
         key = (self.swarm_id, int(tv.level or 0), int(tv.urlId or 0), int(segmentView.sn or 0))
-        req = self.node.request(key, url, headers, callbacks, agent=self)
+        req = self.node.request(key, url, headers, callbacks, agent=self, view=segmentView)
         return req
 
     get_segment = getSegment

@@ -20,6 +20,7 @@ from typing import Any, Dict, List, Optional, Tuple
 from .events import ErrorDetails, ErrorTypes, Events
 from .level import Fragment, Level, LevelDetails
 from .playlist import PlaylistError, is_master, parse_master, parse_media
+from ..parallel.fleet import RemoteSegment
 from .transmux import TransmuxJob, pipeline_for
 
 log = logging.getLogger("hlsjs_p2p_wrapper_amd.player")
@@ -606,6 +607,9 @@ class StreamController:
         iv = frag.iv_for_decrypt() if key is not None else None
         stats = data["stats"]
         payload = data["payload"]
+        if type(payload) is RemoteSegment:  # fleet player: the node process already transmuxed it
+            self.loop.call_soon(self._on_parsed, frag, stats, payload.transmux_result)
+            return
         dev = self.hls.transmux_device(payload)
         pipeline_for(dev, self.loop).submit(
             TransmuxJob(payload, key, iv, lambda r: self._on_parsed(frag, stats, r), frag))

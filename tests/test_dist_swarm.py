@@ -166,3 +166,14 @@ def test_four_process_gloo_swarm_with_churn_and_late_joiner():
     assert out[3][1]["cdn"] == 0 or out[3][1]["p2p"] > 0  # the late joiner mostly rides the swarm
     assert sum(v[1]["p2p"] for v in out.values()) > 0
     assert 0 < out[0][2] < 1
+
+
+def test_bench_fleet_two_ranks_two_players():
+    """Fleet mode through the driver's launch path: 2 ranks x 2 player processes (gloo, CPU).
+    Every player's fragments are counted between the in-band window marks; the swarm still
+    fetches each segment from the CDN once (player w plays the same DVR slice on each rank)."""
+    res = _bench_cpu(_free_port(), "--players", "2", config="hostcost-micro")
+    assert res["errors"] == 0 and res["value"] > 0
+    assert res["config"]["players_per_gpu"] == 2 and res["config"]["player_processes"]
+    assert res["config"]["global_batch"] == 8 * 2 * 2
+    assert res["offload_ratio"] == pytest.approx(0.5, abs=0.02)
