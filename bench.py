@@ -329,6 +329,7 @@ def _fleet(args, world, rank, device, use_gpu, node, origin, origin_kwargs, p2p_
     import collections
     import multiprocessing as mp
 
+    from hlsjs_p2p_wrapper_amd.net.event_loop import get_event_loop
     from hlsjs_p2p_wrapper_amd.parallel.fleet import FleetServer, player_main
     from hlsjs_p2p_wrapper_amd.player.transmux import pipeline_for
     from hlsjs_p2p_wrapper_amd.utils.runtime import tune_gc
@@ -357,12 +358,21 @@ def _fleet(args, world, rank, device, use_gpu, node, origin, origin_kwargs, p2p_
                 os.environ.pop(k, None)
             else:
                 os.environ[k] = v
-    pipe = pipeline_for(device)
+    loop = get_event_loop()  # the node's loop: cache hits and failures are delivered from it
+    pipe = pipeline_for(device, loop)
     pipe.auto_flush = False
     server = FleetServer(node, pipe, conns)
+    node.max_wants_per_round = K * W  # every player gets K fragments per round
     state = {"hs": collections.deque(), "b": None}
 
+    def drain_ready():
+        for _ in range(1000):
+            if not loop._ready:
+                return
+            loop.run_once(block=False)
+
     def step():
+        drain_ready()
         server.poll()
         state["hs"].append(node.launch_round())
         if len(state["hs"]) > args.lag:
@@ -386,12 +396,21 @@ def _fleet(args, world, rank, device, use_gpu, node, origin, origin_kwargs, p2p_
                 c.send(("mark", tag))
 
     try:
-        # players start (import, playlists, keys): step until every one of them has requests in
-        # flight.  Collective: every rank steps until all ranks' players are up.
+        # players start (imports, origin): wait for every player of every rank, then let them
+        # all load at once; step until each has sent requests (collective on every rank)
         t_end = time.perf_counter() + 180
+        while len(server.ready) < W:
+            server.poll()
+            time.sleep(0.005)
+            if time.perf_counter() > t_end or not all(pr.is_alive() for pr in procs):
+                raise RuntimeError("fleet players did not start")
+        if world > 1:
+            node.comm.barrier()
+        for c in conns:
+            c.send(("go",))
         while True:
             step()
-            up = np.array([int(all(len(r) > 0 or not o for r, o in zip(server._by_rid, server.open)))],
+            up = np.array([int(all(n > 0 or not o for n, o in zip(server.requests, server.open)))],
                           dtype=np.int64)
             if world > 1:
                 up = np.array([min(int(x[0]) for x in node.comm.allgather_control(up))], dtype=np.int64)

@@ -309,6 +309,8 @@ class FleetServer:
         self._delivered: List[Tuple[_Pending, Any]] = []
         self._outbox: List[List[tuple]] = [[] for _ in self.conns]
         self.marks: Dict[Any, Dict[int, Any]] = {}
+        self.ready: set = set()
+        self.requests = [0] * len(self.conns)
         self.sent = 0
 
     # -------------------------------------------------------------- inbound
@@ -330,6 +332,7 @@ class FleetServer:
                             by_rid[rid] = p
                             p.req = node.request(key, url, headers, _Callbacks(self, p))
                             n += 1
+                        self.requests[w] += len(msg[1])
                     elif kind == "abort":
                         by_rid = self._by_rid[w]
                         for rid in msg[1]:
@@ -342,6 +345,8 @@ class FleetServer:
                         node.download_on, node.upload_on = bool(msg[1]), bool(msg[2])
                     elif kind == "mark":
                         self.marks.setdefault(msg[1], {})[w] = msg[2]
+                    elif kind == "ready":
+                        self.ready.add(w)
                     elif kind == "bye":
                         self.open[w] = False
                         break
@@ -458,6 +463,15 @@ def player_main(conn: Any, spec: Dict[str, Any]) -> None:
     hls.on(Hls.Events.ERROR, lambda e, d: counters.__setitem__("errors", counters["errors"] + 1))
     hls.on(Hls.Events.LEVEL_SWITCH, lambda e, d: counters.__setitem__("level_switches",
                                                                      counters["level_switches"] + 1))
+    # start together: a player that started early would run ahead into the next one's slice
+    conn.send(("ready",))
+    while True:
+        msg = conn.recv()
+        if msg[0] == "go":
+            break
+        if msg[0] == "stop":
+            node.close()
+            return
     hls.loadSource(origin.master_url())
     hls.attachMedia(media)
     hls.on(Hls.Events.MANIFEST_PARSED, lambda e, d: media.play())
