@@ -371,8 +371,12 @@ def _fleet(args, world, rank, device, use_gpu, node, origin, origin_kwargs, p2p_
                 return
             loop.run_once(block=False)
 
+    debug = os.environ.get("HLSP2P_FLEET_DEBUG")
+    nstep = [0]
+
     def step():
         drain_ready()
+        server.await_players()  # the players' next requests (paces the rounds by the players)
         server.poll()
         state["hs"].append(node.launch_round())
         if len(state["hs"]) > args.lag:
@@ -381,6 +385,11 @@ def _fleet(args, world, rank, device, use_gpu, node, origin, origin_kwargs, p2p_
         server.complete_transmux(state["b"])
         server.send()
         state["b"] = b
+        nstep[0] += 1
+        if debug and nstep[0] % 20 == 0:
+            print(f"# fleet step {nstep[0]} round {node.round} wants {len(node._wants)} "
+                  f"pending {[len(r) for r in server._by_rid]} requests {server.requests} sent {server.sent} "
+                  f"delivered-queue {len(server._delivered)} last {node.last_round}", file=sys.stderr, flush=True)
 
     def sync():
         if use_gpu:

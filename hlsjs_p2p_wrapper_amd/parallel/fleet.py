@@ -28,6 +28,7 @@ transmuxes what was delivered and answers each player with one batch.
 from __future__ import annotations
 
 import logging
+import os
 import time
 from typing import Any, Dict, List, Tuple
 
@@ -312,6 +313,7 @@ class FleetServer:
         self.ready: set = set()
         self.requests = [0] * len(self.conns)
         self.sent = 0
+        self._awaiting: set = set()  # players sent answers whose next requests have not come in yet
 
     # -------------------------------------------------------------- inbound
     def poll(self) -> int:
@@ -333,6 +335,7 @@ class FleetServer:
                             p.req = node.request(key, url, headers, _Callbacks(self, p))
                             n += 1
                         self.requests[w] += len(msg[1])
+                        self._awaiting.discard(w)
                     elif kind == "abort":
                         by_rid = self._by_rid[w]
                         for rid in msg[1]:
@@ -392,11 +395,31 @@ class FleetServer:
             try:
                 self.conns[w].send(("done", rows, st))
                 n += len(rows)
+                self._awaiting.add(w)
             except (OSError, BrokenPipeError):
                 self.open[w] = False
             self._outbox[w] = []
         self.sent += n
         return n
+
+    def await_players(self, timeout_s: float = 0.02) -> None:
+        """Pace the node by its players: wait until every player that was sent answers has
+        sent its next requests (it does so right after handling them), at most
+        ``timeout_s`` (a player with nothing left to ask must not stall the rounds)."""
+        from multiprocessing.connection import wait
+
+        end = time.monotonic() + timeout_s
+        while self._awaiting:
+            left = end - time.monotonic()
+            if left <= 0:
+                self._awaiting.clear()
+                return
+            waiting = [self.conns[w] for w in self._awaiting if self.open[w]]
+            if not waiting:
+                self._awaiting.clear()
+                return
+            wait(waiting, left)
+            self.poll()
 
     def wait_marks(self, tag: Any, timeout_s: float = 120.0) -> Dict[int, Any]:
         """Block until every open player has sent ``("mark", tag, ...)``."""
@@ -484,8 +507,15 @@ def player_main(conn: Any, spec: Dict[str, Any]) -> None:
             loop.run_once(block=False)
 
     gc_tuned = False
+    debug = os.environ.get("HLSP2P_FLEET_DEBUG")
+    t_dbg = time.monotonic()
     try:
         while True:
+            if debug and time.monotonic() - t_dbg > 1.0:
+                t_dbg = time.monotonic()
+                log.warning("player %s: state %s inflight %d node-inflight %d t %.1f ranges %s counters %s "
+                            "retry_until %.1f now %.1f", spec.get("rank"), sc.state, len(sc.inflight), node.inflight,
+                            media.currentTime, media.buffered, counters, sc._retry_until, loop.now())
             node.poll(0.0005)
             drain()
             sc.tick()
