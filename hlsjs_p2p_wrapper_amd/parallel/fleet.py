@@ -122,6 +122,8 @@ class RemoteNode:
         self._next = 0
         self.inflight = 0
         self.control: List[tuple] = []
+        self.batches = 0  # answer batches handled (reported to the node, which paces on it)
+        self._reported = 0
 
     # -------------------------------------------------------------- SwarmNode surface
     def attach(self, agent: Any) -> None:
@@ -174,10 +176,15 @@ class RemoteNode:
 
     # -------------------------------------------------------------- transport
     def flush(self) -> None:
-        """Send everything queued since the last flush (one message per kind)."""
+        """Send everything queued since the last flush (one message per kind), with the count
+        of answer batches handled so far (the node paces its rounds on it)."""
         if self._reqs:
-            self.conn.send(("req", self._reqs))
+            self.conn.send(("req", self._reqs, self.batches))
             self._reqs = []
+            self._reported = self.batches
+        elif self.batches != self._reported:
+            self.conn.send(("ack", self.batches))
+            self._reported = self.batches
         if self._aborts:
             self.conn.send(("abort", self._aborts))
             self._aborts = []
@@ -195,6 +202,7 @@ class RemoteNode:
             msg = conn.recv()
             if msg[0] == "done":
                 n += self._deliver(msg[1])
+                self.batches += 1
                 st = msg[2]
                 if st is not None:
                     self.stats["upload"] = st["upload"]
@@ -313,7 +321,8 @@ class FleetServer:
         self.ready: set = set()
         self.requests = [0] * len(self.conns)
         self.sent = 0
-        self._awaiting: set = set()  # players sent answers whose next requests have not come in yet
+        self.batches_sent = [0] * len(self.conns)  # answer batches sent to each player ...
+        self.batches_done = [0] * len(self.conns)  # ... and handled by it (reported back)
 
     # -------------------------------------------------------------- inbound
     def poll(self) -> int:
@@ -335,7 +344,9 @@ class FleetServer:
                             p.req = node.request(key, url, headers, _Callbacks(self, p))
                             n += 1
                         self.requests[w] += len(msg[1])
-                        self._awaiting.discard(w)
+                        self.batches_done[w] = msg[2]
+                    elif kind == "ack":
+                        self.batches_done[w] = msg[1]
                     elif kind == "abort":
                         by_rid = self._by_rid[w]
                         for rid in msg[1]:
@@ -395,30 +406,30 @@ class FleetServer:
             try:
                 self.conns[w].send(("done", rows, st))
                 n += len(rows)
-                self._awaiting.add(w)
+                self.batches_sent[w] += 1
             except (OSError, BrokenPipeError):
                 self.open[w] = False
             self._outbox[w] = []
         self.sent += n
         return n
 
-    def await_players(self, timeout_s: float = 0.02) -> None:
-        """Pace the node by its players: wait until every player that was sent answers has
-        sent its next requests (it does so right after handling them), at most
-        ``timeout_s`` (a player with nothing left to ask must not stall the rounds)."""
+    def await_players(self, depth: int = 1, timeout_s: float = 0.02) -> None:
+        """Pace the node by its players: wait until every player has handled all but at most
+        ``depth`` of the answer batches sent to it (a player sends its next requests right
+        after handling a batch).  ``depth`` 1 overlaps one batch of player work with one node
+        step; at most ``timeout_s`` (a player with nothing left to ask must not stall)."""
         from multiprocessing.connection import wait
 
         end = time.monotonic() + timeout_s
-        while self._awaiting:
+        while True:
+            behind = [self.conns[w] for w in range(len(self.conns))
+                      if self.open[w] and self.batches_sent[w] - self.batches_done[w] > depth]
+            if not behind:
+                return
             left = end - time.monotonic()
             if left <= 0:
-                self._awaiting.clear()
                 return
-            waiting = [self.conns[w] for w in self._awaiting if self.open[w]]
-            if not waiting:
-                self._awaiting.clear()
-                return
-            wait(waiting, left)
+            wait(behind, left)
             self.poll()
 
     def wait_marks(self, tag: Any, timeout_s: float = 120.0) -> Dict[int, Any]:
