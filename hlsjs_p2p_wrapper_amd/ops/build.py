@@ -175,8 +175,8 @@ ACCEL_MODULES = [
     "integration/p2p_loader.py", "agent/node.py", "agent/peer_agent.py",
     "models/segment_view.py", "models/track_view.py",
     "player/hls.py", "player/config.py", "utils/trace.py", "integration/player_interface.py",
-    "models/media_map.py", "parallel/comm.py", "parallel/fleet.py", "ops/desc.py", "ops/aes.py", "ops/tsdemux.py", "ops/crc.py",
-    "ops/segment.py",
+    "models/media_map.py", "parallel/comm.py", "parallel/fleet.py", "ops/desc.py", "ops/aes.py", "ops/tsdemux.py",
+    "ops/crc.py", "ops/segment.py",
 ]
 ACCEL_MANIFEST = "_accel.json"
 
