@@ -2,19 +2,26 @@
 """Headline benchmark: segments/s + P2P offload ratio, 1080p 6 Mb/s HLS, 1/2/4/8 MI355X.
 
 Metric and config come from BASELINE.json.  One rank per GPU (``torchrun``), each rank a
-swarm peer running the full public API path:
+swarm peer; every fragment runs the full public API path:
 
     Hls(hlsjsConfig, p2pConfig)  (bundle)  ->  P2PLoader (fLoader)  ->  PeerAgent
     ->  SwarmNode round:  CDN phase (pinned host -> HBM, side stream) + MFMA CRC ingest
-                          P2P phase (RCCL batch_isend_irecv over xGMI, CRC-verified)
+                          P2P phase (one native RCCL send/recv group over xGMI, CRC-verified)
     ->  onProgress/onSuccess  ->  FRAG_LOADED  ->  batched AES-128-CBC decrypt + TS demux
     ->  buffer append  ->  FRAG_BUFFERED
+
+By default each GPU serves ``--players`` (3) player processes ("fleet", parallel/fleet.py):
+each runs the bundle player above its ``PeerAgent`` over a ``RemoteNode`` and plays its
+own slice of the DVR window, while the rank process runs the node rounds and the GPU
+transmux for all of them (the players never touch the GPU).  ``--players 0`` runs one
+player inside the rank process.  Player ``w`` plays the same slice on every rank, so the
+swarm shares it as before.
 
 Workload (synthetic, see ``--help``): every peer plays the same 1080p 6 Mb/s AES-128
 stream (4 s MPEG-TS segments of ~3.0 MB) as fast as the engine delivers ("drain" media
 sink, e.g. an edge/restream node catching up a DVR window), with ``--inflight``
-fragments in flight per peer.  One step = one swarm exchange round in which every peer
-completes ``--inflight`` segments end to end.  Per-GPU work is fixed (weak scaling).
+fragments in flight per player and step.  One step = one swarm exchange round.  Per-GPU
+work is fixed (weak scaling).
 
 ``value`` = completed (loaded + decrypted + demuxed + buffered) segments per second over
 all ranks (timed region bracketed by barrier + device sync, max time over ranks).
@@ -82,10 +89,10 @@ def parse():
     p.add_argument("--no-gc-tune", action="store_true", help="keep Python's default GC settings")
     p.add_argument("--metrics-port", type=int, default=None,
                    help="serve Prometheus GET /metrics on port + rank while the bench runs (idle unless scraped)")
-    p.add_argument("--players", type=int, default=0,
+    p.add_argument("--players", type=int, default=3,
                    help="fleet mode: this many player processes per GPU feed the node (each plays its own "
-                        "slice of the DVR window with --inflight fragments per step); 0 = the player runs in "
-                        "the node's process")
+                        "slice of the DVR window with --inflight fragments per step; parallel/fleet.py); 0 = "
+                        "one player in the node's process")
     p.add_argument("--numa", default="auto", choices=["auto", "off", "remote"],
                    help="auto: run on (and first-touch pinned buffers from) the CPUs local to the GPU; "
                         "remote: the other socket's CPUs (diagnostic); off: leave the affinity alone")
