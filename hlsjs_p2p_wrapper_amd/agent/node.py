@@ -96,7 +96,7 @@ class _Want:
     class: one per request, and a dataclass ``__init__`` is interpreted code even here."""
 
     __slots__ = ("key", "url", "headers", "size", "want_id", "waiters", "force_cdn", "attempts", "round",
-                 "prefetch", "row", "net", "staged", "staging")
+                 "prefetch", "row", "net", "staged", "staging", "src")
 
     def __init__(self, key: Tuple[int, int, int, int], url: str, headers: Dict[str, str], size: int,
                  want_id: int, waiters: Optional[List[Request]] = None, force_cdn: bool = False,
@@ -117,6 +117,7 @@ class _Want:
         self.net = None
         self.staged = True
         self.staging = False
+        self.src = None  # (origin, path, range) resolved at creation: the CDN phase reuses it
 
     def __repr__(self) -> str:
         return f"_Want(key={self.key}, size={self.size}, want_id={self.want_id}, round={self.round})"
@@ -320,6 +321,8 @@ class SwarmNode:
             w.net = net
             w.staged = size is not None
             self._net_wants = True
+        else:
+            w.src = (origin, path, rng)
         w.encode()
         self._next_want_id += 1
         return w
@@ -710,9 +713,12 @@ class SwarmNode:
                     corrupt = False
                     h.release.append(w)
                 else:
-                    origin, path = http.resolve(w.url)
+                    if w.src is not None:
+                        origin, path, rng = w.src
+                    else:
+                        origin, path = http.resolve(w.url)
+                        rng = http.parse_range(w.headers) if w.headers else None
                     data, off, n, _ = origin.resource(path)
-                    rng = http.parse_range(w.headers) if w.headers else None
                     if rng is not None:
                         s, e = rng
                         e = n - 1 if e is None else min(e, n - 1)

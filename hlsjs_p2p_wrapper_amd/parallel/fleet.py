@@ -267,9 +267,12 @@ class RemoteNode:
 
 # ============================================================================ node side
 class _Pending:
-    __slots__ = ("w", "rid", "aes_key", "iv", "req", "source", "nbytes", "cdn_ms", "p2p_ms")
+    """One remote request on the node side; also its ``getSegment`` callbacks object."""
 
-    def __init__(self, w: int, rid: int, aes_key, iv) -> None:
+    __slots__ = ("server", "w", "rid", "aes_key", "iv", "req", "source", "nbytes", "cdn_ms", "p2p_ms")
+
+    def __init__(self, server: "FleetServer", w: int, rid: int, aes_key, iv) -> None:
+        self.server = server
         self.w = w
         self.rid = rid
         self.aes_key = aes_key
@@ -280,30 +283,18 @@ class _Pending:
         self.cdn_ms = 0.0
         self.p2p_ms = 0.0
 
-
-class _Callbacks:
-    """The node's ``getSegment`` callbacks for one remote request."""
-
-    __slots__ = ("server", "p")
-
-    def __init__(self, server: "FleetServer", p: _Pending) -> None:
-        self.server = server
-        self.p = p
-
     def onProgress(self, ev: dict) -> None:  # noqa: N802 - loader callback contract
-        p = self.p
         if ev["p2pDownloaded"]:
-            p.source, p.nbytes, p.p2p_ms = "p2p", ev["p2pDownloaded"], ev["p2pDuration"]
+            self.source, self.nbytes, self.p2p_ms = "p2p", ev["p2pDownloaded"], ev["p2pDuration"]
         else:
-            p.source, p.nbytes, p.cdn_ms = "cdn", ev["cdnDownloaded"], ev["cdnDuration"]
+            self.source, self.nbytes, self.cdn_ms = "cdn", ev["cdnDownloaded"], ev["cdnDuration"]
 
     def onSuccess(self, data: Any) -> None:  # noqa: N802
-        self.server._delivered.append((self.p, data))
+        self.server._delivered.append((self, data))
 
     def onError(self, err: Any) -> None:  # noqa: N802
-        p = self.p
-        self.server._outbox[p.w].append((p.rid, int(getattr(err, "status", 0) or 0) or 500, "", 0, 0.0, 0.0,
-                                         None, 0))
+        self.server._outbox[self.w].append((self.rid, int(getattr(err, "status", 0) or 0) or 500, "", 0, 0.0,
+                                            0.0, None, 0))
 
 
 class FleetServer:
@@ -339,9 +330,9 @@ class FleetServer:
                     if kind == "req":
                         by_rid = self._by_rid[w]
                         for rid, key, url, headers, aes_key, iv in msg[1]:
-                            p = _Pending(w, rid, aes_key, iv)
+                            p = _Pending(self, w, rid, aes_key, iv)
                             by_rid[rid] = p
-                            p.req = node.request(key, url, headers, _Callbacks(self, p))
+                            p.req = node.request(key, url, headers, p)
                             n += 1
                         self.requests[w] += len(msg[1])
                         self.batches_done[w] = msg[2]
