@@ -443,10 +443,15 @@ def _fleet(args, world, rank, device, use_gpu, node, origin, origin_kwargs, p2p_
         s0 = dict(node.stats)
         mark("t0")
         t0 = time.perf_counter()
+        if _PROF is not None:
+            _PROF.enable()
         for _ in range(args.steps):
             step()
         sync()
         elapsed = time.perf_counter() - t0
+        if _PROF is not None:
+            _PROF.disable()
+            _dump_profile(rank)
         mark("t1")
         s1 = dict(node.stats)
         # keep serving until every player has acknowledged both marks (collective rounds)
