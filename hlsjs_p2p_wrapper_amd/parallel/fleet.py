@@ -369,20 +369,16 @@ class FleetServer:
             return None
         pipe = self.pipe
         for p, data in items:
-            pipe.submit(TransmuxJob(data, p.aes_key, p.iv, _Done(self, p)))
+            pipe.submit(TransmuxJob(data, p.aes_key, p.iv, None, p))  # the pending rides as the job's frag
         return pipe.launch()
 
     def complete_transmux(self, batch) -> None:
-        """Wait for a launched transmux batch; its results go into the outboxes."""
-        self.pipe.complete(batch)
-
-    def _result(self, p: _Pending, r: Any) -> None:
-        self._by_rid[p.w].pop(p.rid, None)
-        if r.get("error") is not None and "info" not in r:
-            row, plain = None, -1
-        else:
-            row, plain = r["info"]._row, int(r.get("plain_bytes", 0))
-        self._outbox[p.w].append((p.rid, 0, p.source, p.nbytes, p.cdn_ms, p.p2p_ms, row, plain))
+        """Wait for a launched transmux batch; the info rows go into the outboxes as they are."""
+        outbox, by_rid = self._outbox, self._by_rid
+        for job, row, plain in self.pipe.complete_rows(batch):
+            p = job.frag
+            by_rid[p.w].pop(p.rid, None)
+            outbox[p.w].append((p.rid, 0, p.source, p.nbytes, p.cdn_ms, p.p2p_ms, row, plain))
 
     def send(self) -> int:
         """One answer batch per player (plus the swarm state the agents' stats read)."""
@@ -437,16 +433,6 @@ class FleetServer:
                     c.poll(0.01)
             self.poll()
 
-
-class _Done:
-    __slots__ = ("server", "p")
-
-    def __init__(self, server: FleetServer, p: _Pending) -> None:
-        self.server = server
-        self.p = p
-
-    def __call__(self, r: Any) -> None:
-        self.server._result(self.p, r)
 
 
 # ============================================================================ player process

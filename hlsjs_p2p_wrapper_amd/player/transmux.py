@@ -243,6 +243,31 @@ class MediaPipeline:
         tm.add("demux_launch", time.perf_counter() - t2)
         return _Batch(jobs, infos=infos, host=host, event=ev, results=results, keep=(dec, host_block))
 
+    def complete_rows(self, batch: Optional["_Batch"]) -> List[Tuple["TransmuxJob", Optional[list], int]]:
+        """Wait for a launched batch and return ``(job, info row, plaintext length)`` per job
+        without building the per-fragment result dicts or running callbacks (a fleet node
+        ships the rows to its player processes; ``row`` is None for a rejected job)."""
+        if batch is None:
+            return []
+        if batch.error is not None:
+            return [(j, None, -1) for j in batch.jobs]
+        t3 = time.perf_counter()
+        if batch.event is not None:
+            batch.event.synchronize()
+            self._free_events.append(batch.event)
+            batch.event = None
+        self.timer.add("wait_device", time.perf_counter() - t3)
+        out: List[Any] = [None] * len(batch.jobs)
+        for (idx, _res, _es_offs, _lens), (hinfo, hlens) in zip(batch.infos, batch.host):
+            rows = (hinfo.numpy() if isinstance(hinfo, torch.Tensor) else hinfo).tolist()
+            plain = (hlens.numpy() if isinstance(hlens, torch.Tensor) else np.asarray(hlens)).tolist()
+            for k, i in enumerate(idx):
+                out[i] = (batch.jobs[i], rows[k], int(plain[k]))
+        for i, o in enumerate(out):
+            if o is None:  # rejected before launch (e.g. not a multiple of 16 bytes)
+                out[i] = (batch.jobs[i], None, -1)
+        return out
+
     def _complete(self, b: "_Batch") -> List[Dict[str, Any]]:
         tm = self.timer
         t3 = time.perf_counter()
