@@ -385,6 +385,7 @@ def _fleet(args, world, rank, device, use_gpu, node, origin, origin_kwargs, p2p_
         drain_ready()
         server.await_players()  # the players' next requests (paces the rounds by the players)
         server.poll()
+        server.admit(K)  # K per player and round: players keep the same pace on every rank
         state["hs"].append(node.launch_round())
         if len(state["hs"]) > args.lag:
             node.complete_round(state["hs"].popleft())

@@ -27,6 +27,7 @@ transmuxes what was delivered and answers each player with one batch.
 """
 from __future__ import annotations
 
+import collections
 import logging
 import os
 import time
@@ -312,6 +313,9 @@ class FleetServer:
         self.ready: set = set()
         self.requests = [0] * len(self.conns)
         self.sent = 0
+        # requests wait here until admitted: at most `per_player` per player and round, so
+        # each player advances at the same pace on every rank and the swarm shares its slice
+        self._queued: List[collections.deque] = [collections.deque() for _ in self.conns]
         self.batches_sent = [0] * len(self.conns)  # answer batches sent to each player ...
         self.batches_done = [0] * len(self.conns)  # ... and handled by it (reported back)
 
@@ -328,22 +332,24 @@ class FleetServer:
                     msg = conn.recv()
                     kind = msg[0]
                     if kind == "req":
-                        by_rid = self._by_rid[w]
-                        for rid, key, url, headers, aes_key, iv in msg[1]:
-                            p = _Pending(self, w, rid, aes_key, iv)
-                            by_rid[rid] = p
-                            p.req = node.request(key, url, headers, p)
-                            n += 1
+                        self._queued[w].extend(msg[1])
+                        n += len(msg[1])
                         self.requests[w] += len(msg[1])
                         self.batches_done[w] = msg[2]
                     elif kind == "ack":
                         self.batches_done[w] = msg[1]
                     elif kind == "abort":
                         by_rid = self._by_rid[w]
+                        aborted = set()
                         for rid in msg[1]:
                             p = by_rid.pop(rid, None)
                             if p is not None and p.req is not None:
                                 p.req.abort()
+                            elif p is None:
+                                aborted.add(rid)
+                        if aborted:  # not handed to the node yet
+                            q = self._queued[w]
+                            self._queued[w] = collections.deque(r for r in q if r[0] not in aborted)
                     elif kind == "evict":
                         node.store.evict_below(msg[1], msg[2])
                     elif kind == "flags":
@@ -357,6 +363,23 @@ class FleetServer:
                         break
             except (EOFError, OSError):
                 self.open[w] = False
+        return n
+
+    def admit(self, per_player: int) -> int:
+        """Hand up to ``per_player`` queued requests of every player to the node (call right
+        before the node's round)."""
+        node = self.node
+        n = 0
+        for w, q in enumerate(self._queued):
+            if not q:
+                continue
+            by_rid = self._by_rid[w]
+            for _ in range(min(per_player, len(q))):
+                rid, key, url, headers, aes_key, iv = q.popleft()
+                p = _Pending(self, w, rid, aes_key, iv)
+                by_rid[rid] = p
+                p.req = node.request(key, url, headers, p)
+                n += 1
         return n
 
     # -------------------------------------------------------------- outbound
