@@ -10,7 +10,7 @@ swarm peer; every fragment runs the full public API path:
     ->  onProgress/onSuccess  ->  FRAG_LOADED  ->  batched AES-128-CBC decrypt + TS demux
     ->  buffer append  ->  FRAG_BUFFERED
 
-By default each GPU serves ``--players`` (3) player processes ("fleet", parallel/fleet.py):
+By default each GPU serves ``--players`` (4) player processes ("fleet", parallel/fleet.py):
 each runs the bundle player above its ``PeerAgent`` over a ``RemoteNode`` and plays its
 own slice of the DVR window, while the rank process runs the node rounds and the GPU
 transmux for all of them (the players never touch the GPU).  ``--players 0`` runs one
@@ -89,7 +89,7 @@ def parse():
     p.add_argument("--no-gc-tune", action="store_true", help="keep Python's default GC settings")
     p.add_argument("--metrics-port", type=int, default=None,
                    help="serve Prometheus GET /metrics on port + rank while the bench runs (idle unless scraped)")
-    p.add_argument("--players", type=int, default=3,
+    p.add_argument("--players", type=int, default=4,
                    help="fleet mode: this many player processes per GPU feed the node (each plays its own "
                         "slice of the DVR window with --inflight fragments per step; parallel/fleet.py); 0 = "
                         "one player in the node's process")

@@ -100,13 +100,13 @@ def test_bench_two_ranks_abr_ladder_with_churn():
 
 def test_bench_eight_ranks_driver_shape():
     """The driver's N=8 launch (torchrun, 8 ranks, one bench.py each) rehearsed on CPU with
-    gloo: shared-memory control plane across 8 processes with 3 player processes each,
+    gloo: shared-memory control plane across 8 processes with 4 player processes each,
     segments fetched from the CDN once and forwarded to the 7 other peers (offload ~7/8),
     no errors."""
-    res = _bench_cpu(_free_port(), nproc=8, config="hostcost-micro")  # the default: 3 player processes per rank
+    res = _bench_cpu(_free_port(), nproc=8, config="hostcost-micro")  # the default: 4 player processes per rank
     assert res["n_gpus"] == 8 and res["errors"] == 0
-    assert res["config"]["players_per_gpu"] == 3 and res["config"]["player_processes"]
-    assert res["config"]["global_batch"] == 8 * 3 * 8 and res["config"]["parallelism"] == "swarm8-gloo"
+    assert res["config"]["players_per_gpu"] == 4 and res["config"]["player_processes"]
+    assert res["config"]["global_batch"] == 8 * 4 * 8 and res["config"]["parallelism"] == "swarm8-gloo"
     # players are not in lockstep across ranks: a few segments are fetched from the CDN by a
     # second rank (a player that reached them after the window mark), so offload is ~7/8
     assert 0.75 < res["offload_ratio"] <= 0.9
