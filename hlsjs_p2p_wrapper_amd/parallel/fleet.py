@@ -128,14 +128,17 @@ class RemoteNode:
 
     # -------------------------------------------------------------- SwarmNode surface
     def attach(self, agent: Any) -> None:
+        """Register the player's PeerAgent (as on a SwarmNode)."""
         self._agents.append(agent)
 
     def detach(self, agent: Any) -> None:
+        """Unregister an agent."""
         if agent in self._agents:
             self._agents.remove(agent)
 
     @property
     def download_on(self) -> bool:
+        """Read / write: P2P download, forwarded to the node."""
         return self._down
 
     @download_on.setter
@@ -145,6 +148,7 @@ class RemoteNode:
 
     @property
     def upload_on(self) -> bool:
+        """Read / write: P2P upload, forwarded to the node."""
         return self._up
 
     @upload_on.setter
@@ -153,6 +157,8 @@ class RemoteNode:
         self._out.append(("flags", self._down, self._up))
 
     def request(self, key, url: str, headers, callbacks: Any, agent: Any = None, view: Any = None):
+        """Queue a fragment request for the node (sent at the next flush); ``view`` finds the
+        fragment's AES key / IV for the GPU transmux.  Returns the handle (``abort()``)."""
         rid = self._next
         self._next += 1
         req = _RemoteRequest(self, rid, key, callbacks, agent)
@@ -169,9 +175,11 @@ class RemoteNode:
         return req
 
     def prefetch(self, key, url: str, headers=None) -> bool:
+        """Agent-driven prefetch is a single-process feature: nothing is issued."""
         return False  # agent-driven prefetch stays a single-process feature
 
     def swarm_offload_ratio(self) -> float:
+        """P2P / (P2P + CDN) bytes over the whole swarm, as last reported by the node."""
         c, p = self.swarm_stats["cdn"], self.swarm_stats["p2p"]
         return p / (p + c) if (p + c) else 0.0
 
@@ -257,6 +265,7 @@ class RemoteNode:
         return n
 
     def close(self) -> None:
+        """Flush and tell the node this player is leaving."""
         if not self.closed:
             self.closed = True
             try:

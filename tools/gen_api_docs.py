@@ -43,6 +43,9 @@ SURFACE = [
     ("xhrSetup sandbox", "hlsjs_p2p_wrapper_amd.utils.xhr", "extractInfoFromXhrSetup"),
     ("Statics", "hlsjs_p2p_wrapper_amd.utils.statics", "inheritStaticPropertiesReadOnly"),
     ("Metrics", "hlsjs_p2p_wrapper_amd.utils.metrics", "MetricsServer"),
+    ("Fleet (player processes per GPU)", "hlsjs_p2p_wrapper_amd.parallel.fleet", "FleetServer"),
+    ("Fleet (player processes per GPU)", "hlsjs_p2p_wrapper_amd.parallel.fleet", "RemoteNode"),
+    ("Fleet (player processes per GPU)", "hlsjs_p2p_wrapper_amd.parallel.fleet", "player_main"),
     ("Network CDN", "hlsjs_p2p_wrapper_amd.net.http", "enable_network"),
     ("Network CDN", "hlsjs_p2p_wrapper_amd.net.network", "HttpOrigin"),
     ("Checkpoint", "hlsjs_p2p_wrapper_amd.agent.checkpoint", "save_cache"),
