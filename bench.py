@@ -115,17 +115,84 @@ def _numa(mode: str, dev: int):
     return f"remote-of-{node}"
 
 
+def _workload(args):
+    """The synthetic stream and player settings (no GPU needed: fleet players are spawned
+    from them before this process touches the GPU)."""
+    from hlsjs_p2p_wrapper_amd.net.origin import PRESET_1080P_6M, PRESET_4K_25M, PRESET_ABR5, Rendition
+
+    preset, encrypted, seg_dur, desc = CONFIGS[args.config]
+    rends = {"1080p": PRESET_1080P_6M, "4k": PRESET_4K_25M, "abr5": PRESET_ABR5,
+             "tiny": [Rendition(60_000, 320, 180, name="180p")],
+             "micro": [Rendition(8_000, 160, 90, name="90p")],
+             "tiny-abr": [Rendition(20_000 * (i + 1), 160 * (i + 1), 90 * (i + 1), name=f"t{i}")
+                          for i in range(5)]}[preset]
+    K = args.inflight
+    n_segments = (args.warmup + args.steps + 4) * K
+    W = max(0, args.players)
+    origin_kwargs = dict(base_url="http://cdn.bench/live/", renditions=rends,
+                         num_segments=n_segments * max(1, W) + (16 * K if W else 0),
+                         segment_duration=seg_dur, encrypted=encrypted, pool_size=args.pool, seed=7)
+    depth = 1 if args.sync_steps else args.lag + 2  # rounds a fragment spends in flight (see step())
+    hls_config = {"maxFragLoadsInFlight": K * depth, "maxBufferLength": 1e9, "maxMaxBufferLength": 1e9,
+                  "startPosition": 0, "fragLoadingTimeOut": 600_000, "tickInterval": 1e9}
+    if preset != "abr5":
+        hls_config["startLevel"] = 0
+    p2p_base = {"streamrootKey": "bench", "contentId": "bench-1080p"}
+    return preset, encrypted, seg_dur, desc, K, n_segments, W, origin_kwargs, hls_config, p2p_base
+
+
+def _spawn_players(W, world, rank, origin_kwargs, hls_config, p2p_base, n_segments, seg_dur):
+    """Start the fleet's player processes (spawn: fresh interpreters that never open the GPU;
+    started before this process initialises it)."""
+    import multiprocessing as mp
+
+    from hlsjs_p2p_wrapper_amd.parallel.fleet import player_main
+
+    ctx = mp.get_context("spawn")
+    conns, procs = [], []
+    saved = {k: os.environ.get(k) for k in ("HIP_VISIBLE_DEVICES", "CUDA_VISIBLE_DEVICES")}
+    os.environ["HIP_VISIBLE_DEVICES"] = os.environ["CUDA_VISIBLE_DEVICES"] = "-1"
+    try:
+        for w in range(W):
+            parent, child = ctx.Pipe()
+            spec = {"origin": dict(origin_kwargs, pin_memory=False),
+                    "hls_config": dict(hls_config, startPosition=w * n_segments * seg_dur),
+                    "p2p_config": dict(p2p_base), "world": world, "rank": rank}
+            pr = ctx.Process(target=player_main, args=(child, spec), daemon=True, name=f"hlsp2p-player{w}")
+            pr.start()
+            child.close()
+            conns.append(parent)
+            procs.append(pr)
+    finally:
+        for k, v in saved.items():
+            if v is None:
+                os.environ.pop(k, None)
+            else:
+                os.environ[k] = v
+    return conns, procs
+
+
 def main() -> int:
     args = parse()
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    (preset, encrypted, seg_dur, desc, K, n_segments, W, origin_kwargs, hls_config,
+     p2p_base) = _workload(args)
+    players = _spawn_players(W, world, rank, origin_kwargs, hls_config, p2p_base, n_segments, seg_dur) \
+        if W else None
     use_gpu = torch.cuda.is_available() and not args.cpu
     if use_gpu:
         local_dev = local_rank % torch.cuda.device_count()  # rehearsals may share one GPU
         torch.cuda.set_device(local_dev)
         device = torch.device("cuda", local_dev)
         numa_node = _numa(args.numa, local_dev)  # before the pinned CDN buffers are allocated
+        if players is not None and numa_node is not None:  # the players run next to their node
+            for pr in players[1]:
+                try:
+                    os.sched_setaffinity(pr.pid, os.sched_getaffinity(0))
+                except OSError:
+                    pass
     else:
         device = torch.device("cpu")
         numa_node = None
@@ -139,43 +206,24 @@ def main() -> int:
     from hlsjs_p2p_wrapper_amd import Hls
     from hlsjs_p2p_wrapper_amd.agent import node_for_config
     from hlsjs_p2p_wrapper_amd.net import new_event_loop
-    from hlsjs_p2p_wrapper_amd.net.origin import (PRESET_1080P_6M, PRESET_4K_25M, PRESET_ABR5, Rendition,
-                                                SyntheticHlsOrigin)
+    from hlsjs_p2p_wrapper_amd.net.origin import SyntheticHlsOrigin
     from hlsjs_p2p_wrapper_amd.player import MediaElement
     from hlsjs_p2p_wrapper_amd.player.transmux import pipeline_for
 
-    preset, encrypted, seg_dur, desc = CONFIGS[args.config]
-    rends = {"1080p": PRESET_1080P_6M, "4k": PRESET_4K_25M, "abr5": PRESET_ABR5,
-             "tiny": [Rendition(60_000, 320, 180, name="180p")],
-             "micro": [Rendition(8_000, 160, 90, name="90p")],
-             "tiny-abr": [Rendition(20_000 * (i + 1), 160 * (i + 1), 90 * (i + 1), name=f"t{i}")
-                          for i in range(5)]}[preset]
-    K = args.inflight
-    total_steps = args.warmup + args.steps
-    n_segments = (total_steps + 4) * K
-    W = max(0, args.players)
-    origin_kwargs = dict(base_url="http://cdn.bench/live/", renditions=rends,
-                         num_segments=n_segments * max(1, W) + (16 * K if W else 0),
-                         segment_duration=seg_dur, encrypted=encrypted, pool_size=args.pool, seed=7)
     loop = new_event_loop("real")
     t_pack = time.perf_counter()
     origin = SyntheticHlsOrigin(**origin_kwargs, pin_memory=use_gpu)
     t_pack = time.perf_counter() - t_pack
-    p2p_config = {"streamrootKey": "bench", "contentId": "bench-1080p",
+    p2p_config = {**p2p_base,
                   "gpuSwarm": {"backend": "dist" if world > 1 else "local", "device": str(device),
                                "cacheBytes": int(args.cache_gb * (1 << 30)), "autoTick": False,
                                "cdnDedup": not args.no_dedup, "maxWantsPerRound": K}}
     if args.metrics_port is not None:
         p2p_config["gpuSwarm"]["metricsPort"] = args.metrics_port
     node = node_for_config(p2p_config)
-    depth = 1 if args.sync_steps else args.lag + 2  # rounds a fragment spends in flight (see step())
-    hls_config = {"maxFragLoadsInFlight": K * depth, "maxBufferLength": 1e9, "maxMaxBufferLength": 1e9,
-                  "startPosition": 0, "fragLoadingTimeOut": 600_000, "tickInterval": 1e9}
-    if preset != "abr5":
-        hls_config["startLevel"] = 0
     if W:
-        return _fleet(args, world, rank, device, use_gpu, node, origin, origin_kwargs, p2p_config, hls_config,
-                      n_segments, seg_dur, desc, encrypted, numa_node, dist, t_pack)
+        return _fleet(args, world, rank, device, use_gpu, node, origin, players, desc, encrypted, seg_dur,
+                      numa_node, dist, t_pack)
     hls = Hls(hls_config, p2p_config)
     media = MediaElement(mode="drain", loop=loop)
     counters = {"buffered": 0, "errors": 0, "level_switches": 0}
@@ -325,8 +373,8 @@ def main() -> int:
     return 0
 
 
-def _fleet(args, world, rank, device, use_gpu, node, origin, origin_kwargs, p2p_config, hls_config, n_segments,
-           seg_dur, desc, encrypted, numa_node, dist, t_pack):
+def _fleet(args, world, rank, device, use_gpu, node, origin, players, desc, encrypted, seg_dur, numa_node, dist,
+           t_pack):
     """Fleet mode (``--players W``): W player processes per GPU, each playing its own slice of
     the DVR window through the bundle ``Hls`` over a ``RemoteNode``; this process runs the
     node (rounds, CDN DMA, RCCL, CRC) and the batched GPU transmux (``parallel/fleet.py``).
@@ -334,37 +382,14 @@ def _fleet(args, world, rank, device, use_gpu, node, origin, origin_kwargs, p2p_
     between two in-band marks sent at its edges (a mark follows every answer sent before it
     through the same pipe)."""
     import collections
-    import multiprocessing as mp
 
     from hlsjs_p2p_wrapper_amd.net.event_loop import get_event_loop
-    from hlsjs_p2p_wrapper_amd.parallel.fleet import FleetServer, player_main
+    from hlsjs_p2p_wrapper_amd.parallel.fleet import FleetServer
     from hlsjs_p2p_wrapper_amd.player.transmux import pipeline_for
     from hlsjs_p2p_wrapper_amd.utils.runtime import tune_gc
 
     W, K = args.players, args.inflight
-    ctx = mp.get_context("spawn")
-    conns, procs = [], []
-    # the players never touch the GPU: hide it from them (set only around the spawns)
-    saved = {k: os.environ.get(k) for k in ("HIP_VISIBLE_DEVICES", "CUDA_VISIBLE_DEVICES")}
-    os.environ["HIP_VISIBLE_DEVICES"] = os.environ["CUDA_VISIBLE_DEVICES"] = "-1"
-    try:
-        for w in range(W):
-            parent, child = ctx.Pipe()
-            spec = {"origin": dict(origin_kwargs, pin_memory=False),
-                    "hls_config": dict(hls_config, startPosition=w * n_segments * seg_dur),
-                    "p2p_config": {k: v for k, v in p2p_config.items() if k != "gpuSwarm"},
-                    "world": world, "rank": rank}
-            pr = ctx.Process(target=player_main, args=(child, spec), daemon=True, name=f"hlsp2p-player{w}")
-            pr.start()
-            child.close()
-            conns.append(parent)
-            procs.append(pr)
-    finally:
-        for k, v in saved.items():
-            if v is None:
-                os.environ.pop(k, None)
-            else:
-                os.environ[k] = v
+    conns, procs = players
     loop = get_event_loop()  # the node's loop: cache hits and failures are delivered from it
     pipe = pipeline_for(device, loop)
     pipe.auto_flush = False
