@@ -1,0 +1,132 @@
+"""Fleet internals (``parallel/fleet.py``) in one process: a player thread running
+``player_main`` over a pipe, the node side stepping a CPU ``SwarmNode`` with a
+``FleetServer`` (the bench runs the same pieces across processes)."""
+import collections
+import multiprocessing as mp
+import threading
+import time
+
+import pytest
+import torch
+
+from hlsjs_p2p_wrapper_amd.agent import node_for_config, set_current_node
+from hlsjs_p2p_wrapper_amd.net import clear_origins, new_event_loop
+from hlsjs_p2p_wrapper_amd.net.origin import Rendition, SyntheticHlsOrigin
+from hlsjs_p2p_wrapper_amd.parallel.fleet import FleetServer, RemoteNode, RemoteResult, RemoteSegment, player_main
+from hlsjs_p2p_wrapper_amd.player.transmux import pipeline_for
+
+ORIGIN = dict(base_url="http://fleet.test/live/", renditions=[Rendition(400_000, 320, 180)], num_segments=40,
+              segment_duration=4.0, encrypted=True, pool_size=6, seed=3)
+
+
+@pytest.fixture
+def node_side():
+    clear_origins()
+    set_current_node(None)
+    loop = new_event_loop("real")
+    SyntheticHlsOrigin(**ORIGIN, pin_memory=False)
+    node = node_for_config({"gpuSwarm": {"backend": "local", "device": "cpu", "cacheBytes": 64 << 20,
+                                         "autoTick": False}})
+    yield loop, node
+    node.close()
+    set_current_node(None)
+    clear_origins()
+
+
+def _serve(loop, node, conns, until, timeout_s=60.0):
+    pipe = pipeline_for(torch.device("cpu"), loop)
+    pipe.auto_flush = False
+    server = FleetServer(node, pipe, conns)
+    end = time.monotonic() + timeout_s
+    while len(server.ready) < len(conns):
+        server.poll()
+        time.sleep(0.002)
+        assert time.monotonic() < end, "players did not start"
+    for c in conns:
+        c.send(("go",))
+    hs, b = collections.deque(), None
+    while not until(server):
+        assert time.monotonic() < end, "fleet did not make progress"
+        while loop._ready:
+            loop.run_once(block=False)
+        server.await_players(timeout_s=0.005)
+        server.poll()
+        server.admit(4)
+        hs.append(node.launch_round())
+        if len(hs) > 1:
+            node.complete_round(hs.popleft())
+        nb = server.launch_transmux()
+        server.complete_transmux(b)
+        server.send()
+        b = nb
+    return server
+
+
+def _player_thread(conn, start_position, w):
+    spec = {"origin": dict(ORIGIN, pin_memory=False),
+            "hls_config": {"maxFragLoadsInFlight": 8, "maxBufferLength": 1e9, "maxMaxBufferLength": 1e9,
+                           "startPosition": start_position, "startLevel": 0, "tickInterval": 1e9},
+            "p2p_config": {"streamrootKey": "t", "contentId": "fleet-test"}, "world": 1, "rank": 0}
+    t = threading.Thread(target=player_main, args=(conn, spec), name=f"player{w}", daemon=True)
+    t.start()
+    return t
+
+
+def test_two_players_are_served_their_slices(node_side):
+    loop, node = node_side
+    pairs = [mp.Pipe() for _ in range(2)]
+    threads = [_player_thread(child, w * 60.0, w) for w, (_, child) in enumerate(pairs)]
+    conns = [parent for parent, _ in pairs]
+    server = _serve(loop, node, conns, lambda s: min(s.requests) >= 12 and s.sent >= 24)
+    for c in conns:
+        c.send(("mark", "end"))
+    end = time.monotonic() + 30
+    while len(server.marks.get("end", {})) < 2:
+        server.poll()
+        time.sleep(0.002)
+        assert time.monotonic() < end
+    marks = server.marks["end"]
+    assert all(m["buffered"] > 0 and m["errors"] == 0 for m in marks.values())
+    # each player fetched its own slice: 60 s apart -> disjoint segment keys on the node
+    assert node.stats["cdn_segments"] >= sum(m["buffered"] for m in marks.values())
+    for c in conns:
+        c.send(("stop",))
+    for t in threads:
+        t.join(10)
+        assert not t.is_alive()
+
+
+def test_remote_node_delivers_result_rows_and_errors():
+    a, b = mp.Pipe()
+    node = RemoteNode(a)
+    got = []
+
+    class Cb:
+        def onProgress(self, ev):  # noqa: N802
+            got.append(("progress", ev["cdnDownloaded"], ev["p2pDownloaded"]))
+
+        def onSuccess(self, data):  # noqa: N802
+            got.append(("ok", data))
+
+        def onError(self, err):  # noqa: N802
+            got.append(("err", err.status))
+
+    r1 = node.request((1, 0, 0, 5), "http://x/seg5.ts", None, Cb())
+    node.request((1, 0, 0, 6), "http://x/seg6.ts", None, Cb())
+    node.flush()
+    kind, reqs, handled = b.recv()
+    assert kind == "req" and [r[0] for r in reqs] == [0, 1] and handled == 0
+    row = [0] + [7] * 30
+    b.send(("done", [(r1.rid, 0, "p2p", 1000, 0.0, 2.5, row, 990), (1, 404, "", 0, 0.0, 0.0, None, 0)],
+            {"upload": 5, "swarm": {"cdn": 1, "p2p": 3, "upload": 0}, "online": [True, True]}))
+    assert node.poll(1.0) == 1
+    assert got[0] == ("progress", 0, 1000)
+    seg = got[1][1]
+    assert isinstance(seg, RemoteSegment) and seg.numel() == 1000
+    res = seg.transmux_result
+    assert isinstance(res, RemoteResult) and res["plain_bytes"] == 990 and res["info"]._row == row
+    assert res["video"].numel() == 0  # the elementary streams stay in the GPU process
+    assert got[2] == ("err", 404)
+    assert node.stats["p2p"] == 1000 and node.stats["upload"] == 5 and node.swarm_offload_ratio() == 0.75
+    node.flush()  # the handled batch is acknowledged even without new requests
+    assert b.recv() == ("ack", 1)
