@@ -130,3 +130,23 @@ def test_remote_node_delivers_result_rows_and_errors():
     assert node.stats["p2p"] == 1000 and node.stats["upload"] == 5 and node.swarm_offload_ratio() == 0.75
     node.flush()  # the handled batch is acknowledged even without new requests
     assert b.recv() == ("ack", 1)
+
+
+@pytest.mark.gpu
+def test_bench_fleet_on_the_gpu():
+    """``bench.py`` in its default fleet shape on one MI355X, tiny segments: the players are
+    served over pipes, the transmux runs on the GPU, every player's fragments are counted."""
+    import json
+    import os
+    import subprocess
+    import sys
+    from pathlib import Path
+
+    repo = Path(__file__).resolve().parents[1]
+    p = subprocess.run([sys.executable, str(repo / "bench.py"), "--config", "hostcost", "--players", "2",
+                        "--steps", "6", "--warmup", "2"], cwd=repo, capture_output=True, text=True, timeout=240,
+                       env=dict(os.environ, PYTHONPATH=str(repo)))
+    assert p.returncode == 0, p.stderr[-3000:]
+    res = json.loads([ln for ln in p.stdout.splitlines() if ln.startswith("{")][-1])
+    assert res["errors"] == 0 and res["value"] > 0
+    assert res["config"]["players_per_gpu"] == 2 and res["config"]["device"] == "MI355X"
