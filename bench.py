@@ -96,6 +96,11 @@ def parse():
     p.add_argument("--numa", default="auto", choices=["auto", "off", "remote"],
                    help="auto: run on (and first-touch pinned buffers from) the CPUs local to the GPU; "
                         "remote: the other socket's CPUs (diagnostic); off: leave the affinity alone")
+    p.add_argument("--ingest", default="pcie", choices=["pcie", "hbm"],
+                   help="pcie: the CDN origin is pinned host memory (the benchmark); hbm: DIAGNOSTIC, the "
+                        "origin's segment pools live in HBM, so CDN fetches are device-to-device copies "
+                        "standing in for segments that arrive over xGMI (the per-GPU ceiling at N=8 "
+                        "without the PCIe bound)")
     p.add_argument("--verbose", action="store_true")
     return p.parse_args()
 
@@ -213,6 +218,9 @@ def main() -> int:
     loop = new_event_loop("real")
     t_pack = time.perf_counter()
     origin = SyntheticHlsOrigin(**origin_kwargs, pin_memory=use_gpu)
+    if args.ingest == "hbm" and use_gpu:
+        for pool in origin.pools:
+            pool.data = pool.data.to(device)
     t_pack = time.perf_counter() - t_pack
     p2p_config = {**p2p_base,
                   "gpuSwarm": {"backend": "dist" if world > 1 else "local", "device": str(device),
@@ -559,7 +567,8 @@ def _result(args, world, tot, max_s, origin, K, desc, encrypted, seg_dur, use_gp
                                                      if world > 1 else ""),
                    "inflight_per_gpu": inflight, "players_per_gpu": max(1, players),
                    "player_processes": players > 0, "encrypted": encrypted, "segment_s": seg_dur,
-                   "churn_steps": args.churn, "device": "MI355X" if use_gpu else "cpu", "numa": numa_node},
+                   "churn_steps": args.churn, "device": "MI355X" if use_gpu else "cpu", "numa": numa_node,
+                   "ingest": args.ingest if use_gpu else "host"},
     }
 
 

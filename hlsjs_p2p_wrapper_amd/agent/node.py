@@ -989,9 +989,12 @@ def _h2d_batch(arena: torch.Tensor, dst_offs: np.ndarray, sources: List[Tuple[to
     from ..ops._native import device as _dev
 
     bases = []
+    on_dev = sources[0][0].is_cuda
     for d, _, _, _ in sources:
+        if d.is_cuda != on_dev:
+            raise RuntimeError("CDN origin buffers of one round must all be pinned host or all HBM")
         p = d.data_ptr()
-        if p not in _PINNED_OK:
+        if not on_dev and p not in _PINNED_OK:
             if not d.is_pinned():
                 raise RuntimeError("CDN origin buffers must be pinned host memory for the async H2D path")
             _PINNED_OK.add(p)
@@ -999,7 +1002,8 @@ def _h2d_batch(arena: torch.Tensor, dst_offs: np.ndarray, sources: List[Tuple[to
     src_alloc = np.asarray(bases, dtype=np.int64)
     src_ptrs = src_alloc + np.asarray([o for _, o, _, _ in sources], dtype=np.int64)
     lens = np.asarray([n for _, _, n, _ in sources], dtype=np.int64)
-    return _dev().h2d_batch(arena, np.ascontiguousarray(dst_offs, dtype=np.int64), src_ptrs, lens, src_alloc, ALIGN)
+    return _dev().h2d_batch(arena, np.ascontiguousarray(dst_offs, dtype=np.int64), src_ptrs, lens, src_alloc, ALIGN,
+                            on_dev)
 
 
 _PINNED_OK: set = set()  # base pointers of origin tensors already checked to be pinned

@@ -234,8 +234,11 @@ int64_t device_cus(Tensor t) { return num_cus(t); }
 // 192 MB copy moves at ~57 GB/s where 64 x 3 MB copies reach ~48 GB/s on MI355X.
 // A gap below the arena alignment is the previous entry's own padding (entries start on
 // aligned offsets), so a merged copy never touches another entry.  Returns #DMAs issued.
+// device_src: the sources are HBM (a diagnostic origin kept on the GPU, standing in for
+// segments that arrive over xGMI), so the copies are device-to-device.
 int64_t h2d_batch(Tensor dst, pybind11::array_t<int64_t> dst_off, pybind11::array_t<int64_t> src_ptr,
-                  pybind11::array_t<int64_t> len, pybind11::array_t<int64_t> src_alloc, int64_t max_gap) {
+                  pybind11::array_t<int64_t> len, pybind11::array_t<int64_t> src_alloc, int64_t max_gap,
+                  bool device_src) {
   check(dst, "dst", torch::kUInt8);
   const int64_t n = dst_off.size();
   TORCH_CHECK(src_ptr.size() == n && len.size() == n && src_alloc.size() == n, "h2d_batch: argument sizes differ");
@@ -263,7 +266,7 @@ int64_t h2d_batch(Tensor dst, pybind11::array_t<int64_t> dst_off, pybind11::arra
     }
     const int64_t bytes = o[j] + l[j] - o[i];
     ok(hipMemcpyAsync(base + o[i], reinterpret_cast<const void*>(s[i]), static_cast<size_t>(bytes),
-                      hipMemcpyHostToDevice, st),
+                      device_src ? hipMemcpyDeviceToDevice : hipMemcpyHostToDevice, st),
        "hipMemcpyAsync");
     ++issued;
     i = j + 1;
@@ -339,7 +342,9 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("table_lookup", &table_lookup);
   m.def("segment_copy", &segment_copy);
   m.def("device_cus", &device_cus);
-  m.def("h2d_batch", &h2d_batch);
+  m.def("h2d_batch", &h2d_batch, pybind11::arg("dst"), pybind11::arg("dst_off"), pybind11::arg("src_ptr"),
+        pybind11::arg("len"), pybind11::arg("src_alloc"), pybind11::arg("max_gap"),
+        pybind11::arg("device_src") = false);
   m.def("pack_h2d", &pack_h2d);
   register_rccl(m);
   register_transmux(m);

@@ -1,4 +1,4 @@
-# Validation with the fleet default: GPU tests, smoke, headline bench (default = 3 players)
+# Validation with the fleet default: GPU tests, smoke, headline bench (default = 4 players)
 # and single-process, host-bound probe, 2/4-rank rehearsals (gloo-staged data plane).
 set -e
 R=$GRAFT_REPO_ROOT
