@@ -63,8 +63,12 @@ _registry: Dict[str, Any] = {}
 _reg_lock = threading.Lock()
 # url -> (origin, path): every fragment URL is resolved at request (size) and again at
 # fetch time; the longest-prefix scan is done once per URL.  Cleared on any registry change.
-_resolved: Dict[str, Tuple[Any, str]] = {}
-_RESOLVED_MAX = 1 << 16
+# URL directory (everything up to the last "/") -> (origin, length of its base URL).  Base
+# URLs end with "/", so a base is a prefix of a URL iff it is a prefix of the URL's directory:
+# every URL of one directory resolves to the same origin, and the cache holds one entry per
+# playlist directory instead of one per segment URL.
+_resolved: Dict[str, Tuple[Any, int]] = {}
+_RESOLVED_MAX = 1 << 12
 
 
 def register_origin(base_url: str, origin: Any) -> None:
@@ -129,22 +133,24 @@ def _network_origin(url: str) -> Optional[Tuple[str, Any]]:
 
 
 def resolve(url: str) -> Tuple[Any, str]:
-    hit = _resolved.get(url)
+    """``(origin, path)`` for ``url``: the registered origin with the longest base-URL prefix
+    (or, with :func:`enable_network`, the host's :class:`~.network.HttpOrigin`)."""
+    d = url[:url.rfind("/") + 1]
+    hit = _resolved.get(d)
     if hit is not None:
-        return hit
+        return hit[0], url[hit[1]:]
     best = None
     for base, origin in list(_registry.items()):
-        if url.startswith(base) and (best is None or len(base) > len(best[0])):
+        if d.startswith(base) and (best is None or len(base) > len(best[0])):
             best = (base, origin)
     if best is None:
         best = _network_origin(url)
     if best is None:
         raise HttpError(0, url, f"no origin serves {url}")  # status 0 = network error
-    hit = (best[1], url[len(best[0]):])
     if len(_resolved) >= _RESOLVED_MAX:
         _resolved.clear()
-    _resolved[url] = hit
-    return hit
+    _resolved[d] = (best[1], len(best[0]))
+    return best[1], url[len(best[0]):]
 
 
 _RANGE = re.compile(r"bytes=(\d+)-(\d*)")

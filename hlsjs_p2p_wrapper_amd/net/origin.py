@@ -63,6 +63,23 @@ PRESET_ABR5 = [
 ]
 
 
+def _seg_path(path: str) -> Optional[Tuple[int, int]]:
+    """``(level, sn)`` of a canonical segment path ``[<a-h>/]r<level>/seg<sn>.ts`` without a
+    regex (one parse per fragment on the node's request path); None: use the regex."""
+    if not path.endswith(".ts"):
+        return None
+    slash = path.rfind("/")
+    if slash <= 0:
+        return None
+    name = path[slash + 1:-3]
+    start = path.rfind("/", 0, slash) + 1
+    lvl = path[start:slash]
+    if (name[:3] != "seg" or lvl[:1] != "r" or not name[3:].isdecimal() or not lvl[1:].isdecimal()
+            or not (start == 0 or (start == 2 and path[0] in "abcdefgh"))):
+        return None
+    return int(lvl[1:]), int(name[3:])
+
+
 @dataclass
 class _Pool:
     data: torch.Tensor              # pinned uint8
@@ -239,10 +256,12 @@ class SyntheticHlsOrigin:
         """(pinned tensor, offset, length, crc) of a segment, for zero-copy device fetches."""
         ls = self._paths.get(path)
         if ls is None:  # parse once per path (each is resolved at request and at fetch time)
-            m = self._SEG.search(path)
-            if not m:
-                raise HttpError(404, path)
-            ls = (int(m.group(1)), int(m.group(2)))
+            ls = _seg_path(path)
+            if ls is None:
+                m = self._SEG.search(path)
+                if not m:
+                    raise HttpError(404, path)
+                ls = (int(m.group(1)), int(m.group(2)))
             if len(self._paths) > 65536:
                 self._paths.clear()
             self._paths[path] = ls

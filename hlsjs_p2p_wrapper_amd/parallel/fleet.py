@@ -14,9 +14,11 @@ Protocol (one ``multiprocessing`` pipe per player process, batched per loop iter
   request as ``PeerAgent.getSegment`` issues it, plus the AES key / IV the GPU transmux
   needs; ``("abort", [rid, ...])``; ``("evict", swarm, sn)``; ``("flags", down, up)``;
   ``("mark", tag, counters)`` (bench window markers); ``("bye",)``.
-* node -> player: ``("done", [(rid, status, source, nbytes, cdn_ms, p2p_ms, info_row,
-  plain_bytes), ...], swarm_state)`` — ``status`` 0 = delivered (the transmux result rides
-  along), else the HTTP-like error status.
+* node -> player: ``("done", chunks, errors, swarm_state)``.  Each chunk holds the fragments of
+  one transmux batch as columns (numpy arrays, pickled as flat buffers): ``rid``, ``source``
+  code (:data:`SOURCES`), ``nbytes``, ``cdn_ms``, ``p2p_ms``, ``plain`` bytes, ``has_row`` and
+  the transmux info ``rows`` ``[n, INFO_WORDS]``.  ``errors``: ``[(rid, status), ...]`` with
+  the HTTP-like error status of requests the node could not serve.
 
 Player side, :class:`RemoteNode` stands in for the ``SwarmNode`` behind the unchanged
 ``PeerAgent`` (``gpuSwarm.backend = "remote"``): the loader's ``onSuccess`` gets a
@@ -38,6 +40,9 @@ import numpy as np
 from ..net.http import HttpError
 
 log = logging.getLogger("hlsjs_p2p_wrapper_amd.fleet")
+
+SOURCES = ("cdn", "p2p", "cache")  # source codes of the answer columns
+_SOURCE_CODE = {s: i for i, s in enumerate(SOURCES)}
 
 
 # ============================================================================ player side
@@ -210,9 +215,12 @@ class RemoteNode:
         while True:
             msg = conn.recv()
             if msg[0] == "done":
-                n += self._deliver(msg[1])
+                for chunk in msg[1]:
+                    n += self._deliver(chunk)
+                if msg[2]:
+                    self._fail(msg[2])
                 self.batches += 1
-                st = msg[2]
+                st = msg[3]
                 if st is not None:
                     self.stats["upload"] = st["upload"]
                     self.swarm_stats = st["swarm"]
@@ -223,13 +231,9 @@ class RemoteNode:
             if not conn.poll(0):
                 return n
 
-    def _deliver(self, rows: List[tuple]) -> int:
-        from ..player.transmux import InfoRow
-
+    def _fail(self, errors: List[Tuple[int, int]]) -> None:
         pending = self._pending
-        stats = self.stats
-        n = 0
-        for rid, status, source, nbytes, cdn_ms, p2p_ms, info, plain in rows:
+        for rid, status in errors:
             req = pending.pop(rid, None)
             if req is None:
                 continue
@@ -238,11 +242,29 @@ class RemoteNode:
                 continue
             req.done = True
             cb = req.callbacks
-            if status:
-                on_error = cb.get("onError") if isinstance(cb, dict) else getattr(cb, "onError", None)
-                if on_error is not None:
-                    on_error(HttpError(status, ""))
+            on_error = cb.get("onError") if isinstance(cb, dict) else getattr(cb, "onError", None)
+            if on_error is not None:
+                on_error(HttpError(status, ""))
+
+    def _deliver(self, chunk: tuple) -> int:
+        from ..player.transmux import InfoRow
+
+        rid_a, src_a, nbytes_a, cdn_a, p2p_a, plain_a, has_a, rows_a = chunk
+        pending = self._pending
+        stats = self.stats
+        n = 0
+        for rid, code, nbytes, cdn_ms, p2p_ms, plain, has, info in zip(
+                rid_a.tolist(), src_a.tolist(), nbytes_a.tolist(), cdn_a.tolist(), p2p_a.tolist(),
+                plain_a.tolist(), has_a.tolist(), rows_a.tolist()):
+            req = pending.pop(rid, None)
+            if req is None:
                 continue
+            self.inflight -= 1
+            if req.aborted:
+                continue
+            req.done = True
+            cb = req.callbacks
+            source = SOURCES[code]
             stats[source] = stats.get(source, 0) + nbytes
             stats["segments"] += 1
             if req.agent is not None:
@@ -251,12 +273,14 @@ class RemoteNode:
                 on_progress, on_success = cb.get("onProgress"), cb.get("onSuccess")
             else:
                 on_progress, on_success = getattr(cb, "onProgress", None), getattr(cb, "onSuccess", None)
-            p2p = source in ("p2p", "cache")
+            p2p = code != 0
             if on_progress is not None:
                 on_progress({"cdnDownloaded": 0 if p2p else nbytes, "p2pDownloaded": nbytes if p2p else 0,
                              "cdnDuration": 0.0 if p2p else cdn_ms, "p2pDuration": p2p_ms if p2p else 0.0})
             if req.aborted or on_success is None:
                 continue
+            if not has:
+                info = None
             r = RemoteResult(status=int(info[0]) if info else -1, info=InfoRow(info), plain_bytes=plain)
             if plain < 0:
                 r["error"] = ValueError("decryption failed (bad PKCS#7 padding)")
@@ -303,8 +327,7 @@ class _Pending:
         self.server._delivered.append((self, data))
 
     def onError(self, err: Any) -> None:  # noqa: N802
-        self.server._outbox[self.w].append((self.rid, int(getattr(err, "status", 0) or 0) or 500, "", 0, 0.0,
-                                            0.0, None, 0))
+        self.server._errors[self.w].append((self.rid, int(getattr(err, "status", 0) or 0) or 500))
 
 
 class FleetServer:
@@ -317,7 +340,8 @@ class FleetServer:
         self.open = [True] * len(self.conns)
         self._by_rid: List[Dict[int, _Pending]] = [{} for _ in self.conns]
         self._delivered: List[Tuple[_Pending, Any]] = []
-        self._outbox: List[List[tuple]] = [[] for _ in self.conns]
+        self._chunks: List[List[tuple]] = [[] for _ in self.conns]  # answer columns per player
+        self._errors: List[List[Tuple[int, int]]] = [[] for _ in self.conns]
         self.marks: Dict[Any, Dict[int, Any]] = {}
         self.ready: set = set()
         self.requests = [0] * len(self.conns)
@@ -405,12 +429,29 @@ class FleetServer:
         return pipe.launch()
 
     def complete_transmux(self, batch) -> None:
-        """Wait for a launched transmux batch; the info rows go into the outboxes as they are."""
-        outbox, by_rid = self._outbox, self._by_rid
-        for job, row, plain in self.pipe.complete_rows(batch):
+        """Wait for a launched transmux batch; its info rows go to the players as columns."""
+        jobs, rows, plain, has = self.pipe.complete_arrays(batch)
+        if not jobs:
+            return
+        by_rid = self._by_rid
+        per: Dict[int, List[Tuple[int, _Pending]]] = {}
+        for i, job in enumerate(jobs):
             p = job.frag
             by_rid[p.w].pop(p.rid, None)
-            outbox[p.w].append((p.rid, 0, p.source, p.nbytes, p.cdn_ms, p.p2p_ms, row, plain))
+            c = per.get(p.w)
+            if c is None:
+                c = per[p.w] = []
+            c.append((i, p))
+        code = _SOURCE_CODE
+        for w, c in per.items():
+            idx = np.fromiter([i for i, _ in c], dtype=np.int64, count=len(c))
+            self._chunks[w].append((
+                np.fromiter([p.rid for _, p in c], dtype=np.int64, count=len(c)),
+                np.fromiter([code[p.source] for _, p in c], dtype=np.int8, count=len(c)),
+                np.fromiter([p.nbytes for _, p in c], dtype=np.int64, count=len(c)),
+                np.fromiter([p.cdn_ms for _, p in c], dtype=np.float64, count=len(c)),
+                np.fromiter([p.p2p_ms for _, p in c], dtype=np.float64, count=len(c)),
+                plain[idx], has[idx], rows[idx]))
 
     def send(self) -> int:
         """One answer batch per player (plus the swarm state the agents' stats read)."""
@@ -419,16 +460,18 @@ class FleetServer:
                                                              {"cdn": 0, "p2p": 0, "upload": 0}),
               "online": np.asarray(node.peer_online, dtype=bool).tolist()}
         n = 0
-        for w, rows in enumerate(self._outbox):
-            if not rows or not self.open[w]:
+        for w in range(len(self.conns)):
+            chunks, errs = self._chunks[w], self._errors[w]
+            if not (chunks or errs) or not self.open[w]:
                 continue
             try:
-                self.conns[w].send(("done", rows, st))
-                n += len(rows)
+                self.conns[w].send(("done", chunks, errs, st))
+                n += sum(len(c[0]) for c in chunks) + len(errs)
                 self.batches_sent[w] += 1
             except (OSError, BrokenPipeError):
                 self.open[w] = False
-            self._outbox[w] = []
+            self._chunks[w] = []
+            self._errors[w] = []
         self.sent += n
         return n
 

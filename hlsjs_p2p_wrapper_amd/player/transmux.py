@@ -268,6 +268,32 @@ class MediaPipeline:
                 out[i] = (batch.jobs[i], None, -1)
         return out
 
+    def complete_arrays(self, batch: Optional["_Batch"]):
+        """Wait for a launched batch; return ``(jobs, rows, plain, has_row)``: the info rows as
+        one int64 array ``[n, INFO_WORDS]`` aligned with ``jobs``, the plaintext lengths, and
+        whether each job has a row (False: rejected before launch; its ``plain`` is -1).  The
+        columnar form a fleet node ships to its players without a Python object per word."""
+        if batch is None:
+            return [], None, None, None
+        n = len(batch.jobs)
+        rows = np.zeros((n, _ts.INFO_WORDS), dtype=np.int64)
+        plain = np.full(n, -1, dtype=np.int64)
+        has = np.zeros(n, dtype=bool)
+        if batch.error is not None:
+            return batch.jobs, rows, plain, has
+        t3 = time.perf_counter()
+        if batch.event is not None:
+            batch.event.synchronize()
+            self._free_events.append(batch.event)
+            batch.event = None
+        self.timer.add("wait_device", time.perf_counter() - t3)
+        for (idx, _res, _es_offs, _lens), (hinfo, hlens) in zip(batch.infos, batch.host):
+            k = len(idx)
+            rows[idx] = (hinfo.numpy() if isinstance(hinfo, torch.Tensor) else np.asarray(hinfo))[:k]
+            plain[idx] = (hlens.numpy() if isinstance(hlens, torch.Tensor) else np.asarray(hlens))[:k]
+            has[idx] = True
+        return batch.jobs, rows, plain, has
+
     def _complete(self, b: "_Batch") -> List[Dict[str, Any]]:
         tm = self.timer
         t3 = time.perf_counter()

@@ -6,13 +6,16 @@ import multiprocessing as mp
 import threading
 import time
 
+import numpy as np
 import pytest
 import torch
 
 from hlsjs_p2p_wrapper_amd.agent import node_for_config, set_current_node
 from hlsjs_p2p_wrapper_amd.net import clear_origins, new_event_loop
 from hlsjs_p2p_wrapper_amd.net.origin import Rendition, SyntheticHlsOrigin
-from hlsjs_p2p_wrapper_amd.parallel.fleet import FleetServer, RemoteNode, RemoteResult, RemoteSegment, player_main
+from hlsjs_p2p_wrapper_amd.ops.tsdemux import INFO_WORDS
+from hlsjs_p2p_wrapper_amd.parallel.fleet import (SOURCES, FleetServer, RemoteNode, RemoteResult, RemoteSegment,
+                                                  player_main)
 from hlsjs_p2p_wrapper_amd.player.transmux import pipeline_for
 
 ORIGIN = dict(base_url="http://fleet.test/live/", renditions=[Rendition(400_000, 320, 180)], num_segments=40,
@@ -116,8 +119,10 @@ def test_remote_node_delivers_result_rows_and_errors():
     node.flush()
     kind, reqs, handled = b.recv()
     assert kind == "req" and [r[0] for r in reqs] == [0, 1] and handled == 0
-    row = [0] + [7] * 30
-    b.send(("done", [(r1.rid, 0, "p2p", 1000, 0.0, 2.5, row, 990), (1, 404, "", 0, 0.0, 0.0, None, 0)],
+    row = [0] + [7] * (INFO_WORDS - 1)
+    chunk = (np.array([r1.rid]), np.array([SOURCES.index("p2p")], dtype=np.int8), np.array([1000]),
+             np.array([0.0]), np.array([2.5]), np.array([990]), np.array([True]), np.array([row], dtype=np.int64))
+    b.send(("done", [chunk], [(1, 404)],
             {"upload": 5, "swarm": {"cdn": 1, "p2p": 3, "upload": 0}, "online": [True, True]}))
     assert node.poll(1.0) == 1
     assert got[0] == ("progress", 0, 1000)
