@@ -316,15 +316,17 @@ class SwarmNode:
             net = (origin, path, rng)
         else:
             size = origin.size(path, url, rng)
-        w = _Want(key, url, headers, int(size or 0), self._next_want_id, prefetch=prefetch)
+        wid = self._next_want_id
+        self._next_want_id = wid + 1
+        w = _Want(key, url, headers, int(size or 0), wid, prefetch=prefetch)
         if net is not None:
             w.net = net
             w.staged = size is not None
             self._net_wants = True
+            w.encode()
         else:
             w.src = (origin, path, rng)
-        w.encode()
-        self._next_want_id += 1
+            w.row = key + (w.size, wid)  # encode() of a fresh, staged, not forced want
         return w
 
     def _stage(self, w: _Want) -> None:

@@ -268,7 +268,10 @@ class SyntheticHlsOrigin:
         level, sn = ls
         if level >= len(self.pools):
             raise HttpError(404, path)
-        if sn < self.first_sn() - (self.window if self.live else 0) or sn > self.live_edge() or sn < self.start_sn:
+        if self.live:
+            if sn < self.first_sn() - self.window or sn > self.live_edge() or sn < self.start_sn:
+                raise HttpError(404, path)
+        elif sn < self.start_sn or sn >= self.start_sn + (self.num_segments or 0):
             raise HttpError(404, path)
         pool = self.pools[level]
         i = sn % self.pool_size
