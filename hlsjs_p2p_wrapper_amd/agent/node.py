@@ -96,7 +96,7 @@ class _Want:
     class: one per request, and a dataclass ``__init__`` is interpreted code even here."""
 
     __slots__ = ("key", "url", "headers", "size", "want_id", "waiters", "force_cdn", "attempts", "round",
-                 "prefetch", "row", "net", "staged", "staging", "src")
+                 "prefetch", "row", "net", "staged", "staging", "src", "loc")
 
     def __init__(self, key: Tuple[int, int, int, int], url: str, headers: Dict[str, str], size: int,
                  want_id: int, waiters: Optional[List[Request]] = None, force_cdn: bool = False,
@@ -118,6 +118,7 @@ class _Want:
         self.staged = True
         self.staging = False
         self.src = None  # (origin, path, range) resolved at creation: the CDN phase reuses it
+        self.loc = None  # (host tensor, offset, length) when the origin's bytes never move (VOD)
 
     def __repr__(self) -> str:
         return f"_Want(key={self.key}, size={self.size}, want_id={self.want_id}, round={self.round})"
@@ -310,12 +311,14 @@ class SwarmNode:
         not staged yet, size 0 and ``staged=False`` (the planner then has it staged first)."""
         origin, path = http.resolve(url)
         rng = http.parse_range(headers) if headers else None
-        net = None
+        net = loc = None
         if getattr(origin, "staged_fetch", False):
             size = origin.staged_size(path, rng)
             net = (origin, path, rng)
         else:
-            size = origin.size(path, url, rng)
+            locate = getattr(origin, "locate", None)
+            loc = locate(path, url, rng) if locate is not None else None
+            size = loc[2] if loc is not None else origin.size(path, url, rng)
         wid = self._next_want_id
         self._next_want_id = wid + 1
         w = _Want(key, url, headers, int(size or 0), wid, prefetch=prefetch)
@@ -326,6 +329,7 @@ class SwarmNode:
             w.encode()
         else:
             w.src = (origin, path, rng)
+            w.loc = loc
             w.row = key + (w.size, wid)  # encode() of a fresh, staged, not forced want
         return w
 
@@ -714,6 +718,9 @@ class SwarmNode:
                     data, off, n, _ = origin.resource_range(path, rng)
                     corrupt = False
                     h.release.append(w)
+                elif w.loc is not None:  # VOD origin: located when the want was created
+                    data, off, n = w.loc
+                    corrupt = w.src[0].should_corrupt(w.src[1])
                 else:
                     if w.src is not None:
                         origin, path, rng = w.src

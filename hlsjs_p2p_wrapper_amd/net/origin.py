@@ -277,6 +277,22 @@ class SyntheticHlsOrigin:
         i = sn % self.pool_size
         return pool.data, pool.offsets[i], pool.lengths[i], pool.crcs[i]
 
+    def locate(self, path: str, url: str = "", rng=None) -> Optional[Tuple[torch.Tensor, int, int]]:
+        """``(pinned tensor, offset, length)`` of a segment's (ranged) bytes, resolved once
+        when the node creates the want: a VOD origin's pools never change, so the CDN phase
+        reuses it.  None for a live origin (its window moves: resolved again at fetch time)
+        and for non-segment paths.
+        Raises like :meth:`size`."""
+        if self.live or not path.endswith(".ts"):
+            return None
+        self._check_fail(path)
+        data, off, n, _ = self.resource(path)
+        if rng is not None:
+            s, e = rng
+            e = n - 1 if e is None else min(e, n - 1)
+            off, n = off + s, max(0, e - s + 1)
+        return data, off, n
+
     def size(self, path: str, url: str = "", rng=None) -> int:
         self._check_fail(path)
         if path.endswith(".ts"):
