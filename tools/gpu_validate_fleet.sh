@@ -12,6 +12,7 @@ timeout -k 10 300 python bench.py > $O/bench_default_1.log 2>&1
 timeout -k 10 300 python bench.py --players 0 > $O/bench_p0.log 2>&1
 timeout -k 10 300 python bench.py > $O/bench_default_2.log 2>&1
 timeout -k 10 300 python bench.py --config hostcost --steps 40 --warmup 6 --verbose > $O/hostcost_default.log 2>&1
+timeout -k 10 300 python bench.py --ingest hbm --steps 30 --warmup 5 --verbose > $O/hbm_default.log 2>&1
 for N in 2 4; do
   timeout -k 10 300 python -m torch.distributed.run --nnodes=1 --nproc-per-node $N --master-addr 127.0.0.1 \
     --master-port $((29830 + N)) bench.py --gpus $N --steps 10 --warmup 3 --dist-backend gloo --cache-gb 4 \
