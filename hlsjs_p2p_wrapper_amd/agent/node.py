@@ -907,6 +907,10 @@ class SwarmNode:
             if isinstance(cb, dict):
                 on_progress, on_success = cb.get("onProgress"), cb.get("onSuccess")
             else:
+                delivered = getattr(cb, "onDelivered", None)
+                if delivered is not None:  # one call instead of a progress event + onSuccess (fleet)
+                    delivered(c.source, c.nbytes, c.cdn_ms, c.p2p_ms, c.data)
+                    continue
                 on_progress, on_success = getattr(cb, "onProgress", None), getattr(cb, "onSuccess", None)
             if on_progress is not None:
                 p2p = c.source in ("p2p", "cache")

@@ -326,6 +326,15 @@ class _Pending:
     def onSuccess(self, data: Any) -> None:  # noqa: N802
         self.server._delivered.append((self, data))
 
+    def onDelivered(self, source: str, nbytes: int, cdn_ms: float, p2p_ms: float, data: Any) -> None:  # noqa: N802
+        """The node's one-call delivery (progress + success): cache hits count as P2P, as
+        the progress event reports them."""
+        if source == "cdn":
+            self.source, self.nbytes, self.cdn_ms = "cdn", nbytes, cdn_ms
+        else:
+            self.source, self.nbytes, self.p2p_ms = "p2p", nbytes, p2p_ms
+        self.server._delivered.append((self, data))
+
     def onError(self, err: Any) -> None:  # noqa: N802
         self.server._errors[self.w].append((self.rid, int(getattr(err, "status", 0) or 0) or 500))
 

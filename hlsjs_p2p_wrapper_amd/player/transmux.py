@@ -115,19 +115,22 @@ class MediaPipeline:
         self.timer.add("callbacks", time.perf_counter() - t)
 
     # ------------------------------------------------------------------ batch
-    def _stage(self, tensors: List[torch.Tensor]) -> Tuple[torch.Tensor, List[int]]:
+    def _stage(self, tensors: List[torch.Tensor], sizes: List[int]) -> Tuple[torch.Tensor, List[int]]:
         """One source buffer + offsets: in place when every payload is a view of the same
-        device storage (the HBM arena), otherwise one staging copy."""
+        device storage (the HBM arena), otherwise one staging copy.  Same-storage check: one
+        ``data_ptr()`` per payload, every view inside the first payload's allocation
+        (allocations never overlap), instead of a storage object per payload."""
         dev = self.device
-        if all(t.device == dev for t in tensors):
-            ptrs = [t.untyped_storage().data_ptr() for t in tensors]
-            if len(set(ptrs)) == 1:
-                base_t = tensors[0]
-                storage = base_t.untyped_storage()
-                base = torch.empty(0, dtype=torch.uint8, device=dev).set_(storage, 0, (storage.nbytes(),))
-                offs = [t.data_ptr() - ptrs[0] for t in tensors]
-                if all(o % 16 == 0 for o in offs):
-                    return base, offs
+        t0 = tensors[0]
+        if t0.device == dev:
+            cuda = dev.type == "cuda"
+            storage = t0.untyped_storage()
+            base_ptr, cap = storage.data_ptr(), storage.nbytes()
+            offs = [t.data_ptr() - base_ptr for t in tensors]
+            if all(o >= 0 and o + n <= cap and o % 16 == 0 and t.is_cuda == cuda
+                   for o, n, t in zip(offs, sizes, tensors)):
+                base = torch.empty(0, dtype=torch.uint8, device=dev).set_(storage, 0, (cap,))
+                return base, offs
         offs, pos = [], 0
         for t in tensors:
             offs.append(pos)
@@ -146,7 +149,7 @@ class MediaPipeline:
         self.batches += 1
         tm = self.timer
         t0 = time.perf_counter()
-        src, src_offs = self._stage(tensors)
+        src, src_offs = self._stage(tensors, sizes)
         t1 = time.perf_counter()
         tm.add("stage", t1 - t0)
         enc = [i for i, j in enumerate(jobs) if j.key is not None]
