@@ -311,3 +311,32 @@ def test_live_window_eviction():
     assert len(keys) and keys[:, 3].min() >= agent._evicted_below and agent._evicted_below <= first
     hls.destroy()
     set_current_node(None)
+
+
+def test_origin_resolution_and_vod_locate():
+    """``http.resolve`` picks the longest registered base (cached per URL directory, so nested
+    bases keep working), and a VOD origin locates a (ranged) segment's bytes once."""
+    from hlsjs_p2p_wrapper_amd.net import http
+    from hlsjs_p2p_wrapper_amd.net.origin import _seg_path
+
+    clear_origins()
+    try:
+        outer = SyntheticHlsOrigin(base_url="http://nest.test/", renditions=[Rendition(100_000, 320, 180)],
+                                   num_segments=4, pin_memory=False)
+        inner = SyntheticHlsOrigin(base_url="http://nest.test/live/", renditions=[Rendition(100_000, 320, 180)],
+                                   num_segments=4, pin_memory=False)
+        for _ in range(2):  # second pass: from the directory cache
+            assert http.resolve("http://nest.test/live/r0/seg1.ts") == (inner, "r0/seg1.ts")
+            assert http.resolve("http://nest.test/r0/seg2.ts") == (outer, "r0/seg2.ts")
+            assert http.resolve("http://nest.test/live/r0/seg3.ts?tok=a/b") == (inner, "r0/seg3.ts?tok=a/b")
+        with pytest.raises(http.HttpError):
+            http.resolve("http://elsewhere.test/r0/seg1.ts")
+        assert _seg_path("a/r3/seg17.ts") == (3, 17) and _seg_path("x/a/r3/seg17.ts") is None
+        data, off, n, _ = inner.resource("r0/seg1.ts")
+        assert inner.locate("r0/seg1.ts") == (data, off, n)
+        assert inner.locate("r0/seg1.ts", rng=(10, 19))[1:] == (off + 10, 10)
+        assert inner.locate("r0/index.m3u8") is None
+        with pytest.raises(http.HttpError):
+            inner.locate("r0/seg4.ts")  # past the VOD's last segment
+    finally:
+        clear_origins()

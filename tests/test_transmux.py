@@ -58,3 +58,57 @@ def test_pipeline_results_match_oracle(device, request):
     # wrong key: bad padding (overwhelmingly likely) or garbage that fails demux
     bad = out["bad"]
     assert bad.get("error") is not None or bad["status"] != 0
+
+
+def _arena_jobs(device):
+    """Payloads as views of one arena (the swarm node's delivery form), 16-byte aligned."""
+    jobs = _batch()
+    offs, pos = [], 0
+    for _, payload, _, _ in jobs:
+        offs.append(pos)
+        pos += (len(payload) + 255) // 256 * 256
+    arena = torch.zeros(pos, dtype=torch.uint8, device=device)
+    for (_, payload, _, _), o in zip(jobs, offs):
+        arena[o:o + len(payload)] = torch.from_numpy(payload.copy()).to(device)
+    views = [arena[o:o + len(p)] for (_, p, _, _), o in zip(jobs, offs)]
+    return jobs, arena, views, offs
+
+
+@pytest.mark.parametrize("device", ["cpu", pytest.param("cuda", marks=pytest.mark.gpu)])
+def test_stage_uses_arena_views_in_place(device):
+    """Views of one allocation are staged without a copy (base = the arena storage, offsets =
+    the views' positions); a payload from another allocation forces the staging copy."""
+    _, arena, views, offs = _arena_jobs(device)
+    pipe = MediaPipeline(torch.device(device), new_event_loop("virtual"))
+    base, got = pipe._stage(views, [v.numel() for v in views])
+    assert base.data_ptr() == arena.data_ptr() and got == offs
+    other = torch.zeros(4096, dtype=torch.uint8, device=device)
+    mixed = views[:2] + [other]
+    base2, got2 = pipe._stage(mixed, [v.numel() for v in mixed])
+    assert base2.data_ptr() != arena.data_ptr() and got2[0] == 0
+    for v, o in zip(mixed, got2):
+        assert torch.equal(base2[o:o + v.numel()].cpu(), v.cpu())
+
+
+@pytest.mark.parametrize("device", ["cpu", pytest.param("cuda", marks=pytest.mark.gpu)])
+def test_complete_arrays_matches_per_job_results(device):
+    """The fleet's columnar completion (one info-row array per batch) carries the same rows
+    and plaintext lengths as the per-fragment results; a rejected job has no row."""
+    jobs, _, views, _ = _arena_jobs(device)
+    loop = new_event_loop("virtual")
+    ref = {}
+    pipe = MediaPipeline(torch.device(device), loop)
+    for n, ((_, _, key, iv), v) in enumerate(zip(jobs, views)):
+        pipe.submit(TransmuxJob(v, key, iv, lambda r, n=n: ref.__setitem__(n, r)))
+    pipe.flush()
+    pipe.auto_flush = False
+    subs = [TransmuxJob(v, key, iv, None, n) for n, ((_, _, key, iv), v) in enumerate(zip(jobs, views))]
+    subs.append(TransmuxJob(views[0][:100], bytes(16), bytes(16), None, "odd"))  # not a multiple of 16
+    for j in subs:
+        pipe.submit(j)
+    got_jobs, rows, plain, has = pipe.complete_arrays(pipe.launch())
+    assert [j.frag for j in got_jobs] == list(range(len(jobs))) + ["odd"]
+    assert rows.shape == (len(subs), tsdemux.INFO_WORDS)
+    for n in range(len(jobs)):
+        assert has[n] and rows[n].tolist() == ref[n]["info"]._row and plain[n] == ref[n]["plain_bytes"]
+    assert not has[-1] and plain[-1] == -1
