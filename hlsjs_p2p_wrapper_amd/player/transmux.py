@@ -67,6 +67,9 @@ def _align(n: int) -> int:
 class MediaPipeline:
     def __init__(self, device: torch.device, loop=None) -> None:
         self.device = torch.device(device)
+        if self.device.type == "cuda" and self.device.index is None:
+            # "cuda" != "cuda:0": an index-less device would fail the in-place staging check
+            self.device = torch.device("cuda", torch.cuda.current_device())
         self.loop = loop or get_event_loop()
         self._jobs: List[TransmuxJob] = []
         self._scheduled = False
