@@ -74,9 +74,10 @@ def parse():
     p.add_argument("--cache-gb", type=float, default=8.0, help="HBM segment-cache arena per GPU")
     p.add_argument("--no-dedup", action="store_true", help="disable CDN de-duplication (seeding)")
     p.add_argument("--cpu", action="store_true", help="CPU rehearsal (gloo, no GPU)")
-    p.add_argument("--dist-backend", default="auto", choices=["auto", "nccl", "gloo"],
+    p.add_argument("--dist-backend", default="auto", choices=["auto", "nccl", "gloo", "ipc"],
                    help="data-plane backend for N>1 (auto: nccl = RCCL on GPUs; gloo stages GPU "
-                        "tensors through host memory: multi-rank rehearsal on a single GPU)")
+                        "tensors through host memory; ipc: gloo control with device-to-device "
+                        "HIP-IPC outboxes -- both are multi-rank rehearsals on a single GPU)")
     p.add_argument("--sync-steps", action="store_true",
                    help="no software pipelining: each step = load, round, transmux, synchronously")
     p.add_argument("--lag", type=int, default=2,
@@ -206,6 +207,9 @@ def main() -> int:
     if world > 1:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         backend = args.dist_backend if args.dist_backend != "auto" else ("nccl" if use_gpu else "gloo")
+        if backend == "ipc":  # rehearsal data plane (parallel/comm.py:_IpcOutbox) on a gloo group
+            os.environ["HLSP2P_DATA_PLANE"] = "ipc"
+            backend = "gloo"
         dist.init_process_group(backend, device_id=device if (use_gpu and backend == "nccl") else None)
 
     from hlsjs_p2p_wrapper_amd import Hls
@@ -228,6 +232,11 @@ def main() -> int:
                                "cdnDedup": not args.no_dedup, "maxWantsPerRound": K}}
     if args.metrics_port is not None:
         p2p_config["gpuSwarm"]["metricsPort"] = args.metrics_port
+    if os.environ.get("HLSP2P_DATA_PLANE") == "ipc" and world > 1:
+        # rehearsal outbox (fixed size): a rank forwards at most every peer's wants of a round
+        seg = max(max(pool.lengths) for pool in origin.pools)
+        per_round = (world - 1) * K * max(1, W) * (seg + 512) + (1 << 20)
+        os.environ.setdefault("HLSP2P_IPC_OUTBOX_BYTES", str(per_round))
     node = node_for_config(p2p_config)
     if W:
         return _fleet(args, world, rank, device, use_gpu, node, origin, players, desc, encrypted, seg_dur,
@@ -364,7 +373,8 @@ def main() -> int:
     else:
         tot, max_ns = vals, int(vals[3])
     max_s = max_ns / 1e9
-    result = _result(args, world, tot, max_s, origin, K, desc, encrypted, seg_dur, use_gpu, numa_node, dist)
+    result = _result(args, world, tot, max_s, origin, K, desc, encrypted, seg_dur, use_gpu, numa_node, dist,
+                     transport=getattr(node.comm, "data_transport", None))
     if args.verbose:
         print(f"# rank {rank} pack {t_pack:.2f}s counters {counters} level {hls.currentLevel}\n"
               f"#   node stats {node.stats} last round {node.last_round}\n"
@@ -513,7 +523,7 @@ def _fleet(args, world, rank, device, use_gpu, node, origin, players, desc, encr
         else:
             tot, max_ns = vals, int(vals[3])
         result = _result(args, world, tot, max_ns / 1e9, origin, K, desc, encrypted, seg_dur, use_gpu, numa_node,
-                         dist, players=W)
+                         dist, players=W, transport=getattr(node.comm, "data_transport", None))
         if args.verbose:
             print(f"# rank {rank} pack {t_pack:.2f}s players {W} marks {dict(m1)}\n"
                   f"#   node stats {node.stats} last round {node.last_round}\n"
@@ -540,7 +550,8 @@ def _fleet(args, world, rank, device, use_gpu, node, origin, players, desc, encr
     return 0
 
 
-def _result(args, world, tot, max_s, origin, K, desc, encrypted, seg_dur, use_gpu, numa_node, dist, players=0):
+def _result(args, world, tot, max_s, origin, K, desc, encrypted, seg_dur, use_gpu, numa_node, dist, players=0,
+            transport=None):
     """The JSON line (``tot``: [fragments buffered, cdn bytes, p2p bytes, ns, errors, segments]
     summed over ranks; ``max_s``: the slowest rank's timed window)."""
     # bytes per delivered segment over the timed region (an ABR ladder mixes renditions)
@@ -563,13 +574,20 @@ def _result(args, world, tot, max_s, origin, K, desc, encrypted, seg_dur, use_gp
         "goodput_GBps": round(float(tot[1] + tot[2]) / max_s / 1e9, 3),  # bytes delivered to the players
         "errors": int(tot[4]),
         "config": {"model": desc, "global_batch": inflight * world, "seq_len": seg_bytes,
-                   "parallelism": f"swarm{world}" + (f"-{'rccl' if dist.get_backend() == 'nccl' else 'gloo'}"
-                                                     if world > 1 else ""),
+                   "parallelism": f"swarm{world}" + (f"-{_data_plane(dist, transport)}" if world > 1 else ""),
                    "inflight_per_gpu": inflight, "players_per_gpu": max(1, players),
                    "player_processes": players > 0, "encrypted": encrypted, "segment_s": seg_dur,
                    "churn_steps": args.churn, "device": "MI355X" if use_gpu else "cpu", "numa": numa_node,
                    "ingest": args.ingest if use_gpu else "host"},
     }
+
+
+def _data_plane(dist, transport) -> str:
+    """Label of the data plane the node's comm actually uses (an IPC request that could not
+    be honoured reports gloo)."""
+    if dist.get_backend() == "nccl":
+        return "rccl"
+    return "ipc" if transport == "hip-ipc" else "gloo"
 
 
 def _dump_profile(rank: int) -> None:

@@ -24,7 +24,10 @@ Backends:
   node's own RCCL communicator, one ``ncclGroupStart / ncclSend* / ncclRecv* /
   ncclGroupEnd`` call per round enqueued on the node stream, one contiguous buffer per peer
   pair), or with ``HLSP2P_NATIVE_RCCL=0`` through torch's ``batch_isend_irecv``; gloo in
-  CPU tests.  ``HLSP2P_CONTROL=gloo`` forces the gloo control plane.
+  CPU tests.  ``HLSP2P_CONTROL=gloo`` forces the gloo control plane.  With
+  ``HLSP2P_DATA_PLANE=ipc`` on a gloo group whose ranks share a host, GPU segment bytes move
+  device to device through HIP-IPC outboxes (:class:`_IpcOutbox`): the multi-rank
+  rehearsal on one MI355X, where RCCL refuses two ranks per device.
 """
 from __future__ import annotations
 
@@ -154,6 +157,10 @@ class DistComm(SwarmComm):
         self._shm = self._open_shm_control() if self.world_size > 1 else None
         self.control_transport = "shm" if self._shm is not None else "gloo"
         self._rccl = None
+        self._ipc: Optional[_IpcOutbox] = None
+        if (backend == "gloo" and os.environ.get("HLSP2P_DATA_PLANE", "") == "ipc" and self.world_size > 1
+                and torch.cuda.is_available()):
+            self._ipc = _IpcOutbox.open(self)
         if backend == "nccl" and torch.cuda.is_available():
             # batch_isend_irecv runs on the group's full communicator; when that is created
             # lazily every rank must take part in its first use.  Node construction is
@@ -164,7 +171,8 @@ class DistComm(SwarmComm):
             if os.environ.get("HLSP2P_NATIVE_RCCL", "1") != "0":
                 self._rccl = self._open_native_rccl()
         self.data_transport = ("rccl-native" if self._rccl is not None else
-                               "rccl-torch" if backend == "nccl" else backend)
+                               "rccl-torch" if backend == "nccl" else
+                               "hip-ipc" if self._ipc is not None else backend)
 
     def _open_native_rccl(self):
         """The node's own RCCL communicator (collective).  Every rank first reports whether
@@ -272,6 +280,9 @@ class DistComm(SwarmComm):
         if self._rccl is not None:
             self._exchange_native(sends, recvs)
             return
+        if self._ipc is not None:
+            self._ipc.exchange(sends, recvs)
+            return
         if self.data_backend == "gloo" and any(t.is_cuda for _, t in list(sends) + list(recvs)):
             self._exchange_staged(sends, recvs)
             return
@@ -311,6 +322,8 @@ class DistComm(SwarmComm):
             if torch.cuda.is_available():
                 torch.cuda.synchronize()
             self._rccl.abort()
+        if self._ipc is not None:
+            self._ipc.close()
 
     def _exchange_staged(self, sends, recvs) -> None:
         """gloo data plane with GPU tensors (several ranks sharing one GPU, e.g. rehearsing
@@ -343,3 +356,153 @@ class DistComm(SwarmComm):
             self._shm.barrier(self.control_timeout_s)
             return
         self.dist.barrier(group=self.control_group)
+
+
+def _as_bytes(t: torch.Tensor) -> torch.Tensor:
+    """A contiguous tensor's bytes as a flat uint8 view (no copy)."""
+    if not t.is_contiguous():
+        raise ValueError("IPC data plane needs contiguous tensors")
+    return t.reshape(-1).view(torch.uint8)
+
+
+class _IpcOutbox:
+    """Device-resident data plane for ranks that share one host but no RCCL communicator.
+
+    This is the multi-rank rehearsal on a single MI355X: RCCL refuses two ranks on one
+    device, and the gloo data plane stages every byte through host memory.  Here each rank
+    packs its sends into an HBM "outbox" that is exported once over HIP IPC (dmabuf).  Peers
+    copy their receives straight out of it, device to device, on their node stream, so the
+    rest of the round stays stream-ordered exactly as with RCCL.
+
+    Protocol, per exchange (collective, like an RCCL group):
+
+    1. Wait for this rank's receive copies of the previous exchange.  After that, no peer
+       can still be reading an outbox that is about to be rewritten.
+    2. All-gather the send tables ``[outbox bytes, n, (dst, nbytes) * n]`` (a round larger
+       than the fixed outbox fails on every rank).
+    3. Pack the sends into the outbox (256-byte aligned, in order), wait for the packing
+       copies, then barrier.
+    4. For the k-th receive from ``src``, copy the k-th of ``src``'s sends addressed to this
+       rank (two-sided, ordered, as RCCL point-to-point), then record an event for step 1.
+
+    Enabled with ``HLSP2P_DATA_PLANE=ipc`` on a gloo group (``bench.py --dist-backend
+    ipc``).  Every rank must be on the same host; otherwise every rank keeps gloo."""
+
+    ALIGN = 256
+
+    def __init__(self, comm: "DistComm") -> None:
+        self.comm = comm
+        self.cap = 0
+        self.buf: Optional[torch.Tensor] = None
+        self.peers: List[torch.Tensor] = []
+        self._pending = None
+        self.exchanges = 0
+
+    @classmethod
+    def open(cls, comm: "DistComm") -> Optional["_IpcOutbox"]:
+        dist, g = comm.dist, comm.control_group
+        try:
+            with open("/proc/sys/kernel/random/boot_id") as f:
+                boot = f.read().strip()
+        except OSError:
+            boot = ""
+        hosts: List[object] = [None] * comm.world_size
+        dist.all_gather_object(hosts, (socket.gethostname(), boot), group=g)
+        if any(h != hosts[0] for h in hosts):
+            return None
+        box = cls(comm)
+        ok = True
+        try:
+            box._share(int(os.environ.get("HLSP2P_IPC_OUTBOX_BYTES", str(1 << 30))))
+        except Exception:  # noqa: BLE001 - IPC unavailable on some rank: every rank keeps gloo
+            ok = False
+        flags: List[object] = [None] * comm.world_size
+        dist.all_gather_object(flags, ok, group=g)
+        return box if all(flags) else None
+
+    def _share(self, cap: int) -> None:
+        """Collective, once: allocate this rank's outbox and open every peer's.  The
+        capacity is fixed for the communicator's life: re-exporting a fresh allocation
+        while peers still map the old one proved unreliable (a peer could keep reading
+        through its cached mapping of the old handle), so a round that needs more fails
+        loudly instead (``HLSP2P_IPC_OUTBOX_BYTES``; ``bench.py`` sizes it from the
+        workload)."""
+        from torch.multiprocessing.reductions import reduce_tensor
+
+        comm = self.comm
+        cap = (max(cap, 1 << 20) + (1 << 20) - 1) // (1 << 20) * (1 << 20)
+        self.buf = torch.empty(cap, dtype=torch.uint8, device=torch.device("cuda", torch.cuda.current_device()))
+        torch.cuda.synchronize()
+        handle = reduce_tensor(self.buf)
+        handles: List[object] = [None] * comm.world_size
+        comm.dist.all_gather_object(handles, handle, group=comm.control_group)
+        me = comm.rank
+        self.peers = [self.buf if r == me else h[0](*h[1]) for r, h in enumerate(handles)]  # type: ignore[index]
+        self.cap = cap
+        comm.barrier()  # every rank holds every outbox before any is written
+
+    def exchange(self, sends, recvs) -> None:
+        comm = self.comm
+        if self._pending is not None:
+            self._pending.synchronize()
+            self._pending = None
+        A = self.ALIGN
+        sizes = [int(t.numel()) * t.element_size() for _, t in sends]
+        offs, pos = [], 0
+        for n in sizes:
+            offs.append(pos)
+            pos += (n + A - 1) // A * A
+        msg = np.empty(2 + 2 * len(sends), dtype=np.int64)
+        msg[0], msg[1] = pos, len(sends)
+        msg[2::2] = [d for d, _ in sends]
+        msg[3::2] = sizes
+        parts = comm.allgather_control(msg)
+        need = max(int(p[0]) for p in parts)
+        if need > self.cap:  # every rank sees the same tables: all raise together
+            raise RuntimeError(f"IPC outbox of {self.cap} bytes cannot hold a round of {need} bytes "
+                               "(raise HLSP2P_IPC_OUTBOX_BYTES)")
+        stream = torch.cuda.current_stream()
+        if sends:
+            buf = self.buf
+            for (_, t), o, n in zip(sends, offs, sizes):
+                if n:
+                    buf[o:o + n].copy_(_as_bytes(t), non_blocking=True)
+            stream.synchronize()
+        comm.barrier()  # every outbox is packed
+        me = comm.rank
+        mine: dict = {}  # src -> [(offset, nbytes)] of src's sends to this rank, in order
+        cursor: dict = {}
+        for src, t in recvs:
+            lst = mine.get(src)
+            if lst is None:
+                p = parts[src]
+                k = int(p[1])
+                dsts, lens = p[2:2 + 2 * k:2].tolist(), p[3:3 + 2 * k:2].tolist()
+                lst, o = [], 0
+                for d, n in zip(dsts, lens):
+                    if d == me:
+                        lst.append((o, n))
+                    o += (n + A - 1) // A * A
+                mine[src] = lst
+            i = cursor.get(src, 0)
+            if i >= len(lst):
+                raise RuntimeError(f"rank {me}: no matching send from {src}")
+            cursor[src] = i + 1
+            o, n = lst[i]
+            dst = _as_bytes(t)
+            if dst.numel() != n:
+                raise RuntimeError(f"rank {me}: size mismatch from {src}: {n} != {dst.numel()}")
+            if n:
+                dst.copy_(self.peers[src][o:o + n], non_blocking=True)
+        if recvs:
+            ev = torch.cuda.Event()
+            ev.record(stream)
+            self._pending = ev
+        self.exchanges += 1
+
+    def close(self) -> None:
+        if self._pending is not None:
+            self._pending.synchronize()
+            self._pending = None
+        self.peers = []
+        self.buf = None

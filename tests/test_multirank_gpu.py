@@ -1,6 +1,7 @@
 """multi-rank runs on the GPU box.  The pool's box has ONE MI355X and RCCL
 cannot place two ranks on one GPU, so two torchrun ranks share the card with a gloo data
-plane (GPU tensors staged through host memory).  Everything else is the production N>1
+plane (GPU tensors staged through host memory) or the HIP-IPC outbox data plane
+(device-to-device copies, ``parallel/comm.py:_IpcOutbox``).  Everything else is the production N>1
 path of bench.py: control all-gather, native planning, CDN seeding + same-round
 forwarding, per-pair buffers with CRC trailers verified on device, async rounds, batched
 decrypt + demux, FRAG_BUFFERED accounting."""
@@ -25,10 +26,13 @@ def _free_port() -> int:
 
 
 @pytest.mark.gpu
-def test_two_ranks_share_one_gpu_bench_path(cuda):
+@pytest.mark.parametrize("plane", ["gloo", "ipc"])
+def test_two_ranks_share_one_gpu_bench_path(cuda, plane):
+    """``gloo``: GPU tensors staged through host memory; ``ipc``: device-to-device copies out
+    of the peers' HIP-IPC outboxes (parallel/comm.py:_IpcOutbox)."""
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2", "--master-addr",
            "127.0.0.1", "--master-port", str(_free_port()), str(REPO / "bench.py"), "--gpus", "2", "--steps", "4",
-           "--warmup", "2", "--inflight", "16", "--pool", "16", "--cache-gb", "1", "--dist-backend", "gloo"]
+           "--warmup", "2", "--inflight", "16", "--pool", "16", "--cache-gb", "1", "--dist-backend", plane]
     env = dict(os.environ, PYTHONPATH=str(REPO))
     p = subprocess.run(cmd, cwd=REPO, env=env, capture_output=True, text=True, timeout=420)
     assert p.returncode == 0, p.stderr[-4000:]
@@ -36,4 +40,4 @@ def test_two_ranks_share_one_gpu_bench_path(cuda):
     res = json.loads(line)
     assert res["n_gpus"] == 2 and res["errors"] == 0
     assert res["offload_ratio"] == pytest.approx(0.5, abs=0.02)  # every segment fetched once, shared once
-    assert res["value"] > 0 and res["config"]["parallelism"] == "swarm2-gloo"
+    assert res["value"] > 0 and res["config"]["parallelism"] == f"swarm2-{plane}"
