@@ -411,35 +411,47 @@ class _IpcOutbox:
         if any(h != hosts[0] for h in hosts):
             return None
         box = cls(comm)
-        ok = True
-        try:
-            box._share(int(os.environ.get("HLSP2P_IPC_OUTBOX_BYTES", str(1 << 30))))
-        except Exception:  # noqa: BLE001 - IPC unavailable on some rank: every rank keeps gloo
-            ok = False
-        flags: List[object] = [None] * comm.world_size
-        dist.all_gather_object(flags, ok, group=g)
-        return box if all(flags) else None
+        return box if box._share(int(os.environ.get("HLSP2P_IPC_OUTBOX_BYTES", str(1 << 30)))) else None
 
-    def _share(self, cap: int) -> None:
-        """Collective, once: allocate this rank's outbox and open every peer's.  The
-        capacity is fixed for the communicator's life: re-exporting a fresh allocation
-        while peers still map the old one proved unreliable (a peer could keep reading
-        through its cached mapping of the old handle), so a round that needs more fails
+    def _share(self, cap: int) -> bool:
+        """Collective, once: allocate this rank's outbox and open every peer's.  Each local
+        step that can fail sits between two all-gathers that report success, so a rank
+        that fails never leaves the others blocked in a collective: either every rank ends
+        up with every outbox, or every rank returns False (and keeps gloo).
+
+        The capacity is fixed for the communicator's life.  Re-exporting a fresh allocation
+        while peers still mapped the old one proved unreliable (CRC failures: a peer kept
+        reading through its mapping of the old handle), so a round that needs more fails
         loudly instead (``HLSP2P_IPC_OUTBOX_BYTES``; ``bench.py`` sizes it from the
         workload)."""
         from torch.multiprocessing.reductions import reduce_tensor
 
         comm = self.comm
+        dist, g, me = comm.dist, comm.control_group, comm.rank
         cap = (max(cap, 1 << 20) + (1 << 20) - 1) // (1 << 20) * (1 << 20)
-        self.buf = torch.empty(cap, dtype=torch.uint8, device=torch.device("cuda", torch.cuda.current_device()))
-        torch.cuda.synchronize()
-        handle = reduce_tensor(self.buf)
+        handle = None
+        try:
+            self.buf = torch.empty(cap, dtype=torch.uint8, device=torch.device("cuda", torch.cuda.current_device()))
+            torch.cuda.synchronize()
+            handle = reduce_tensor(self.buf)
+        except Exception:  # noqa: BLE001 - reported to every rank below
+            handle = None
         handles: List[object] = [None] * comm.world_size
-        comm.dist.all_gather_object(handles, handle, group=comm.control_group)
-        me = comm.rank
-        self.peers = [self.buf if r == me else h[0](*h[1]) for r, h in enumerate(handles)]  # type: ignore[index]
+        dist.all_gather_object(handles, handle, group=g)
+        ok = all(h is not None for h in handles)
+        if ok:
+            try:
+                self.peers = [self.buf if r == me else h[0](*h[1])  # type: ignore[index]
+                              for r, h in enumerate(handles)]
+            except Exception:  # noqa: BLE001
+                ok = False
+        flags: List[object] = [None] * comm.world_size
+        dist.all_gather_object(flags, ok, group=g)  # also: every rank holds every outbox
+        if not all(flags):
+            self.peers, self.buf = [], None
+            return False
         self.cap = cap
-        comm.barrier()  # every rank holds every outbox before any is written
+        return True
 
     def exchange(self, sends, recvs) -> None:
         comm = self.comm
