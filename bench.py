@@ -525,7 +525,10 @@ def _fleet(args, world, rank, device, use_gpu, node, origin, players, desc, encr
         result = _result(args, world, tot, max_ns / 1e9, origin, K, desc, encrypted, seg_dur, use_gpu, numa_node,
                          dist, players=W, transport=getattr(node.comm, "data_transport", None))
         if args.verbose:
-            print(f"# rank {rank} pack {t_pack:.2f}s players {W} marks {dict(m1)}\n"
+            ipc = getattr(node.comm, "_ipc", None)
+            plane = getattr(node.comm, "data_transport", "local") + (
+                f" (events: {ipc._peer_ev is not None})" if ipc is not None else "")
+            print(f"# rank {rank} pack {t_pack:.2f}s players {W} data plane {plane} marks {dict(m1)}\n"
                   f"#   node stats {node.stats} last round {node.last_round}\n"
                   f"#   node ms {node.timer.summary_ms(args.steps)}\n"
                   f"#   transmux ms {pipe.timer.summary_ms(args.steps)}", file=sys.stderr)

@@ -36,7 +36,7 @@ import os
 import secrets
 import socket
 import threading
-from typing import List, Optional, Sequence, Tuple
+from typing import Any, List, Optional, Sequence, Tuple
 
 import numpy as np
 import torch
@@ -380,10 +380,17 @@ class _IpcOutbox:
        can still be reading an outbox that is about to be rewritten.
     2. All-gather the send tables ``[outbox bytes, n, (dst, nbytes) * n]`` (a round larger
        than the fixed outbox fails on every rank).
-    3. Pack the sends into the outbox (256-byte aligned, in order), wait for the packing
-       copies, then barrier.
-    4. For the k-th receive from ``src``, copy the k-th of ``src``'s sends addressed to this
-       rank (two-sided, ordered, as RCCL point-to-point), then record an event for step 1.
+    3. Pack the sends into the outbox (256-byte aligned, in order) on the node stream and
+       record this rank's interprocess event after them, then barrier.  The host never
+       waits for the packing: like an RCCL group, it stays behind the round's CDN DMA in
+       stream order.  (If interprocess events are unavailable, every rank waits for its
+       packing copies on the host instead.)
+    4. For the k-th receive from ``src``, the node stream first waits on ``src``'s event,
+       then copies the k-th of ``src``'s sends addressed to this rank (two-sided, ordered,
+       as RCCL point-to-point).  An event recorded after the copies serves step 1.
+       A peer's event is re-recorded only in its next exchange, after the all-gather of
+       step 2, which this rank joins only once these copies (and the wait before them)
+       have run.
 
     Enabled with ``HLSP2P_DATA_PLANE=ipc`` on a gloo group (``bench.py --dist-backend
     ipc``).  Every rank must be on the same host; otherwise every rank keeps gloo."""
@@ -396,6 +403,8 @@ class _IpcOutbox:
         self.buf: Optional[torch.Tensor] = None
         self.peers: List[torch.Tensor] = []
         self._pending = None
+        self._ev = None  # this rank's interprocess event: recorded after packing
+        self._peer_ev: Optional[List[Any]] = None  # every rank's event (None: host-side waits)
         self.exchanges = 0
 
     @classmethod
@@ -451,7 +460,35 @@ class _IpcOutbox:
             self.peers, self.buf = [], None
             return False
         self.cap = cap
+        self._share_events()
         return True
+
+    def _share_events(self) -> None:
+        """Collective: export an interprocess event per rank (optional: on any failure every
+        rank packs with a host-side wait instead)."""
+        comm = self.comm
+        dist, g, me = comm.dist, comm.control_group, comm.rank
+        dev = torch.cuda.current_device()
+        handle = None
+        try:
+            self._ev = torch.cuda.Event(enable_timing=False, interprocess=True)
+            self._ev.record()
+            torch.cuda.synchronize()
+            handle = self._ev.ipc_handle()
+        except Exception:  # noqa: BLE001 - reported to every rank below
+            handle = None
+        handles: List[object] = [None] * comm.world_size
+        dist.all_gather_object(handles, handle, group=g)
+        evs: Optional[List[Any]] = None
+        if all(h is not None for h in handles):
+            try:
+                evs = [self._ev if r == me else torch.cuda.Event.from_ipc_handle(dev, h)
+                       for r, h in enumerate(handles)]
+            except Exception:  # noqa: BLE001
+                evs = None
+        flags: List[object] = [None] * comm.world_size
+        dist.all_gather_object(flags, evs is not None, group=g)
+        self._peer_ev = evs if all(flags) else None
 
     def exchange(self, sends, recvs) -> None:
         comm = self.comm
@@ -479,8 +516,12 @@ class _IpcOutbox:
             for (_, t), o, n in zip(sends, offs, sizes):
                 if n:
                     buf[o:o + n].copy_(_as_bytes(t), non_blocking=True)
-            stream.synchronize()
-        comm.barrier()  # every outbox is packed
+            if self._peer_ev is not None:
+                self._ev.record(stream)
+            else:
+                stream.synchronize()
+        comm.barrier()  # every outbox's packing is enqueued (or done) and its event recorded
+        peer_ev = self._peer_ev
         me = comm.rank
         mine: dict = {}  # src -> [(offset, nbytes)] of src's sends to this rank, in order
         cursor: dict = {}
@@ -496,6 +537,8 @@ class _IpcOutbox:
                         lst.append((o, n))
                     o += (n + A - 1) // A * A
                 mine[src] = lst
+                if peer_ev is not None and lst:
+                    stream.wait_event(peer_ev[src])  # src's packing has run
             i = cursor.get(src, 0)
             if i >= len(lst):
                 raise RuntimeError(f"rank {me}: no matching send from {src}")
