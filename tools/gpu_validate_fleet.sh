@@ -1,5 +1,6 @@
 # Validation with the fleet default: GPU tests, smoke, headline bench (default = 4 players)
-# and single-process, host-bound probe, 2/4-rank rehearsals (gloo-staged data plane).
+# and single-process, host-bound probe, 2/4-rank rehearsals (HIP-IPC data plane; the gloo-staged
+# plane is covered by tests/test_multirank_gpu.py).
 set -e
 R=$GRAFT_REPO_ROOT
 cd $R
@@ -15,6 +16,6 @@ timeout -k 10 300 python bench.py --config hostcost --steps 40 --warmup 6 --verb
 timeout -k 10 300 python bench.py --ingest hbm --steps 30 --warmup 5 --verbose > $O/hbm_default.log 2>&1
 for N in 2 4; do
   timeout -k 10 300 python -m torch.distributed.run --nnodes=1 --nproc-per-node $N --master-addr 127.0.0.1 \
-    --master-port $((29830 + N)) bench.py --gpus $N --steps 10 --warmup 3 --dist-backend gloo --cache-gb 4 \
+    --master-port $((29830 + N)) bench.py --gpus $N --steps 10 --warmup 3 --dist-backend ipc --cache-gb 4 --players 2 \
     --verbose > $O/n$N.log 2>&1
 done
