@@ -365,6 +365,19 @@ def _as_bytes(t: torch.Tensor) -> torch.Tensor:
     return t.reshape(-1).view(torch.uint8)
 
 
+def _outbox_slots(table: np.ndarray, me: int, align: int) -> List[Tuple[int, int]]:
+    """``(offset, nbytes)`` in a peer's outbox of each of its sends to rank ``me``, in send
+    order, from its table ``[outbox bytes, n, (dst, nbytes) * n]`` (sends are packed in
+    order at ``align``-byte boundaries)."""
+    k = int(table[1])
+    out, o = [], 0
+    for d, n in zip(table[2:2 + 2 * k:2].tolist(), table[3:3 + 2 * k:2].tolist()):
+        if d == me:
+            out.append((o, n))
+        o += (n + align - 1) // align * align
+    return out
+
+
 class _IpcOutbox:
     """Device-resident data plane for ranks that share one host but no RCCL communicator.
 
@@ -528,15 +541,7 @@ class _IpcOutbox:
         for src, t in recvs:
             lst = mine.get(src)
             if lst is None:
-                p = parts[src]
-                k = int(p[1])
-                dsts, lens = p[2:2 + 2 * k:2].tolist(), p[3:3 + 2 * k:2].tolist()
-                lst, o = [], 0
-                for d, n in zip(dsts, lens):
-                    if d == me:
-                        lst.append((o, n))
-                    o += (n + A - 1) // A * A
-                mine[src] = lst
+                lst = mine[src] = _outbox_slots(parts[src], me, A)
                 if peer_ev is not None and lst:
                     stream.wait_event(peer_ev[src])  # src's packing has run
             i = cursor.get(src, 0)

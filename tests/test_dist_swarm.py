@@ -184,3 +184,20 @@ def test_bench_fleet_two_ranks_two_players():
     # window the rank ahead fetches segments its peer only receives after it (GPU rehearsals,
     # profiles/r2_fleet_validation: exactly 0.50 / 0.75 at 2 / 4 ranks)
     assert 0.3 < res["offload_ratio"] <= 0.52
+
+
+def test_ipc_outbox_slots_follow_the_packing_order():
+    """The IPC rehearsal plane (parallel/comm.py:_IpcOutbox): a receiver finds each send
+    addressed to it in the sender's outbox from the sender's table alone -- sends packed in
+    order at 256-byte boundaries, per (src, dst) pair in send order (RCCL p2p semantics)."""
+    import numpy as np
+
+    from hlsjs_p2p_wrapper_amd.parallel.comm import _outbox_slots
+
+    sends = [(1, 1000), (2, 300), (1, 4), (3, 0), (1, 256)]  # (dst, nbytes) of one sender
+    table = np.array([0, len(sends)] + [v for s in sends for v in s], dtype=np.int64)
+    assert _outbox_slots(table, 1, 256) == [(0, 1000), (1536, 4), (1792, 256)]
+    assert _outbox_slots(table, 2, 256) == [(1024, 300)]
+    assert _outbox_slots(table, 3, 256) == [(1792, 0)]
+    assert _outbox_slots(table, 0, 256) == []
+    assert _outbox_slots(np.array([0, 0], dtype=np.int64), 1, 256) == []
