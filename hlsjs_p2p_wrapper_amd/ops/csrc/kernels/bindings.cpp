@@ -1,5 +1,6 @@
 // torch binding module `_C`: argument checking + current-HIP-stream launch of the gfx950
-// kernels.  Host-only translation unit; kernels live in *.hip objects.
+// kernels, as pybind functions and as dispatcher ops (torch.ops.hlsp2p.*).  Host-only
+// translation unit; kernels live in *.hip objects.
 #include <c10/hip/HIPStream.h>
 #include <hip/hip_runtime_api.h>
 #include <torch/extension.h>
@@ -321,6 +322,41 @@ std::vector<Tensor> pack_h2d(const std::vector<pybind11::array>& arrays, int64_t
 }
 
 }  // namespace
+
+// The same launches registered with the PyTorch dispatcher: torch.ops.hlsp2p.<name> (CUDA
+// key, which is HIP on ROCm).  Each op writes its outputs in place (schemas mark them
+// mutable) on the current stream, exactly like the pybind entry points above.  The
+// dispatcher path lets torch-level code (custom autograd-free pipelines, torch.library
+// tooling, opcheck) call the gfx950 kernels without this module's Python wrappers.
+TORCH_LIBRARY(hlsp2p, m) {
+  m.def("aes128_cbc_decrypt(Tensor src, Tensor(a!) dst, Tensor src_off, Tensor dst_off, Tensor blk_prefix, "
+        "Tensor chunk_prefix, Tensor drk, Tensor iv, Tensor td0, Tensor isb, Tensor(b!) out_len, "
+        "int total_chunks) -> ()");
+  m.def("crc32_batch(Tensor buf, Tensor seg_off, Tensor seg_len, Tensor tile_prefix, Tensor res_off, Tensor wfrag, "
+        "Tensor tables, Tensor(a!) residues, Tensor(b!) crc_out, Tensor? expect, Tensor(c!)? ok_out, "
+        "int total_tiles, Tensor? scatter_idx, Tensor(d!)? scatter_out) -> ()");
+  m.def("ts_demux(Tensor buf, Tensor seg_off, Tensor seg_len, Tensor blk_prefix, int total_blocks, "
+        "Tensor(a!) meta, Tensor(b!) pts_dts, Tensor(c!) blk_sums, Tensor(d!) es, Tensor es_off, Tensor(e!) pes, "
+        "int max_pes, Tensor(f!) info) -> ()");
+  m.def("range_select(Tensor starts, Tensor track_off, Tensor q_track, Tensor q_begin, Tensor q_dur, "
+        "Tensor(a!) out_lo, Tensor(b!) out_hi) -> ()");
+  m.def("key_hash(Tensor keys, Tensor(a!) out) -> ()");
+  m.def("table_insert(Tensor(a!) slots, Tensor keys, Tensor values, Tensor(b!) ok_out) -> ()");
+  m.def("table_lookup(Tensor(a!) slots, Tensor keys, Tensor(b!) out, bool erase) -> ()");
+  m.def("segment_copy(Tensor src, Tensor(a!) dst, Tensor src_off, Tensor dst_off, Tensor len, Tensor chunk_prefix, "
+        "int total_chunks) -> ()");
+}
+
+TORCH_LIBRARY_IMPL(hlsp2p, CUDA, m) {
+  m.impl("aes128_cbc_decrypt", &aes128_cbc_decrypt);
+  m.impl("crc32_batch", &crc32_batch);
+  m.impl("ts_demux", &ts_demux);
+  m.impl("range_select", &range_select);
+  m.impl("key_hash", &key_hash);
+  m.impl("table_insert", &table_insert);
+  m.impl("table_lookup", &table_lookup);
+  m.impl("segment_copy", &segment_copy);
+}
 
 void register_rccl(pybind11::module& m);      // rccl_comm.cpp: native RCCL data plane
 void register_transmux(pybind11::module& m);  // transmux.cpp: one native call per transmux batch
