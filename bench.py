@@ -106,13 +106,18 @@ def parse():
     return p.parse_args()
 
 
-def _numa(mode: str, dev: int):
+def _numa(mode: str, dev: int, world: int = 1, players: int = 0):
     from hlsjs_p2p_wrapper_amd.utils.runtime import bind_to_gpu_numa, gpu_local_cpus
 
     if mode == "off":
         return None
     if mode == "auto":
-        return bind_to_gpu_numa(dev)
+        # every rank on this GPU's NUMA node brings 1 + players busy processes: bind only when
+        # the node's CPUs can hold all of them (else leave the affinity alone)
+        node, _ = gpu_local_cpus(dev)
+        ranks_here = sum(1 for i in range(min(max(1, world), torch.cuda.device_count()))
+                         if node is not None and gpu_local_cpus(i)[0] == node)
+        return bind_to_gpu_numa(dev, min_cpus=max(8, max(1, ranks_here) * (1 + players)))
     node, local = gpu_local_cpus(dev)  # remote: every allowed CPU NOT local to the GPU
     other = os.sched_getaffinity(0).difference(local)
     if node is None or len(other) < 8:
@@ -192,7 +197,7 @@ def main() -> int:
         local_dev = local_rank % torch.cuda.device_count()  # rehearsals may share one GPU
         torch.cuda.set_device(local_dev)
         device = torch.device("cuda", local_dev)
-        numa_node = _numa(args.numa, local_dev)  # before the pinned CDN buffers are allocated
+        numa_node = _numa(args.numa, local_dev, world, W)  # before the pinned CDN buffers are allocated
         if players is not None and numa_node is not None:  # the players run next to their node
             for pr in players[1]:
                 try:
