@@ -430,6 +430,10 @@ def _fleet(args, world, rank, device, use_gpu, node, origin, players, desc, encr
     nstep = [0]
 
     def step():
+        if args.churn > 0 and world > 1:  # BASELINE config 3: the same rotation as the in-process path
+            online = (nstep[0] // args.churn) % (world + 1) != rank
+            if online != node.online:
+                node.set_online(online)
         drain_ready()
         server.await_players()  # the players' next requests (paces the rounds by the players)
         server.poll()

@@ -87,12 +87,14 @@ def _bench_cpu(port: int, *extra: str, nproc: int = 2, config: str = "abr5") -> 
     return json.loads([ln for ln in p.stdout.splitlines() if ln.startswith("{")][-1])
 
 
-def test_bench_two_ranks_abr_ladder_with_churn():
-    # BASELINE config 3 through the driver's launch path (torchrun + bench.py), gloo on CPU:
-    # with churn, a rank masked offline fetches everything from the CDN, so the swarm
-    # offload ratio drops below the churn-free run's; nothing errors either way
-    calm = _bench_cpu(_free_port(), "--players", "0")
-    churn = _bench_cpu(_free_port(), "--churn", "2", "--players", "0")
+@pytest.mark.parametrize("players", ["0", "2"])
+def test_bench_two_ranks_abr_ladder_with_churn(players):
+    # BASELINE config 3 through the driver's launch path (torchrun + bench.py), gloo on CPU,
+    # with one in-process player and with the fleet (player processes): with churn, a rank
+    # masked offline fetches everything from the CDN, so the swarm offload ratio drops below
+    # the churn-free run's; nothing errors either way
+    calm = _bench_cpu(_free_port(), "--players", players)
+    churn = _bench_cpu(_free_port(), "--churn", "2", "--players", players)
     assert calm["errors"] == 0 and churn["errors"] == 0
     assert calm["n_gpus"] == 2 and churn["config"]["churn_steps"] == 2
     assert 0 < churn["offload_ratio"] < calm["offload_ratio"]
