@@ -185,6 +185,10 @@ def _spawn_players(W, world, rank, origin_kwargs, hls_config, p2p_base, n_segmen
 
 def main() -> int:
     args = parse()
+    if args.sync_steps and args.players:
+        # the fleet's players pace the rounds with batches in flight; an unpipelined step is
+        # a diagnostic of the in-process path only
+        raise SystemExit("--sync-steps runs one player in the rank process: add --players 0")
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
@@ -488,7 +492,8 @@ def _fleet(args, world, rank, device, use_gpu, node, origin, players, desc, encr
             if time.perf_counter() > t_end or not all(pr.is_alive() for pr in procs):
                 raise RuntimeError("fleet players did not start")
             time.sleep(0.002)
-        tune_gc()
+        if not args.no_gc_tune:
+            tune_gc()
         for _ in range(args.warmup):
             step()
         sync()
