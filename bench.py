@@ -35,8 +35,13 @@ import os
 import sys
 import time
 
-import numpy as np
-import torch
+# multi-process GPU work on this ROCm stack (RCCL peer buffers, HIP-IPC rehearsal outboxes)
+# needs the dmabuf IPC mode; set it before the HSA runtime starts (torch import) unless the
+# environment already chose
+os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
 
 _PROF = None
 if os.environ.get("HLSP2P_PROFILE"):  # cProfile the timed steps (host-overhead analysis)
