@@ -570,8 +570,8 @@ class SwarmNode:
             self.last_round = {"wants": 0, "ms": (time.perf_counter() - h.t0) * 1e3}
             return
         t0 = time.perf_counter()
-        if h.done is not None:
-            h.done.synchronize()
+        if h.done is not None and not h.done.query():
+            self._wait_round(h)
         t1 = time.perf_counter()
         self.timer.add("wait_device", t1 - t0)
         if h.ev_cdn is not None:
@@ -661,6 +661,33 @@ class SwarmNode:
                            "ms": (time.perf_counter() - h.t0) * 1e3}
         if any(w.round < 0 and not w.staging for w in self._wants.values()):
             self._schedule()  # (a want being downloaded is rescheduled when it lands)
+
+    ROUND_SPIN_S = 0.02  # busy-poll a round's completion this long before checking for peer failures
+
+    def _wait_round(self, h: RoundHandle) -> None:
+        """Wait for a round's device work without hanging on a dead peer.
+
+        A round whose RCCL transfers wait for a peer that crashed never completes, and
+        ``hipEventSynchronize`` would block forever.  Instead: poll the round's event (the
+        common case finishes within the first ``ROUND_SPIN_S``), then poll it every
+        millisecond while asking the communicator for an asynchronous error
+        (``ncclCommGetAsyncError``) and watching the ``HLSP2P_ROUND_TIMEOUT`` deadline
+        (default 600 s); either one raises instead of hanging the rank."""
+        ev = h.done
+        spin_end = time.perf_counter() + self.ROUND_SPIN_S
+        while time.perf_counter() < spin_end:
+            if ev.query():
+                return
+        check = getattr(self.comm, "async_error", None)
+        deadline = time.perf_counter() + float(os.environ.get("HLSP2P_ROUND_TIMEOUT", "600"))
+        while not ev.query():
+            err = check() if check is not None else ""
+            if err:
+                raise RuntimeError(f"rank {self.rank}: swarm round {h.round} failed in the data plane: {err}")
+            if time.perf_counter() > deadline:
+                raise TimeoutError(f"rank {self.rank}: swarm round {h.round} did not complete on the device "
+                                   "(HLSP2P_ROUND_TIMEOUT); a peer may have stopped")
+            time.sleep(1e-3)
 
     def _views(self, offs: List[int], lens: List[int]) -> List[torch.Tensor]:
         """Zero-copy uint8 views of the arena for a round's deliveries (one native call on

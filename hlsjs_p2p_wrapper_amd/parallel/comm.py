@@ -314,6 +314,14 @@ class DistComm(SwarmComm):
         stream = torch.cuda.current_stream().cuda_stream
         self._rccl.exchange(ptr[:ns], nbytes[:ns], peer[:ns], ptr[ns:], nbytes[ns:], peer[ns:], stream)
 
+    def async_error(self) -> str:
+        """The data plane's asynchronous error ("" = none): RCCL reports a failed peer here
+        while the transfers waiting on it never complete (the node polls this instead of
+        blocking on a round that cannot finish)."""
+        if self._rccl is not None:
+            return self._rccl.async_error()
+        return ""
+
     def close(self) -> None:
         """Release the native RCCL communicator.  Callers close after their last round has
         completed on the device, so this aborts (returns without waiting on peers) rather

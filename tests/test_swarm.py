@@ -340,3 +340,39 @@ def test_origin_resolution_and_vod_locate():
             inner.locate("r0/seg4.ts")  # past the VOD's last segment
     finally:
         clear_origins()
+
+
+def test_round_wait_reports_a_dead_peer_instead_of_hanging(monkeypatch):
+    """SURVEY §5.3 failure detection: a round whose transfers wait on a crashed peer never
+    completes on the device.  The node polls the round instead of blocking on it, and raises
+    on the data plane's asynchronous error (RCCL's ncclCommGetAsyncError) or on the
+    HLSP2P_ROUND_TIMEOUT deadline.  A round that finishes late is simply waited for."""
+    from hlsjs_p2p_wrapper_amd.agent.node import RoundHandle, SwarmNode
+
+    node = SwarmNode(device="cpu", cache_bytes=64 << 10, loop=new_event_loop("virtual"), auto_tick=False)
+    monkeypatch.setattr(SwarmNode, "ROUND_SPIN_S", 0.001)
+
+    class Never:
+        def query(self):
+            return False
+
+    class Later:
+        def __init__(self):
+            self.n = 0
+
+        def query(self):
+            self.n += 1
+            return self.n > 3
+
+    h = RoundHandle(7, False)
+    h.done = Never()
+    node.comm.async_error = lambda: "unhandled system error (remote process exited)"
+    with pytest.raises(RuntimeError, match="round 7 failed in the data plane"):
+        node._wait_round(h)
+    node.comm.async_error = lambda: ""
+    monkeypatch.setenv("HLSP2P_ROUND_TIMEOUT", "0.01")
+    with pytest.raises(TimeoutError, match="round 7 did not complete"):
+        node._wait_round(h)
+    h.done = Later()
+    node._wait_round(h)  # completes once the event reports done
+    assert h.done.n == 4
