@@ -390,7 +390,7 @@ def main() -> int:
     result = _result(args, world, tot, max_s, origin, K, desc, encrypted, seg_dur, use_gpu, numa_node, dist,
                      transport=getattr(node.comm, "data_transport", None))
     if args.verbose:
-        print(f"# rank {rank} pack {t_pack:.2f}s counters {counters} level {hls.currentLevel}\n"
+        print(f"# rank {rank} pack {t_pack:.2f}s {_mem(use_gpu, device)} counters {counters} level {hls.currentLevel}\n"
               f"#   node stats {node.stats} last round {node.last_round}\n"
               f"#   step ms {bt.summary_ms(args.steps)}\n"
               f"#   node ms {node.timer.summary_ms(args.steps)}\n"
@@ -547,7 +547,8 @@ def _fleet(args, world, rank, device, use_gpu, node, origin, players, desc, encr
             ipc = getattr(node.comm, "_ipc", None)
             plane = getattr(node.comm, "data_transport", "local") + (
                 f" (events: {ipc._peer_ev is not None})" if ipc is not None else "")
-            print(f"# rank {rank} pack {t_pack:.2f}s players {W} data plane {plane} marks {dict(m1)}\n"
+            print(f"# rank {rank} pack {t_pack:.2f}s players {W} data plane {plane} {_mem(use_gpu, device)} "
+                  f"marks {dict(m1)}\n"
                   f"#   node stats {node.stats} last round {node.last_round}\n"
                   f"#   node ms {node.timer.summary_ms(args.steps)}\n"
                   f"#   transmux ms {pipe.timer.summary_ms(args.steps)}", file=sys.stderr)
@@ -602,6 +603,19 @@ def _result(args, world, tot, max_s, origin, K, desc, encrypted, seg_dur, use_gp
                    "churn_steps": args.churn, "device": "MI355X" if use_gpu else "cpu", "numa": numa_node,
                    "ingest": args.ingest if use_gpu else "host"},
     }
+
+
+def _mem(use_gpu, device) -> str:
+    """Peak memory of this rank (soak runs: the HBM arena is allocated once, so the device
+    peak must not grow with the step count; host: the process's peak RSS)."""
+    hwm = "?"
+    try:
+        with open("/proc/self/status") as f:
+            hwm = next((ln.split()[1] for ln in f if ln.startswith("VmHWM:")), "?")
+    except OSError:
+        pass
+    dev = f"hbm peak {torch.cuda.max_memory_allocated(device) / 2**30:.2f} GiB " if use_gpu else ""
+    return f"{dev}host peak {int(hwm) / 2**20:.2f} GiB" if hwm != "?" else dev
 
 
 def _data_plane(dist, transport) -> str:
