@@ -401,17 +401,19 @@ class _IpcOutbox:
        can still be reading an outbox that is about to be rewritten.
     2. All-gather the send tables ``[outbox bytes, n, (dst, nbytes) * n]`` (a round larger
        than the fixed outbox fails on every rank).
-    3. Pack the sends into the outbox (256-byte aligned, in order) on the node stream and
-       record this rank's interprocess event after them, then barrier.  The host never
-       waits for the packing: like an RCCL group, it stays behind the round's CDN DMA in
-       stream order.  (If interprocess events are unavailable, every rank waits for its
-       packing copies on the host instead.)
-    4. For the k-th receive from ``src``, the node stream first waits on ``src``'s event,
-       then copies the k-th of ``src``'s sends addressed to this rank (two-sided, ordered,
-       as RCCL point-to-point).  An event recorded after the copies serves step 1.
-       A peer's event is re-recorded only in its next exchange, after the all-gather of
-       step 2, which this rank joins only once these copies (and the wait before them)
-       have run.
+    3. Pack the sends into the outbox (256-byte aligned, in order) on the node stream, wait
+       for the packing copies on the host, then barrier.
+    4. For the k-th receive from ``src``, copy the k-th of ``src``'s sends addressed to this
+       rank (two-sided, ordered, as RCCL point-to-point) on the node stream.  An event
+       recorded after the copies serves step 1.
+
+    ``HLSP2P_IPC_EVENTS=1`` replaces the host wait of step 3 with an interprocess event per
+    rank, recorded after packing.  Peers' node streams wait on it before copying, so the host
+    never waits, as with an RCCL group.  A peer's event is re-recorded only in its next
+    exchange, after the all-gather of step 2, which this rank joins only once its copies
+    (and the wait before them) have run.  The mode is opt-in.  On this ROCm build,
+    ``hipStreamWaitEvent`` on an IPC event starts failing with ``invalid argument`` after a
+    few hundred rounds (`profiles/r2_ipc_rehearsal/soak`), while 20-step runs pass.
 
     Enabled with ``HLSP2P_DATA_PLANE=ipc`` on a gloo group (``bench.py --dist-backend
     ipc``).  Every rank must be on the same host; otherwise every rank keeps gloo."""
@@ -481,7 +483,8 @@ class _IpcOutbox:
             self.peers, self.buf = [], None
             return False
         self.cap = cap
-        self._share_events()
+        if os.environ.get("HLSP2P_IPC_EVENTS", "0") == "1":
+            self._share_events()
         return True
 
     def _share_events(self) -> None:
