@@ -1,6 +1,5 @@
-# IPC rehearsal plane, default (host-side packing wait): short 2/4-rank runs and a 600-step
-# 4-rank soak; then the opt-in event mode's soak for the record (expected to fail on this
-# ROCm build after a few hundred rounds: it runs last and its failure does not stop the script).
+# IPC rehearsal plane, default mode (host-side packing wait): short 2/4-rank runs and a
+# 600-step 4-rank soak.
 set -e
 cd $GRAFT_REPO_ROOT
 export PYTHONPATH=$GRAFT_REPO_ROOT
