@@ -447,6 +447,7 @@ class FleetServer:
         for i, job in enumerate(jobs):
             p = job.frag
             by_rid[p.w].pop(p.rid, None)
+            p.req = None  # Request.callbacks is p: drop the cycle so refcounting frees both now
             c = per.get(p.w)
             if c is None:
                 c = per[p.w] = []
