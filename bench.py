@@ -166,8 +166,10 @@ def _spawn_players(W, world, rank, origin_kwargs, hls_config, p2p_base, n_segmen
 
     ctx = mp.get_context("spawn")
     conns, procs = [], []
-    saved = {k: os.environ.get(k) for k in ("HIP_VISIBLE_DEVICES", "CUDA_VISIBLE_DEVICES")}
+    saved = {k: os.environ.get(k) for k in ("HIP_VISIBLE_DEVICES", "CUDA_VISIBLE_DEVICES", "HLSJS_P2P_PURE")}
     os.environ["HIP_VISIBLE_DEVICES"] = os.environ["CUDA_VISIBLE_DEVICES"] = "-1"
+    if os.environ.get("HLSP2P_PLAYER_PROFILE"):  # profiled players run pure Python (compiled frames are opaque)
+        os.environ["HLSJS_P2P_PURE"] = "1"
     try:
         for w in range(W):
             parent, child = ctx.Pipe()

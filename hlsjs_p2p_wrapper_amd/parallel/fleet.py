@@ -580,6 +580,11 @@ def player_main(conn: Any, spec: Dict[str, Any]) -> None:
             loop.run_once(block=False)
 
     gc_tuned = False
+    prof = None
+    if os.environ.get("HLSP2P_PLAYER_PROFILE"):  # cProfile this player from its first request to stop
+        import cProfile
+
+        prof = cProfile.Profile()
     debug = os.environ.get("HLSP2P_FLEET_DEBUG")
     t_dbg = time.monotonic()
     try:
@@ -597,6 +602,8 @@ def player_main(conn: Any, spec: Dict[str, Any]) -> None:
             if not gc_tuned and node.inflight:  # started: freeze the start-up heap
                 tune_gc()
                 gc_tuned = True
+                if prof is not None:
+                    prof.enable()
             while node.control:
                 msg = node.control.pop(0)
                 if msg[0] == "mark":
@@ -605,6 +612,15 @@ def player_main(conn: Any, spec: Dict[str, Any]) -> None:
                 elif msg[0] == "stop":
                     return
     finally:
+        if prof is not None:
+            import io
+            import pstats
+
+            prof.disable()
+            out = io.StringIO()
+            pstats.Stats(prof, stream=out).sort_stats("tottime").print_stats(40)
+            with open(f"{os.environ['HLSP2P_PLAYER_PROFILE']}.player{spec.get('rank', 0)}_{os.getpid()}.txt", "w") as f:
+                f.write(f"buffered {counters['buffered']}\n" + out.getvalue())
         try:
             hls.destroy()
         finally:
