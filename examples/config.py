@@ -22,6 +22,9 @@ from pathlib import Path
 from typing import Any, Callable, Dict
 
 sys.path.insert(0, str(Path(__file__).resolve().parents[1]))
+# torchrun peers share RCCL buffers across processes: this ROCm stack needs the dmabuf IPC
+# mode, chosen before the HSA runtime starts (unless the environment already set it)
+os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
 
 import torch  # noqa: E402
 
