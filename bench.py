@@ -226,7 +226,13 @@ def main() -> int:
         if backend == "ipc":  # rehearsal data plane (parallel/comm.py:_IpcOutbox) on a gloo group
             os.environ["HLSP2P_DATA_PLANE"] = "ipc"
             backend = "gloo"
-        dist.init_process_group(backend, device_id=device if (use_gpu and backend == "nccl") else None)
+        elif backend == "nccl":
+            # RCCL data plane: the swarm node opens ONE native RCCL communicator per rank
+            # (kernels/rccl_comm.cpp) over a gloo default group (rendezvous + control fallback);
+            # an nccl default group would add torch's own, idle, communicator
+            os.environ["HLSP2P_DATA_PLANE"] = "rccl"
+            backend = "gloo"
+        dist.init_process_group(backend)
 
     from hlsjs_p2p_wrapper_amd import Hls
     from hlsjs_p2p_wrapper_amd.agent import node_for_config
@@ -623,7 +629,7 @@ def _mem(use_gpu, device) -> str:
 def _data_plane(dist, transport) -> str:
     """Label of the data plane the node's comm actually uses (an IPC request that could not
     be honoured reports gloo)."""
-    if dist.get_backend() == "nccl":
+    if transport and transport.startswith("rccl"):
         return "rccl"
     return "ipc" if transport == "hip-ipc" else "gloo"
 

@@ -30,6 +30,7 @@ from __future__ import annotations
 import concurrent.futures as cf
 import http.client
 import logging
+import re
 import ssl
 import threading
 import urllib.parse
@@ -43,6 +44,35 @@ log = logging.getLogger("hlsjs_p2p_wrapper_amd.network")
 
 _TEXT_SUFFIXES = (".m3u8", ".m3u", ".txt", ".xml", ".json")
 Range = Optional[Tuple[int, Optional[int]]]
+_CONTENT_RANGE = re.compile(r"bytes\s+(\d+)-(\d+)/(\d+|\*)$")
+
+
+def _check_content_range(value: Optional[str], rng: Tuple[int, Optional[int]], url: str) -> None:
+    """A 206 must carry the range that was asked for (``Content-Range: bytes s-e/total``)."""
+    if not value:
+        return  # some servers omit it; Content-Length still bounds the body
+    m = _CONTENT_RANGE.match(value.strip())
+    if m is None:
+        raise HttpError(502, url, f"malformed Content-Range {value!r}")
+    s, e = int(m.group(1)), int(m.group(2))
+    want_s, want_e = rng
+    if s != want_s or (want_e is not None and e > want_e):
+        raise HttpError(502, url, f"Content-Range {value!r} does not match the requested bytes={want_s}-"
+                                  + ("" if want_e is None else str(want_e)))
+
+
+def _slice_range(body: Any, n: int, rng: Tuple[int, Optional[int]], pin: bool, url: str) -> Tuple[Any, int]:
+    """Cut the requested inclusive range out of a full-resource (200) body."""
+    s, e = rng
+    e = n - 1 if e is None else min(e, n - 1)
+    if s >= n:
+        raise HttpError(416, url, f"range start {s} beyond the {n}-byte resource")
+    k = max(0, e - s + 1)
+    if isinstance(body, str):
+        return body.encode()[s:s + k].decode("utf-8", errors="replace"), k
+    out = torch.empty(max(k, 1), dtype=torch.uint8, pin_memory=pin)
+    out[:k] = body[s:s + k]
+    return out, k
 
 
 class HttpOrigin:
@@ -141,6 +171,14 @@ class HttpOrigin:
                 self.errors += 1
             raise HttpError(status, url)
         n = resp.getheader("Content-Length")
+        if rng is not None:
+            if status == 206:
+                _check_content_range(resp.getheader("Content-Range"), rng, url)
+            elif status != 200:  # a range request answered 204 / 2xx without the body part
+                resp.read()
+                with self._lock:
+                    self.errors += 1
+                raise HttpError(status, url, "unexpected status for a Range request")
         if binary and n is not None:
             n = int(n)
             body = torch.empty(max(n, 1), dtype=torch.uint8, pin_memory=self.pin_memory)
@@ -160,6 +198,10 @@ class HttpOrigin:
                     body[:n] = torch.frombuffer(bytearray(raw), dtype=torch.uint8)
             else:
                 body = raw.decode("utf-8", errors="replace")
+        if rng is not None and status == 200:
+            # the CDN ignored the Range header and sent the whole resource: keep only the
+            # requested part (the node must stage, DMA and deliver exactly that range)
+            body, n = _slice_range(body, n, rng, self.pin_memory, url)
         with self._lock:
             self.requests += 1
             self.bytes_in += n
@@ -180,13 +222,23 @@ class HttpOrigin:
             hit = self._staged.get(key)
             fut = self._inflight.get(key)
             if hit is None and fut is None:
-                fut = self._pool.submit(self._stage_job, key, url, dict(headers or {}))
-                self._inflight[key] = fut
+                try:
+                    fut = self._pool.submit(self._stage_job, key, url, dict(headers or {}))
+                except RuntimeError:  # submit after close(): fail the stage instead of dropping it
+                    fut = None
+                else:
+                    self._inflight[key] = fut
+        if hit is None and fut is None:
+            on_done(None, HttpError(0, url, "cancelled: origin closed"))
+            return
         if hit is not None:
             on_done(hit[1], None)
             return
 
         def _cb(f: cf.Future) -> None:
+            if f.cancelled():  # the pool shut down first: still complete the caller's hold
+                on_done(None, HttpError(0, url, "cancelled: origin closed"))
+                return
             err = f.exception()
             if err is None:
                 on_done(f.result(), None)
@@ -266,7 +318,14 @@ class HttpOrigin:
             except Exception as e:  # noqa: BLE001 - surfaced to the loader as a network error
                 on_done(None, HttpError(0, url, str(e)))
 
-        self._pool.submit(job)
+        try:
+            fut = self._pool.submit(job)
+        except RuntimeError:  # submit after close()
+            on_done(None, HttpError(0, url, "cancelled: origin closed"))
+            return
+        # a job cancelled by close() never runs: answer it here so the caller's hold is released
+        fut.add_done_callback(lambda f: on_done(None, HttpError(0, url, "cancelled: origin closed"))
+                              if f.cancelled() else None)
 
     def close(self) -> None:
         """Stop the worker pool and drop every staged copy."""

@@ -103,6 +103,14 @@ int cus(int device) {
   return n;
 }
 
+// CUs the persistent decrypt grid leaves free (set_cu_reserve): with a live RCCL data plane
+// the node stream's send/recv kernels must find a CU while a decrypt batch runs -- one
+// 1024-thread AES workgroup with its 160 KiB LDS image fills a CU (waves, VGPRs and LDS), so
+// a full-chip persistent grid would hold RCCL back for the whole batch.
+int g_cu_reserve = 0;
+
+int decrypt_cus(int device) { return std::max(8, cus(device) - g_cu_reserve); }
+
 void hip_ok(hipError_t e, const char* what) { TORCH_CHECK(e == hipSuccess, what, " failed: ", hipGetErrorString(e)); }
 
 // src: uint8 device buffer holding every payload at src_off[i] (16-byte aligned) with
@@ -201,7 +209,7 @@ py::tuple transmux_launch(Tensor src, I64 src_off, I64 nbytes, py::array_t<uint8
                desc.at<int64_t>(d_so), desc.at<int64_t>(d_do), desc.at<int64_t>(d_bp), desc.at<int64_t>(d_cp),
                desc.at<uint32_t>(d_drk), desc.at<uint32_t>(d_iv), static_cast<const uint32_t*>(td0.data_ptr()),
                static_cast<const uint8_t*>(isb.data_ptr()), out_len.data_ptr<int64_t>(), static_cast<int>(ne),
-               a_cp.back(), cus(device), st),
+               a_cp.back(), decrypt_cus(device), st),
            "aes128_cbc_decrypt");
   }
 
@@ -255,6 +263,9 @@ py::tuple transmux_launch(Tensor src, I64 src_off, I64 nbytes, py::array_t<uint8
 }  // namespace
 
 void register_transmux(py::module& m) {
+  m.def("set_cu_reserve", [](int n) { g_cu_reserve = std::max(0, n); }, py::arg("n"),
+        "CUs the persistent decrypt grid leaves free for concurrent (RCCL) kernels");
+  m.def("cu_reserve", [] { return g_cu_reserve; });
   m.def("transmux_launch", &transmux_launch, py::arg("src"), py::arg("src_off"), py::arg("nbytes"), py::arg("enc"),
         py::arg("drk"), py::arg("iv"), py::arg("td0"), py::arg("isb"), py::arg("max_pes"));
 }

@@ -147,6 +147,7 @@ class DistComm(SwarmComm):
         self.rank = dist.get_rank()
         self.world_size = dist.get_world_size()
         backend = dist.get_backend(data_group)
+        plane = os.environ.get("HLSP2P_DATA_PLANE", "")
         if control_group is None:
             control_group = dist.new_group(backend="gloo") if backend != "gloo" else None
         self.control_group = control_group
@@ -158,20 +159,35 @@ class DistComm(SwarmComm):
         self.control_transport = "shm" if self._shm is not None else "gloo"
         self._rccl = None
         self._ipc: Optional[_IpcOutbox] = None
-        if (backend == "gloo" and os.environ.get("HLSP2P_DATA_PLANE", "") == "ipc" and self.world_size > 1
-                and torch.cuda.is_available()):
+        if backend == "gloo" and plane == "ipc" and self.world_size > 1 and torch.cuda.is_available():
             self._ipc = _IpcOutbox.open(self)
-        if backend == "nccl" and torch.cuda.is_available():
+        # RCCL data plane: on a gloo default group with HLSP2P_DATA_PLANE=rccl (bench.py's GPU
+        # launch: the node's native communicator is then the ONLY RCCL communicator of the
+        # rank -- no idle torch one doubling channel buffers and proxy threads), or on an nccl
+        # default group (torch's communicator exists anyway: the fallback transport)
+        want_rccl = (backend == "nccl" or plane == "rccl") and torch.cuda.is_available()
+        if want_rccl and os.environ.get("HLSP2P_NATIVE_RCCL", "1") != "0":
+            self._rccl = self._open_native_rccl()
+        if want_rccl and self._rccl is None:
+            if backend != "nccl":  # torch's batch_isend_irecv needs an nccl group (collective)
+                self.data_group = dist.new_group(backend="nccl")
+                self.data_backend = "nccl"
             # batch_isend_irecv runs on the group's full communicator; when that is created
             # lazily every rank must take part in its first use.  Node construction is
             # collective, so create it here rather than at the first (partial) exchange.
             t = torch.zeros(1, dtype=torch.int64, device=torch.device("cuda", torch.cuda.current_device()))
-            dist.all_reduce(t, group=data_group)
+            dist.all_reduce(t, group=self.data_group)
             torch.cuda.synchronize()
-            if os.environ.get("HLSP2P_NATIVE_RCCL", "1") != "0":
-                self._rccl = self._open_native_rccl()
+        if self._rccl is not None and torch.cuda.is_available():
+            # the persistent decrypt grid leaves one CU per XCD to the node stream's RCCL kernels
+            try:
+                from ..ops._native import device as _dev
+
+                _dev().set_cu_reserve(int(os.environ.get("HLSP2P_RCCL_CU_RESERVE", "8")))
+            except Exception:  # noqa: BLE001 - older extension without the knob: full grid
+                pass
         self.data_transport = ("rccl-native" if self._rccl is not None else
-                               "rccl-torch" if backend == "nccl" else
+                               "rccl-torch" if self.data_backend == "nccl" else
                                "hip-ipc" if self._ipc is not None else backend)
 
     def _open_native_rccl(self):
@@ -182,20 +198,31 @@ class DistComm(SwarmComm):
         dist, g = self.dist, self.control_group
         dev = None
         ok = True
+        uid: List[object] = [None]
         try:
             from ..ops._native import device as _dev
 
             dev = _dev()
             dev.rccl_version()
+            if self.rank == 0:  # a failure here is reported through the all-gather below
+                uid[0] = dev.rccl_unique_id()
         except Exception:  # noqa: BLE001 - no native module / RCCL: torch's path
             ok = False
-        uid = [dev.rccl_unique_id() if (ok and self.rank == 0) else None]
         flags: List[object] = [None] * self.world_size
         dist.all_gather_object(flags, ok, group=g)
         if not all(flags):
             return None
         dist.broadcast_object_list(uid, src=0, group=g)
-        comm = dev.RcclComm(uid[0], self.world_size, self.rank, torch.cuda.current_device())
+        comm, err = None, ""
+        try:
+            comm = dev.RcclComm(uid[0], self.world_size, self.rank, torch.cuda.current_device())
+        except Exception as e:  # noqa: BLE001 - agreed on below: nobody keeps a half-built group
+            err = f"{type(e).__name__}: {e}"
+        dist.all_gather_object(flags, err, group=g)  # second agreement: every rank joined
+        if any(flags):
+            if comm is not None:
+                comm.abort()
+            raise RuntimeError(f"native RCCL communicator init failed on some rank: {flags}")
         atexit.register(comm.abort)  # no-op once closed
         return comm
 

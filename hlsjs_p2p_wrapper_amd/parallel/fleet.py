@@ -94,7 +94,12 @@ class _RemoteRequest:
     def abort(self) -> None:
         if not self.aborted and not self.done:
             self.aborted = True
-            self.node._aborts.append(self.rid)
+            node = self.node
+            node._aborts.append(self.rid)
+            # the node never answers an aborted request: forget it here (a late answer that
+            # crossed the abort finds no pending entry and is dropped)
+            if node._pending.pop(self.rid, None) is not None:
+                node.inflight -= 1
 
 
 class _RemoteStore:

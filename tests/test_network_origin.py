@@ -28,6 +28,8 @@ class _Cdn:
     def __init__(self, num_segments=10):
         cdn = self
         self.sent = {}
+        self.ignore_range = False  # answer a Range request with 200 and the whole resource
+        self.bad_content_range = False  # answer 206 with a Content-Range of other bytes
         self.lock = threading.Lock()
 
         class H(BaseHTTPRequestHandler):
@@ -38,7 +40,7 @@ class _Cdn:
                 rel = path[len("/vod/"):] if path.startswith("/vod/") else None
                 rng = None
                 r = self.headers.get("Range")
-                if r:
+                if r and not cdn.ignore_range:
                     s, e = r.split("=")[1].split("-")
                     rng = (int(s), int(e) if e else None)
                 try:
@@ -58,6 +60,9 @@ class _Cdn:
                 else:
                     data = bytes(body)
                 self.send_response(resp.status)
+                if rng is not None:
+                    s0 = rng[0] + (1 if cdn.bad_content_range else 0)
+                    self.send_header("Content-Range", f"bytes {s0}-{s0 + len(data) - 1}/*")
                 self.send_header("Content-Length", str(len(data)))
                 self.end_headers()
                 self.wfile.write(data)
@@ -131,6 +136,47 @@ def test_http_origin_text_binary_range_and_errors(cdn):
         assert done.wait(10) and res["n"] is None and res["err"].status == 404
     finally:
         o.close()
+
+
+def test_range_request_against_a_cdn_that_ignores_range(cdn):
+    """A CDN answering a Range request with 200 + the whole file: only the requested bytes are
+    staged; a 206 whose Content-Range names other bytes is an error, not silent corruption."""
+    o = HttpOrigin(cdn.base, pin_memory=False, register=False, workers=2)
+    path = "r0/seg2.ts"
+    data, off, n, _ = cdn.origin.resource(path)
+    ref = data[off:off + n].numpy()
+    done = threading.Event()
+    res = {}
+
+    def cb(length, err):
+        res["n"], res["err"] = length, err
+        done.set()
+
+    try:
+        cdn.ignore_range = True
+        rng = (376, 376 + 188 * 5 - 1)
+        o.stage(path, cdn.base + path, rng, {}, cb)
+        assert done.wait(10) and res["err"] is None and res["n"] == 188 * 5
+        t, toff, tn, _ = o.resource_range(path, rng)
+        assert tn == 188 * 5 and np.array_equal(t[toff:toff + tn].numpy(), ref[376:376 + 188 * 5])
+        cdn.ignore_range = False
+        cdn.bad_content_range = True
+        done.clear()
+        o.stage(path, cdn.base + path, (0, 187), {}, cb)
+        assert done.wait(10) and res["n"] is None and res["err"].status == 502
+    finally:
+        o.close()
+
+
+def test_stage_after_close_completes_with_an_error(cdn):
+    """Work submitted to (or cancelled by) a closed origin still calls back, so the node's loop
+    hold is always released."""
+    o = HttpOrigin(cdn.base, pin_memory=False, register=False, workers=1)
+    o.close()
+    got = []
+    o.stage("r0/seg1.ts", cdn.base + "r0/seg1.ts", None, {}, lambda n, e: got.append((n, e)))
+    o.serve_async("master.m3u8", cdn.base + "master.m3u8", None, {}, False, lambda r, e: got.append((r, e)))
+    assert len(got) == 2 and all(x is None and e.status == 0 for x, e in got)
 
 
 def test_network_error_is_status_zero():

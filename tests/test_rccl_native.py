@@ -83,17 +83,27 @@ def test_native_rccl_self_exchange_on_stream(cuda):
 
 
 @pytest.mark.gpu
-def test_distcomm_uses_native_rccl_in_an_nccl_group(cuda):
-    """DistComm over a one-rank nccl group opens the native plane and moves a round's
-    (segment buffer, CRC trailer) pair through it on the node-style side stream."""
+@pytest.mark.parametrize("group", ["nccl", "gloo+rccl"])
+def test_distcomm_uses_native_rccl(cuda, group):
+    """DistComm opens the native plane and moves a round's (segment buffer, CRC trailer) pair
+    through it on the node-style side stream: over a one-rank nccl group, and over the gloo
+    default group that ``bench.py`` uses (HLSP2P_DATA_PLANE=rccl), where the native
+    communicator is the rank's only RCCL communicator and the decrypt grid leaves CUs free."""
+    init = ("dist.init_process_group('nccl', init_method='tcp://127.0.0.1:%d', world_size=1, rank=0, device_id=dev)"
+            if group == "nccl" else
+            "dist.init_process_group('gloo', init_method='tcp://127.0.0.1:%d', world_size=1, rank=0)") % _free_port()
     code = f"""
 import torch, torch.distributed as dist
 from hlsjs_p2p_wrapper_amd.parallel.comm import DistComm
+from hlsjs_p2p_wrapper_amd.ops._native import device as _dev
 dev = torch.device('cuda', 0)
 torch.cuda.set_device(dev)
-dist.init_process_group('nccl', init_method='tcp://127.0.0.1:{_free_port()}', world_size=1, rank=0, device_id=dev)
+{init}
 c = DistComm()
 assert c.data_transport == 'rccl-native', c.data_transport
+if '{group}' != 'nccl':
+    assert c.data_backend == 'gloo' and c.data_group is None  # no torch RCCL communicator
+    assert _dev().cu_reserve() == 8
 buf = torch.arange(1 << 20, dtype=torch.int32, device=dev).view(torch.uint8)
 tr = torch.tensor([7, 8, 9], dtype=torch.int32, device=dev)
 rb, rt = torch.empty_like(buf), torch.empty_like(tr)
@@ -107,6 +117,9 @@ c.close()
 dist.destroy_process_group()
 print('NATIVE_OK')
 """
+    env = dict(os.environ, PYTHONPATH=str(REPO))
+    if group != "nccl":
+        env["HLSP2P_DATA_PLANE"] = "rccl"
     p = subprocess.run([sys.executable, "-c", code], cwd=REPO, capture_output=True, text=True, timeout=180,
-                       env=dict(os.environ, PYTHONPATH=str(REPO)))
+                       env=env)
     assert p.returncode == 0 and "NATIVE_OK" in p.stdout, (p.stdout[-2000:], p.stderr[-4000:])
