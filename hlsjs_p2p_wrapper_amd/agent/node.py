@@ -30,7 +30,6 @@ zero-copy ``uint8`` view of the arena, or ``onError(HttpError)``
 from __future__ import annotations
 
 import contextlib
-import itertools
 import logging
 import os
 import threading
@@ -66,10 +65,17 @@ def swarm_id_for(content_id: str) -> int:
 _M32 = 0xFFFFFFFF
 
 
-class Request:
-    """One ``getSegment`` request: the loader handle (``abort()``) and its delivery state."""
+W_FORCE_CDN, W_NOT_STAGED, W_STAGING, W_PREFETCH, W_PY, W_CORRUPT = 1, 2, 4, 8, 16, 32
+W_ON_DEV = 64  # the origin bytes live in device memory (diagnostic HBM origin): D2D copies
+SRC_CDN, SRC_P2P, SRC_CACHE = 0, 1, 2  # source codes of delivery columns (parallel/fleet.SOURCES)
+SOURCE_NAMES = ("cdn", "p2p", "cache")
 
-    __slots__ = ("node", "key", "url", "headers", "callbacks", "agent", "aborted", "done", "t_submit")
+
+class Request:
+    """One in-process ``getSegment`` request: the loader handle (``abort()``) and its
+    delivery state.  Its want-table token is negative (fleet tokens are >= 0)."""
+
+    __slots__ = ("node", "key", "url", "headers", "callbacks", "agent", "aborted", "done", "t_submit", "token")
 
     def __init__(self, node: "SwarmNode", key: Tuple[int, int, int, int], url: str, headers: Dict[str, str],
                  callbacks: Any, agent: Any = None, aborted: bool = False, done: bool = False,
@@ -83,65 +89,32 @@ class Request:
         self.aborted = aborted
         self.done = done
         self.t_submit = t_submit
+        self.token = None
 
     def abort(self) -> None:
-        self.aborted = True
+        if not self.aborted:
+            self.aborted = True
+            if self.token is not None:
+                self.node._abort_token(self.token)
 
     def __repr__(self) -> str:
         return f"Request(key={self.key}, url={self.url!r}, aborted={self.aborted}, done={self.done})"
 
 
-class _Want:
-    """One wanted segment of this rank (all requests for one key share it).  Slotted plain
-    class: one per request, and a dataclass ``__init__`` is interpreted code even here."""
+class _WantX:
+    """Python-side state of a want whose bytes the CDN phase cannot take from a fixed
+    address: a network origin (staged into host memory first) or a live origin (resolved at
+    fetch time).  Every other want is a row of the native want table only."""
 
-    __slots__ = ("key", "url", "headers", "size", "want_id", "waiters", "force_cdn", "attempts", "round",
-                 "prefetch", "row", "net", "staged", "staging", "src", "loc")
+    __slots__ = ("url", "headers", "net", "src", "staged", "staging")
 
-    def __init__(self, key: Tuple[int, int, int, int], url: str, headers: Dict[str, str], size: int,
-                 want_id: int, waiters: Optional[List[Request]] = None, force_cdn: bool = False,
-                 attempts: int = 0, round: int = -1, prefetch: bool = False) -> None:
-        self.key = key
+    def __init__(self, url: str, headers: Dict[str, str], net=None, src=None, staged: bool = True) -> None:
         self.url = url
         self.headers = headers
-        self.size = size
-        self.want_id = want_id
-        self.waiters = [] if waiters is None else waiters
-        self.force_cdn = force_cdn
-        self.attempts = attempts
-        self.round = round  # round it is in flight in (-1: waiting)
-        self.prefetch = prefetch  # issued by an agent's prefetch planner (may have no waiters)
-        self.row = ()  # control-message encoding (key x4, size, want_id | force_cdn << 62 | ...)
-        # network origin (net/network.py): (origin, path, range); the body must be staged in
-        # host memory (staged) before a round may fetch it; staging: download in progress
-        self.net = None
-        self.staged = True
+        self.net = net  # (origin, path, range) of a network origin
+        self.src = src  # (origin, path, range) resolved again at fetch time
+        self.staged = staged
         self.staging = False
-        self.src = None  # (origin, path, range) resolved at creation: the CDN phase reuses it
-        self.loc = None  # (host tensor, offset, length) when the origin's bytes never move (VOD)
-
-    def __repr__(self) -> str:
-        return f"_Want(key={self.key}, size={self.size}, want_id={self.want_id}, round={self.round})"
-
-    def encode(self) -> None:
-        self.row = (*self.key, self.size,
-                    self.want_id | ((1 if self.force_cdn else 0) << 62) | ((0 if self.staged else 1) << 61)
-                    | ((1 if self.staging else 0) << 60))
-
-
-class _Completion:
-    __slots__ = ("req", "data", "source", "nbytes", "cdn_ms", "p2p_ms", "entry", "delay", "peer")
-
-    def __init__(self, req, data, source, nbytes, cdn_ms, p2p_ms, entry=-1, delay=0.0, peer=-1):
-        self.peer = peer
-        self.req = req
-        self.data = data
-        self.source = source
-        self.nbytes = nbytes
-        self.cdn_ms = cdn_ms
-        self.p2p_ms = p2p_ms
-        self.entry = entry
-        self.delay = delay
 
 
 @dataclass(eq=False)
@@ -149,13 +122,15 @@ class RoundHandle:
     round: int
     all_leaving: bool
     empty: bool = True
-    wants: List[_Want] = field(default_factory=list)
-    by_id: Dict[int, _Want] = field(default_factory=dict)
-    cdn_entries: List[Tuple[_Want, int, int, int]] = field(default_factory=list)
-    # received segments, plain ints: (want_id, src rank, entry id, arena offset, length)
-    recv_entries: List[Tuple[int, int, int, int, int]] = field(default_factory=list)
+    ids: Any = None  # want ids admitted into this round (int64[k])
+    # CDN fetches of this rank: want ids, store entry ids, arena offsets, lengths, keys [n, 4]
+    cdn: Any = None
+    # received segments: want ids, source ranks, entry ids, arena offsets, lengths, keys [n, 4]
+    recv: Any = None
+    failed: Any = None  # want ids failed in the CDN phase (origin error)
     send_pins: Optional[np.ndarray] = None
     hold: List[np.ndarray] = field(default_factory=list)  # in-flight entries pinned until delivered
+    keep: List[Any] = field(default_factory=list)  # origin buffers this round's DMAs read
     release: List[Any] = field(default_factory=list)  # network-origin wants whose staged copy this round DMAs
     sent_bytes: int = 0
     ev_cdn: Any = None
@@ -190,7 +165,13 @@ class _EventPool:
 
 class SwarmNode:
     """One swarm peer (one GPU per process): HBM segment cache, collective exchange rounds,
-    the request queue the peer agents feed."""
+    and the want table every request of the rank joins.
+
+    Two request paths feed the same table: :meth:`request` (one ``getSegment`` of an
+    in-process agent: a :class:`Request` handle and loader callbacks) and
+    :meth:`request_batch` (columns of requests, e.g. a fleet's player processes: tokens in,
+    delivery columns out through :meth:`set_bulk_sink`, no per-request Python object)."""
+
     def __init__(self, comm: Optional[SwarmComm] = None, device: Any = "auto", cache_bytes: int = 1 << 30,
                  loop=None, cdn_dedup: bool = True, round_interval_ms: Optional[float] = None,
                  auto_tick: bool = True, max_wants_per_round: Optional[int] = None) -> None:
@@ -220,8 +201,12 @@ class SwarmNode:
                             os.environ.get("HLSP2P_COPY_STREAM", "1") != "0" else None)
         self._events = _EventPool()
         self.online = True
-        self.upload_on = True
-        self.download_on = True
+        self._upload_default = True
+        self._download_default = True
+        # per-session P2P toggles (p2pDownloadOn / p2pUploadOn of each attached agent or fleet
+        # player): a session with download off gets its fragments from the CDN only; the node
+        # serves peers while any session (or the node default, without sessions) has upload on
+        self._sessions: Dict[Any, Tuple[bool, bool]] = {}
         self.cdn_dedup = cdn_dedup
         self.round = 0
         self.round_interval_ms = round_interval_ms
@@ -229,8 +214,18 @@ class SwarmNode:
         self.max_wants_per_round = max_wants_per_round
         self.leaving = False
         self.closed = False
-        self._wants: Dict[Tuple[int, int, int, int], _Want] = {}
-        self._next_want_id = 1
+        # the want table: every wanted segment and the tokens waiting for it (native rows)
+        self._wt = self.rt.WantTable()
+        self._wx: Dict[int, _WantX] = {}  # want id -> Python-side state (network / live origins)
+        self._tok_req: Dict[int, Request] = {}  # in-process request tokens (< -1) -> handle
+        self._next_tok = -2
+        self._bulk: Any = None  # delivery sink of request_batch (deliver / fail columns)
+        self._bulk_hits: List[Tuple[np.ndarray, np.ndarray]] = []  # cache hits to answer next
+        self._bulk_hits_scheduled = False
+        # (url, Range header) -> (size, address, allocation base, want flags) of VOD origin bytes
+        self._locs: Dict[Tuple[str, Optional[str]], Tuple[int, int, int, int]] = {}
+        self._locs_gen = -1
+        self._loc_keep: Dict[int, torch.Tensor] = {}  # origin allocations the table points into
         self._tick_scheduled = False
         self._timer = None
         self._pins: List[Tuple[int, np.ndarray]] = []  # (release at launch #, entry ids)
@@ -253,17 +248,51 @@ class SwarmNode:
         if self.world > 1 and auto_tick:
             self._timer = self.loop.set_interval(self._timer_tick, round_interval_ms or 10.0)
 
-    # ------------------------------------------------------------------ agents
+    # ------------------------------------------------------------------ agents / sessions
     def attach(self, agent: Any) -> None:
         """Register a peer agent (its requests, stats and metrics)."""
         self._agents.append(agent)
 
     def detach(self, agent: Any) -> None:
-        """Unregister an agent and fail its pending requests."""
+        """Unregister an agent: its pending requests are withdrawn (no callback runs)."""
         if agent in self._agents:
             self._agents.remove(agent)
-        for w in list(self._wants.values()):
-            w.waiters = [r for r in w.waiters if r.agent is not agent]
+        self._sessions.pop(agent, None)
+        gone = [t for t, r in self._tok_req.items() if r.agent is agent]
+        for t in gone:
+            self._tok_req.pop(t, None)
+            self._wt.abort1(t)
+
+    def set_session_flags(self, session: Any, download: bool, upload: bool) -> None:
+        """Per-session ``p2pDownloadOn`` / ``p2pUploadOn`` (``lib/hlsjs-p2p-wrapper.js:20-36``)."""
+        self._sessions[session] = (bool(download), bool(upload))
+
+    def session_flags(self, session: Any) -> Tuple[bool, bool]:
+        """``(download, upload)`` of a session (the node defaults until it set its own)."""
+        return self._sessions.get(session, (self._download_default, self._upload_default))
+
+    @property
+    def download_on(self) -> bool:
+        """Node-wide P2P download: on while any session (or, without sessions, the node
+        default) downloads from peers.  The setter sets the node default."""
+        if self._sessions:
+            return any(d for d, _ in self._sessions.values())
+        return self._download_default
+
+    @download_on.setter
+    def download_on(self, on: bool) -> None:
+        self._download_default = bool(on)
+
+    @property
+    def upload_on(self) -> bool:
+        """Node-wide P2P upload (serving peers): on while any session has it on."""
+        if self._sessions:
+            return any(u for _, u in self._sessions.values())
+        return self._upload_default
+
+    @upload_on.setter
+    def upload_on(self, on: bool) -> None:
+        self._upload_default = bool(on)
 
     @property
     def flags(self) -> int:
@@ -279,6 +308,56 @@ class SwarmNode:
             f |= self.rt.FLAG_CDN_DEDUP
         return f
 
+    def pending(self) -> int:
+        """Wanted segments not delivered yet."""
+        return len(self._wt)
+
+    # ------------------------------------------------------------------ sources
+    def _resolve(self, url: str, headers: Optional[Dict[str, str]]) -> Tuple[int, int, int, int, Optional[_WantX]]:
+        """Where a want's bytes come from: ``(size, address, allocation base, want flags,
+        Python state)``.  A VOD origin's bytes never move: their pinned-host (or HBM) address
+        is taken once and the CDN phase DMAs from it with no Python per want; a network
+        origin's body is staged first (size 0 and ``W_NOT_STAGED`` until then); a live
+        origin is resolved again at fetch time (its window moves)."""
+        rng_hdr = (headers.get("Range") or headers.get("range")) if headers else None
+        gen = http.generation()
+        if gen != self._locs_gen:
+            self._locs.clear()
+            self._locs_gen = gen
+        ck = (url, rng_hdr)
+        hit = self._locs.get(ck)
+        if hit is not None:
+            return hit[0], hit[1], hit[2], hit[3], None
+        origin, path = http.resolve(url)
+        rng = http.parse_range(headers) if headers else None
+        if getattr(origin, "staged_fetch", False):
+            size = origin.staged_size(path, rng)
+            self._net_wants = True
+            x = _WantX(url, dict(headers or {}), net=(origin, path, rng), staged=size is not None)
+            return int(size or 0), 0, 0, W_PY | (0 if size is not None else W_NOT_STAGED), x
+        locate = getattr(origin, "locate", None)
+        loc = locate(path, url, rng) if locate is not None else None
+        if loc is None:
+            size = origin.size(path, url, rng)
+            return int(size or 0), 0, 0, W_PY, _WantX(url, dict(headers or {}), src=(origin, path, rng))
+        data, off, n = loc
+        base = data.data_ptr()
+        flags = 0
+        if data.is_cuda:
+            flags |= W_ON_DEV
+        elif base not in self._loc_keep and self.is_cuda and not data.is_pinned():
+            raise RuntimeError("CDN origin buffers must be pinned host memory for the async H2D path")
+        self._loc_keep.setdefault(base, data)
+        corrupt = bool(getattr(origin, "_corrupt", None)) and origin.should_corrupt(path)
+        if corrupt:
+            flags |= W_CORRUPT
+        res = (int(n), base + int(off), base, flags)
+        if not corrupt and not getattr(origin, "_failures", None):
+            if len(self._locs) > 1 << 16:
+                self._locs.clear()
+            self._locs[ck] = res
+        return res[0], res[1], res[2], res[3], None
+
     # ------------------------------------------------------------------ requests
     def request(self, key: Tuple[int, int, int, int], url: str, headers: Optional[Dict[str, str]],
                 callbacks: Any, agent: Any = None, view: Any = None) -> Request:
@@ -286,102 +365,168 @@ class SwarmNode:
         a peer or the CDN in the next round.  (``view``: the agent's SegmentView, which a
         fleet's remote node uses to find the fragment's AES key; unused here.)"""
         k0, k1, k2, k3 = key
-        req = Request(self, (int(k0) & _M32, int(k1) & _M32, int(k2) & _M32, int(k3) & _M32), url,
-                      dict(headers) if headers else {}, callbacks, agent, False, False, self.loop.now())
-        eid = self.store.lookup1(*req.key)
+        k = (int(k0) & _M32, int(k1) & _M32, int(k2) & _M32, int(k3) & _M32)
+        req = Request(self, k, url, dict(headers) if headers else {}, callbacks, agent, False, False,
+                      self.loop.now())
+        eid = self.store.lookup1(*k)
         if eid >= 0:  # local cache hit
             self.store.pin(np.array([eid], dtype=np.int64))
             self.loop.call_soon(self._serve_local, req, eid)
             return req
-        self._prefetched.pop(req.key, None)  # evicted before use
-        w = self._wants.get(req.key)
-        if w is None:
+        if self._prefetched:
+            self._prefetched.pop(k, None)  # evicted before use
+        wt = self._wt
+        flags = 0
+        if agent is not None and self._sessions and not self.session_flags(agent)[0]:
+            flags = W_FORCE_CDN  # this session does not download from peers
+        size = ptr = base = 0
+        x = None
+        if wt.lookup1(*k) < 0:
             try:
-                w = self._new_want(req.key, url, req.headers)
+                size, ptr, base, wf, x = self._resolve(url, req.headers)
             except http.HttpError as e:
                 self.loop.call_soon(self._fail, req, e)
                 return req
-            self._wants[req.key] = w
-        w.waiters.append(req)
+            flags |= wf
+        tok = self._next_tok
+        self._next_tok = tok - 1
+        req.token = tok
+        self._tok_req[tok] = req
+        r = wt.add1(k[0], k[1], k[2], k[3], size, ptr, base, flags, tok)
+        if r < 0 and x is not None:
+            self._wx[-r - 1] = x
         self._schedule()
         return req
 
-    def _new_want(self, key, url: str, headers: Dict[str, str], prefetch: bool = False) -> _Want:
-        """A want for ``url``: its size from the origin, or, for a network origin whose body is
-        not staged yet, size 0 and ``staged=False`` (the planner then has it staged first)."""
-        origin, path = http.resolve(url)
-        rng = http.parse_range(headers) if headers else None
-        net = loc = None
-        if getattr(origin, "staged_fetch", False):
-            size = origin.staged_size(path, rng)
-            net = (origin, path, rng)
-        else:
-            locate = getattr(origin, "locate", None)
-            loc = locate(path, url, rng) if locate is not None else None
-            size = loc[2] if loc is not None else origin.size(path, url, rng)
-        wid = self._next_want_id
-        self._next_want_id = wid + 1
-        w = _Want(key, url, headers, int(size or 0), wid, prefetch=prefetch)
-        if net is not None:
-            w.net = net
-            w.staged = size is not None
-            self._net_wants = True
-            w.encode()
-        else:
-            w.src = (origin, path, rng)
-            w.loc = loc
-            w.row = key + (w.size, wid)  # encode() of a fresh, staged, not forced want
-        return w
+    def set_bulk_sink(self, sink: Any) -> None:
+        """Where :meth:`request_batch` deliveries go: ``sink.deliver(tokens, source, nbytes,
+        cdn_ms, p2p_ms, arena_off, entry)`` (columns; ``source`` codes ``SRC_*``; the bytes are
+        ``arena[arena_off : arena_off + nbytes]``, pinned for ``PIN_DELAY_ROUNDS`` launches)
+        and ``sink.fail(tokens, status)``."""
+        self._bulk = sink
 
-    def _stage(self, w: _Want) -> None:
-        """Plan said: download ``w``'s body from its network origin into host memory.  The
-        completion comes back to this loop; the want is planned again once staged."""
-        if w.staging or w.staged or w.net is None:
+    def request_batch(self, keys: np.ndarray, urls: List[str], headers: Optional[List[Optional[Dict[str, str]]]],
+                      tokens: np.ndarray, force_cdn: Optional[np.ndarray] = None) -> None:
+        """Columns of fragment requests (``keys`` int64[n, 4] = ``(swarm, level, urlId, sn)``,
+        one URL and optional header dict each, caller ``tokens`` >= 0 int64[n]); the answers
+        go to the bulk sink.  ``force_cdn[i]``: request ``i`` may not be served by a peer (its
+        session has P2P download off).  One native lookup for the cache, one native insert
+        into the want table; per request only a dict lookup of its URL's source."""
+        n = len(tokens)
+        if n == 0:
             return
-        origin, path, rng = w.net
-        w.staging = True
-        w.encode()  # published as downloading: the planner stages it nowhere else meanwhile
+        keys = np.ascontiguousarray(np.asarray(keys, dtype=np.int64).reshape(n, 4) & _M32)
+        tokens = np.ascontiguousarray(tokens, dtype=np.int64)
+        eids = self.store.lookup(keys, False)
+        hit = eids >= 0
+        if hit.any():
+            he = eids[hit]
+            self.store.pin(he)
+            self._bulk_hits.append((tokens[hit], he))
+            if not self._bulk_hits_scheduled:
+                self._bulk_hits_scheduled = True
+                self.loop.call_soon(self._serve_bulk_hits)
+            miss = np.flatnonzero(~hit)
+            if not len(miss):
+                return
+        else:
+            miss = None
+        idx = range(n) if miss is None else miss.tolist()
+        m = n if miss is None else len(miss)
+        sizes = np.zeros(m, dtype=np.int64)
+        ptrs = np.zeros(m, dtype=np.int64)
+        bases = np.zeros(m, dtype=np.int64)
+        flags = np.zeros(m, dtype=np.int64)
+        if force_cdn is not None:
+            fc = np.asarray(force_cdn, dtype=bool)
+            flags[:] = np.where(fc if miss is None else fc[miss], W_FORCE_CDN, 0)
+        xs: Dict[int, _WantX] = {}
+        bad: List[Tuple[int, int]] = []
+        resolve = self._resolve
+        for j, i in enumerate(idx):
+            try:
+                sizes[j], ptrs[j], bases[j], wf, x = resolve(urls[i], headers[i] if headers is not None else None)
+            except http.HttpError as e:
+                bad.append((j, int(e.status or 0) or 500))
+                continue
+            flags[j] |= wf
+            if x is not None:
+                xs[j] = x
+        sel_keys = keys if miss is None else keys[miss]
+        sel_tok = tokens if miss is None else tokens[miss]
+        if bad:
+            bj = np.asarray([j for j, _ in bad], dtype=np.int64)
+            self._fail_bulk(sel_tok[bj], np.asarray([s for _, s in bad], dtype=np.int64))
+            keep = np.ones(m, dtype=bool)
+            keep[bj] = False
+            remap = np.cumsum(keep) - 1
+            xs = {int(remap[j]): x for j, x in xs.items()}
+            sel_keys, sel_tok = sel_keys[keep], sel_tok[keep]
+            sizes, ptrs, bases, flags = sizes[keep], ptrs[keep], bases[keep], flags[keep]
+        if self._prefetched:
+            for kk in map(tuple, sel_keys.tolist()):
+                self._prefetched.pop(kk, None)
+        ids, created = self._wt.add(sel_keys, sizes, ptrs, bases, flags, sel_tok)
+        for j, x in xs.items():
+            if created[j]:
+                self._wx[int(ids[j])] = x
+        self._schedule()
+
+    def abort_tokens(self, tokens: np.ndarray) -> int:
+        """Withdraw bulk requests (no answer is sent for them)."""
+        return int(self._wt.abort(np.ascontiguousarray(tokens, dtype=np.int64)))
+
+    def _abort_token(self, token: int) -> None:
+        self._tok_req.pop(token, None)
+        self._wt.abort1(token)
+
+    def _stage(self, wid: int, x: _WantX) -> None:
+        """Plan said: download want ``wid``'s body from its network origin into host memory.
+        The completion comes back to this loop; the want is planned again once staged."""
+        if x.staging or x.staged or x.net is None:
+            return
+        origin, path, rng = x.net
+        x.staging = True
+        self._wt.set(wid, -1, W_STAGING, 0)  # announced as downloading: staged nowhere else meanwhile
         loop = self.loop
         loop.hold()
 
         def done(n, err):  # worker thread
             try:
-                loop.call_soon_threadsafe(self._on_staged, w, n, err)
+                loop.call_soon_threadsafe(self._on_staged, wid, x, n, err)
             finally:
                 loop.release()
 
-        origin.stage(path, w.url, rng, w.headers, done)
+        origin.stage(path, x.url, rng, x.headers, done)
 
-    def _on_staged(self, w: _Want, n, err) -> None:
-        w.staging = False
-        w.encode()
+    def _on_staged(self, wid: int, x: _WantX, n, err) -> None:
+        x.staging = False
+        alive = self._wx.get(wid) is x
         if err is not None:
-            if self._wants.get(w.key) is w:
-                del self._wants[w.key]
-            for req in w.waiters:
-                self._fail(req, err)
+            if alive:
+                self._finish_failed(np.array([wid], dtype=np.int64), err)
             return
-        w.size = int(n)
-        w.staged = True
-        w.encode()
-        if self._wants.get(w.key) is w:
+        x.staged = True
+        if alive and self._wt.set(wid, int(n), 0, W_STAGING | W_NOT_STAGED):
             self._schedule()
         else:  # nobody waits any more (aborted / served meanwhile): drop the host copy
-            origin, path, rng = w.net
+            origin, path, rng = x.net
             origin.release(path, rng)
 
     def prefetch(self, key: Tuple[int, int, int, int], url: str, headers: Optional[Dict[str, str]] = None) -> bool:
         """Fill the cache with a segment no player asked for yet (agent prefetch planning,
         SURVEY §2.3).  It travels in the next round like any want (P2P from a holder, or
         the CDN); a player request arriving meanwhile simply joins it.  True if issued."""
-        key = tuple(int(k) & 0xFFFFFFFF for k in key)
-        if key in self._wants or self.store.lookup1(*key) >= 0:
+        k = tuple(int(v) & _M32 for v in key)
+        if self._wt.lookup1(*k) >= 0 or self.store.lookup1(*k) >= 0:
             return False
         try:
-            w = self._new_want(key, url, dict(headers or {}), prefetch=True)
+            size, ptr, base, wf, x = self._resolve(url, dict(headers or {}))
         except http.HttpError:
             return False
-        self._wants[key] = w
+        r = self._wt.add1(k[0], k[1], k[2], k[3], size, ptr, base, wf | W_PREFETCH, self.rt.NO_TOKEN)
+        if r < 0 and x is not None:
+            self._wx[-r - 1] = x
         self.stats["prefetched"] += 1
         self._schedule()
         return True
@@ -393,7 +538,7 @@ class SwarmNode:
 
     def _local_tick(self) -> None:
         self._tick_scheduled = False
-        if self._wants:
+        if len(self._wt):
             self.tick()
 
     def _timer_tick(self) -> None:
@@ -409,9 +554,23 @@ class SwarmNode:
             src = self._prefetched.pop(req.key, None)
             if src is None:
                 self.stats["cache"] += n
-            self._deliver_now([_Completion(req, self.arena[off:off + n], src or "cache", n, 0.0, 0.0)])
+            self._deliver_req(req, src or "cache", n, 0.0, 0.0, self.arena[off:off + n], -1, eid)
         finally:
             self.store.unpin(np.array([eid], dtype=np.int64))
+
+    def _serve_bulk_hits(self) -> None:
+        """Answer the bulk requests that hit the cache (pinned at request time)."""
+        self._bulk_hits_scheduled = False
+        hits, self._bulk_hits = self._bulk_hits, []
+        for tok, eids in hits:
+            try:
+                ent = self.store.entries(eids)
+                offs, lens = ent[:, 0].copy(), ent[:, 1].copy()
+                self.stats["cache"] += int(lens.sum())
+                z = np.zeros(len(tok), dtype=np.float64)
+                self._deliver_cols(tok, np.full(len(tok), SRC_CACHE, dtype=np.int8), lens, z, z, offs, eids)
+            finally:
+                self.store.unpin(eids)
 
     def _fail(self, req: Request, err: Exception) -> None:
         if req.aborted or req.done:
@@ -422,12 +581,34 @@ class SwarmNode:
         if on_error is not None:
             on_error(err)
 
+    def _fail_bulk(self, tokens: np.ndarray, status: np.ndarray) -> None:
+        if self._bulk is not None and len(tokens):
+            self._bulk.fail(tokens, status)
+
+    def _finish_failed(self, wids: np.ndarray, err: http.HttpError) -> None:
+        """Remove wants whose fetch failed and report ``err`` to every waiter (the loader
+        falls through to its retry logic, as after a failed XHR)."""
+        tok, _, _ = self._wt.finish(np.ascontiguousarray(wids, dtype=np.int64))
+        for w in wids.tolist():
+            x = self._wx.pop(w, None)
+            if x is not None and x.net is not None and x.staged:
+                x.net[0].release(x.net[1], x.net[2])
+        if not len(tok):
+            return
+        bulk = tok >= 0
+        if bulk.any():
+            self._fail_bulk(tok[bulk], np.full(int(bulk.sum()), int(err.status or 0) or 500, dtype=np.int64))
+        for t in tok[~bulk].tolist():
+            req = self._tok_req.pop(t, None)
+            if req is not None:
+                self.loop.call_soon(self._fail, req, err)
+
     # ------------------------------------------------------------------ control messages
-    def _encode(self, wants: List[_Want], adds: np.ndarray, rms: np.ndarray) -> np.ndarray:
+    def _encode(self, rows: np.ndarray, adds: np.ndarray, rms: np.ndarray) -> np.ndarray:
         hdr = np.zeros(HDR, dtype=np.int64)
         hdr[0] = MAGIC
         hdr[1] = self.flags
-        hdr[2] = len(wants)
+        hdr[2] = len(rows)
         hdr[3] = len(adds)
         hdr[4] = len(rms)
         hdr[5] = 1 if self.leaving else 0
@@ -435,13 +616,7 @@ class SwarmNode:
         hdr[7] = self.stats["cdn"]
         hdr[8] = self.stats["p2p"]
         hdr[9] = self.stats["upload"]
-        if wants:
-            # rows pre-encoded at want creation: one flat fromiter (~3x faster than np.array of tuples)
-            w = np.fromiter(itertools.chain.from_iterable([x.row for x in wants]), dtype=np.int64,
-                            count=6 * len(wants))
-        else:
-            w = np.zeros((0, 6), dtype=np.int64)
-        return np.concatenate([hdr, w.reshape(-1), adds.reshape(-1).astype(np.int64),
+        return np.concatenate([hdr, rows.reshape(-1), adds.reshape(-1).astype(np.int64),
                                rms.reshape(-1).astype(np.int64)])
 
     def _grow_crc(self, n: int) -> None:
@@ -466,45 +641,41 @@ class SwarmNode:
         t0 = time.perf_counter()
         self.round += 1
         self.stats["rounds"] += 1
-        keep = []
-        for rel, ids in self._pins:
-            if rel <= self.round:
-                self.store.unpin(ids)
-            else:
-                keep.append((rel, ids))
-        self._pins = keep
+        if self._pins:
+            keep = []
+            for rel, ids in self._pins:
+                if rel <= self.round:
+                    self.store.unpin(ids)
+                else:
+                    keep.append((rel, ids))
+            self._pins = keep
         # ---------------- 1. control plane
         for agent in self._agents:  # agents plan (prefetch, live-window eviction) before wants go out
             hook = getattr(agent, "before_round", None)
             if hook is not None:
                 hook()
-        wants, spec = [], []  # player requests first, then speculative (prefetch-only) wants
+        # the round's wants, in one native pass: FIFO, requests before prefetch, capped,
+        # admitted only as far as the HBM ring can place them now (backpressure)
         cap = self.max_wants_per_round
-        for k in list(self._wants):
-            w = self._wants[k]
-            if w.round >= 0:
-                continue
-            if not w.waiters and w.prefetch:
-                spec.append(w)
-                continue
-            if not any(not r.aborted for r in w.waiters):
-                del self._wants[k]
-                if w.net is not None and w.staged:  # nobody wants it any more: drop the host copy
-                    w.net[0].release(w.net[1], w.net[2])
-                continue
-            wants.append(w)
-            if cap is not None and len(wants) >= cap:
-                break
-        if spec and (cap is None or len(wants) < cap):
-            wants.extend(spec if cap is None else spec[:cap - len(wants)])
-        wants = self._admit(wants)
+        ids, rows, dropped, too_big, deferred = self._wt.select(self.store, self.directory,
+                                                               -1 if cap is None else int(cap), self.round)
+        if len(dropped) and self._wx:  # every waiter aborted: drop staged host copies
+            for w in dropped.tolist():
+                x = self._wx.pop(w, None)
+                if x is not None and x.net is not None and x.staged:
+                    x.net[0].release(x.net[1], x.net[2])
+        if len(too_big):
+            self._finish_failed(too_big, http.HttpError(507, "", f"segment exceeds the {self.cache_bytes}-byte cache"))
+        if deferred:
+            self.stats["deferred"] = self.stats.get("deferred", 0) + int(deferred)
         adds, rms = self.store.take_delta()
-        parts = self.comm.allgather_control(self._encode(wants, adds, rms))
+        parts = self.comm.allgather_control(self._encode(rows, adds, rms))
         # every rank's deltas into the directory + the round's want rows, in one native call
         all_wants, flags, all_leaving, swarm_tot = rt.ingest_control(self.directory, parts, MAGIC, HDR)
         self.peer_online = (flags & rt.FLAG_ONLINE) != 0
         self.swarm_stats = {"cdn": int(swarm_tot[0]), "p2p": int(swarm_tot[1]), "upload": int(swarm_tot[2])}
         h = RoundHandle(self.round, all_leaving, t0=t0)
+        h.ids = ids
         t_ctrl = time.perf_counter()
         self.timer.add("control", t_ctrl - t0)
         if not len(all_wants):
@@ -512,17 +683,13 @@ class SwarmNode:
         h.empty = False
         plan = rt.plan_round(self.directory, all_wants, flags, self.world)
         me = self.rank
-        h.wants = wants
-        h.by_id = {w.want_id: w for w in wants}
-        for w in wants:
-            w.round = self.round
         h.n_wants = len(all_wants)
         cdn_rows = plan[(plan[:, 5] == -1) & (plan[:, 6] == me)]
-        if self._net_wants:  # network-origin wants this rank must download first (STAGE rows)
+        if self._net_wants and self._wx:  # network-origin wants this rank must download first (STAGE rows)
             for wid in plan[(plan[:, 5] == -2) & (plan[:, 6] == me), 7].tolist():
-                w = h.by_id.get(wid)
-                if w is not None:
-                    self._stage(w)
+                x = self._wx.get(wid)
+                if x is not None:
+                    self._stage(wid, x)
         send_rows = plan[plan[:, 5] == me]
         recv_rows = plan[(plan[:, 6] == me) & (plan[:, 5] >= 0)]
         h.n_send = len(send_rows)
@@ -531,9 +698,9 @@ class SwarmNode:
         send_eids = np.full(len(send_rows), -1, dtype=np.int64)
         cached = send_rows[:, 8] == 0
         if cached.any():
-            ids = self.store.lookup(np.ascontiguousarray(send_rows[cached, :4]), False)
-            send_eids[cached] = ids
-            valid = ids[ids >= 0]
+            eids = self.store.lookup(np.ascontiguousarray(send_rows[cached, :4]), False)
+            send_eids[cached] = eids
+            valid = eids[eids >= 0]
             if len(valid):
                 self.store.pin(valid)
                 h.send_pins = valid
@@ -544,9 +711,9 @@ class SwarmNode:
             if len(cdn_rows):
                 self._cdn_phase(h, cdn_rows)
                 seeded = np.flatnonzero(~cached)
-                if len(seeded) and h.cdn_entries:  # forwarded in this same round
-                    fetched = {w.key: eid for w, eid, _, _ in h.cdn_entries}
-                    send_eids[seeded] = [fetched.get(k, -1) for k in map(tuple, send_rows[seeded, :4].tolist())]
+                if len(seeded) and h.cdn is not None:  # forwarded in this same round: the CDN
+                    # phase committed (and pinned) them, so the store finds them by key
+                    send_eids[seeded] = self.store.lookup(np.ascontiguousarray(send_rows[seeded, :4]), False)
             t_p2p0 = time.perf_counter()
             self.timer.add("cdn_enqueue", t_p2p0 - t_cdn0)
             # ---------------- 4. P2P phase: entered by EVERY rank when the (identical) plan
@@ -568,6 +735,8 @@ class SwarmNode:
         h.completed = True
         if h.empty:
             self.last_round = {"wants": 0, "ms": (time.perf_counter() - h.t0) * 1e3}
+            if h.ids is not None and len(h.ids):  # (a lone rank's wants always plan: defensive)
+                self._wt.requeue(h.ids, False)
             return
         t0 = time.perf_counter()
         if h.done is not None and not h.done.query():
@@ -583,84 +752,92 @@ class SwarmNode:
         if h.done is not None:
             self._events.put(False, h.done)
             h.done = None
-        okl = h.ok_host.numpy().tolist() if h.ok_host is not None else None
-        if okl is None or all(okl):
-            good, bad = h.recv_entries, []
-        else:
-            good = [e for e, k in zip(h.recv_entries, okl) if k]
-            bad = [e for e, k in zip(h.recv_entries, okl) if not k]
-        if good:
-            self.store.commit(np.asarray([e[2] for e in good], dtype=np.int64))
-        if bad:
-            self.store.drop(np.asarray([e[2] for e in bad], dtype=np.int64))
-            self.stats["crc_failures"] += len(bad)
+        wt = self._wt
+        recv = h.recv
+        good = bad = None
+        if recv is not None:
+            ok = (h.ok_host.numpy() if isinstance(h.ok_host, torch.Tensor) else np.asarray(h.ok_host)).astype(bool)
+            if ok.all():
+                good = recv
+            else:
+                good = tuple(c[ok] for c in recv)
+                bad = tuple(c[~ok] for c in recv)
+            if len(good[0]):
+                self.store.commit(good[2])
+            if bad is not None:
+                self.store.drop(bad[2])
+                self.stats["crc_failures"] += len(bad[0])
         if h.send_pins is not None:
             self.store.unpin(h.send_pins)
-        for w in h.release:  # the round's DMAs are done: drop the staged host copies
-            origin, path, rng = w.net
+        for x in h.release:  # the round's DMAs are done: drop the staged host copies
+            origin, path, rng = x.net
             origin.release(path, rng)
         self.stats["upload"] += h.sent_bytes
-        completions: List[_Completion] = []
-        cdn_views = self._views([e[2] for e in h.cdn_entries], [e[3] for e in h.cdn_entries])
-        cdn_ms = max(h.cdn_ms, h.shaped_ms)
-        for (w, eid, off, n), view in zip(h.cdn_entries, cdn_views):
-            if self._wants.get(w.key) is w:
-                del self._wants[w.key]
-            if w.prefetch and not w.waiters:
-                self._prefetched[w.key] = "cdn"
-            for req in w.waiters:
-                completions.append(_Completion(req, view, "cdn", n, cdn_ms, 0.0, eid, h.shaped_ms))
-        link_q: Dict[int, int] = {}  # slow-link fault injection: bytes queued per source link
-        link_kbps = self.link_kbps
-        wants_map = self._wants
-        p2p_views = self._views([e[3] for e in good], [e[4] for e in good])
-        for (want_id, src, eid, off, n), view in zip(good, p2p_views):
-            w = h.by_id.get(want_id)
-            if w is None:
-                continue
-            if wants_map.get(w.key) is w:
-                del wants_map[w.key]
-            if w.net is not None and w.staged:  # staged here, but a peer's copy came first
-                w.net[0].release(w.net[1], w.net[2])
-            if w.prefetch and not w.waiters:
-                self._prefetched[w.key] = "p2p"
-            p2p_ms, delay = h.p2p_ms, 0.0
-            kbps = link_kbps.get(src) if link_kbps else None
-            if kbps:
-                link_q[src] = link_q.get(src, 0) + n
-                delay = link_q[src] * 8.0 / kbps  # kbit/s == bit/ms
-                p2p_ms = max(p2p_ms, delay)
-            for req in w.waiters:
-                completions.append(_Completion(req, view, "p2p", n, 0.0, p2p_ms, eid, delay, peer=src))
-        for e in bad:
-            w = h.by_id.get(e[0])
-            if w is not None:
-                w.force_cdn = True  # corrupted peer copy: go to the CDN next round
-                w.encode()
-                w.attempts += 1
-                w.round = -1
-        served = None
-        for w in h.wants:  # planned but not served (e.g. a CDN error already reported)
-            if w.round == h.round and wants_map.get(w.key) is w:
-                if served is None:
-                    served = {id(e[0]) for e in h.cdn_entries}
-                    served.update(id(h.by_id.get(e[0])) for e in h.recv_entries)
-                if id(w) not in served:
-                    w.round = -1
         t2 = time.perf_counter()
-        self.timer.add("commit", t2 - t1)
-        self._deliver(completions)  # delivered entries stay pinned PIN_DELAY_ROUNDS launches
+        # ---- deliveries: served wants leave the table, their tokens come back as columns
+        if h.cdn is not None and len(h.cdn[0]):
+            wids, eids, offs, lens = h.cdn[0], h.cdn[1], h.cdn[2], h.cdn[3]
+            tok, idx, pf = wt.finish(wids)
+            self._after_finish(wids, pf, h.cdn[4], "cdn")
+            cdn_ms = max(h.cdn_ms, h.shaped_ms)
+            k = len(tok)
+            if k:
+                self._deliver_cols(tok, np.zeros(k, dtype=np.int8), lens[idx], np.full(k, cdn_ms),
+                                   np.zeros(k), offs[idx], eids[idx], delay=h.shaped_ms)
+        if good is not None and len(good[0]):
+            wids, srcs, eids, offs, lens, keys = good
+            tok, idx, pf = wt.finish(wids)
+            self._after_finish(wids, pf, keys, "p2p")
+            k = len(tok)
+            if k:
+                p2p_ms = np.full(len(wids), h.p2p_ms)
+                delay = None
+                if self.link_kbps:  # slow-link fault injection: bytes queued per source link
+                    delay = np.zeros(len(wids))
+                    link_q: Dict[int, int] = {}
+                    for i, (src, n) in enumerate(zip(srcs.tolist(), lens.tolist())):
+                        kbps = self.link_kbps.get(src)
+                        if kbps:
+                            link_q[src] = link_q.get(src, 0) + n
+                            delay[i] = link_q[src] * 8.0 / kbps  # kbit/s == bit/ms
+                            p2p_ms[i] = max(p2p_ms[i], delay[i])
+                    delay = delay[idx]
+                self._deliver_cols(tok, np.ones(k, dtype=np.int8), lens[idx], np.zeros(k), p2p_ms[idx], offs[idx],
+                                   eids[idx], peers=srcs[idx], delay=delay)
+        if bad is not None and len(bad[0]):
+            wt.requeue(bad[0], True)  # corrupted peer copy: from the CDN next round
+        # planned but not served (a STAGE row, a CDN error already reported): waiting again
+        if h.ids is not None and len(h.ids):
+            served = [a for a in (h.cdn[0] if h.cdn is not None else None,
+                                  h.recv[0] if h.recv is not None else None, h.failed) if a is not None and len(a)]
+            rest = np.setdiff1d(h.ids, np.concatenate(served), assume_unique=False) if served else h.ids
+            if len(rest):
+                wt.requeue(rest, False)
         for ids in h.hold:  # in-flight pins from reservation (dropped entries: no-op)
             self.store.unpin(ids)
         h.hold = []
+        self.timer.add("commit", t2 - t1)
         self.timer.add("deliver", time.perf_counter() - t2)
         self.timer.add("dev_cdn_ms", h.cdn_ms / 1e3)
         self.timer.add("dev_p2p_ms", h.p2p_ms / 1e3)
-        self.last_round = {"wants": h.n_wants, "cdn": len(h.cdn_entries), "send": h.n_send,
-                           "recv": len(h.recv_entries), "cdn_ms": h.cdn_ms, "dmas": h.dmas, "p2p_ms": h.p2p_ms,
-                           "ms": (time.perf_counter() - h.t0) * 1e3}
-        if any(w.round < 0 and not w.staging for w in self._wants.values()):
+        self.last_round = {"wants": h.n_wants, "cdn": 0 if h.cdn is None else len(h.cdn[0]), "send": h.n_send,
+                           "recv": 0 if h.recv is None else len(h.recv[0]), "cdn_ms": h.cdn_ms, "dmas": h.dmas,
+                           "p2p_ms": h.p2p_ms, "ms": (time.perf_counter() - h.t0) * 1e3}
+        if wt.waiting:
             self._schedule()  # (a want being downloaded is rescheduled when it lands)
+
+    def _after_finish(self, wids: np.ndarray, prefetch_only: np.ndarray, keys: np.ndarray, source: str) -> None:
+        """Bookkeeping of wants that just left the table: Python-side state, and where a
+        prefetched segment nobody asked for yet came from (its first cache hit is accounted
+        as that source)."""
+        if self._wx:
+            for w in wids.tolist():
+                x = self._wx.pop(w, None)
+                if x is not None and x.net is not None and x.staged and source == "p2p":
+                    x.net[0].release(x.net[1], x.net[2])  # staged here, but a peer's copy came first
+        if prefetch_only.any():
+            for i in np.flatnonzero(prefetch_only).tolist():
+                self._prefetched[tuple(int(v) for v in keys[i])] = source
 
     ROUND_SPIN_S = 0.02  # busy-poll a round's completion this long before checking for peer failures
 
@@ -692,7 +869,7 @@ class SwarmNode:
     def _views(self, offs: List[int], lens: List[int]) -> List[torch.Tensor]:
         """Zero-copy uint8 views of the arena for a round's deliveries (one native call on
         the GPU; a Python slice costs ~1.5 us per view)."""
-        if not offs:
+        if not len(offs):
             return []
         if self.is_cuda:
             from ..ops._native import device as _dev
@@ -702,111 +879,98 @@ class SwarmNode:
         return [arena[o:o + n] for o, n in zip(offs, lens)]
 
     # ------------------------------------------------------------------ phases
-    def _admit(self, wants: List[_Want]) -> List[_Want]:
-        """Backpressure: a rank only ever receives what it asked for, so cap this round's
-        wants to what the ring can place now without evicting pinned (in-flight or
-        being-consumed) entries; the rest wait for the next round."""
-        if not wants:
-            return wants
-        st = self.store
-        sizes = [st.aligned(w.size) for w in wants]
-        total = sum(sizes)
-        if st.fits(total):
-            return wants
-        lo, hi = 0, len(wants)  # largest prefix that fits
-        while lo < hi:
-            mid = (lo + hi + 1) // 2
-            if st.fits(sum(sizes[:mid])):
-                lo = mid
-            else:
-                hi = mid - 1
-        kept = wants[:lo]
-        for w, a in zip(wants[lo:], sizes[lo:]):
-            if a > self.cache_bytes:  # can never fit: fail it
-                if self._wants.get(w.key) is w:
-                    del self._wants[w.key]
-                if w.net is not None and w.staged:
-                    w.net[0].release(w.net[1], w.net[2])
-                err = http.HttpError(507, f"segment of {w.size} bytes exceeds the {self.cache_bytes}-byte cache")
-                for req in w.waiters:
-                    self.loop.call_soon(self._fail, req, err)
-        self.stats["deferred"] = self.stats.get("deferred", 0) + len(wants) - lo
-        return kept
-
     def _cdn_phase(self, h: RoundHandle, cdn_rows: np.ndarray) -> None:
-        wants, sources = [], []
-        for wid in cdn_rows[:, 7].tolist():
-            w = h.by_id.get(wid)
-            if w is None:
-                continue
+        wids = np.ascontiguousarray(cdn_rows[:, 7])
+        info = self._wt.info(wids)  # [n, 10]: key x4, size, src_ptr, src_base, flags, round, attempts
+        ptrs = info[:, 5].copy()
+        bases = info[:, 6].copy()
+        lens = info[:, 4].copy()
+        wflags = info[:, 7]
+        keep = info[:, 0] >= 0
+        failed: List[int] = []
+        slow = np.flatnonzero(keep & ((wflags & W_PY) != 0))
+        for i in slow.tolist():  # network / live origins: Python resolves the bytes now
+            wid = int(wids[i])
+            x = self._wx.get(wid)
             try:
-                if w.net is not None:  # network origin: the staged (already ranged) host copy
-                    origin, path, rng = w.net
+                if x is None:
+                    raise http.HttpError(500, "", "want lost its origin state")
+                if x.net is not None:  # network origin: the staged (already ranged) host copy
+                    origin, path, rng = x.net
                     data, off, n, _ = origin.resource_range(path, rng)
-                    corrupt = False
-                    h.release.append(w)
-                elif w.loc is not None:  # VOD origin: located when the want was created
-                    data, off, n = w.loc
-                    corrupt = w.src[0].should_corrupt(w.src[1])
+                    h.release.append(x)
+                    self._wx.pop(wid, None)
+                    x.staged = False  # released by this round
                 else:
-                    if w.src is not None:
-                        origin, path, rng = w.src
-                    else:
-                        origin, path = http.resolve(w.url)
-                        rng = http.parse_range(w.headers) if w.headers else None
+                    origin, path, rng = x.src
                     data, off, n, _ = origin.resource(path)
                     if rng is not None:
                         s, e = rng
                         e = n - 1 if e is None else min(e, n - 1)
                         off, n = off + s, max(0, e - s + 1)
-                    corrupt = origin.should_corrupt(path)
+                    if origin.should_corrupt(path):
+                        wflags[i] |= W_CORRUPT
             except http.HttpError as e:
-                if self._wants.get(w.key) is w:
-                    del self._wants[w.key]
-                for req in w.waiters:
-                    self.loop.call_soon(self._fail, req, e)
+                self._finish_failed(np.array([wid], dtype=np.int64), e)
+                failed.append(wid)
+                keep[i] = False
                 continue
-            wants.append(w)
-            sources.append((data, off, n, corrupt))
-        if not wants:
+            base = data.data_ptr()
+            if not data.is_cuda and self.is_cuda and base not in self._loc_keep and not data.is_pinned():
+                raise RuntimeError("CDN origin buffers must be pinned host memory for the async H2D path")
+            if data.is_cuda:
+                wflags[i] |= W_ON_DEV
+            h.keep.append(data)  # the source stays alive until the round completes
+            ptrs[i], bases[i], lens[i] = base + int(off), base, int(n)
+        if failed:
+            h.failed = np.asarray(failed, dtype=np.int64)
+        if not keep.all():
+            wids, ptrs, bases, lens, wflags = wids[keep], ptrs[keep], bases[keep], lens[keep], wflags[keep]
+            keys = np.ascontiguousarray(info[keep, :4])
+        else:
+            keys = np.ascontiguousarray(info[:, :4])
+        if not len(wids):
             return
-        keys = np.asarray([w.key for w in wants], dtype=np.int64)
-        lens = np.asarray([s[2] for s in sources], dtype=np.int64)
         res = self.store.reserve_run(keys, lens, self.round)
-        if res is None:  # _admit guarantees room; reaching this is a bookkeeping bug
+        if res is None:  # admission guarantees room; reaching this is a bookkeeping bug
             raise RuntimeError("segment cache cannot make room (pinned entries block eviction)")
-        _, ids, offs = res
-        self.store.pin(ids)  # in flight until delivered (complete_round unpins)
-        h.hold.append(ids)
-        self._grow_crc(int(ids.max()) + 1)
+        _, eids, offs = res
+        self.store.pin(eids)  # in flight until delivered (complete_round unpins)
+        h.hold.append(eids)
+        self._grow_crc(int(eids.max()) + 1)
         if self.is_cuda:
+            on_dev = (wflags & W_ON_DEV) != 0
+            if on_dev.any() and not on_dev.all():
+                raise RuntimeError("CDN origin buffers of one round must all be pinned host or all HBM")
             start = self._events.get(True)
             end = self._events.get(True)
             cs = self.copy_stream
             with (torch.cuda.stream(cs) if cs is not None else contextlib.nullcontext()):
                 start.record(cs if cs is not None else self.stream)
-                h.dmas = _h2d_batch(self.arena, offs, sources)
+                from ..ops._native import device as _dev
+
+                h.dmas = _dev().h2d_batch(self.arena, offs, ptrs, lens, bases, ALIGN, bool(on_dev[0]))
                 end.record(cs if cs is not None else self.stream)
             if cs is not None:
                 self.stream.wait_event(end)  # ingest CRC / forwarding sends read the DMA'd bytes
             h.ev_cdn = (start, end)
         else:
             t = time.perf_counter()
-            arena = self.arena.numpy()  # numpy slices: a small torch copy_ costs ~0.1 ms on CPU
-            for (data, off, n, _), doff in zip(sources, offs.tolist()):
-                arena[doff:doff + n] = data.numpy()[off:off + n]
+            self.rt.host_copy_batch(self.arena.data_ptr(), self.arena.numel(), offs, ptrs, lens)
             h.cdn_ms = (time.perf_counter() - t) * 1e3
-        for (_, _, n, corrupt), doff in zip(sources, offs.tolist()):
-            if corrupt and n:
-                self.arena[doff + n // 2] ^= 0xFF
-        _crc.crc32_batch(self.arena, offs, lens, scatter_to=self.crc_dev, scatter_idx=ids)  # ingest CRCs
-        self.store.commit(ids)  # announced next round; peers' reads are stream-ordered after the H2D
+        corrupt = np.flatnonzero((wflags & W_CORRUPT) != 0)
+        for i in corrupt.tolist():
+            if lens[i]:
+                self.arena[int(offs[i]) + int(lens[i]) // 2] ^= 0xFF
+        _crc.crc32_batch(self.arena, offs, lens, scatter_to=self.crc_dev, scatter_idx=eids)  # ingest CRCs
+        self.store.commit(eids)  # announced next round; peers' reads are stream-ordered after the H2D
         # CDN bandwidth shaping (xhr-shaper analog): completions are deferred by the modelled
         # transfer time of this round's CDN bytes
-        h.shaped_ms = http.Shaper.transfer_ms(int(lens.sum()))
-        self.stats["cdn"] += int(lens.sum())
-        self.stats["cdn_segments"] += len(wants)
-        h.cdn_entries = [(w, eid, o, n) for w, eid, o, n in zip(wants, ids.tolist(), offs.tolist(), lens.tolist())]
+        total = int(lens.sum())
+        h.shaped_ms = http.Shaper.transfer_ms(total)
+        self.stats["cdn"] += total
+        self.stats["cdn_segments"] += len(wids)
+        h.cdn = (wids, eids, offs, lens, keys)
 
     def _p2p_phase(self, h: RoundHandle, send_rows: np.ndarray, recv_rows: np.ndarray,
                    send_eids: np.ndarray) -> None:
@@ -845,6 +1009,7 @@ class SwarmNode:
                 sends.append((dst, buf))
                 sends.append((dst, trailer_all[a:b]))
         # --- recvs: the reserved runs; one trailer buffer for all of them
+        trailers = None
         if len(rrun):
             trailers = torch.empty(len(recv_rows), dtype=torch.int32, device=dev)
             views = self._views(rrun[:, 3].tolist(), rrun[:, 4].tolist())
@@ -853,10 +1018,8 @@ class SwarmNode:
                 recvs.append((src, trailers[a:b]))
             h.hold.append(rid_a)  # pinned by p2p_layout until complete_round
             self._grow_crc(int(rid_a.max()) + 1)
-            rlen = recv_rows[:, 4]
-            rsrc = recv_rows[:, 5]
-            h.recv_entries = list(zip(recv_rows[:, 7].tolist(), rsrc.tolist(), rid_a.tolist(), roff_a.tolist(),
-                                      rlen.tolist()))
+            h.recv = (np.ascontiguousarray(recv_rows[:, 7]), np.ascontiguousarray(recv_rows[:, 5]), rid_a, roff_a,
+                      np.ascontiguousarray(recv_rows[:, 4]), np.ascontiguousarray(recv_rows[:, :4]))
         self.timer.add("p2p_prep", time.perf_counter() - t_prep)
         t = time.perf_counter()
         if self.is_cuda:
@@ -869,11 +1032,11 @@ class SwarmNode:
             h.ev_p2p = (start, end)
         else:
             h.p2p_ms = (time.perf_counter() - t) * 1e3
-        if not h.recv_entries:
+        if h.recv is None:
             return
         if self.corrupt_next_recv > 0:  # fault injection: transport corruption
             self.corrupt_next_recv -= 1
-            o, n = h.recv_entries[0][3:5]
+            o, n = int(roff_a[0]), int(recv_rows[0, 4])
             if n:
                 self.arena[o + n // 2] ^= 0x5A
         # verify against the senders' trailers; the combine kernel also scatters the computed
@@ -890,63 +1053,99 @@ class SwarmNode:
         self.stats["p2p_segments"] += len(recv_rows)
 
     # ------------------------------------------------------------------ delivery
-    def _deliver(self, completions: List[_Completion]) -> None:
-        now_list = [c for c in completions if c.delay <= 0]
-        later = [c for c in completions if c.delay > 0]
-        if later:  # shaped CDN / slowed-link transfers complete after their modelled duration
-            ids = np.asarray([c.entry for c in later if c.entry is not None and c.entry >= 0], dtype=np.int64)
-            if len(ids):
-                self.store.pin(ids)
-            delay = max(c.delay for c in later)
-            for c in later:
-                c.delay = 0.0
-            self.loop.set_timeout(self._deliver_deferred, delay, later, ids)
-        self._deliver_now(now_list)
+    def _deliver_cols(self, tok: np.ndarray, src: np.ndarray, nbytes: np.ndarray, cdn_ms: np.ndarray,
+                      p2p_ms: np.ndarray, offs: np.ndarray, eids: np.ndarray, peers: Optional[np.ndarray] = None,
+                      delay: Any = None) -> None:
+        """Answer waiting tokens.  Entries stay pinned ``PIN_DELAY_ROUNDS`` launches (their
+        consumers read the arena asynchronously); shaped / slowed transfers are answered
+        after their modelled duration."""
+        if delay is not None and not (np.isscalar(delay) and delay <= 0):
+            d = np.broadcast_to(np.asarray(delay, dtype=np.float64), tok.shape)
+            later = d > 0
+            if later.any():
+                li = np.flatnonzero(later)
+                le = eids[li]
+                le = le[le >= 0]
+                if len(le):
+                    self.store.pin(le)
+                self.loop.set_timeout(self._deliver_deferred, float(d[li].max()),
+                                      (tok[li], src[li], nbytes[li], cdn_ms[li], p2p_ms[li], offs[li], eids[li],
+                                       None if peers is None else peers[li]), le)
+                if later.all():
+                    return
+                ni = np.flatnonzero(~later)
+                tok, src, nbytes, cdn_ms, p2p_ms, offs, eids = (tok[ni], src[ni], nbytes[ni], cdn_ms[ni], p2p_ms[ni],
+                                                                offs[ni], eids[ni])
+                peers = None if peers is None else peers[ni]
+        pin = eids[eids >= 0]
+        if len(pin):
+            self.store.pin(pin)
+            self._pins.append((self.round + PIN_DELAY_ROUNDS, pin))
+        bulk = tok >= 0
+        nb = int(bulk.sum())
+        if nb:
+            self.stats["segments"] += nb
+            if self._bulk is not None:
+                if nb == len(tok):
+                    self._bulk.deliver(tok, src, nbytes, cdn_ms, p2p_ms, offs, eids)
+                else:
+                    self._bulk.deliver(tok[bulk], src[bulk], nbytes[bulk], cdn_ms[bulk], p2p_ms[bulk], offs[bulk],
+                                       eids[bulk])
+        if nb == len(tok):
+            return
+        obj = np.flatnonzero(~bulk)
+        reqs = [self._tok_req.pop(t, None) for t in tok[obj].tolist()]
+        live = [i for i, r in zip(obj.tolist(), reqs) if r is not None]
+        if not live:
+            return
+        views = self._views(offs[live].tolist(), nbytes[live].tolist())
+        for i, r, view in zip(live, [r for r in reqs if r is not None], views):
+            self._deliver_req(r, SOURCE_NAMES[int(src[i])], int(nbytes[i]), float(cdn_ms[i]), float(p2p_ms[i]), view,
+                              self.rank if peers is None else int(peers[i]), int(eids[i]), pin=False)
 
-    def _deliver_deferred(self, completions: List[_Completion], ids: np.ndarray) -> None:
+    def _deliver_deferred(self, cols, ids: np.ndarray) -> None:
         try:
-            self._deliver_now(completions)
+            self._deliver_cols(*cols)
         finally:
             if len(ids):
                 self.store.unpin(ids)
 
-    def _deliver_now(self, completions: List[_Completion]) -> None:
-        pin = [c.entry for c in completions if c.entry is not None and c.entry >= 0]
-        if pin:
-            arr = np.asarray(pin, dtype=np.int64)
+    def _deliver_req(self, req: Request, source: str, nbytes: int, cdn_ms: float, p2p_ms: float, data: Any,
+                     peer: int, eid: int, pin: bool = True) -> None:
+        """Loader callbacks of one in-process request: ``onProgress`` then ``onSuccess``."""
+        if req.aborted or req.done:
+            return
+        if pin and eid >= 0:
+            arr = np.array([eid], dtype=np.int64)
             self.store.pin(arr)
             self._pins.append((self.round + PIN_DELAY_ROUNDS, arr))
+        req.done = True
+        self.stats["segments"] += 1
         trace = self.trace
-        now = self.loop.now() if trace is not None else 0.0
-        for c in completions:
-            req = c.req
-            if req.aborted or req.done:
-                continue
-            req.done = True
-            self.stats["segments"] += 1
-            if trace is not None:
-                xfer = c.p2p_ms if c.source == "p2p" else c.cdn_ms
-                trace.add(RequestTrace(req.key, req.t_submit, max(req.t_submit, now - xfer), now, c.source,
-                                       c.nbytes, c.peer if c.source == "p2p" else self.rank, self.round))
-            if req.agent is not None:
-                req.agent._account(c.source, c.nbytes)
-            cb = req.callbacks
-            if isinstance(cb, dict):
-                on_progress, on_success = cb.get("onProgress"), cb.get("onSuccess")
-            else:
-                delivered = getattr(cb, "onDelivered", None)
-                if delivered is not None:  # one call instead of a progress event + onSuccess (fleet)
-                    delivered(c.source, c.nbytes, c.cdn_ms, c.p2p_ms, c.data)
-                    continue
-                on_progress, on_success = getattr(cb, "onProgress", None), getattr(cb, "onSuccess", None)
-            if on_progress is not None:
-                p2p = c.source in ("p2p", "cache")
-                on_progress({"cdnDownloaded": 0 if p2p else c.nbytes, "p2pDownloaded": c.nbytes if p2p else 0,
-                             "cdnDuration": 0.0 if p2p else c.cdn_ms, "p2pDuration": c.p2p_ms if p2p else 0.0})
-            if req.aborted:
-                continue
-            if on_success is not None:
-                on_success(c.data)
+        if trace is not None:
+            now = self.loop.now()
+            xfer = p2p_ms if source == "p2p" else cdn_ms
+            trace.add(RequestTrace(req.key, req.t_submit, max(req.t_submit, now - xfer), now, source, nbytes,
+                                   peer if source == "p2p" else self.rank, self.round))
+        if req.agent is not None:
+            req.agent._account(source, nbytes)
+        cb = req.callbacks
+        if isinstance(cb, dict):
+            on_progress, on_success = cb.get("onProgress"), cb.get("onSuccess")
+        else:
+            delivered = getattr(cb, "onDelivered", None)
+            if delivered is not None:  # one call instead of a progress event + onSuccess
+                delivered(source, nbytes, cdn_ms, p2p_ms, data)
+                return
+            on_progress, on_success = getattr(cb, "onProgress", None), getattr(cb, "onSuccess", None)
+        if on_progress is not None:
+            p2p = source in ("p2p", "cache")
+            on_progress({"cdnDownloaded": 0 if p2p else nbytes, "p2pDownloaded": nbytes if p2p else 0,
+                         "cdnDuration": 0.0 if p2p else cdn_ms, "p2pDuration": p2p_ms if p2p else 0.0})
+        if req.aborted:
+            return
+        if on_success is not None:
+            on_success(data)
 
     # ------------------------------------------------------------------ lifecycle
     def enable_trace(self, maxlen: int = 100_000) -> TraceLog:
@@ -1003,17 +1202,6 @@ class SwarmNode:
         return p / (p + c) if (p + c) else 0.0
 
 
-def _runs(col: np.ndarray) -> List[Tuple[int, int, int]]:
-    """(value, start, end) of each run of equal values in a sorted column."""
-    n = len(col)
-    if n == 0:
-        return []
-    cuts = np.flatnonzero(col[1:] != col[:-1]) + 1
-    starts = [0] + cuts.tolist()
-    ends = cuts.tolist() + [n]
-    return list(zip(col[starts].tolist(), starts, ends))
-
-
 def _dev_index(idx: np.ndarray, dev: torch.device) -> torch.Tensor:
     """int64 index array on ``dev`` (pinned staging + one async H2D on GPUs)."""
     if dev.type == "cuda":
@@ -1021,33 +1209,6 @@ def _dev_index(idx: np.ndarray, dev: torch.device) -> torch.Tensor:
 
         return pack_to_device({"i": np.ascontiguousarray(idx, dtype=np.int64)}, dev)["i"]
     return torch.from_numpy(np.ascontiguousarray(idx, dtype=np.int64))
-
-
-def _h2d_batch(arena: torch.Tensor, dst_offs: np.ndarray, sources: List[Tuple[torch.Tensor, int, int, bool]]) -> None:
-    """Enqueue the pinned-host -> HBM copies of a round on the current stream in a single
-    native call; copies contiguous in both the origin pool and the arena are merged into
-    one DMA (see ``h2d_batch`` in ``kernels/bindings.cpp``)."""
-    from ..ops._native import device as _dev
-
-    bases = []
-    on_dev = sources[0][0].is_cuda
-    for d, _, _, _ in sources:
-        if d.is_cuda != on_dev:
-            raise RuntimeError("CDN origin buffers of one round must all be pinned host or all HBM")
-        p = d.data_ptr()
-        if not on_dev and p not in _PINNED_OK:
-            if not d.is_pinned():
-                raise RuntimeError("CDN origin buffers must be pinned host memory for the async H2D path")
-            _PINNED_OK.add(p)
-        bases.append(p)
-    src_alloc = np.asarray(bases, dtype=np.int64)
-    src_ptrs = src_alloc + np.asarray([o for _, o, _, _ in sources], dtype=np.int64)
-    lens = np.asarray([n for _, _, n, _ in sources], dtype=np.int64)
-    return _dev().h2d_batch(arena, np.ascontiguousarray(dst_offs, dtype=np.int64), src_ptrs, lens, src_alloc, ALIGN,
-                            on_dev)
-
-
-_PINNED_OK: set = set()  # base pointers of origin tensors already checked to be pinned
 
 
 # ---------------------------------------------------------------------- registry
@@ -1099,7 +1260,8 @@ def node_for_config(p2p_config: Any) -> SwarmNode:
     elif backend == "remote":  # fleet player process: the node lives in the GPU process
         from ..parallel.fleet import RemoteNode
 
-        node = RemoteNode(cfg["conn"], world=int(cfg.get("world", 1)), rank=int(cfg.get("rank", 0)))
+        node = RemoteNode(cfg["conn"], world=int(cfg.get("world", 1)), rank=int(cfg.get("rank", 0)),
+                          payload=bool(cfg.get("fleetPayload", False)))
         set_current_node(node)
         return node
     else:

@@ -123,7 +123,7 @@ class PeerAgent:
         current track's segments in ``[currentTime, currentTime + prefetchSeconds]`` that
         are neither cached nor in flight.  The player's own later request for one of them
         is then a local cache hit (or joins the in-flight want)."""
-        if self.prefetch_seconds <= 0 or self.disposed or self.media is None or not self.node.download_on:
+        if self.prefetch_seconds <= 0 or self.disposed or self.media is None or not self.p2pDownloadOn:
             return
         track = self.currentTrack
         if track is None:
@@ -168,23 +168,29 @@ class PeerAgent:
         return JsObject(cdn=self._stats["cdn"], p2p=self._stats["p2p"],
                         upload=node.stats["upload"] - self._stats["upload_base"], peers=max(0, peers))
 
+    # The toggles belong to this session, as in the reference (``lib/hlsjs-p2p-wrapper.js:20-36``
+    # sets them on the session's own agent): several sessions share one GPU node, and turning
+    # one player's download off must not touch the others.  The node serves this session's
+    # fragments from the CDN only while its download is off, and uploads to peers while any
+    # of its sessions allows it.
     @property
     def p2pDownloadOn(self) -> bool:
-        """Read / write: fetch fragments from peers."""
-        return self.node.download_on
+        """Read / write: fetch this session's fragments from peers."""
+        return self.node.session_flags(self)[0]
 
     @p2pDownloadOn.setter
     def p2pDownloadOn(self, on: bool) -> None:
-        self.node.download_on = bool(on)
+        self.node.set_session_flags(self, bool(on), self.node.session_flags(self)[1])
 
     @property
     def p2pUploadOn(self) -> bool:
-        """Read / write: serve cached fragments to peers."""
-        return self.node.upload_on
+        """Read / write: let peers be served from the cache (the node uploads while any of its
+        sessions has this on)."""
+        return self.node.session_flags(self)[1]
 
     @p2pUploadOn.setter
     def p2pUploadOn(self, on: bool) -> None:
-        self.node.upload_on = bool(on)
+        self.node.set_session_flags(self, self.node.session_flags(self)[0], bool(on))
 
     # ------------------------------------------------------------------ internals
     def _account(self, source: str, nbytes: int) -> None:

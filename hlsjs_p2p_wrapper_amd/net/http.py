@@ -69,6 +69,19 @@ _reg_lock = threading.Lock()
 # playlist directory instead of one per segment URL.
 _resolved: Dict[str, Tuple[Any, int]] = {}
 _RESOLVED_MAX = 1 << 12
+# bumped on every registry change: callers that cache what a URL resolved to (the swarm
+# node's source locators) drop their cache when it moves
+_generation = 0
+
+
+def generation() -> int:
+    """Registry generation (changes whenever an origin is (un)registered or cleared)."""
+    return _generation
+
+
+def _bump() -> None:
+    global _generation
+    _generation += 1
 
 
 def register_origin(base_url: str, origin: Any) -> None:
@@ -77,6 +90,7 @@ def register_origin(base_url: str, origin: Any) -> None:
     with _reg_lock:
         _registry[base_url] = origin
         _resolved.clear()
+        _bump()
 
 
 def unregister_origin(base_url: str) -> None:
@@ -85,6 +99,7 @@ def unregister_origin(base_url: str) -> None:
     with _reg_lock:
         _registry.pop(base_url, None)
         _resolved.clear()
+        _bump()
 
 
 def clear_origins() -> None:
@@ -92,6 +107,7 @@ def clear_origins() -> None:
         origins = list(_registry.values())
         _registry.clear()
         _resolved.clear()
+        _bump()
     for o in origins:  # network origins own worker threads and staged host buffers
         if getattr(o, "staged_fetch", False):
             o.close()
@@ -109,6 +125,7 @@ def enable_network(on: bool = True, **options: Any) -> None:
     with _reg_lock:
         _network = dict(options) if on else None
         _resolved.clear()
+        _bump()
 
 
 def network_enabled() -> bool:

@@ -20,6 +20,7 @@
 #include "shm_control.hpp"
 #include "store.hpp"
 #include "ts.hpp"
+#include "wants.hpp"
 
 namespace py = pybind11;
 using namespace hlsp2p;
@@ -526,6 +527,130 @@ PYBIND11_MODULE(_runtime, m) {
     }
     return out;
   });
+  // CPU-mode CDN phase: copy origin byte ranges (raw host addresses, as the want table holds
+  // them) into the node's host arena at `dst_base + dst_off[i]` (bounds-checked against cap)
+  m.def("host_copy_batch", [](int64_t dst_base, int64_t dst_cap, Arr<int64_t> dst_off, Arr<int64_t> src_ptr,
+                              Arr<int64_t> len) {
+    const int64_t n = len.size();
+    if (dst_off.size() != n || src_ptr.size() != n) throw std::invalid_argument("host_copy_batch: sizes differ");
+    for (int64_t i = 0; i < n; ++i) {
+      const int64_t o = dst_off.data()[i], l = len.data()[i];
+      if (o < 0 || l < 0 || o + l > dst_cap) throw std::out_of_range("host_copy_batch: destination out of bounds");
+      if (l && src_ptr.data()[i] == 0) throw std::invalid_argument("host_copy_batch: null source");
+      if (l) std::memcpy(reinterpret_cast<uint8_t*>(dst_base) + o, reinterpret_cast<const uint8_t*>(src_ptr.data()[i]),
+                         static_cast<size_t>(l));
+    }
+  });
+
+  // ------------------------------------------------------------------ want table
+  // (agent/node.py: the rank's per-request state as rows; see wants.hpp)
+  py::class_<WantTable>(m, "WantTable")
+      .def(py::init<>())
+      .def("__len__", &WantTable::size)
+      .def_property_readonly("waiting", &WantTable::waiting)
+      .def_property_readonly("num_tokens", &WantTable::tokens)
+      .def("add", [](WantTable& t, Arr<int64_t> keys, Arr<int64_t> sizes, Arr<int64_t> ptr, Arr<int64_t> base,
+                     Arr<int64_t> flags, Arr<int64_t> tokens) {
+        // -> (want ids int64[n], created uint8[n])
+        const int64_t n = tokens.size();
+        if (keys.size() != 4 * n || sizes.size() != n || ptr.size() != n || base.size() != n || flags.size() != n)
+          throw std::invalid_argument("WantTable.add: keys int64[n,4] and n-long columns");
+        Arr<int64_t> ids(n);
+        Arr<uint8_t> created(n);
+        const int64_t* k = keys.data();
+        for (int64_t i = 0; i < n; ++i) {
+          bool c = false;
+          ids.mutable_data()[i] = t.add(key_from(k + 4 * i), sizes.data()[i], ptr.data()[i], base.data()[i],
+                                        static_cast<int32_t>(flags.data()[i]), tokens.data()[i], &c);
+          created.mutable_data()[i] = c ? 1 : 0;
+        }
+        return py::make_tuple(ids, created);
+      })
+      .def("add1", [](WantTable& t, uint32_t swarm, uint32_t level, uint32_t url_id, uint32_t sn, int64_t size,
+                      int64_t ptr, int64_t base, int64_t flags, int64_t token) {
+        // -> want id, negated - 1 when the want was created (one int back, no tuple)
+        bool c = false;
+        const int64_t id = t.add(SegKey{swarm, level, url_id, sn}, size, ptr, base, static_cast<int32_t>(flags),
+                                 token, &c);
+        return c ? -id - 1 : id;
+      })
+      .def("abort", [](WantTable& t, Arr<int64_t> tokens) {
+        int64_t n = 0;
+        for (int64_t i = 0; i < tokens.size(); ++i) n += t.abort(tokens.data()[i]) ? 1 : 0;
+        return n;
+      })
+      .def("abort1", &WantTable::abort)
+      .def("lookup1", [](const WantTable& t, uint32_t swarm, uint32_t level, uint32_t url_id, uint32_t sn) {
+        return t.lookup(SegKey{swarm, level, url_id, sn});
+      })
+      .def("select", [](WantTable& t, const SegmentStore& store, const Directory* dir, int64_t cap, int32_t round) {
+        // -> (admitted ids, control rows int64[k, 6], dropped ids, too-big ids, deferred count)
+        std::vector<int64_t> adm, dropped, big;
+        int64_t deferred = 0;
+        t.select(store, dir, cap, round, &adm, &dropped, &big, &deferred);
+        const int64_t k = static_cast<int64_t>(adm.size());
+        Arr<int64_t> rows({k, int64_t(6)});
+        if (k) t.encode(adm.data(), k, rows.mutable_data());
+        auto vec = [](const std::vector<int64_t>& v) {
+          Arr<int64_t> a(static_cast<py::ssize_t>(v.size()));
+          if (!v.empty()) std::memcpy(a.mutable_data(), v.data(), v.size() * sizeof(int64_t));
+          return a;
+        };
+        return py::make_tuple(vec(adm), rows, vec(dropped), vec(big), deferred);
+      }, py::arg("store"), py::arg("directory").none(true), py::arg("cap"), py::arg("round"))
+      .def("info", [](const WantTable& t, Arr<int64_t> ids) {
+        // -> int64[n, 10]: key x4, size, src_ptr, src_base, flags, round, attempts (row of -1: unknown id)
+        const int64_t n = ids.size();
+        Arr<int64_t> out({n, int64_t(10)});
+        int64_t* o = out.mutable_data();
+        for (int64_t i = 0; i < n; ++i, o += 10) {
+          const WantRec* r = t.get(ids.data()[i]);
+          if (r == nullptr) {
+            std::fill(o, o + 10, -1);
+            continue;
+          }
+          o[0] = r->key.swarm; o[1] = r->key.level; o[2] = r->key.url_id; o[3] = r->key.sn;
+          o[4] = r->size; o[5] = r->src_ptr; o[6] = r->src_base; o[7] = r->flags; o[8] = r->round;
+          o[9] = r->attempts;
+        }
+        return out;
+      })
+      .def("set", [](WantTable& t, int64_t id, int64_t size, int64_t set_flags, int64_t clear_flags) {
+        // size < 0: unchanged; returns False for an unknown id
+        WantRec* r = t.get(id);
+        if (r == nullptr) return false;
+        if (size >= 0) r->size = size;
+        r->flags = static_cast<int32_t>((r->flags | set_flags) & ~clear_flags);
+        return true;
+      }, py::arg("id"), py::arg("size") = -1, py::arg("set_flags") = 0, py::arg("clear_flags") = 0)
+      .def("waiters", [](const WantTable& t, int64_t id) {
+        const WantRec* r = t.get(id);
+        std::vector<int64_t> w;
+        if (r != nullptr) w = r->waiters;
+        return w;
+      })
+      .def("finish", [](WantTable& t, Arr<int64_t> ids) {
+        // -> (tokens int64[m], index of each token's want in ids int64[m], prefetch-only uint8[n])
+        std::vector<int64_t> tok, idx;
+        std::vector<uint8_t> pf;
+        t.finish(ids.data(), ids.size(), &tok, &idx, &pf);
+        Arr<int64_t> a(static_cast<py::ssize_t>(tok.size())), b(static_cast<py::ssize_t>(idx.size()));
+        Arr<uint8_t> c(static_cast<py::ssize_t>(pf.size()));
+        if (!tok.empty()) std::memcpy(a.mutable_data(), tok.data(), tok.size() * sizeof(int64_t));
+        if (!idx.empty()) std::memcpy(b.mutable_data(), idx.data(), idx.size() * sizeof(int64_t));
+        if (!pf.empty()) std::memcpy(c.mutable_data(), pf.data(), pf.size());
+        return py::make_tuple(a, b, c);
+      })
+      .def("requeue", [](WantTable& t, Arr<int64_t> ids, bool force_cdn) { t.requeue(ids.data(), ids.size(), force_cdn); },
+           py::arg("ids"), py::arg("force_cdn") = false);
+  m.attr("WANT_FORCE_CDN") = int64_t(kWForceCdn);
+  m.attr("WANT_NOT_STAGED") = int64_t(kWNotStaged);
+  m.attr("WANT_STAGING") = int64_t(kWStaging);
+  m.attr("WANT_PREFETCH") = int64_t(kWPrefetch);
+  m.attr("WANT_PY") = int64_t(kWPy);
+  m.attr("WANT_CORRUPT") = int64_t(kWCorrupt);
+  m.attr("NO_TOKEN") = kNoToken;
+
   // ------------------------------------------------------------------ intra-node control plane
   py::class_<ShmControl>(m, "ShmControl")
       .def(py::init<const std::string&, int, int, int64_t, bool>(), py::arg("name"), py::arg("rank"),

@@ -44,6 +44,9 @@ std::vector<Transfer> plan_round(const Directory& dir, const std::vector<Want>& 
     return a.want_id < b.want_id;
   });
   auto flag = [&](int r, int64_t f) { return (flags[r] & f) != 0; };
+  // may want `wt` receive a peer copy of `size` bytes?  Staged (or in-process) wants always
+  // announce the size they reserved; a not-staged one only once it reserved at least that
+  auto fits_recv = [](const Want& wt, int64_t size) { return !(wt.flags & kNotStaged) || wt.size >= size; };
 
   std::vector<int64_t> link(size_t(world) * world, 0);  // bytes src->dst this round
   std::vector<int64_t> send_total(world, 0), cdn_total(world, 0);
@@ -90,6 +93,10 @@ std::vector<Transfer> plan_round(const Directory& dir, const std::vector<Want>& 
         unserved.push_back(w);
         continue;
       }
+      // a wanter only receives what its admission reserved: a not-staged network want that
+      // does not know the holder's length yet waits a round (its node reads the length from
+      // the directory and reserves it before announcing the want again)
+      if (!fits_recv(wt, de ? de->length : wt.size)) continue;
       int best = -1;
       for (int k = 1; k <= world; ++k) {  // rotation start: the rank after d
         int h = (d + k) % world;
@@ -183,6 +190,7 @@ std::vector<Transfer> plan_round(const Directory& dir, const std::vector<Want>& 
       for (size_t w : g.unserved) {
         const Want& wt = wants[w];
         if (wt.rank == seeder) continue;
+        if (!fits_recv(wt, sz)) continue;  // (see above) it gets the seeder's copy next round
         p2p.push_back({g.key, sz, seeder, wt.rank, wt.want_id, 1});
         link[size_t(seeder) * world + wt.rank] += sz;
         send_total[seeder] += sz;

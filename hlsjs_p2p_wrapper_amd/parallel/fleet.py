@@ -8,32 +8,43 @@ With a fleet, ``W`` player processes run that path in parallel; the GPU process 
 the node side (rounds, CDN DMA, RCCL, CRC) and the transmux, which it runs in batches.
 The player processes never touch the GPU (``HIP_VISIBLE_DEVICES`` is empty for them).
 
+The rank side is columnar end to end: requests arrive as arrays, join the node's native
+want table as 64-bit tokens (``player << 40 | rid``) through ``SwarmNode.request_batch``,
+come back from the round as delivery columns (token, source, bytes, timings, arena
+offset), feed the batched GPU transmux as columns, and leave as answer columns.  No
+per-fragment Python object exists on the rank: the ``getSegment(reqInfo, callbacks,
+segmentView)`` hop of ``lib/integration/p2p-loader-generator.js:133-165`` is one row.
+
 Protocol (one ``multiprocessing`` pipe per player process, batched per loop iteration):
 
-* player -> node: ``("req", [(rid, key4, url, headers, aes_key, iv), ...])`` — a fragment
-  request as ``PeerAgent.getSegment`` issues it, plus the AES key / IV the GPU transmux
-  needs; ``("abort", [rid, ...])``; ``("evict", swarm, sn)``; ``("flags", down, up)``;
-  ``("mark", tag, counters)`` (bench window markers); ``("bye",)``.
-* node -> player: ``("done", chunks, errors, swarm_state)``.  Each chunk holds the fragments of
-  one transmux batch as columns (numpy arrays, pickled as flat buffers): ``rid``, ``source``
-  code (:data:`SOURCES`), ``nbytes``, ``cdn_ms``, ``p2p_ms``, ``plain`` bytes, ``has_row`` and
-  the transmux info ``rows`` ``[n, INFO_WORDS]``.  ``errors``: ``[(rid, status), ...]`` with
-  the HTTP-like error status of requests the node could not serve.
+* player -> node: ``("req", cols, handled)`` with ``cols`` = ``(rid int64[n], key int64[n, 4],
+  urls, headers or None, key_id int32[n] (-1: clear), iv uint8[n, 16], new_keys {id: 16 B})``
+  -- the fragment requests as ``PeerAgent.getSegment`` issues them plus the AES-128 key id /
+  IV the GPU transmux needs (each distinct key crosses the pipe once);
+  ``("abort", [rid, ...])``; ``("evict", swarm, sn)``; ``("flags", down, up)`` (this
+  player's ``p2pDownloadOn`` / ``p2pUploadOn``); ``("mark", tag, counters)`` (bench window
+  markers); ``("payload", on)``; ``("bye",)``.
+* node -> player: ``("done", chunks, errors, swarm_state)``.  Each chunk holds the fragments
+  of one transmux batch as columns: ``rid``, ``source`` code (:data:`SOURCES`), ``nbytes``,
+  ``cdn_ms``, ``p2p_ms``, ``plain`` bytes, ``has_row``, the transmux info ``rows`` ``[n,
+  INFO_WORDS]``, and, for a player that asked for payloads, ``(shm name, offsets, lengths)``
+  of the fragments' bytes.  ``errors``: ``[(rid, status), ...]``.
 
 Player side, :class:`RemoteNode` stands in for the ``SwarmNode`` behind the unchanged
 ``PeerAgent`` (``gpuSwarm.backend = "remote"``): the loader's ``onSuccess`` gets a
 :class:`RemoteSegment` whose ``transmux_result`` the stream controller uses instead of
-transmuxing itself (it holds the info row: durations, PTS, ES byte counts; the ES bytes stay
-on the GPU).  Node side, :class:`FleetServer` feeds requests to the node, and per node round
-transmuxes what was delivered and answers each player with one batch.
+transmuxing itself (it holds the info row: durations, PTS, ES byte counts).  With
+``gpuSwarm.fleetPayload`` the segment also carries its bytes (``RemoteSegment.data()``, the
+reference ``onSuccess`` contract ``{currentTarget: {response: ArrayBuffer}}``,
+``lib/integration/p2p-loader-generator.js:92-99``): the rank copies them device-to-host
+into a shared-memory ring the player maps.
 """
 from __future__ import annotations
 
-import collections
 import logging
 import os
 import time
-from typing import Any, Dict, List, Tuple
+from typing import Any, Dict, List, Optional, Tuple
 
 import numpy as np
 
@@ -41,25 +52,34 @@ from ..net.http import HttpError
 
 log = logging.getLogger("hlsjs_p2p_wrapper_amd.fleet")
 
-SOURCES = ("cdn", "p2p", "cache")  # source codes of the answer columns
+SOURCES = ("cdn", "p2p", "cache")  # source codes of the answer columns (agent/node.py SRC_*)
 _SOURCE_CODE = {s: i for i, s in enumerate(SOURCES)}
+TOKEN_SHIFT = 40  # token = player << TOKEN_SHIFT | rid
+_RID_MASK = (1 << TOKEN_SHIFT) - 1
+_RING = 1 << 16  # per-player request slots (rid % _RING): far above the fragments in flight
 
 
 # ============================================================================ player side
 class RemoteSegment:
-    """``onSuccess`` payload of a remotely served fragment: its size and transmux result."""
+    """``onSuccess`` payload of a remotely served fragment: its size, its transmux result and,
+    when the player asked for payloads, its bytes (:meth:`data`)."""
 
-    __slots__ = ("nbytes", "transmux_result")
+    __slots__ = ("nbytes", "transmux_result", "_bytes")
 
-    def __init__(self, nbytes: int, transmux_result: Any) -> None:
+    def __init__(self, nbytes: int, transmux_result: Any, data: Any = None) -> None:
         self.nbytes = nbytes
         self.transmux_result = transmux_result
+        self._bytes = data
 
     def numel(self) -> int:
         return self.nbytes
 
     def __len__(self) -> int:
         return self.nbytes
+
+    def data(self) -> Optional[np.ndarray]:
+        """The fragment's bytes as a ``uint8`` array (``gpuSwarm.fleetPayload``), else None."""
+        return self._bytes
 
 
 class RemoteResult(dict):
@@ -111,10 +131,39 @@ class _RemoteStore:
         return 0
 
 
+class _ShmRing:
+    """Player side of the payload ring: the rank's shared-memory segment, mapped once."""
+
+    def __init__(self) -> None:
+        self.name = None
+        self.shm = None
+        self.buf: Optional[np.ndarray] = None
+
+    def view(self, name: str) -> np.ndarray:
+        if name != self.name:
+            from multiprocessing import shared_memory
+
+            self.close()
+            self.shm = shared_memory.SharedMemory(name=name, create=False)
+            self.buf = np.ndarray((self.shm.size,), dtype=np.uint8, buffer=self.shm.buf)
+            self.name = name
+        return self.buf
+
+    def close(self) -> None:
+        if self.shm is not None:
+            self.buf = None
+            try:
+                self.shm.close()
+            except BufferError:  # a payload view is still referenced: the OS unmaps at exit
+                pass
+            self.shm = None
+            self.name = None
+
+
 class RemoteNode:
     """The ``SwarmNode`` surface ``PeerAgent`` uses, served by a node in another process."""
 
-    def __init__(self, conn: Any, world: int = 1, rank: int = 0) -> None:
+    def __init__(self, conn: Any, world: int = 1, rank: int = 0, payload: bool = False) -> None:
         self.conn = conn
         self.world = world
         self.rank = rank
@@ -127,7 +176,15 @@ class RemoteNode:
         self.store = _RemoteStore(self)
         self._agents: List[Any] = []
         self._pending: Dict[int, _RemoteRequest] = {}
-        self._reqs: List[tuple] = []
+        # request columns accumulated until the next flush
+        self._rid: List[int] = []
+        self._key: List[Tuple[int, int, int, int]] = []
+        self._url: List[str] = []
+        self._hdr: List[Optional[Dict[str, str]]] = []
+        self._kid: List[int] = []
+        self._iv: List[bytes] = []
+        self._key_ids: Dict[bytes, int] = {}
+        self._new_keys: Dict[int, bytes] = {}
         self._aborts: List[int] = []
         self._out: List[tuple] = []
         self._next = 0
@@ -135,6 +192,9 @@ class RemoteNode:
         self.control: List[tuple] = []
         self.batches = 0  # answer batches handled (reported to the node, which paces on it)
         self._reported = 0
+        self._ring = _ShmRing()
+        if payload:
+            self._out.append(("payload", True))
 
     # -------------------------------------------------------------- SwarmNode surface
     def attach(self, agent: Any) -> None:
@@ -146,25 +206,33 @@ class RemoteNode:
         if agent in self._agents:
             self._agents.remove(agent)
 
+    def session_flags(self, session: Any) -> Tuple[bool, bool]:
+        """``(download, upload)`` of this player's session."""
+        return self._down, self._up
+
+    def set_session_flags(self, session: Any, download: bool, upload: bool) -> None:
+        """This player's ``p2pDownloadOn`` / ``p2pUploadOn``, forwarded to the node (which
+        applies them to this player's requests only)."""
+        self._down, self._up = bool(download), bool(upload)
+        self._out.append(("flags", self._down, self._up))
+
     @property
     def download_on(self) -> bool:
-        """Read / write: P2P download, forwarded to the node."""
+        """Read / write: P2P download of this player's session."""
         return self._down
 
     @download_on.setter
     def download_on(self, on: bool) -> None:
-        self._down = bool(on)
-        self._out.append(("flags", self._down, self._up))
+        self.set_session_flags(None, on, self._up)
 
     @property
     def upload_on(self) -> bool:
-        """Read / write: P2P upload, forwarded to the node."""
+        """Read / write: P2P upload of this player's session."""
         return self._up
 
     @upload_on.setter
     def upload_on(self, on: bool) -> None:
-        self._up = bool(on)
-        self._out.append(("flags", self._down, self._up))
+        self.set_session_flags(None, self._down, on)
 
     def request(self, key, url: str, headers, callbacks: Any, agent: Any = None, view: Any = None):
         """Queue a fragment request for the node (sent at the next flush); ``view`` finds the
@@ -172,21 +240,31 @@ class RemoteNode:
         rid = self._next
         self._next += 1
         req = _RemoteRequest(self, rid, key, callbacks, agent)
-        aes_key = iv = None
+        kid, iv = -1, b"\0" * 16
         if agent is not None and view is not None:  # the GPU transmux needs the AES key / IV
             frag = agent.mediaMap.fragment(view)
             if frag is not None:
                 dd = frag.decryptdata
                 if dd is not None and dd.method == "AES-128" and dd.key is not None:
-                    aes_key, iv = bytes(dd.key), frag.iv_for_decrypt()
+                    kb = bytes(dd.key)
+                    kid = self._key_ids.get(kb)
+                    if kid is None:
+                        kid = self._key_ids[kb] = len(self._key_ids)
+                        self._new_keys[kid] = kb
+                    iv = bytes(frag.iv_for_decrypt())
         self._pending[rid] = req
-        self._reqs.append((rid, tuple(key), url, dict(headers) if headers else None, aes_key, iv))
+        self._rid.append(rid)
+        self._key.append(tuple(int(k) for k in key))
+        self._url.append(url)
+        self._hdr.append(dict(headers) if headers else None)
+        self._kid.append(kid)
+        self._iv.append(iv)
         self.inflight += 1
         return req
 
     def prefetch(self, key, url: str, headers=None) -> bool:
         """Agent-driven prefetch is a single-process feature: nothing is issued."""
-        return False  # agent-driven prefetch stays a single-process feature
+        return False
 
     def swarm_offload_ratio(self) -> float:
         """P2P / (P2P + CDN) bytes over the whole swarm, as last reported by the node."""
@@ -194,12 +272,24 @@ class RemoteNode:
         return p / (p + c) if (p + c) else 0.0
 
     # -------------------------------------------------------------- transport
+    def _columns(self) -> tuple:
+        n = len(self._rid)
+        hdr = self._hdr if any(h is not None for h in self._hdr) else None
+        cols = (np.asarray(self._rid, dtype=np.int64), np.asarray(self._key, dtype=np.int64).reshape(n, 4),
+                self._url, hdr, np.asarray(self._kid, dtype=np.int32),
+                np.frombuffer(b"".join(self._iv), dtype=np.uint8).reshape(n, 16), self._new_keys)
+        self._rid, self._key, self._url, self._hdr, self._kid, self._iv = [], [], [], [], [], []
+        self._new_keys = {}
+        return cols
+
     def flush(self) -> None:
         """Send everything queued since the last flush (one message per kind), with the count
         of answer batches handled so far (the node paces its rounds on it)."""
-        if self._reqs:
-            self.conn.send(("req", self._reqs, self.batches))
-            self._reqs = []
+        for m in self._out:  # flags / payload mode first: they apply to the requests below
+            self.conn.send(m)
+        self._out = []
+        if self._rid:
+            self.conn.send(("req", self._columns(), self.batches))
             self._reported = self.batches
         elif self.batches != self._reported:
             self.conn.send(("ack", self.batches))
@@ -207,9 +297,6 @@ class RemoteNode:
         if self._aborts:
             self.conn.send(("abort", self._aborts))
             self._aborts = []
-        for m in self._out:
-            self.conn.send(m)
-        self._out = []
 
     def poll(self, timeout: float = 0.0) -> int:
         """Deliver every answer that has arrived (waiting up to ``timeout`` s for the first)."""
@@ -254,13 +341,18 @@ class RemoteNode:
     def _deliver(self, chunk: tuple) -> int:
         from ..player.transmux import InfoRow
 
-        rid_a, src_a, nbytes_a, cdn_a, p2p_a, plain_a, has_a, rows_a = chunk
+        rid_a, src_a, nbytes_a, cdn_a, p2p_a, plain_a, has_a, rows_a = chunk[:8]
+        payload = chunk[8] if len(chunk) > 8 else None
+        buf = poff = None
+        if payload is not None:
+            buf = self._ring.view(payload[0])
+            poff = payload[1].tolist()
         pending = self._pending
         stats = self.stats
         n = 0
-        for rid, code, nbytes, cdn_ms, p2p_ms, plain, has, info in zip(
+        for i, (rid, code, nbytes, cdn_ms, p2p_ms, plain, has, info) in enumerate(zip(
                 rid_a.tolist(), src_a.tolist(), nbytes_a.tolist(), cdn_a.tolist(), p2p_a.tolist(),
-                plain_a.tolist(), has_a.tolist(), rows_a.tolist()):
+                plain_a.tolist(), has_a.tolist(), rows_a.tolist())):
             req = pending.pop(rid, None)
             if req is None:
                 continue
@@ -289,7 +381,8 @@ class RemoteNode:
             r = RemoteResult(status=int(info[0]) if info else -1, info=InfoRow(info), plain_bytes=plain)
             if plain < 0:
                 r["error"] = ValueError("decryption failed (bad PKCS#7 padding)")
-            on_success(RemoteSegment(nbytes, r))
+            data = buf[poff[i]:poff[i] + nbytes].copy() if buf is not None else None
+            on_success(RemoteSegment(nbytes, r, data))
             n += 1
         return n
 
@@ -302,71 +395,170 @@ class RemoteNode:
                 self.conn.send(("bye",))
             except (OSError, EOFError, BrokenPipeError):
                 pass
+            self._ring.close()
 
 
 # ============================================================================ node side
-class _Pending:
-    """One remote request on the node side; also its ``getSegment`` callbacks object."""
+class _Queue:
+    """One player's admitted-later requests: column chunks consumed front to back."""
 
-    __slots__ = ("server", "w", "rid", "aes_key", "iv", "req", "source", "nbytes", "cdn_ms", "p2p_ms")
+    __slots__ = ("chunks", "pos", "n")
 
-    def __init__(self, server: "FleetServer", w: int, rid: int, aes_key, iv) -> None:
-        self.server = server
-        self.w = w
-        self.rid = rid
-        self.aes_key = aes_key
-        self.iv = iv
-        self.req = None
-        self.source = "cdn"
-        self.nbytes = 0
-        self.cdn_ms = 0.0
-        self.p2p_ms = 0.0
+    def __init__(self) -> None:
+        self.chunks: List[tuple] = []  # (rid, key, urls, headers, force)
+        self.pos = 0  # rows of chunks[0] already taken
+        self.n = 0
 
-    def onProgress(self, ev: dict) -> None:  # noqa: N802 - loader callback contract
-        if ev["p2pDownloaded"]:
-            self.source, self.nbytes, self.p2p_ms = "p2p", ev["p2pDownloaded"], ev["p2pDuration"]
-        else:
-            self.source, self.nbytes, self.cdn_ms = "cdn", ev["cdnDownloaded"], ev["cdnDuration"]
+    def push(self, rid, key, urls, headers, force) -> None:
+        self.chunks.append((rid, key, urls, headers, force))
+        self.n += len(rid)
 
-    def onSuccess(self, data: Any) -> None:  # noqa: N802
-        self.server._delivered.append((self, data))
+    def take(self, k: int):
+        """Up to ``k`` rows as ``(rid, key, urls, headers, force)`` (None when empty)."""
+        if not self.n or k <= 0:
+            return None
+        parts = []
+        while k > 0 and self.chunks:
+            rid, key, urls, hdr, force = self.chunks[0]
+            a = self.pos
+            b = min(len(rid), a + k)
+            parts.append((rid[a:b], key[a:b], urls[a:b], None if hdr is None else hdr[a:b], force[a:b]))
+            k -= b - a
+            self.n -= b - a
+            if b == len(rid):
+                self.chunks.pop(0)
+                self.pos = 0
+            else:
+                self.pos = b
+        if len(parts) == 1:
+            return parts[0]
+        hdr = None
+        if any(p[3] is not None for p in parts):
+            hdr = [h for p in parts for h in (p[3] if p[3] is not None else [None] * len(p[0]))]
+        return (np.concatenate([p[0] for p in parts]), np.concatenate([p[1] for p in parts]),
+                [u for p in parts for u in p[2]], hdr, np.concatenate([p[4] for p in parts]))
 
-    def onDelivered(self, source: str, nbytes: int, cdn_ms: float, p2p_ms: float, data: Any) -> None:  # noqa: N802
-        """The node's one-call delivery (progress + success): cache hits count as P2P, as
-        the progress event reports them."""
-        if source == "cdn":
-            self.source, self.nbytes, self.cdn_ms = "cdn", nbytes, cdn_ms
-        else:
-            self.source, self.nbytes, self.p2p_ms = "p2p", nbytes, p2p_ms
-        self.server._delivered.append((self, data))
+    def drop(self, rids: set) -> None:
+        """Remove not-yet-admitted requests (aborted by their player)."""
+        out = []
+        for i, (rid, key, urls, hdr, force) in enumerate(self.chunks):
+            a = self.pos if i == 0 else 0
+            keep = ~np.isin(rid[a:], np.fromiter(rids, dtype=np.int64, count=len(rids)))
+            idx = np.flatnonzero(keep) + a
+            if len(idx):
+                out.append((rid[idx], key[idx], [urls[j] for j in idx.tolist()],
+                            None if hdr is None else [hdr[j] for j in idx.tolist()], force[idx]))
+        self.chunks = out
+        self.pos = 0
+        self.n = sum(len(c[0]) for c in out)
 
-    def onError(self, err: Any) -> None:  # noqa: N802
-        self.server._errors[self.w].append((self.rid, int(getattr(err, "status", 0) or 0) or 500))
+
+class _PayloadRing:
+    """Rank side of the payload ring: a shared-memory segment the fragments' bytes are copied
+    into (device -> pinned host -> shared memory) for players that asked for them."""
+
+    def __init__(self, nbytes: int) -> None:
+        from multiprocessing import shared_memory
+
+        self.shm = shared_memory.SharedMemory(create=True, size=nbytes)
+        self.buf = np.ndarray((nbytes,), dtype=np.uint8, buffer=self.shm.buf)
+        self.head = 0
+
+    def place(self, lens: np.ndarray) -> np.ndarray:
+        """Offsets for a batch of ``lens`` bytes (wrapping; the oldest bytes are overwritten:
+        a player copies its fragments out when it handles the batch)."""
+        al = (lens + 63) // 64 * 64
+        total = int(al.sum())
+        if total > len(self.buf):
+            raise RuntimeError(f"payload ring of {len(self.buf)} bytes cannot hold a {total}-byte batch")
+        if self.head + total > len(self.buf):
+            self.head = 0
+        offs = self.head + np.concatenate([[0], np.cumsum(al)[:-1]]).astype(np.int64)
+        self.head += total
+        return offs
+
+    def close(self) -> None:
+        self.buf = None
+        try:
+            self.shm.close()
+            self.shm.unlink()
+        except (BufferError, FileNotFoundError):
+            pass
 
 
 class FleetServer:
-    """Node-process side of a fleet: requests in, transmuxed deliveries out."""
+    """Node-process side of a fleet: request columns in, transmuxed answer columns out."""
 
     def __init__(self, node: Any, pipeline: Any, conns: List[Any]) -> None:
         self.node = node
         self.pipe = pipeline
         self.conns = list(conns)
-        self.open = [True] * len(self.conns)
-        self._by_rid: List[Dict[int, _Pending]] = [{} for _ in self.conns]
-        self._delivered: List[Tuple[_Pending, Any]] = []
-        self._chunks: List[List[tuple]] = [[] for _ in self.conns]  # answer columns per player
-        self._errors: List[List[Tuple[int, int]]] = [[] for _ in self.conns]
+        W = len(self.conns)
+        self.open = [True] * W
+        self._q = [_Queue() for _ in range(W)]
+        # per player request slots (rid % _RING): AES key index (global, -1 = clear) and IV
+        self._gkey = [np.full(_RING, -1, dtype=np.int32) for _ in range(W)]
+        self._iv = [np.zeros((_RING, 16), dtype=np.uint8) for _ in range(W)]
+        self._kmap: List[Dict[int, int]] = [{} for _ in range(W)]  # player key id -> global key index
+        self._gk: Dict[bytes, int] = {}
+        self._drk = np.zeros((0, 44), dtype=np.uint32)  # round keys per global key index
+        self._rawkeys = np.zeros((0, 16), dtype=np.uint8)  # the keys themselves (CPU transmux)
+        self._down = [True] * W
+        self._payload = [False] * W
+        self._ring: Optional[_PayloadRing] = None
+        self._delivered: List[tuple] = []  # delivery columns from the node, not transmuxed yet
+        self._chunks: List[List[tuple]] = [[] for _ in range(W)]  # answer columns per player
+        self._errors: List[List[Tuple[int, int]]] = [[] for _ in range(W)]
         self.marks: Dict[Any, Dict[int, Any]] = {}
         self.ready: set = set()
-        self.requests = [0] * len(self.conns)
+        self.requests = [0] * W
         self.sent = 0
-        # requests wait here until admitted: at most `per_player` per player and round, so
-        # each player advances at the same pace on every rank and the swarm shares its slice
-        self._queued: List[collections.deque] = [collections.deque() for _ in self.conns]
-        self.batches_sent = [0] * len(self.conns)  # answer batches sent to each player ...
-        self.batches_done = [0] * len(self.conns)  # ... and handled by it (reported back)
+        self.batches_sent = [0] * W  # answer batches sent to each player ...
+        self.batches_done = [0] * W  # ... and handled by it (reported back)
+        node.set_bulk_sink(self)
+
+    # -------------------------------------------------------------- node sink
+    def deliver(self, tok, src, nbytes, cdn_ms, p2p_ms, offs, eids) -> None:
+        """Delivery columns of the node's round (``SwarmNode.set_bulk_sink``)."""
+        self._delivered.append((tok, src, nbytes, cdn_ms, p2p_ms, offs))
+
+    def fail(self, tok, status) -> None:
+        """Requests the node could not serve (HTTP-like status per token)."""
+        w = (tok >> TOKEN_SHIFT).tolist()
+        rid = (tok & _RID_MASK).tolist()
+        for p, r, s in zip(w, rid, np.asarray(status).tolist()):
+            if 0 <= p < len(self._errors):
+                self._errors[p].append((r, int(s) or 500))
 
     # -------------------------------------------------------------- inbound
+    def _take_requests(self, w: int, cols: tuple) -> int:
+        rid, key, urls, hdr, kid, iv, new_keys = cols
+        if new_keys:
+            from ..ops import aes as _aes
+
+            for k_id, kb in new_keys.items():
+                g = self._gk.get(kb)
+                if g is None:
+                    g = self._gk[kb] = len(self._gk)
+                    self._drk = np.concatenate([self._drk, np.asarray(_aes.round_keys_le(kb),
+                                                                      dtype=np.uint32).reshape(1, 44)])
+                    self._rawkeys = np.concatenate([self._rawkeys, np.frombuffer(kb, dtype=np.uint8).reshape(1, 16)])
+                self._kmap[w][int(k_id)] = g
+        slot = rid % _RING
+        if (kid >= 0).any():
+            km = self._kmap[w]
+            lut = np.full(max(km) + 2 if km else 1, -1, dtype=np.int32)
+            for k_id, g in km.items():
+                lut[k_id] = g
+            self._gkey[w][slot] = np.where(kid >= 0, lut[np.maximum(kid, 0)], -1)
+        else:
+            self._gkey[w][slot] = -1
+        self._iv[w][slot] = iv
+        force = np.full(len(rid), not self._down[w], dtype=bool)
+        self._q[w].push(rid, key, urls, hdr, force)
+        self.requests[w] += len(rid)
+        return len(rid)
+
     def poll(self) -> int:
         """Take every queued player message; returns the number of new requests."""
         n = 0
@@ -379,28 +571,22 @@ class FleetServer:
                     msg = conn.recv()
                     kind = msg[0]
                     if kind == "req":
-                        self._queued[w].extend(msg[1])
-                        n += len(msg[1])
-                        self.requests[w] += len(msg[1])
+                        n += self._take_requests(w, msg[1])
                         self.batches_done[w] = msg[2]
                     elif kind == "ack":
                         self.batches_done[w] = msg[1]
                     elif kind == "abort":
-                        by_rid = self._by_rid[w]
-                        aborted = set()
-                        for rid in msg[1]:
-                            p = by_rid.pop(rid, None)
-                            if p is not None and p.req is not None:
-                                p.req.abort()
-                            elif p is None:
-                                aborted.add(rid)
-                        if aborted:  # not handed to the node yet
-                            q = self._queued[w]
-                            self._queued[w] = collections.deque(r for r in q if r[0] not in aborted)
+                        rids = set(int(r) for r in msg[1])
+                        self._q[w].drop(rids)  # not handed to the node yet
+                        tok = (np.fromiter(rids, dtype=np.int64, count=len(rids)) | (w << TOKEN_SHIFT))
+                        node.abort_tokens(tok)
                     elif kind == "evict":
                         node.store.evict_below(msg[1], msg[2])
-                    elif kind == "flags":
-                        node.download_on, node.upload_on = bool(msg[1]), bool(msg[2])
+                    elif kind == "flags":  # this player's session toggles only
+                        self._down[w] = bool(msg[1])
+                        node.set_session_flags(("fleet", w), bool(msg[1]), bool(msg[2]))
+                    elif kind == "payload":
+                        self._payload[w] = bool(msg[1])
                     elif kind == "mark":
                         self.marks.setdefault(msg[1], {})[w] = msg[2]
                     elif kind == "ready":
@@ -414,59 +600,86 @@ class FleetServer:
 
     def admit(self, per_player: int) -> int:
         """Hand up to ``per_player`` queued requests of every player to the node (call right
-        before the node's round)."""
+        before the node's round): one ``request_batch`` per player."""
         node = self.node
         n = 0
-        for w, q in enumerate(self._queued):
-            if not q:
+        for w, q in enumerate(self._q):
+            got = q.take(per_player)
+            if got is None:
                 continue
-            by_rid = self._by_rid[w]
-            for _ in range(min(per_player, len(q))):
-                rid, key, url, headers, aes_key, iv = q.popleft()
-                p = _Pending(self, w, rid, aes_key, iv)
-                by_rid[rid] = p
-                p.req = node.request(key, url, headers, p)
-                n += 1
+            rid, key, urls, hdr, force = got
+            node.request_batch(key, urls, hdr, rid | (w << TOKEN_SHIFT), force if force.any() else None)
+            n += len(rid)
         return n
 
     # -------------------------------------------------------------- outbound
     def launch_transmux(self):
-        """Enqueue the GPU transmux of everything the node delivered since the last call."""
-        from ..player.transmux import TransmuxJob
-
+        """Enqueue the GPU transmux of everything the node delivered since the last call:
+        decrypt keys and IVs looked up by token, one columnar launch."""
         items, self._delivered = self._delivered, []
         if not items:
             return None
-        pipe = self.pipe
-        for p, data in items:
-            pipe.submit(TransmuxJob(data, p.aes_key, p.iv, None, p))  # the pending rides as the job's frag
-        return pipe.launch()
+        if len(items) == 1:
+            tok, src, nbytes, cdn_ms, p2p_ms, offs = items[0]
+        else:
+            tok, src, nbytes, cdn_ms, p2p_ms, offs = (np.concatenate(c) for c in zip(*items))
+        w = tok >> TOKEN_SHIFT
+        slot = (tok & _RID_MASK) % _RING
+        gk = np.empty(len(tok), dtype=np.int32)
+        iv = np.empty((len(tok), 16), dtype=np.uint8)
+        for p in np.unique(w).tolist():
+            sel = w == p
+            gk[sel] = self._gkey[p][slot[sel]]
+            iv[sel] = self._iv[p][slot[sel]]
+        enc = gk >= 0
+        if len(self._drk):
+            drk, keys = self._drk[np.maximum(gk, 0)], self._rawkeys[np.maximum(gk, 0)]
+        else:
+            drk, keys = np.zeros((len(tok), 44), dtype=np.uint32), None
+        tag = (tok, src, nbytes, cdn_ms, p2p_ms, offs)
+        return self.pipe.launch_columns(self.node.arena, offs, nbytes, enc, drk, iv, tag, keys=keys)
 
     def complete_transmux(self, batch) -> None:
         """Wait for a launched transmux batch; its info rows go to the players as columns."""
-        jobs, rows, plain, has = self.pipe.complete_arrays(batch)
-        if not jobs:
+        if batch is None:
             return
-        by_rid = self._by_rid
-        per: Dict[int, List[Tuple[int, _Pending]]] = {}
-        for i, job in enumerate(jobs):
-            p = job.frag
-            by_rid[p.w].pop(p.rid, None)
-            p.req = None  # Request.callbacks is p: drop the cycle so refcounting frees both now
-            c = per.get(p.w)
-            if c is None:
-                c = per[p.w] = []
-            c.append((i, p))
-        code = _SOURCE_CODE
-        for w, c in per.items():
-            idx = np.fromiter([i for i, _ in c], dtype=np.int64, count=len(c))
-            self._chunks[w].append((
-                np.fromiter([p.rid for _, p in c], dtype=np.int64, count=len(c)),
-                np.fromiter([code[p.source] for _, p in c], dtype=np.int8, count=len(c)),
-                np.fromiter([p.nbytes for _, p in c], dtype=np.int64, count=len(c)),
-                np.fromiter([p.cdn_ms for _, p in c], dtype=np.float64, count=len(c)),
-                np.fromiter([p.p2p_ms for _, p in c], dtype=np.float64, count=len(c)),
-                plain[idx], has[idx], rows[idx]))
+        tag, rows, plain, has = self.pipe.complete_columns(batch)
+        tok, src, nbytes, cdn_ms, p2p_ms, offs = tag
+        w = tok >> TOKEN_SHIFT
+        rid = tok & _RID_MASK
+        for p in np.unique(w).tolist():
+            sel = np.flatnonzero(w == p)
+            chunk = (rid[sel], src[sel].astype(np.int8), nbytes[sel], cdn_ms[sel], p2p_ms[sel], plain[sel],
+                     has[sel], rows[sel])
+            if self._payload[p]:
+                chunk = chunk + (self._payload_copy(offs[sel], nbytes[sel]),)
+            self._chunks[p].append(chunk)
+
+    def _payload_copy(self, offs: np.ndarray, lens: np.ndarray) -> tuple:
+        """Copy fragments' bytes from the HBM arena into the shared payload ring (one gather on
+        the device, one D2H, one host copy); returns ``(ring name, offsets, lengths)``."""
+        import torch
+
+        from ..ops import segment as _seg
+
+        if self._ring is None:
+            self._ring = _PayloadRing(int(os.environ.get("HLSP2P_FLEET_PAYLOAD_BYTES", str(1 << 30))))
+        ring_off = self._ring.place(lens)
+        arena = self.node.arena
+        al = (lens + 63) // 64 * 64
+        pack = np.concatenate([[0], np.cumsum(al)[:-1]]).astype(np.int64)
+        total = int(al.sum())
+        if arena.is_cuda:
+            staged = torch.empty(max(total, 1), dtype=torch.uint8, device=arena.device)
+            _seg.copy_segments(arena, staged, offs, pack, lens)
+            host = staged.cpu().numpy()
+        else:
+            host = arena.numpy()
+            pack = offs
+        buf = self._ring.buf
+        for o, p, n in zip(ring_off.tolist(), pack.tolist(), lens.tolist()):
+            buf[o:o + n] = host[p:p + n]
+        return (self._ring.shm.name, ring_off, lens)
 
     def send(self) -> int:
         """One answer batch per player (plus the swarm state the agents' stats read)."""
@@ -523,6 +736,11 @@ class FleetServer:
                     c.poll(0.01)
             self.poll()
 
+    def close(self) -> None:
+        """Release the payload ring (after the players stopped)."""
+        if self._ring is not None:
+            self._ring.close()
+            self._ring = None
 
 
 # ============================================================================ player process
@@ -551,7 +769,9 @@ def player_main(conn: Any, spec: Dict[str, Any]) -> None:
     loop = new_event_loop("real")
     origin = SyntheticHlsOrigin(**spec["origin"])
     p2p = copy.deepcopy(spec["p2p_config"])
-    p2p["gpuSwarm"] = {"backend": "remote", "conn": conn, "world": spec.get("world", 1), "rank": spec.get("rank", 0)}
+    gs = dict(p2p.get("gpuSwarm") or {})
+    p2p["gpuSwarm"] = {"backend": "remote", "conn": conn, "world": spec.get("world", 1), "rank": spec.get("rank", 0),
+                       "fleetPayload": bool(gs.get("fleetPayload", False))}
     node = node_for_config(p2p)
     hls = Hls(dict(spec["hls_config"]), p2p)
     media = MediaElement(mode="drain", loop=loop)

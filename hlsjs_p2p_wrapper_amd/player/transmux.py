@@ -249,6 +249,83 @@ class MediaPipeline:
         tm.add("demux_launch", time.perf_counter() - t2)
         return _Batch(jobs, infos=infos, host=host, event=ev, results=results, keep=(dec, host_block))
 
+    # ------------------------------------------------------------------ columnar batch
+    def launch_columns(self, src: torch.Tensor, offs: np.ndarray, nbytes: np.ndarray, enc: np.ndarray,
+                       drk: np.ndarray, iv: np.ndarray, tag: Any = None, keys: Optional[np.ndarray] = None
+                       ) -> Optional["_Batch"]:
+        """A batch given as columns (a fleet rank: no job object per fragment).  Fragment
+        ``i`` is ``src[offs[i] : offs[i] + nbytes[i]]`` (the node's HBM arena, 16-byte aligned
+        offsets); ``enc[i]``: AES-128-CBC with round keys ``drk[i]`` (44 little-endian words,
+        ``ops.aes.round_keys_le``) and ``iv[i]``; ``keys[i]`` (raw 16-byte keys) is only read
+        by the CPU path.  ``tag`` comes back from :meth:`complete_columns`."""
+        n = len(offs)
+        if n == 0:
+            return None
+        offs = np.ascontiguousarray(offs, dtype=np.int64)
+        nb = np.ascontiguousarray(nbytes, dtype=np.int64)
+        enc = np.asarray(enc, dtype=bool)
+        self.segments += n
+        self.bytes_in += int(nb.sum())
+        self.batches += 1
+        t1 = time.perf_counter()
+        if self.device.type != "cuda":  # CPU mode: the job path (host kernels)
+            jobs = []
+            for i in range(n):
+                o, k = int(offs[i]), int(nb[i])
+                key = bytes(keys[i]) if (enc[i] and keys is not None) else None
+                jobs.append(TransmuxJob(src[o:o + k], key, bytes(iv[i]) if key is not None else None, None))
+            b = self.launch_jobs(jobs)
+            b.tag = tag
+            return b
+        ok = ~(enc & ((nb <= 0) | (nb % 16 != 0)))  # encrypted payloads must be whole AES blocks
+        idx_ok = np.flatnonzero(ok)
+        if not len(idx_ok):
+            return _Batch(None, infos=[], host=[], event=None, tag=tag, n=n)
+        if not ok.all():
+            offs, nb, enc, drk, iv = offs[ok], nb[ok], enc[ok], drk[ok], iv[ok]
+        td0, isb = _aes.device_tables(self.device)
+        groups, dec, host_block = _native_device().transmux_launch(
+            src, offs, nb, enc.astype(np.uint8), np.ascontiguousarray(drk, dtype=np.uint32),
+            np.ascontiguousarray(iv, dtype=np.uint8), td0, isb, _ts.DEFAULT_MAX_PES)
+        infos, host = [], []
+        for gidx, info, pes, es, es_offs, hinfo, hlens in groups:
+            infos.append((idx_ok[gidx], _ts.DemuxResult(info, pes, es, es_offs), es_offs, hlens))
+            host.append((hinfo, hlens))
+        ev = self._free_events.pop() if self._free_events else torch.cuda.Event()
+        ev.record()
+        self.timer.add("launch_columns", time.perf_counter() - t1)
+        return _Batch(None, infos=infos, host=host, event=ev, keep=(dec, host_block), tag=tag, n=n)
+
+    def launch_jobs(self, jobs: List[TransmuxJob]) -> "_Batch":
+        """:meth:`launch` for an explicit job list (the pipeline's own queue untouched)."""
+        try:
+            return self._launch(jobs)
+        except Exception as e:  # noqa: BLE001 - delivered to every job of the batch
+            return _Batch(jobs, error=e)
+
+    def complete_columns(self, batch: "_Batch"):
+        """Wait for a :meth:`launch_columns` batch: ``(tag, rows int64[n, INFO_WORDS], plain
+        int64[n], has_row bool[n])`` aligned with the launch columns."""
+        if batch.jobs is not None:  # CPU job path
+            _, rows, plain, has = self.complete_arrays(batch)
+            return batch.tag, rows, plain, has
+        n = batch.n
+        rows = np.zeros((n, _ts.INFO_WORDS), dtype=np.int64)
+        plain = np.full(n, -1, dtype=np.int64)
+        has = np.zeros(n, dtype=bool)
+        t3 = time.perf_counter()
+        if batch.event is not None:
+            batch.event.synchronize()
+            self._free_events.append(batch.event)
+            batch.event = None
+        self.timer.add("wait_device", time.perf_counter() - t3)
+        for (idx, _res, _es_offs, _lens), (hinfo, hlens) in zip(batch.infos, batch.host):
+            k = len(idx)
+            rows[idx] = (hinfo.numpy() if isinstance(hinfo, torch.Tensor) else np.asarray(hinfo))[:k]
+            plain[idx] = (hlens.numpy() if isinstance(hlens, torch.Tensor) else np.asarray(hlens))[:k]
+            has[idx] = True
+        return batch.tag, rows, plain, has
+
     def complete_rows(self, batch: Optional["_Batch"]) -> List[Tuple["TransmuxJob", Optional[list], int]]:
         """Wait for a launched batch and return ``(job, info row, plaintext length)`` per job
         without building the per-fragment result dicts or running callbacks (a fleet node
@@ -397,6 +474,8 @@ class _Batch:
     results: Any = None
     error: Optional[BaseException] = None
     keep: Any = None  # device/pinned buffers the batch's in-flight work uses
+    tag: Any = None  # launch_columns: the caller's columns, handed back by complete_columns
+    n: int = 0  # launch_columns: fragments in the batch
 
 
 _local = threading.local()

@@ -117,8 +117,10 @@ def test_remote_node_delivers_result_rows_and_errors():
     r1 = node.request((1, 0, 0, 5), "http://x/seg5.ts", None, Cb())
     node.request((1, 0, 0, 6), "http://x/seg6.ts", None, Cb())
     node.flush()
-    kind, reqs, handled = b.recv()
-    assert kind == "req" and [r[0] for r in reqs] == [0, 1] and handled == 0
+    kind, cols, handled = b.recv()
+    assert kind == "req" and cols[0].tolist() == [0, 1] and handled == 0
+    assert cols[1].tolist() == [[1, 0, 0, 5], [1, 0, 0, 6]] and cols[2] == ["http://x/seg5.ts", "http://x/seg6.ts"]
+    assert cols[4].tolist() == [-1, -1]  # no AES key known for these fragments
     row = [0] + [7] * (INFO_WORDS - 1)
     chunk = (np.array([r1.rid]), np.array([SOURCES.index("p2p")], dtype=np.int8), np.array([1000]),
              np.array([0.0]), np.array([2.5]), np.array([990]), np.array([True]), np.array([row], dtype=np.int64))

@@ -216,18 +216,28 @@ def test_planner_stage_rows():
     # nobody staged: the seeder stages it (src -2), the other wanter waits
     p = plan([key + [0, 1, 0, 2], key + [0, 5, 1, 2]])
     assert p.shape[0] == 1 and p[0, 5] == -2
-    # rank 1 staged (size known): it fetches (CDN row) and forwards its size to rank 0
+    # rank 1 staged (size known): it fetches (CDN row); rank 0 reserved nothing for the body
+    # (size 0), so it is not sent a copy this round -- it waits and reserves next round
     p = plan([key + [0, 1, 0, 2], key + [3000, 5, 1, 0]])
     cdn = p[p[:, 5] == -1]
     fwd = p[p[:, 5] == 1]
     assert cdn.tolist() == [key + [3000, -1, 1, 5, 0, 0]]
-    assert fwd.tolist() == [key + [3000, 1, 0, 1, 1, 0]]
+    assert fwd.tolist() == []
+    # once rank 0 announces the length it reserved (its node read it from the directory),
+    # the seeder forwards in the same round
+    p = plan([key + [3000, 1, 0, 2], key + [3000, 5, 1, 0]])
+    assert p[p[:, 5] == 1].tolist() == [key + [3000, 1, 0, 1, 1, 0]]
     # a lone unstaged want without de-duplication: stage row for itself
     p = plan([key + [0, 9, 0, 2]])
     assert p.tolist() == [key + [0, -2, 0, 9, 0, 0]]
     # one wanter is downloading it (staging): nobody else is told to, everybody waits
     assert plan([key + [0, 1, 0, 2 | 4], key + [0, 5, 1, 2]]).shape[0] == 0
     assert plan([key + [0, 9, 0, 2 | 4]]).shape[0] == 0
+    # a holder exists: an unstaged wanter that reserved too little waits, one that reserved
+    # enough gets the P2P copy
+    d.apply(1, np.array([key + [3000]], dtype=np.int64), np.zeros((0, 4), dtype=np.int64))
+    assert plan([key + [0, 1, 0, 2]]).shape[0] == 0
+    assert plan([key + [3000, 1, 0, 2]]).tolist() == [key + [3000, 1, 0, 1, 0, 0]]
 
 
 def test_player_plays_from_an_http_cdn(cdn):

@@ -228,3 +228,81 @@ def test_planner_seeds_contiguous_runs(rt):
         assert len(sns) == 16 and sns == list(range(sns[0], sns[0] + 16))
     p2p = plan[plan[:, 5] >= 0]
     assert len(p2p) == 64 * 3 and np.all(p2p[:, 8] == 1)
+
+
+# ---------------------------------------------------------------- want table
+def _add(wt, ks, size=1000, flags=0, tokens=None, ptr=0):
+    n = len(ks)
+    tok = np.arange(n, dtype=np.int64) if tokens is None else np.asarray(tokens, dtype=np.int64)
+    return wt.add(ks, np.full(n, size, dtype=np.int64), np.full(n, ptr, dtype=np.int64),
+                  np.zeros(n, dtype=np.int64), np.full(n, flags, dtype=np.int64), tok)
+
+
+def test_want_table_join_abort_finish(rt):
+    """Requests join the want of their key as tokens; aborted tokens are forgotten; a want
+    nobody waits for any more is dropped at the next selection; finishing a want returns its
+    live tokens (the delivery columns)."""
+    wt = rt.WantTable()
+    st = rt.SegmentStore(1 << 20, 256)
+    ids, created = _add(wt, keys(1, 2, 1), tokens=[10, 11, 12])
+    assert created.tolist() == [1, 1, 0] and ids[0] == ids[2] and len(wt) == 2 and wt.num_tokens == 3
+    assert wt.abort(np.array([11], dtype=np.int64)) == 1 and wt.abort1(99) is False
+    adm, rows, dropped, big, deferred = wt.select(st, None, -1, 1)
+    assert adm.tolist() == [ids[0]] and dropped.tolist() == [ids[1]] and len(big) == 0 and deferred == 0
+    assert rows[0, :5].tolist() == [1, 0, 0, 1, 1000] and rows[0, 5] == ids[0]
+    assert wt.select(st, None, -1, 2)[0].tolist() == []  # in flight: not announced again
+    tok, idx, pf = wt.finish(adm)
+    assert sorted(tok.tolist()) == [10, 12] and idx.tolist() == [0, 0] and pf.tolist() == [0]
+    assert len(wt) == 0 and wt.num_tokens == 0
+    # in-process object path: add1 returns -id-1 for a new want, the id when joining
+    r = wt.add1(1, 0, 0, 7, 500, 0, 0, 0, -2)
+    assert r < 0 and wt.add1(1, 0, 0, 7, 500, 0, 0, 0, -3) == -r - 1 and wt.lookup1(1, 0, 0, 7) == -r - 1
+
+
+def test_want_table_select_order_cap_and_backpressure(rt):
+    """Requested wants go first (FIFO, capped), prefetch-only ones fill the room left; only
+    the largest prefix the ring can place now is admitted; a want larger than the whole
+    cache is reported, the rest wait; requeued wants keep their place."""
+    wt = rt.WantTable()
+    st = rt.SegmentStore(8 * 1024, 256)
+    pf_ids, _ = _add(wt, keys(100), flags=rt.WANT_PREFETCH, tokens=[rt.NO_TOKEN])
+    ids, _ = _add(wt, keys(1, 2, 3), size=2048, tokens=[1, 2, 3])
+    adm, _, _, _, _ = wt.select(st, None, 2, 1)
+    assert adm.tolist() == ids[:2].tolist()  # cap 2: requests before the prefetch
+    wt.requeue(adm, False)
+    adm, _, _, _, deferred = wt.select(st, None, -1, 2)
+    assert adm.tolist() == ids.tolist() + pf_ids.tolist() and deferred == 0  # 3 x 2 KiB + 1 KiB fits 8 KiB
+    wt.requeue(adm, False)
+    # fill the ring with a pinned entry: only 2 KiB stay free
+    _, e, _ = st.reserve_run(keys(50), np.array([6 * 1024]), 0)
+    st.commit(e)
+    st.pin(e)
+    big, _ = _add(wt, keys(9), size=64 * 1024, tokens=[9])
+    adm, _, _, too_big, deferred = wt.select(st, None, -1, 3)
+    assert adm.tolist() == ids[:1].tolist() and too_big.tolist() == big.tolist() and deferred == 3
+    # a CRC failure requeues with force_cdn (row bit 62) and one more attempt
+    wt.requeue(adm, True)
+    info = wt.info(adm)
+    assert info[0, 7] & rt.WANT_FORCE_CDN and info[0, 9] == 1 and info[0, 8] == -1
+
+
+def test_want_table_unstaged_size_from_directory(rt):
+    """A network want whose body is not staged yet has no size; once a holder announced the
+    segment, selection reserves the holder's length (so a peer copy always fits what the
+    receiver admitted: never a reservation failure mid-round), and backpressure applies to it."""
+    wt = rt.WantTable()
+    st = rt.SegmentStore(4096, 256)
+    d = rt.Directory()
+    ids, _ = _add(wt, keys(5), size=0, flags=rt.WANT_NOT_STAGED, tokens=[1])
+    adm, rows, _, _, _ = wt.select(st, d, -1, 1)
+    assert adm.tolist() == ids.tolist() and rows[0, 4] == 0 and (rows[0, 5] >> 61) & 1
+    wt.requeue(adm, False)
+    d.apply(0, np.array([[1, 0, 0, 5, 3000]], dtype=np.int64), np.zeros((0, 4), dtype=np.int64))
+    _, e, _ = st.reserve_run(keys(60), np.array([2048]), 0)  # nearly full: 2 KiB free, 3000 B needed
+    st.commit(e)
+    st.pin(e)
+    adm, _, _, _, deferred = wt.select(st, d, -1, 2)
+    assert adm.tolist() == [] and deferred == 1  # waits rather than over-commit the ring
+    st.unpin(e)
+    adm, rows, _, _, _ = wt.select(st, d, -1, 3)
+    assert adm.tolist() == ids.tolist() and rows[0, 4] == 3000

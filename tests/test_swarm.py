@@ -3,6 +3,8 @@ exchange + CDN de-duplication, offload ratio, CRC fault injection -> CDN fallbac
 churn (offline peer), P2P toggles, live streams."""
 import threading
 
+import numpy as np
+
 import pytest
 
 from hlsjs_p2p_wrapper_amd import Hls
@@ -376,3 +378,60 @@ def test_round_wait_reports_a_dead_peer_instead_of_hanging(monkeypatch):
     h.done = Later()
     node._wait_round(h)  # completes once the event reports done
     assert h.done.n == 4
+
+
+class _Sink:
+    def __init__(self):
+        self.got = {}
+        self.failed = {}
+
+    def deliver(self, tok, src, nbytes, cdn_ms, p2p_ms, offs, eids):
+        for t, s, n in zip(tok.tolist(), src.tolist(), nbytes.tolist()):
+            self.got[t] = ("cdn", "p2p", "cache")[s], n
+
+    def fail(self, tok, status):
+        self.failed.update(zip(tok.tolist(), status.tolist()))
+
+
+def test_per_session_download_toggle_on_one_node(vod):
+    """Columnar requests of two sessions on ONE node (a fleet's players): the session with P2P
+    download off gets its fragments from the CDN, the other one from the peer that holds
+    them; the node keeps uploading (``lib/hlsjs-p2p-wrapper.js:20-36`` toggles the session's
+    own agent, not the machine)."""
+    from hlsjs_p2p_wrapper_amd.agent.node import SwarmNode
+
+    hub = ThreadHub(2)
+    urls = [f"http://cdn.test/vod/r0/seg{i}.ts" for i in range(10)]
+    ks = np.array([[7, 0, 0, i] for i in range(10)], dtype=np.int64)
+    sinks, errs = [_Sink(), _Sink()], []
+    nodes = {}
+
+    def rank(r):
+        try:
+            new_event_loop("virtual")
+            node = SwarmNode(hub.comm(r), device="cpu", cache_bytes=64 << 20, auto_tick=False)
+            nodes[r] = node
+            node.set_bulk_sink(sinks[r])
+            if r == 0:  # the holder: fetches everything first
+                node.request_batch(ks, urls, None, np.arange(10, dtype=np.int64))
+            for step in range(4):
+                if r == 1 and step == 2:
+                    node.set_session_flags(("fleet", 0), False, True)
+                    node.set_session_flags(("fleet", 1), True, True)
+                    node.request_batch(ks[:5], urls[:5], None, np.arange(5, dtype=np.int64),
+                                       force_cdn=np.ones(5, dtype=bool))  # session 0: download off
+                    node.request_batch(ks[5:], urls[5:], None, np.arange(5, 10, dtype=np.int64) | (1 << 40))
+                node.complete_round(node.launch_round())
+        except BaseException as e:  # noqa: BLE001
+            errs.append(e)
+            hub.abort()
+
+    ts = [threading.Thread(target=rank, args=(r,)) for r in range(2)]
+    [t.start() for t in ts]
+    [t.join(60) for t in ts]
+    assert not errs, errs
+    assert all(v[0] == "cdn" for v in sinks[0].got.values()) and len(sinks[0].got) == 10
+    s1 = sinks[1].got
+    assert [s1[t][0] for t in range(5)] == ["cdn"] * 5  # download off: CDN only
+    assert [s1[t | (1 << 40)][0] for t in range(5, 10)] == ["p2p"] * 5  # the other session: peers
+    assert nodes[1].download_on and nodes[1].upload_on and nodes[1].session_flags(("fleet", 0)) == (False, True)
