@@ -64,6 +64,17 @@ class PeerAgent:
         self.live_evict = bool(gs.get("liveWindowEvict", True))
         self._evicted_below = -1
         self.evicted = 0
+        # live buffer negotiation: the reference moved ``liveMinBufferMargin`` into the agent
+        # (``CHANGELOG.md:13-15``), and the bridge exposes ``isLive`` / ``getBufferLevelMax`` /
+        # ``setBufferMarginLive`` for it (``lib/integration/player-interface.js:31-66``).  On a
+        # live stream the agent keeps the player's buffer target ``liveMinBufferMargin``
+        # seconds below the live sync point, the room the swarm has to exchange the newest
+        # segments before the player needs them; a VOD stream is left alone.
+        margin = gs.get("liveMinBufferMargin", self.p2pConfig.get("liveMinBufferMargin", 4.0)
+                        if isinstance(self.p2pConfig, dict) else 4.0)
+        self.live_margin = float(margin or 0.0)
+        self.is_live: Optional[bool] = None  # unknown until a level playlist is parsed
+        self.live_buffer_level: Optional[float] = None
         self.disposed = False
         self._requests = []
         if playerInterface is not None and hasattr(playerInterface, "addEventListener"):
@@ -75,6 +86,8 @@ class PeerAgent:
         ``onSuccess(data)`` / ``onError(err)``.  Returns the request handle (``abort()``)."""
         if self.disposed:
             raise RuntimeError("PeerAgent is disposed")
+        if self.is_live is None:
+            self.negotiate_live_buffer()
         url = _get(reqInfo, "url")
         headers = _get(reqInfo, "headers") or {}
         tv = segmentView.trackView
@@ -88,8 +101,37 @@ class PeerAgent:
         """The media element whose playhead drives prefetch and eviction."""
         self.media = media
 
+    def negotiate_live_buffer(self) -> Optional[bool]:
+        """Once a level playlist is parsed: on a live stream, set the player's buffer target
+        to ``getBufferLevelMax() - liveMinBufferMargin`` through ``setBufferMarginLive``.
+        Returns whether the stream is live (None: not known yet, asked again later)."""
+        if self.is_live is not None or self.disposed or self.player is None or not hasattr(self.player, "isLive"):
+            return self.is_live
+        try:
+            live = bool(self.player.isLive())
+        except Exception:  # noqa: BLE001 - playlists not parsed yet
+            return None
+        self.is_live = live
+        if not live:
+            return False
+        try:
+            level_max = float(self.player.getBufferLevelMax())
+        except Exception as e:  # noqa: BLE001 - a negative buffer target in the player config
+            log.error("%s", e)
+            return True
+        level = level_max - self.live_margin
+        if level <= 0:
+            log.error("Invalid configuration: hlsjsConfig buffer target (%.1f s) must be greater than "
+                      "p2pConfig.liveMinBufferMargin (%.1f s)", level_max, self.live_margin)
+            return True
+        self.player.setBufferMarginLive(level)
+        self.live_buffer_level = level
+        return True
+
     def before_round(self) -> None:
         """Node hook, run right before each round's wants are sent."""
+        if self.is_live is None:
+            self.negotiate_live_buffer()
         if self.live_evict:
             self.evict_live_window()
         self.plan_prefetch()

@@ -9,7 +9,9 @@ browser's timer queue, and every loader timestamp comes from ``performance.now()
 Two clocks:
 
 * ``clock="real"``    — ``time.perf_counter`` in milliseconds; timers fire when due.  Used
-  by ``bench.py`` and production players.
+  by ``bench.py`` and production players.  ``speed`` > 1 compresses time (the live bench
+  plays a channel faster than real time) and ``epoch`` pins the origin of the clock to a
+  wall-clock instant shared by processes.
 * ``clock="virtual"`` — a discrete-event clock: when no callback is ready the loop *jumps*
   to the next timer.  Tests run minutes of playback (retries with 64 s back-off, live
   playlist refreshes) in milliseconds, deterministically.
@@ -50,10 +52,17 @@ class TimerHandle:
 class EventLoop:
     """Timer queue with a real or virtual millisecond clock."""
 
-    def __init__(self, clock: str = "real") -> None:
+    def __init__(self, clock: str = "real", speed: float = 1.0, epoch: Optional[float] = None) -> None:
         if clock not in ("real", "virtual"):
             raise ValueError("clock must be 'real' or 'virtual'")
+        if speed <= 0:
+            raise ValueError("speed must be positive")
         self.clock = clock
+        # a real clock may run `speed` times faster than the wall (a time-compressed live
+        # channel: playlist reloads, ticks and the origin's live edge all advance together);
+        # with `epoch` (a time.time() value) every process's loop reads the same time
+        self.speed = float(speed)
+        self.epoch = epoch
         self._t0 = time.perf_counter()
         self._vnow = 0.0
         # heap of (when, seq, handle): tuple order compares in C (a handle __lt__ cost a
@@ -75,7 +84,9 @@ class EventLoop:
         """``performance.now()``: milliseconds since loop creation."""
         if self.clock == "virtual":
             return self._vnow
-        return (time.perf_counter() - self._t0) * 1000.0
+        if self.epoch is not None:
+            return (time.time() - self.epoch) * 1000.0 * self.speed
+        return (time.perf_counter() - self._t0) * 1000.0 * self.speed
 
     performance_now = now
 
@@ -211,7 +222,7 @@ class EventLoop:
             if not block:
                 return True
             wait = max_wait_ms if deadline is None or self.clock == "virtual" else \
-                min(max(0.0, deadline - self.now()), max_wait_ms)
+                min(max(0.0, deadline - self.now()) / self.speed, max_wait_ms)
             self._wake.wait(wait / 1000.0)
             self._wake.clear()
             return True
@@ -220,8 +231,8 @@ class EventLoop:
         if self.clock == "virtual":
             self._vnow = max(self._vnow, deadline)
             return True
-        if block:
-            wait = min(max(0.0, deadline - self.now()), max_wait_ms) / 1000.0
+        if block:  # (loop ms -> wall seconds)
+            wait = min(max(0.0, deadline - self.now()) / self.speed, max_wait_ms) / 1000.0
             if wait > 0:
                 self._wake.wait(wait)
                 self._wake.clear()
@@ -268,8 +279,8 @@ def set_event_loop(loop: Optional[EventLoop]) -> None:
     _local.loop = loop
 
 
-def new_event_loop(clock: str = "real") -> EventLoop:
-    loop = EventLoop(clock)
+def new_event_loop(clock: str = "real", speed: float = 1.0, epoch: Optional[float] = None) -> EventLoop:
+    loop = EventLoop(clock, speed=speed, epoch=epoch)
     set_event_loop(loop)
     return loop
 

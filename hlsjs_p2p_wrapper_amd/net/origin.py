@@ -27,6 +27,7 @@ import hashlib
 import math
 import re
 import threading
+import time
 from dataclasses import dataclass, field
 from typing import Dict, List, Optional, Sequence, Tuple
 
@@ -93,7 +94,8 @@ class SyntheticHlsOrigin:
                  segment_duration: float = 4.0, num_segments: Optional[int] = 10, live: bool = False,
                  window: int = 6, encrypted: bool = False, pool_size: Optional[int] = None, redundant: int = 1,
                  seed: int = 1, with_id3: bool = False, start_sn: int = 0, pin_memory: Optional[bool] = None,
-                 loop=None, register: bool = True, live_speed: float = 1.0) -> None:
+                 loop=None, register: bool = True, live_speed: float = 1.0,
+                 live_epoch: Optional[float] = None) -> None:
         self.base_url = base_url if base_url.endswith("/") else base_url + "/"
         self.renditions = list(renditions) or list(PRESET_1080P_6M)
         self.segment_duration = float(segment_duration)
@@ -106,6 +108,9 @@ class SyntheticHlsOrigin:
         self.with_id3 = with_id3
         self.start_sn = start_sn
         self.live_speed = live_speed
+        # live edge from the wall clock (time.time() at which the window was full): every
+        # process serving or playing the channel agrees on it without sharing a loop
+        self.live_epoch = live_epoch
         self._paths: Dict[str, Tuple[int, int]] = {}  # segment path -> (level, sn)
         if pool_size is None:
             pool_size = num_segments if (num_segments is not None and not live) else 16
@@ -161,6 +166,9 @@ class SyntheticHlsOrigin:
             return self.start_sn + (self.num_segments or 0) - 1
         if self._manual_edge is not None:
             return self._manual_edge
+        if self.live_epoch is not None:
+            produced = int(max(0.0, time.time() - self.live_epoch) * self.live_speed / self.segment_duration)
+            return self.start_sn + self.window - 1 + produced
         now = self.loop.now() if self.loop is not None else 0.0
         produced = int(((now - self._t0) / 1000.0) * self.live_speed / self.segment_duration)
         return self.start_sn + self.window - 1 + produced

@@ -284,7 +284,13 @@ class RemoteNode:
 
     def flush(self) -> None:
         """Send everything queued since the last flush (one message per kind), with the count
-        of answer batches handled so far (the node paces its rounds on it)."""
+        of answer batches handled so far (the node paces its rounds on it).  The agents'
+        per-round planning (live buffer negotiation, live-window eviction) runs first, as it
+        does before a local node's round."""
+        for agent in self._agents:
+            hook = getattr(agent, "before_round", None)
+            if hook is not None:
+                hook()
         for m in self._out:  # flags / payload mode first: they apply to the requests below
             self.conn.send(m)
         self._out = []

@@ -435,3 +435,35 @@ def test_per_session_download_toggle_on_one_node(vod):
     assert [s1[t][0] for t in range(5)] == ["cdn"] * 5  # download off: CDN only
     assert [s1[t | (1 << 40)][0] for t in range(5, 10)] == ["p2p"] * 5  # the other session: peers
     assert nodes[1].download_on and nodes[1].upload_on and nodes[1].session_flags(("fleet", 0)) == (False, True)
+
+
+def _agent_of(w):
+    return w._wrapper.peerAgentModule
+
+
+def test_agent_negotiates_the_live_buffer_margin():
+    """On a live stream the agent asks the bridge ``isLive()`` and sets the player's buffer
+    target to ``getBufferLevelMax() - liveMinBufferMargin`` through ``setBufferMarginLive``
+    (``lib/integration/player-interface.js:31-66``, ``CHANGELOG.md:15``); on VOD it leaves the
+    player's config alone."""
+    live = SyntheticHlsOrigin("http://cdn.test/live/", renditions=[Rendition(800_000, 640, 360)], live=True,
+                              window=6, num_segments=None, pool_size=8, encrypted=True)
+    live.advance(4)
+    seen = {}
+
+    def grab(r, node, w):
+        seen[r] = w
+
+    out = run_swarm(1, live, until=lambda m: m.currentTime > 18.0, before=grab,
+                    cfg_extra={"liveMinBufferMargin": 6.0})
+    assert out[0]["ok"]
+    agent = _agent_of(seen[0])
+    assert agent.is_live is True and agent.live_buffer_level == pytest.approx(30.0 - 6.0)
+    cfg = agent.player.hls.config
+    assert cfg.maxBufferLength == pytest.approx(24.0) and cfg.maxBufferSize == 0
+
+    vod = SyntheticHlsOrigin("http://cdn.test/vod2/", renditions=[Rendition(800_000, 640, 360)], num_segments=6)
+    out = run_swarm(1, vod, until=10.0, before=grab)
+    agent = _agent_of(seen[0])
+    assert out[0]["ok"] and agent.is_live is False and agent.live_buffer_level is None
+    assert agent.player.hls.config.maxBufferLength == 30  # the wrapper default, untouched
