@@ -56,7 +56,7 @@ CONFIGS = {
     # real-time live pace every peer would take 1 segment per 4 s); the window is served as a
     # complete playlist, so no mid-run playlist reloads (live mode, sliding windows and
     # live-window eviction are covered by tests/test_swarm.py)
-    "1080p6m": ("1080p", True, 4.0, "1080p 6 Mb/s HLS live-channel DVR catch-up (AES-128, 4 s TS segments, 8 peers)"),
+    "1080p6m": ("1080p", True, 4.0, "1080p 6 Mb/s HLS live-channel DVR catch-up (AES-128, 4 s TS segments)"),
     "1080p6m-clear": ("1080p", False, 4.0, "1080p 6 Mb/s HLS (clear, 4 s TS segments)"),
     "abr5": ("abr5", True, 4.0, "5-rendition ABR ladder (AES-128, 4 s TS)"),
     "4k25m": ("4k", True, 4.0, "4K 25 Mb/s HLS (AES-128, 4 s TS segments)"),
@@ -65,7 +65,12 @@ CONFIGS = {
     "hostcost-abr": ("tiny-abr", True, 4.0, "5 x 20-100 kb/s ABR ladder (AES-128) - host-overhead probe"),
     # diagnostic only: ~4 KB segments, for the CPU host-cost harness (device ops ~free)
     "hostcost-micro": ("micro", True, 4.0, "8 kb/s HLS (AES-128) - host-overhead probe, CPU harness"),
+    # BASELINE config 2 at the live edge: a sliding live playlist (reloads, window slides,
+    # live-window eviction in the timed region) played in real time by every player, on a
+    # clock running --live-speed times faster than the wall; the rate is the channel's
+    "1080p6m-live": ("1080p", True, 4.0, "1080p 6 Mb/s live HLS at the live edge (AES-128, 4 s TS segments)"),
 }
+LIVE = {"1080p6m-live"}
 
 
 def parse():
@@ -107,6 +112,12 @@ def parse():
                         "origin's segment pools live in HBM, so CDN fetches are device-to-device copies "
                         "standing in for segments that arrive over xGMI (the per-GPU ceiling at N=8 "
                         "without the PCIe bound)")
+    p.add_argument("--live-speed", type=float, default=100.0,
+                   help="live configs: media seconds per wall second (the channel publishes a segment "
+                        "every segment_s / speed seconds; players reload and play on the same clock)")
+    p.add_argument("--live-window", type=int, default=15, help="live configs: playlist window in segments")
+    p.add_argument("--round-ms", type=float, default=5.0,
+                   help="live configs: one node round per this many wall milliseconds (paced)")
     p.add_argument("--verbose", action="store_true")
     return p.parse_args()
 
@@ -151,6 +162,11 @@ def _workload(args):
     depth = 1 if args.sync_steps else args.lag + 2  # rounds a fragment spends in flight (see step())
     hls_config = {"maxFragLoadsInFlight": K * depth, "maxBufferLength": 1e9, "maxMaxBufferLength": 1e9,
                   "startPosition": 0, "fragLoadingTimeOut": 600_000, "tickInterval": 1e9}
+    if args.config in LIVE:
+        # every player watches the same live channel at the live sync point, in real time on
+        # the compressed clock; the agent negotiates its buffer target (live margin)
+        origin_kwargs.update(live=True, window=args.live_window, num_segments=None, live_speed=args.live_speed)
+        hls_config = {"maxFragLoadsInFlight": 8, "fragLoadingTimeOut": 60_000}
     if preset != "abr5":
         hls_config["startLevel"] = 0
     p2p_base = {"streamrootKey": "bench", "contentId": "bench-1080p"}
@@ -174,8 +190,12 @@ def _spawn_players(W, world, rank, origin_kwargs, hls_config, p2p_base, n_segmen
         for w in range(W):
             parent, child = ctx.Pipe()
             spec = {"origin": dict(origin_kwargs, pin_memory=False),
-                    "hls_config": dict(hls_config, startPosition=w * n_segments * seg_dur),
+                    "hls_config": dict(hls_config, startPosition=w * n_segments * seg_dur)
+                    if not origin_kwargs.get("live") else dict(hls_config),
                     "p2p_config": dict(p2p_base), "world": world, "rank": rank}
+            if origin_kwargs.get("live"):  # the player's loop runs on the channel's clock
+                spec["clock_speed"] = float(origin_kwargs["live_speed"])
+                spec["media_mode"] = "realtime"
             pr = ctx.Process(target=player_main, args=(child, spec), daemon=True, name=f"hlsp2p-player{w}")
             pr.start()
             child.close()
@@ -192,6 +212,8 @@ def _spawn_players(W, world, rank, origin_kwargs, hls_config, p2p_base, n_segmen
 
 def main() -> int:
     args = parse()
+    if args.config in LIVE and args.players < 1:
+        raise SystemExit("live configs run in fleet mode: --players >= 1")
     if args.sync_steps and args.players:
         # the fleet's players pace the rounds with batches in flight; an unpipelined step is
         # a diagnostic of the in-process path only
@@ -446,7 +468,15 @@ def _fleet(args, world, rank, device, use_gpu, node, origin, players, desc, encr
     debug = os.environ.get("HLSP2P_FLEET_DEBUG")
     nstep = [0]
 
+    live = args.config in LIVE
+    pace = {"next": 0.0}
+
     def step():
+        if live:  # a live channel: rounds at a fixed wall-clock cadence, not as fast as possible
+            now = time.perf_counter()
+            if pace["next"] > now:
+                time.sleep(pace["next"] - now)
+            pace["next"] = max(pace["next"], now) + args.round_ms / 1e3
         if args.churn > 0 and world > 1:  # BASELINE config 3: the same rotation as the in-process path
             online = (nstep[0] // args.churn) % (world + 1) != rank
             if online != node.online:
@@ -464,8 +494,8 @@ def _fleet(args, world, rank, device, use_gpu, node, origin, players, desc, encr
         state["b"] = b
         nstep[0] += 1
         if debug and nstep[0] % 20 == 0:
-            print(f"# fleet step {nstep[0]} round {node.round} wants {len(node._wants)} "
-                  f"pending {[len(r) for r in server._by_rid]} requests {server.requests} sent {server.sent} "
+            print(f"# fleet step {nstep[0]} round {node.round} wants {node.pending()} "
+                  f"queued {[q.n for q in server._q]} requests {server.requests} sent {server.sent} "
                   f"delivered-queue {len(server._delivered)} last {node.last_round}", file=sys.stderr, flush=True)
 
     def sync():
@@ -492,8 +522,14 @@ def _fleet(args, world, rank, device, use_gpu, node, origin, players, desc, encr
                 raise RuntimeError("fleet players did not start")
         if world > 1:
             node.comm.barrier()
+        go = {}
+        if live:  # the channel's epoch: rank 0's clock, shared by every rank's node and players
+            ep = np.array([int((time.time() + 0.2) * 1e6)], dtype=np.int64)
+            if world > 1:
+                ep = node.comm.allgather_control(ep)[0]
+            origin.live_epoch = go["live_epoch"] = float(ep[0]) / 1e6
         for c in conns:
-            c.send(("go",))
+            c.send(("go", go))
         while True:
             step()
             up = np.array([int(all(n > 0 or not o for n, o in zip(server.requests, server.open)))],
@@ -539,6 +575,7 @@ def _fleet(args, world, rank, device, use_gpu, node, origin, players, desc, encr
                 raise TimeoutError("fleet players did not acknowledge the window marks")
         m0, m1 = server.marks.get("t0", {}), server.marks["t1"]
         done = sum(m1[w]["buffered"] - m0.get(w, {"buffered": 0})["buffered"] for w in m1)
+        lat = [x for w in m1 for x in m1[w].get("live_latency_s", [])]
         errors = sum(m1[w]["errors"] for w in m1)
         d_segs = sum(s1[k] - s0[k] for k in ("cdn_segments", "p2p_segments"))
         vals = np.array([done, s1["cdn"] - s0["cdn"], s1["p2p"] - s0["p2p"], int(elapsed * 1e9), errors, d_segs],
@@ -551,6 +588,12 @@ def _fleet(args, world, rank, device, use_gpu, node, origin, players, desc, encr
             tot, max_ns = vals, int(vals[3])
         result = _result(args, world, tot, max_ns / 1e9, origin, K, desc, encrypted, seg_dur, use_gpu, numa_node,
                          dist, players=W, transport=getattr(node.comm, "data_transport", None))
+        if live:
+            result["config"].update(live=True, live_speed=args.live_speed, live_window=args.live_window,
+                                    round_ms=args.round_ms, evicted_segments=server.evicted)
+            if lat:  # publication -> buffered, in media seconds (the live sync point is 30 s back)
+                result["live_latency_s"] = {"p50": round(float(np.percentile(lat, 50)), 2),
+                                            "p95": round(float(np.percentile(lat, 95)), 2), "n": len(lat)}
         if args.verbose:
             ipc = getattr(node.comm, "_ipc", None)
             plane = getattr(node.comm, "data_transport", "local") + (
@@ -604,7 +647,10 @@ def _result(args, world, tot, max_s, origin, K, desc, encrypted, seg_dur, use_gp
         "offload_ratio": round(float(tot[2]) / max(1.0, float(tot[1] + tot[2])), 4),
         "goodput_GBps": round(float(tot[1] + tot[2]) / max_s / 1e9, 3),  # bytes delivered to the players
         "errors": int(tot[4]),
-        "config": {"model": desc, "global_batch": inflight * world, "seq_len": seg_bytes,
+        "config": {"model": f"{desc}, {world} peer{'s' if world > 1 else ''} ({world} x MI355X)" if use_gpu
+                   else f"{desc}, {world} peer{'s' if world > 1 else ''} (CPU)",
+                   "offload": "measured" if world > 1 else "n/a (no peers: one rank fetches everything from the CDN)",
+                   "global_batch": inflight * world, "seq_len": seg_bytes,
                    "parallelism": f"swarm{world}" + (f"-{_data_plane(dist, transport)}" if world > 1 else ""),
                    "inflight_per_gpu": inflight, "players_per_gpu": max(1, players),
                    "player_processes": players > 0, "encrypted": encrypted, "segment_s": seg_dur,

@@ -519,6 +519,7 @@ class FleetServer:
         self.ready: set = set()
         self.requests = [0] * W
         self.sent = 0
+        self.evicted = 0  # cache entries dropped by the players' live-window eviction
         self.batches_sent = [0] * W  # answer batches sent to each player ...
         self.batches_done = [0] * W  # ... and handled by it (reported back)
         node.set_bulk_sink(self)
@@ -586,8 +587,8 @@ class FleetServer:
                         self._q[w].drop(rids)  # not handed to the node yet
                         tok = (np.fromiter(rids, dtype=np.int64, count=len(rids)) | (w << TOKEN_SHIFT))
                         node.abort_tokens(tok)
-                    elif kind == "evict":
-                        node.store.evict_below(msg[1], msg[2])
+                    elif kind == "evict":  # a live window slid: its old segments cannot be asked for
+                        self.evicted += int(node.store.evict_below(msg[1], msg[2]))
                     elif kind == "flags":  # this player's session toggles only
                         self._down[w] = bool(msg[1])
                         node.set_session_flags(("fleet", w), bool(msg[1]), bool(msg[2]))
@@ -772,7 +773,8 @@ def player_main(conn: Any, spec: Dict[str, Any]) -> None:
     if torch.cuda.device_count():
         log.warning("fleet player sees %d GPU(s); it should not (HIP_VISIBLE_DEVICES)", torch.cuda.device_count())
     set_current_node(None)
-    loop = new_event_loop("real")
+    speed = float(spec.get("clock_speed", 1.0))
+    loop = new_event_loop("real", speed=speed)  # a live bench's channel runs on a compressed clock
     origin = SyntheticHlsOrigin(**spec["origin"])
     p2p = copy.deepcopy(spec["p2p_config"])
     gs = dict(p2p.get("gpuSwarm") or {})
@@ -780,11 +782,17 @@ def player_main(conn: Any, spec: Dict[str, Any]) -> None:
                        "fleetPayload": bool(gs.get("fleetPayload", False))}
     node = node_for_config(p2p)
     hls = Hls(dict(spec["hls_config"]), p2p)
-    media = MediaElement(mode="drain", loop=loop)
+    media = MediaElement(mode=spec.get("media_mode", "drain"), loop=loop)
     counters = {"buffered": 0, "errors": 0, "level_switches": 0, "bytes": 0}
+    live_lat: List[float] = []  # media seconds from a live segment's publication to its buffering
 
     def on_buffered(e, d):
         counters["buffered"] += 1
+        if origin.live and origin.live_epoch is not None:
+            sn = d["frag"].sn
+            published = origin.live_epoch + (sn - (origin.start_sn + origin.window - 1)) * \
+                origin.segment_duration / origin.live_speed
+            live_lat.append((time.time() - published) * origin.live_speed)
 
     hls.on(Hls.Events.FRAG_BUFFERED, on_buffered)
     hls.on(Hls.Events.ERROR, lambda e, d: counters.__setitem__("errors", counters["errors"] + 1))
@@ -795,6 +803,9 @@ def player_main(conn: Any, spec: Dict[str, Any]) -> None:
     while True:
         msg = conn.recv()
         if msg[0] == "go":
+            opts = msg[1] if len(msg) > 1 else {}
+            if opts.get("live_epoch") is not None:  # the channel's clock, shared with the node
+                origin.live_epoch = float(opts["live_epoch"])
             break
         if msg[0] == "stop":
             node.close()
@@ -805,6 +816,7 @@ def player_main(conn: Any, spec: Dict[str, Any]) -> None:
     sc = hls.streamController
 
     def drain():
+        loop.run_once(block=False)  # due timers too (live playlist reloads, the playback clock)
         for _ in range(1000):
             if not loop._ready and not loop._threadsafe:
                 return
@@ -839,7 +851,11 @@ def player_main(conn: Any, spec: Dict[str, Any]) -> None:
                 msg = node.control.pop(0)
                 if msg[0] == "mark":
                     counters["bytes"] = node.stats.get("cdn", 0) + node.stats.get("p2p", 0)
-                    conn.send(("mark", msg[1], dict(counters)))
+                    out = dict(counters)
+                    if live_lat:  # live latency behind the edge since the previous mark
+                        out["live_latency_s"] = live_lat[:]
+                        live_lat.clear()
+                    conn.send(("mark", msg[1], out))
                 elif msg[0] == "stop":
                     return
     finally:

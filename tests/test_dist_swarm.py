@@ -203,3 +203,17 @@ def test_ipc_outbox_slots_follow_the_packing_order():
     assert _outbox_slots(table, 3, 256) == [(1792, 0)]
     assert _outbox_slots(table, 0, 256) == []
     assert _outbox_slots(np.array([0, 0], dtype=np.int64), 1, 256) == []
+
+
+def test_bench_live_edge_two_ranks():
+    """BASELINE config 2 at the live edge through the driver's launch path (2 ranks x 2
+    players, gloo, CPU): a sliding live playlist on a compressed clock, every player in real
+    time at the live sync point, playlist reloads, the cache evicting segments that slid out
+    of the window inside the timed region; the swarm fetches each segment from the CDN once."""
+    res = _bench_cpu(_free_port(), "--players", "2", "--steps", "400", "--live-speed", "100", "--live-window", "10",
+                     config="1080p6m-live")
+    assert res["errors"] == 0 and res["value"] > 0
+    cfg = res["config"]
+    assert cfg["live"] is True and "live" in cfg["model"] and cfg["evicted_segments"] > 0
+    assert 0.3 < res["offload_ratio"] <= 0.52  # each segment crosses the CDN once per swarm of 2
+    assert res["live_latency_s"]["p50"] < 30.0  # well ahead of the 30 s live sync point
