@@ -22,9 +22,6 @@ hipError_t launch_ts_demux(const uint8_t*, const int64_t*, const int64_t*, const
                            int64_t*, int32_t*, uint8_t*, const int64_t*, int64_t*, int64_t, int64_t*, hipStream_t);
 hipError_t launch_range_select(const double*, const int64_t*, const int64_t*, const double*, const double*, int64_t*,
                                int64_t*, int64_t, int64_t, hipStream_t);
-hipError_t launch_key_hash(const int32_t*, uint64_t*, int64_t, hipStream_t);
-hipError_t launch_table_insert(void*, uint64_t, const int32_t*, const int64_t*, int64_t, int32_t*, hipStream_t);
-hipError_t launch_table_lookup(const void*, uint64_t, const int32_t*, int64_t*, int64_t, int, hipStream_t);
 hipError_t launch_segment_copy(const uint8_t*, uint8_t*, const int64_t*, const int64_t*, const int64_t*,
                                const int64_t*, int, int64_t, hipStream_t);
 }  // namespace dev
@@ -179,38 +176,6 @@ void range_select(Tensor starts, Tensor track_off, Tensor q_track, Tensor q_begi
      "range_select");
 }
 
-void key_hash(Tensor keys, Tensor out) {
-  const int64_t n = keys.numel() / 4;
-  check(keys, "keys", torch::kInt32);
-  check(out, "out", torch::kInt64, n);
-  ok(D::launch_key_hash(cptr<int32_t>(keys), mptr<uint64_t>(out), n, stream()), "key_hash");
-}
-
-void table_insert(Tensor slots, Tensor keys, Tensor values, Tensor ok_out) {
-  const int64_t n = keys.numel() / 4;
-  check(slots, "slots", torch::kInt64);
-  check(keys, "keys", torch::kInt32);
-  check(values, "values", torch::kInt64, n);
-  check(ok_out, "ok", torch::kInt32, n);
-  const int64_t cap = slots.numel() / 4;
-  TORCH_CHECK(cap > 0 && (cap & (cap - 1)) == 0, "slot count must be a power of two");
-  ok(D::launch_table_insert(slots.data_ptr(), static_cast<uint64_t>(cap - 1), cptr<int32_t>(keys),
-                            cptr<int64_t>(values), n, mptr<int32_t>(ok_out), stream()),
-     "table_insert");
-}
-
-void table_lookup(Tensor slots, Tensor keys, Tensor out, bool erase) {
-  const int64_t n = keys.numel() / 4;
-  check(slots, "slots", torch::kInt64);
-  check(keys, "keys", torch::kInt32);
-  check(out, "out", torch::kInt64, n);
-  const int64_t cap = slots.numel() / 4;
-  TORCH_CHECK(cap > 0 && (cap & (cap - 1)) == 0, "slot count must be a power of two");
-  ok(D::launch_table_lookup(slots.data_ptr(), static_cast<uint64_t>(cap - 1), cptr<int32_t>(keys), mptr<int64_t>(out),
-                            n, erase ? 1 : 0, stream()),
-     "table_lookup");
-}
-
 void segment_copy(Tensor src, Tensor dst, Tensor src_off, Tensor dst_off, Tensor len, Tensor chunk_prefix,
                   int64_t total_chunks) {
   const int64_t n = src_off.numel();
@@ -340,9 +305,6 @@ TORCH_LIBRARY(hlsp2p, m) {
         "int max_pes, Tensor(f!) info) -> ()");
   m.def("range_select(Tensor starts, Tensor track_off, Tensor q_track, Tensor q_begin, Tensor q_dur, "
         "Tensor(a!) out_lo, Tensor(b!) out_hi) -> ()");
-  m.def("key_hash(Tensor keys, Tensor(a!) out) -> ()");
-  m.def("table_insert(Tensor(a!) slots, Tensor keys, Tensor values, Tensor(b!) ok_out) -> ()");
-  m.def("table_lookup(Tensor(a!) slots, Tensor keys, Tensor(b!) out, bool erase) -> ()");
   m.def("segment_copy(Tensor src, Tensor(a!) dst, Tensor src_off, Tensor dst_off, Tensor len, Tensor chunk_prefix, "
         "int total_chunks) -> ()");
 }
@@ -352,9 +314,6 @@ TORCH_LIBRARY_IMPL(hlsp2p, CUDA, m) {
   m.impl("crc32_batch", &crc32_batch);
   m.impl("ts_demux", &ts_demux);
   m.impl("range_select", &range_select);
-  m.impl("key_hash", &key_hash);
-  m.impl("table_insert", &table_insert);
-  m.impl("table_lookup", &table_lookup);
   m.impl("segment_copy", &segment_copy);
 }
 
@@ -373,9 +332,6 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("scatter_out") = py::none());
   m.def("ts_demux", &ts_demux);
   m.def("range_select", &range_select);
-  m.def("key_hash", &key_hash);
-  m.def("table_insert", &table_insert);
-  m.def("table_lookup", &table_lookup);
   m.def("segment_copy", &segment_copy);
   m.def("device_cus", &device_cus);
   m.def("h2d_batch", &h2d_batch, pybind11::arg("dst"), pybind11::arg("dst_off"), pybind11::arg("src_ptr"),

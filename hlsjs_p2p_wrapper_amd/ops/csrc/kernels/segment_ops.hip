@@ -1,18 +1,16 @@
-// Segment-identity and data-movement kernels.
+// Segment data-movement kernels.
 //
 //  * range_select_kernel  (K1) — batched MediaMap.getSegmentList: for (track, t0, dur)
 //    queries over per-track sorted fragment start times (f64), two binary searches give
 //    the contiguous index range with t0 <= start <= t0 + dur (closed, as the reference's
 //    linear scan at media-map.js:41-51).
-//  * key_hash_kernel      (K2) — 64-bit hash of [swarm, level, urlId, sn] keys (the same
-//    mix as the host SegKeyHash, so host and device agree).
-//  * device hash table    (K3) — open addressing, linear probing, 32-byte slots
-//    {u64 tag, u32 key[4], i64 value}; insert claims a slot with a 64-bit CAS on the tag,
-//    lookup / erase are read-mostly.  This is the HBM-resident cache index used for
-//    on-device residency queries (batched lookups of wanted keys without a host trip).
 //  * segment_copy_kernel  (K4) — batched byte-range copy (pack a peer's non-contiguous
-//    segments into one send buffer, byte-range slicing of cached segments); dwordx4
-//    when both sides are 16-byte aligned, byte tail otherwise.
+//    segments into one send buffer, byte-range slicing of cached segments, the fleet's
+//    payload copies); dwordx4 when both sides are 16-byte aligned, byte tail otherwise.
+//
+// The segment index (K2 key hash, K3 cache table) is host-native by design: every round is
+// planned on the host (runtime/store.cpp SegmentStore, runtime/wants.cpp WantTable, both
+// keyed by SegKeyHash), so a device-side copy of the index had no consumer and was removed.
 #include "common.h"
 
 namespace hlsp2p {
@@ -47,88 +45,6 @@ __global__ void range_select_kernel(const double* __restrict__ starts, const int
   }
   out_lo[q] = first;
   out_hi[q] = lo;
-}
-
-// ------------------------------------------------------------------ K2
-__device__ __forceinline__ uint64_t mix64(uint64_t z) {
-  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
-  z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
-  return z ^ (z >> 31);
-}
-
-__device__ __forceinline__ uint64_t key_hash(uint32_t s, uint32_t l, uint32_t u, uint32_t n) {
-  const uint64_t a = (uint64_t(s) << 32) | l;
-  const uint64_t b = (uint64_t(u) << 32) | n;
-  return mix64(a ^ mix64(b + 0x9E3779B97F4A7C15ull));
-}
-
-__global__ void key_hash_kernel(const int32_t* __restrict__ keys, uint64_t* __restrict__ out, int64_t n) {
-  const int64_t i = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
-  if (i >= n) return;
-  const uint4 k = reinterpret_cast<const uint4*>(keys)[i];
-  out[i] = key_hash(k.x, k.y, k.z, k.w);
-}
-
-// ------------------------------------------------------------------ K3
-struct alignas(32) Slot {
-  unsigned long long tag;  // 0 empty, 1 tombstone, else hash | 2
-  uint32_t key[4];
-  long long value;
-};
-
-__device__ __forceinline__ unsigned long long make_tag(uint64_t h) { return (h | 2ull); }
-
-__global__ void table_insert_kernel(Slot* __restrict__ slots, uint64_t mask, const int32_t* __restrict__ keys,
-                                    const int64_t* __restrict__ values, int64_t n, int32_t* __restrict__ ok) {
-  const int64_t i = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
-  if (i >= n) return;
-  const uint4 k = reinterpret_cast<const uint4*>(keys)[i];
-  const uint64_t h = key_hash(k.x, k.y, k.z, k.w);
-  const unsigned long long tag = make_tag(h);
-  uint64_t pos = h & mask;
-  for (uint64_t probe = 0; probe <= mask; ++probe, pos = (pos + 1) & mask) {
-    Slot* s = slots + pos;
-    unsigned long long cur = __hip_atomic_load(&s->tag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    if (cur == tag && s->key[0] == k.x && s->key[1] == k.y && s->key[2] == k.z && s->key[3] == k.w) {
-      s->value = values[i];  // update in place
-      ok[i] = 1;
-      return;
-    }
-    if (cur == 0 || cur == 1) {
-      const unsigned long long prev = atomicCAS(&s->tag, cur, tag);
-      if (prev == cur) {
-        s->key[0] = k.x; s->key[1] = k.y; s->key[2] = k.z; s->key[3] = k.w;
-        s->value = values[i];
-        ok[i] = 1;
-        return;
-      }
-      // lost the race: re-examine this slot
-      --probe;
-      pos = (pos - 1) & mask;
-    }
-  }
-  ok[i] = 0;  // table full
-}
-
-__global__ void table_lookup_kernel(const Slot* __restrict__ slots, uint64_t mask, const int32_t* __restrict__ keys,
-                                    int64_t* __restrict__ out, int64_t n, int erase) {
-  const int64_t i = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
-  if (i >= n) return;
-  const uint4 k = reinterpret_cast<const uint4*>(keys)[i];
-  const uint64_t h = key_hash(k.x, k.y, k.z, k.w);
-  const unsigned long long tag = make_tag(h);
-  uint64_t pos = h & mask;
-  for (uint64_t probe = 0; probe <= mask; ++probe, pos = (pos + 1) & mask) {
-    const Slot* s = slots + pos;
-    const unsigned long long cur = s->tag;
-    if (cur == 0) break;
-    if (cur == tag && s->key[0] == k.x && s->key[1] == k.y && s->key[2] == k.z && s->key[3] == k.w) {
-      out[i] = s->value;
-      if (erase) const_cast<Slot*>(s)->tag = 1ull;
-      return;
-    }
-  }
-  out[i] = -1;
 }
 
 // ------------------------------------------------------------------ K4
@@ -182,28 +98,6 @@ hipError_t launch_range_select(const double* starts, const int64_t* track_off, c
   if (nq <= 0) return hipSuccess;
   hipLaunchKernelGGL(range_select_kernel, dim3(ceil_div(nq, 256)), dim3(256), 0, stream, starts, track_off, q_track,
                      q_begin, q_dur, out_lo, out_hi, nq, ntracks);
-  return hipGetLastError();
-}
-
-hipError_t launch_key_hash(const int32_t* keys, uint64_t* out, int64_t n, hipStream_t stream) {
-  if (n <= 0) return hipSuccess;
-  hipLaunchKernelGGL(key_hash_kernel, dim3(ceil_div(n, 256)), dim3(256), 0, stream, keys, out, n);
-  return hipGetLastError();
-}
-
-hipError_t launch_table_insert(void* slots, uint64_t mask, const int32_t* keys, const int64_t* values, int64_t n,
-                               int32_t* ok, hipStream_t stream) {
-  if (n <= 0) return hipSuccess;
-  hipLaunchKernelGGL(table_insert_kernel, dim3(ceil_div(n, 256)), dim3(256), 0, stream, static_cast<Slot*>(slots),
-                     mask, keys, values, n, ok);
-  return hipGetLastError();
-}
-
-hipError_t launch_table_lookup(const void* slots, uint64_t mask, const int32_t* keys, int64_t* out, int64_t n,
-                               int erase, hipStream_t stream) {
-  if (n <= 0) return hipSuccess;
-  hipLaunchKernelGGL(table_lookup_kernel, dim3(ceil_div(n, 256)), dim3(256), 0, stream,
-                     static_cast<const Slot*>(slots), mask, keys, out, n, erase);
   return hipGetLastError();
 }
 

@@ -16,8 +16,11 @@
 #include <pybind11/stl.h>
 
 #include <algorithm>
+#include <cstdlib>
 #include <cstring>
 #include <vector>
+
+#include "transmux_args.h"
 
 namespace hlsp2p {
 namespace dev {
@@ -66,6 +69,7 @@ class Desc {
   }
   template <typename T>
   T* at(int64_t off) const { return reinterpret_cast<T*>(static_cast<uint8_t*>(dev_.data_ptr()) + off); }
+  Tensor device() const { return dev_; }
 
  private:
   std::vector<uint8_t> buf_;
@@ -113,6 +117,98 @@ int decrypt_cus(int device) { return std::max(8, cus(device) - g_cu_reserve); }
 
 void hip_ok(hipError_t e, const char* what) { TORCH_CHECK(e == hipSuccess, what, " failed: ", hipGetErrorString(e)); }
 
+// Fused path by default; HLSP2P_TRANSMUX=split runs the decrypt / psi / scan / prefix /
+// gather kernel sequence instead (A/B measurements).
+int g_mode = -1;  // 1 fused, 0 split; -1: read HLSP2P_TRANSMUX on first use
+
+bool use_fused() {
+  if (g_mode < 0) {
+    const char* v = std::getenv("HLSP2P_TRANSMUX");
+    g_mode = (v != nullptr && std::strcmp(v, "split") == 0) ? 0 : 1;
+  }
+  return g_mode == 1;
+}
+
+// The fused decrypt + demux batch (transmux_fused.hip): one descriptor H2D, two memsets for
+// the hand-off words and the -1 tables, the persistent fused kernel + the per-segment tail
+// kernel, the info rows and plaintext lengths D2H.  One group covering the whole batch.
+py::tuple transmux_launch_fused(Tensor src, const int64_t* so, const int64_t* nb, const uint8_t* en,
+                                const uint32_t* drk, const uint8_t* iv, int64_t B, Tensor td0, Tensor isb,
+                                int64_t max_pes, int device, hipStream_t st) {
+  const auto dev_opts = torch::TensorOptions().device(torch::kCUDA, device);
+  const int64_t tile_bytes = hlsp2p::dev::transmux_tile_bytes();
+  std::vector<int64_t> v_so(so, so + B), v_nb(nb, nb + B), tile_prefix(B + 1, 0), es_off(B), es_cap(B);
+  std::vector<uint8_t> v_en(en, en + B);
+  int64_t pos = 0;
+  for (int64_t i = 0; i < B; ++i) {
+    tile_prefix[i + 1] = tile_prefix[i] + (nb[i] + tile_bytes - 1) / tile_bytes;
+    es_cap[i] = align_up(std::max<int64_t>(nb[i], 1));
+    es_off[i] = pos;
+    pos += 3 * es_cap[i];  // [video | audio scratch | id3 scratch]
+  }
+  const int64_t tiles = tile_prefix[B];
+  Desc desc;
+  const int64_t d_so = desc.add(v_so), d_nb = desc.add(v_nb), d_en = desc.add(v_en),
+                d_drk = desc.add(drk, B * 44 * 4), d_iv = desc.add(iv, B * 16), d_tp = desc.add(tile_prefix),
+                d_eo = desc.add(es_off), d_ec = desc.add(es_cap);
+  desc.upload(device);
+  Tensor es = torch::empty({pos + kAlign}, dev_opts.dtype(torch::kUInt8));
+  // zeroed words: info [B, 24] | look [tiles, 3] | psi [B, 2] | ticket, timeout (+ pad)
+  const int64_t z_info = 0, z_look = B * kInfo, z_psi = z_look + tiles * 3, z_tk = z_psi + 2 * B;
+  const int64_t z_words = z_tk + 2;
+  Tensor zw = torch::empty({z_words}, dev_opts.dtype(torch::kInt64));
+  hip_ok(hipMemsetAsync(zw.data_ptr(), 0, static_cast<size_t>(z_words * 8), st), "hipMemsetAsync");
+  // -1 words: pes [B, 3, max_pes, 3] | lastpes [tiles, 3, 2]
+  const int64_t m_pes = B * 3 * max_pes * 3, m_words = m_pes + tiles * 6;
+  Tensor mw = torch::empty({std::max<int64_t>(m_words, 1)}, dev_opts.dtype(torch::kInt64));
+  hip_ok(hipMemsetAsync(mw.data_ptr(), 0xff, static_cast<size_t>(std::max<int64_t>(m_words, 1) * 8), st),
+         "hipMemsetAsync");
+  Tensor out_len = torch::empty({std::max<int64_t>(B, 1)}, dev_opts.dtype(torch::kInt64));
+  int64_t* zp = zw.data_ptr<int64_t>();
+  int64_t* mp = mw.data_ptr<int64_t>();
+  hlsp2p::dev::TransmuxArgs a{};
+  a.src = static_cast<const uint8_t*>(src.data_ptr());
+  a.src_off = desc.at<int64_t>(d_so);
+  a.src_len = desc.at<int64_t>(d_nb);
+  a.enc = desc.at<uint8_t>(d_en);
+  a.drk = desc.at<uint32_t>(d_drk);
+  a.ivw = desc.at<uint32_t>(d_iv);
+  a.tdl = static_cast<const uint32_t*>(td0.data_ptr());
+  a.isb = static_cast<const uint8_t*>(isb.data_ptr());
+  a.tile_prefix = desc.at<int64_t>(d_tp);
+  a.es = es.data_ptr<uint8_t>();
+  a.es_off = desc.at<int64_t>(d_eo);
+  a.es_cap = desc.at<int64_t>(d_ec);
+  a.pes = mp;
+  a.info = zp + z_info;
+  a.out_len = out_len.data_ptr<int64_t>();
+  a.look = reinterpret_cast<uint64_t*>(zp + z_look);
+  a.psi = reinterpret_cast<uint64_t*>(zp + z_psi);
+  a.lastpes = mp + m_pes;
+  a.ticket = reinterpret_cast<unsigned int*>(zp + z_tk);
+  a.timeout = reinterpret_cast<unsigned int*>(zp + z_tk) + 1;
+  a.max_pes = max_pes;
+  a.nseg = static_cast<int>(B);
+  a.total_tiles = tiles;
+  hip_ok(hlsp2p::dev::launch_transmux_fused(a, decrypt_cus(device), st), "transmux_fused");
+  Tensor info = zw.narrow(0, z_info, B * kInfo).view({B, kInfo});
+  Tensor pes = mw.narrow(0, 0, m_pes).view({B, 3, max_pes, 3});
+  // host block: info rows | plaintext lengths (one pinned allocation, two D2H on `st`)
+  Tensor host = torch::empty({B * kInfo + B + 1}, torch::TensorOptions().dtype(torch::kInt64).pinned_memory(true));
+  Tensor hinfo = host.narrow(0, 0, B * kInfo).view({B, kInfo});
+  hinfo.copy_(info, /*non_blocking=*/true);
+  Tensor hl = host.narrow(0, B * kInfo, B);
+  hl.copy_(out_len.narrow(0, 0, B), /*non_blocking=*/true);
+  I64 idx(static_cast<py::ssize_t>(B)), eo(static_cast<py::ssize_t>(B));
+  for (int64_t i = 0; i < B; ++i) idx.mutable_data()[i] = i;
+  std::memcpy(eo.mutable_data(), es_off.data(), static_cast<size_t>(B * 8));
+  py::list groups;
+  groups.append(py::make_tuple(idx, info, pes, es, eo, hinfo, py::cast(hl)));
+  // keep-alive: the descriptor block's device copy, the hand-off words (a timeout word != 0
+  // in zw[z_tk] + 4 bytes means a spin gave up: tests read it through `keep`)
+  return py::make_tuple(groups, py::make_tuple(zw, mw, out_len, desc.device()), host);
+}
+
 // src: uint8 device buffer holding every payload at src_off[i] (16-byte aligned) with
 // nbytes[i] bytes; enc[i] != 0 -> AES-128-CBC with round keys drk[i] (44 little-endian
 // words, equivalent inverse cipher) and IV iv[i]; encrypted sizes must be positive
@@ -144,6 +240,8 @@ py::tuple transmux_launch(Tensor src, I64 src_off, I64 nbytes, py::array_t<uint8
   }
   const auto dev_opts = torch::TensorOptions().device(torch::kCUDA, device);
   hipStream_t st = c10::hip::getCurrentHIPStream(device).stream();
+  if (use_fused())
+    return transmux_launch_fused(src, so, nb, en, drk.data(), iv.data(), B, td0, isb, max_pes, device, st);
 
   // ---- plans: AES over the encrypted segments, demux per group
   std::vector<int64_t> a_so, a_do, a_bp{0}, a_cp{0};
@@ -266,6 +364,12 @@ void register_transmux(py::module& m) {
   m.def("set_cu_reserve", [](int n) { g_cu_reserve = std::max(0, n); }, py::arg("n"),
         "CUs the persistent decrypt grid leaves free for concurrent (RCCL) kernels");
   m.def("cu_reserve", [] { return g_cu_reserve; });
+  m.def("transmux_mode", [] { return std::string(use_fused() ? "fused" : "split"); });
+  m.def("set_transmux_mode", [](const std::string& m) {
+    TORCH_CHECK_VALUE(m == "fused" || m == "split", "transmux mode must be 'fused' or 'split'");
+    g_mode = m == "fused" ? 1 : 0;
+  });
+  m.def("transmux_tile_bytes", &hlsp2p::dev::transmux_tile_bytes);
   m.def("transmux_launch", &transmux_launch, py::arg("src"), py::arg("src_off"), py::arg("nbytes"), py::arg("enc"),
         py::arg("drk"), py::arg("iv"), py::arg("td0"), py::arg("isb"), py::arg("max_pes"));
 }

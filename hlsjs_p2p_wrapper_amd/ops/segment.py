@@ -1,9 +1,9 @@
-"""Segment identity, range selection, device index and batched copies.
+"""Segment identity, range selection and batched copies.
 
-* :func:`range_select`  — batched ``MediaMap.getSegmentList`` (K1).
-* :func:`pack_keys` / :func:`key_hash` — 12/16-byte segment keys and their 64-bit hash
-  (K2).  ``pack_keys`` produces exactly ``SegmentView.toArrayBuffer()`` rows.
-* :class:`DeviceSegmentTable` — HBM-resident open-addressing key -> value table (K3).
+* :func:`range_select`  — batched ``MediaMap.getSegmentList`` (K1, HIP kernel on a GPU).
+* :func:`pack_keys` / :func:`wire_keys` / :func:`key_hash_host` — 16-byte segment keys, their
+  12-byte wire form (exactly ``SegmentView.toArrayBuffer()`` rows) and the 64-bit hash the
+  native cache index and want table use (K2, ``runtime/store.hpp`` SegKeyHash).
 * :func:`copy_segments` — batched byte-range gather/scatter between buffers (K4).
 """
 from __future__ import annotations
@@ -55,16 +55,6 @@ def wire_keys(keys: np.ndarray) -> bytes:
     return k.tobytes()
 
 
-def key_hash(keys: torch.Tensor) -> torch.Tensor:
-    """64-bit hashes (as int64) of an ``int32[n,4]`` key tensor."""
-    n = keys.numel() // 4
-    if keys.device.type == "cpu":
-        return torch.from_numpy(key_hash_host(keys.numpy().view(np.uint32)).view(np.int64))
-    out = torch.empty(n, dtype=torch.int64, device=keys.device)
-    _dev().key_hash(keys.contiguous(), out)
-    return out
-
-
 def range_select(starts: Sequence[Sequence[float]], queries: Sequence[Tuple[int, float, float]],
                  device: torch.device) -> Tuple[np.ndarray, np.ndarray]:
     """For each (track, begin, duration) query return [lo, hi) indices of fragments with
@@ -89,46 +79,6 @@ def range_select(starts: Sequence[Sequence[float]], queries: Sequence[Tuple[int,
     hi = torch.empty(len(q), dtype=torch.int64, device=device)
     _dev().range_select(d["s"], d["to"], d["qt"], d["qb"], d["qd"], lo, hi)
     return lo.cpu().numpy(), hi.cpu().numpy()
-
-
-class DeviceSegmentTable:
-    """Open-addressing hash table in HBM: key(int32[4]) -> int64 value."""
-
-    def __init__(self, capacity: int, device: torch.device) -> None:
-        cap = 1
-        while cap < max(2, capacity) * 2:
-            cap <<= 1
-        self.capacity = cap
-        self.device = device
-        self.slots = torch.zeros(cap * 4, dtype=torch.int64, device=device)  # 32-byte slots
-        self._host: dict = {} if device.type == "cpu" else None  # type: ignore[assignment]
-
-    def insert(self, keys: np.ndarray, values: np.ndarray) -> np.ndarray:
-        keys = np.ascontiguousarray(np.asarray(keys, dtype=np.int64).astype(np.uint32).view(np.int32).reshape(-1, 4))
-        vals = np.asarray(values, dtype=np.int64)
-        if self.device.type == "cpu":
-            for k, v in zip(map(tuple, keys.tolist()), vals.tolist()):
-                self._host[k] = v
-            return np.ones(len(vals), dtype=np.int32)
-        d = pack_to_device({"k": keys, "v": vals}, self.device)
-        ok = torch.empty(len(vals), dtype=torch.int32, device=self.device)
-        _dev().table_insert(self.slots, d["k"], d["v"], ok)
-        return ok.cpu().numpy()
-
-    def lookup(self, keys: np.ndarray, erase: bool = False) -> np.ndarray:
-        keys = np.ascontiguousarray(np.asarray(keys, dtype=np.int64).astype(np.uint32).view(np.int32).reshape(-1, 4))
-        if self.device.type == "cpu":
-            out = []
-            for k in map(tuple, keys.tolist()):
-                out.append(self._host.pop(k, -1) if erase else self._host.get(k, -1))
-            return np.asarray(out, dtype=np.int64)
-        d = pack_to_device({"k": keys}, self.device)
-        out = torch.empty(len(keys), dtype=torch.int64, device=self.device)
-        _dev().table_lookup(self.slots, d["k"], out, bool(erase))
-        return out.cpu().numpy()
-
-    def erase(self, keys: np.ndarray) -> np.ndarray:
-        return self.lookup(keys, erase=True)
 
 
 def copy_segments(src: torch.Tensor, dst: torch.Tensor, src_offs: Sequence[int], dst_offs: Sequence[int],

@@ -131,25 +131,13 @@ def test_decrypt_then_demux_on_device(cuda):
     assert tuple(info[9:12]) == tuple(st["n_pes"])
 
 
-def test_range_select_and_keys(cuda):
+def test_range_select(cuda):
     starts = [[10.0 * i for i in range(25, 200)], [4.0 * i for i in range(10)]]
     queries = [(0, 365, 33), (0, 10, 275), (0, 1975, 3000), (0, 240, 2100), (0, 2100, 3000), (1, 0, 8), (5, 0, 1)]
     lo, hi = segment.range_select(starts, queries, cuda)
     clo, chi = segment.range_select(starts, queries, torch.device("cpu"))
     assert lo.tolist() == clo.tolist() and hi.tolist() == chi.tolist()
     assert (lo[0], hi[0]) == (12, 15)
-    keys = segment.pack_keys([0, 1, 2], [1, 1, 0], [25, 26, 27], swarm=3)
-    h = segment.key_hash(torch.from_numpy(keys).to(cuda)).cpu().numpy().view(np.uint64)
-    assert np.array_equal(h, segment.key_hash_host(keys.view(np.uint32)))
-    tab = segment.DeviceSegmentTable(1000, cuda)
-    ks = segment.pack_keys(np.arange(500) % 5, np.arange(500) % 2, np.arange(500), swarm=1)
-    assert tab.insert(ks, np.arange(500) * 7).all()
-    got = tab.lookup(ks)
-    assert got.tolist() == (np.arange(500) * 7).tolist()
-    miss = segment.pack_keys([9], [9], [9], swarm=1)
-    assert tab.lookup(miss).tolist() == [-1]
-    assert tab.erase(ks[:10]).tolist() == (np.arange(10) * 7).tolist()
-    assert tab.lookup(ks[:12]).tolist() == [-1] * 10 + [70, 77]
 
 
 def test_copy_segments(cuda):
