@@ -188,6 +188,10 @@ py::tuple transmux_launch_fused(Tensor src, const int64_t* so, const int64_t* nb
   a.ticket = reinterpret_cast<unsigned int*>(zp + z_tk);
   a.timeout = reinterpret_cast<unsigned int*>(zp + z_tk) + 1;
   a.max_pes = max_pes;
+  {
+    const char* d = std::getenv("HLSP2P_FUSED_DIAG");  // timing decomposition only
+    a.diag = d != nullptr ? std::atoi(d) : 0;
+  }
   a.nseg = static_cast<int>(B);
   a.total_tiles = tiles;
   hip_ok(hlsp2p::dev::launch_transmux_fused(a, decrypt_cus(device), st), "transmux_fused");

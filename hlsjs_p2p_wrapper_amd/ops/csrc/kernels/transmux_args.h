@@ -17,9 +17,9 @@ struct TransmuxArgs {
   const uint32_t* tdl;       // TdL[256]
   const uint8_t* isb;        // InvSbox[256]
   const int64_t* tile_prefix;  // [nseg + 1] tiles per segment, exclusive prefix
-  uint8_t* es;               // ES buffer: per segment [video | audio | id3] + two scratch regions
+  uint8_t* es;               // ES buffer: per segment three class regions (video, audio, id3)
   const int64_t* es_off;     // [nseg] (3 x es_cap bytes from here belong to the segment)
-  const int64_t* es_cap;     // [nseg] region size: audio / id3 scratch at + es_cap / + 2 es_cap
+  const int64_t* es_cap;     // [nseg] region size: audio at + es_cap, id3 at + 2 es_cap
   int64_t* pes;              // [nseg][3][max_pes][3], pre-filled with -1
   int64_t* info;             // [nseg][24], pre-zeroed
   int64_t* out_len;          // [nseg] plaintext length (-1: bad padding)
@@ -29,6 +29,7 @@ struct TransmuxArgs {
   unsigned int* ticket;      // pre-zeroed
   unsigned int* timeout;     // pre-zeroed; nonzero = a hand-off spin gave up
   int64_t max_pes;
+  int diag;                  // diagnostics only: 1 = decrypt alone, 2 = skip the payload copy-out
   int nseg;
   int64_t total_tiles;
 };

@@ -31,13 +31,13 @@
 // (by then tile 0 is long past its decrypt).  Every spin is bounded: a hand-off that never
 // arrives sets the launch's timeout word and the tile proceeds (wrong output, no hang).
 //
-// ES layout per segment at es_off[seg], three regions of es_cap[seg] bytes: video bytes go
-// straight to their final place; audio and id3 bytes to scratch regions at + es_cap and
-// + 2 es_cap (their final place after the video needs the segment's video total, known
-// only once its last tile is done);
-// transmux_tail_kernel moves them and finishes the info rows.  The output contract (ES
-// [video | audio | id3], PES tables, info rows) is the split pipeline's and the host
-// oracle's (runtime/ts.cpp).
+// ES layout per segment at es_off[seg]: three regions of es_cap[seg] bytes, video / audio /
+// id3, each class written at its running offset in its own region (packing the classes back
+// to back would need the segment's video total before the first audio byte is written, i.e.
+// another pass); the info row says where each class starts (slots 22, 23).  PES tables and
+// info rows are the split pipeline's and the host oracle's (runtime/ts.cpp);
+// transmux_tail_kernel finishes what only the whole segment knows (first / last PTS, a
+// failed padding check).
 #include "common.h"
 #include "transmux_args.h"
 
@@ -62,7 +62,8 @@ constexpr int kInfoF = 24;
 constexpr int kScanWaves = (kTilePkts + 63) / 64;  // 6 waves hold one packet per lane
 // info slots / status bits (runtime/ts.hpp, ts_demux.hip)
 constexpr int kStatusF = 0, kPmtPidF = 1, kVideoPidF = 2, kNumPacketsF = 5, kBytes0F = 6, kPes0F = 9,
-              kVideoTypeF = 12, kAudioTypeF = 13, kPayloadBytesF = 14, kFirstPtsF = 16, kLastPtsF = 19;
+              kVideoTypeF = 12, kAudioTypeF = 13, kPayloadBytesF = 14, kFirstPtsF = 16, kLastPtsF = 19,
+              kAudioEsOffsetF = 22, kId3EsOffsetF = 23;
 constexpr uint32_t kBadSyncF = 1, kNoPatF = 2, kNoPmtF = 4, kPesOverflowF = 8, kPesHeaderErrorF = 16,
                    kBadLengthF = 32;
 constexpr uint64_t kAgg = 1ull << 62, kIncl = 2ull << 62;
@@ -260,6 +261,7 @@ __global__ __launch_bounds__(kFThreads, 1) void transmux_fused_kernel(TransmuxAr
       }
     }
     __syncthreads();
+    if (a.diag == 1) continue;  // diagnostics: the decrypt alone
 
     // valid packets of this tile: all of them unless it holds the segment's end
     const int64_t plen = s_len;  // -2: not the last tile; -1: bad padding; else the plaintext length
@@ -555,9 +557,9 @@ __global__ __launch_bounds__(kFThreads, 1) void transmux_fused_kernel(TransmuxAr
     // Five packets per wave iteration: a 12-lane group moves one payload (<= 184 B = 46
     // dwords): lane `sub` funnels body dwords 4sub..4sub+3 out of 5 LDS dwords (v_alignbyte)
     // and writes them with ONE dwordx4 buffer store to a dword-aligned address; byte stores
-    // for the <= 3 + 3 unaligned head / tail bytes.  Video goes to its final place, audio
-    // and id3 to the segment's scratch regions (one buffer resource per segment covers all).
-    {
+    // for the <= 3 + 3 unaligned head / tail bytes.  Each class goes to its own region (one
+    // buffer resource per segment covers all three).
+    if (a.diag != 2) {
       typedef unsigned int v4u __attribute__((ext_vector_type(4)));
       uint8_t* ebase = a.es + a.es_off[seg];
       const int64_t cap = a.es_cap[seg];
@@ -571,7 +573,7 @@ __global__ __launch_bounds__(kFThreads, 1) void transmux_fused_kernel(TransmuxAr
         const int jc = m & 3, jps = (m >> 2) & 0xff;
         const int jlen = (jc < 3) ? static_cast<int>((m >> 10) & 0xff) : 0;
         if (jlen == 0) continue;
-        const int64_t dst64 = jc * cap + s_dst[j];  // class region: video final, audio / id3 scratch
+        const int64_t dst64 = jc * cap + s_dst[j];  // the class's region
         const int jdst = static_cast<int>(dst64);
         const int s = j * kPktF + jps;  // LDS byte offset of the payload
         uint8_t* d = ebase + dst64;
@@ -618,16 +620,17 @@ __global__ __launch_bounds__(kFThreads, 1) void transmux_fused_kernel(TransmuxAr
       }
       inf[kPayloadBytesF] = total_b;
       inf[kNumPacketsF] = n / kPktF;
+      inf[kAudioEsOffsetF] = a.es_cap[seg];  // per-class regions (no compaction pass)
+      inf[kId3EsOffsetF] = 2 * a.es_cap[seg];
       status |= static_cast<uint32_t>(over);
       if (status) atomicOr(reinterpret_cast<unsigned long long*>(inf + kStatusF), static_cast<unsigned long long>(status));
     }
   }
 }
 
-// One workgroup per segment, after the fused kernel: audio + id3 from the scratch half to
-// their place after the video bytes, first / last PTS per class, and a segment whose
-// padding failed reports no media (its tiles could not know before they wrote).
-__global__ __launch_bounds__(256) void transmux_tail_kernel(TransmuxArgs a) {
+// One wave per segment, after the fused kernel: first / last PTS per class, and a segment
+// whose padding failed reports no media (its tiles could not know before they wrote).
+__global__ __launch_bounds__(64) void transmux_tail_kernel(TransmuxArgs a) {
   const int seg = blockIdx.x;
   const int tid = threadIdx.x;
   int64_t* inf = a.info + static_cast<int64_t>(seg) * kInfoF;
@@ -650,16 +653,12 @@ __global__ __launch_bounds__(256) void transmux_tail_kernel(TransmuxArgs a) {
       inf[kAudioTypeF] = 0;
       inf[kPayloadBytesF] = 0;
       inf[kNumPacketsF] = 0;
+      inf[kAudioEsOffsetF] = 0;
+      inf[kId3EsOffsetF] = 0;
       inf[kStatusF] = kNoPatF | (plen < 0 || plen % kPktF ? kBadLengthF : 0);
     }
     return;
   }
-  const int64_t vb = inf[kBytes0F], ab = inf[kBytes0F + 1], ib = inf[kBytes0F + 2];
-  uint8_t* ebase = a.es + a.es_off[seg];
-  const int64_t cap = a.es_cap[seg];
-  // audio and id3 from their scratch regions to their place after the video bytes
-  for (int64_t i = tid; i < ab; i += 256) ebase[vb + i] = ebase[cap + i];
-  for (int64_t i = tid; i < ib; i += 256) ebase[vb + ab + i] = ebase[2 * cap + i];
   if (tid < 3) {
     const int k = tid;
     const int64_t np = inf[kPes0F + k];
@@ -688,7 +687,7 @@ hipError_t launch_transmux_fused(const TransmuxArgs& args, int num_cu, hipStream
     const hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
   }
-  hipLaunchKernelGGL(transmux_tail_kernel, dim3(static_cast<unsigned>(args.nseg)), dim3(256), 0, stream, args);
+  hipLaunchKernelGGL(transmux_tail_kernel, dim3(static_cast<unsigned>(args.nseg)), dim3(64), 0, stream, args);
   return hipGetLastError();
 }
 

@@ -30,7 +30,8 @@ constexpr int kInfo = 24;
 constexpr int kPsiScan = 64;
 // info slots / status bits (must match runtime/ts.hpp)
 constexpr int kStatus = 0, kPmtPid = 1, kVideoPid = 2, kNumPackets = 5, kBytes0 = 6, kPes0 = 9, kVideoType = 12,
-              kAudioType = 13, kPayloadBytes = 14, kFirstPts = 16, kLastPts = 19;
+              kAudioType = 13, kPayloadBytes = 14, kFirstPts = 16, kLastPts = 19, kAudioEsOffset = 22,
+              kId3EsOffset = 23;
 constexpr int64_t kBadSync = 1, kNoPat = 2, kNoPmt = 4, kPesOverflow = 8, kPesHeaderError = 16, kBadLength = 32;
 
 __device__ __forceinline__ int64_t read_pts(const uint8_t* p) {
@@ -269,6 +270,8 @@ __global__ __launch_bounds__(64) void ts_prefix_kernel(const int64_t* __restrict
       if (carry[2 * k + 1] > max_pes) over = kPesOverflow;
     }
     inf[kPayloadBytes] = static_cast<int64_t>(carry[0]) + carry[2] + carry[4];
+    inf[kAudioEsOffset] = carry[0];  // [video | audio | id3] packed
+    inf[kId3EsOffset] = static_cast<int64_t>(carry[0]) + carry[2];
     if (over) atomicOr(reinterpret_cast<unsigned long long*>(inf + kStatus), static_cast<unsigned long long>(over));
   }
 }

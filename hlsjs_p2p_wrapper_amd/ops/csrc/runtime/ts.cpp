@@ -417,6 +417,8 @@ void demux_segment(const uint8_t* data, int64_t n, uint8_t* es_out, int64_t* pes
     if (npes[k] > 0) info[kLastPts + k] = last_pts[k];
   }
   info[kPayloadBytes] = bytes[0] + bytes[1] + bytes[2];
+  info[kAudioEsOffset] = bytes[0];
+  info[kId3EsOffset] = bytes[0] + bytes[1];
   info[kStatus] = status;
 }
 

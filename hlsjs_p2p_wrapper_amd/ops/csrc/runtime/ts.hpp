@@ -34,6 +34,9 @@ enum Info : int {
   kPayloadBytes = 14,  // total ES bytes (video+audio+id3)
   kFirstPts = 16,      // kFirstPts + class: PTS of the class's first PES (-1 if none)
   kLastPts = 19,       // kLastPts + class: PTS of the class's last PES
+  kAudioEsOffset = 22,  // byte offset of the audio ES from the segment's ES start (video at 0)
+  kId3EsOffset = 23,    // byte offset of the id3 ES (the host and the split kernels pack
+                        // [video | audio | id3]; the fused kernel uses fixed per-class regions)
 };
 // status bits
 enum Status : int64_t {

@@ -2,7 +2,9 @@
 
 Output per segment (identical for the gfx950 kernels and the host oracle):
 
-* ES bytes ``[video | audio | id3]`` at ``es_offs[i]`` of the ES buffer;
+* ES bytes per class at ``es_offs[i]`` of the ES buffer: video at 0, audio and id3 at the
+  offsets the info row gives (``audio_es_offset`` / ``id3_es_offset``: packed back to back by
+  the host oracle and the split kernels, fixed per-class regions in the fused kernel);
 * ``pes[i, class, k] = (es_offset, pts, dts)`` for the k-th PES of each class;
 * ``info[i]`` = status bits, PIDs, packet count, per-class byte and PES counts
   (slot names in :data:`INFO`).
@@ -29,7 +31,8 @@ INFO = {"status": 0, "pmt_pid": 1, "video_pid": 2, "audio_pid": 3, "id3_pid": 4,
         "video_bytes": 6, "audio_bytes": 7, "id3_bytes": 8, "n_video_pes": 9, "n_audio_pes": 10,
         "n_id3_pes": 11, "video_type": 12, "audio_type": 13, "payload_bytes": 14,
         "video_first_pts": 16, "audio_first_pts": 17, "id3_first_pts": 18,
-        "video_last_pts": 19, "audio_last_pts": 20, "id3_last_pts": 21}
+        "video_last_pts": 19, "audio_last_pts": 20, "id3_last_pts": 21,
+        "audio_es_offset": 22, "id3_es_offset": 23}
 INFO_WORDS = 24
 STATUS = {"bad_sync": 1, "no_pat": 2, "no_pmt": 4, "pes_overflow": 8, "pes_header_error": 16, "bad_length": 32}
 DEFAULT_MAX_PES = 512
@@ -49,7 +52,7 @@ class DemuxResult:
         out = {k: int(info[v]) for k, v in INFO.items()}
         base = int(self.es_offs[i])
         sizes = [out["video_bytes"], out["audio_bytes"], out["id3_bytes"]]
-        starts = [base, base + sizes[0], base + sizes[0] + sizes[1]]
+        starts = [base, base + out["audio_es_offset"], base + out["id3_es_offset"]]
         counts = [out["n_video_pes"], out["n_audio_pes"], out["n_id3_pes"]]
         for c, name in enumerate(CLASSES):
             out[name] = {"es": self.es[starts[c]:starts[c] + sizes[c]],

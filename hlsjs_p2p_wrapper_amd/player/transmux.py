@@ -394,10 +394,10 @@ class MediaPipeline:
             es = res.es
             for k, i in enumerate(idx):
                 row = rows[k]
-                # ES views (video | audio | id3 at es_offs[k]) are built on first access: the
+                # ES views (per class, at the row's offsets from es_offs[k]) are built on first access: the
                 # buffer path only needs their byte counts, which the info row holds
                 r = _Result(status=row[0], info=InfoRow(row), plain_bytes=int(plain_lens[k]), demux=res, index=k)
-                r._es = (es, es_offs[k], row[_VB], row[_AB], row[_IB])
+                r._es = (es, es_offs[k], row[_VB], row[_AB], row[_IB], row[_AO], row[_IO])
                 if plain_lens[k] < 0:
                     r["error"] = ValueError("decryption failed (bad PKCS#7 padding)")
                 results[i] = r
@@ -406,6 +406,7 @@ class MediaPipeline:
 
 
 _VB, _AB, _IB = _ts.INFO["video_bytes"], _ts.INFO["audio_bytes"], _ts.INFO["id3_bytes"]
+_AO, _IO = _ts.INFO["audio_es_offset"], _ts.INFO["id3_es_offset"]
 
 
 class _Result(dict):
@@ -418,10 +419,10 @@ class _Result(dict):
     def __missing__(self, key):
         if key not in ("video", "audio", "id3"):
             raise KeyError(key)
-        es, base, vb, ab, ib = self._es
+        es, base, vb, ab, ib, ao, io = self._es
         v = es.narrow(0, base, vb)
-        a = es.narrow(0, base + vb, ab)
-        i = es.narrow(0, base + vb + ab, ib)
+        a = es.narrow(0, base + ao, ab)
+        i = es.narrow(0, base + io, ib)
         self["video"], self["audio"], self["id3"] = v, a, i
         return self[key]
 

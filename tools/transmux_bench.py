@@ -1,0 +1,70 @@
+"""Isolated timing of one transmux batch (decrypt + demux) on the MI355X: the fused kernel
+(kernels/transmux_fused.hip) against the split sequence (aes_cbc.hip + ts_demux.hip), plus
+the fused kernel's decomposition (HLSP2P_FUSED_DIAG=1: decrypt alone; =2: no payload
+copy-out).  Batches of 1080p 6 Mb/s AES-128 segments (~3 MB), as a bench round delivers them.
+
+    PYTHONPATH=. python tools/transmux_bench.py [--segs 256] [--iters 10]
+"""
+import argparse
+import json
+import os
+
+import numpy as np
+import torch
+
+from hlsjs_p2p_wrapper_amd.net.origin import PRESET_1080P_6M, SyntheticHlsOrigin
+from hlsjs_p2p_wrapper_amd.ops import aes, tsdemux
+from hlsjs_p2p_wrapper_amd.ops._native import device
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--segs", type=int, default=256)
+    ap.add_argument("--iters", type=int, default=10)
+    args = ap.parse_args()
+    cuda = torch.device("cuda", 0)
+    dev = device()
+    pool_n = min(args.segs, 64)
+    origin = SyntheticHlsOrigin("http://cdn.tb/", renditions=PRESET_1080P_6M, num_segments=pool_n, encrypted=True,
+                                pool_size=pool_n, pin_memory=True, seed=5, register=False)
+    pool = origin.pools[0]
+    src = pool.data.to(cuda)
+    offs = np.array([pool.offsets[i % pool_n] for i in range(args.segs)], dtype=np.int64)
+    lens = np.array([pool.lengths[i % pool_n] for i in range(args.segs)], dtype=np.int64)
+    enc = np.ones(args.segs, dtype=np.uint8)
+    drk = np.tile(aes.round_keys_le(origin.key), (args.segs, 1)).astype(np.uint32)
+    iv = np.tile(np.frombuffer(origin.iv, dtype=np.uint8), (args.segs, 1))
+    td0, isb = aes.device_tables(cuda)
+    total = int(lens.sum())
+    out = {"segs": args.segs, "bytes": total}
+
+    def launch():
+        return dev.transmux_launch(src, offs, lens, enc, drk, iv, td0, isb, tsdemux.DEFAULT_MAX_PES)
+
+    for name, mode, diag in (("split", "split", None), ("fused", "fused", None), ("fused_decrypt_only", "fused", "1"),
+                             ("fused_no_copyout", "fused", "2")):
+        dev.set_transmux_mode(mode)
+        if diag is None:
+            os.environ.pop("HLSP2P_FUSED_DIAG", None)
+        else:
+            os.environ["HLSP2P_FUSED_DIAG"] = diag
+        keep = [launch() for _ in range(2)]
+        torch.cuda.synchronize()
+        a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        a.record()
+        for _ in range(args.iters):
+            keep.append(launch())
+        b.record()
+        torch.cuda.synchronize()
+        us = a.elapsed_time(b) * 1e3 / args.iters
+        out[f"{name}_us"] = round(us, 1)
+        out[f"{name}_us_per_seg"] = round(us / args.segs, 3)
+        out[f"{name}_GBps"] = round(total / (us * 1e-6) / 1e9, 1)
+        del keep
+    os.environ.pop("HLSP2P_FUSED_DIAG", None)
+    dev.set_transmux_mode("fused")
+    print(json.dumps(out))
+
+
+if __name__ == "__main__":
+    main()
