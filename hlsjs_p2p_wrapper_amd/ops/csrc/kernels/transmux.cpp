@@ -117,17 +117,20 @@ int decrypt_cus(int device) { return std::max(8, cus(device) - g_cu_reserve); }
 
 void hip_ok(hipError_t e, const char* what) { TORCH_CHECK(e == hipSuccess, what, " failed: ", hipGetErrorString(e)); }
 
-// Fused path by default; HLSP2P_TRANSMUX=split runs the decrypt / psi / scan / prefix /
-// gather kernel sequence instead (A/B measurements).
+// Split kernel sequence by default (decrypt / psi / scan / prefix / gather: measured faster on
+// MI355X, profiles/r3_transmux_fused_vs_split.md); HLSP2P_TRANSMUX=fused runs the
+// wave-specialised fused kernel (transmux_fused.hip) instead.
 int g_mode = -1;  // 1 fused, 0 split; -1: read HLSP2P_TRANSMUX on first use
 
 bool use_fused() {
   if (g_mode < 0) {
     const char* v = std::getenv("HLSP2P_TRANSMUX");
-    g_mode = (v != nullptr && std::strcmp(v, "split") == 0) ? 0 : 1;
+    g_mode = (v != nullptr && std::strcmp(v, "fused") == 0) ? 1 : 0;
   }
   return g_mode == 1;
 }
+
+constexpr int64_t kProfSlots = 512 * 16;  // >= grid x 16 role timers
 
 // The fused decrypt + demux batch (transmux_fused.hip): one descriptor H2D, two memsets for
 // the hand-off words and the -1 tables, the persistent fused kernel + the per-segment tail
@@ -147,15 +150,24 @@ py::tuple transmux_launch_fused(Tensor src, const int64_t* so, const int64_t* nb
     pos += 3 * es_cap[i];  // [video | audio scratch | id3 scratch]
   }
   const int64_t tiles = tile_prefix[B];
+  std::vector<uint32_t> drk_rot(drk, drk + B * 44);  // rounds 1..9 rotated left by 24
+  for (int64_t i = 0; i < B; ++i)
+    for (int k = 4; k < 40; ++k) {
+      const uint32_t v = drk_rot[i * 44 + k];
+      drk_rot[i * 44 + k] = (v << 24) | (v >> 8);
+    }
   Desc desc;
-  const int64_t d_so = desc.add(v_so), d_nb = desc.add(v_nb), d_en = desc.add(v_en),
+  const int64_t d_so = desc.add(v_so), d_nb = desc.add(v_nb), d_en = desc.add(v_en), d_drr = desc.add(drk_rot),
                 d_drk = desc.add(drk, B * 44 * 4), d_iv = desc.add(iv, B * 16), d_tp = desc.add(tile_prefix),
                 d_eo = desc.add(es_off), d_ec = desc.add(es_cap);
   desc.upload(device);
   Tensor es = torch::empty({pos + kAlign}, dev_opts.dtype(torch::kUInt8));
   // zeroed words: info [B, 24] | look [tiles, 3] | psi [B, 2] | ticket, timeout (+ pad)
   const int64_t z_info = 0, z_look = B * kInfo, z_psi = z_look + tiles * 3, z_tk = z_psi + 2 * B;
-  const int64_t z_words = z_tk + 2;
+  // HLSP2P_FUSED_PROF=1: per-workgroup role timers after the hand-off words (diagnostics)
+  const char* prof_env = std::getenv("HLSP2P_FUSED_PROF");
+  const bool prof = prof_env != nullptr && std::atoi(prof_env) != 0;
+  const int64_t z_prof = z_tk + 2, z_words = z_prof + (prof ? kProfSlots : 0);
   Tensor zw = torch::empty({z_words}, dev_opts.dtype(torch::kInt64));
   hip_ok(hipMemsetAsync(zw.data_ptr(), 0, static_cast<size_t>(z_words * 8), st), "hipMemsetAsync");
   // -1 words: pes [B, 3, max_pes, 3] | lastpes [tiles, 3, 2]
@@ -172,6 +184,7 @@ py::tuple transmux_launch_fused(Tensor src, const int64_t* so, const int64_t* nb
   a.src_len = desc.at<int64_t>(d_nb);
   a.enc = desc.at<uint8_t>(d_en);
   a.drk = desc.at<uint32_t>(d_drk);
+  a.drk_rot = desc.at<uint32_t>(d_drr);
   a.ivw = desc.at<uint32_t>(d_iv);
   a.tdl = static_cast<const uint32_t*>(td0.data_ptr());
   a.isb = static_cast<const uint8_t*>(isb.data_ptr());
@@ -187,10 +200,13 @@ py::tuple transmux_launch_fused(Tensor src, const int64_t* so, const int64_t* nb
   a.lastpes = mp + m_pes;
   a.ticket = reinterpret_cast<unsigned int*>(zp + z_tk);
   a.timeout = reinterpret_cast<unsigned int*>(zp + z_tk) + 1;
+  a.prof = prof ? reinterpret_cast<uint64_t*>(zp + z_prof) : nullptr;
   a.max_pes = max_pes;
   {
     const char* d = std::getenv("HLSP2P_FUSED_DIAG");  // timing decomposition only
     a.diag = d != nullptr ? std::atoi(d) : 0;
+    const char* f = std::getenv("HLSP2P_FUSED_FLAGS");  // A/B experiments only
+    a.flags = f != nullptr ? std::atoi(f) : 0;
   }
   a.nseg = static_cast<int>(B);
   a.total_tiles = tiles;

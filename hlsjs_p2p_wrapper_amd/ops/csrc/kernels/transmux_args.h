@@ -13,6 +13,7 @@ struct TransmuxArgs {
   const int64_t* src_len;    // [nseg] source bytes (encrypted: a positive multiple of 16)
   const uint8_t* enc;        // [nseg] 1 = AES-128-CBC
   const uint32_t* drk;       // [nseg][44] little-endian equivalent-inverse-cipher round keys
+  const uint32_t* drk_rot;   // [nseg][44] the same, rounds 1..9 rotated left by 24 (the fused rounds' form)
   const uint32_t* ivw;       // [nseg][4]
   const uint32_t* tdl;       // TdL[256]
   const uint8_t* isb;        // InvSbox[256]
@@ -28,8 +29,10 @@ struct TransmuxArgs {
   int64_t* lastpes;          // [tiles][3][2] (last PES index in the tile, its PTS), pre-filled with -1
   unsigned int* ticket;      // pre-zeroed
   unsigned int* timeout;     // pre-zeroed; nonzero = a hand-off spin gave up
+  uint64_t* prof;            // diagnostics only: [grid][16] per-role cycle counters, or null
   int64_t max_pes;
   int diag;                  // diagnostics only: 1 = decrypt alone, 2 = skip the payload copy-out
+  int flags;                 // experiments only: bit 0 = no s_setprio for the latency-bound roles
   int nseg;
   int64_t total_tiles;
 };

@@ -21,6 +21,8 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--segs", type=int, default=256)
     ap.add_argument("--iters", type=int, default=10)
+    ap.add_argument("--prof", action="store_true", help="also print the fused kernel's per-role timers")
+    ap.add_argument("--flags", default="0", help="HLSP2P_FUSED_FLAGS for the fused runs (A/B experiments)")
     args = ap.parse_args()
     cuda = torch.device("cuda", 0)
     dev = device()
@@ -37,6 +39,8 @@ def main():
     td0, isb = aes.device_tables(cuda)
     total = int(lens.sum())
     out = {"segs": args.segs, "bytes": total}
+
+    os.environ["HLSP2P_FUSED_FLAGS"] = args.flags
 
     def launch():
         return dev.transmux_launch(src, offs, lens, enc, drk, iv, td0, isb, tsdemux.DEFAULT_MAX_PES)
@@ -57,13 +61,29 @@ def main():
         b.record()
         torch.cuda.synchronize()
         us = a.elapsed_time(b) * 1e3 / args.iters
+        if mode == "fused":  # launches whose hand-off spins gave up (transmux.cpp: zw[z_tk] + 4 bytes)
+            out[f"{name}_timeouts"] = sum(int(k[1][0][-2]) >> 32 != 0 for k in keep)
         out[f"{name}_us"] = round(us, 1)
         out[f"{name}_us_per_seg"] = round(us / args.segs, 3)
         out[f"{name}_GBps"] = round(total / (us * 1e-6) / 1e9, 1)
         del keep
     os.environ.pop("HLSP2P_FUSED_DIAG", None)
-    dev.set_transmux_mode("fused")
+    dev.set_transmux_mode("split")
     print(json.dumps(out))
+    if args.prof:  # HLSP2P_FUSED_PROF=1: [grid][16] shader-clock sums after the hand-off words
+        os.environ["HLSP2P_FUSED_PROF"] = "1"
+        launch()
+        groups, keep, _ = launch()
+        torch.cuda.synchronize()
+        os.environ.pop("HLSP2P_FUSED_PROF", None)
+        p = keep[0][-512 * 16:].view(512, 16).cpu().numpy().astype(np.float64)
+        live = p[:, 7] > 0
+        names = ["c_job", "c_plain", "c_parse", "c_lookback", "c_plan", "", "", "c_tiles",
+                 "d_next", "d_stage", "d_decrypt", "d_tiles", "s_ring", "s_stage", "x_wait", "x_copy"]
+        per_tile = {n: round(float(p[live, k].sum() / max(p[live, 7].sum(), 1)), 1) for k, n in enumerate(names)
+                    if n and not n.endswith("tiles")}
+        print(json.dumps({"workgroups": int(live.sum()), "tiles": int(p[live, 7].sum()),
+                          "cycles_per_tile": per_tile}))
 
 
 if __name__ == "__main__":
