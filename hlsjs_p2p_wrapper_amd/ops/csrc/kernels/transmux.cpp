@@ -21,6 +21,7 @@
 #include <vector>
 
 #include "transmux_args.h"
+#include "ts_onepass.h"
 
 namespace hlsp2p {
 namespace dev {
@@ -76,21 +77,39 @@ class Desc {
   Tensor dev_;
 };
 
+// The demux after a decrypt: the psi / scan / prefix / gather sequence (the default, classes
+// packed) or, with HLSP2P_DEMUX=onepass, ts_onepass_kernel (scan + prefix + gather in one
+// kernel with a decoupled look-back, ES classes in three regions per segment; measured
+// slower, profiles/r3_transmux_fused_vs_split.md).
+int g_onepass = -1;
+
+bool use_onepass() {
+  if (g_onepass < 0) {
+    const char* v = std::getenv("HLSP2P_DEMUX");
+    g_onepass = (v != nullptr && std::strcmp(v, "onepass") == 0) ? 1 : 0;
+  }
+  return g_onepass == 1;
+}
+
 struct DemuxPlan {
-  std::vector<int64_t> idx, off, len, cap, es_off, blk_prefix;
+  std::vector<int64_t> idx, off, len, cap, es_off, es_cap, blk_prefix;
   int64_t es_bytes = 0, total_blocks = 0;
-  int64_t d_off = -1, d_len = -1, d_bp = -1, d_eo = -1;
+  int64_t d_off = -1, d_len = -1, d_bp = -1, d_eo = -1, d_ec = -1;
 };
 
 void plan_demux(DemuxPlan& p) {
   const size_t B = p.idx.size();
+  const int64_t regions = use_onepass() ? 3 : 1;  // one-pass: video | audio | id3 regions
   p.es_off.resize(B);
+  p.es_cap.resize(B);
   p.blk_prefix.assign(B + 1, 0);
   int64_t pos = 0;
   for (size_t i = 0; i < B; ++i) {
     p.es_off[i] = pos;
-    pos += align_up(p.cap[i]);
-    const int64_t blocks = ((p.cap[i] + kPacket - 1) / kPacket + 255) / 256;
+    p.es_cap[i] = align_up(std::max<int64_t>(p.cap[i], 1));
+    pos += regions * p.es_cap[i];
+    const int64_t bp = use_onepass() ? hlsp2p::dev::onepass_block_packets() : 256;
+    const int64_t blocks = ((p.cap[i] + kPacket - 1) / kPacket + bp - 1) / bp;
     p.blk_prefix[i + 1] = p.blk_prefix[i] + blocks;
   }
   p.es_bytes = pos + kAlign;
@@ -307,12 +326,14 @@ py::tuple transmux_launch(Tensor src, I64 src_off, I64 nbytes, py::array_t<uint8
     pe.d_off = desc.add(pe.off);
     pe.d_bp = desc.add(pe.blk_prefix);
     pe.d_eo = desc.add(pe.es_off);
+    pe.d_ec = desc.add(pe.es_cap);
   }
   if (nc) {
     pc.d_off = desc.add(pc.off);
     pc.d_len = desc.add(pc.len);
     pc.d_bp = desc.add(pc.blk_prefix);
     pc.d_eo = desc.add(pc.es_off);
+    pc.d_ec = desc.add(pc.es_cap);
   }
   desc.upload(device);
 
@@ -331,7 +352,7 @@ py::tuple transmux_launch(Tensor src, I64 src_off, I64 nbytes, py::array_t<uint8
            "aes128_cbc_decrypt");
   }
 
-  py::list groups;
+  py::list groups, keep;  // keep: scratch the kernels use until the batch completes
   int64_t row0 = 0;
   for (int g = 0; g < 2; ++g) {
     DemuxPlan& p = g == 0 ? pe : pc;
@@ -342,18 +363,45 @@ py::tuple transmux_launch(Tensor src, I64 src_off, I64 nbytes, py::array_t<uint8
     const int64_t* lens = g == 0 ? out_len.data_ptr<int64_t>() : desc.at<int64_t>(p.d_len);
     const int64_t nb_blocks = std::max<int64_t>(1, p.total_blocks);
     Tensor es = torch::empty({p.es_bytes}, dev_opts.dtype(torch::kUInt8));
-    Tensor meta = torch::empty({nb_blocks * 256}, dev_opts.dtype(torch::kInt32));
-    Tensor pts = torch::empty({nb_blocks * 256 * 2}, dev_opts.dtype(torch::kInt64));
-    Tensor aux = torch::empty({nb_blocks * 12 + n * 7}, dev_opts.dtype(torch::kInt32));
     Tensor info = torch::empty({n, kInfo}, dev_opts.dtype(torch::kInt64));
     Tensor pes = torch::empty({n, 3, max_pes, 3}, dev_opts.dtype(torch::kInt64));
-    hip_ok(hlsp2p::dev::launch_ts_demux(buf, desc.at<int64_t>(p.d_off), lens, desc.at<int64_t>(p.d_bp),
-                                        static_cast<int>(n), p.total_blocks,
-                                        reinterpret_cast<uint32_t*>(meta.data_ptr<int32_t>()),
-                                        pts.data_ptr<int64_t>(), aux.data_ptr<int32_t>(), es.data_ptr<uint8_t>(),
-                                        desc.at<int64_t>(p.d_eo), pes.data_ptr<int64_t>(), max_pes,
-                                        info.data_ptr<int64_t>(), st),
-           "ts_demux");
+    if (use_onepass()) {
+      // zeroed: look-back granules [blocks x 3] | ticket + timeout; -1: last PES per block [blocks x 6]
+      Tensor zw = torch::empty({nb_blocks * 3 + 1}, dev_opts.dtype(torch::kInt64));
+      hip_ok(hipMemsetAsync(zw.data_ptr(), 0, static_cast<size_t>((nb_blocks * 3 + 1) * 8), st), "hipMemsetAsync");
+      Tensor lastpes = torch::empty({nb_blocks * 6}, dev_opts.dtype(torch::kInt64));
+      hip_ok(hipMemsetAsync(lastpes.data_ptr(), 0xff, static_cast<size_t>(nb_blocks * 6 * 8), st), "hipMemsetAsync");
+      hlsp2p::dev::OnepassArgs oa{};
+      oa.buf = buf;
+      oa.seg_off = desc.at<int64_t>(p.d_off);
+      oa.seg_len = lens;
+      oa.blk_prefix = desc.at<int64_t>(p.d_bp);
+      oa.nseg = static_cast<int>(n);
+      oa.total_blocks = p.total_blocks;
+      oa.es = es.data_ptr<uint8_t>();
+      oa.es_off = desc.at<int64_t>(p.d_eo);
+      oa.es_cap = desc.at<int64_t>(p.d_ec);
+      oa.pes = pes.data_ptr<int64_t>();
+      oa.max_pes = max_pes;
+      oa.info = info.data_ptr<int64_t>();
+      oa.look = reinterpret_cast<uint64_t*>(zw.data_ptr<int64_t>());
+      oa.lastpes = lastpes.data_ptr<int64_t>();
+      oa.ticket = reinterpret_cast<unsigned int*>(zw.data_ptr<int64_t>() + nb_blocks * 3);
+      hip_ok(hlsp2p::dev::launch_ts_onepass(oa, st), "ts_onepass");
+      keep.append(py::make_tuple(zw, lastpes));
+    } else {
+      Tensor meta = torch::empty({nb_blocks * 256}, dev_opts.dtype(torch::kInt32));
+      Tensor pts = torch::empty({nb_blocks * 256 * 2}, dev_opts.dtype(torch::kInt64));
+      Tensor aux = torch::empty({nb_blocks * 12 + n * 7}, dev_opts.dtype(torch::kInt32));
+      hip_ok(hlsp2p::dev::launch_ts_demux(buf, desc.at<int64_t>(p.d_off), lens, desc.at<int64_t>(p.d_bp),
+                                          static_cast<int>(n), p.total_blocks,
+                                          reinterpret_cast<uint32_t*>(meta.data_ptr<int32_t>()),
+                                          pts.data_ptr<int64_t>(), aux.data_ptr<int32_t>(), es.data_ptr<uint8_t>(),
+                                          desc.at<int64_t>(p.d_eo), pes.data_ptr<int64_t>(), max_pes,
+                                          info.data_ptr<int64_t>(), st),
+             "ts_demux");
+      keep.append(py::make_tuple(meta, pts, aux));
+    }
     // D2H through torch's copy so the caching host allocator records the use of the pinned
     // block on `st` (it is not handed out again before the copy has run, even if the batch
     // is dropped uncompleted)
@@ -375,7 +423,9 @@ py::tuple transmux_launch(Tensor src, I64 src_off, I64 nbytes, py::array_t<uint8
     groups.append(py::make_tuple(idx, info, pes, es, eo, hinfo, hlens));
     row0 += n;
   }
-  return py::make_tuple(groups, dec.defined() ? py::cast(dec) : py::none(), host);
+  keep.append(dec.defined() ? py::cast(dec) : py::none());
+  keep.append(desc.device());
+  return py::make_tuple(groups, keep, host);
 }
 
 }  // namespace
@@ -388,6 +438,11 @@ void register_transmux(py::module& m) {
   m.def("set_transmux_mode", [](const std::string& m) {
     TORCH_CHECK_VALUE(m == "fused" || m == "split", "transmux mode must be 'fused' or 'split'");
     g_mode = m == "fused" ? 1 : 0;
+  });
+  m.def("demux_mode", [] { return std::string(use_onepass() ? "onepass" : "fourpass"); });
+  m.def("set_demux_mode", [](const std::string& m) {
+    TORCH_CHECK_VALUE(m == "onepass" || m == "fourpass", "demux mode must be 'onepass' or 'fourpass'");
+    g_onepass = m == "onepass" ? 1 : 0;
   });
   m.def("transmux_tile_bytes", &hlsp2p::dev::transmux_tile_bytes);
   m.def("transmux_launch", &transmux_launch, py::arg("src"), py::arg("src_off"), py::arg("nbytes"), py::arg("enc"),

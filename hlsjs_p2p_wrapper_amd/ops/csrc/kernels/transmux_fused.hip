@@ -64,6 +64,7 @@
 // each class starts (slots 22, 23).  PES tables and info rows are the split pipeline's and
 // the host oracle's (runtime/ts.cpp).
 #include "common.h"
+#include "demux_dev.h"
 #include "transmux_args.h"
 
 namespace hlsp2p {
@@ -137,10 +138,12 @@ struct CopyPlan {
 // T-table address of byte k of w in the Td0 (td0_base) or Td2 (td2_base) half-row
 #define TDA(w, base, k) __builtin_amdgcn_perm((w), (base), SELF(k))
 
-__device__ __forceinline__ int64_t pts5(uint32_t b0, uint32_t b1, uint32_t b2, uint32_t b3, uint32_t b4) {
-  return (int64_t((b0 >> 1) & 0x07) << 30) | (int64_t(b1) << 22) | (int64_t(b2 >> 1) << 15) | (int64_t(b3) << 7) |
-         int64_t(b4 >> 1);
-}
+using demux::dpp_scan;
+using demux::dpp_sum;
+using demux::gload;
+using demux::gstore;
+using demux::parse_pkt;
+using demux::Pkt;
 
 __device__ __forceinline__ int64_t pkcs7_len_f(uint4 p, int64_t nbytes) {
   const uint32_t pad = p.w >> 24;
@@ -161,31 +164,6 @@ __device__ __forceinline__ int64_t uniform64f(int64_t v) {
   return static_cast<int64_t>((static_cast<uint64_t>(hi) << 32) | lo);
 }
 __device__ __forceinline__ int uniform32f(int v) { return __builtin_amdgcn_readfirstlane(v); }
-
-// Wave64 inclusive prefix sum on the DPP paths (row shifts, then the row broadcasts): VALU
-// only — a __shfl_up scan is ds_bpermute traffic that would queue behind the AES reads.
-__device__ __forceinline__ uint32_t dpp_scan(uint32_t v) {
-  int x = static_cast<int>(v);
-  x += __builtin_amdgcn_update_dpp(0, x, 0x111, 0xf, 0xf, false);  // row_shr:1
-  x += __builtin_amdgcn_update_dpp(0, x, 0x112, 0xf, 0xf, false);  // row_shr:2
-  x += __builtin_amdgcn_update_dpp(0, x, 0x114, 0xf, 0xf, false);  // row_shr:4
-  x += __builtin_amdgcn_update_dpp(0, x, 0x118, 0xf, 0xf, false);  // row_shr:8
-  x += __builtin_amdgcn_update_dpp(0, x, 0x142, 0xa, 0xf, false);  // row_bcast:15 -> rows 1, 3
-  x += __builtin_amdgcn_update_dpp(0, x, 0x143, 0xc, 0xf, false);  // row_bcast:31 -> rows 2, 3
-  return static_cast<uint32_t>(x);
-}
-__device__ __forceinline__ uint32_t dpp_sum(uint32_t v) {
-  return static_cast<uint32_t>(__builtin_amdgcn_readlane(static_cast<int>(dpp_scan(v)), 63));
-}
-
-// agent-scope 8-byte granules (stores and loads bypass the non-coherent L1; the value is
-// its own ready flag)
-__device__ __forceinline__ void gstore(uint64_t* p, uint64_t v) {
-  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-__device__ __forceinline__ uint64_t gload(uint64_t* p) {
-  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
 
 // Intra-workgroup hand-off on a monotonic LDS counter.  signal / publish: the wave's LDS
 // writes land first (lgkmcnt(0) only: a workgroup-scope release fence would also wait for
@@ -294,52 +272,6 @@ __device__ Psi psi_scan(const uint8_t* s, int scan) {
       q += 5 + eil;
     }
   }
-  return r;
-}
-
-// One TS packet's header as the oracle reads it, from the packet's first dword and the 20
-// bytes at its payload start `s` (h: five funnel-aligned dwords).
-struct Pkt {
-  int c, ps, len, pesf;
-  int64_t pts, dts;
-  uint32_t err;
-};
-__device__ __forceinline__ Pkt parse_pkt(bool valid, uint32_t w0, const uint32_t* h, int s, int p0, int p1, int p2) {
-  Pkt r{3, 0, 0, 0, -1, -1, 0};
-  if (!valid) return r;
-  if ((w0 & 0xff) != 0x47) {
-    r.err = kBadSyncF;
-    return r;
-  }
-  const int b1 = (w0 >> 8) & 0xff, b2 = (w0 >> 16) & 0xff, b3 = w0 >> 24;
-  const int pid = ((b1 & 0x1f) << 8) | b2;
-  const int cls = (p0 >= 0 && pid == p0) ? 0 : (p1 >= 0 && pid == p1) ? 1 : (p2 >= 0 && pid == p2) ? 2 : 3;
-  const int afc = (b3 >> 4) & 3;
-  if (cls == 3 || !(afc & 1)) return r;
-  if (s > kPktF) {
-    r.err = kBadLengthF;
-    return r;
-  }
-  int l = kPktF - s;
-  if (b1 & 0x40) {
-    const uint32_t h0 = h[0], h1 = h[1], h2 = h[2], h3 = h[3], h4 = h[4];
-    const uint32_t h7 = h1 >> 24, h8 = h2 & 0xff;
-    if (l < 9 || (h0 & 0xffffff) != 0x010000 || 9 + static_cast<int>(h8) > l) {
-      r.err = kPesHeaderErrorF;
-      return r;
-    }
-    r.pts = ((h7 & 0x80) && l >= 14) ? pts5((h2 >> 8) & 0xff, (h2 >> 16) & 0xff, h2 >> 24, h3 & 0xff, (h3 >> 8) & 0xff)
-                                     : -1;
-    r.dts = ((h7 & 0xC0) == 0xC0 && l >= 19)
-                ? pts5((h3 >> 16) & 0xff, h3 >> 24, h4 & 0xff, (h4 >> 8) & 0xff, (h4 >> 16) & 0xff)
-                : -1;
-    r.pesf = 1;
-    s += 9 + static_cast<int>(h8);
-    l -= 9 + static_cast<int>(h8);
-  }
-  r.c = cls;
-  r.ps = s;
-  r.len = l;
   return r;
 }
 

@@ -36,11 +36,12 @@ def _segments():
     return out
 
 
-def _launch(mode, jobs, max_pes, bad=None):
+def _launch(mode, jobs, max_pes, bad=None, demux="fourpass"):
     from hlsjs_p2p_wrapper_amd.ops._native import device
 
     dev = device()
     dev.set_transmux_mode(mode)
+    dev.set_demux_mode(demux)
     cuda = torch.device("cuda", 0)
     offs, pos = [], 0
     for _, p, _, _ in jobs:
@@ -73,6 +74,7 @@ def _launch(mode, jobs, max_pes, bad=None):
             res[i] = {"info": row, "pes": pes[k].cpu().numpy(), "es": np.concatenate(esb),
                       "plain": int(np.asarray(hlens)[k] if not isinstance(hlens, torch.Tensor) else hlens[k])}
     dev.set_transmux_mode("split")
+    dev.set_demux_mode("fourpass")
     return res, keep
 
 
@@ -109,6 +111,24 @@ def test_fused_matches_oracle_and_split(cuda, max_pes):
         _same(fused[i], split[i], max_pes)
     if max_pes == 7:  # the 3 MB segment overflows a 7-entry PES table: flagged, counts exact
         assert fused[0]["info"][0] & tsdemux.STATUS["pes_overflow"] and fused[0]["info"][9] > 7
+
+
+@pytest.mark.parametrize("max_pes", [512, 7])
+def test_split_demux_modes_match_oracle(cuda, max_pes):
+    """The split sequence's demux after the decrypt: the four-kernel sequence (the default) and
+    the one-pass kernel (scan + prefix + gather in one, decoupled look-back) agree with the
+    host oracle byte for byte."""
+    jobs = _segments()
+    onepass, keep = _launch("split", jobs, max_pes, demux="onepass")
+    fourpass, _ = _launch("split", jobs, max_pes)
+    for i, (seg, _, _, _) in enumerate(jobs):
+        ref = _oracle(seg, max_pes)
+        assert onepass[i]["plain"] == len(seg) == fourpass[i]["plain"], i
+        _same(onepass[i], ref, max_pes)
+        _same(fourpass[i], ref, max_pes)
+        assert fourpass[i]["info"][22] == fourpass[i]["info"][6]  # packed classes
+        if onepass[i]["info"][5] > 0:  # class regions
+            assert onepass[i]["info"][23] == 2 * onepass[i]["info"][22] > 0
 
 
 def test_fused_wrong_key_reports_no_media(cuda):

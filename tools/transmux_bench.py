@@ -45,9 +45,10 @@ def main():
     def launch():
         return dev.transmux_launch(src, offs, lens, enc, drk, iv, td0, isb, tsdemux.DEFAULT_MAX_PES)
 
-    for name, mode, diag in (("split", "split", None), ("fused", "fused", None), ("fused_decrypt_only", "fused", "1"),
-                             ("fused_no_copyout", "fused", "2")):
-        dev.set_transmux_mode(mode)
+    for name, mode, diag in (("split", "split", None), ("split_onepass", "split1", None), ("fused", "fused", None),
+                             ("fused_decrypt_only", "fused", "1"), ("fused_no_copyout", "fused", "2")):
+        dev.set_transmux_mode("split" if mode == "split1" else mode)
+        dev.set_demux_mode("onepass" if mode == "split1" else "fourpass")
         if diag is None:
             os.environ.pop("HLSP2P_FUSED_DIAG", None)
         else:
@@ -69,6 +70,7 @@ def main():
         del keep
     os.environ.pop("HLSP2P_FUSED_DIAG", None)
     dev.set_transmux_mode("split")
+    dev.set_demux_mode("fourpass")
     print(json.dumps(out))
     if args.prof:  # HLSP2P_FUSED_PROF=1: [grid][16] shader-clock sums after the hand-off words
         os.environ["HLSP2P_FUSED_PROF"] = "1"
