@@ -15,7 +15,8 @@ Parity: ``lib/integration/mapping/media-map.js:4-88`` (component C9, SURVEY §A.
 Hot-path note (K1 in SURVEY §2.2): the reference does a linear scan per query.  HLS
 fragment lists are sorted by ``start``, so the closed interval maps to one contiguous
 index range; we cache a start-time array per ``details`` object and answer with two
-binary searches (falling back to the literal scan if the list is ever unsorted).  Batched
+binary searches (falling back to the literal scan if the list is ever unsorted); the cache
+is dropped on any fragment-start rewrite (``player.level.fragment_generation``).  Batched
 multi-track queries go to the HIP range-select kernel (:mod:`..ops.range_select`).
 """
 from __future__ import annotations
@@ -30,15 +31,37 @@ from .track_view import TrackView
 log = logging.getLogger("hlsjs_p2p_wrapper_amd.media_map")
 
 
+def _generation() -> int:
+    """The engine's fragment-start mutation counter (player.level), 0 for engines without one."""
+    try:
+        from ..player.level import fragment_generation
+    except ImportError:  # pragma: no cover - the bundled engine always has it
+        return 0
+    return fragment_generation()
+
+
 class _StartIndex:
-    __slots__ = ("frags_id", "n", "starts", "sorted")
+    """Start times of one fragment list, valid while the list object, its length, the
+    fragment-start generation and its end points are unchanged."""
+    __slots__ = ("frags_id", "n", "gen", "first", "last", "starts", "sorted")
 
     def __init__(self, fragments: List[Any]) -> None:
         self.frags_id = id(fragments)
         self.n = len(fragments)
+        self.gen = _generation()
         self.starts = [f.start for f in fragments]
         s = self.starts
+        self.first = fragments[0] if fragments else None
+        self.last = fragments[-1] if fragments else None
         self.sorted = all(s[i] <= s[i + 1] for i in range(len(s) - 1))
+
+    def valid_for(self, fragments: List[Any]) -> bool:
+        # list identity and length catch replaced / grown playlists; the generation catches
+        # in-place start rewrites (PTS realignment); the end points catch objects swapped in
+        # without a start assignment
+        n = len(fragments)
+        return (self.frags_id == id(fragments) and self.n == n and self.gen == _generation()
+                and (n == 0 or (fragments[0] is self.first and fragments[-1] is self.last)))
 
 
 class MediaMap:
@@ -74,7 +97,7 @@ class MediaMap:
         fragments = details.fragments
         end = beginTime + duration
         idx = self._idx.get(trackView.level)
-        if idx is None or idx.frags_id != id(fragments) or idx.n != len(fragments):
+        if idx is None or not idx.valid_for(fragments):
             idx = _StartIndex(fragments)
             self._idx[trackView.level] = idx
         if idx.sorted:

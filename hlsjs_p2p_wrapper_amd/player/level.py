@@ -23,6 +23,17 @@ class DecryptData:
         return self.method == "AES-128" and self.uri is not None and self.key is None
 
 
+# Bumped whenever any Fragment's ``start`` is assigned (construction included): consumers
+# that cache derived start-time arrays (models.media_map) compare generations instead of
+# trusting list identity — hls.js rewrites ``frag.start`` in place on PTS realignment.
+_START_GENERATION = [0]
+
+
+def fragment_generation() -> int:
+    """Counter of ``Fragment.start`` assignments in this process."""
+    return _START_GENERATION[0]
+
+
 @dataclass(eq=False)
 class Fragment:
     url: str
@@ -41,6 +52,11 @@ class Fragment:
     loader: Any = None
     title: str = ""
     programDateTime: Any = None
+
+    def __setattr__(self, name: str, value: Any) -> None:
+        object.__setattr__(self, name, value)
+        if name == "start":
+            _START_GENERATION[0] += 1
 
     @property
     def end(self) -> float:

@@ -102,3 +102,30 @@ def test_batched_segment_lists_on_device(cuda):
     qs = [(tv, b + 7 * i, d) for i in range(12) for b, d in _QUERIES]
     assert len(qs) >= MediaMap.DEVICE_BATCH_MIN
     assert mm.getSegmentLists(qs, device=cuda) == [mm.getSegmentList(tv, b, d) for _, b, d in qs]
+
+
+def test_start_index_cache_follows_fragment_mutations():
+    """The start-time cache must not outlive the playlist it was built from: an in-place
+    ``frag.start`` rewrite (hls.js PTS realignment), a fragment object swapped in without a
+    start assignment, and a re-sorted list each answer from the new starts."""
+    from types import SimpleNamespace
+
+    from hlsjs_p2p_wrapper_amd.player.level import Fragment, LevelDetails
+
+    frags = [Fragment(url=f"s{i}.ts", sn=i, start=10.0 * i, duration=10.0) for i in range(10)]
+    level = SimpleNamespace(url=["l0.m3u8"], details=LevelDetails(url="l0.m3u8", fragments=frags))
+    mm = MediaMap(SimpleNamespace(levels=[level]))
+    tv = TrackView(level=0, urlId=0)
+    assert [s.sn for s in mm.getSegmentList(tv, 30, 20)] == [3, 4, 5]
+    for f in frags:  # realignment shifts every start by +5 s in place (same list, same length)
+        f.start += 5.0
+    assert [s.sn for s in mm.getSegmentList(tv, 30, 20)] == [3, 4]      # starts 35, 45
+    assert [s.time for s in mm.getSegmentList(tv, 30, 20)] == [35.0, 45.0]
+    # a fragment object replaced without touching `start` on the list's own objects
+    swapped = Fragment(url="x.ts", sn=99, start=1000.0, duration=10.0)
+    object.__setattr__(swapped, "start", 1000.0)
+    frags[-1] = swapped
+    assert [s.sn for s in mm.getSegmentList(tv, 990, 20)] == [99]
+    # a list re-sorted in place after a start rewrite falls back to / rebuilds the index
+    frags[0].start = 500.0
+    assert 0 in [s.sn for s in mm.getSegmentList(tv, 495, 10)]
