@@ -1,13 +1,15 @@
-# Round validation on one MI355X: GPU tests, smoke, kernel bench, headline bench, host-cost probe.
-set -e
+# Round validation on one MI355X (what the driver runs, plus the two probes):
+#   GPU tests, smoke(), the headline bench, the host-cost probe and the HBM-origin probe.
+#   bash tools/gpu_validate.sh            -> gpurun_out/validate/*.log
+set -eo pipefail
 R=$GRAFT_REPO_ROOT
 cd $R
 export PYTHONPATH=$R
-mkdir -p gpurun_out/val
-timeout -k 10 600 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread > gpurun_out/val/gpu_tests.log 2>&1
-timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/val/smoke.log 2>&1
-for i in 1 2; do
-  timeout -k 10 200 python tools/kernel_bench.py > gpurun_out/val/kb_$i.json 2> gpurun_out/val/kb_$i.err
-done
-timeout -k 10 300 python bench.py --verbose > gpurun_out/val/bench_1080p.log 2>&1
-timeout -k 10 300 python bench.py --config hostcost --steps 30 --warmup 6 --verbose > gpurun_out/val/hostcost.log 2>&1
+O=gpurun_out/validate
+mkdir -p $O
+timeout -k 10 600 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread > $O/gpu_tests.log 2>&1
+timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.log 2>&1
+timeout -k 10 300 python bench.py --verbose > $O/headline.log 2>&1
+timeout -k 10 300 python bench.py --config hostcost --steps 60 --warmup 6 --verbose > $O/hostcost.log 2>&1
+timeout -k 10 300 python bench.py --ingest hbm --steps 60 --warmup 6 --verbose > $O/hbm.log 2>&1
+grep -h '^{' $O/headline.log $O/hostcost.log $O/hbm.log

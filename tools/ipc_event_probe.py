@@ -2,19 +2,20 @@
 (parallel/comm.py:_IpcOutbox, HLSP2P_IPC_EVENTS=1): `hipStreamWaitEvent` on a peer's
 interprocess event returned `invalid argument` after a few hundred rounds of a 4-rank soak.
 
-Two ranks on ONE MI355X (torchrun --nproc-per-node 2, gloo): rank 0 records its
-interprocess event once per round after a small kernel (as a rank does after packing its
-outbox), rank 1 waits on it once per round on its own stream, with the protocol's
-host barriers around.  Counts the rounds until the first failure.
+N ranks on ONE MI355X (torchrun --nproc-per-node N, gloo), the outbox protocol stripped to
+its event traffic: each round a rank runs a small kernel and records its interprocess event
+(only on rounds where it "has sends", --send-prob), host barrier, then its stream waits on
+the event of every peer that recorded this round, runs a kernel, host barrier.  Prints the
+first failing round per rank with the record / wait counts at that point.
 
-  --mode wait      : rank 1 waits every round on the event opened once (the protocol)
-  --mode reopen    : rank 1 re-opens the handle every --every rounds
-  --mode nowait    : rank 1 never waits (does recording alone fail?)
-  --mode query     : rank 1 only queries the event (hipEventQuery) every round
-  --waits N        : stream waits per round (a 4-rank round waits on 3 peers)
+  --mode wait      : the protocol (events opened once)
+  --mode reopen    : re-open the peers' handles every --every rounds
+  --mode query     : hipEventQuery on the peers' events instead of stream waits
+  --mode sync      : hipEventSynchronize (host) on the peers' events instead of stream waits
 """
 import argparse
 import os
+import random
 import sys
 import time
 
@@ -24,58 +25,68 @@ import torch.distributed as dist
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--mode", default="wait", choices=["wait", "reopen", "nowait", "query"])
-    ap.add_argument("--rounds", type=int, default=3000)
+    ap.add_argument("--mode", default="wait", choices=["wait", "reopen", "query", "sync"])
+    ap.add_argument("--rounds", type=int, default=2000)
     ap.add_argument("--every", type=int, default=100)
-    ap.add_argument("--waits", type=int, default=1)
+    ap.add_argument("--send-prob", type=float, default=1.0, help="probability a rank records in a round")
     args = ap.parse_args()
-    rank = int(os.environ["RANK"])
+    rank, world = int(os.environ["RANK"]), int(os.environ["WORLD_SIZE"])
     dist.init_process_group("gloo")
     dev = torch.device("cuda", 0)
     torch.cuda.set_device(dev)
     s = torch.cuda.Stream()
     x = torch.zeros(1 << 16, device=dev)
-    if rank == 0:
-        ev = torch.cuda.Event(interprocess=True)
-        ev.record(s)
-        torch.cuda.synchronize()
-        h = [ev.ipc_handle()]
-    else:
-        h = [None]
-    dist.broadcast_object_list(h, src=0)
-    if rank == 1:
-        ev = torch.cuda.Event.from_ipc_handle(dev, h[0])
+    ev = torch.cuda.Event(interprocess=True)
+    ev.record(s)
+    torch.cuda.synchronize()
+    handles = [None] * world
+    dist.all_gather_object(handles, ev.ipc_handle())
+
+    def open_peers():
+        return [None if r == rank else torch.cuda.Event.from_ipc_handle(dev, h) for r, h in enumerate(handles)]
+
+    peers = open_peers()
+    rng = random.Random(1234)  # identical on every rank: everyone knows who recorded
+    records = waits = 0
+    failed, err = -1, ""
     t0 = time.perf_counter()
-    failed = -1
-    err = ""
     for r in range(args.rounds):
-        if rank == 0:
+        rec = [rng.random() < args.send_prob for _ in range(world)]
+        if failed < 0 and rec[rank]:
             with torch.cuda.stream(s):
                 x.add_(1.0)
             ev.record(s)
+            records += 1
         dist.barrier()
-        if rank == 1 and failed < 0:
+        if failed < 0:
             try:
                 if args.mode == "reopen" and r and r % args.every == 0:
-                    ev = torch.cuda.Event.from_ipc_handle(dev, h[0])
-                if args.mode in ("wait", "reopen"):
-                    for _ in range(args.waits):
-                        s.wait_event(ev)
-                    with torch.cuda.stream(s):
-                        x.add_(1.0)
-                elif args.mode == "query":
-                    ev.query()
+                    peers = open_peers()
+                for src in range(world):
+                    if src == rank or not rec[src]:
+                        continue
+                    if args.mode in ("wait", "reopen"):
+                        s.wait_event(peers[src])
+                    elif args.mode == "query":
+                        peers[src].query()
+                    else:
+                        peers[src].synchronize()
+                    waits += 1
+                with torch.cuda.stream(s):
+                    x.add_(1.0)
             except Exception as e:  # noqa: BLE001 - the failure being probed
                 failed, err = r, f"{type(e).__name__}: {str(e).splitlines()[0]}"
-        if r % 100 == 0:
+        if r % 50 == 0:
             torch.cuda.synchronize()
         dist.barrier()
     torch.cuda.synchronize()
-    out = [None, None]
-    dist.all_gather_object(out, (failed, err))
+    out = [None] * world
+    dist.all_gather_object(out, (failed, records, waits, err))
     if rank == 0:
-        print(f"mode={args.mode} waits/round={args.waits} rounds={args.rounds} every={args.every} "
-              f"first failure round={out[1][0]} ({out[1][1]}) in {time.perf_counter() - t0:.1f} s", flush=True)
+        print(f"mode={args.mode} world={world} rounds={args.rounds} send_prob={args.send_prob} every={args.every} "
+              f"({time.perf_counter() - t0:.1f} s)", flush=True)
+        for k, (f, rc, w, e) in enumerate(out):
+            print(f"  rank {k}: first failure round {f} records {rc} waits {w} {e}", flush=True)
     dist.barrier()
     dist.destroy_process_group()
 
