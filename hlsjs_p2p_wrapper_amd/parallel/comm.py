@@ -434,18 +434,28 @@ class _IpcOutbox:
        rank (two-sided, ordered, as RCCL point-to-point) on the node stream.  An event
        recorded after the copies serves step 1.
 
-    ``HLSP2P_IPC_EVENTS=1`` replaces the host wait of step 3 with an interprocess event per
-    rank, recorded after packing.  Peers' node streams wait on it before copying, so the host
-    never waits, as with an RCCL group.  A peer's event is re-recorded only in its next
+    Interprocess events recorded after packing replace the host wait of step 3 (the default;
+    ``HLSP2P_IPC_EVENTS=0`` restores the wait: the event mode measured +15 % on the 4-rank
+    soak).  Peers' node streams wait on them before copying, so the host
+    never waits, as with an RCCL group.  A peer's event is re-recorded only in a later
     exchange, after the all-gather of step 2, which this rank joins only once its copies
-    (and the wait before them) have run.  The mode is opt-in.  On this ROCm build,
-    ``hipStreamWaitEvent`` on an IPC event starts failing with ``invalid argument`` after a
-    few hundred rounds (`profiles/r2_ipc_rehearsal/soak`), while 20-step runs pass.
+    (and the wait before them) have run.
+
+    Event lifetime (root cause of the round-2 soak failure, ``tools/ipc_event_probe.py``,
+    ``profiles/r3_ipc_events``): on ROCm 7.2 an interprocess event survives exactly 32
+    records — the peer's ``hipStreamWaitEvent`` after the 33rd fails with ``invalid
+    argument``, whatever the rank count, record density or handle re-opening.  So each rank
+    cycles a ring of ``EVENT_RING`` events (exchange ``x`` uses slot ``x % EVENT_RING``) and
+    the whole set is re-created and re-shared (a collective at the same exchange number on
+    every rank) before any event reaches ``EVENT_RECORDS`` records; the previous set stays
+    alive for one generation, as waits queued on the streams may still reference it.
 
     Enabled with ``HLSP2P_DATA_PLANE=ipc`` on a gloo group (``bench.py --dist-backend
     ipc``).  Every rank must be on the same host; otherwise every rank keeps gloo."""
 
     ALIGN = 256
+    EVENT_RING = 8       # interprocess events per rank, used round-robin
+    EVENT_RECORDS = 30   # records per event before the set is renewed (the runtime allows 32)
 
     def __init__(self, comm: "DistComm") -> None:
         self.comm = comm
@@ -453,8 +463,10 @@ class _IpcOutbox:
         self.buf: Optional[torch.Tensor] = None
         self.peers: List[torch.Tensor] = []
         self._pending = None
-        self._ev = None  # this rank's interprocess event: recorded after packing
-        self._peer_ev: Optional[List[Any]] = None  # every rank's event (None: host-side waits)
+        self._ev: Optional[List[Any]] = None  # this rank's event ring: recorded after packing
+        self._peer_ev: Optional[List[List[Any]]] = None  # every rank's ring (None: host-side waits)
+        self._ev_prev = None  # the previous generation, alive until the next renewal
+        self._ev_gen_start = 0
         self.exchanges = 0
 
     @classmethod
@@ -510,36 +522,44 @@ class _IpcOutbox:
             self.peers, self.buf = [], None
             return False
         self.cap = cap
-        if os.environ.get("HLSP2P_IPC_EVENTS", "0") == "1":
+        if os.environ.get("HLSP2P_IPC_EVENTS", "1") == "1":  # default since the event-ring fix (+15 %)
             self._share_events()
         return True
 
     def _share_events(self) -> None:
-        """Collective: export an interprocess event per rank (optional: on any failure every
-        rank packs with a host-side wait instead)."""
+        """Collective: export a fresh ring of interprocess events per rank (optional: on any
+        failure every rank packs with a host-side wait instead).  Called once at set-up and
+        again every ``EVENT_RING * EVENT_RECORDS`` exchanges (see the class notes)."""
         comm = self.comm
         dist, g, me = comm.dist, comm.control_group, comm.rank
         dev = torch.cuda.current_device()
+        self._ev_prev = (self._ev, self._peer_ev)
         handle = None
+        own: Optional[List[Any]] = None
         try:
-            self._ev = torch.cuda.Event(enable_timing=False, interprocess=True)
-            self._ev.record()
+            own = [torch.cuda.Event(enable_timing=False, interprocess=True) for _ in range(self.EVENT_RING)]
+            for e in own:
+                e.record()
             torch.cuda.synchronize()
-            handle = self._ev.ipc_handle()
+            handle = [e.ipc_handle() for e in own]
         except Exception:  # noqa: BLE001 - reported to every rank below
             handle = None
         handles: List[object] = [None] * comm.world_size
         dist.all_gather_object(handles, handle, group=g)
-        evs: Optional[List[Any]] = None
+        evs: Optional[List[List[Any]]] = None
         if all(h is not None for h in handles):
             try:
-                evs = [self._ev if r == me else torch.cuda.Event.from_ipc_handle(dev, h)
+                evs = [own if r == me else [torch.cuda.Event.from_ipc_handle(dev, x) for x in h]  # type: ignore[union-attr]
                        for r, h in enumerate(handles)]
             except Exception:  # noqa: BLE001
                 evs = None
         flags: List[object] = [None] * comm.world_size
         dist.all_gather_object(flags, evs is not None, group=g)
-        self._peer_ev = evs if all(flags) else None
+        if all(flags):
+            self._ev, self._peer_ev = own, evs
+        else:
+            self._ev, self._peer_ev = None, None
+        self._ev_gen_start = self.exchanges
 
     def exchange(self, sends, recvs) -> None:
         comm = self.comm
@@ -562,13 +582,16 @@ class _IpcOutbox:
             raise RuntimeError(f"IPC outbox of {self.cap} bytes cannot hold a round of {need} bytes "
                                "(raise HLSP2P_IPC_OUTBOX_BYTES)")
         stream = torch.cuda.current_stream()
+        if self._peer_ev is not None and self.exchanges - self._ev_gen_start >= self.EVENT_RING * self.EVENT_RECORDS:
+            self._share_events()  # collective at the same exchange number on every rank
+        slot = self.exchanges % self.EVENT_RING
         if sends:
             buf = self.buf
             for (_, t), o, n in zip(sends, offs, sizes):
                 if n:
                     buf[o:o + n].copy_(_as_bytes(t), non_blocking=True)
             if self._peer_ev is not None:
-                self._ev.record(stream)
+                self._ev[slot].record(stream)  # type: ignore[index]
             else:
                 stream.synchronize()
         comm.barrier()  # every outbox's packing is enqueued (or done) and its event recorded
@@ -581,7 +604,7 @@ class _IpcOutbox:
             if lst is None:
                 lst = mine[src] = _outbox_slots(parts[src], me, A)
                 if peer_ev is not None and lst:
-                    stream.wait_event(peer_ev[src])  # src's packing has run
+                    stream.wait_event(peer_ev[src][slot])  # src's packing has run
             i = cursor.get(src, 0)
             if i >= len(lst):
                 raise RuntimeError(f"rank {me}: no matching send from {src}")
