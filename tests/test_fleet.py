@@ -157,3 +157,77 @@ def test_bench_fleet_on_the_gpu():
     res = json.loads([ln for ln in p.stdout.splitlines() if ln.startswith("{")][-1])
     assert res["errors"] == 0 and res["value"] > 0
     assert res["config"]["players_per_gpu"] == 2 and res["config"]["device"] == "MI355X"
+
+
+@pytest.mark.gpu
+def test_fleet_player_reads_fragment_bytes_on_the_gpu(cuda):
+    """A fleet player that asked for payloads (``gpuSwarm.fleetPayload``) reads each served
+    fragment's bytes from ``onSuccess`` — copied from the rank's HBM arena into the shared
+    payload ring — and they match the origin's bytes (CRC-32), the reference ``onSuccess``
+    contract (``lib/integration/p2p-loader-generator.js:92-99``)."""
+    import zlib
+
+    clear_origins()
+    set_current_node(None)
+    loop = new_event_loop("real")
+    spec = dict(ORIGIN, encrypted=False, base_url="http://fleet.payload/live/")
+    origin = SyntheticHlsOrigin(**spec, pin_memory=True)
+    node = node_for_config({"gpuSwarm": {"backend": "local", "device": "cuda", "cacheBytes": 256 << 20,
+                                         "autoTick": False}})
+    a, b = mp.Pipe()
+    player = RemoteNode(b, payload=True)
+    pipe = pipeline_for(cuda, loop)
+    pipe.auto_flush = False
+    server = FleetServer(node, pipe, [a])
+    try:
+        got, errs = {}, []
+
+        class Cb:
+            def __init__(self, sn):
+                self.sn = sn
+
+            def onProgress(self, ev):  # noqa: N802
+                pass
+
+            def onSuccess(self, seg):  # noqa: N802
+                got[self.sn] = seg
+
+            def onError(self, err):  # noqa: N802
+                errs.append((self.sn, err.status))
+
+        sns = list(range(3, 15))
+        for sn in sns:
+            player.request((7, 0, 0, sn), spec["base_url"] + origin.segment_path(0, sn), None, Cb(sn))
+        player.flush()
+        hs, tb = collections.deque(), None
+        end = time.monotonic() + 60
+        while len(got) + len(errs) < len(sns):
+            assert time.monotonic() < end, f"fleet did not deliver: {len(got)} / {len(sns)}"
+            while loop._ready:
+                loop.run_once(block=False)
+            server.poll()
+            server.admit(16)
+            hs.append(node.launch_round())
+            if len(hs) > 1:
+                node.complete_round(hs.popleft())
+            nb = server.launch_transmux()
+            server.complete_transmux(tb)
+            tb = nb
+            server.send()
+            player.poll(0.002)
+        assert not errs
+        for sn in sns:
+            seg = got[sn]
+            assert isinstance(seg, RemoteSegment)
+            data = seg.data()
+            assert data is not None and data.dtype == np.uint8 and len(data) == seg.numel()
+            pool_data, off, n, crc = origin.resource(origin.segment_path(0, sn))
+            assert n == seg.numel()
+            assert zlib.crc32(data.tobytes()) == crc == zlib.crc32(pool_data[off:off + n].numpy().tobytes())
+            assert seg.transmux_result["plain_bytes"] == n  # clear segment: demuxed on the GPU
+    finally:
+        player.close()
+        server.close()
+        node.close()
+        set_current_node(None)
+        clear_origins()
