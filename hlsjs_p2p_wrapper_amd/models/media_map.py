@@ -16,8 +16,10 @@ Hot-path note (K1 in SURVEY §2.2): the reference does a linear scan per query. 
 fragment lists are sorted by ``start``, so the closed interval maps to one contiguous
 index range; we cache a start-time array per ``details`` object and answer with two
 binary searches (falling back to the literal scan if the list is ever unsorted); the cache
-is dropped on any fragment-start rewrite (``player.level.fragment_generation``).  Batched
-multi-track queries go to the HIP range-select kernel (:mod:`..ops.range_select`).
+is dropped on any fragment-start rewrite (``player.level.fragment_generation``).
+Batched multi-track queries (``getSegmentLists``) share that index.  The answer is always
+consumed on the host (the agent's prefetch planning), so a device range-select launch plus
+its D2H sync would cost more than the bisects; round 3 removed that kernel.
 """
 from __future__ import annotations
 
@@ -113,47 +115,11 @@ class MediaMap:
         return out
 
     # ------------------------------------------------------------------ batched (K1)
-    DEVICE_BATCH_MIN = 64  # below this many queries two host bisects beat a kernel launch
-
-    def getSegmentLists(self, queries: List[Any], device: Any = None) -> List[List[SegmentView]]:
-        """Batched ``getSegmentList`` over ``[(trackView, beginTime, duration), ...]`` —
-        one HIP range-select launch (``ops.segment.range_select``, K1) for all queries
-        when ``device`` is a GPU and the batch is large, host bisects otherwise.  Same
-        semantics per query as :meth:`getSegmentList` (closed interval, playlist order;
-        unparsed level -> ``[]``, missing level -> raises)."""
-        import torch
-
-        dev = torch.device(device) if device is not None else torch.device("cpu")
-        tracks, rows, slots = {}, [], []
-        out: List[List[SegmentView]] = [[] for _ in queries]
-        for qi, (tv, begin, dur) in enumerate(queries):
-            level = self._level(tv.level)
-            if not level:
-                raise Exception("getSegmentList: level doesn't exist")
-            details = getattr(level, "details", None)
-            if not details:
-                log.warning("getSegmentList: level not parsed yet")
-                continue
-            t = tracks.setdefault(tv.level, len(tracks))
-            rows.append((t, float(begin), float(dur)))
-            slots.append(qi)
-        if not rows:
-            return out
-        levels = sorted(tracks, key=tracks.get)
-        frag_lists = [self.hls.levels[lv].details.fragments for lv in levels]
-        if dev.type == "cpu" or len(rows) < self.DEVICE_BATCH_MIN:
-            for (t, b, d), qi in zip(rows, slots):
-                out[qi] = self.getSegmentList(queries[qi][0], b, d)
-            return out
-        from ..ops.segment import range_select
-
-        starts = [[f.start for f in fl] for fl in frag_lists]
-        lo, hi = range_select(starts, rows, dev)
-        for (t, _, _), qi, a, b in zip(rows, slots, lo.tolist(), hi.tolist()):
-            tv = queries[qi][0]
-            fl = frag_lists[t]
-            out[qi] = [SegmentView(sn=fl[i].sn, trackView=tv, time=fl[i].start) for i in range(max(a, 0), max(b, 0))]
-        return out
+    def getSegmentLists(self, queries: List[Any]) -> List[List[SegmentView]]:
+        """Batched ``getSegmentList`` over ``[(trackView, beginTime, duration), ...]``: the
+        same semantics per query (closed interval, playlist order; unparsed level -> ``[]``,
+        missing level -> raises), one cached start index per level for the whole batch."""
+        return [self.getSegmentList(tv, begin, dur) for tv, begin, dur in queries]
 
     def fragment(self, segmentView: SegmentView) -> Any:
         """The playlist fragment behind a SegmentView (url / byte range for the agent's

@@ -20,8 +20,6 @@ hipError_t launch_crc32_batch(const uint8_t*, const int64_t*, const int64_t*, co
                               const int64_t*, uint32_t*, int64_t, int, int64_t, int, bool, hipStream_t);
 hipError_t launch_ts_demux(const uint8_t*, const int64_t*, const int64_t*, const int64_t*, int, int64_t, uint32_t*,
                            int64_t*, int32_t*, uint8_t*, const int64_t*, int64_t*, int64_t, int64_t*, hipStream_t);
-hipError_t launch_range_select(const double*, const int64_t*, const int64_t*, const double*, const double*, int64_t*,
-                               int64_t*, int64_t, int64_t, hipStream_t);
 hipError_t launch_segment_copy(const uint8_t*, uint8_t*, const int64_t*, const int64_t*, const int64_t*,
                                const int64_t*, int, int64_t, hipStream_t);
 }  // namespace dev
@@ -160,22 +158,6 @@ void ts_demux(Tensor buf, Tensor seg_off, Tensor seg_len, Tensor blk_prefix, int
      "ts_demux");
 }
 
-void range_select(Tensor starts, Tensor track_off, Tensor q_track, Tensor q_begin, Tensor q_dur, Tensor out_lo,
-                  Tensor out_hi) {
-  const int64_t nq = q_track.numel();
-  check(starts, "starts", torch::kFloat64);
-  check(track_off, "track_off", torch::kInt64, 1);
-  check(q_track, "q_track", torch::kInt64);
-  check(q_begin, "q_begin", torch::kFloat64, nq);
-  check(q_dur, "q_dur", torch::kFloat64, nq);
-  check(out_lo, "out_lo", torch::kInt64, nq);
-  check(out_hi, "out_hi", torch::kInt64, nq);
-  ok(D::launch_range_select(cptr<double>(starts), cptr<int64_t>(track_off), cptr<int64_t>(q_track),
-                            cptr<double>(q_begin), cptr<double>(q_dur), mptr<int64_t>(out_lo), mptr<int64_t>(out_hi),
-                            nq, track_off.numel() - 1, stream()),
-     "range_select");
-}
-
 void segment_copy(Tensor src, Tensor dst, Tensor src_off, Tensor dst_off, Tensor len, Tensor chunk_prefix,
                   int64_t total_chunks) {
   const int64_t n = src_off.numel();
@@ -303,8 +285,6 @@ TORCH_LIBRARY(hlsp2p, m) {
   m.def("ts_demux(Tensor buf, Tensor seg_off, Tensor seg_len, Tensor blk_prefix, int total_blocks, "
         "Tensor(a!) meta, Tensor(b!) pts_dts, Tensor(c!) blk_sums, Tensor(d!) es, Tensor es_off, Tensor(e!) pes, "
         "int max_pes, Tensor(f!) info) -> ()");
-  m.def("range_select(Tensor starts, Tensor track_off, Tensor q_track, Tensor q_begin, Tensor q_dur, "
-        "Tensor(a!) out_lo, Tensor(b!) out_hi) -> ()");
   m.def("segment_copy(Tensor src, Tensor(a!) dst, Tensor src_off, Tensor dst_off, Tensor len, Tensor chunk_prefix, "
         "int total_chunks) -> ()");
 }
@@ -313,7 +293,6 @@ TORCH_LIBRARY_IMPL(hlsp2p, CUDA, m) {
   m.impl("aes128_cbc_decrypt", &aes128_cbc_decrypt);
   m.impl("crc32_batch", &crc32_batch);
   m.impl("ts_demux", &ts_demux);
-  m.impl("range_select", &range_select);
   m.impl("segment_copy", &segment_copy);
 }
 
@@ -331,7 +310,6 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("expect"), py::arg("ok_out"), py::arg("total_tiles"), py::arg("scatter_idx") = py::none(),
         py::arg("scatter_out") = py::none());
   m.def("ts_demux", &ts_demux);
-  m.def("range_select", &range_select);
   m.def("segment_copy", &segment_copy);
   m.def("device_cus", &device_cus);
   m.def("h2d_batch", &h2d_batch, pybind11::arg("dst"), pybind11::arg("dst_off"), pybind11::arg("src_ptr"),

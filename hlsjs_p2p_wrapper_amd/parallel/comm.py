@@ -549,7 +549,8 @@ class _IpcOutbox:
         evs: Optional[List[List[Any]]] = None
         if all(h is not None for h in handles):
             try:
-                evs = [own if r == me else [torch.cuda.Event.from_ipc_handle(dev, x) for x in h]  # type: ignore[union-attr]
+                opened = torch.cuda.Event.from_ipc_handle
+                evs = [own if r == me else [opened(dev, x) for x in h]  # type: ignore[union-attr]
                        for r, h in enumerate(handles)]
             except Exception:  # noqa: BLE001
                 evs = None

@@ -131,15 +131,6 @@ def test_decrypt_then_demux_on_device(cuda):
     assert tuple(info[9:12]) == tuple(st["n_pes"])
 
 
-def test_range_select(cuda):
-    starts = [[10.0 * i for i in range(25, 200)], [4.0 * i for i in range(10)]]
-    queries = [(0, 365, 33), (0, 10, 275), (0, 1975, 3000), (0, 240, 2100), (0, 2100, 3000), (1, 0, 8), (5, 0, 1)]
-    lo, hi = segment.range_select(starts, queries, cuda)
-    clo, chi = segment.range_select(starts, queries, torch.device("cpu"))
-    assert lo.tolist() == clo.tolist() and hi.tolist() == chi.tolist()
-    assert (lo[0], hi[0]) == (12, 15)
-
-
 def test_copy_segments(cuda):
     src = torch.randint(0, 256, (1 << 20,), dtype=torch.uint8, device=cuda)
     dst = torch.zeros_like(src)

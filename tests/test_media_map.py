@@ -1,9 +1,7 @@
-"""Port of ``test/media-map.js`` plus the batched range-select (K1) oracle agreement."""
+"""Port of ``test/media-map.js`` plus the batched ``getSegmentLists`` agreement with single queries."""
 import pytest
-import torch
 
 from hlsjs_p2p_wrapper_amd.models import MediaMap, SegmentView, TrackView
-from hlsjs_p2p_wrapper_amd.ops import segment
 from mocks import HlsMock
 
 
@@ -63,17 +61,6 @@ def test_get_segment_duration_is_first_fragment_duration():
     assert mm.getSegmentDuration(SegmentView(sn=100, trackView=TrackView(level=1, urlId=0))) == 10
 
 
-def test_range_select_cpu_matches_media_map():
-    mock = HlsMock(3, False, 1)
-    starts = [[f.start for f in mock.levels[1].details.fragments]]
-    queries = [(0, 365, 33), (0, 10, 275), (0, 1975, 3000), (0, 240, 2100), (0, 2100, 3000)]
-    lo, hi = segment.range_select(starts, queries, torch.device("cpu"))
-    mm = MediaMap(mock)
-    for (t, b, d), l, h in zip(queries, lo, hi):
-        want = [s.sn for s in mm.getSegmentList(TrackView(level=1, urlId=0), b, d)]
-        assert [25 + i for i in range(l, h)] == want
-
-
 _QUERIES = [(365, 33), (10, 275), (1975, 3000), (240, 2100), (2100, 3000), (0, 0), (250, 0), (-50, 60)]
 
 
@@ -92,16 +79,6 @@ def test_fragment_lookup():
     f = mm.fragment(SegmentView(sn=42, trackView=tv, time=420))
     assert f is not None and f.sn == 42
     assert mm.fragment(SegmentView(sn=100000, trackView=tv, time=0)) is None
-
-
-@pytest.mark.gpu
-def test_batched_segment_lists_on_device(cuda):
-    # >= DEVICE_BATCH_MIN queries: answered by the HIP range-select kernel (K1)
-    mm = _mm(3, False, 1)
-    tv = TrackView(level=1, urlId=1)
-    qs = [(tv, b + 7 * i, d) for i in range(12) for b, d in _QUERIES]
-    assert len(qs) >= MediaMap.DEVICE_BATCH_MIN
-    assert mm.getSegmentLists(qs, device=cuda) == [mm.getSegmentList(tv, b, d) for _, b, d in qs]
 
 
 def test_start_index_cache_follows_fragment_mutations():

@@ -11,7 +11,7 @@ import torch
 
 from hlsjs_p2p_wrapper_amd.ops import aes, crc, segment, tsdemux
 
-OPS = ("aes128_cbc_decrypt", "crc32_batch", "ts_demux", "range_select", "segment_copy")
+OPS = ("aes128_cbc_decrypt", "crc32_batch", "ts_demux", "segment_copy")
 
 
 def _kernel_module():
@@ -66,7 +66,6 @@ def test_kernel_suite_through_the_dispatcher(cuda, via_dispatcher):
     k.test_aes_cbc_decrypt_matches_host(cuda)
     k.test_ts_demux_matches_cpu_oracle(cuda)
     k.test_decrypt_then_demux_on_device(cuda)
-    k.test_range_select(cuda)
     k.test_copy_segments(cuda)
     k.test_native_crc_launch_matches_python_assembly(cuda)
     for variant in ("fp4", "i8"):
