@@ -467,6 +467,9 @@ def _fleet(args, world, rank, device, use_gpu, node, origin, players, desc, encr
 
     debug = os.environ.get("HLSP2P_FLEET_DEBUG")
     nstep = [0]
+    from hlsjs_p2p_wrapper_amd.utils.trace import PhaseTimer
+
+    fleet_timer = PhaseTimer()
 
     live = args.config in LIVE
     pace = {"next": 0.0}
@@ -481,17 +484,31 @@ def _fleet(args, world, rank, device, use_gpu, node, origin, players, desc, encr
             online = (nstep[0] // args.churn) % (world + 1) != rank
             if online != node.online:
                 node.set_online(online)
+        pc = time.perf_counter
+        t0 = pc()
         drain_ready()
         server.await_players()  # the players' next requests (paces the rounds by the players)
+        t1 = pc()
         server.poll()
         server.admit(K)  # K per player and round: players keep the same pace on every rank
+        t2 = pc()
         state["hs"].append(node.launch_round())
         if len(state["hs"]) > args.lag:
             node.complete_round(state["hs"].popleft())
+        t3 = pc()
         b = server.launch_transmux()
         server.complete_transmux(state["b"])
+        t4 = pc()
         server.send()
         state["b"] = b
+        t5 = pc()
+        # the rank's step split: waiting on players vs its own host work (per phase)
+        ft = fleet_timer.total
+        ft["await_players"] += t1 - t0
+        ft["poll_admit"] += t2 - t1
+        ft["rounds"] += t3 - t2
+        ft["transmux"] += t4 - t3
+        ft["send"] += t5 - t4
         nstep[0] += 1
         if debug and nstep[0] % 20 == 0:
             print(f"# fleet step {nstep[0]} round {node.round} wants {node.pending()} "
@@ -547,6 +564,8 @@ def _fleet(args, world, rank, device, use_gpu, node, origin, players, desc, encr
             step()
         sync()
         node.timer.reset()
+        pipe.timer.reset()
+        fleet_timer.reset()
         s0 = dict(node.stats)
         mark("t0")
         t0 = time.perf_counter()
@@ -556,6 +575,8 @@ def _fleet(args, world, rank, device, use_gpu, node, origin, players, desc, encr
             step()
         sync()
         elapsed = time.perf_counter() - t0
+        fleet_ms = fleet_timer.summary_ms(args.steps)
+        node_ms, tm_ms = node.timer.summary_ms(args.steps), pipe.timer.summary_ms(args.steps)
         if _PROF is not None:
             _PROF.disable()
             _dump_profile(rank)
@@ -601,8 +622,9 @@ def _fleet(args, world, rank, device, use_gpu, node, origin, players, desc, encr
             print(f"# rank {rank} pack {t_pack:.2f}s players {W} data plane {plane} {_mem(use_gpu, device)} "
                   f"marks {dict(m1)}\n"
                   f"#   node stats {node.stats} last round {node.last_round}\n"
-                  f"#   node ms {node.timer.summary_ms(args.steps)}\n"
-                  f"#   transmux ms {pipe.timer.summary_ms(args.steps)}", file=sys.stderr)
+                  f"#   node ms {node_ms}\n"
+                  f"#   transmux ms {tm_ms}\n"
+                  f"#   fleet step ms {fleet_ms}", file=sys.stderr)
         if rank == 0:
             print(json.dumps(result), flush=True)
     finally:
