@@ -118,6 +118,8 @@ def parse():
     p.add_argument("--live-window", type=int, default=15, help="live configs: playlist window in segments")
     p.add_argument("--round-ms", type=float, default=5.0,
                    help="live configs: one node round per this many wall milliseconds (paced)")
+    p.add_argument("--playlist-steps", type=int, default=None,
+                   help="size the players' DVR window for this many steps instead of --steps (soak analysis)")
     p.add_argument("--verbose", action="store_true")
     return p.parse_args()
 
@@ -154,7 +156,9 @@ def _workload(args):
              "tiny-abr": [Rendition(20_000 * (i + 1), 160 * (i + 1), 90 * (i + 1), name=f"t{i}")
                           for i in range(5)]}[preset]
     K = args.inflight
-    n_segments = (args.warmup + args.steps + 4) * K
+    # each player's slice of the DVR window covers the run (--playlist-steps: size it for a
+    # longer run, to tell a playlist-size effect from a run-length effect in soaks)
+    n_segments = (args.warmup + max(args.steps, args.playlist_steps or 0) + 4) * K
     W = max(0, args.players)
     origin_kwargs = dict(base_url="http://cdn.bench/live/", renditions=rends,
                          num_segments=n_segments * max(1, W) + (16 * K if W else 0),
@@ -448,7 +452,7 @@ def _fleet(args, world, rank, device, use_gpu, node, origin, players, desc, encr
     from hlsjs_p2p_wrapper_amd.net.event_loop import get_event_loop
     from hlsjs_p2p_wrapper_amd.parallel.fleet import FleetServer
     from hlsjs_p2p_wrapper_amd.player.transmux import pipeline_for
-    from hlsjs_p2p_wrapper_amd.utils.runtime import tune_gc
+    from hlsjs_p2p_wrapper_amd.utils.runtime import cpu_calibration_us, tune_gc
 
     W, K = args.players, args.inflight
     conns, procs = players
@@ -526,7 +530,7 @@ def _fleet(args, world, rank, device, use_gpu, node, origin, players, desc, encr
     def mark(tag):
         for c, o in zip(conns, server.open):
             if o:
-                c.send(("mark", tag))
+                c.send(("mark", tag, {"calib": args.verbose}))
 
     try:
         # players start (imports, origin): wait for every player of every rank, then let them
@@ -567,12 +571,19 @@ def _fleet(args, world, rank, device, use_gpu, node, origin, players, desc, encr
         pipe.timer.reset()
         fleet_timer.reset()
         s0 = dict(node.stats)
+        calib0 = cpu_calibration_us() if args.verbose else 0.0
         mark("t0")
         t0 = time.perf_counter()
         if _PROF is not None:
             _PROF.enable()
-        for _ in range(args.steps):
+        blocks, tb = [], t0  # soak analysis: wall ms per step over blocks of the window
+        bs = max(1, args.steps // 10)
+        for i in range(args.steps):
             step()
+            if (i + 1) % bs == 0:
+                tn = time.perf_counter()
+                blocks.append(round((tn - tb) * 1e3 / bs, 3))
+                tb = tn
         sync()
         elapsed = time.perf_counter() - t0
         fleet_ms = fleet_timer.summary_ms(args.steps)
@@ -580,6 +591,7 @@ def _fleet(args, world, rank, device, use_gpu, node, origin, players, desc, encr
         if _PROF is not None:
             _PROF.disable()
             _dump_profile(rank)
+        calib1 = cpu_calibration_us() if args.verbose else 0.0
         mark("t1")
         s1 = dict(node.stats)
         # keep serving until every player has acknowledged both marks (collective rounds)
@@ -624,7 +636,12 @@ def _fleet(args, world, rank, device, use_gpu, node, origin, players, desc, encr
                   f"#   node stats {node.stats} last round {node.last_round}\n"
                   f"#   node ms {node_ms}\n"
                   f"#   transmux ms {tm_ms}\n"
-                  f"#   fleet step ms {fleet_ms}", file=sys.stderr)
+                  f"#   fleet step ms {fleet_ms}\n"
+                  f"#   step ms by tenth of the window {blocks}\n"
+                  f"#   core speed (fixed loop, us): rank {calib0:.0f} -> {calib1:.0f}; players "
+                  f"{[round(m0[w].get('calib_us', 0)) for w in sorted(m0)]} -> "
+                  f"{[round(m1[w].get('calib_us', 0)) for w in sorted(m1)]}\n"
+                  f"#   player CPU per buffered fragment (us) {_player_cpu(m0, m1)}", file=sys.stderr)
         if rank == 0:
             print(json.dumps(result), flush=True)
     finally:
@@ -700,6 +717,17 @@ def _data_plane(dist, transport) -> str:
     if transport and transport.startswith("rccl"):
         return "rccl"
     return "ipc" if transport == "hip-ipc" else "gloo"
+
+
+def _player_cpu(m0: dict, m1: dict) -> list:
+    """Per fleet player: CPU seconds spent between the window marks over fragments buffered."""
+    out = []
+    for w in sorted(m1):
+        a, b = m0.get(w, {}), m1[w]
+        n = b["buffered"] - a.get("buffered", 0)
+        if n > 0 and "cpu_s" in a and "cpu_s" in b:
+            out.append(round((b["cpu_s"] - a["cpu_s"]) * 1e6 / n, 1))
+    return out
 
 
 def _dump_profile(rank: int) -> None:

@@ -765,7 +765,7 @@ def player_main(conn: Any, spec: Dict[str, Any]) -> None:
     from ..net import new_event_loop
     from ..net.origin import SyntheticHlsOrigin
     from ..player import MediaElement
-    from ..utils.runtime import tune_gc
+    from ..utils.runtime import cpu_calibration_us, tune_gc
 
     import torch
 
@@ -852,6 +852,9 @@ def player_main(conn: Any, spec: Dict[str, Any]) -> None:
                 if msg[0] == "mark":
                     counters["bytes"] = node.stats.get("cdn", 0) + node.stats.get("p2p", 0)
                     out = dict(counters)
+                    out["cpu_s"] = time.process_time()
+                    if len(msg) > 2 and msg[2].get("calib"):  # soak analysis: core speed at the mark
+                        out["calib_us"] = cpu_calibration_us()
                     if live_lat:  # live latency behind the edge since the previous mark
                         out["live_latency_s"] = live_lat[:]
                         live_lat.clear()

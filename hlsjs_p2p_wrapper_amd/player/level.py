@@ -11,7 +11,7 @@ from dataclasses import dataclass, field
 from typing import Any, List, Optional
 
 
-@dataclass
+@dataclass(slots=True)
 class DecryptData:
     method: Optional[str] = None
     uri: Optional[str] = None
@@ -34,7 +34,7 @@ def fragment_generation() -> int:
     return _START_GENERATION[0]
 
 
-@dataclass(eq=False)
+@dataclass(eq=False, slots=True)  # slots: a long DVR playlist holds 10^5..10^6 of these
 class Fragment:
     url: str
     sn: int

@@ -17,6 +17,7 @@ from __future__ import annotations
 
 import gc
 import os
+import time
 from typing import List, Optional, Tuple
 
 
@@ -35,6 +36,21 @@ def tune_gc(gen0_threshold: int = 50_000) -> Tuple[int, int, int]:
     if os.environ.get("HLSP2P_GC_DISABLE") == "1":  # diagnostic: no cyclic GC after start-up at all
         gc.disable()
     return prev
+
+
+def cpu_calibration_us(n: int = 20_000, reps: int = 3) -> float:
+    """Best-of-``reps`` time of a fixed pure-Python loop, in microseconds: a process's own
+    measure of how fast its core runs right now (soak analysis: if this drifts with the rest
+    of a process's phases, the slowdown is the machine's -- clocks, co-tenants -- not growing
+    state in the process)."""
+    best = float("inf")
+    for _ in range(reps):
+        t = time.perf_counter()
+        x = 0
+        for i in range(n):
+            x += i & 7
+        best = min(best, time.perf_counter() - t)
+    return best * 1e6
 
 
 def _parse_cpulist(text: str) -> List[int]:
