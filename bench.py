@@ -107,6 +107,11 @@ def parse():
     p.add_argument("--numa", default="auto", choices=["auto", "off", "remote"],
                    help="auto: run on (and first-touch pinned buffers from) the CPUs local to the GPU; "
                         "remote: the other socket's CPUs (diagnostic); off: leave the affinity alone")
+    p.add_argument("--cpu-place", default=os.environ.get("HLSP2P_CPU_PLACE", "shared"),
+                   choices=["shared", "nosmt", "cores"],
+                   help="CPU placement of the rank and its players inside the NUMA binding (utils/runtime.py "
+                        "place_processes): shared = one common CPU set; nosmt = one thread per physical core "
+                        "(no two of them on SMT siblings); cores = a physical core each")
     p.add_argument("--ingest", default="pcie", choices=["pcie", "hbm"],
                    help="pcie: the CDN origin is pinned host memory (the benchmark); hbm: DIAGNOSTIC, the "
                         "origin's segment pools live in HBM, so CDN fetches are device-to-device copies "
@@ -142,6 +147,19 @@ def _numa(mode: str, dev: int, world: int = 1, players: int = 0):
         return None
     os.sched_setaffinity(0, other)
     return f"remote-of-{node}"
+
+
+def _place(mode: str, dev: int, pids):
+    """Placement of this GPU's host processes (``--cpu-place``); the slot of a rank is its
+    GPU's position among the GPUs on the same NUMA node, so ranks never share cores."""
+    from hlsjs_p2p_wrapper_amd.utils.runtime import gpu_local_cpus, place_processes
+
+    if mode == "shared":
+        return None
+    node, _ = gpu_local_cpus(dev)
+    slot = sum(1 for i in range(dev) if node is not None and gpu_local_cpus(i)[0] == node)
+    sets = place_processes(pids, mode, slot)
+    return None if sets is None else mode
 
 
 def _workload(args):
@@ -241,9 +259,12 @@ def main() -> int:
                     os.sched_setaffinity(pr.pid, os.sched_getaffinity(0))
                 except OSError:
                     pass
+        cpu_place = _place(args.cpu_place, local_dev, [os.getpid()] + ([pr.pid for pr in players[1]] if players else []))
     else:
         device = torch.device("cpu")
         numa_node = None
+        cpu_place = None
+    args.cpu_place_applied = cpu_place
     import torch.distributed as dist
 
     if world > 1:
@@ -694,6 +715,7 @@ def _result(args, world, tot, max_s, origin, K, desc, encrypted, seg_dur, use_gp
                    "inflight_per_gpu": inflight, "players_per_gpu": max(1, players),
                    "player_processes": players > 0, "encrypted": encrypted, "segment_s": seg_dur,
                    "churn_steps": args.churn, "device": "MI355X" if use_gpu else "cpu", "numa": numa_node,
+                   "cpu_place": getattr(args, "cpu_place_applied", None) or "shared",
                    "ingest": args.ingest if use_gpu else "host"},
     }
 

@@ -84,6 +84,63 @@ def gpu_local_cpus(device_index: int = 0) -> Tuple[Optional[int], List[int]]:
     return (node if node >= 0 else None), cpus
 
 
+def physical_cores(cpus) -> List[List[int]]:
+    """Group logical CPUs into physical cores (SMT siblings together, from sysfs
+    ``thread_siblings_list``), in ascending order of each core's first CPU; CPUs whose
+    topology is unreadable count as one-thread cores."""
+    allowed = set(cpus)
+    cores, seen = [], set()
+    for c in sorted(allowed):
+        if c in seen:
+            continue
+        try:
+            with open(f"/sys/devices/system/cpu/cpu{c}/topology/thread_siblings_list") as f:
+                sib = [s for s in _parse_cpulist(f.read()) if s in allowed]
+        except (OSError, ValueError):
+            sib = [c]
+        if c not in sib:
+            sib.append(c)
+        seen.update(sib)
+        cores.append(sorted(sib))
+    return cores
+
+
+def place_processes(pids: List[int], mode: str, slot: int = 0) -> Optional[List[List[int]]]:
+    """CPU placement of one GPU's host processes (the rank first, then its players), inside
+    the affinity the caller already has (e.g. its GPU's NUMA node).
+
+    * ``shared``: leave it (every process may run on every allowed CPU);
+    * ``nosmt``: every process may run on one thread of each allowed physical core, so the
+      scheduler can never put two of them on SMT siblings (two busy Python processes on one
+      core run at ~0.55x each);
+    * ``cores``: each process gets a physical core of its own (all its threads).  ``slot``
+      offsets the cores by ``slot * len(pids)`` so several ranks on one NUMA node do not
+      overlap.
+
+    Returns the CPU lists applied (None: left alone, e.g. too few cores)."""
+    if mode == "shared" or not pids:
+        return None
+    cores = physical_cores(os.sched_getaffinity(0))
+    if mode == "nosmt":
+        if len(cores) < len(pids):
+            return None
+        cpus = [c[0] for c in cores]
+        sets = [cpus] * len(pids)
+    elif mode == "cores":
+        first = slot * len(pids)
+        if first + len(pids) > len(cores):
+            return None
+        sets = [cores[first + i] for i in range(len(pids))]
+    else:
+        raise ValueError(f"unknown CPU placement {mode!r}")
+    for pid, s in zip(pids, sets):
+        try:
+            os.sched_setaffinity(pid, s)
+        except OSError:
+            return None
+    return sets
+
+
 def bind_to_gpu_numa(device_index: int = 0, min_cpus: int = 8) -> Optional[int]:
     """Restrict this process to the CPUs local to its GPU (and so, by first touch, its later
     host allocations to that NUMA node).  Only narrows the current affinity, and only when

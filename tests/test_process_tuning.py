@@ -41,3 +41,44 @@ def test_bind_only_narrows_and_needs_enough_cpus(monkeypatch):
     half = sorted(allowed)[:len(allowed) // 2]
     monkeypatch.setattr(rt, "gpu_local_cpus", lambda d: (1, half + [10_000]))
     assert rt.bind_to_gpu_numa(0, min_cpus=1) == 1 and calls == [set(half)]  # the intersection only
+
+
+def test_place_processes_modes(monkeypatch):
+    # 4 physical cores with two SMT threads each: cpu c and c + 4 are siblings
+    sib = {c: [c % 4, c % 4 + 4] for c in range(8)}
+    monkeypatch.setattr(os, "sched_getaffinity", lambda pid: set(range(8)))
+    monkeypatch.setattr(rt, "physical_cores", lambda cpus: [sorted(sib[c]) for c in range(4)])
+    calls = []
+    monkeypatch.setattr(os, "sched_setaffinity", lambda pid, cpus: calls.append((pid, sorted(cpus))))
+    assert rt.place_processes([10, 11], "shared") is None and not calls
+    # one thread per core, shared by every process
+    assert rt.place_processes([10, 11], "nosmt") == [[0, 1, 2, 3]] * 2
+    assert calls == [(10, [0, 1, 2, 3]), (11, [0, 1, 2, 3])]
+    calls.clear()
+    # a core each; the second rank on the node takes the next cores
+    assert rt.place_processes([10, 11], "cores", slot=1) == [[2, 6], [3, 7]]
+    assert calls == [(10, [2, 6]), (11, [3, 7])]
+    calls.clear()
+    # not enough cores: left alone
+    assert rt.place_processes([10, 11, 12], "cores", slot=1) is None and not calls
+    with pytest.raises(ValueError):
+        rt.place_processes([10], "bogus")
+
+
+def test_physical_cores_groups_siblings(tmp_path, monkeypatch):
+    import builtins
+
+    real_open = builtins.open
+
+    def fake_open(path, *a, **k):
+        p = str(path)
+        if p.startswith("/sys/devices/system/cpu/cpu") and p.endswith("thread_siblings_list"):
+            c = int(p.split("/cpu/cpu")[1].split("/")[0])
+            return io.StringIO(f"{c % 2},{c % 2 + 2}\n")
+        return real_open(path, *a, **k)
+
+    import io
+
+    monkeypatch.setattr(builtins, "open", fake_open)
+    assert rt.physical_cores({0, 1, 2, 3}) == [[0, 2], [1, 3]]
+    assert rt.physical_cores({0, 1, 3}) == [[0], [1, 3]]
