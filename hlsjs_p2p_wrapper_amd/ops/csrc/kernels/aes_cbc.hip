@@ -31,79 +31,77 @@
 // out_len[seg] on device — the demux kernels read it directly (no host round trip).
 #include "common.h"
 
+#include "aes_dev.h"
+#include "demux_dev.h"
+#include "ts_scatter.h"
+
 namespace hlsp2p {
 namespace dev {
 
-constexpr int kAesThreads = 1024;
+constexpr int kAesThreads = kAesImageThreads;
 constexpr int kAesWgPerCu = 1;
 constexpr int kBlk = 4;  // blocks per lane per chunk (chunk = 64 * kBlk blocks): independent chains
-constexpr int kTdDwords = 2 * 256 * 64;  // regions A + B
-constexpr int kIsDwords = 256 * 32;      // region C
-constexpr uint32_t kIsRegion = 0x20000u;
+static_assert(64 * kBlk == kScatterIterBlocks, "the edge kernel's view of a decrypt iteration");
 
-// v_perm_b32 selector: byte k of the state word -> bits 8..15; bits 0..7 and 16..23 from
-// the per-lane table base (S1 bytes 0 and 2); bits 24..31 = 0
-#define SEL(k) (0x0c020000u | ((4u + (k)) << 8))
-#define LDS32(addr) (*reinterpret_cast<const uint32_t*>(s_bytes + (addr)))
-#define TD(t, w, k) LDS32(__builtin_amdgcn_perm((w), td_base[t], SEL(k)))
-#define IS(w, k) LDS32(((((w) >> (8 * (k))) & 0xffu) << 7) + is_base)
+// Scatter epilogue (the scatter demux, ts_scatter.hip): instead of writing the plaintext,
+// every block writes the bytes of it that are TS payload straight to their elementary-stream
+// position.  place[pkt] = (bias, lo | hi << 16): payload bytes y in [lo, hi) of packet pkt go
+// to es + es_off[seg] + bias + y.
+struct AesScatter {
+  const uint2* place;        // per packet slot (the demux's 256-packet block grid)
+  const int64_t* pkt_base;   // [nseg] first packet slot of the segment
+  const int64_t* pkt_slots;  // [nseg] packet slots of the segment
+  uint8_t* es;
+  const int64_t* es_off;     // [nseg]
+};
 
-// CDNA4 3-input bitwise op (truth table 0x96 = a ^ b ^ c); the round key is an SGPR operand
-#define XOR3(a, b, c) __builtin_amdgcn_bitop3_b32((a), (b), (c), 0x96)
-
-// little-endian column form of the equivalent inverse cipher round: TdtL = rotl(Td0L, 8t);
-// per column 4 v_perm + 4 ds_read_b32 + 2 v_bitop3
-#define AES_ROUND(s0, s1, s2, s3, t0, t1, t2, t3, k)                                     \
-  t0 = XOR3(XOR3(TD(0, s0, 0), TD(1, s3, 1), TD(2, s2, 2)), TD(3, s1, 3), (k)[0]);      \
-  t1 = XOR3(XOR3(TD(0, s1, 0), TD(1, s0, 1), TD(2, s3, 2)), TD(3, s2, 3), (k)[1]);      \
-  t2 = XOR3(XOR3(TD(0, s2, 0), TD(1, s1, 1), TD(2, s0, 2)), TD(3, s3, 3), (k)[2]);      \
-  t3 = XOR3(XOR3(TD(0, s3, 0), TD(1, s2, 1), TD(2, s1, 2)), TD(3, s0, 3), (k)[3]);
-
-// The same round split in two phases (used by the kernel for explicit pipelining):
-// 16 table addresses + 16 LDS reads of one state, then the 8 v_bitop3 that fold them.
-#define TDA(t, w, k) __builtin_amdgcn_perm((w), td_base[t], SEL(k))
-#define ROUND_READS(v, s)                                                                   \
-  do {                                                                                      \
-    uint32_t a_[16];                                                                        \
-    a_[0] = TDA(0, s[0], 0); a_[1] = TDA(1, s[3], 1); a_[2] = TDA(2, s[2], 2); a_[3] = TDA(3, s[1], 3);     \
-    a_[4] = TDA(0, s[1], 0); a_[5] = TDA(1, s[0], 1); a_[6] = TDA(2, s[3], 2); a_[7] = TDA(3, s[2], 3);     \
-    a_[8] = TDA(0, s[2], 0); a_[9] = TDA(1, s[1], 1); a_[10] = TDA(2, s[0], 2); a_[11] = TDA(3, s[3], 3);   \
-    a_[12] = TDA(0, s[3], 0); a_[13] = TDA(1, s[2], 1); a_[14] = TDA(2, s[1], 2); a_[15] = TDA(3, s[0], 3); \
-    _Pragma("unroll") for (int q_ = 0; q_ < 16; ++q_) v[q_] = LDS32(a_[q_]);                \
-  } while (0)
-#define ROUND_XORS(s, v, k)                                                                 \
-  do {                                                                                      \
-    s[0] = XOR3(XOR3(v[0], v[1], v[2]), v[3], (k)[0]);                                      \
-    s[1] = XOR3(XOR3(v[4], v[5], v[6]), v[7], (k)[1]);                                      \
-    s[2] = XOR3(XOR3(v[8], v[9], v[10]), v[11], (k)[2]);                                    \
-    s[3] = XOR3(XOR3(v[12], v[13], v[14]), v[15], (k)[3]);                                  \
-  } while (0)
-
-// final round fused with the CBC chaining: o = InvShiftRows/InvSubBytes(s) ^ k ^ px
-#define AES_FINAL(s0, s1, s2, s3, o0, o1, o2, o3, k, px)                                                  \
-  o0 = XOR3(IS(s0, 0) | (IS(s3, 1) << 8) | (IS(s2, 2) << 16) | (IS(s1, 3) << 24), (k)[0], (px).x);        \
-  o1 = XOR3(IS(s1, 0) | (IS(s0, 1) << 8) | (IS(s3, 2) << 16) | (IS(s2, 3) << 24), (k)[1], (px).y);        \
-  o2 = XOR3(IS(s2, 0) | (IS(s1, 1) << 8) | (IS(s0, 2) << 16) | (IS(s3, 3) << 24), (k)[2], (px).z);        \
-  o3 = XOR3(IS(s3, 0) | (IS(s2, 1) << 8) | (IS(s1, 2) << 16) | (IS(s0, 3) << 24), (k)[3], (px).w);
-
-__device__ __forceinline__ int64_t pkcs7_len(uint4 p, int64_t nbytes) {
-  const uint32_t pad = p.w >> 24;
-  if (pad < 1 || pad > 16) return -1;
-  const uint32_t w[4] = {p.x, p.y, p.z, p.w};
-  bool ok = true;
+// Scatter epilogue of one wave iteration: kBlk chains of 64 consecutive blocks each (chain j,
+// lane l = block b0 + 64j + l), plaintext in w[j][0..3].  A block is FAST when it lies inside
+// one packet's payload and the run continues for the `hb` bytes that bring its destination to
+// dword alignment (demux::scatter_block, the rule the edge kernel applies too): a fast
+// lane writes the four dwords whose first byte is in its block with ONE
+// buffer_store_dwordx4 to the ES (the last `hb` bytes come from the next block: lane l + 1 by
+// DPP), so the next block's first `hb` bytes are done.  Every other block -- packet
+// boundaries, headers, the iteration's last block when it would borrow -- and a fast block
+// whose predecessor did not cover its head, stores its plaintext to the side buffer at its
+// own offset; tsx_edge_kernel (ts_scatter.hip) writes those payload bytes.  One store per
+// block, no divergent byte loop (the kernel is VALU-bound: the epilogue must stay lean).
+template <int N>
+__device__ __forceinline__ void scatter_epilogue(const uint32_t (&w)[N][4], int64_t b0, int64_t nblk, int lane,
+                                                 const uint2* __restrict__ place, int64_t pbase, int64_t slots,
+                                                 __amdgpu_buffer_rsrc_t es_rsrc, __amdgpu_buffer_rsrc_t side_rsrc) {
+  typedef unsigned int v4u __attribute__((ext_vector_type(4)));
+  int prev_last = 0;  // fast flag of the previous chain's lane 63 (block b0 + 64j - 1)
 #pragma unroll
-  for (int b = 0; b < 16; ++b) {
-    const uint32_t byte = (w[b >> 2] >> (8 * (b & 3))) & 0xff;
-    if (b >= 16 - static_cast<int>(pad) && byte != pad) ok = false;
+  for (int j = 0; j < N; ++j) {
+    const int64_t b = b0 + 64 * j;
+    const int x0 = static_cast<int>(16 * b);
+    const int p = x0 / 188;
+    const uint2 pl = (b < nblk && p < slots) ? place[pbase + p] : make_uint2(0, 0);
+    // the successor is at hand unless this is the iteration's last block (chain N-1, lane 63)
+    const demux::ScatterBlock sb = demux::scatter_block(b, pl, nblk, (j + 1 < N || lane < 63) && b + 1 < nblk);
+    const int fast = sb.fast, hb = sb.hb, d0 = sb.bias + sb.y0;
+    int pf = __builtin_amdgcn_update_dpp(0, fast, 0x138, 0xf, 0xf, false);  // lane l - 1 (wave_shr:1)
+    pf = lane == 0 ? prev_last : pf;
+    prev_last = __builtin_amdgcn_readlane(fast, 63);
+    // next block's first word: lane l + 1 (wave_shl:1), or the next chain's lane 0 -- read with
+    // every lane active (a DPP source lane outside EXEC would read as 0)
+    uint32_t nx = static_cast<uint32_t>(__builtin_amdgcn_update_dpp(0, static_cast<int>(w[j][0]), 0x130, 0xf, 0xf, false));
+    if (j + 1 < N) {
+      const uint32_t first = static_cast<uint32_t>(__builtin_amdgcn_readlane(static_cast<int>(w[j + 1][0]), 0));
+      nx = lane == 63 ? first : nx;
+    }
+    const uint32_t sh = static_cast<uint32_t>(hb);
+    if (fast) {
+      const v4u q = {__builtin_amdgcn_alignbyte(w[j][1], w[j][0], sh), __builtin_amdgcn_alignbyte(w[j][2], w[j][1], sh),
+                     __builtin_amdgcn_alignbyte(w[j][3], w[j][2], sh), __builtin_amdgcn_alignbyte(nx, w[j][3], sh)};
+      __builtin_amdgcn_raw_buffer_store_b128(q, es_rsrc, d0 + hb, 0, 0);
+    }
+    if (b < nblk && (!fast || (!pf && hb))) {
+      const v4u r = {w[j][0], w[j][1], w[j][2], w[j][3]};
+      __builtin_amdgcn_raw_buffer_store_b128(r, side_rsrc, x0, 0, 0);
+    }
   }
-  return ok ? nbytes - static_cast<int64_t>(pad) : -1;
-}
-
-// 64-bit wave-uniform value (lane 0's) -> SGPRs
-__device__ __forceinline__ int64_t uniform64(int64_t v) {
-  const uint32_t lo = __builtin_amdgcn_readfirstlane(static_cast<uint32_t>(v));
-  const uint32_t hi = __builtin_amdgcn_readfirstlane(static_cast<uint32_t>(static_cast<uint64_t>(v) >> 32));
-  return static_cast<int64_t>((static_cast<uint64_t>(hi) << 32) | lo);
 }
 
 // tdl: little-endian Td0 (256 words); isb: inverse S-box (256 bytes)
@@ -111,38 +109,22 @@ __device__ __forceinline__ int64_t uniform64(int64_t v) {
 // chunk_prefix: exclusive prefix of per-segment 256-block chunks (one chunk = one wave
 //   iteration: lane l decrypts blocks 64j + l, j < kBlk, so every load/store instruction
 //   moves 1 KB contiguous); waves never straddle segments
+// kScatter: the payload bytes go to their ES positions (AesScatter) and dst + dst_off is the
+//   sparse side buffer of the edge blocks (out_len is the scatter demux's, computed before)
+template <bool kScatter>
 __global__ __launch_bounds__(kAesThreads, 1) void aes128_cbc_decrypt_kernel(
     const uint8_t* __restrict__ src, uint8_t* __restrict__ dst, const int64_t* __restrict__ src_off,
     const int64_t* __restrict__ dst_off, const int64_t* __restrict__ blk_prefix,
     const int64_t* __restrict__ chunk_prefix, const uint32_t* __restrict__ drk, const uint32_t* __restrict__ ivw,
     const uint32_t* __restrict__ tdl_g, const uint8_t* __restrict__ isb_g, int64_t* __restrict__ out_len, int nseg,
-    int64_t total_chunks, int64_t per_wg) {
+    int64_t total_chunks, int64_t per_wg, AesScatter sc) {
   __shared__ uint32_t s_tab[kTdDwords + kIsDwords];  // 160 KiB (layout above)
   const int tid = threadIdx.x;
-  {  // image fill: thread tid writes dwords tid + 1024k, i.e. Td rows (tid >> 6) + 16(k & 15) in region
-     // k >> 4 and InvSbox rows (tid >> 5) + 32k; all 24 source loads are issued before the
-     // first LDS store (a strided load/store loop paid ~40 serialised L2 round trips)
-    static_assert(kAesThreads == 1024 && kTdDwords == 32 * kAesThreads && kIsDwords == 8 * kAesThreads, "fill map");
-    uint32_t td[16], is[8];
-#pragma unroll
-    for (int k = 0; k < 16; ++k) td[k] = tdl_g[(tid >> 6) + 16 * k];
-#pragma unroll
-    for (int k = 0; k < 8; ++k) is[k] = isb_g[(tid >> 5) + 32 * k];
-    const int half = (tid >> 5) & 1;
-#pragma unroll
-    for (int k = 0; k < 32; ++k) {
-      const uint32_t v = td[k & 15];
-      const int rot = 8 * (2 * (k >> 4) + half);
-      s_tab[tid + k * kAesThreads] = rot ? __builtin_amdgcn_alignbit(v, v, 32 - rot) : v;
-    }
-#pragma unroll
-    for (int k = 0; k < 8; ++k) s_tab[kTdDwords + tid + k * kAesThreads] = is[k];
-  }
+  aes_image_fill(s_tab, tdl_g, isb_g, tid);
   __syncthreads();
   const uint8_t* s_bytes = reinterpret_cast<const uint8_t*>(s_tab);
-  const uint32_t l4 = static_cast<uint32_t>(tid & 31) << 2;
-  const uint32_t td_base[4] = {l4, 128u | l4, 0x10000u | l4, 0x10000u | 128u | l4};  // Td0..Td3
-  const uint32_t is_base = kIsRegion + l4;
+  uint32_t td_base[4], is_base;
+  aes_image_bases(tid, td_base, is_base);
   const int lane = tid & 63;
   constexpr int kWaves = kAesThreads / 64;
 
@@ -152,7 +134,9 @@ __global__ __launch_bounds__(kAesThreads, 1) void aes128_cbc_decrypt_kernel(
   // segment state is wave-uniform (SGPRs): round keys come in by scalar loads
   int cur = -1;
   uint32_t rk[44];
-  int64_t so = 0, dof = 0, cstart = 0, cend = 0, nblk = 0;
+  int64_t so = 0, dof = 0, cstart = 0, cend = 0, nblk = 0, pbase = 0, slots = 0;
+  uint8_t* esb = nullptr;
+  uint8_t* sideb = nullptr;
   for (int64_t ch = uniform64(begin + (tid >> 6)); ch < end; ch += kWaves) {
     if (cur < 0 || ch >= cend) {
       cur = cur < 0 ? find_seg_wave(chunk_prefix, nseg, ch)  // whole wave active: ch is uniform
@@ -164,6 +148,12 @@ __global__ __launch_bounds__(kAesThreads, 1) void aes128_cbc_decrypt_kernel(
       cstart = chunk_prefix[cur];
       cend = chunk_prefix[cur + 1];
       nblk = blk_prefix[cur + 1] - blk_prefix[cur];
+      if (kScatter) {
+        pbase = sc.pkt_base[cur];
+        slots = sc.pkt_slots[cur];
+        esb = sc.es + sc.es_off[cur];
+        sideb = dst + dof;
+      }
     }
     const int64_t b0 = (ch - cstart) * (64 * kBlk) + lane;  // this lane's first block
     const uint4* cs = reinterpret_cast<const uint4*>(src + so);
@@ -183,60 +173,74 @@ __global__ __launch_bounds__(kAesThreads, 1) void aes128_cbc_decrypt_kernel(
     for (int j = 0; j < kBlk; ++j) {
       st[j][0] = c[j].x ^ rk[0]; st[j][1] = c[j].y ^ rk[1]; st[j][2] = c[j].z ^ rk[2]; st[j][3] = c[j].w ^ rk[3];
     }
-    // Rounds 1..9, software-pipelined across the chains IN SOURCE ORDER (the backend keeps
-    // this huge unrolled block in emission order): chain j's 16 LDS reads are issued before
-    // chain j-1's XORs consume theirs, so each wave keeps ~16 reads in flight instead of 2-3.
+    AES_ROUNDS_PIPELINED(kBlk, st, rk)
+    if (kScatter) {
+      uint32_t w[kBlk][4];
 #pragma unroll
-    for (int r = 1; r < 10; ++r) {
-      const uint32_t* k = rk + 4 * r;
-      uint32_t v[2][16];
-      ROUND_READS(v[0], st[0]);
-#pragma unroll
-      for (int j = 1; j < kBlk; ++j) {
-        ROUND_READS(v[j & 1], st[j]);
-        ROUND_XORS(st[j - 1], v[(j - 1) & 1], k);
+      for (int j = 0; j < kBlk; ++j) {
+        AES_FINAL(st[j][0], st[j][1], st[j][2], st[j][3], w[j][0], w[j][1], w[j][2], w[j][3], rk + 40, pv[j])
       }
-      ROUND_XORS(st[kBlk - 1], v[(kBlk - 1) & 1], k);
-    }
-    uint4* ds = reinterpret_cast<uint4*>(dst + dof);
+      scatter_epilogue<kBlk>(w, b0, nblk, lane, sc.place, pbase, slots,
+                             __builtin_amdgcn_make_buffer_rsrc(esb, 0, 0x7fffffff, 0x00020000),
+                             __builtin_amdgcn_make_buffer_rsrc(sideb, 0, 0x7fffffff, 0x00020000));
+    } else {
+      uint4* ds = reinterpret_cast<uint4*>(dst + dof);
 #pragma unroll
-    for (int j = 0; j < kBlk; ++j) {
-      uint32_t o0, o1, o2, o3;
-      AES_FINAL(st[j][0], st[j][1], st[j][2], st[j][3], o0, o1, o2, o3, rk + 40, pv[j])
-      const uint4 p = make_uint4(o0, o1, o2, o3);
-      const int64_t b = b0 + 64 * j;
-      if (b < nblk) ds[b] = p;
-      if (b == nblk - 1) out_len[cur] = pkcs7_len(p, nblk * 16);
+      for (int j = 0; j < kBlk; ++j) {
+        uint32_t o0, o1, o2, o3;
+        AES_FINAL(st[j][0], st[j][1], st[j][2], st[j][3], o0, o1, o2, o3, rk + 40, pv[j])
+        const uint4 p = make_uint4(o0, o1, o2, o3);
+        const int64_t b = b0 + 64 * j;
+        if (b < nblk) ds[b] = p;
+        if (b == nblk - 1) out_len[cur] = pkcs7_len(p, nblk * 16);
+      }
     }
   }
 }
-#undef TD
-#undef IS
-#undef LDS32
-#undef SEL
-#undef XOR3
-#undef TDA
-#undef ROUND_READS
-#undef ROUND_XORS
 
 // 16-byte blocks per wave iteration (the host sizes its chunk index space with this)
 int aes_chunk_blocks() { return 64 * kBlk; }
+
+namespace {
+void aes_grid(int64_t total_chunks, int num_cu, int64_t& grid, int64_t& per_wg) {
+  constexpr int64_t kWaves = kAesThreads / 64;
+  const int64_t max_wg = static_cast<int64_t>(num_cu) * kAesWgPerCu;
+  grid = (total_chunks + kWaves * 2 - 1) / (kWaves * 2);
+  if (grid > max_wg) grid = max_wg;
+  if (grid < 1) grid = 1;
+  per_wg = (total_chunks + grid - 1) / grid;
+  grid = (total_chunks + per_wg - 1) / per_wg;
+}
+}  // namespace
 
 hipError_t launch_aes128_cbc_decrypt(const uint8_t* src, uint8_t* dst, const int64_t* src_off, const int64_t* dst_off,
                                      const int64_t* blk_prefix, const int64_t* chunk_prefix, const uint32_t* drk,
                                      const uint32_t* ivw, const uint32_t* tdl, const uint8_t* isb, int64_t* out_len,
                                      int nseg, int64_t total_chunks, int num_cu, hipStream_t stream) {
   if (total_chunks <= 0) return hipSuccess;
-  constexpr int64_t kWaves = kAesThreads / 64;
-  const int64_t max_wg = static_cast<int64_t>(num_cu) * kAesWgPerCu;
-  int64_t grid = (total_chunks + kWaves * 2 - 1) / (kWaves * 2);
-  if (grid > max_wg) grid = max_wg;
-  if (grid < 1) grid = 1;
-  const int64_t per_wg = (total_chunks + grid - 1) / grid;
-  grid = (total_chunks + per_wg - 1) / per_wg;
-  hipLaunchKernelGGL(aes128_cbc_decrypt_kernel, dim3(static_cast<unsigned>(grid)), dim3(kAesThreads), 0, stream, src,
-                     dst, src_off, dst_off, blk_prefix, chunk_prefix, drk, ivw, tdl, isb, out_len, nseg, total_chunks,
-                     per_wg);
+  int64_t grid, per_wg;
+  aes_grid(total_chunks, num_cu, grid, per_wg);
+  hipLaunchKernelGGL(aes128_cbc_decrypt_kernel<false>, dim3(static_cast<unsigned>(grid)), dim3(kAesThreads), 0, stream,
+                     src, dst, src_off, dst_off, blk_prefix, chunk_prefix, drk, ivw, tdl, isb, out_len, nseg,
+                     total_chunks, per_wg, AesScatter{});
+  return hipGetLastError();
+}
+
+// The scatter demux's decrypt (ts_scatter.hip): payload bytes straight to the ES buffer, edge
+// blocks to the side buffer (side + side_off[seg] + 16 b, sparse) for tsx_edge_kernel.
+hipError_t launch_aes128_cbc_scatter(const uint8_t* src, uint8_t* side, const int64_t* src_off,
+                                     const int64_t* side_off, const int64_t* blk_prefix,
+                                     const int64_t* chunk_prefix, const uint32_t* drk, const uint32_t* ivw,
+                                     const uint32_t* tdl, const uint8_t* isb, const uint2* place,
+                                     const int64_t* pkt_base, const int64_t* pkt_slots, uint8_t* es,
+                                     const int64_t* es_off, int nseg, int64_t total_chunks, int num_cu,
+                                     hipStream_t stream) {
+  if (total_chunks <= 0) return hipSuccess;
+  int64_t grid, per_wg;
+  aes_grid(total_chunks, num_cu, grid, per_wg);
+  hipLaunchKernelGGL(aes128_cbc_decrypt_kernel<true>, dim3(static_cast<unsigned>(grid)), dim3(kAesThreads), 0, stream,
+                     src, side, src_off, side_off, blk_prefix, chunk_prefix, drk, ivw, tdl, isb, nullptr, nseg,
+                     total_chunks, per_wg, AesScatter{place, pkt_base, pkt_slots, es, es_off});
   return hipGetLastError();
 }
 

@@ -22,6 +22,7 @@
 
 #include "transmux_args.h"
 #include "ts_onepass.h"
+#include "ts_scatter.h"
 
 namespace hlsp2p {
 namespace dev {
@@ -77,19 +78,30 @@ class Desc {
   Tensor dev_;
 };
 
-// The demux after a decrypt: the psi / scan / prefix / gather sequence (the default, classes
-// packed) or, with HLSP2P_DEMUX=onepass, ts_onepass_kernel (scan + prefix + gather in one
-// kernel with a decoupled look-back, ES classes in three regions per segment; measured
-// slower, profiles/r3_transmux_fused_vs_split.md).
-int g_onepass = -1;
+// The demux of the encrypted group (HLSP2P_DEMUX):
+//  * fourpass: decrypt to a plaintext buffer, then the psi / scan / prefix / gather sequence
+//    (classes packed);
+//  * onepass: decrypt, then ts_onepass_kernel (scan + prefix + gather in one kernel with a
+//    decoupled look-back, ES classes in three regions per segment; measured slower,
+//    profiles/r3_transmux_fused_vs_split.md);
+//  * scatter: no plaintext buffer -- header-only decrypt, scan, prefix, place, then the bulk
+//    decrypt stores payload bytes at their ES positions (ts_scatter.hip).
+// Clear segments always take the four-pass sequence.
+enum DemuxMode { kFourpass = 0, kOnepass = 1, kScatterDemux = 2 };
+int g_demux = -1;
 
-bool use_onepass() {
-  if (g_onepass < 0) {
+int demux_mode() {
+  if (g_demux < 0) {
     const char* v = std::getenv("HLSP2P_DEMUX");
-    g_onepass = (v != nullptr && std::strcmp(v, "onepass") == 0) ? 1 : 0;
+    g_demux = v == nullptr ? kFourpass
+              : std::strcmp(v, "onepass") == 0 ? kOnepass
+              : std::strcmp(v, "scatter") == 0 ? kScatterDemux
+              : kFourpass;
   }
-  return g_onepass == 1;
+  return g_demux;
 }
+bool use_onepass() { return demux_mode() == kOnepass; }
+const char* demux_name(int m) { return m == kOnepass ? "onepass" : m == kScatterDemux ? "scatter" : "fourpass"; }
 
 struct DemuxPlan {
   std::vector<int64_t> idx, off, len, cap, es_off, es_cap, blk_prefix;
@@ -283,7 +295,7 @@ py::tuple transmux_launch(Tensor src, I64 src_off, I64 nbytes, py::array_t<uint8
     return transmux_launch_fused(src, so, nb, en, drk.data(), iv.data(), B, td0, isb, max_pes, device, st);
 
   // ---- plans: AES over the encrypted segments, demux per group
-  std::vector<int64_t> a_so, a_do, a_bp{0}, a_cp{0};
+  std::vector<int64_t> a_so, a_do, a_bp{0}, a_cp{0}, a_hp{0};
   std::vector<uint32_t> a_drk;
   std::vector<uint8_t> a_iv;
   DemuxPlan pe, pc;
@@ -300,6 +312,9 @@ py::tuple transmux_launch(Tensor src, I64 src_off, I64 nbytes, py::array_t<uint8
       const int64_t blocks = nb[i] / 16;
       a_bp.push_back(a_bp.back() + blocks);
       a_cp.push_back(a_cp.back() + (blocks + chunk - 1) / chunk);
+      const int64_t groups = (nb[i] / kPacket + hlsp2p::dev::kScatterGroupPackets - 1) /
+                             hlsp2p::dev::kScatterGroupPackets;  // scatter demux header chunks
+      a_hp.push_back(a_hp.back() + (groups + hlsp2p::dev::kScatterChunkGroups - 1) / hlsp2p::dev::kScatterChunkGroups);
       a_drk.insert(a_drk.end(), drk.data(i, 0), drk.data(i, 0) + 44);
       a_iv.insert(a_iv.end(), iv.data(i, 0), iv.data(i, 0) + 16);
     } else {
@@ -312,10 +327,16 @@ py::tuple transmux_launch(Tensor src, I64 src_off, I64 nbytes, py::array_t<uint8
   const int64_t ne = static_cast<int64_t>(pe.idx.size()), nc = static_cast<int64_t>(pc.idx.size());
   plan_demux(pe);
   plan_demux(pc);
+  const bool scatter = ne > 0 && demux_mode() == kScatterDemux;
+  std::vector<int64_t> pkt_base(ne), pkt_slots(ne);
+  for (int64_t i = 0; i < ne; ++i) {
+    pkt_base[i] = pe.blk_prefix[i] * 256;
+    pkt_slots[i] = (pe.blk_prefix[i + 1] - pe.blk_prefix[i]) * 256;
+  }
 
   // ---- every descriptor of the batch in one staging block, one H2D
   Desc desc;
-  int64_t d_so = -1, d_do = -1, d_bp = -1, d_cp = -1, d_drk = -1, d_iv = -1;
+  int64_t d_so = -1, d_do = -1, d_bp = -1, d_cp = -1, d_drk = -1, d_iv = -1, d_hp = -1, d_pb = -1, d_ps = -1;
   if (ne) {
     d_so = desc.add(a_so);
     d_do = desc.add(a_do);
@@ -327,6 +348,11 @@ py::tuple transmux_launch(Tensor src, I64 src_off, I64 nbytes, py::array_t<uint8
     pe.d_bp = desc.add(pe.blk_prefix);
     pe.d_eo = desc.add(pe.es_off);
     pe.d_ec = desc.add(pe.es_cap);
+    if (scatter) {
+      d_hp = desc.add(a_hp);
+      d_pb = desc.add(pkt_base);
+      d_ps = desc.add(pkt_slots);
+    }
   }
   if (nc) {
     pc.d_off = desc.add(pc.off);
@@ -341,8 +367,11 @@ py::tuple transmux_launch(Tensor src, I64 src_off, I64 nbytes, py::array_t<uint8
   Tensor host = torch::empty({(ne + nc) * kInfo + ne + 1}, torch::TensorOptions().dtype(torch::kInt64).pinned_memory(true));
   Tensor dec, out_len;
   if (ne) {
-    dec = torch::empty({dec_pos + kAlign}, dev_opts.dtype(torch::kUInt8));
     out_len = torch::empty({ne}, dev_opts.dtype(torch::kInt64));
+    // the plaintext (split) or, for the scatter demux, the sparse side buffer of edge blocks
+    dec = torch::empty({dec_pos + kAlign}, dev_opts.dtype(torch::kUInt8));
+  }
+  if (ne && !scatter) {
     hip_ok(hlsp2p::dev::launch_aes128_cbc_decrypt(
                static_cast<const uint8_t*>(src.data_ptr()), static_cast<uint8_t*>(dec.data_ptr()),
                desc.at<int64_t>(d_so), desc.at<int64_t>(d_do), desc.at<int64_t>(d_bp), desc.at<int64_t>(d_cp),
@@ -358,14 +387,52 @@ py::tuple transmux_launch(Tensor src, I64 src_off, I64 nbytes, py::array_t<uint8
     DemuxPlan& p = g == 0 ? pe : pc;
     const int64_t n = static_cast<int64_t>(p.idx.size());
     if (!n) continue;
-    const uint8_t* buf = g == 0 ? static_cast<const uint8_t*>(dec.data_ptr())
-                                : static_cast<const uint8_t*>(src.data_ptr());
+    const uint8_t* buf = g == 1 ? static_cast<const uint8_t*>(src.data_ptr())
+                         : dec.defined() ? static_cast<const uint8_t*>(dec.data_ptr()) : nullptr;
     const int64_t* lens = g == 0 ? out_len.data_ptr<int64_t>() : desc.at<int64_t>(p.d_len);
     const int64_t nb_blocks = std::max<int64_t>(1, p.total_blocks);
     Tensor es = torch::empty({p.es_bytes}, dev_opts.dtype(torch::kUInt8));
     Tensor info = torch::empty({n, kInfo}, dev_opts.dtype(torch::kInt64));
     Tensor pes = torch::empty({n, 3, max_pes, 3}, dev_opts.dtype(torch::kInt64));
-    if (use_onepass()) {
+    if (g == 0 && scatter) {
+      Tensor hdr = torch::empty({nb_blocks * 256}, dev_opts.dtype(torch::kInt32));
+      Tensor meta = torch::empty({nb_blocks * 256}, dev_opts.dtype(torch::kInt32));
+      Tensor pts = torch::empty({nb_blocks * 256 * 2}, dev_opts.dtype(torch::kInt64));
+      Tensor aux = torch::empty({nb_blocks * 12 + n * 7}, dev_opts.dtype(torch::kInt32));
+      Tensor place = torch::empty({nb_blocks * 256}, dev_opts.dtype(torch::kInt64));
+      hlsp2p::dev::ScatterArgs sa{};
+      sa.src = static_cast<const uint8_t*>(src.data_ptr());
+      sa.src_off = desc.at<int64_t>(d_so);
+      sa.aes_blk = desc.at<int64_t>(d_bp);
+      sa.aes_chunks = desc.at<int64_t>(d_cp);
+      sa.hdr_chunks = desc.at<int64_t>(d_hp);
+      sa.drk = desc.at<uint32_t>(d_drk);
+      sa.ivw = desc.at<uint32_t>(d_iv);
+      sa.tdl = static_cast<const uint32_t*>(td0.data_ptr());
+      sa.isb = static_cast<const uint8_t*>(isb.data_ptr());
+      sa.blk_prefix = desc.at<int64_t>(p.d_bp);
+      sa.pkt_base = desc.at<int64_t>(d_pb);
+      sa.pkt_slots = desc.at<int64_t>(d_ps);
+      sa.hdr = reinterpret_cast<uint32_t*>(hdr.data_ptr<int32_t>());
+      sa.meta = reinterpret_cast<uint32_t*>(meta.data_ptr<int32_t>());
+      sa.pts_dts = pts.data_ptr<int64_t>();
+      sa.aux = aux.data_ptr<int32_t>();
+      sa.place = reinterpret_cast<uint2*>(place.data_ptr<int64_t>());
+      sa.side = static_cast<uint8_t*>(dec.data_ptr());
+      sa.side_off = desc.at<int64_t>(d_do);
+      sa.es = es.data_ptr<uint8_t>();
+      sa.es_off = desc.at<int64_t>(p.d_eo);
+      sa.pes = pes.data_ptr<int64_t>();
+      sa.info = info.data_ptr<int64_t>();
+      sa.out_len = out_len.data_ptr<int64_t>();
+      sa.max_pes = max_pes;
+      sa.nseg = static_cast<int>(n);
+      sa.total_blocks = p.total_blocks;
+      sa.aes_total_chunks = a_cp.back();
+      sa.hdr_total_chunks = a_hp.back();
+      hip_ok(hlsp2p::dev::launch_ts_scatter(sa, decrypt_cus(device), st), "ts_scatter");
+      keep.append(py::make_tuple(hdr, meta, pts, aux, place));
+    } else if (use_onepass()) {
       // zeroed: look-back granules [blocks x 3] | ticket + timeout; -1: last PES per block [blocks x 6]
       Tensor zw = torch::empty({nb_blocks * 3 + 1}, dev_opts.dtype(torch::kInt64));
       hip_ok(hipMemsetAsync(zw.data_ptr(), 0, static_cast<size_t>((nb_blocks * 3 + 1) * 8), st), "hipMemsetAsync");
@@ -439,10 +506,11 @@ void register_transmux(py::module& m) {
     TORCH_CHECK_VALUE(m == "fused" || m == "split", "transmux mode must be 'fused' or 'split'");
     g_mode = m == "fused" ? 1 : 0;
   });
-  m.def("demux_mode", [] { return std::string(use_onepass() ? "onepass" : "fourpass"); });
+  m.def("demux_mode", [] { return std::string(demux_name(demux_mode())); });
   m.def("set_demux_mode", [](const std::string& m) {
-    TORCH_CHECK_VALUE(m == "onepass" || m == "fourpass", "demux mode must be 'onepass' or 'fourpass'");
-    g_onepass = m == "onepass" ? 1 : 0;
+    TORCH_CHECK_VALUE(m == "onepass" || m == "fourpass" || m == "scatter",
+                      "demux mode must be 'fourpass', 'onepass' or 'scatter'");
+    g_demux = m == "onepass" ? kOnepass : m == "scatter" ? kScatterDemux : kFourpass;
   });
   m.def("transmux_tile_bytes", &hlsp2p::dev::transmux_tile_bytes);
   m.def("transmux_launch", &transmux_launch, py::arg("src"), py::arg("src_off"), py::arg("nbytes"), py::arg("enc"),

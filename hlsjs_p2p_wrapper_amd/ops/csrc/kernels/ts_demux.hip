@@ -131,11 +131,7 @@ __global__ __launch_bounds__(64) void ts_psi_kernel(const uint8_t* __restrict__ 
   }
 }
 
-// per-packet meta word: class (2b, 3 = none) | payload start (8b) << 2 | payload len (8b) << 10 | pes (1b) << 18
-__device__ __forceinline__ uint32_t pack_meta(int c, int ps, int len, int pes) {
-  return static_cast<uint32_t>(c & 3) | (static_cast<uint32_t>(ps) << 2) | (static_cast<uint32_t>(len) << 10) |
-         (static_cast<uint32_t>(pes) << 18);
-}
+using demux::pack_meta;
 
 // ---------------------------------------------------------------- 2. scan
 // inclusive wave prefix sum (wave64)
@@ -439,6 +435,15 @@ __global__ __launch_bounds__(kTsThreads) void ts_gather_kernel(
     }
     if (sub < tail) d[head + 4 * body + sub] = s_bytes[s + head + 4 * body + sub];
   }
+}
+
+// The block-prefix step alone (the scatter demux, ts_scatter.hip, runs its own scan).
+hipError_t launch_ts_prefix(const int64_t* blk_prefix, const int32_t* blk_sums, int32_t* blk_pre, int32_t* seg_tot,
+                            int64_t* info, int64_t max_pes, int nseg, hipStream_t stream) {
+  if (nseg <= 0) return hipSuccess;
+  hipLaunchKernelGGL(ts_prefix_kernel, dim3(nseg), dim3(64), 0, stream, blk_prefix, blk_sums, blk_pre, seg_tot, info,
+                     max_pes);
+  return hipGetLastError();
 }
 
 hipError_t launch_ts_demux(const uint8_t* buf, const int64_t* seg_off, const int64_t* seg_len,

@@ -1,5 +1,6 @@
 """Isolated timing of one transmux batch (decrypt + demux) on the MI355X: the fused kernel
-(kernels/transmux_fused.hip) against the split sequence (aes_cbc.hip + ts_demux.hip), plus
+(kernels/transmux_fused.hip) against the split sequence (aes_cbc.hip + ts_demux.hip) and the
+scatter demux (ts_scatter.hip: no plaintext buffer), plus
 the fused kernel's decomposition (HLSP2P_FUSED_DIAG=1: decrypt alone; =2: no payload
 copy-out).  Batches of 1080p 6 Mb/s AES-128 segments (~3 MB), as a bench round delivers them.
 
@@ -22,6 +23,7 @@ def main():
     ap.add_argument("--segs", type=int, default=256)
     ap.add_argument("--iters", type=int, default=10)
     ap.add_argument("--prof", action="store_true", help="also print the fused kernel's per-role timers")
+    ap.add_argument("--modes", default="", help="comma list of modes to time (default: all)")
     ap.add_argument("--flags", default="0", help="HLSP2P_FUSED_FLAGS for the fused runs (A/B experiments)")
     args = ap.parse_args()
     cuda = torch.device("cuda", 0)
@@ -45,10 +47,13 @@ def main():
     def launch():
         return dev.transmux_launch(src, offs, lens, enc, drk, iv, td0, isb, tsdemux.DEFAULT_MAX_PES)
 
-    for name, mode, diag in (("split", "split", None), ("split_onepass", "split1", None), ("fused", "fused", None),
-                             ("fused_decrypt_only", "fused", "1"), ("fused_no_copyout", "fused", "2")):
-        dev.set_transmux_mode("split" if mode == "split1" else mode)
-        dev.set_demux_mode("onepass" if mode == "split1" else "fourpass")
+    ap_modes = (("split", "split", None), ("scatter", "scatter", None), ("split_onepass", "split1", None),
+                ("fused", "fused", None), ("fused_decrypt_only", "fused", "1"), ("fused_no_copyout", "fused", "2"))
+    for name, mode, diag in ap_modes:
+        if args.modes and name not in args.modes.split(","):
+            continue
+        dev.set_transmux_mode("fused" if mode == "fused" else "split")
+        dev.set_demux_mode({"split1": "onepass", "scatter": "scatter"}.get(mode, "fourpass"))
         if diag is None:
             os.environ.pop("HLSP2P_FUSED_DIAG", None)
         else:
