@@ -259,7 +259,8 @@ def main() -> int:
                     os.sched_setaffinity(pr.pid, os.sched_getaffinity(0))
                 except OSError:
                     pass
-        cpu_place = _place(args.cpu_place, local_dev, [os.getpid()] + ([pr.pid for pr in players[1]] if players else []))
+        pids = [os.getpid()] + ([pr.pid for pr in players[1]] if players else [])
+        cpu_place = _place(args.cpu_place, local_dev, pids)
     else:
         device = torch.device("cpu")
         numa_node = None

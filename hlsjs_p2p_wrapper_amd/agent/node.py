@@ -226,6 +226,12 @@ class SwarmNode:
         self._locs: Dict[Tuple[str, Optional[str]], Tuple[int, int, int, int]] = {}
         self._locs_gen = -1
         self._loc_keep: Dict[int, torch.Tensor] = {}  # origin allocations the table points into
+        # native batch locator of fixed-address origins (runtime/locator.cpp): the directories
+        # of every origin registered this registry generation; `_locator_origins` are checked
+        # for injected faults before each batch (faults take the per-request Python path)
+        self._locator = self.rt.SegmentLocator()
+        self._locator_gen = -1
+        self._locator_origins: Dict[int, Any] = {}
         self._tick_scheduled = False
         self._timer = None
         self._pins: List[Tuple[int, np.ndarray]] = []  # (release at launch #, entry ids)
@@ -329,6 +335,8 @@ class SwarmNode:
         if hit is not None:
             return hit[0], hit[1], hit[2], hit[3], None
         origin, path = http.resolve(url)
+        if id(origin) not in self._locator_origins:
+            self._register_locator(origin)
         rng = http.parse_range(headers) if headers else None
         if getattr(origin, "staged_fetch", False):
             size = origin.staged_size(path, rng)
@@ -357,6 +365,40 @@ class SwarmNode:
                 self._locs.clear()
             self._locs[ck] = res
         return res[0], res[1], res[2], res[3], None
+
+    def _register_locator(self, origin: Any) -> None:
+        """Hand a fixed-address origin's segment directories to the native locator (once per
+        origin and registry generation).  Origins without them, with faults configured, or
+        whose host bytes are not pinned (the async H2D path needs pinned memory: the Python
+        path raises for them) stay on the per-request path."""
+        if http.generation() != self._locator_gen:
+            self._locator.clear()
+            self._locator_origins.clear()
+            self._locator_gen = http.generation()
+        self._locator_origins[id(origin)] = origin
+        dirs_fn = getattr(origin, "segment_dirs", None)
+        dirs = dirs_fn() if dirs_fn is not None else None
+        if not dirs:
+            return
+        for d, prefix, suffix, lo, hi, data, offs, lens in dirs:
+            if not data.is_cuda and self.is_cuda and not data.is_pinned():
+                return
+            base = data.data_ptr()
+            self._loc_keep.setdefault(base, data)
+            self._locator.add_dir(d, prefix, suffix, int(lo), int(hi), base, W_ON_DEV if data.is_cuda else 0,
+                                  np.asarray(offs, dtype=np.int64), np.asarray(lens, dtype=np.int64))
+
+    def _locator_usable(self) -> bool:
+        """The native locator may answer this batch: it holds directories of the current
+        registry generation and none of their origins has faults injected since."""
+        if not len(self._locator) or self._locator_gen != http.generation():
+            return False
+        for o in self._locator_origins.values():
+            if getattr(o, "_failures", None) or getattr(o, "_corrupt", None):
+                self._locator.clear()
+                self._locator_origins.clear()
+                return False
+        return True
 
     # ------------------------------------------------------------------ requests
     def request(self, key: Tuple[int, int, int, int], url: str, headers: Optional[Dict[str, str]],
@@ -443,7 +485,24 @@ class SwarmNode:
         xs: Dict[int, _WantX] = {}
         bad: List[Tuple[int, int]] = []
         resolve = self._resolve
+        done = None
+        if self._locator_usable():  # one native call for the fixed-address origins' URLs
+            sel_urls = urls if miss is None else [urls[i] for i in idx]
+            s_, p_, b_, f_, done, found = self._locator.resolve(sel_urls if isinstance(sel_urls, list)
+                                                                else list(sel_urls))
+            if headers is not None:  # byte ranges take the general path
+                done &= np.fromiter((not h or ("Range" not in h and "range" not in h)
+                                     for h in (headers if miss is None else [headers[i] for i in idx])),
+                                    dtype=bool, count=m)
+            sizes[done] = s_[done]
+            ptrs[done] = p_[done]
+            bases[done] = b_[done]
+            flags[done] |= f_[done]
+            if done.all():
+                idx = ()
         for j, i in enumerate(idx):
+            if done is not None and done[j]:
+                continue
             try:
                 sizes[j], ptrs[j], bases[j], wf, x = resolve(urls[i], headers[i] if headers is not None else None)
             except http.HttpError as e:

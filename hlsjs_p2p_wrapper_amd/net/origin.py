@@ -285,6 +285,23 @@ class SyntheticHlsOrigin:
         i = sn % self.pool_size
         return pool.data, pool.offsets[i], pool.lengths[i], pool.crcs[i]
 
+    def segment_dirs(self) -> Optional[List[Tuple[str, str, str, int, int, torch.Tensor, List[int], List[int]]]]:
+        """Where every segment's bytes live, per URL directory, for the swarm node's native
+        batch locator (``runtime/locator.cpp``): ``(directory URL, name prefix, name suffix,
+        first sn, end sn, pool tensor, slot offsets, slot lengths)``; the slot of ``sn`` is
+        ``sn % pool_size``.  None when the bytes are not fixed per URL: a live window, or
+        injected failures / corruption (those go through :meth:`locate` per request)."""
+        if self.live or self._failures or self._corrupt or self.num_segments is None:
+            return None
+        out = []
+        trees = [""] + [f"{c}/" for c in "abcdefgh"[:self.redundant]]
+        for level, pool in enumerate(self.pools):
+            offs, lens = list(pool.offsets[:self.pool_size]), list(pool.lengths[:self.pool_size])
+            for t in trees:
+                out.append((f"{self.base_url}{t}r{level}/", "seg", ".ts", self.start_sn,
+                            self.start_sn + self.num_segments, pool.data, offs, lens))
+        return out
+
     def locate(self, path: str, url: str = "", rng=None) -> Optional[Tuple[torch.Tensor, int, int]]:
         """``(pinned tensor, offset, length)`` of a segment's (ranged) bytes, resolved once
         when the node creates the want: a VOD origin's pools never change, so the CDN phase

@@ -16,6 +16,7 @@
 
 #include "aes_host.hpp"
 #include "crc_host.hpp"
+#include "locator.hpp"
 #include "planner.hpp"
 #include "shm_control.hpp"
 #include "store.hpp"
@@ -544,6 +545,50 @@ PYBIND11_MODULE(_runtime, m) {
 
   // ------------------------------------------------------------------ want table
   // (agent/node.py: the rank's per-request state as rows; see wants.hpp)
+  py::class_<SegmentLocator>(m, "SegmentLocator")
+      .def(py::init<>())
+      .def("add_dir",
+           [](SegmentLocator& l, const std::string& dir, const std::string& prefix, const std::string& suffix,
+              int64_t sn_lo, int64_t sn_hi, int64_t base, int64_t flags, Arr<int64_t> off, Arr<int64_t> len) {
+             if (off.size() != len.size()) throw std::invalid_argument("add_dir: off / len sizes differ");
+             SegmentLocator::Dir d;
+             d.prefix = prefix;
+             d.suffix = suffix;
+             d.sn_lo = sn_lo;
+             d.sn_hi = sn_hi;
+             d.base = base;
+             d.flags = flags;
+             d.off.assign(off.data(), off.data() + off.size());
+             d.len.assign(len.data(), len.data() + len.size());
+             l.add_dir(dir, std::move(d));
+           },
+           py::arg("dir"), py::arg("prefix"), py::arg("suffix"), py::arg("sn_lo"), py::arg("sn_hi"), py::arg("base"),
+           py::arg("flags"), py::arg("off"), py::arg("len"))
+      .def("resolve",
+           [](const SegmentLocator& l, const py::list& urls) {
+             // string views into the list's str objects (their UTF-8 buffers live as long as
+             // the list does, which outlives this call)
+             const size_t n = urls.size();
+             std::vector<std::string_view> v(n);
+             for (size_t i = 0; i < n; ++i) {
+               Py_ssize_t len = 0;
+               const char* s = PyUnicode_AsUTF8AndSize(urls[i].ptr(), &len);
+               if (s == nullptr) throw py::error_already_set();
+               v[i] = std::string_view(s, static_cast<size_t>(len));
+             }
+             py::array_t<int64_t> size(n), ptr(n), base(n), flags(n);
+             py::array_t<uint8_t> ok(n);
+             int64_t found;
+             {
+               py::gil_scoped_release nogil;
+               found = l.resolve(v, size.mutable_data(), ptr.mutable_data(), base.mutable_data(),
+                                 flags.mutable_data(), ok.mutable_data());
+             }
+             return py::make_tuple(size, ptr, base, flags, ok.attr("astype")("bool"), found);
+           })
+      .def("clear", &SegmentLocator::clear)
+      .def("__len__", &SegmentLocator::size);
+
   py::class_<WantTable>(m, "WantTable")
       .def(py::init<>())
       .def("__len__", &WantTable::size)
