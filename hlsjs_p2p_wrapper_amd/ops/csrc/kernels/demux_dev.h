@@ -22,28 +22,6 @@ __device__ __forceinline__ uint32_t pack_meta(int c, int ps, int len, int pes) {
          (static_cast<uint32_t>(pes) << 18);
 }
 
-// The scatter demux's block rule, shared by the bulk decrypt's epilogue (aes_cbc.hip) and the
-// edge kernel (ts_scatter.hip).  Block b (16 bytes at segment offset 16 b) starts in packet
-// p at byte y0; the packet's place entry pl = (bias, lo | hi << 16) sends its payload bytes
-// y in [lo, hi) to ES offset bias + y.  hb = bytes until the block's destination is dword
-// aligned.  FAST = the whole block is payload and the run goes on for hb more bytes, which
-// the block borrows from its successor (next_ok: that block is at hand).
-struct ScatterBlock {
-  int p, y0, bias, lo, hi, hb, fast;
-};
-__device__ __forceinline__ ScatterBlock scatter_block(int64_t b, uint2 pl, int64_t nblk, bool next_ok) {
-  ScatterBlock r;
-  const int x0 = static_cast<int>(16 * b);
-  r.p = x0 / kPkt;
-  r.y0 = x0 - kPkt * r.p;
-  r.bias = static_cast<int>(pl.x);
-  r.lo = static_cast<int>(pl.y & 0xffff);
-  r.hi = static_cast<int>(pl.y >> 16);
-  r.hb = (-(r.bias + r.y0)) & 3;
-  r.fast = b < nblk && r.y0 >= r.lo && r.y0 + 16 + r.hb <= r.hi && (r.hb == 0 || next_ok);
-  return r;
-}
-
 __device__ __forceinline__ int64_t pts5(uint32_t b0, uint32_t b1, uint32_t b2, uint32_t b3, uint32_t b4) {
   return (int64_t((b0 >> 1) & 0x07) << 30) | (int64_t(b1) << 22) | (int64_t(b2 >> 1) << 15) | (int64_t(b3) << 7) |
          int64_t(b4 >> 1);

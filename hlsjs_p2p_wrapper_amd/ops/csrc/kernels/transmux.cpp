@@ -295,7 +295,7 @@ py::tuple transmux_launch(Tensor src, I64 src_off, I64 nbytes, py::array_t<uint8
     return transmux_launch_fused(src, so, nb, en, drk.data(), iv.data(), B, td0, isb, max_pes, device, st);
 
   // ---- plans: AES over the encrypted segments, demux per group
-  std::vector<int64_t> a_so, a_do, a_bp{0}, a_cp{0}, a_hp{0};
+  std::vector<int64_t> a_so, a_do, a_bp{0}, a_cp{0}, a_sp{0}, a_hp{0};
   std::vector<uint32_t> a_drk;
   std::vector<uint8_t> a_iv;
   DemuxPlan pe, pc;
@@ -312,6 +312,8 @@ py::tuple transmux_launch(Tensor src, I64 src_off, I64 nbytes, py::array_t<uint8
       const int64_t blocks = nb[i] / 16;
       a_bp.push_back(a_bp.back() + blocks);
       a_cp.push_back(a_cp.back() + (blocks + chunk - 1) / chunk);
+      constexpr int64_t sc = hlsp2p::dev::kScatterChunkBlocks;  // scatter decrypt chunks
+      a_sp.push_back(a_sp.back() + (blocks + sc - 1) / sc);
       const int64_t groups = (nb[i] / kPacket + hlsp2p::dev::kScatterGroupPackets - 1) /
                              hlsp2p::dev::kScatterGroupPackets;  // scatter demux header chunks
       a_hp.push_back(a_hp.back() + (groups + hlsp2p::dev::kScatterChunkGroups - 1) / hlsp2p::dev::kScatterChunkGroups);
@@ -336,7 +338,7 @@ py::tuple transmux_launch(Tensor src, I64 src_off, I64 nbytes, py::array_t<uint8
 
   // ---- every descriptor of the batch in one staging block, one H2D
   Desc desc;
-  int64_t d_so = -1, d_do = -1, d_bp = -1, d_cp = -1, d_drk = -1, d_iv = -1, d_hp = -1, d_pb = -1, d_ps = -1;
+  int64_t d_so = -1, d_do = -1, d_bp = -1, d_cp = -1, d_drk = -1, d_iv = -1, d_hp = -1, d_pb = -1, d_ps = -1, d_sp = -1;
   if (ne) {
     d_so = desc.add(a_so);
     d_do = desc.add(a_do);
@@ -349,6 +351,7 @@ py::tuple transmux_launch(Tensor src, I64 src_off, I64 nbytes, py::array_t<uint8
     pe.d_eo = desc.add(pe.es_off);
     pe.d_ec = desc.add(pe.es_cap);
     if (scatter) {
+      d_sp = desc.add(a_sp);
       d_hp = desc.add(a_hp);
       d_pb = desc.add(pkt_base);
       d_ps = desc.add(pkt_slots);
@@ -366,12 +369,9 @@ py::tuple transmux_launch(Tensor src, I64 src_off, I64 nbytes, py::array_t<uint8
   // ---- host results block: info rows (enc group, then clear group) | enc plaintext lengths
   Tensor host = torch::empty({(ne + nc) * kInfo + ne + 1}, torch::TensorOptions().dtype(torch::kInt64).pinned_memory(true));
   Tensor dec, out_len;
-  if (ne) {
-    out_len = torch::empty({ne}, dev_opts.dtype(torch::kInt64));
-    // the plaintext (split) or, for the scatter demux, the sparse side buffer of edge blocks
-    dec = torch::empty({dec_pos + kAlign}, dev_opts.dtype(torch::kUInt8));
-  }
+  if (ne) out_len = torch::empty({ne}, dev_opts.dtype(torch::kInt64));
   if (ne && !scatter) {
+    dec = torch::empty({dec_pos + kAlign}, dev_opts.dtype(torch::kUInt8));
     hip_ok(hlsp2p::dev::launch_aes128_cbc_decrypt(
                static_cast<const uint8_t*>(src.data_ptr()), static_cast<uint8_t*>(dec.data_ptr()),
                desc.at<int64_t>(d_so), desc.at<int64_t>(d_do), desc.at<int64_t>(d_bp), desc.at<int64_t>(d_cp),
@@ -400,11 +400,12 @@ py::tuple transmux_launch(Tensor src, I64 src_off, I64 nbytes, py::array_t<uint8
       Tensor pts = torch::empty({nb_blocks * 256 * 2}, dev_opts.dtype(torch::kInt64));
       Tensor aux = torch::empty({nb_blocks * 12 + n * 7}, dev_opts.dtype(torch::kInt32));
       Tensor place = torch::empty({nb_blocks * 256}, dev_opts.dtype(torch::kInt64));
+      Tensor seam = torch::empty({nb_blocks * 256}, dev_opts.dtype(torch::kInt64));  // 2 words per packet
       hlsp2p::dev::ScatterArgs sa{};
       sa.src = static_cast<const uint8_t*>(src.data_ptr());
       sa.src_off = desc.at<int64_t>(d_so);
       sa.aes_blk = desc.at<int64_t>(d_bp);
-      sa.aes_chunks = desc.at<int64_t>(d_cp);
+      sa.aes_chunks = desc.at<int64_t>(d_sp);
       sa.hdr_chunks = desc.at<int64_t>(d_hp);
       sa.drk = desc.at<uint32_t>(d_drk);
       sa.ivw = desc.at<uint32_t>(d_iv);
@@ -418,8 +419,7 @@ py::tuple transmux_launch(Tensor src, I64 src_off, I64 nbytes, py::array_t<uint8
       sa.pts_dts = pts.data_ptr<int64_t>();
       sa.aux = aux.data_ptr<int32_t>();
       sa.place = reinterpret_cast<uint2*>(place.data_ptr<int64_t>());
-      sa.side = static_cast<uint8_t*>(dec.data_ptr());
-      sa.side_off = desc.at<int64_t>(d_do);
+      sa.seam = reinterpret_cast<uint32_t*>(seam.data_ptr<int64_t>());
       sa.es = es.data_ptr<uint8_t>();
       sa.es_off = desc.at<int64_t>(p.d_eo);
       sa.pes = pes.data_ptr<int64_t>();
@@ -428,10 +428,10 @@ py::tuple transmux_launch(Tensor src, I64 src_off, I64 nbytes, py::array_t<uint8
       sa.max_pes = max_pes;
       sa.nseg = static_cast<int>(n);
       sa.total_blocks = p.total_blocks;
-      sa.aes_total_chunks = a_cp.back();
+      sa.aes_total_chunks = a_sp.back();
       sa.hdr_total_chunks = a_hp.back();
       hip_ok(hlsp2p::dev::launch_ts_scatter(sa, decrypt_cus(device), st), "ts_scatter");
-      keep.append(py::make_tuple(hdr, meta, pts, aux, place));
+      keep.append(py::make_tuple(hdr, meta, pts, aux, place, seam));
     } else if (use_onepass()) {
       // zeroed: look-back granules [blocks x 3] | ticket + timeout; -1: last PES per block [blocks x 6]
       Tensor zw = torch::empty({nb_blocks * 3 + 1}, dev_opts.dtype(torch::kInt64));

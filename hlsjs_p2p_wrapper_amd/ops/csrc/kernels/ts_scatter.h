@@ -11,7 +11,7 @@ struct ScatterArgs {
   const uint8_t* src;           // ciphertext segments (16-byte aligned)
   const int64_t* src_off;       // [nseg]
   const int64_t* aes_blk;       // [nseg + 1] 16-byte blocks per segment, exclusive prefix
-  const int64_t* aes_chunks;    // [nseg + 1] bulk-decrypt chunks (aes_chunk_blocks() blocks), prefix
+  const int64_t* aes_chunks;    // [nseg + 1] scatter-decrypt chunks (kScatterChunkBlocks blocks), prefix
   const int64_t* hdr_chunks;    // [nseg + 1] header chunks (64 groups of 4 packets), prefix
   const uint32_t* drk;          // [nseg][44] little-endian equivalent-inverse-cipher round keys
   const uint32_t* ivw;          // [nseg][4]
@@ -25,8 +25,7 @@ struct ScatterArgs {
   int64_t* pts_dts;             // [blocks * 256 * 2]
   int32_t* aux;                 // [blocks * 12 + nseg * 7]: block sums | block prefixes | segment totals
   uint2* place;                 // [blocks * 256] (ES bias, payload range) per packet
-  uint8_t* side;                // sparse plaintext of the edge blocks (bulk decrypt -> edge kernel)
-  const int64_t* side_off;      // [nseg] segment offset in `side` (>= the segment's bytes each)
+  uint32_t* seam;               // [blocks * 256][2] head / tail seam bytes per packet
   uint8_t* es;                  // ES buffer, [video | audio | id3] packed per segment at es_off
   const int64_t* es_off;        // [nseg]
   int64_t* pes;                 // [nseg][3][max_pes][3]
@@ -39,9 +38,9 @@ struct ScatterArgs {
   int64_t hdr_total_chunks;
 };
 
-// blocks one wave of the bulk decrypt covers per iteration (aes_cbc.hip: 64 lanes x kBlk chains);
-// the iteration's last block has no successor at hand for the scatter epilogue
-constexpr int kScatterIterBlocks = 256;
+// blocks one wave of the scatter decrypt owns per iteration (aes_cbc.hip: 64 lanes x kBlk
+// chains decrypt 256; the last is a lookahead lending its first bytes to the 255th)
+constexpr int kScatterChunkBlocks = 255;
 // header chunk = 64 lanes x one 4-packet group (752 bytes = 47 AES blocks) each
 constexpr int kScatterGroupPackets = 4;
 constexpr int kScatterChunkGroups = 64;

@@ -22,7 +22,9 @@
 //                         split gather), PES table rows, first / last PTS; the packet's
 //                         (ES bias, payload range) entry.
 //   6. aes128_cbc_decrypt_kernel<true> — (aes_cbc.hip) the bulk decrypt at full rate; its
-//                         epilogue stores payload bytes to es + bias + offset in packet.
+//                         epilogue stores every whole aligned ES dword of payload (dwordx4 for
+//                         a block inside a payload) and leaves each run's <= 3 + 3 seam bytes.
+//   7. tsx_seam_kernel  — one lane per packet: the seam bytes (shared ES dwords) as bytes.
 //
 // HBM traffic per segment: the header pass touches one 128 B line per packet (~0.7 of the
 // segment), the bulk decrypt reads the ciphertext once and writes the ES once — against
@@ -38,13 +40,12 @@ namespace dev {
 
 hipError_t launch_ts_prefix(const int64_t* blk_prefix, const int32_t* blk_sums, int32_t* blk_pre, int32_t* seg_tot,
                             int64_t* info, int64_t max_pes, int nseg, hipStream_t stream);
-hipError_t launch_aes128_cbc_scatter(const uint8_t* src, uint8_t* side, const int64_t* src_off,
-                                     const int64_t* side_off, const int64_t* blk_prefix,
+hipError_t launch_aes128_cbc_scatter(const uint8_t* src, const int64_t* src_off, const int64_t* blk_prefix,
                                      const int64_t* chunk_prefix, const uint32_t* drk, const uint32_t* ivw,
                                      const uint32_t* tdl, const uint8_t* isb, const uint2* place,
                                      const int64_t* pkt_base, const int64_t* pkt_slots, uint8_t* es,
-                                     const int64_t* es_off, int nseg, int64_t total_chunks, int num_cu,
-                                     hipStream_t stream);
+                                     const int64_t* es_off, uint32_t* seam, int nseg, int64_t total_chunks,
+                                     int num_cu, hipStream_t stream);
 
 namespace {
 
@@ -453,73 +454,24 @@ __global__ __launch_bounds__(kThreads) void tsx_place_kernel(ScatterArgs a) {
   a.place[gpk] = out;
 }
 
-// ---------------------------------------------------------------- 7. edges
-// One lane per packet: the payload bytes the bulk decrypt could not store as whole aligned
-// dwords -- those of non-fast blocks (packet boundaries, headers, the decrypt iteration's last
-// block) minus the head a fast predecessor covered, and the head bytes of a fast block whose
-// predecessor did not cover them -- copied from the side buffer, where the decrypt left those
-// blocks' plaintext.  The fast rule is demux::scatter_block, as in the decrypt's epilogue;
-// inside one packet it reduces to arithmetic on the block offset (the alignment `hb` is the
-// packet's), so only the 2-4 edge blocks of a packet touch memory: one 16-byte load each,
-// then head bytes, aligned dwords, tail bytes.
-__device__ __forceinline__ bool next_at_hand(int64_t b, int64_t nb) {
-  return (b % kScatterIterBlocks) != kScatterIterBlocks - 1 && b + 1 < nb;
-}
-__device__ __forceinline__ uint32_t word_at(const uint4& v, int i) {
-  return i == 0 ? v.x : i == 1 ? v.y : i == 2 ? v.z : i == 3 ? v.w : 0u;
-}
-// bytes [off, off + n) of the 16-byte block v to dst (any alignment)
-__device__ __forceinline__ void copy_run(const uint4& v, int off, int n, uint8_t* dst) {
-  const int head = min(static_cast<int>((0u - static_cast<uint32_t>(reinterpret_cast<uintptr_t>(dst))) & 3u), n);
-  for (int i = 0; i < head; ++i) dst[i] = static_cast<uint8_t>(word_at(v, (off + i) >> 2) >> (8 * ((off + i) & 3)));
-  const int body = (n - head) >> 2;
-  uint32_t* dw = reinterpret_cast<uint32_t*>(dst + head);
-  for (int k = 0; k < body; ++k) {
-    const int u = off + head + 4 * k;
-    dw[k] = __builtin_amdgcn_alignbyte(word_at(v, (u >> 2) + 1), word_at(v, u >> 2), static_cast<uint32_t>(u & 3));
-  }
-  for (int i = head + 4 * body; i < n; ++i)
-    dst[i] = static_cast<uint8_t>(word_at(v, (off + i) >> 2) >> (8 * ((off + i) & 3)));
-}
-
-__global__ __launch_bounds__(kThreads) void tsx_edge_kernel(ScatterArgs a) {
+// ---------------------------------------------------------------- 7. seams
+// One lane per packet: its payload run's head bytes (until its first aligned ES dword) and
+// tail bytes (after its last full dword), <= 3 each, share an ES dword with the neighbouring
+// same-class runs; the bulk decrypt left them in seam[2 * pkt + {0, 1}] (low bytes first).
+__global__ __launch_bounds__(kThreads) void tsx_seam_kernel(ScatterArgs a) {
   const int64_t gblk = blockIdx.x;
   const int seg = find_seg_wave(a.blk_prefix, a.nseg, gblk);
-  const int tid = threadIdx.x;
-  const int64_t gpk = gblk * kThreads + tid;
-  const int64_t pk = (gblk - a.blk_prefix[seg]) * kThreads + tid;
+  const int64_t gpk = gblk * kThreads + threadIdx.x;
   const uint2 pl = a.place[gpk];
   const int lo = static_cast<int>(pl.y & 0xffff), hi = static_cast<int>(pl.y >> 16);
   if (hi <= lo) return;
-  const int64_t nb = a.aes_blk[seg + 1] - a.aes_blk[seg];
-  const int64_t P = kPkt * pk;
-  const int64_t A = P + lo, E = P + hi;  // the payload's segment bytes [A, E)
-  const uint4* side = reinterpret_cast<const uint4*>(a.side + a.side_off[seg]);
-  uint8_t* es = a.es + a.es_off[seg] + static_cast<int32_t>(pl.x) - P;  // ES address of segment byte 0
-  const int64_t fb = A / 16, lb = (E - 1) / 16;
-  const int hbp = (-(static_cast<int>(pl.x) + static_cast<int>(16 * fb - P))) & 3;  // blocks of this packet
-  // the first block may start in the previous packet (then it is not fast); so may its predecessor
-  bool prev_fast = false;
-  int prev_hb = 0;
-  if (fb > 0) {
-    const uint2 e = 16 * (fb - 1) >= P ? pl : (pk > 0 ? a.place[gpk - 1] : make_uint2(0, 0));
-    const demux::ScatterBlock pb = demux::scatter_block(fb - 1, e, nb, next_at_hand(fb - 1, nb));
-    prev_fast = pb.fast;
-    prev_hb = pb.hb;
-  }
-  for (int64_t b = fb; b <= lb; ++b) {
-    const int y0 = static_cast<int>(16 * b - P);  // < 0: the block starts in the previous packet
-    const bool fast = y0 >= lo && y0 + 16 + hbp <= hi && (hbp == 0 || next_at_hand(b, nb));
-    int64_t s = 16 * b > A ? 16 * b : A, e = 16 * b + 16 < E ? 16 * b + 16 : E;
-    if (fast) {
-      e = (!prev_fast && hbp) ? 16 * b + hbp : s;  // only the uncovered head
-    } else if (prev_fast && s < 16 * b + prev_hb) {
-      s = 16 * b + prev_hb;
-    }
-    if (s < e) copy_run(side[b], static_cast<int>(s - 16 * b), static_cast<int>(e - s), es + s);
-    prev_fast = fast;
-    prev_hb = hbp;
-  }
+  uint8_t* es = a.es + a.es_off[seg];
+  const int d = static_cast<int>(pl.x) + lo;  // ES offset of the run's first byte
+  const int hh = (-d) & 3, h = hh < hi - lo ? hh : hi - lo;
+  const int t = h + ((hi - lo - h) & ~3);  // run offset of the tail
+  const uint32_t head = h ? a.seam[2 * gpk] : 0u, tail = t < hi - lo ? a.seam[2 * gpk + 1] : 0u;
+  for (int i = 0; i < h; ++i) es[d + i] = static_cast<uint8_t>(head >> (8 * i));
+  for (int i = 0; i < hi - lo - t; ++i) es[d + t + i] = static_cast<uint8_t>(tail >> (8 * i));
 }
 
 }  // namespace
@@ -551,11 +503,11 @@ hipError_t launch_ts_scatter(const ScatterArgs& a, int num_cu, hipStream_t strea
   hipLaunchKernelGGL(tsx_place_kernel, dim3(static_cast<unsigned>(a.total_blocks)), dim3(kThreads), 0, stream, a);
   e = hipGetLastError();
   if (e != hipSuccess) return e;
-  e = launch_aes128_cbc_scatter(a.src, a.side, a.src_off, a.side_off, a.aes_blk, a.aes_chunks, a.drk, a.ivw, a.tdl, a.isb, a.place,
-                                   a.pkt_base, a.pkt_slots, a.es, a.es_off, a.nseg, a.aes_total_chunks, num_cu,
-                                   stream);
+  e = launch_aes128_cbc_scatter(a.src, a.src_off, a.aes_blk, a.aes_chunks, a.drk, a.ivw, a.tdl, a.isb, a.place,
+                                   a.pkt_base, a.pkt_slots, a.es, a.es_off, a.seam, a.nseg, a.aes_total_chunks,
+                                   num_cu, stream);
   if (e != hipSuccess) return e;
-  hipLaunchKernelGGL(tsx_edge_kernel, dim3(static_cast<unsigned>(a.total_blocks)), dim3(kThreads), 0, stream, a);
+  hipLaunchKernelGGL(tsx_seam_kernel, dim3(static_cast<unsigned>(a.total_blocks)), dim3(kThreads), 0, stream, a);
   return hipGetLastError();
 }
 
