@@ -144,7 +144,19 @@ int cus(int device) {
 // a full-chip persistent grid would hold RCCL back for the whole batch.
 int g_cu_reserve = 0;
 
-int decrypt_cus(int device) { return std::max(8, cus(device) - g_cu_reserve); }
+// HLSP2P_DECRYPT_CUS: at most this many CUs for the decrypt grid -- the rest stay free for the
+// memory-bound kernels of the other streams (ingest copies, CRC, the previous batch's demux):
+// one 160 KiB decrypt workgroup fills a CU's LDS, so nothing that needs LDS co-resides with it
+int g_decrypt_cap = -1;
+int decrypt_cus(int device) {
+  if (g_decrypt_cap < 0) {
+    const char* v = std::getenv("HLSP2P_DECRYPT_CUS");
+    g_decrypt_cap = v != nullptr ? std::max(0, std::atoi(v)) : 0;
+  }
+  int n = cus(device) - g_cu_reserve;
+  if (g_decrypt_cap > 0) n = std::min(n, g_decrypt_cap);
+  return std::max(8, n);
+}
 
 void hip_ok(hipError_t e, const char* what) { TORCH_CHECK(e == hipSuccess, what, " failed: ", hipGetErrorString(e)); }
 
