@@ -23,12 +23,15 @@ def main():
     ap.add_argument("--segs", type=int, default=256)
     ap.add_argument("--iters", type=int, default=10)
     ap.add_argument("--prof", action="store_true", help="also print the fused kernel's per-role timers")
+    ap.add_argument("--pool", type=int, default=64,
+                    help="distinct segments (the batch cycles through them): 64 x 3 MB fits the 256 MB "
+                         "Infinity Cache (MALL), 256 does not -- as in the pipeline, where every segment is new")
     ap.add_argument("--modes", default="", help="comma list of modes to time (default: all)")
     ap.add_argument("--flags", default="0", help="HLSP2P_FUSED_FLAGS for the fused runs (A/B experiments)")
     args = ap.parse_args()
     cuda = torch.device("cuda", 0)
     dev = device()
-    pool_n = min(args.segs, 64)
+    pool_n = min(args.segs, args.pool)
     origin = SyntheticHlsOrigin("http://cdn.tb/", renditions=PRESET_1080P_6M, num_segments=pool_n, encrypted=True,
                                 pool_size=pool_n, pin_memory=True, seed=5, register=False)
     pool = origin.pools[0]
