@@ -566,8 +566,8 @@ PYBIND11_MODULE(_runtime, m) {
            py::arg("flags"), py::arg("off"), py::arg("len"))
       .def("resolve",
            [](const SegmentLocator& l, const py::list& urls) {
-             // string views into the list's str objects (their UTF-8 buffers live as long as
-             // the list does, which outlives this call)
+             // string views into the list's str objects (the GIL stays held: no other thread
+             // can drop an item of the list while the views are in use)
              const size_t n = urls.size();
              std::vector<std::string_view> v(n);
              for (size_t i = 0; i < n; ++i) {
@@ -578,12 +578,8 @@ PYBIND11_MODULE(_runtime, m) {
              }
              py::array_t<int64_t> size(n), ptr(n), base(n), flags(n);
              py::array_t<uint8_t> ok(n);
-             int64_t found;
-             {
-               py::gil_scoped_release nogil;
-               found = l.resolve(v, size.mutable_data(), ptr.mutable_data(), base.mutable_data(),
-                                 flags.mutable_data(), ok.mutable_data());
-             }
+             const int64_t found = l.resolve(v, size.mutable_data(), ptr.mutable_data(), base.mutable_data(),
+                                             flags.mutable_data(), ok.mutable_data());
              return py::make_tuple(size, ptr, base, flags, ok.attr("astype")("bool"), found);
            })
       .def("clear", &SegmentLocator::clear)
