@@ -80,10 +80,10 @@ def parse():
     p.add_argument("--warmup", type=int, default=5)
     p.add_argument("--config", default="1080p6m", choices=sorted(CONFIGS))
     p.add_argument("--inflight", type=int, default=None,
-                   help="fragments in flight per player (per step); default 128 (64 for live configs, which "
-                        "the channel paces): bigger steps amortise the per-step device and host costs -- 128 "
-                        "gave +20 %% over 64 on the HBM-origin probe, the PCIe-bound headline is flat "
-                        "(profiles/r3_inflight)")
+                   help="fragments in flight per player (per step); default 64 on one GPU and for live "
+                        "configs, 128 with peers (N > 1) or --ingest hbm: bigger steps amortise the per-step "
+                        "device and host costs -- +10-20 %% on the device-bound HBM-origin probe, flat on the "
+                        "PCIe-bound one-GPU headline (profiles/r3_inflight)")
     p.add_argument("--pool", type=int, default=64, help="distinct packaged segments per rendition")
     p.add_argument("--cache-gb", type=float, default=None,
                    help="segment-cache arena per GPU (default 32 GB of the MI355X's 288 GB HBM; 8 GB of host "
@@ -241,7 +241,12 @@ def _spawn_players(W, world, rank, origin_kwargs, hls_config, p2p_base, n_segmen
 def main() -> int:
     args = parse()
     if args.inflight is None:
-        args.inflight = 64 if args.config in LIVE else 128
+        # one GPU is PCIe-bound (bigger steps buy nothing there, and a short timed window's edges
+        # weigh less with smaller ones); with peers each GPU moves far more segments per second
+        # through the device, where bigger steps amortise the per-step costs (+10-20 % on the
+        # device-bound HBM-origin probe, profiles/r3_inflight)
+        multi = int(os.environ.get("WORLD_SIZE", "1")) > 1 or args.ingest == "hbm"
+        args.inflight = 128 if (multi and args.config not in LIVE) else 64
     if args.cache_gb is None:
         # device_count() does not initialise HIP: the fleet players are spawned before the rank opens the GPU
         args.cache_gb = 8.0 if (args.cpu or torch.cuda.device_count() == 0) else 32.0
