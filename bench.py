@@ -80,14 +80,12 @@ def parse():
     p.add_argument("--warmup", type=int, default=5)
     p.add_argument("--config", default="1080p6m", choices=sorted(CONFIGS))
     p.add_argument("--inflight", type=int, default=None,
-                   help="fragments in flight per player (per step); default 64 on one GPU and for live "
-                        "configs, 128 with peers (N > 1) or --ingest hbm: bigger steps amortise the per-step "
-                        "device and host costs -- +10-20 %% on the device-bound HBM-origin probe, flat on the "
-                        "PCIe-bound one-GPU headline (profiles/r3_inflight)")
+                   help="fragments in flight per player (per step), default 64; 128 amortises the per-step "
+                        "device and host costs (+10-20 %% on the device-bound HBM-origin probe, flat on the "
+                        "PCIe-bound headline, profiles/r3_inflight) but is not validated with peers yet")
     p.add_argument("--pool", type=int, default=64, help="distinct packaged segments per rendition")
     p.add_argument("--cache-gb", type=float, default=None,
-                   help="segment-cache arena per GPU (default 32 GB of the MI355X's 288 GB HBM; 8 GB of host "
-                        "memory for CPU runs)")
+                   help="segment-cache arena per GPU (default 8 GB)")
     p.add_argument("--no-dedup", action="store_true", help="disable CDN de-duplication (seeding)")
     p.add_argument("--cpu", action="store_true", help="CPU rehearsal (gloo, no GPU)")
     p.add_argument("--dist-backend", default="auto", choices=["auto", "nccl", "gloo", "ipc"],
@@ -241,15 +239,12 @@ def _spawn_players(W, world, rank, origin_kwargs, hls_config, p2p_base, n_segmen
 def main() -> int:
     args = parse()
     if args.inflight is None:
-        # one GPU is PCIe-bound (bigger steps buy nothing there, and a short timed window's edges
-        # weigh less with smaller ones); with peers each GPU moves far more segments per second
-        # through the device, where bigger steps amortise the per-step costs (+10-20 % on the
-        # device-bound HBM-origin probe, profiles/r3_inflight)
-        multi = int(os.environ.get("WORLD_SIZE", "1")) > 1 or args.ingest == "hbm"
-        args.inflight = 128 if (multi and args.config not in LIVE) else 64
+        # 64: the setting every N > 1 path (RCCL, HIP-IPC rehearsal) was validated with.  The
+        # device-bound HBM-origin probe gains 10-20 % at 128 (profiles/r3_inflight), but a 2-rank
+        # HIP-IPC rehearsal at 128 faulted on the device (open item), so bigger steps stay opt-in
+        args.inflight = 64
     if args.cache_gb is None:
-        # device_count() does not initialise HIP: the fleet players are spawned before the rank opens the GPU
-        args.cache_gb = 8.0 if (args.cpu or torch.cuda.device_count() == 0) else 32.0
+        args.cache_gb = 8.0
     if args.config in LIVE and args.players < 1:
         raise SystemExit("live configs run in fleet mode: --players >= 1")
     if args.sync_steps and args.players:

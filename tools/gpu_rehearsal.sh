@@ -13,7 +13,7 @@ mkdir -p $O
 timeout -k 10 400 python -u -m pytest tests/test_multirank_gpu.py -x -v --timeout 300 --timeout-method thread > $O/test.log 2>&1
 for N in 2 4; do
   timeout -k 10 300 python -m torch.distributed.run --nnodes=1 --nproc-per-node $N --master-addr 127.0.0.1 \
-    --master-port $((29840 + N)) bench.py --gpus $N --steps 20 --warmup 4 --dist-backend $PLANE --cache-gb 12 \
+    --master-port $((29840 + N)) bench.py --gpus $N --steps 20 --warmup 4 --dist-backend $PLANE --cache-gb 4 \
     --players $((8 / N)) --verbose "$@" > $O/n${N}_${PLANE}.log 2>&1
   grep '^{' $O/n${N}_${PLANE}.log
 done
