@@ -318,6 +318,11 @@ def main() -> int:
         seg = max(max(pool.lengths) for pool in origin.pools)
         per_round = (world - 1) * K * max(1, W) * (seg + 512) + (1 << 20)
         os.environ.setdefault("HLSP2P_IPC_OUTBOX_BYTES", str(per_round))
+        if args.inflight > 64:
+            # host-side packing waits instead of interprocess events: at 128 in flight the event
+            # mode faulted on the device once, the host-wait mode ran clean
+            # (profiles/r3_validation/NOTES.md); events stay on at the validated 64
+            os.environ.setdefault("HLSP2P_IPC_EVENTS", "0")
     node = node_for_config(p2p_config)
     if W:
         return _fleet(args, world, rank, device, use_gpu, node, origin, players, desc, encrypted, seg_dur,
