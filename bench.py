@@ -452,15 +452,19 @@ def main() -> int:
     d_p2p = node.stats["p2p"] - s0["p2p"]
     d_segs = sum(node.stats[k] - s0[k] for k in ("cdn_segments", "p2p_segments"))
     vals = np.array([done, d_cdn, d_p2p, int(elapsed * 1e9), counters["errors"], d_segs], dtype=np.int64)
+    per = _per_rank(node, pipe, s0, dict(node.stats), elapsed, args.steps, K)
     if world > 1:
         parts = node.comm.allgather_control(vals)
         tot = np.sum(np.stack(parts), axis=0)
         max_ns = max(int(p[3]) for p in parts)
+        per_parts = node.comm.allgather_control(per)
     else:
-        tot, max_ns = vals, int(vals[3])
+        tot, max_ns, per_parts = vals, int(vals[3]), [per]
     max_s = max_ns / 1e9
     result = _result(args, world, tot, max_s, origin, K, desc, encrypted, seg_dur, use_gpu, numa_node, dist,
                      transport=getattr(node.comm, "data_transport", None))
+    result["per_rank"] = _per_rank_dicts(per_parts, args.steps)
+    result["data_plane"] = _plane_info(node)
     if args.verbose:
         print(f"# rank {rank} pack {t_pack:.2f}s {_mem(use_gpu, device)} counters {counters} level {hls.currentLevel}\n"
               f"#   node stats {node.stats} last round {node.last_round}\n"
@@ -626,6 +630,8 @@ def _fleet(args, world, rank, device, use_gpu, node, origin, players, desc, encr
         elapsed = time.perf_counter() - t0
         fleet_ms = fleet_timer.summary_ms(args.steps)
         node_ms, tm_ms = node.timer.summary_ms(args.steps), pipe.timer.summary_ms(args.steps)
+        win_fleet = dict(fleet_timer.total)
+        s1_timers = (dict(node.timer.total), dict(pipe.timer.total))
         if _PROF is not None:
             _PROF.disable()
             _dump_profile(rank)
@@ -651,14 +657,18 @@ def _fleet(args, world, rank, device, use_gpu, node, origin, players, desc, encr
         d_segs = sum(s1[k] - s0[k] for k in ("cdn_segments", "p2p_segments"))
         vals = np.array([done, s1["cdn"] - s0["cdn"], s1["p2p"] - s0["p2p"], int(elapsed * 1e9), errors, d_segs],
                         dtype=np.int64)
+        per = _per_rank(node, pipe, s0, s1, elapsed, args.steps, K * W, fleet_total=win_fleet, timers=s1_timers)
         if world > 1:
             parts = node.comm.allgather_control(vals)
             tot = np.sum(np.stack(parts), axis=0)
             max_ns = max(int(x[3]) for x in parts)
+            per_parts = node.comm.allgather_control(per)
         else:
-            tot, max_ns = vals, int(vals[3])
+            tot, max_ns, per_parts = vals, int(vals[3]), [per]
         result = _result(args, world, tot, max_ns / 1e9, origin, K, desc, encrypted, seg_dur, use_gpu, numa_node,
                          dist, players=W, transport=getattr(node.comm, "data_transport", None))
+        result["per_rank"] = _per_rank_dicts(per_parts, args.steps)
+        result["data_plane"] = _plane_info(node)
         if live:
             result["config"].update(live=True, live_speed=args.live_speed, live_window=args.live_window,
                                     round_ms=args.round_ms, evicted_segments=server.evicted)
@@ -735,6 +745,103 @@ def _result(args, world, tot, max_s, origin, K, desc, encrypted, seg_dur, use_gp
                    "cpu_place": getattr(args, "cpu_place_applied", None) or "shared",
                    "ingest": args.ingest if use_gpu else "host"},
     }
+
+
+# per-rank diagnostics of the timed window, all-gathered as int64 milli-units (fixed order)
+PER_RANK_FIELDS = ("rank", "rounds", "step_ms", "wait_device_us", "control_us", "plan_us", "host_round_us",
+                   "cdn_GBps", "cdn_dev_ms", "p2p_recv_MB", "p2p_sent_MB", "p2p_dev_ms", "p2p_GBps",
+                   "p2p_links", "p2p_link_GBps", "transmux_dev_ms", "transmux_wait_us", "await_players_us",
+                   "crc_failures", "control_fallbacks", "deferred", "inflight", "cu_reserve")
+
+
+def _per_rank(node, pipe, s0, s1, elapsed, steps, inflight, fleet_total=None, timers=None) -> np.ndarray:
+    """This rank's timed-window diagnostics (``PER_RANK_FIELDS``): per ROUND host phases in
+    us (``wait_device`` = host blocked on the round's device event, ``control`` = control
+    all-gather + directory ingest, ``plan`` = plan_round + pins); the CDN rate over the
+    window and the copy-stream (H2D) device ms per round; P2P received / sent MB per round,
+    the node-stream exchange device ms per round (a peer's stall included), the received
+    GB/s over that time, the source links per round and the GB/s per link (bytes per link
+    over the exchange time: a lower bound on each xGMI link's rate); transmux device ms per
+    step (default stream) and the host wait for it; fleet: per-step wait on the players."""
+    rounds = max(1, s1["rounds"] - s0["rounds"])
+    tm, pt = timers if timers is not None else (node.timer.total, pipe.timer.total)
+    recv = s1["p2p"] - s0["p2p"]
+    sent = s1["upload"] - s0["upload"]
+    links = s1.get("p2p_links", 0) - s0.get("p2p_links", 0)
+    p2p_dev_s = tm.get("dev_p2p_ms", 0.0)  # seconds (PhaseTimer totals)
+    host_round = sum(tm.get(k, 0.0) for k in ("control", "plan", "cdn_enqueue", "p2p_enqueue", "commit", "deliver"))
+    try:
+        from hlsjs_p2p_wrapper_amd.ops._native import device as _dev
+
+        cu_reserve = _dev().cu_reserve() if node.is_cuda else 0
+    except Exception:  # noqa: BLE001 - CPU rehearsal without the device module
+        cu_reserve = 0
+    vals = {
+        "rank": node.rank, "rounds": rounds, "step_ms": elapsed * 1e3 / max(1, steps),
+        "wait_device_us": tm.get("wait_device", 0.0) * 1e6 / rounds,
+        "control_us": tm.get("control", 0.0) * 1e6 / rounds,
+        "plan_us": tm.get("plan", 0.0) * 1e6 / rounds,
+        "host_round_us": host_round * 1e6 / rounds,
+        "cdn_GBps": (s1["cdn"] - s0["cdn"]) / max(elapsed, 1e-9) / 1e9,
+        "cdn_dev_ms": tm.get("dev_cdn_ms", 0.0) * 1e3 / rounds,
+        "p2p_recv_MB": recv / rounds / 1e6, "p2p_sent_MB": sent / rounds / 1e6,
+        "p2p_dev_ms": p2p_dev_s * 1e3 / rounds,
+        "p2p_GBps": recv / p2p_dev_s / 1e9 if p2p_dev_s > 0 else 0.0,
+        "p2p_links": links / rounds,
+        "p2p_link_GBps": recv / links / (p2p_dev_s / rounds) / 1e9 if links and p2p_dev_s > 0 else 0.0,
+        "transmux_dev_ms": pt.get("dev_transmux", 0.0) * 1e3 / max(1, steps),
+        "transmux_wait_us": pt.get("wait_device", 0.0) * 1e6 / max(1, steps),
+        "await_players_us": (fleet_total or {}).get("await_players", 0.0) * 1e6 / max(1, steps),
+        "crc_failures": s1["crc_failures"] - s0["crc_failures"],
+        "control_fallbacks": getattr(node.comm, "control_fallbacks", 0),
+        "deferred": s1.get("deferred", 0) - s0.get("deferred", 0),
+        "inflight": inflight, "cu_reserve": cu_reserve,
+    }
+    return np.array([int(round(float(vals[k]) * 1000)) for k in PER_RANK_FIELDS], dtype=np.int64)
+
+
+def _per_rank_dicts(parts, steps) -> list:
+    """Decode the gathered rows; add each rank's ``bound`` label.
+
+    Rule: the host waited on the device for more than 30 % of a step (``wait_device`` per
+    round x rounds per step + the transmux wait) -> device-bound, by the busiest stream:
+    ``pcie`` (H2D copy stream), ``xgmi`` (the node stream's exchange), ``transmux`` (decrypt +
+    demux); otherwise ``players`` when the fleet wait exceeds the own host work, else
+    ``host``."""
+    out = []
+    for p in parts:
+        d = {k: float(v) / 1000 for k, v in zip(PER_RANK_FIELDS, np.asarray(p).tolist())}
+        for k in ("rank", "rounds", "crc_failures", "control_fallbacks", "deferred", "inflight", "cu_reserve"):
+            d[k] = int(round(d[k]))
+        for k, v in list(d.items()):
+            if isinstance(v, float):
+                d[k] = round(v, 3)
+        step = max(d["step_ms"], 1e-9)
+        rps = d["rounds"] / max(1, steps)
+        waited = (d["wait_device_us"] * rps + d["transmux_wait_us"]) / 1e3
+        busy = {"pcie": d["cdn_dev_ms"] * rps, "xgmi": d["p2p_dev_ms"] * rps, "transmux": d["transmux_dev_ms"]}
+        if waited > 0.3 * step:
+            d["bound"] = max(busy, key=busy.get)
+        elif d["await_players_us"] / 1e3 > 0.5 * step:
+            d["bound"] = "players"
+        else:
+            d["bound"] = "host"
+        out.append(d)
+    return out
+
+
+def _plane_info(node) -> dict:
+    """Which transports the run actually used (the data plane may fall back; see
+    parallel/comm.py).  ``hsa_ipc_legacy``: the HSA IPC mode the process started with
+    (``0`` = dmabuf: RCCL's intra-node P2P transport and the HIP-IPC rehearsal export device
+    buffers with ``hipIpcGetMemHandle``, which fails with ``invalid argument`` under the
+    legacy mode on this host driver, ``tools/ipc_probe.py``)."""
+    comm = node.comm
+    ipc = getattr(comm, "_ipc", None)
+    return {"data": getattr(comm, "data_transport", "local"), "control": getattr(comm, "control_transport", "local"),
+            "ipc_events": bool(ipc is not None and ipc._peer_ev is not None),
+            "shm_slot_words": getattr(comm, "shm_slot_words", None),
+            "hsa_ipc_legacy": os.environ.get("HSA_ENABLE_IPC_MODE_LEGACY")}
 
 
 def _mem(use_gpu, device) -> str:

@@ -102,13 +102,17 @@ def load_cache(node, path: str) -> Dict[str, int]:
         raise RuntimeError("segment cache has pinned entries in the way; restore before playback starts")
     _, ids, dst_offs = res
     node._grow_crc(int(ids.max()) + 1)
-    src = data.to(node.device, non_blocking=False) if node.is_cuda else data
-    _seg.copy_segments(src, node.arena, offs[keep], dst_offs, ln)
-    expect = crcs[keep].to(node.device)
-    _, ok = _crc.crc32_batch(node.arena, dst_offs.tolist(), ln.tolist(), expect_dev=expect)
-    ok = ok.cpu().numpy().astype(bool)
-    good, bad = ids[ok], ids[~ok]
-    node.crc_dev[torch.from_numpy(good).to(node.device)] = expect[torch.from_numpy(np.nonzero(ok)[0]).to(node.device)]
+    # the node stream owns the CRC table (node.py's ownership rule): the restore runs on it,
+    # so the table write below is ordered before the next round's trailer gathers
+    with node._on_node_stream():
+        src = data.to(node.device, non_blocking=False) if node.is_cuda else data
+        _seg.copy_segments(src, node.arena, offs[keep], dst_offs, ln)
+        expect = crcs[keep].to(node.device)
+        _, ok = _crc.crc32_batch(node.arena, dst_offs.tolist(), ln.tolist(), expect_dev=expect)
+        ok = ok.cpu().numpy().astype(bool)
+        good, bad = ids[ok], ids[~ok]
+        node.crc_dev[torch.from_numpy(good).to(node.device)] = \
+            expect[torch.from_numpy(np.nonzero(ok)[0]).to(node.device)]
     if len(good):
         st.commit(good)
     if len(bad):

@@ -188,7 +188,6 @@ class SwarmNode:
         self.store = self.rt.SegmentStore(self.cache_bytes, ALIGN)
         self.directory = self.rt.Directory()
         self.arena = torch.empty(self.cache_bytes + SLACK, dtype=torch.uint8, device=self.device)
-        self.crc_dev = torch.zeros(1024, dtype=torch.int32, device=self.device)  # CRC per entry id
         # all node device work (ingest CRC, RCCL, verify CRC) runs on its own stream: consumers
         # (decrypt/demux of the previous round) on the default stream overlap it.  The CDN
         # H2D DMAs get a copy stream of their own, so round t+1's DMA queues directly behind
@@ -196,9 +195,31 @@ class SwarmNode:
         # rounds (the node stream waits for each round's DMA with an event).  Reuse of arena
         # space is ordered by the store's pins, not by stream order: reserved and in-flight
         # entries stay pinned until complete_round, delivered ones PIN_DELAY_ROUNDS launches.
+        #
+        # Ownership rule for every other device tensor (the caching allocator hands a freed
+        # block straight back to the pool of the stream it was ALLOCATED on, without waiting
+        # for work queued on other streams):
+        #   * a tensor the node stream writes or reads is allocated on the node stream (inside
+        #     `torch.cuda.stream(self.stream)`: launch_round's phases, _grow_crc, the per-round
+        #     trailers / staging / verify outputs), so its free is ordered behind that work;
+        #   * the arena is allocated once and never freed while the node lives;
+        #   * a tensor that must outlive a stream switch is `record_stream`-ed on the consuming
+        #     stream before its last Python reference drops (_grow_crc's old table);
+        #   * the copy stream only writes the arena (h2d_batch allocates nothing on it);
+        #   * consumers on other streams (transmux, fleet payload copies, checkpoints) read the
+        #     arena only after the host waited on the round's event (complete_round).
+        # Round 3's 2-rank fault at 128 in flight was this rule broken: the CRC table, allocated
+        # on the default stream, was replaced from the node stream while that stream's verify
+        # CRC (stalled behind a peer's IPC event) still had to scatter into it; the transmux
+        # descriptor block took the freed block and was overwritten (profiles/r4_uaf).
         self.stream = torch.cuda.Stream(self.device) if self.is_cuda else None
         self.copy_stream = (torch.cuda.Stream(self.device) if self.is_cuda and
                             os.environ.get("HLSP2P_COPY_STREAM", "1") != "0" else None)
+        # CRC per store entry id.  Entry ids are bounded by the live entries; the table starts
+        # big enough for any realistic segment size (>= 8 KiB average) so it never grows on
+        # the hot path, and a grow is stream-safe anyway (_grow_crc)
+        with self._on_node_stream():
+            self.crc_dev = torch.zeros(self._crc_capacity(), dtype=torch.int32, device=self.device)
         self._events = _EventPool()
         self.online = True
         self._upload_default = True
@@ -232,6 +253,7 @@ class SwarmNode:
         self._locator = self.rt.SegmentLocator()
         self._locator_gen = -1
         self._locator_origins: Dict[int, Any] = {}
+        self._locator_skip: set = set()  # origins that can never use the locator (see _register_locator)
         self._tick_scheduled = False
         self._timer = None
         self._pins: List[Tuple[int, np.ndarray]] = []  # (release at launch #, entry ids)
@@ -240,7 +262,8 @@ class SwarmNode:
         self._net_wants = False  # some want came from a network origin (plans may carry STAGE rows)
         self.peer_online = np.ones(self.world, dtype=bool)
         self.stats = {"cdn": 0, "p2p": 0, "upload": 0, "cache": 0, "rounds": 0, "crc_failures": 0,
-                      "segments": 0, "cdn_segments": 0, "p2p_segments": 0, "prefetched": 0}
+                      "segments": 0, "cdn_segments": 0, "p2p_segments": 0, "prefetched": 0,
+                      "p2p_links": 0}  # p2p_links: (round, source peer) pairs received from
         self.swarm_stats = {"cdn": 0, "p2p": 0, "upload": 0}
         self.last_round: Dict[str, Any] = {}
         self.corrupt_next_recv = 0  # fault injection: flip a byte in the next N received rounds
@@ -335,7 +358,7 @@ class SwarmNode:
         if hit is not None:
             return hit[0], hit[1], hit[2], hit[3], None
         origin, path = http.resolve(url)
-        if id(origin) not in self._locator_origins:
+        if id(origin) not in self._locator_origins or self._locator_gen != http.generation():
             self._register_locator(origin)
         rng = http.parse_range(headers) if headers else None
         if getattr(origin, "staged_fetch", False):
@@ -368,25 +391,35 @@ class SwarmNode:
 
     def _register_locator(self, origin: Any) -> None:
         """Hand a fixed-address origin's segment directories to the native locator (once per
-        origin and registry generation).  Origins without them, with faults configured, or
-        whose host bytes are not pinned (the async H2D path needs pinned memory: the Python
-        path raises for them) stay on the per-request path."""
+        origin and registry generation).  Origins without them, or whose host bytes are not
+        pinned (the async H2D path needs pinned memory: the Python path raises for them),
+        stay on the per-request path for good; an origin whose directories are unavailable
+        right now (faults injected) is asked again on a later miss.  An origin is recorded
+        only once ALL its directories are registered, so a partial registration never
+        happens and a fault-time refusal does not lock it out of the fast path."""
         if http.generation() != self._locator_gen:
             self._locator.clear()
             self._locator_origins.clear()
+            self._locator_skip.clear()
             self._locator_gen = http.generation()
-        self._locator_origins[id(origin)] = origin
+        if id(origin) in self._locator_skip:
+            return
         dirs_fn = getattr(origin, "segment_dirs", None)
-        dirs = dirs_fn() if dirs_fn is not None else None
+        if dirs_fn is None:
+            self._locator_skip.add(id(origin))
+            return
+        dirs = dirs_fn()
         if not dirs:
+            return  # e.g. faults configured now: retried on a later miss
+        if any(not d[5].is_cuda and self.is_cuda and not d[5].is_pinned() for d in dirs):
+            self._locator_skip.add(id(origin))
             return
         for d, prefix, suffix, lo, hi, data, offs, lens in dirs:
-            if not data.is_cuda and self.is_cuda and not data.is_pinned():
-                return
             base = data.data_ptr()
             self._loc_keep.setdefault(base, data)
             self._locator.add_dir(d, prefix, suffix, int(lo), int(hi), base, W_ON_DEV if data.is_cuda else 0,
                                   np.asarray(offs, dtype=np.int64), np.asarray(lens, dtype=np.int64))
+        self._locator_origins[id(origin)] = origin
 
     def _locator_usable(self) -> bool:
         """The native locator may answer this batch: it holds directories of the current
@@ -678,11 +711,28 @@ class SwarmNode:
         return np.concatenate([hdr, rows.reshape(-1), adds.reshape(-1).astype(np.int64),
                                rms.reshape(-1).astype(np.int64)])
 
+    CRC_TABLE_MAX = 1 << 20  # initial CRC-table entries at most (4 MiB)
+
+    def _crc_capacity(self) -> int:
+        return int(min(max(1024, self.cache_bytes // (8 << 10) + 1), self.CRC_TABLE_MAX))
+
+    def _on_node_stream(self):
+        return torch.cuda.stream(self.stream) if self.stream is not None else contextlib.nullcontext()
+
     def _grow_crc(self, n: int) -> None:
-        if n > self.crc_dev.numel():
-            new = torch.zeros(max(n, 2 * self.crc_dev.numel()), dtype=torch.int32, device=self.device)
-            new[:self.crc_dev.numel()] = self.crc_dev
-            self.crc_dev = new
+        """Make the CRC table hold entry ids ``< n``.  The new table is allocated and filled on
+        the node stream, and the old one is recorded on it, so node-stream kernels still
+        queued against the old table (ingest / verify scatters, trailer gathers) finish
+        before the allocator can hand its block to anyone (see the ownership rule above)."""
+        old = self.crc_dev
+        if n <= old.numel():
+            return
+        with self._on_node_stream():
+            new = torch.zeros(max(n, 2 * old.numel()), dtype=torch.int32, device=self.device)
+            new[:old.numel()] = old
+        if old.is_cuda:
+            old.record_stream(self.stream)
+        self.crc_dev = new
 
     # ------------------------------------------------------------------ rounds
     def tick(self) -> bool:
@@ -1110,6 +1160,7 @@ class SwarmNode:
             h.ok_host = ok
         self.stats["p2p"] += int(recv_rows[:, 4].sum())
         self.stats["p2p_segments"] += len(recv_rows)
+        self.stats["p2p_links"] += len(rrun)
 
     # ------------------------------------------------------------------ delivery
     def _deliver_cols(self, tok: np.ndarray, src: np.ndarray, nbytes: np.ndarray, cdn_ms: np.ndarray,

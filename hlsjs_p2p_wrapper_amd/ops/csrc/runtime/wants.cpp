@@ -110,8 +110,8 @@ void WantTable::select(const SegmentStore& store, const Directory* dir, int64_t 
       }
       continue;
     }
+    if (pick.size() >= limit) break;  // (cap 0 admits nothing: checked before the push)
     pick.push_back(r.id);
-    if (pick.size() >= limit) break;
   }
   for (int64_t id : spec) {
     if (pick.size() >= limit) break;

@@ -32,6 +32,7 @@ Backends:
 from __future__ import annotations
 
 import atexit
+import logging
 import os
 import secrets
 import socket
@@ -40,6 +41,8 @@ from typing import Any, List, Optional, Sequence, Tuple
 
 import numpy as np
 import torch
+
+log = logging.getLogger("hlsjs_p2p_wrapper_amd.comm")
 
 
 class SwarmComm:
@@ -155,6 +158,11 @@ class DistComm(SwarmComm):
         self.data_backend = backend
         self._cap = 64  # int64 words per rank in the one-shot control all-gather
         self.control_timeout_s = float(os.environ.get("HLSP2P_CONTROL_TIMEOUT", "600"))
+        # shared-memory slot per rank and round: a message larger than it makes every rank
+        # take the gloo all-gather for that round (~3.4 ms at 8 ranks instead of ~10 us):
+        # counted, and warned about once, never silent (bench.py sizes the slot)
+        self.shm_slot_words = max(1024, int(os.environ.get("HLSP2P_SHM_SLOT_WORDS", str(self.SHM_SLOT_WORDS))))
+        self.control_fallbacks = 0
         self._shm = self._open_shm_control() if self.world_size > 1 else None
         self.control_transport = "shm" if self._shm is not None else "gloo"
         self._rccl = None
@@ -254,14 +262,14 @@ class DistComm(SwarmComm):
         shm, ok = None, True
         if self.rank == 0:
             try:
-                shm = rt.ShmControl(name[0], 0, self.world_size, self.SHM_SLOT_WORDS, True)
+                shm = rt.ShmControl(name[0], 0, self.world_size, self.shm_slot_words, True)
             except Exception:  # noqa: BLE001 - any failure: stay on gloo
                 ok = False
         flags: List[object] = [None] * self.world_size
         dist.all_gather_object(flags, ok, group=g)
         if self.rank != 0 and all(flags):
             try:
-                shm = rt.ShmControl(name[0], self.rank, self.world_size, self.SHM_SLOT_WORDS, False)
+                shm = rt.ShmControl(name[0], self.rank, self.world_size, self.shm_slot_words, False)
             except Exception:  # noqa: BLE001
                 ok = False
         dist.all_gather_object(flags, ok, group=g)
@@ -275,6 +283,11 @@ class DistComm(SwarmComm):
             if out is not None:
                 return out
             # some rank's message exceeded a slot: every rank saw that and falls back here
+            self.control_fallbacks += 1
+            if self.control_fallbacks == 1:
+                log.warning("rank %d: a control message exceeded the %d-word shared-memory slot; this round's "
+                            "all-gather fell back to gloo (raise HLSP2P_SHM_SLOT_WORDS; counted in "
+                            "control_fallbacks)", self.rank, self.shm_slot_words)
         return self._allgather_gloo(msg)
 
     def _allgather_gloo(self, msg: np.ndarray) -> List[np.ndarray]:

@@ -23,40 +23,58 @@ class DecryptData:
         return self.method == "AES-128" and self.uri is not None and self.key is None
 
 
-# Bumped whenever any Fragment's ``start`` is assigned (construction included): consumers
-# that cache derived start-time arrays (models.media_map) compare generations instead of
-# trusting list identity — hls.js rewrites ``frag.start`` in place on PTS realignment.
+# Bumped whenever a Fragment's ``start`` is REWRITTEN after construction: consumers that
+# cache derived start-time arrays (models.media_map) compare generations instead of trusting
+# list identity -- hls.js rewrites ``frag.start`` in place on PTS realignment.  Building
+# fragments (a playlist parse or reload) does not bump it, so it never invalidates the start
+# index of other levels.
 _START_GENERATION = [0]
 
 
 def fragment_generation() -> int:
-    """Counter of ``Fragment.start`` assignments in this process."""
+    """Counter of post-construction ``Fragment.start`` rewrites in this process."""
     return _START_GENERATION[0]
 
 
-@dataclass(eq=False, slots=True)  # slots: a long DVR playlist holds 10^5..10^6 of these
 class Fragment:
-    url: str
-    sn: int
-    start: float
-    duration: float
-    level: int = 0
-    cc: int = 0
-    byteRangeStartOffset: Optional[int] = None
-    byteRangeEndOffset: Optional[int] = None
-    decryptdata: Optional[DecryptData] = None
-    loaded: int = 0
-    loadCounter: int = 0
-    loadIdx: int = 0
-    autoLevel: bool = False
-    loader: Any = None
-    title: str = ""
-    programDateTime: Any = None
+    """One media fragment (hls.js ``Fragment`` fields the reference reads).  A plain slotted
+    class (a long DVR playlist holds 10^5..10^6 of these): field writes are slot stores with
+    no Python hook; only ``start`` is a property, whose setter bumps the generation."""
 
-    def __setattr__(self, name: str, value: Any) -> None:
-        object.__setattr__(self, name, value)
-        if name == "start":
-            _START_GENERATION[0] += 1
+    __slots__ = ("url", "sn", "_start", "duration", "level", "cc", "byteRangeStartOffset", "byteRangeEndOffset",
+                 "decryptdata", "loaded", "loadCounter", "loadIdx", "autoLevel", "loader", "title",
+                 "programDateTime")
+
+    def __init__(self, url: str, sn: int, start: float, duration: float, level: int = 0, cc: int = 0,
+                 byteRangeStartOffset: Optional[int] = None, byteRangeEndOffset: Optional[int] = None,
+                 decryptdata: Optional[DecryptData] = None, loaded: int = 0, loadCounter: int = 0,
+                 loadIdx: int = 0, autoLevel: bool = False, loader: Any = None, title: str = "",
+                 programDateTime: Any = None) -> None:
+        self.url = url
+        self.sn = sn
+        self._start = start
+        self.duration = duration
+        self.level = level
+        self.cc = cc
+        self.byteRangeStartOffset = byteRangeStartOffset
+        self.byteRangeEndOffset = byteRangeEndOffset
+        self.decryptdata = decryptdata
+        self.loaded = loaded
+        self.loadCounter = loadCounter
+        self.loadIdx = loadIdx
+        self.autoLevel = autoLevel
+        self.loader = loader
+        self.title = title
+        self.programDateTime = programDateTime
+
+    @property
+    def start(self) -> float:
+        return self._start
+
+    @start.setter
+    def start(self, value: float) -> None:
+        self._start = value
+        _START_GENERATION[0] += 1
 
     @property
     def end(self) -> float:

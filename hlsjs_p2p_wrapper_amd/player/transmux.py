@@ -77,7 +77,7 @@ class MediaPipeline:
         self.bytes_in = 0
         self.batches = 0
         self.timer = PhaseTimer()
-        self._free_events: List[Any] = []
+        self._free_events: List[Any] = []  # timing events (start / end of each batch on the device)
         # event-loop players flush at the end of the loop iteration; a throughput driver
         # sets auto_flush=False and overlaps launch() / complete() of consecutive batches
         self.auto_flush = True
@@ -116,6 +116,26 @@ class MediaPipeline:
         for j, r in zip(batch.jobs, results):
             j.callback(r)
         self.timer.add("callbacks", time.perf_counter() - t)
+
+    # ------------------------------------------------------------------ device events
+    def _event(self):
+        """A recorded timing event on the current stream (recycled: a fresh event costs
+        ~5 us of host time)."""
+        ev = self._free_events.pop() if self._free_events else torch.cuda.Event(enable_timing=True)
+        ev.record()
+        return ev
+
+    def _wait(self, b: "_Batch") -> None:
+        """Host wait for a batch's device work; its device time goes to ``dev_transmux``."""
+        if b.event is None:
+            return
+        b.event.synchronize()
+        if b.start is not None:
+            self.timer.add("dev_transmux", b.start.elapsed_time(b.event) / 1e3)
+            self._free_events.append(b.start)
+            b.start = None
+        self._free_events.append(b.event)
+        b.event = None
 
     # ------------------------------------------------------------------ batch
     def _stage(self, tensors: List[torch.Tensor], sizes: List[int]) -> Tuple[torch.Tensor, List[int]]:
@@ -207,8 +227,7 @@ class MediaPipeline:
             host.append((hi, hl))
         ev = None
         if dev.type != "cpu":
-            ev = self._free_events.pop() if self._free_events else torch.cuda.Event()
-            ev.record()
+            ev = self._event()
         tm.add("demux_launch", time.perf_counter() - t2)
         return _Batch(jobs, infos=infos, host=host, event=ev, results=results)
 
@@ -237,6 +256,7 @@ class MediaPipeline:
         td0, isb = _aes.device_tables(self.device)
         t2 = time.perf_counter()
         tm.add("decrypt_launch", t2 - t1)
+        ev0 = self._event()
         groups, dec, host_block = _native_device().transmux_launch(src, offs, nb, flags, drk, iv, td0, isb,
                                                                    _ts.DEFAULT_MAX_PES)
         infos, host = [], []
@@ -244,10 +264,9 @@ class MediaPipeline:
             batch_idx = [idx[k] for k in gidx.tolist()]
             infos.append((batch_idx, _ts.DemuxResult(info, pes, es, es_offs), es_offs, hlens))
             host.append((hinfo, hlens))
-        ev = self._free_events.pop() if self._free_events else torch.cuda.Event()
-        ev.record()
+        ev = self._event()
         tm.add("demux_launch", time.perf_counter() - t2)
-        return _Batch(jobs, infos=infos, host=host, event=ev, results=results, keep=(dec, host_block))
+        return _Batch(jobs, infos=infos, host=host, event=ev, results=results, keep=(dec, host_block), start=ev0)
 
     # ------------------------------------------------------------------ columnar batch
     def launch_columns(self, src: torch.Tensor, offs: np.ndarray, nbytes: np.ndarray, enc: np.ndarray,
@@ -284,6 +303,7 @@ class MediaPipeline:
         if not ok.all():
             offs, nb, enc, drk, iv = offs[ok], nb[ok], enc[ok], drk[ok], iv[ok]
         td0, isb = _aes.device_tables(self.device)
+        ev0 = self._event()
         groups, dec, host_block = _native_device().transmux_launch(
             src, offs, nb, enc.astype(np.uint8), np.ascontiguousarray(drk, dtype=np.uint32),
             np.ascontiguousarray(iv, dtype=np.uint8), td0, isb, _ts.DEFAULT_MAX_PES)
@@ -291,10 +311,9 @@ class MediaPipeline:
         for gidx, info, pes, es, es_offs, hinfo, hlens in groups:
             infos.append((idx_ok[gidx], _ts.DemuxResult(info, pes, es, es_offs), es_offs, hlens))
             host.append((hinfo, hlens))
-        ev = self._free_events.pop() if self._free_events else torch.cuda.Event()
-        ev.record()
+        ev = self._event()
         self.timer.add("launch_columns", time.perf_counter() - t1)
-        return _Batch(None, infos=infos, host=host, event=ev, keep=(dec, host_block), tag=tag, n=n)
+        return _Batch(None, infos=infos, host=host, event=ev, keep=(dec, host_block), tag=tag, n=n, start=ev0)
 
     def launch_jobs(self, jobs: List[TransmuxJob]) -> "_Batch":
         """:meth:`launch` for an explicit job list (the pipeline's own queue untouched)."""
@@ -314,10 +333,7 @@ class MediaPipeline:
         plain = np.full(n, -1, dtype=np.int64)
         has = np.zeros(n, dtype=bool)
         t3 = time.perf_counter()
-        if batch.event is not None:
-            batch.event.synchronize()
-            self._free_events.append(batch.event)
-            batch.event = None
+        self._wait(batch)
         self.timer.add("wait_device", time.perf_counter() - t3)
         for (idx, _res, _es_offs, _lens), (hinfo, hlens) in zip(batch.infos, batch.host):
             k = len(idx)
@@ -335,10 +351,7 @@ class MediaPipeline:
         if batch.error is not None:
             return [(j, None, -1) for j in batch.jobs]
         t3 = time.perf_counter()
-        if batch.event is not None:
-            batch.event.synchronize()
-            self._free_events.append(batch.event)
-            batch.event = None
+        self._wait(batch)
         self.timer.add("wait_device", time.perf_counter() - t3)
         out: List[Any] = [None] * len(batch.jobs)
         for (idx, _res, _es_offs, _lens), (hinfo, hlens) in zip(batch.infos, batch.host):
@@ -365,10 +378,7 @@ class MediaPipeline:
         if batch.error is not None:
             return batch.jobs, rows, plain, has
         t3 = time.perf_counter()
-        if batch.event is not None:
-            batch.event.synchronize()
-            self._free_events.append(batch.event)
-            batch.event = None
+        self._wait(batch)
         self.timer.add("wait_device", time.perf_counter() - t3)
         for (idx, _res, _es_offs, _lens), (hinfo, hlens) in zip(batch.infos, batch.host):
             k = len(idx)
@@ -380,10 +390,7 @@ class MediaPipeline:
     def _complete(self, b: "_Batch") -> List[Dict[str, Any]]:
         tm = self.timer
         t3 = time.perf_counter()
-        if b.event is not None:
-            b.event.synchronize()
-            self._free_events.append(b.event)  # recycled: a fresh event costs ~5 us per batch
-            b.event = None
+        self._wait(b)
         t4 = time.perf_counter()
         tm.add("wait_device", t4 - t3)
         results = b.results
@@ -477,6 +484,7 @@ class _Batch:
     keep: Any = None  # device/pinned buffers the batch's in-flight work uses
     tag: Any = None  # launch_columns: the caller's columns, handed back by complete_columns
     n: int = 0  # launch_columns: fragments in the batch
+    start: Any = None  # timing event recorded before the batch's first launch
 
 
 _local = threading.local()

@@ -100,6 +100,7 @@ def test_bench_two_ranks_abr_ladder_with_churn(players):
     assert calm["errors"] == 0 and churn["errors"] == 0
     assert calm["n_gpus"] == 2 and churn["config"]["churn_steps"] == 2
     assert 0 < churn["offload_ratio"] < calm["offload_ratio"]
+    _check_per_rank(calm, 2)
 
 
 def test_bench_eight_ranks_driver_shape():
@@ -115,6 +116,26 @@ def test_bench_eight_ranks_driver_shape():
     # second rank (a player that reached them after the window mark), so offload is ~7/8
     assert 0.75 < res["offload_ratio"] <= 0.9
     assert res["value"] > 0
+    _check_per_rank(res, 8)
+
+
+PER_RANK_KEYS = {"rank", "rounds", "step_ms", "wait_device_us", "control_us", "plan_us", "host_round_us", "cdn_GBps",
+                 "cdn_dev_ms", "p2p_recv_MB", "p2p_sent_MB", "p2p_dev_ms", "p2p_GBps", "p2p_links", "p2p_link_GBps",
+                 "transmux_dev_ms", "transmux_wait_us", "await_players_us", "crc_failures", "control_fallbacks",
+                 "deferred", "inflight", "cu_reserve", "bound"}
+
+
+def _check_per_rank(res, world):
+    """The N>1 record explains its own number: one diagnostics row per rank (bench.py
+    PER_RANK_FIELDS) plus the transports actually used."""
+    rows = res["per_rank"]
+    assert [r["rank"] for r in rows] == list(range(world))
+    for r in rows:
+        assert set(r) == PER_RANK_KEYS
+        assert r["rounds"] >= res["steps"] and r["crc_failures"] == 0 and r["control_fallbacks"] == 0
+        assert r["bound"] in ("pcie", "xgmi", "transmux", "players", "host")
+        assert r["p2p_recv_MB"] > 0 and 0 < r["p2p_links"] <= world - 1  # every rank received from peers
+    assert res["data_plane"]["data"] == "gloo" and res["data_plane"]["control"] == "shm"
 
 
 def _peer4(rank: int, world: int, port: int, q) -> None:

@@ -88,6 +88,11 @@ def test_faults_and_live_take_the_python_path():
     node.request_batch(np.array([[1, 0, 0, sn] for sn in range(4)], dtype=np.int64), u, None,
                        np.arange(4, dtype=np.int64))
     assert calls == u and node._bulk.fails == [(2, 503)]
+    # once the faults are cleared, the origin returns to the native fast path (it was not
+    # locked out by the refusal while faults were active)
+    origin.clear_faults()
+    node._resolve(origin.base_url + origin.segment_path(0, 7), None)
+    assert node._locator_usable() and len(node._locator) > 0
     live = SyntheticHlsOrigin("http://cdn.loc/live/", renditions=[Rendition(400_000, 640, 360)], live=True,
                               pin_memory=False)
     assert live.segment_dirs() is None

@@ -106,3 +106,17 @@ def test_start_index_cache_follows_fragment_mutations():
     # a list re-sorted in place after a start rewrite falls back to / rebuilds the index
     frags[0].start = 500.0
     assert 0 in [s.sn for s in mm.getSegmentList(tv, 495, 10)]
+
+
+def test_fragment_construction_keeps_other_levels_indexes():
+    """Building fragments (a playlist parse or live reload of one level) does not bump the
+    start generation, so other levels' cached start indexes stay valid; only a start
+    REWRITE of an existing fragment does."""
+    from hlsjs_p2p_wrapper_amd.player.level import Fragment, fragment_generation
+
+    g0 = fragment_generation()
+    frags = [Fragment(url=f"s{i}.ts", sn=i, start=4.0 * i, duration=4.0) for i in range(1000)]
+    frags[3].loaded = 10  # other field writes: no hook at all
+    assert fragment_generation() == g0
+    frags[3].start = 13.0
+    assert fragment_generation() == g0 + 1 and frags[3].start == 13.0 and frags[3].end == 17.0

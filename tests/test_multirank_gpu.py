@@ -41,3 +41,22 @@ def test_two_ranks_share_one_gpu_bench_path(cuda, plane):
     assert res["n_gpus"] == 2 and res["errors"] == 0
     assert res["offload_ratio"] == pytest.approx(0.5, abs=0.02)  # every segment fetched once, shared once
     assert res["value"] > 0 and res["config"]["parallelism"] == f"swarm2-{plane}"
+
+
+@pytest.mark.gpu
+def test_two_ranks_ipc_events_bench_scale(cuda):
+    """Bench-scale state on the rehearsal plane (round-3 VERDICT weak 3): 4 players x 64 in
+    flight per rank (256 wants a round: the store's entry ids pass 1024 by round 5, where the
+    old CRC table grew under queued scatters), a 6 GB arena per rank, interprocess events
+    on, and 250 timed rounds (the event ring is renewed after 240 exchanges)."""
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2", "--master-addr",
+           "127.0.0.1", "--master-port", str(_free_port()), str(REPO / "bench.py"), "--gpus", "2", "--steps", "250",
+           "--warmup", "5", "--inflight", "64", "--players", "4", "--cache-gb", "6", "--dist-backend", "ipc"]
+    env = dict(os.environ, PYTHONPATH=str(REPO), HLSP2P_IPC_EVENTS="1")
+    p = subprocess.run(cmd, cwd=REPO, env=env, capture_output=True, text=True, timeout=600)
+    assert p.returncode == 0, p.stderr[-4000:]
+    res = json.loads([ln for ln in p.stdout.splitlines() if ln.startswith("{")][-1])
+    assert res["errors"] == 0 and res["data_plane"]["ipc_events"]
+    assert res["offload_ratio"] == pytest.approx(0.5, abs=0.05)
+    for r in res["per_rank"]:
+        assert r["rounds"] >= 250 and r["crc_failures"] == 0 and r["control_fallbacks"] == 0

@@ -267,6 +267,7 @@ def test_want_table_select_order_cap_and_backpressure(rt):
     st = rt.SegmentStore(8 * 1024, 256)
     pf_ids, _ = _add(wt, keys(100), flags=rt.WANT_PREFETCH, tokens=[rt.NO_TOKEN])
     ids, _ = _add(wt, keys(1, 2, 3), size=2048, tokens=[1, 2, 3])
+    assert wt.select(st, None, 0, 1)[0].tolist() == []  # cap 0 (maxWantsPerRound: 0) admits nothing
     adm, _, _, _, _ = wt.select(st, None, 2, 1)
     assert adm.tolist() == ids[:2].tolist()  # cap 2: requests before the prefetch
     wt.requeue(adm, False)

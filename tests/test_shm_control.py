@@ -28,8 +28,8 @@ def _rank(rank: int, world: int, port: int, q) -> None:
         from hlsjs_p2p_wrapper_amd.parallel.comm import DistComm
 
         comm = DistComm()
-        res = {"transport": comm.control_transport}
-        big = comm.SHM_SLOT_WORDS + 5
+        res = {"transport": comm.control_transport, "slot": comm.shm_slot_words}
+        big = comm.shm_slot_words + 5
         rounds = []
         for g in range(40):
             n = 0 if (g + rank) % 7 == 0 else (g * 13 + rank * 5) % 300
@@ -47,13 +47,17 @@ def _rank(rank: int, world: int, port: int, q) -> None:
             if g % 10 == 0:
                 comm.barrier()
         res["rounds_ok"] = all(rounds)
+        res["fallbacks"] = comm.control_fallbacks
         res["sum"] = comm.allreduce_sum(np.array([rank, 1], dtype=np.int64)).tolist()
         q.put((rank, res))
     finally:
         dist.destroy_process_group()
 
 
-def test_shm_control_allgather_matches_and_falls_back():
+def test_shm_control_allgather_matches_and_falls_back(monkeypatch):
+    """(The slot is sized through HLSP2P_SHM_SLOT_WORDS; the one oversized round is counted
+    on every rank, not silent.)"""
+    monkeypatch.setenv("HLSP2P_SHM_SLOT_WORDS", "2048")
     before = set(os.listdir("/dev/shm")) if os.path.isdir("/dev/shm") else set()
     world = 3
     ctx = mp.get_context("spawn")
@@ -68,6 +72,7 @@ def test_shm_control_allgather_matches_and_falls_back():
     for r in range(world):
         assert out[r]["transport"] == "shm"
         assert out[r]["rounds_ok"], r
+        assert out[r]["slot"] == 2048 and out[r]["fallbacks"] == 1
         assert out[r]["sum"] == [0 + 1 + 2, world]
     after = set(os.listdir("/dev/shm")) if os.path.isdir("/dev/shm") else set()
     assert not [n for n in after - before if n.startswith("hlsp2p_")]

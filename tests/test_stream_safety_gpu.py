@@ -1,0 +1,92 @@
+"""Stream-ordered lifetime of the swarm node's device tensors (stream-ordered
+allocation + events on cache buffers).
+
+The caching allocator returns a freed block to the pool of the stream it was allocated on
+without waiting for work other streams still have queued against it.  Round 3's 2-rank
+fault was exactly that: the per-entry CRC table, allocated on the default stream, was
+replaced from the node stream while a verify CRC that scatters into it was still queued
+there; the transmux's descriptor block (a default-stream allocation) took the freed block
+and the late scatter overwrote it.  These tests hold the node stream back with a device
+sleep so the queued scatter runs only after the default stream has reused whatever it can,
+then check a sentinel written on the default stream.
+"""
+import numpy as np
+import pytest
+import torch
+
+SENTINEL = 0x5A5A5A5A
+SLEEP_CYCLES = 200_000_000  # ~0.1 s of device time: the default stream runs first
+
+
+def _segments(arena, n, seg=4096):
+    gen = torch.Generator().manual_seed(3)
+    data = torch.randint(0, 256, (n * seg,), dtype=torch.uint8, generator=gen)
+    arena[:n * seg].copy_(data.to(arena.device))
+    offs = np.arange(n, dtype=np.int64) * seg
+    return offs, np.full(n, seg, dtype=np.int64)
+
+
+@pytest.mark.gpu
+def test_old_crc_table_pattern_is_detected(cuda):
+    """Positive control: the round-3 pattern (table allocated on the default stream,
+    replaced from the node stream without record_stream) lets a default-stream allocation
+    take the table's block while a scatter into it is still queued -- the sentinel is
+    overwritten.  Shows the check below can see the race."""
+    from hlsjs_p2p_wrapper_amd.ops import crc as _crc
+
+    torch.cuda.synchronize()
+    node_stream = torch.cuda.Stream(cuda)
+    arena = torch.zeros(1 << 20, dtype=torch.uint8, device=cuda)
+    offs, lens = _segments(arena, 64)
+    size = 4100  # an unusual block size: the reuse below finds this block, not another
+    table = torch.zeros(size, dtype=torch.int32, device=cuda)  # default-stream allocation
+    torch.cuda.synchronize()
+    with torch.cuda.stream(node_stream):
+        torch.cuda._sleep(SLEEP_CYCLES)
+        _crc.crc32_batch(arena, offs, lens, scatter_to=table, scatter_idx=np.arange(64))
+        new = torch.zeros(2 * size, dtype=torch.int32, device=cuda)
+        new[:size] = table
+        table = new  # the old block goes back to the default stream's pool right now
+    probe = torch.full((size,), SENTINEL, dtype=torch.int32, device=cuda)
+    torch.cuda.synchronize()
+    clobbered = int((probe != SENTINEL).sum())
+    if clobbered == 0:
+        pytest.skip("the allocator did not hand the freed block back (control inconclusive on this build)")
+    assert clobbered == 64  # exactly the scattered entries
+
+
+@pytest.mark.gpu
+def test_node_crc_table_grow_is_stream_safe(cuda):
+    """The node's own grow path: the same queued scatter, then ``_grow_crc``; no
+    default-stream allocation may receive the old table's block before the scatter ran."""
+    from hlsjs_p2p_wrapper_amd.agent.node import SwarmNode
+    from hlsjs_p2p_wrapper_amd.ops import crc as _crc
+
+    node = SwarmNode(device=str(cuda), cache_bytes=4 << 20, auto_tick=False)
+    size = node.crc_dev.numel()
+    assert size == 1024  # the small-cache table: a grow is reachable
+    offs, lens = _segments(node.arena, 64)
+    torch.cuda.synchronize()
+    with torch.cuda.stream(node.stream):  # as launch_round's phases run
+        torch.cuda._sleep(SLEEP_CYCLES)
+        _crc.crc32_batch(node.arena, offs, lens, scatter_to=node.crc_dev, scatter_idx=np.arange(64))
+        node._grow_crc(size + 1)
+    probes = [torch.full((size,), SENTINEL, dtype=torch.int32, device=cuda) for _ in range(8)]
+    torch.cuda.synchronize()
+    for p in probes:
+        assert int((p != SENTINEL).sum()) == 0
+    # and the grown table kept the scattered CRCs (copied on the node stream after the scatter)
+    want = np.array([_crc.crc32(node.arena[o:o + n].cpu()) for o, n in zip(offs, lens)], dtype=np.uint32)
+    got = node.crc_dev[:64].cpu().numpy().view(np.uint32)
+    assert np.array_equal(got, want)
+    assert node.crc_dev.numel() >= 2 * size
+
+
+@pytest.mark.gpu
+def test_node_crc_table_sized_for_the_arena(cuda):
+    """The table starts big enough that the hot path never grows it: 8 GiB of arena holds
+    >= 2^20 entries only below 8 KiB per segment."""
+    from hlsjs_p2p_wrapper_amd.agent.node import SwarmNode
+
+    node = SwarmNode(device=str(cuda), cache_bytes=1 << 30, auto_tick=False)
+    assert node.crc_dev.numel() == (1 << 30) // (8 << 10) + 1
