@@ -129,6 +129,10 @@ def parse():
                    help="live configs: one node round per this many wall milliseconds (paced)")
     p.add_argument("--playlist-steps", type=int, default=None,
                    help="size the players' DVR window for this many steps instead of --steps (soak analysis)")
+    p.add_argument("--fleet-payload", action="store_true",
+                   help="fleet players receive every fragment's bytes in onSuccess (gpuSwarm.fleetPayload: "
+                        "HBM gather + D2H + shared-memory ring per batch); off: the players get the "
+                        "transmux result rows only (the bytes stay in HBM)")
     p.add_argument("--verbose", action="store_true")
     return p.parse_args()
 
@@ -196,6 +200,8 @@ def _workload(args):
     if preset != "abr5":
         hls_config["startLevel"] = 0
     p2p_base = {"streamrootKey": "bench", "contentId": "bench-1080p"}
+    if args.fleet_payload:
+        p2p_base["gpuSwarm"] = {"fleetPayload": True}
     return preset, encrypted, seg_dur, desc, K, n_segments, W, origin_kwargs, hls_config, p2p_base
 
 
@@ -748,7 +754,8 @@ def _result(args, world, tot, max_s, origin, K, desc, encrypted, seg_dur, use_gp
 
 
 # per-rank diagnostics of the timed window, all-gathered as int64 milli-units (fixed order)
-PER_RANK_FIELDS = ("rank", "rounds", "step_ms", "wait_device_us", "control_us", "plan_us", "host_round_us",
+PER_RANK_FIELDS = ("rank", "rounds", "step_ms", "wait_device_us", "exchange_us", "control_us", "plan_us",
+                   "host_round_us",
                    "cdn_GBps", "cdn_dev_ms", "p2p_recv_MB", "p2p_sent_MB", "p2p_dev_ms", "p2p_GBps",
                    "p2p_links", "p2p_link_GBps", "transmux_dev_ms", "transmux_wait_us", "await_players_us",
                    "crc_failures", "control_fallbacks", "deferred", "inflight", "cu_reserve")
@@ -756,8 +763,10 @@ PER_RANK_FIELDS = ("rank", "rounds", "step_ms", "wait_device_us", "control_us", 
 
 def _per_rank(node, pipe, s0, s1, elapsed, steps, inflight, fleet_total=None, timers=None) -> np.ndarray:
     """This rank's timed-window diagnostics (``PER_RANK_FIELDS``): per ROUND host phases in
-    us (``wait_device`` = host blocked on the round's device event, ``control`` = control
-    all-gather + directory ingest, ``plan`` = plan_round + pins); the CDN rate over the
+    us (``wait_device`` = host blocked on the round's device event, ``exchange`` = posting
+    the data plane: microseconds for RCCL, which only enqueues, but the HIP-IPC rehearsal
+    plane blocks there on its peers' packing, ``control`` = control all-gather + directory
+    ingest, ``plan`` = plan_round + pins); the CDN rate over the
     window and the copy-stream (H2D) device ms per round; P2P received / sent MB per round,
     the node-stream exchange device ms per round (a peer's stall included), the received
     GB/s over that time, the source links per round and the GB/s per link (bytes per link
@@ -779,6 +788,7 @@ def _per_rank(node, pipe, s0, s1, elapsed, steps, inflight, fleet_total=None, ti
     vals = {
         "rank": node.rank, "rounds": rounds, "step_ms": elapsed * 1e3 / max(1, steps),
         "wait_device_us": tm.get("wait_device", 0.0) * 1e6 / rounds,
+        "exchange_us": tm.get("p2p_enqueue", 0.0) * 1e6 / rounds,
         "control_us": tm.get("control", 0.0) * 1e6 / rounds,
         "plan_us": tm.get("plan", 0.0) * 1e6 / rounds,
         "host_round_us": host_round * 1e6 / rounds,
@@ -803,8 +813,9 @@ def _per_rank(node, pipe, s0, s1, elapsed, steps, inflight, fleet_total=None, ti
 def _per_rank_dicts(parts, steps) -> list:
     """Decode the gathered rows; add each rank's ``bound`` label.
 
-    Rule: the host waited on the device for more than 30 % of a step (``wait_device`` per
-    round x rounds per step + the transmux wait) -> device-bound, by the busiest stream:
+    Rule: the host waited on the device for more than 30 % of a step (``wait_device`` and
+    ``exchange`` per round x rounds per step + the transmux wait) -> device-bound, by the
+    busiest stream:
     ``pcie`` (H2D copy stream), ``xgmi`` (the node stream's exchange), ``transmux`` (decrypt +
     demux); otherwise ``players`` when the fleet wait exceeds the own host work, else
     ``host``."""
@@ -818,7 +829,7 @@ def _per_rank_dicts(parts, steps) -> list:
                 d[k] = round(v, 3)
         step = max(d["step_ms"], 1e-9)
         rps = d["rounds"] / max(1, steps)
-        waited = (d["wait_device_us"] * rps + d["transmux_wait_us"]) / 1e3
+        waited = ((d["wait_device_us"] + d["exchange_us"]) * rps + d["transmux_wait_us"]) / 1e3
         busy = {"pcie": d["cdn_dev_ms"] * rps, "xgmi": d["p2p_dev_ms"] * rps, "transmux": d["transmux_dev_ms"]}
         if waited > 0.3 * step:
             d["bound"] = max(busy, key=busy.get)

@@ -790,8 +790,10 @@ class SwarmNode:
         if not len(all_wants):
             return h
         h.empty = False
-        plan = rt.plan_round(self.directory, all_wants, flags, self.world)
+        # only the rows this rank sends, receives or fetches (the full plan is identical on
+        # every rank; any_p2p says whether the round has transfers at all)
         me = self.rank
+        plan, any_p2p = rt.plan_round_for(self.directory, all_wants, flags, self.world, me)
         h.n_wants = len(all_wants)
         cdn_rows = plan[(plan[:, 5] == -1) & (plan[:, 6] == me)]
         if self._net_wants and self._wx:  # network-origin wants this rank must download first (STAGE rows)
@@ -828,7 +830,7 @@ class SwarmNode:
             # ---------------- 4. P2P phase: entered by EVERY rank when the (identical) plan
             # has any transfer, so a collective transport (the in-process hub) stays in step;
             # RCCL point-to-point with no local ops posts nothing
-            if bool((plan[:, 5] >= 0).any()):
+            if any_p2p:
                 self._p2p_phase(h, send_rows, recv_rows, send_eids)
             h.sent_bytes = int(send_rows[:, 4].sum()) if len(send_rows) else 0
             if self.is_cuda:

@@ -466,15 +466,23 @@ PYBIND11_MODULE(_runtime, m) {
     Arr<int64_t> flags(world);
     int64_t tot[3] = {0, 0, 0};
     bool all_leaving = true;
-    std::vector<int64_t> rows;
+    // pass 1: validate every header (nothing is applied from a round with a bad message) and
+    // size the output; pass 2: apply the deltas and write the want rows straight into it
+    int64_t n = 0;
     for (int r = 0; r < world; ++r) {
-      const Arr<int64_t>& m = parts[r];
-      const int64_t* p = m.data();
-      const int64_t size = m.size();
+      const int64_t* p = parts[r].data();
+      const int64_t size = parts[r].size();
       if (size < hdr_words || p[0] != magic) throw std::runtime_error("bad swarm control message");
       const int64_t nw = p[2], na = p[3], nr = p[4];
       if (nw < 0 || na < 0 || nr < 0 || hdr_words + 6 * nw + 5 * na + 4 * nr > size)
         throw std::runtime_error("truncated swarm control message");
+      n += nw;
+    }
+    Arr<int64_t> out({n, int64_t(8)});
+    int64_t* o = out.mutable_data();
+    for (int r = 0; r < world; ++r) {
+      const int64_t* p = parts[r].data();
+      const int64_t nw = p[2], na = p[3], nr = p[4];
       flags.mutable_data()[r] = p[1];
       all_leaving = all_leaving && p[5] != 0;
       tot[0] += p[7];
@@ -485,18 +493,20 @@ PYBIND11_MODULE(_runtime, m) {
       const int64_t* rm = a + 5 * na;
       for (int64_t i = 0; i < na; ++i) d.apply_add(r, key_from(a + 5 * i), a[5 * i + 4]);
       for (int64_t i = 0; i < nr; ++i) d.apply_remove(r, key_from(rm + 4 * i));
-      for (int64_t i = 0; i < nw; ++i) {
+      for (int64_t i = 0; i < nw; ++i, o += 8) {
         const int64_t* x = w + 6 * i;
         // want word: want_id | force_cdn << 62 | not_staged << 61 | staging << 60 -> WantFlag bits
-        const int64_t id = x[5] & ((int64_t(1) << 60) - 1);
-        const int64_t wflags = ((x[5] >> 62) & 1 ? kForceCdn : 0) | ((x[5] >> 61) & 1 ? kNotStaged : 0) |
-                               ((x[5] >> 60) & 1 ? kStaging : 0);
-        rows.insert(rows.end(), {x[0], x[1], x[2], x[3], x[4], id, r, wflags});
+        o[0] = x[0];
+        o[1] = x[1];
+        o[2] = x[2];
+        o[3] = x[3];
+        o[4] = x[4];
+        o[5] = x[5] & ((int64_t(1) << 60) - 1);
+        o[6] = r;
+        o[7] = ((x[5] >> 62) & 1 ? kForceCdn : 0) | ((x[5] >> 61) & 1 ? kNotStaged : 0) |
+               ((x[5] >> 60) & 1 ? kStaging : 0);
       }
     }
-    const int64_t n = static_cast<int64_t>(rows.size() / 8);
-    Arr<int64_t> out({n, int64_t(8)});
-    if (n) std::memcpy(out.mutable_data(), rows.data(), rows.size() * sizeof(int64_t));
     Arr<int64_t> totals(3);
     std::memcpy(totals.mutable_data(), tot, sizeof(tot));
     return py::make_tuple(out, flags, all_leaving, totals);
@@ -504,9 +514,17 @@ PYBIND11_MODULE(_runtime, m) {
   // wants: int64[n, 8] = (key4, size, want_id, rank, want_flags); flags int64[world]
   // -> int64[m, 10] = (key4, size, src, dst, want_id, seeded, reserved); src -1 = CDN fetch,
   // -2 = stage (download from a network origin into host memory for a later round)
-  m.def("plan_round", [](const Directory& d, Arr<int64_t> wants, Arr<int64_t> flags, int world) {
+  // plan_round_for: the same plan, but only the rows this rank takes part in (src == me or
+  // dst == me, canonical order kept) plus whether the round has any P2P transfer at all
+  // (every rank enters the exchange then).  At 8 ranks a rank needs ~1/4 of the rows: the
+  // rest would be built into numpy and masked away in Python every round.
+  auto plan_rows = [](const Directory& d, const Arr<int64_t>& wants, const Arr<int64_t>& flags, int world,
+                      int me) {
     const int64_t n = wants.size() / 8;
+    if (flags.size() != world) throw std::invalid_argument("flags must have world entries");
     std::vector<Want> w(n);
+    std::vector<Transfer> t;
+    std::vector<int64_t> f;
     const int64_t* p = wants.data();
     for (int64_t i = 0; i < n; ++i) {
       w[i].key = key_from(p + 8 * i);
@@ -516,17 +534,32 @@ PYBIND11_MODULE(_runtime, m) {
       w[i].flags = p[8 * i + 7];
       if (w[i].rank < 0 || w[i].rank >= world) throw std::invalid_argument("want rank out of range");
     }
-    if (flags.size() != world) throw std::invalid_argument("flags must have world entries");
-    std::vector<int64_t> f(flags.data(), flags.data() + world);
-    std::vector<Transfer> t = plan_round(d, w, f, world);
-    Arr<int64_t> out({int64_t(t.size()), int64_t(10)});
-    int64_t* o = out.mutable_data();
-    for (size_t i = 0; i < t.size(); ++i) {
-      int64_t* r = o + 10 * i;
-      r[0] = t[i].key.swarm; r[1] = t[i].key.level; r[2] = t[i].key.url_id; r[3] = t[i].key.sn;
-      r[4] = t[i].size; r[5] = t[i].src; r[6] = t[i].dst; r[7] = t[i].want_id; r[8] = t[i].seeded; r[9] = 0;
+    f.assign(flags.data(), flags.data() + world);
+    plan_round_into(d, w.data(), w.size(), f, world, &t);
+    bool any_p2p = false;
+    int64_t m = 0;
+    for (const Transfer& x : t) {
+      any_p2p = any_p2p || x.src >= 0;
+      if (me < 0 || x.src == me || x.dst == me) ++m;
     }
-    return out;
+    Arr<int64_t> out({m, int64_t(10)});
+    int64_t* o = out.mutable_data();
+    for (const Transfer& x : t) {
+      if (me >= 0 && x.src != me && x.dst != me) continue;
+      o[0] = x.key.swarm; o[1] = x.key.level; o[2] = x.key.url_id; o[3] = x.key.sn;
+      o[4] = x.size; o[5] = x.src; o[6] = x.dst; o[7] = x.want_id; o[8] = x.seeded; o[9] = 0;
+      o += 10;
+    }
+    return std::make_pair(out, any_p2p);
+  };
+  m.def("plan_round", [plan_rows](const Directory& d, Arr<int64_t> wants, Arr<int64_t> flags, int world) {
+    return plan_rows(d, wants, flags, world, -1).first;
+  });
+  m.def("plan_round_for", [plan_rows](const Directory& d, Arr<int64_t> wants, Arr<int64_t> flags, int world,
+                                      int me) {
+    if (me < 0 || me >= world) throw std::invalid_argument("rank out of range");
+    auto r = plan_rows(d, wants, flags, world, me);
+    return py::make_tuple(r.first, r.second);
   });
   // CPU-mode CDN phase: copy origin byte ranges (raw host addresses, as the want table holds
   // them) into the node's host arena at `dst_base + dst_off[i]` (bounds-checked against cap)

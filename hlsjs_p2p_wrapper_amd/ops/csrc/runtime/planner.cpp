@@ -1,56 +1,188 @@
 #include "planner.hpp"
 
 #include <algorithm>
+#include <mutex>
 #include <stdexcept>
 
 namespace hlsp2p {
 
+Directory::Directory() { rehash(1024); }
+
+void Directory::rehash(size_t cap) {
+  std::vector<Slot> old;
+  old.swap(slots_);
+  slots_.assign(cap, Slot{});
+  mask_ = cap - 1;
+  size_ = 0;
+  for (const Slot& s : old) {
+    if (s.e.holders == 0) continue;
+    size_t i = home(s.key);
+    while (slots_[i].e.holders != 0) i = (i + 1) & mask_;
+    slots_[i] = s;
+    ++size_;
+  }
+}
+
 void Directory::apply_add(int rank, const SegKey& k, int64_t length) {
-  DirEntry& e = map_[k];
-  e.holders |= (uint64_t(1) << rank);
-  e.length = length;
+  if (size_t(size_ + 1) * 2 > slots_.size()) rehash(slots_.size() * 2);
+  size_t i = home(k);
+  while (slots_[i].e.holders != 0 && !(slots_[i].key == k)) i = (i + 1) & mask_;
+  Slot& s = slots_[i];
+  if (s.e.holders == 0) {
+    s.key = k;
+    ++size_;
+  }
+  s.e.holders |= (uint64_t(1) << rank);
+  s.e.length = length;
+}
+
+// backward-shift deletion: pull later members of the probe run into the hole so every key
+// stays reachable from its home slot without tombstones
+void Directory::erase_at(size_t i) {
+  size_t j = i;
+  for (;;) {
+    j = (j + 1) & mask_;
+    if (slots_[j].e.holders == 0) break;
+    const size_t k = home(slots_[j].key);
+    // slot j may move to i iff its home k is not cyclically inside (i, j]
+    const bool stays = (i <= j) ? (i < k && k <= j) : (i < k || k <= j);
+    if (stays) continue;
+    slots_[i] = slots_[j];
+    i = j;
+  }
+  slots_[i] = Slot{};
+  --size_;
 }
 
 void Directory::apply_remove(int rank, const SegKey& k) {
-  auto it = map_.find(k);
-  if (it == map_.end()) return;
-  it->second.holders &= ~(uint64_t(1) << rank);
-  if (it->second.holders == 0) map_.erase(it);
+  size_t i = home(k);
+  while (slots_[i].e.holders != 0) {
+    if (slots_[i].key == k) {
+      slots_[i].e.holders &= ~(uint64_t(1) << rank);
+      if (slots_[i].e.holders == 0) {
+        slots_[i].e.holders = 1;  // still occupied while erase_at shifts the run
+        erase_at(i);
+      }
+      return;
+    }
+    i = (i + 1) & mask_;
+  }
 }
 
 void Directory::drop_rank(int rank) {
   const uint64_t mask = ~(uint64_t(1) << rank);
-  for (auto it = map_.begin(); it != map_.end();) {
-    it->second.holders &= mask;
-    if (it->second.holders == 0)
-      it = map_.erase(it);
-    else
-      ++it;
-  }
+  for (Slot& s : slots_) s.e.holders &= mask;
+  rehash(slots_.size());  // drops the emptied entries, re-packs the probe runs
 }
 
 const DirEntry* Directory::find(const SegKey& k) const {
-  auto it = map_.find(k);
-  return it == map_.end() ? nullptr : &it->second;
+  size_t i = home(k);
+  while (slots_[i].e.holders != 0) {
+    if (slots_[i].key == k) return &slots_[i].e;
+    i = (i + 1) & mask_;
+  }
+  return nullptr;
 }
 
-std::vector<Transfer> plan_round(const Directory& dir, const std::vector<Want>& wants_in,
-                                 const std::vector<int64_t>& flags, int world) {
+namespace {
+// Working storage of plan_round: every vector keeps its capacity from round to round, so a
+// warm round allocates (and page-faults) nothing -- at 8 ranks x 512 wants a fresh ~1 MB of
+// vectors per call cost ~40 % of the planner's time.  One process-wide instance behind a
+// mutex (in-process swarms plan from several threads): a thread_local one measured ~35 %
+// slower inside the dlopen-ed module (every access through the TLS wrapper).
+struct PlanScratch {
+  std::vector<Want> wants;
+  std::vector<int32_t> tab;
+  std::vector<SegKey> gkey;
+  std::vector<uint32_t> gcount, gid, gord, gpos;
+  std::vector<int64_t> link, send_total, cdn_total, seeded;
+  std::vector<Transfer> cdn, p2p, sorted;
+  std::vector<size_t> members, unserved;
+  std::vector<uint32_t> start, split, fill;
+};
+PlanScratch g_scratch;
+std::mutex g_scratch_mu;
+}  // namespace
+
+void plan_round_into(const Directory& dir, const Want* wants_in, size_t n_in, const std::vector<int64_t>& flags,
+                     int world, std::vector<Transfer>* out_rows) {
   if (world <= 0 || world > kMaxRanks) throw std::invalid_argument("world size out of range");
-  std::vector<Want> wants(wants_in);
-  std::stable_sort(wants.begin(), wants.end(), [](const Want& a, const Want& b) {
-    if (!(a.key == b.key)) return a.key < b.key;
-    if (a.rank != b.rank) return a.rank < b.rank;
-    return a.want_id < b.want_id;
-  });
+  if (flags.size() < size_t(world)) throw std::invalid_argument("flags must have world entries");
+  std::lock_guard<std::mutex> lock(g_scratch_mu);
+  PlanScratch& S = g_scratch;
+  // Wants in (key, rank, want id) order -- a total order, so every rank gets the same plan
+  // -- without a comparison sort of all n wants (8 ranks x 512 wants: ~0.4 ms): group by key
+  // with a hash table (n is 8x the distinct keys when every rank wants the same segments),
+  // sort only the distinct keys (already ascending in the common case: players ask for
+  // consecutive sns), place each want in its group's slot range, and order each group by
+  // (rank, want id) with an insertion sort (a group holds at most one want per rank).
+  const size_t n = n_in;
+  std::vector<Want>& wants = S.wants;
+  wants.resize(n);
+  {
+    size_t cap = 16;
+    while (cap < 2 * n) cap <<= 1;
+    const size_t mask = cap - 1;
+    std::vector<int32_t>& tab = S.tab;
+    tab.assign(cap, -1);
+    std::vector<SegKey>& gkey = S.gkey;
+    std::vector<uint32_t>& gcount = S.gcount;
+    std::vector<uint32_t>& gid = S.gid;
+    gkey.clear();
+    gcount.clear();
+    gid.resize(n);
+    for (size_t i = 0; i < n; ++i) {
+      const SegKey& k = wants_in[i].key;
+      size_t h = DirKeyHash{}(k) & mask;
+      while (tab[h] >= 0 && !(gkey[size_t(tab[h])] == k)) h = (h + 1) & mask;
+      if (tab[h] < 0) {
+        tab[h] = static_cast<int32_t>(gkey.size());
+        gkey.push_back(k);
+        gcount.push_back(0);
+      }
+      gid[i] = static_cast<uint32_t>(tab[h]);
+      ++gcount[gid[i]];
+    }
+    const size_t G = gkey.size();
+    std::vector<uint32_t>& gord = S.gord;
+    gord.resize(G);
+    for (size_t g = 0; g < G; ++g) gord[g] = static_cast<uint32_t>(g);
+    auto key_less = [&](uint32_t a, uint32_t b) { return gkey[a] < gkey[b]; };
+    if (!std::is_sorted(gord.begin(), gord.end(), key_less)) std::sort(gord.begin(), gord.end(), key_less);
+    std::vector<uint32_t>& gpos = S.gpos;
+    gpos.resize(G);
+    uint32_t pos = 0;
+    for (uint32_t g : gord) {
+      gpos[g] = pos;
+      pos += gcount[g];
+    }
+    for (size_t i = 0; i < n; ++i) wants[gpos[gid[i]]++] = wants_in[i];
+    auto within = [](const Want& a, const Want& b) {
+      return a.rank != b.rank ? a.rank < b.rank : a.want_id < b.want_id;
+    };
+    size_t a = 0;
+    for (uint32_t g : gord) {
+      const size_t b = a + gcount[g];
+      for (size_t x = a + 1; x < b; ++x)  // insertion sort: already ordered for rank-major input
+        for (size_t y = x; y > a && within(wants[y], wants[y - 1]); --y) std::swap(wants[y], wants[y - 1]);
+      a = b;
+    }
+  }
   auto flag = [&](int r, int64_t f) { return (flags[r] & f) != 0; };
   // may want `wt` receive a peer copy of `size` bytes?  Staged (or in-process) wants always
   // announce the size they reserved; a not-staged one only once it reserved at least that
   auto fits_recv = [](const Want& wt, int64_t size) { return !(wt.flags & kNotStaged) || wt.size >= size; };
 
-  std::vector<int64_t> link(size_t(world) * world, 0);  // bytes src->dst this round
-  std::vector<int64_t> send_total(world, 0), cdn_total(world, 0);
-  std::vector<Transfer> cdn, p2p;
+  std::vector<int64_t>& link = S.link;  // bytes src->dst this round
+  link.assign(size_t(world) * world, 0);
+  std::vector<int64_t>& send_total = S.send_total;
+  std::vector<int64_t>& cdn_total = S.cdn_total;
+  send_total.assign(world, 0);
+  cdn_total.assign(world, 0);
+  std::vector<Transfer>& cdn = S.cdn;
+  std::vector<Transfer>& p2p = S.p2p;
+  cdn.clear();
+  p2p.clear();
   // a CDN fetch for want w, or its STAGE row when w's body is not in host memory yet
   auto cdn_or_stage = [&](const Want& wt, const SegKey& key) {
     if (wt.flags & kStaging) return;  // its download is running: nothing to plan yet
@@ -62,12 +194,15 @@ std::vector<Transfer> plan_round(const Directory& dir, const std::vector<Want>& 
   // forwards in the same round ("seeding"); assigned after the pass (run-affine, below)
   struct SeedGroup {
     SegKey key;
-    size_t i, j;
-    std::vector<size_t> unserved;
+    size_t a, b;     // its unserved wants: members[a, b)
     uint64_t cands;  // wanting ranks that may upload (staged ones only, when any is)
     bool staged;     // the seeder has the body in host memory (else it only stages it)
   };
   std::vector<SeedGroup> seeds;
+  seeds.reserve(64);
+  std::vector<size_t>& members = S.members;  // every seed group's unserved want indices, back to back
+  std::vector<size_t>& unserved = S.unserved;  // reused per key
+  members.clear();
 
   size_t i = 0;
   while (i < wants.size()) {
@@ -80,7 +215,7 @@ std::vector<Transfer> plan_round(const Directory& dir, const std::vector<Want>& 
       for (int r = 0; r < world; ++r)
         if (((de->holders >> r) & 1u) && flag(r, kOnline) && flag(r, kUploadOn)) holders |= uint64_t(1) << r;
     }
-    std::vector<size_t> unserved;
+    unserved.clear();
     for (size_t w = i; w < j; ++w) {
       const Want& wt = wants[w];
       const int d = wt.rank;
@@ -125,15 +260,19 @@ std::vector<Transfer> plan_round(const Directory& dir, const std::vector<Want>& 
           if (!(wants[w].flags & kNotStaged)) ready |= uint64_t(1) << wants[w].rank;
           staging = staging || (wants[w].flags & kStaging);
         }
-        if ((cands & ready) || !staging)  // else a wanter is downloading it: all wait this round
-          seeds.push_back({key, i, j, std::move(unserved), (cands & ready) ? (cands & ready) : cands,
+        if ((cands & ready) || !staging) {  // else a wanter is downloading it: all wait this round
+          const size_t a = members.size();
+          members.insert(members.end(), unserved.begin(), unserved.end());
+          seeds.push_back({key, a, members.size(), (cands & ready) ? (cands & ready) : cands,
                            (cands & ready) != 0});  // seeder chosen below
+        }
       } else {
         for (size_t w : unserved) cdn_or_stage(wants[w], key);
       }
     }
     i = j;
   }
+  const size_t p2p_main = p2p.size();  // holder transfers, generated in key order
   // Seeder assignment, run-affine: consecutive keys (sorted: same track, ascending sn) go
   // to the same rank until it holds its share of the round's seed bytes.  Load stays
   // balanced, and each rank's CDN fetches form ONE contiguous sn run, i.e. one merged
@@ -143,14 +282,15 @@ std::vector<Transfer> plan_round(const Directory& dir, const std::vector<Want>& 
     uint64_t all = 0;
     for (const auto& g : seeds) {
       int64_t sz = 0;  // a not-yet-staged network want does not know its size (0)
-      for (size_t w : g.unserved) sz = std::max(sz, wants[w].size);
+      for (size_t m = g.a; m < g.b; ++m) sz = std::max(sz, wants[members[m]].size);
       seed_bytes += sz;
       all |= g.cands;
     }
     int nseed = 0;
     for (int r = 0; r < world; ++r) nseed += int((all >> r) & 1u);
     const int64_t quota = (seed_bytes + nseed - 1) / std::max(nseed, 1);
-    std::vector<int64_t> seeded(world, 0);
+    std::vector<int64_t>& seeded = S.seeded;
+    seeded.assign(world, 0);
     int cur = -1;
     for (const auto& g : seeds) {
       int seeder = -1;
@@ -172,23 +312,23 @@ std::vector<Transfer> plan_round(const Directory& dir, const std::vector<Want>& 
       // the seeder's want carries the size every forwarded copy has (a wanter that has not
       // staged the body itself may not know it)
       const Want* own = nullptr;
-      for (size_t w : g.unserved)
-        if (wants[w].rank == seeder && own == nullptr) own = &wants[w];
+      for (size_t m = g.a; m < g.b; ++m)
+        if (wants[members[m]].rank == seeder && own == nullptr) own = &wants[members[m]];
       const int64_t sz = own->size;
       seeded[seeder] += sz;
       if (!g.staged) {  // nobody has the body yet: the seeder stages it, the rest wait
         cdn.push_back({g.key, sz, kStage, seeder, own->want_id, 0});
         continue;
       }
-      for (size_t w : g.unserved) {
-        const Want& wt = wants[w];
+      for (size_t m = g.a; m < g.b; ++m) {
+        const Want& wt = wants[members[m]];
         if (wt.rank == seeder) {
           cdn.push_back({g.key, wt.size, kCdn, seeder, wt.want_id, 0});
           cdn_total[seeder] += wt.size;
         }
       }
-      for (size_t w : g.unserved) {
-        const Want& wt = wants[w];
+      for (size_t m = g.a; m < g.b; ++m) {
+        const Want& wt = wants[members[m]];
         if (wt.rank == seeder) continue;
         if (!fits_recv(wt, sz)) continue;  // (see above) it gets the seeder's copy next round
         p2p.push_back({g.key, sz, seeder, wt.rank, wt.want_id, 1});
@@ -197,15 +337,48 @@ std::vector<Transfer> plan_round(const Directory& dir, const std::vector<Want>& 
       }
     }
   }
-  std::stable_sort(p2p.begin(), p2p.end(), [](const Transfer& a, const Transfer& b) {
-    if (a.src != b.src) return a.src < b.src;
-    if (a.dst != b.dst) return a.dst < b.dst;
-    return a.key < b.key;
-  });
-  std::vector<Transfer> out;
+  // P2P rows grouped by (src, dst), key order inside a pair.  Both parts of `p2p` (holder
+  // transfers, then seeded forwards) were generated in ascending key order and a pair sees a
+  // key at most once, so a stable counting sort by pair plus one merge of the two runs
+  // inside each pair gives exactly the (src, dst, key) order, in O(n).
+  {
+    const size_t P = size_t(world) * world;
+    std::vector<uint32_t>& start = S.start;
+    std::vector<uint32_t>& split = S.split;
+    start.assign(P + 1, 0);
+    split.assign(P, 0);
+    for (const Transfer& t : p2p) ++start[size_t(t.src) * world + t.dst + 1];
+    for (size_t b = 0; b < P; ++b) start[b + 1] += start[b];
+    std::vector<uint32_t>& fill = S.fill;
+    fill.assign(start.begin(), start.end() - 1);
+    std::vector<Transfer>& sorted = S.sorted;
+    sorted.resize(p2p.size());
+    for (size_t x = 0; x < p2p.size(); ++x) {
+      const size_t b = size_t(p2p[x].src) * world + p2p[x].dst;
+      if (x < p2p_main) ++split[b];
+      sorted[fill[b]++] = p2p[x];
+    }
+    auto by_key = [](const Transfer& a, const Transfer& b) {
+      return !(a.key == b.key) ? a.key < b.key : a.want_id < b.want_id;
+    };
+    for (size_t b = 0; b < P; ++b) {
+      const size_t lo = start[b], mid = lo + split[b], hi = start[b + 1];
+      if (mid > lo && mid < hi)
+        std::inplace_merge(sorted.begin() + lo, sorted.begin() + mid, sorted.begin() + hi, by_key);
+    }
+    p2p.swap(sorted);
+  }
+  std::vector<Transfer>& out = *out_rows;
+  out.clear();
   out.reserve(cdn.size() + p2p.size());
   out.insert(out.end(), cdn.begin(), cdn.end());
   out.insert(out.end(), p2p.begin(), p2p.end());
+}
+
+std::vector<Transfer> plan_round(const Directory& dir, const std::vector<Want>& wants_in,
+                                 const std::vector<int64_t>& flags, int world) {
+  std::vector<Transfer> out;
+  plan_round_into(dir, wants_in.data(), wants_in.size(), flags, world, &out);
   return out;
 }
 

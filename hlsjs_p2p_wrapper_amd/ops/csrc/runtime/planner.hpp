@@ -65,16 +65,43 @@ struct Transfer {  // one segment moving src -> dst
   int32_t seeded;   // 1: src fetched it from the CDN this round (forwarding)
 };
 
+// The replicated "who holds what" map.  Every rank applies every rank's adds and removes each
+// round (8 ranks x hundreds of deltas), so this is an open-addressing table (linear probing,
+// backward-shift deletion, load <= 1/2) of 32-byte slots in one array: no node allocation
+// per insert or free per erase, one or two cache lines per probe.  A slot is empty iff its
+// holder mask is 0 (an entry is erased the moment its last holder drops it).
+// One multiply-xorshift: the directory and the planner's key grouping hash a key per
+// delta / want (~10^4 a round at 8 ranks), so the two-round mix of SegKeyHash is not paid
+// here.  Consecutive sns (the common key stream) land in distinct slots.
+struct DirKeyHash {
+  size_t operator()(const SegKey& k) const {
+    uint64_t x = ((uint64_t(k.swarm) << 32) | k.level) * 0x9E3779B97F4A7C15ull;
+    x ^= ((uint64_t(k.url_id) << 32) | k.sn);
+    x *= 0xD6E8FEB86659FD93ull;
+    return static_cast<size_t>(x ^ (x >> 32));
+  }
+};
+
 class Directory {
  public:
+  Directory();
   void apply_add(int rank, const SegKey& k, int64_t length);
   void apply_remove(int rank, const SegKey& k);
   void drop_rank(int rank);  // a rank left: forget everything it held
   const DirEntry* find(const SegKey& k) const;
-  int64_t size() const { return static_cast<int64_t>(map_.size()); }
+  int64_t size() const { return size_; }
 
  private:
-  std::unordered_map<SegKey, DirEntry, SegKeyHash> map_;
+  struct Slot {
+    SegKey key;
+    DirEntry e;
+  };
+  size_t home(const SegKey& k) const { return DirKeyHash{}(k) & mask_; }
+  void rehash(size_t cap);
+  void erase_at(size_t i);
+  std::vector<Slot> slots_;
+  size_t mask_ = 0;
+  int64_t size_ = 0;
 };
 
 // Returns every transfer of the round (CDN fetches have src = -1), in a canonical order:
@@ -82,5 +109,8 @@ class Directory {
 // in which both sides pack / unpack their per-pair buffers.
 std::vector<Transfer> plan_round(const Directory& dir, const std::vector<Want>& wants,
                                  const std::vector<int64_t>& rank_flags, int world);
+// The same plan written into `out` (cleared first; its capacity is reused round to round).
+void plan_round_into(const Directory& dir, const Want* wants, size_t n, const std::vector<int64_t>& rank_flags,
+                     int world, std::vector<Transfer>* out);
 
 }  // namespace hlsp2p
