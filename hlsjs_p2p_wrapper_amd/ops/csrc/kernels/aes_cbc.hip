@@ -32,8 +32,6 @@
 #include "common.h"
 
 #include "aes_dev.h"
-#include "demux_dev.h"
-#include "ts_scatter.h"
 
 namespace hlsp2p {
 namespace dev {
@@ -41,113 +39,18 @@ namespace dev {
 constexpr int kAesThreads = kAesImageThreads;
 constexpr int kAesWgPerCu = 1;
 constexpr int kBlk = 4;  // blocks per lane per chunk (chunk = 64 * kBlk blocks): independent chains
-static_assert(64 * kBlk == kScatterChunkBlocks + 1, "scatter chunks: one lookahead block per iteration");
-
-// Scatter epilogue (the scatter demux, ts_scatter.hip): instead of writing the plaintext,
-// every block writes the bytes of it that are TS payload straight to their elementary-stream
-// position.  place[pkt] = (bias, lo | hi << 16): payload bytes y in [lo, hi) of packet pkt go
-// to es + es_off[seg] + bias + y.
-struct AesScatter {
-  const uint2* place;        // per packet slot (the demux's 256-packet block grid)
-  const int64_t* pkt_base;   // [nseg] first packet slot of the segment
-  const int64_t* pkt_slots;  // [nseg] packet slots of the segment
-  uint8_t* es;
-  const int64_t* es_off;     // [nseg]
-  uint32_t* seam;            // [packet slots][2] head / tail seam bytes
-};
-
-// Scatter epilogue of one wave iteration.  The scatter decrypt walks a segment in chunks of
-// kScatterChunkBlocks = 255 blocks but decrypts 256: chain j, lane l holds block b0 + 64j + l,
-// and the last (chain N-1, lane 63) is a LOOKAHEAD: the next chunk owns it, it only lends its
-// first bytes.  Every owned block writes the payload bytes of the (at most two) packets it
-// overlaps: per packet run [s, e) in the block,
-//  * the aligned ES dwords whose first byte is in [s, e) and whose four bytes are all payload
-//    of the run -- one buffer_store_dwordx4 for a block inside a payload, else up to three
-//    dword stores; up to 3 bytes may come from the next block (lane l + 1 by DPP, or the next
-//    chain's lane 0);
-//  * the run's SEAM bytes, which share an ES dword with the previous / next same-class
-//    packet: the head (until the run's first aligned dword) and the tail (after its last
-//    full dword), each <= 3 bytes, as one word into seam[2 * pkt + {0, 1}]; tsx_seam_kernel
-//    (ts_scatter.hip) stores them as bytes.
-// No byte stores and no divergent loops here: the bulk decrypt is VALU/LDS bound.
-__device__ __forceinline__ uint32_t sel4(uint32_t a, uint32_t b, uint32_t c, uint32_t d, int i) {
-  return i == 0 ? a : i == 1 ? b : i == 2 ? c : d;
-}
-// the 4 bytes at offset u (0..15) of the 20 bytes w0..w3, nx
-__device__ __forceinline__ uint32_t funnel(const uint32_t* w, uint32_t nx, int u) {
-  const int i = u >> 2;
-  return __builtin_amdgcn_alignbyte(sel4(w[1], w[2], w[3], nx, i), sel4(w[0], w[1], w[2], w[3], i),
-                                    static_cast<uint32_t>(u & 3));
-}
-
-template <int N>
-__device__ __forceinline__ void scatter_epilogue(const uint32_t (&w)[N][4], int64_t b0, int64_t nblk, int lane,
-                                                 const uint2* __restrict__ place, int64_t pbase, int64_t slots,
-                                                 __amdgpu_buffer_rsrc_t es_rsrc, uint32_t* __restrict__ seam) {
-  typedef unsigned int v4u __attribute__((ext_vector_type(4)));
-#pragma unroll
-  for (int j = 0; j < N; ++j) {
-    const int64_t b = b0 + 64 * j;
-    // next block's first word: lane l + 1 (wave_shl:1), or the next chain's lane 0 -- read with
-    // every lane active (a DPP source lane outside EXEC would read as 0)
-    uint32_t nx = static_cast<uint32_t>(__builtin_amdgcn_update_dpp(0, static_cast<int>(w[j][0]), 0x130, 0xf, 0xf, false));
-    if (j + 1 < N) {
-      const uint32_t first = static_cast<uint32_t>(__builtin_amdgcn_readlane(static_cast<int>(w[j + 1][0]), 0));
-      nx = lane == 63 ? first : nx;
-    }
-    const bool own = b < nblk && !(j == N - 1 && lane == 63);
-    const int x0 = static_cast<int>(16 * b);
-    const int p = x0 / demux::kPkt;
-#pragma unroll
-    for (int r = 0; r < 2; ++r) {
-      const int pk = p + r, P = demux::kPkt * pk;
-      const bool any = own && pk < slots && P < x0 + 16;
-      const uint2 pl = any ? place[pbase + pk] : make_uint2(0, 0);
-      const int lo = static_cast<int>(pl.y & 0xffff), hi = static_cast<int>(pl.y >> 16);
-      const int RS = P + lo, RE = P + hi;
-      const int s = x0 > RS ? x0 : RS, e = x0 + 16 < RE ? x0 + 16 : RE;
-      if (!(any && s < e)) continue;
-      const int dbias = static_cast<int>(pl.x) - P;  // ES offset of segment byte x = dbias + x
-      const int xf = s + ((-(dbias + s)) & 3);       // first owned aligned dword's source byte
-      const int lim = e < RE - 3 ? e : RE - 3;       // owned: x < e and x + 4 <= RE
-      const int n = xf < lim ? (lim - xf + 3) >> 2 : 0;
-      const int u0 = xf - x0;
-      const uint32_t sh = static_cast<uint32_t>(u0 & 3);
-      const uint32_t g0 = __builtin_amdgcn_alignbyte(w[j][1], w[j][0], sh),
-                     g1 = __builtin_amdgcn_alignbyte(w[j][2], w[j][1], sh),
-                     g2 = __builtin_amdgcn_alignbyte(w[j][3], w[j][2], sh),
-                     g3 = __builtin_amdgcn_alignbyte(nx, w[j][3], sh);
-      if (n == 4) {  // u0 < 4: the whole dword window of the block
-        const v4u q = {g0, g1, g2, g3};
-        __builtin_amdgcn_raw_buffer_store_b128(q, es_rsrc, dbias + xf, 0, 0);
-      } else {
-        const int i0 = u0 >> 2;
-#pragma unroll
-        for (int k = 0; k < 3; ++k)
-          if (k < n) __builtin_amdgcn_raw_buffer_store_b32(sel4(g0, g1, g2, g3, i0 + k), es_rsrc, dbias + xf + 4 * k, 0, 0);
-      }
-      const int hh = (-(dbias + RS)) & 3, h = hh < RE - RS ? hh : RE - RS;
-      if (s == RS && h > 0) seam[2 * (pbase + pk)] = funnel(w[j], nx, RS - x0);
-      const int T = RS + h + ((RE - RS - h) & ~3);
-      if (T < RE && T >= s && T < e) seam[2 * (pbase + pk) + 1] = funnel(w[j], nx, T - x0);
-    }
-  }
-}
 
 // tdl: little-endian Td0 (256 words); isb: inverse S-box (256 bytes)
 // drk: per-segment little-endian equivalent-inverse-cipher round keys (44 words)
 // chunk_prefix: exclusive prefix of per-segment 256-block chunks (one chunk = one wave
 //   iteration: lane l decrypts blocks 64j + l, j < kBlk, so every load/store instruction
 //   moves 1 KB contiguous); waves never straddle segments
-// kScatter: the payload bytes go to their ES positions (AesScatter); dst / out_len are unused
-//   (out_len is the scatter demux's, computed before this launch)
-template <bool kScatter>
 __global__ __launch_bounds__(kAesThreads, 1) void aes128_cbc_decrypt_kernel(
     const uint8_t* __restrict__ src, uint8_t* __restrict__ dst, const int64_t* __restrict__ src_off,
     const int64_t* __restrict__ dst_off, const int64_t* __restrict__ blk_prefix,
     const int64_t* __restrict__ chunk_prefix, const uint32_t* __restrict__ drk, const uint32_t* __restrict__ ivw,
     const uint32_t* __restrict__ tdl_g, const uint8_t* __restrict__ isb_g, int64_t* __restrict__ out_len, int nseg,
-    int64_t total_chunks, int64_t per_wg, AesScatter sc) {
+    int64_t total_chunks, int64_t per_wg) {
   __shared__ uint32_t s_tab[kTdDwords + kIsDwords];  // 160 KiB (layout above)
   const int tid = threadIdx.x;
   aes_image_fill(s_tab, tdl_g, isb_g, tid);
@@ -164,8 +67,7 @@ __global__ __launch_bounds__(kAesThreads, 1) void aes128_cbc_decrypt_kernel(
   // segment state is wave-uniform (SGPRs): round keys come in by scalar loads
   int cur = -1;
   uint32_t rk[44];
-  int64_t so = 0, dof = 0, cstart = 0, cend = 0, nblk = 0, pbase = 0, slots = 0;
-  uint8_t* esb = nullptr;
+  int64_t so = 0, dof = 0, cstart = 0, cend = 0, nblk = 0;
   for (int64_t ch = uniform64(begin + (tid >> 6)); ch < end; ch += kWaves) {
     if (cur < 0 || ch >= cend) {
       cur = cur < 0 ? find_seg_wave(chunk_prefix, nseg, ch)  // whole wave active: ch is uniform
@@ -177,14 +79,8 @@ __global__ __launch_bounds__(kAesThreads, 1) void aes128_cbc_decrypt_kernel(
       cstart = chunk_prefix[cur];
       cend = chunk_prefix[cur + 1];
       nblk = blk_prefix[cur + 1] - blk_prefix[cur];
-      if (kScatter) {
-        pbase = sc.pkt_base[cur];
-        slots = sc.pkt_slots[cur];
-        esb = sc.es + sc.es_off[cur];
-      }
     }
-    // this lane's first block (scatter: chunks of kScatterChunkBlocks, the last lane a lookahead)
-    const int64_t b0 = (ch - cstart) * (kScatter ? kScatterChunkBlocks : 64 * kBlk) + lane;
+    const int64_t b0 = (ch - cstart) * (64 * kBlk) + lane;  // this lane's first block
     const uint4* cs = reinterpret_cast<const uint4*>(src + so);
     uint4 c[kBlk], pv[kBlk];
 #pragma unroll
@@ -203,25 +99,15 @@ __global__ __launch_bounds__(kAesThreads, 1) void aes128_cbc_decrypt_kernel(
       st[j][0] = c[j].x ^ rk[0]; st[j][1] = c[j].y ^ rk[1]; st[j][2] = c[j].z ^ rk[2]; st[j][3] = c[j].w ^ rk[3];
     }
     AES_ROUNDS_PIPELINED(kBlk, st, rk)
-    if (kScatter) {
-      uint32_t w[kBlk][4];
+    uint4* ds = reinterpret_cast<uint4*>(dst + dof);
 #pragma unroll
-      for (int j = 0; j < kBlk; ++j) {
-        AES_FINAL(st[j][0], st[j][1], st[j][2], st[j][3], w[j][0], w[j][1], w[j][2], w[j][3], rk + 40, pv[j])
-      }
-      scatter_epilogue<kBlk>(w, b0, nblk, lane, sc.place, pbase, slots,
-                             __builtin_amdgcn_make_buffer_rsrc(esb, 0, 0x7fffffff, 0x00020000), sc.seam);
-    } else {
-      uint4* ds = reinterpret_cast<uint4*>(dst + dof);
-#pragma unroll
-      for (int j = 0; j < kBlk; ++j) {
-        uint32_t o0, o1, o2, o3;
-        AES_FINAL(st[j][0], st[j][1], st[j][2], st[j][3], o0, o1, o2, o3, rk + 40, pv[j])
-        const uint4 p = make_uint4(o0, o1, o2, o3);
-        const int64_t b = b0 + 64 * j;
-        if (b < nblk) ds[b] = p;
-        if (b == nblk - 1) out_len[cur] = pkcs7_len(p, nblk * 16);
-      }
+    for (int j = 0; j < kBlk; ++j) {
+      uint32_t o0, o1, o2, o3;
+      AES_FINAL(st[j][0], st[j][1], st[j][2], st[j][3], o0, o1, o2, o3, rk + 40, pv[j])
+      const uint4 p = make_uint4(o0, o1, o2, o3);
+      const int64_t b = b0 + 64 * j;
+      if (b < nblk) ds[b] = p;
+      if (b == nblk - 1) out_len[cur] = pkcs7_len(p, nblk * 16);
     }
   }
 }
@@ -248,26 +134,9 @@ hipError_t launch_aes128_cbc_decrypt(const uint8_t* src, uint8_t* dst, const int
   if (total_chunks <= 0) return hipSuccess;
   int64_t grid, per_wg;
   aes_grid(total_chunks, num_cu, grid, per_wg);
-  hipLaunchKernelGGL(aes128_cbc_decrypt_kernel<false>, dim3(static_cast<unsigned>(grid)), dim3(kAesThreads), 0, stream,
+  hipLaunchKernelGGL(aes128_cbc_decrypt_kernel, dim3(static_cast<unsigned>(grid)), dim3(kAesThreads), 0, stream,
                      src, dst, src_off, dst_off, blk_prefix, chunk_prefix, drk, ivw, tdl, isb, out_len, nseg,
-                     total_chunks, per_wg, AesScatter{});
-  return hipGetLastError();
-}
-
-// The scatter demux's decrypt (ts_scatter.hip): payload dwords straight to the ES buffer, seam
-// bytes to `seam` for tsx_seam_kernel.  chunk_prefix counts kScatterChunkBlocks-block chunks.
-hipError_t launch_aes128_cbc_scatter(const uint8_t* src, const int64_t* src_off, const int64_t* blk_prefix,
-                                     const int64_t* chunk_prefix, const uint32_t* drk, const uint32_t* ivw,
-                                     const uint32_t* tdl, const uint8_t* isb, const uint2* place,
-                                     const int64_t* pkt_base, const int64_t* pkt_slots, uint8_t* es,
-                                     const int64_t* es_off, uint32_t* seam, int nseg, int64_t total_chunks,
-                                     int num_cu, hipStream_t stream) {
-  if (total_chunks <= 0) return hipSuccess;
-  int64_t grid, per_wg;
-  aes_grid(total_chunks, num_cu, grid, per_wg);
-  hipLaunchKernelGGL(aes128_cbc_decrypt_kernel<true>, dim3(static_cast<unsigned>(grid)), dim3(kAesThreads), 0, stream,
-                     src, nullptr, src_off, src_off, blk_prefix, chunk_prefix, drk, ivw, tdl, isb, nullptr, nseg,
-                     total_chunks, per_wg, AesScatter{place, pkt_base, pkt_slots, es, es_off, seam});
+                     total_chunks, per_wg);
   return hipGetLastError();
 }
 

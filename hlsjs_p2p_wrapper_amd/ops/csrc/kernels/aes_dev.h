@@ -1,15 +1,10 @@
-// AES-128 decryption building blocks shared by the CDNA4 kernels that decrypt (aes_cbc.hip:
-// the bulk CBC decrypt, plain or scattering payloads; ts_scatter.hip: the header / PES /
-// PSI decrypts of the scatter demux).
+// AES-128 decryption building blocks of the CDNA4 bulk CBC decrypt (aes_cbc.hip).
 //
-// Two table forms:
-//  * the per-CU 160 KiB LDS IMAGE (bulk decrypt, 1024-thread workgroups): Td0..Td3 in
-//    little-endian column form, 32 lane copies per row, plus 32 copies of InvSbox — every
-//    lookup of a 32-lane group is bank-conflict free (layout in aes_cbc.hip's header).
-//    Used through the macros below, which expect `s_bytes`, `td_base[4]` and `is_base` in
-//    scope (aes_image_fill + aes_image_bases set them up).
-//  * a SMALL table (Td0L 1 KiB + InvSbox 256 B in LDS, Td1..Td3 by rotation): for sparse
-//    work where few lanes decrypt a few blocks each (aes_dec_small).
+// The per-CU 160 KiB LDS IMAGE (1024-thread workgroups): Td0..Td3 in little-endian column
+// form, 32 lane copies per row, plus 32 copies of InvSbox — every lookup of a 32-lane group
+// is bank-conflict free (layout in aes_cbc.hip's header).  Used through the macros below,
+// which expect `s_bytes`, `td_base[4]` and `is_base` in scope (aes_image_fill +
+// aes_image_bases set them up).
 //
 // Round keys: per segment 44 little-endian words of the equivalent inverse cipher (host
 // pre-swapped): [0..3] initial whitening, [4r..4r+3] round r (1..9), [40..43] last round.
@@ -129,46 +124,6 @@ __device__ __forceinline__ int64_t uniform64(int64_t v) {
   const uint32_t lo = __builtin_amdgcn_readfirstlane(static_cast<uint32_t>(v));
   const uint32_t hi = __builtin_amdgcn_readfirstlane(static_cast<uint32_t>(static_cast<uint64_t>(v) >> 32));
   return static_cast<int64_t>((static_cast<uint64_t>(hi) << 32) | lo);
-}
-
-// ---- small-table form: one block, one lane (Td0L + InvSbox in LDS, Td1..3 by rotation)
-__device__ __forceinline__ uint32_t aes_rotl8(uint32_t v, int t) {
-  return t ? __builtin_amdgcn_alignbit(v, v, 32 - 8 * t) : v;
-}
-
-// Load the small tables into LDS (any block size; the caller synchronises).
-__device__ __forceinline__ void aes_small_fill(uint32_t* s_td, uint8_t* s_is, const uint32_t* __restrict__ tdl_g,
-                                               const uint8_t* __restrict__ isb_g, int tid, int nthreads) {
-  for (int i = tid; i < 256; i += nthreads) {
-    s_td[i] = tdl_g[i];
-    s_is[i] = isb_g[i];
-  }
-}
-
-// P = D_K(C) ^ prev for one 16-byte block (all 10 rounds; rk: the segment's 44 words).
-__device__ __forceinline__ uint4 aes_dec_small(const uint32_t* s_td, const uint8_t* s_is,
-                                               const uint32_t* __restrict__ rk, uint4 c, uint4 prev) {
-  uint32_t s[4] = {c.x ^ rk[0], c.y ^ rk[1], c.z ^ rk[2], c.w ^ rk[3]};
-#define AES_SB(w, k) (((w) >> (8 * (k))) & 0xffu)
-#pragma unroll
-  for (int r = 1; r < 10; ++r) {
-    uint32_t t[4];
-#pragma unroll
-    for (int i = 0; i < 4; ++i)
-      t[i] = s_td[AES_SB(s[i], 0)] ^ aes_rotl8(s_td[AES_SB(s[(i + 3) & 3], 1)], 1) ^
-             aes_rotl8(s_td[AES_SB(s[(i + 2) & 3], 2)], 2) ^ aes_rotl8(s_td[AES_SB(s[(i + 1) & 3], 3)], 3) ^
-             rk[4 * r + i];
-#pragma unroll
-    for (int i = 0; i < 4; ++i) s[i] = t[i];
-  }
-  uint32_t o[4];
-#pragma unroll
-  for (int i = 0; i < 4; ++i)
-    o[i] = (uint32_t(s_is[AES_SB(s[i], 0)]) | (uint32_t(s_is[AES_SB(s[(i + 3) & 3], 1)]) << 8) |
-            (uint32_t(s_is[AES_SB(s[(i + 2) & 3], 2)]) << 16) | (uint32_t(s_is[AES_SB(s[(i + 1) & 3], 3)]) << 24)) ^
-           rk[40 + i];
-#undef AES_SB
-  return make_uint4(o[0] ^ prev.x, o[1] ^ prev.y, o[2] ^ prev.z, o[3] ^ prev.w);
 }
 
 }  // namespace dev

@@ -20,10 +20,6 @@
 #include <cstring>
 #include <vector>
 
-#include "transmux_args.h"
-#include "ts_onepass.h"
-#include "ts_scatter.h"
-
 namespace hlsp2p {
 namespace dev {
 int aes_chunk_blocks();
@@ -78,40 +74,14 @@ class Desc {
   Tensor dev_;
 };
 
-// The demux of the encrypted group (HLSP2P_DEMUX):
-//  * fourpass: decrypt to a plaintext buffer, then the psi / scan / prefix / gather sequence
-//    (classes packed);
-//  * onepass: decrypt, then ts_onepass_kernel (scan + prefix + gather in one kernel with a
-//    decoupled look-back, ES classes in three regions per segment; measured slower,
-//    profiles/r3_transmux_fused_vs_split.md);
-//  * scatter: no plaintext buffer -- header-only decrypt, scan, prefix, place, then the bulk
-//    decrypt stores payload bytes at their ES positions (ts_scatter.hip).
-// Clear segments always take the four-pass sequence.
-enum DemuxMode { kFourpass = 0, kOnepass = 1, kScatterDemux = 2 };
-int g_demux = -1;
-
-int demux_mode() {
-  if (g_demux < 0) {
-    const char* v = std::getenv("HLSP2P_DEMUX");
-    g_demux = v == nullptr ? kFourpass
-              : std::strcmp(v, "onepass") == 0 ? kOnepass
-              : std::strcmp(v, "scatter") == 0 ? kScatterDemux
-              : kFourpass;
-  }
-  return g_demux;
-}
-bool use_onepass() { return demux_mode() == kOnepass; }
-const char* demux_name(int m) { return m == kOnepass ? "onepass" : m == kScatterDemux ? "scatter" : "fourpass"; }
-
 struct DemuxPlan {
   std::vector<int64_t> idx, off, len, cap, es_off, es_cap, blk_prefix;
   int64_t es_bytes = 0, total_blocks = 0;
-  int64_t d_off = -1, d_len = -1, d_bp = -1, d_eo = -1, d_ec = -1;
+  int64_t d_off = -1, d_len = -1, d_bp = -1, d_eo = -1;
 };
 
 void plan_demux(DemuxPlan& p) {
   const size_t B = p.idx.size();
-  const int64_t regions = use_onepass() ? 3 : 1;  // one-pass: video | audio | id3 regions
   p.es_off.resize(B);
   p.es_cap.resize(B);
   p.blk_prefix.assign(B + 1, 0);
@@ -119,9 +89,8 @@ void plan_demux(DemuxPlan& p) {
   for (size_t i = 0; i < B; ++i) {
     p.es_off[i] = pos;
     p.es_cap[i] = align_up(std::max<int64_t>(p.cap[i], 1));
-    pos += regions * p.es_cap[i];
-    const int64_t bp = use_onepass() ? hlsp2p::dev::onepass_block_packets() : 256;
-    const int64_t blocks = ((p.cap[i] + kPacket - 1) / kPacket + bp - 1) / bp;
+    pos += p.es_cap[i];
+    const int64_t blocks = ((p.cap[i] + kPacket - 1) / kPacket + 255) / 256;  // 256-packet demux blocks
     p.blk_prefix[i + 1] = p.blk_prefix[i] + blocks;
   }
   p.es_bytes = pos + kAlign;
@@ -160,118 +129,6 @@ int decrypt_cus(int device) {
 
 void hip_ok(hipError_t e, const char* what) { TORCH_CHECK(e == hipSuccess, what, " failed: ", hipGetErrorString(e)); }
 
-// Split kernel sequence by default (decrypt / psi / scan / prefix / gather: measured faster on
-// MI355X, profiles/r3_transmux_fused_vs_split.md); HLSP2P_TRANSMUX=fused runs the
-// wave-specialised fused kernel (transmux_fused.hip) instead.
-int g_mode = -1;  // 1 fused, 0 split; -1: read HLSP2P_TRANSMUX on first use
-
-bool use_fused() {
-  if (g_mode < 0) {
-    const char* v = std::getenv("HLSP2P_TRANSMUX");
-    g_mode = (v != nullptr && std::strcmp(v, "fused") == 0) ? 1 : 0;
-  }
-  return g_mode == 1;
-}
-
-constexpr int64_t kProfSlots = 512 * 16;  // >= grid x 16 role timers
-
-// The fused decrypt + demux batch (transmux_fused.hip): one descriptor H2D, two memsets for
-// the hand-off words and the -1 tables, the persistent fused kernel + the per-segment tail
-// kernel, the info rows and plaintext lengths D2H.  One group covering the whole batch.
-py::tuple transmux_launch_fused(Tensor src, const int64_t* so, const int64_t* nb, const uint8_t* en,
-                                const uint32_t* drk, const uint8_t* iv, int64_t B, Tensor td0, Tensor isb,
-                                int64_t max_pes, int device, hipStream_t st) {
-  const auto dev_opts = torch::TensorOptions().device(torch::kCUDA, device);
-  const int64_t tile_bytes = hlsp2p::dev::transmux_tile_bytes();
-  std::vector<int64_t> v_so(so, so + B), v_nb(nb, nb + B), tile_prefix(B + 1, 0), es_off(B), es_cap(B);
-  std::vector<uint8_t> v_en(en, en + B);
-  int64_t pos = 0;
-  for (int64_t i = 0; i < B; ++i) {
-    tile_prefix[i + 1] = tile_prefix[i] + (nb[i] + tile_bytes - 1) / tile_bytes;
-    es_cap[i] = align_up(std::max<int64_t>(nb[i], 1));
-    es_off[i] = pos;
-    pos += 3 * es_cap[i];  // [video | audio scratch | id3 scratch]
-  }
-  const int64_t tiles = tile_prefix[B];
-  std::vector<uint32_t> drk_rot(drk, drk + B * 44);  // rounds 1..9 rotated left by 24
-  for (int64_t i = 0; i < B; ++i)
-    for (int k = 4; k < 40; ++k) {
-      const uint32_t v = drk_rot[i * 44 + k];
-      drk_rot[i * 44 + k] = (v << 24) | (v >> 8);
-    }
-  Desc desc;
-  const int64_t d_so = desc.add(v_so), d_nb = desc.add(v_nb), d_en = desc.add(v_en), d_drr = desc.add(drk_rot),
-                d_drk = desc.add(drk, B * 44 * 4), d_iv = desc.add(iv, B * 16), d_tp = desc.add(tile_prefix),
-                d_eo = desc.add(es_off), d_ec = desc.add(es_cap);
-  desc.upload(device);
-  Tensor es = torch::empty({pos + kAlign}, dev_opts.dtype(torch::kUInt8));
-  // zeroed words: info [B, 24] | look [tiles, 3] | psi [B, 2] | ticket, timeout (+ pad)
-  const int64_t z_info = 0, z_look = B * kInfo, z_psi = z_look + tiles * 3, z_tk = z_psi + 2 * B;
-  // HLSP2P_FUSED_PROF=1: per-workgroup role timers after the hand-off words (diagnostics)
-  const char* prof_env = std::getenv("HLSP2P_FUSED_PROF");
-  const bool prof = prof_env != nullptr && std::atoi(prof_env) != 0;
-  const int64_t z_prof = z_tk + 2, z_words = z_prof + (prof ? kProfSlots : 0);
-  Tensor zw = torch::empty({z_words}, dev_opts.dtype(torch::kInt64));
-  hip_ok(hipMemsetAsync(zw.data_ptr(), 0, static_cast<size_t>(z_words * 8), st), "hipMemsetAsync");
-  // -1 words: pes [B, 3, max_pes, 3] | lastpes [tiles, 3, 2]
-  const int64_t m_pes = B * 3 * max_pes * 3, m_words = m_pes + tiles * 6;
-  Tensor mw = torch::empty({std::max<int64_t>(m_words, 1)}, dev_opts.dtype(torch::kInt64));
-  hip_ok(hipMemsetAsync(mw.data_ptr(), 0xff, static_cast<size_t>(std::max<int64_t>(m_words, 1) * 8), st),
-         "hipMemsetAsync");
-  Tensor out_len = torch::empty({std::max<int64_t>(B, 1)}, dev_opts.dtype(torch::kInt64));
-  int64_t* zp = zw.data_ptr<int64_t>();
-  int64_t* mp = mw.data_ptr<int64_t>();
-  hlsp2p::dev::TransmuxArgs a{};
-  a.src = static_cast<const uint8_t*>(src.data_ptr());
-  a.src_off = desc.at<int64_t>(d_so);
-  a.src_len = desc.at<int64_t>(d_nb);
-  a.enc = desc.at<uint8_t>(d_en);
-  a.drk = desc.at<uint32_t>(d_drk);
-  a.drk_rot = desc.at<uint32_t>(d_drr);
-  a.ivw = desc.at<uint32_t>(d_iv);
-  a.tdl = static_cast<const uint32_t*>(td0.data_ptr());
-  a.isb = static_cast<const uint8_t*>(isb.data_ptr());
-  a.tile_prefix = desc.at<int64_t>(d_tp);
-  a.es = es.data_ptr<uint8_t>();
-  a.es_off = desc.at<int64_t>(d_eo);
-  a.es_cap = desc.at<int64_t>(d_ec);
-  a.pes = mp;
-  a.info = zp + z_info;
-  a.out_len = out_len.data_ptr<int64_t>();
-  a.look = reinterpret_cast<uint64_t*>(zp + z_look);
-  a.psi = reinterpret_cast<uint64_t*>(zp + z_psi);
-  a.lastpes = mp + m_pes;
-  a.ticket = reinterpret_cast<unsigned int*>(zp + z_tk);
-  a.timeout = reinterpret_cast<unsigned int*>(zp + z_tk) + 1;
-  a.prof = prof ? reinterpret_cast<uint64_t*>(zp + z_prof) : nullptr;
-  a.max_pes = max_pes;
-  {
-    const char* d = std::getenv("HLSP2P_FUSED_DIAG");  // timing decomposition only
-    a.diag = d != nullptr ? std::atoi(d) : 0;
-    const char* f = std::getenv("HLSP2P_FUSED_FLAGS");  // A/B experiments only
-    a.flags = f != nullptr ? std::atoi(f) : 0;
-  }
-  a.nseg = static_cast<int>(B);
-  a.total_tiles = tiles;
-  hip_ok(hlsp2p::dev::launch_transmux_fused(a, decrypt_cus(device), st), "transmux_fused");
-  Tensor info = zw.narrow(0, z_info, B * kInfo).view({B, kInfo});
-  Tensor pes = mw.narrow(0, 0, m_pes).view({B, 3, max_pes, 3});
-  // host block: info rows | plaintext lengths (one pinned allocation, two D2H on `st`)
-  Tensor host = torch::empty({B * kInfo + B + 1}, torch::TensorOptions().dtype(torch::kInt64).pinned_memory(true));
-  Tensor hinfo = host.narrow(0, 0, B * kInfo).view({B, kInfo});
-  hinfo.copy_(info, /*non_blocking=*/true);
-  Tensor hl = host.narrow(0, B * kInfo, B);
-  hl.copy_(out_len.narrow(0, 0, B), /*non_blocking=*/true);
-  I64 idx(static_cast<py::ssize_t>(B)), eo(static_cast<py::ssize_t>(B));
-  for (int64_t i = 0; i < B; ++i) idx.mutable_data()[i] = i;
-  std::memcpy(eo.mutable_data(), es_off.data(), static_cast<size_t>(B * 8));
-  py::list groups;
-  groups.append(py::make_tuple(idx, info, pes, es, eo, hinfo, py::cast(hl)));
-  // keep-alive: the descriptor block's device copy, the hand-off words (a timeout word != 0
-  // in zw[z_tk] + 4 bytes means a spin gave up: tests read it through `keep`)
-  return py::make_tuple(groups, py::make_tuple(zw, mw, out_len, desc.device()), host);
-}
-
 // src: uint8 device buffer holding every payload at src_off[i] (16-byte aligned) with
 // nbytes[i] bytes; enc[i] != 0 -> AES-128-CBC with round keys drk[i] (44 little-endian
 // words, equivalent inverse cipher) and IV iv[i]; encrypted sizes must be positive
@@ -303,11 +160,9 @@ py::tuple transmux_launch(Tensor src, I64 src_off, I64 nbytes, py::array_t<uint8
   }
   const auto dev_opts = torch::TensorOptions().device(torch::kCUDA, device);
   hipStream_t st = c10::hip::getCurrentHIPStream(device).stream();
-  if (use_fused())
-    return transmux_launch_fused(src, so, nb, en, drk.data(), iv.data(), B, td0, isb, max_pes, device, st);
 
   // ---- plans: AES over the encrypted segments, demux per group
-  std::vector<int64_t> a_so, a_do, a_bp{0}, a_cp{0}, a_sp{0}, a_hp{0};
+  std::vector<int64_t> a_so, a_do, a_bp{0}, a_cp{0};
   std::vector<uint32_t> a_drk;
   std::vector<uint8_t> a_iv;
   DemuxPlan pe, pc;
@@ -324,11 +179,6 @@ py::tuple transmux_launch(Tensor src, I64 src_off, I64 nbytes, py::array_t<uint8
       const int64_t blocks = nb[i] / 16;
       a_bp.push_back(a_bp.back() + blocks);
       a_cp.push_back(a_cp.back() + (blocks + chunk - 1) / chunk);
-      constexpr int64_t sc = hlsp2p::dev::kScatterChunkBlocks;  // scatter decrypt chunks
-      a_sp.push_back(a_sp.back() + (blocks + sc - 1) / sc);
-      const int64_t groups = (nb[i] / kPacket + hlsp2p::dev::kScatterGroupPackets - 1) /
-                             hlsp2p::dev::kScatterGroupPackets;  // scatter demux header chunks
-      a_hp.push_back(a_hp.back() + (groups + hlsp2p::dev::kScatterChunkGroups - 1) / hlsp2p::dev::kScatterChunkGroups);
       a_drk.insert(a_drk.end(), drk.data(i, 0), drk.data(i, 0) + 44);
       a_iv.insert(a_iv.end(), iv.data(i, 0), iv.data(i, 0) + 16);
     } else {
@@ -341,16 +191,10 @@ py::tuple transmux_launch(Tensor src, I64 src_off, I64 nbytes, py::array_t<uint8
   const int64_t ne = static_cast<int64_t>(pe.idx.size()), nc = static_cast<int64_t>(pc.idx.size());
   plan_demux(pe);
   plan_demux(pc);
-  const bool scatter = ne > 0 && demux_mode() == kScatterDemux;
-  std::vector<int64_t> pkt_base(ne), pkt_slots(ne);
-  for (int64_t i = 0; i < ne; ++i) {
-    pkt_base[i] = pe.blk_prefix[i] * 256;
-    pkt_slots[i] = (pe.blk_prefix[i + 1] - pe.blk_prefix[i]) * 256;
-  }
 
   // ---- every descriptor of the batch in one staging block, one H2D
   Desc desc;
-  int64_t d_so = -1, d_do = -1, d_bp = -1, d_cp = -1, d_drk = -1, d_iv = -1, d_hp = -1, d_pb = -1, d_ps = -1, d_sp = -1;
+  int64_t d_so = -1, d_do = -1, d_bp = -1, d_cp = -1, d_drk = -1, d_iv = -1;
   if (ne) {
     d_so = desc.add(a_so);
     d_do = desc.add(a_do);
@@ -361,20 +205,12 @@ py::tuple transmux_launch(Tensor src, I64 src_off, I64 nbytes, py::array_t<uint8
     pe.d_off = desc.add(pe.off);
     pe.d_bp = desc.add(pe.blk_prefix);
     pe.d_eo = desc.add(pe.es_off);
-    pe.d_ec = desc.add(pe.es_cap);
-    if (scatter) {
-      d_sp = desc.add(a_sp);
-      d_hp = desc.add(a_hp);
-      d_pb = desc.add(pkt_base);
-      d_ps = desc.add(pkt_slots);
-    }
   }
   if (nc) {
     pc.d_off = desc.add(pc.off);
     pc.d_len = desc.add(pc.len);
     pc.d_bp = desc.add(pc.blk_prefix);
     pc.d_eo = desc.add(pc.es_off);
-    pc.d_ec = desc.add(pc.es_cap);
   }
   desc.upload(device);
 
@@ -382,7 +218,7 @@ py::tuple transmux_launch(Tensor src, I64 src_off, I64 nbytes, py::array_t<uint8
   Tensor host = torch::empty({(ne + nc) * kInfo + ne + 1}, torch::TensorOptions().dtype(torch::kInt64).pinned_memory(true));
   Tensor dec, out_len;
   if (ne) out_len = torch::empty({ne}, dev_opts.dtype(torch::kInt64));
-  if (ne && !scatter) {
+  if (ne) {
     dec = torch::empty({dec_pos + kAlign}, dev_opts.dtype(torch::kUInt8));
     hip_ok(hlsp2p::dev::launch_aes128_cbc_decrypt(
                static_cast<const uint8_t*>(src.data_ptr()), static_cast<uint8_t*>(dec.data_ptr()),
@@ -406,81 +242,17 @@ py::tuple transmux_launch(Tensor src, I64 src_off, I64 nbytes, py::array_t<uint8
     Tensor es = torch::empty({p.es_bytes}, dev_opts.dtype(torch::kUInt8));
     Tensor info = torch::empty({n, kInfo}, dev_opts.dtype(torch::kInt64));
     Tensor pes = torch::empty({n, 3, max_pes, 3}, dev_opts.dtype(torch::kInt64));
-    if (g == 0 && scatter) {
-      Tensor hdr = torch::empty({nb_blocks * 256}, dev_opts.dtype(torch::kInt32));
-      Tensor meta = torch::empty({nb_blocks * 256}, dev_opts.dtype(torch::kInt32));
-      Tensor pts = torch::empty({nb_blocks * 256 * 2}, dev_opts.dtype(torch::kInt64));
-      Tensor aux = torch::empty({nb_blocks * 12 + n * 7}, dev_opts.dtype(torch::kInt32));
-      Tensor place = torch::empty({nb_blocks * 256}, dev_opts.dtype(torch::kInt64));
-      Tensor seam = torch::empty({nb_blocks * 256}, dev_opts.dtype(torch::kInt64));  // 2 words per packet
-      hlsp2p::dev::ScatterArgs sa{};
-      sa.src = static_cast<const uint8_t*>(src.data_ptr());
-      sa.src_off = desc.at<int64_t>(d_so);
-      sa.aes_blk = desc.at<int64_t>(d_bp);
-      sa.aes_chunks = desc.at<int64_t>(d_sp);
-      sa.hdr_chunks = desc.at<int64_t>(d_hp);
-      sa.drk = desc.at<uint32_t>(d_drk);
-      sa.ivw = desc.at<uint32_t>(d_iv);
-      sa.tdl = static_cast<const uint32_t*>(td0.data_ptr());
-      sa.isb = static_cast<const uint8_t*>(isb.data_ptr());
-      sa.blk_prefix = desc.at<int64_t>(p.d_bp);
-      sa.pkt_base = desc.at<int64_t>(d_pb);
-      sa.pkt_slots = desc.at<int64_t>(d_ps);
-      sa.hdr = reinterpret_cast<uint32_t*>(hdr.data_ptr<int32_t>());
-      sa.meta = reinterpret_cast<uint32_t*>(meta.data_ptr<int32_t>());
-      sa.pts_dts = pts.data_ptr<int64_t>();
-      sa.aux = aux.data_ptr<int32_t>();
-      sa.place = reinterpret_cast<uint2*>(place.data_ptr<int64_t>());
-      sa.seam = reinterpret_cast<uint32_t*>(seam.data_ptr<int64_t>());
-      sa.es = es.data_ptr<uint8_t>();
-      sa.es_off = desc.at<int64_t>(p.d_eo);
-      sa.pes = pes.data_ptr<int64_t>();
-      sa.info = info.data_ptr<int64_t>();
-      sa.out_len = out_len.data_ptr<int64_t>();
-      sa.max_pes = max_pes;
-      sa.nseg = static_cast<int>(n);
-      sa.total_blocks = p.total_blocks;
-      sa.aes_total_chunks = a_sp.back();
-      sa.hdr_total_chunks = a_hp.back();
-      hip_ok(hlsp2p::dev::launch_ts_scatter(sa, decrypt_cus(device), st), "ts_scatter");
-      keep.append(py::make_tuple(hdr, meta, pts, aux, place, seam));
-    } else if (use_onepass()) {
-      // zeroed: look-back granules [blocks x 3] | ticket + timeout; -1: last PES per block [blocks x 6]
-      Tensor zw = torch::empty({nb_blocks * 3 + 1}, dev_opts.dtype(torch::kInt64));
-      hip_ok(hipMemsetAsync(zw.data_ptr(), 0, static_cast<size_t>((nb_blocks * 3 + 1) * 8), st), "hipMemsetAsync");
-      Tensor lastpes = torch::empty({nb_blocks * 6}, dev_opts.dtype(torch::kInt64));
-      hip_ok(hipMemsetAsync(lastpes.data_ptr(), 0xff, static_cast<size_t>(nb_blocks * 6 * 8), st), "hipMemsetAsync");
-      hlsp2p::dev::OnepassArgs oa{};
-      oa.buf = buf;
-      oa.seg_off = desc.at<int64_t>(p.d_off);
-      oa.seg_len = lens;
-      oa.blk_prefix = desc.at<int64_t>(p.d_bp);
-      oa.nseg = static_cast<int>(n);
-      oa.total_blocks = p.total_blocks;
-      oa.es = es.data_ptr<uint8_t>();
-      oa.es_off = desc.at<int64_t>(p.d_eo);
-      oa.es_cap = desc.at<int64_t>(p.d_ec);
-      oa.pes = pes.data_ptr<int64_t>();
-      oa.max_pes = max_pes;
-      oa.info = info.data_ptr<int64_t>();
-      oa.look = reinterpret_cast<uint64_t*>(zw.data_ptr<int64_t>());
-      oa.lastpes = lastpes.data_ptr<int64_t>();
-      oa.ticket = reinterpret_cast<unsigned int*>(zw.data_ptr<int64_t>() + nb_blocks * 3);
-      hip_ok(hlsp2p::dev::launch_ts_onepass(oa, st), "ts_onepass");
-      keep.append(py::make_tuple(zw, lastpes));
-    } else {
-      Tensor meta = torch::empty({nb_blocks * 256}, dev_opts.dtype(torch::kInt32));
-      Tensor pts = torch::empty({nb_blocks * 256 * 2}, dev_opts.dtype(torch::kInt64));
-      Tensor aux = torch::empty({nb_blocks * 12 + n * 7}, dev_opts.dtype(torch::kInt32));
-      hip_ok(hlsp2p::dev::launch_ts_demux(buf, desc.at<int64_t>(p.d_off), lens, desc.at<int64_t>(p.d_bp),
-                                          static_cast<int>(n), p.total_blocks,
-                                          reinterpret_cast<uint32_t*>(meta.data_ptr<int32_t>()),
-                                          pts.data_ptr<int64_t>(), aux.data_ptr<int32_t>(), es.data_ptr<uint8_t>(),
-                                          desc.at<int64_t>(p.d_eo), pes.data_ptr<int64_t>(), max_pes,
-                                          info.data_ptr<int64_t>(), st),
-             "ts_demux");
-      keep.append(py::make_tuple(meta, pts, aux));
-    }
+    Tensor meta = torch::empty({nb_blocks * 256}, dev_opts.dtype(torch::kInt32));
+    Tensor pts = torch::empty({nb_blocks * 256 * 2}, dev_opts.dtype(torch::kInt64));
+    Tensor aux = torch::empty({nb_blocks * 12 + n * 7}, dev_opts.dtype(torch::kInt32));
+    hip_ok(hlsp2p::dev::launch_ts_demux(buf, desc.at<int64_t>(p.d_off), lens, desc.at<int64_t>(p.d_bp),
+                                        static_cast<int>(n), p.total_blocks,
+                                        reinterpret_cast<uint32_t*>(meta.data_ptr<int32_t>()),
+                                        pts.data_ptr<int64_t>(), aux.data_ptr<int32_t>(), es.data_ptr<uint8_t>(),
+                                        desc.at<int64_t>(p.d_eo), pes.data_ptr<int64_t>(), max_pes,
+                                        info.data_ptr<int64_t>(), st),
+           "ts_demux");
+    keep.append(py::make_tuple(meta, pts, aux));
     // D2H through torch's copy so the caching host allocator records the use of the pinned
     // block on `st` (it is not handed out again before the copy has run, even if the batch
     // is dropped uncompleted)
@@ -513,18 +285,6 @@ void register_transmux(py::module& m) {
   m.def("set_cu_reserve", [](int n) { g_cu_reserve = std::max(0, n); }, py::arg("n"),
         "CUs the persistent decrypt grid leaves free for concurrent (RCCL) kernels");
   m.def("cu_reserve", [] { return g_cu_reserve; });
-  m.def("transmux_mode", [] { return std::string(use_fused() ? "fused" : "split"); });
-  m.def("set_transmux_mode", [](const std::string& m) {
-    TORCH_CHECK_VALUE(m == "fused" || m == "split", "transmux mode must be 'fused' or 'split'");
-    g_mode = m == "fused" ? 1 : 0;
-  });
-  m.def("demux_mode", [] { return std::string(demux_name(demux_mode())); });
-  m.def("set_demux_mode", [](const std::string& m) {
-    TORCH_CHECK_VALUE(m == "onepass" || m == "fourpass" || m == "scatter",
-                      "demux mode must be 'fourpass', 'onepass' or 'scatter'");
-    g_demux = m == "onepass" ? kOnepass : m == "scatter" ? kScatterDemux : kFourpass;
-  });
-  m.def("transmux_tile_bytes", &hlsp2p::dev::transmux_tile_bytes);
   m.def("transmux_launch", &transmux_launch, py::arg("src"), py::arg("src_off"), py::arg("nbytes"), py::arg("enc"),
         py::arg("drk"), py::arg("iv"), py::arg("td0"), py::arg("isb"), py::arg("max_pes"));
 }

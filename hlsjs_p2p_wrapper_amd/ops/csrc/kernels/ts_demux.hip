@@ -19,8 +19,6 @@
 //                          iteration with dword-aligned stores (v_alignbyte funnel for the
 //                          unaligned LDS source).
 #include "common.h"
-#include "demux_dev.h"
-#include "ts_onepass.h"
 
 namespace hlsp2p {
 namespace dev {
@@ -131,7 +129,12 @@ __global__ __launch_bounds__(64) void ts_psi_kernel(const uint8_t* __restrict__ 
   }
 }
 
-using demux::pack_meta;
+// per-packet meta word (scan -> gather): class (2b, 3 = none) | payload start (8b) << 2 |
+// payload len (8b) << 10 | PES start (1b) << 18
+__device__ __forceinline__ uint32_t pack_meta(int c, int ps, int len, int pes) {
+  return static_cast<uint32_t>(c & 3) | (static_cast<uint32_t>(ps) << 2) | (static_cast<uint32_t>(len) << 10) |
+         (static_cast<uint32_t>(pes) << 18);
+}
 
 // ---------------------------------------------------------------- 2. scan
 // inclusive wave prefix sum (wave64)
@@ -437,14 +440,6 @@ __global__ __launch_bounds__(kTsThreads) void ts_gather_kernel(
   }
 }
 
-// The block-prefix step alone (the scatter demux, ts_scatter.hip, runs its own scan).
-hipError_t launch_ts_prefix(const int64_t* blk_prefix, const int32_t* blk_sums, int32_t* blk_pre, int32_t* seg_tot,
-                            int64_t* info, int64_t max_pes, int nseg, hipStream_t stream) {
-  if (nseg <= 0) return hipSuccess;
-  hipLaunchKernelGGL(ts_prefix_kernel, dim3(nseg), dim3(64), 0, stream, blk_prefix, blk_sums, blk_pre, seg_tot, info,
-                     max_pes);
-  return hipGetLastError();
-}
 
 hipError_t launch_ts_demux(const uint8_t* buf, const int64_t* seg_off, const int64_t* seg_len,
                            const int64_t* blk_prefix, int nseg, int64_t total_blocks, uint32_t* meta,
@@ -469,263 +464,6 @@ hipError_t launch_ts_demux(const uint8_t* buf, const int64_t* seg_off, const int
   hipLaunchKernelGGL(ts_gather_kernel, dim3(static_cast<unsigned>(total_blocks)), dim3(kTsThreads), 0, stream, buf,
                      seg_off, seg_len, blk_prefix, nseg, meta, pts_dts, blk_pre, seg_tot, es, es_off, pes, max_pes,
                      info);
-  return hipGetLastError();
-}
-
-// ---------------------------------------------------------------- one pass (opt-in)
-// HLSP2P_DEMUX=onepass.  Measured slower than scan + prefix + gather on MI355X (524 vs 438 µs
-// per 256 x 3 MB segments, profiles/r3_transmux_fused_vs_split.md): a block's ordered ticket
-// and its agent-scope look-back round trip across XCDs cost more than the kernel boundary
-// they replace.  Kept, tested against the oracle, for the batch shapes where it may win.
-// blocks of 256 packets (four waves, 49 KiB of LDS, three workgroups per CU; 128-packet blocks
-// at six per CU measured slower: more blocks, more look-back round trips)
-constexpr int kOpThreads = 256, kOpWaves = kOpThreads / 64;
-int onepass_block_packets() { return kOpThreads; }
-
-// Scan + prefix + gather in ONE kernel: each 256-packet block reads its plaintext once (LDS-
-// DMA), parses it, learns its ES destinations from the blocks before it by a decoupled
-// look-back (three class granules per block, agent-scope, the value is its own flag), and
-// writes the elementary streams — so the plaintext crosses HBM once instead of twice and the
-// block-sum round trip between kernels disappears.  Blocks take tickets in order (every lower
-// ticket belongs to a running or finished block: the look-back always makes progress), and
-// three 49 KiB workgroups per CU hide one another's look-back latency.  Classes are written
-// to three regions per segment (info slots 22 / 23 say where audio and id3 start), as the
-// video total is not known when the first audio byte is.
-__global__ __launch_bounds__(kOpThreads) void ts_onepass_kernel(OnepassArgs a) {
-  constexpr int kStageVec = (kOpThreads * kPkt + 16 * kOpThreads - 1) / (16 * kOpThreads);  // 12
-  __shared__ __attribute__((aligned(16))) uint32_t s_pk[kStageVec * kOpThreads * 4 + 8];
-  __shared__ uint32_t s_wave[kOpWaves][3];   // per-wave packed totals (bytes v|a, bytes i|PES v|PES a, PES i)
-  __shared__ int64_t s_ex[2 * kClasses];
-  __shared__ uint8_t s_order[kOpWaves][64];  // per wave: active-packet rank -> lane
-  __shared__ uint32_t s_tk, s_err;
-  const int tid = threadIdx.x, lane = tid & 63;
-  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  if (tid == 0) {
-    s_tk = atomicAdd(a.ticket, 1u);
-    s_err = 0;
-  }
-  __syncthreads();
-  const int64_t gblk = static_cast<int64_t>(__builtin_amdgcn_readfirstlane(s_tk));
-  const int seg = find_seg_wave(a.blk_prefix, a.nseg, gblk);
-  const int64_t tile0 = a.blk_prefix[seg];
-  const int64_t blk = gblk - tile0;
-  const bool last_blk = gblk == a.blk_prefix[seg + 1] - 1;
-  const int64_t raw_len = a.seg_len[seg];
-  const int64_t n = raw_len < 0 ? 0 : raw_len;
-  const int64_t np = n / kPkt;
-  const int64_t first = blk * kOpThreads;
-  const int npk = static_cast<int>(np - first < kOpThreads ? (np - first > 0 ? np - first : 0) : kOpThreads);
-  {  // stage the block's packets (<= 47 KiB) by LDS-DMA: 12 x 1 KiB per wave, all in flight
-    const int nvec = (npk * kPkt + 15) / 16;
-    const uint8_t* g = a.buf + a.seg_off[seg] + first * kPkt;
-    const int last = nvec - 1;
-#pragma unroll
-    for (int k = 0; k < kStageVec; ++k) {
-      const int wbase = k * kOpThreads + wave * 64;  // wave-uniform
-      if (wbase < nvec) {
-        const int i = wbase + lane < last ? wbase + lane : last;
-        __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)(g + 16 * static_cast<int64_t>(i)),
-                                         (__attribute__((address_space(3))) void*)(
-                                             reinterpret_cast<uint8_t*>(s_pk) + 16 * wbase),
-                                         16, 0, 0);
-      }
-    }
-  }
-  int64_t* inf = a.info + static_cast<int64_t>(seg) * kInfo;
-  const int pid0 = static_cast<int>(inf[kVideoPid]), pid1 = static_cast<int>(inf[kVideoPid + 1]),
-            pid2 = static_cast<int>(inf[kVideoPid + 2]);  // ts_psi_kernel's
-  const int64_t cap = a.es_cap[seg];
-  uint8_t* ebase = a.es + a.es_off[seg];
-  __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0): this wave's LDS-DMA has landed
-  __syncthreads();
-
-  // ---- parse (one lane per packet) and the in-wave packed scans (bytes < 2^16, PES < 2^8 per wave)
-  const demux::Pkt p = demux::parse_lds(tid < npk, s_pk + tid * (kPkt / 4), pid0, pid1, pid2);
-  const int c = p.c, len = p.len;
-  const uint32_t lb = static_cast<uint32_t>(len), pf = static_cast<uint32_t>(p.pesf);
-  const uint32_t lA = (c == 0 ? lb : 0u) | ((c == 1 ? lb : 0u) << 16);
-  const uint32_t lB = (c == 2 ? lb : 0u) | ((c == 0 ? pf : 0u) << 16) | ((c == 1 ? pf : 0u) << 24);
-  const uint32_t lC = c == 2 ? pf : 0u;
-  const uint32_t iA = demux::dpp_scan(lA), iB = demux::dpp_scan(lB), iC = demux::dpp_scan(lC);
-  if (lane == 63) {
-    s_wave[wave][0] = iA;
-    s_wave[wave][1] = iB;
-    s_wave[wave][2] = iC;
-  }
-  if (p.err) atomicOr(&s_err, p.err);
-  __syncthreads();
-  // per class: bytes / PES of the earlier waves of this block, and the block aggregate
-  // (unpacked: a block of 256 PES starts would overflow a packed 8-bit field)
-  int32_t wb[3] = {0, 0, 0}, wq[3] = {0, 0, 0}, ab[3] = {0, 0, 0}, aq[3] = {0, 0, 0};
-#pragma unroll
-  for (int w = 0; w < kOpWaves; ++w) {
-    const uint32_t A = s_wave[w][0], B = s_wave[w][1], C = s_wave[w][2];
-    const int32_t vb[3] = {static_cast<int32_t>(A & 0xffff), static_cast<int32_t>(A >> 16),
-                           static_cast<int32_t>(B & 0xffff)};
-    const int32_t vq[3] = {static_cast<int32_t>((B >> 16) & 0xff), static_cast<int32_t>(B >> 24),
-                           static_cast<int32_t>(C)};
-#pragma unroll
-    for (int k = 0; k < 3; ++k) {
-      ab[k] += vb[k];
-      aq[k] += vq[k];
-      if (w < wave) {
-        wb[k] += vb[k];
-        wq[k] += vq[k];
-      }
-    }
-  }
-  // ---- the block's place in its segment: publish the aggregate, look back (wave 0)
-  if (wave == 0) {
-    uint64_t* look = a.look + 3 * gblk;
-    int64_t exb[3] = {0, 0, 0}, exq[3] = {0, 0, 0};
-#pragma unroll
-    for (int k = 0; k < 3; ++k)
-      if (lane == k)
-        demux::gstore(look + k, (blk == 0 ? demux::kIncl : demux::kAgg) | (static_cast<uint64_t>(aq[k]) << 32) |
-                                    static_cast<uint32_t>(ab[k]));
-    if (blk > 0) {
-      demux::look_back(a.look, gblk, tile0, lane, a.ticket + 1, 1u << 22, exb, exq);
-#pragma unroll
-      for (int k = 0; k < 3; ++k)
-        if (lane == k)
-          demux::gstore(look + k, demux::kIncl | (static_cast<uint64_t>(exq[k] + aq[k]) << 32) |
-                                      static_cast<uint32_t>(exb[k] + ab[k]));
-    }
-    if (lane == 0)
-#pragma unroll
-      for (int k = 0; k < 3; ++k) {
-        s_ex[2 * k] = exb[k];
-        s_ex[2 * k + 1] = exq[k];
-      }
-  }
-  __syncthreads();
-
-  // ---- PES entries, first PTS, the block's last PES start per class
-  int64_t es_in_class = 0;
-  if (c < 3) {
-    const uint32_t xA = iA - lA, xB = iB - lB, xC = iC - lC;  // in-wave exclusive
-    const int32_t before_b = (c == 0 ? static_cast<int32_t>(xA & 0xffff) : c == 1 ? static_cast<int32_t>(xA >> 16)
-                                                                                  : static_cast<int32_t>(xB & 0xffff)) +
-                             wb[c];
-    const int32_t before_q = (c == 0 ? static_cast<int32_t>((xB >> 16) & 0xff)
-                                     : c == 1 ? static_cast<int32_t>(xB >> 24) : static_cast<int32_t>(xC)) +
-                             wq[c];
-    es_in_class = s_ex[2 * c] + before_b;
-    if (p.pesf) {
-      const int64_t pidx = s_ex[2 * c + 1] + before_q;
-      if (pidx == 0) inf[kFirstPts + c] = p.pts;
-      if (pidx < a.max_pes) {
-        int64_t* r = a.pes + ((static_cast<int64_t>(seg) * kClasses + c) * a.max_pes + pidx) * 3;
-        r[0] = es_in_class;
-        r[1] = p.pts;
-        r[2] = p.dts;
-      }
-      if (before_q + 1 == aq[c]) {  // the block's last PES start of its class
-        int64_t* lp = a.lastpes + (gblk * kClasses + c) * 2;
-        lp[0] = pidx;
-        lp[1] = p.pts;
-      }
-    }
-  }
-  if (tid == 0 && s_err)
-    atomicOr(reinterpret_cast<unsigned long long*>(inf + kStatus), static_cast<unsigned long long>(s_err));
-  if (last_blk && tid == 0) {  // the last block's inclusive prefix = segment totals
-    int64_t over = 0, total_b = 0;
-    for (int k = 0; k < kClasses; ++k) {
-      const int64_t tb = s_ex[2 * k] + ab[k], tq = s_ex[2 * k + 1] + aq[k];
-      inf[kBytes0 + k] = tb;
-      inf[kPes0 + k] = tq;
-      total_b += tb;
-      if (tq > a.max_pes) over = kPesOverflow;
-    }
-    inf[kPayloadBytes] = total_b;
-    inf[kAudioEsOffset] = np > 0 ? cap : 0;  // per-class regions (no media: 0, as the packed layout)
-    inf[kId3EsOffset] = np > 0 ? 2 * cap : 0;
-    if (over) atomicOr(reinterpret_cast<unsigned long long*>(inf + kStatus), static_cast<unsigned long long>(over));
-  }
-
-  // ---- copy-out (ts_gather_kernel's scheme): five payloads per wave iteration, a 12-lane
-  // group per payload, one dwordx4 buffer store per lane out of a 5-dword LDS funnel
-  const uint8_t* s_bytes = reinterpret_cast<const uint8_t*>(s_pk);
-  const bool act = c < 3 && len > 0;
-  const uint64_t amask = __ballot(act);
-  const int nact = __popcll(amask);
-  if (act) {
-    const int rank = __builtin_amdgcn_mbcnt_hi(static_cast<uint32_t>(amask >> 32),
-                                               __builtin_amdgcn_mbcnt_lo(static_cast<uint32_t>(amask), 0));
-    s_order[wave][rank] = static_cast<uint8_t>(lane);
-  }
-  __builtin_amdgcn_wave_barrier();
-  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-  typedef unsigned int v4u __attribute__((ext_vector_type(4)));
-  const __amdgpu_buffer_rsrc_t es_rsrc = __builtin_amdgcn_make_buffer_rsrc(ebase, 0, 0x7fffffff, 0x00020000);
-  const int dst32 = static_cast<int>((c < 3 ? c : 0) * cap + es_in_class);  // within the segment's 3 regions
-  const int grp = lane / 12, sub = lane - 12 * grp;  // groups 0..4; lanes 60..63 idle
-  for (int base = 0; base < nact; base += 5) {
-    const int r = base + grp;
-    const bool valid = grp < 5 && r < nact;
-    const int j = valid ? s_order[wave][r] : 0;
-    const int jlen_all = __shfl(len, j);
-    const int jps = __shfl(p.ps, j);
-    const int jdst = __shfl(dst32, j);
-    const int jlen = valid ? jlen_all : 0;
-    const int s = (wave * 64 + j) * kPkt + jps;  // LDS byte offset of the payload
-    uint8_t* d = ebase + jdst;
-    const int mis = static_cast<int>((4 - (reinterpret_cast<uintptr_t>(d) & 3)) & 3);
-    const int head = mis < jlen ? mis : jlen;
-    const int body = (jlen - head) >> 2;
-    const int tail = jlen - head - 4 * body;
-    if (sub < head) d[sub] = s_bytes[s + sub];
-    const int k0 = 4 * sub;
-    if (k0 < body) {
-      const int aa = s + head + 4 * k0;
-      const uint32_t sh = static_cast<uint32_t>(aa & 3);
-      const uint32_t* w = s_pk + (aa >> 2);
-      const uint32_t x0 = w[0], x1 = w[1], x2 = w[2], x3 = w[3], x4 = w[4];
-      const uint32_t o0 = __builtin_amdgcn_alignbyte(x1, x0, sh), o1 = __builtin_amdgcn_alignbyte(x2, x1, sh),
-                     o2 = __builtin_amdgcn_alignbyte(x3, x2, sh), o3 = __builtin_amdgcn_alignbyte(x4, x3, sh);
-      uint32_t* dw = reinterpret_cast<uint32_t*>(d + head) + k0;
-      if (k0 + 4 <= body) {
-        const v4u q = {o0, o1, o2, o3};
-        __builtin_amdgcn_raw_buffer_store_b128(q, es_rsrc, jdst + head + 4 * k0, 0, 0);
-      } else {
-        dw[0] = o0;
-        if (k0 + 1 < body) dw[1] = o1;
-        if (k0 + 2 < body) dw[2] = o2;
-      }
-    }
-    if (sub < tail) d[head + 4 * body + sub] = s_bytes[s + head + 4 * body + sub];
-  }
-}
-
-// One wave per segment after the one-pass kernel: the last PTS per class (the last block
-// with a PES start of the class; the blocks do not know which of them that is).
-__global__ __launch_bounds__(64) void ts_onepass_tail_kernel(OnepassArgs a) {
-  const int seg = blockIdx.x;
-  const int tid = threadIdx.x;
-  if (tid >= kClasses) return;
-  int64_t* inf = a.info + static_cast<int64_t>(seg) * kInfo;
-  const int64_t t0 = a.blk_prefix[seg], t1 = a.blk_prefix[seg + 1];
-  if (inf[kPes0 + tid] <= 0) return;
-  for (int64_t t = t1 - 1; t >= t0; --t) {
-    const int64_t* lp = a.lastpes + (t * kClasses + tid) * 2;
-    if (lp[0] >= 0) {
-      inf[kLastPts + tid] = lp[1];
-      return;
-    }
-  }
-}
-
-hipError_t launch_ts_onepass(const OnepassArgs& a, hipStream_t stream) {
-  if (a.nseg <= 0) return hipSuccess;
-  hipLaunchKernelGGL(ts_psi_kernel, dim3(a.nseg), dim3(64), 0, stream, a.buf, a.seg_off, a.seg_len, a.info, a.pes,
-                     a.max_pes);
-  hipError_t e = hipGetLastError();
-  if (e != hipSuccess || a.total_blocks <= 0) return e;
-  hipLaunchKernelGGL(ts_onepass_kernel, dim3(static_cast<unsigned>(a.total_blocks)), dim3(kOpThreads), 0, stream, a);
-  e = hipGetLastError();
-  if (e != hipSuccess) return e;
-  hipLaunchKernelGGL(ts_onepass_tail_kernel, dim3(a.nseg), dim3(64), 0, stream, a);
   return hipGetLastError();
 }
 

@@ -3,8 +3,7 @@
 Output per segment (identical for the gfx950 kernels and the host oracle):
 
 * ES bytes per class at ``es_offs[i]`` of the ES buffer: video at 0, audio and id3 at the
-  offsets the info row gives (``audio_es_offset`` / ``id3_es_offset``: packed back to back by
-  the host oracle and the split kernels, fixed per-class regions in the fused kernel);
+  offsets the info row gives (``audio_es_offset`` / ``id3_es_offset``: packed back to back);
 * ``pes[i, class, k] = (es_offset, pts, dts)`` for the k-th PES of each class;
 * ``info[i]`` = status bits, PIDs, packet count, per-class byte and PES counts
   (slot names in :data:`INFO`).

@@ -120,7 +120,8 @@ def test_bench_eight_ranks_driver_shape():
 
 
 PER_RANK_KEYS = {"rank", "rounds", "step_ms", "wait_device_us", "exchange_us", "control_us", "plan_us",
-                 "host_round_us", "cdn_GBps", "cdn_dev_ms", "p2p_recv_MB", "p2p_sent_MB", "p2p_dev_ms", "p2p_GBps", "p2p_links", "p2p_link_GBps",
+                 "host_round_us", "cdn_GBps", "cdn_dev_ms", "p2p_recv_MB", "p2p_sent_MB", "p2p_dev_ms", "p2p_GBps",
+                 "p2p_links", "p2p_link_GBps",
                  "transmux_dev_ms", "transmux_wait_us", "await_players_us", "crc_failures", "control_fallbacks",
                  "deferred", "inflight", "cu_reserve", "bound"}
 
