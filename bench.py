@@ -133,6 +133,9 @@ def parse():
                    help="fleet players receive every fragment's bytes in onSuccess (gpuSwarm.fleetPayload: "
                         "HBM gather + D2H + shared-memory ring per batch); off: the players get the "
                         "transmux result rows only (the bytes stay in HBM)")
+    p.add_argument("--corrupt-recv", type=int, default=0, metavar="N",
+                   help="fault injection (SURVEY 5.3): flip a byte in the first segment received from a peer in "
+                        "each of the first N timed rounds; the CRC check must drop it and the CDN re-serve it")
     p.add_argument("--verbose", action="store_true")
     return p.parse_args()
 
@@ -444,6 +447,7 @@ def main() -> int:
     node.timer.reset()
     pipe.timer.reset()
     b0, s0 = counters["buffered"], dict(node.stats)
+    node.corrupt_next_recv = args.corrupt_recv
     t0 = time.perf_counter()
     if _PROF is not None and not _PROF_C3:
         _PROF.enable()
@@ -619,6 +623,7 @@ def _fleet(args, world, rank, device, use_gpu, node, origin, players, desc, encr
         pipe.timer.reset()
         fleet_timer.reset()
         s0 = dict(node.stats)
+        node.corrupt_next_recv = args.corrupt_recv
         calib0 = cpu_calibration_us() if args.verbose else 0.0
         mark("t0")
         t0 = time.perf_counter()

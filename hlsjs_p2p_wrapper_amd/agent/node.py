@@ -141,6 +141,8 @@ class RoundHandle:
     shaped_ms: float = 0.0
     ok_dev: Any = None
     ok_host: Any = None
+    defer: Any = None  # bool per received row: its CRC is checked by the consumer's decrypt (fleet)
+    expect_host: Any = None  # the senders' CRC trailers of the received rows (host copy)
     done: Any = None
     n_wants: int = 0
     n_send: int = 0
@@ -267,6 +269,12 @@ class SwarmNode:
         self.swarm_stats = {"cdn": 0, "p2p": 0, "upload": 0}
         self.last_round: Dict[str, Any] = {}
         self.corrupt_next_recv = 0  # fault injection: flip a byte in the next N received rounds
+        # Deferred receive verification (set by a fleet server, parallel/fleet.py): a segment a
+        # peer sent is not CRC-read by the node; its trailer travels with the delivery and the
+        # batch that decrypts it computes the CRC on the way (kernels/aes_cbc.hip AesCrc).  The
+        # entry stays pending -- pinned, not announced, not served -- until verify_done.
+        self.verify_deferred = False
+        self._vpend: Dict[int, np.ndarray] = {}  # entry id -> want info row [10] (a CDN retry's source)
         self.link_kbps: Dict[int, float] = {}  # fault injection: slow link from peer -> kbit/s
         self.timer = PhaseTimer()
         # per-request trace records {key, trequest, tfirst, tload, source, bytes, peer, round}
@@ -866,6 +874,7 @@ class SwarmNode:
         wt = self._wt
         recv = h.recv
         good = bad = None
+        dgood = exp_good = None  # deferred verification (verify_deferred): rows of `good`, their CRCs
         if recv is not None:
             ok = (h.ok_host.numpy() if isinstance(h.ok_host, torch.Tensor) else np.asarray(h.ok_host)).astype(bool)
             if ok.all():
@@ -873,8 +882,15 @@ class SwarmNode:
             else:
                 good = tuple(c[ok] for c in recv)
                 bad = tuple(c[~ok] for c in recv)
-            if len(good[0]):
-                self.store.commit(good[2])
+            if h.defer is not None:
+                dgood = h.defer[ok]
+                eh = h.expect_host.numpy() if isinstance(h.expect_host, torch.Tensor) else np.asarray(h.expect_host)
+                exp_good = eh.astype(np.int64)[ok]
+                if not dgood.any():
+                    dgood = None
+            commit = good[2] if dgood is None else good[2][~dgood]
+            if len(commit):
+                self.store.commit(commit)
             if bad is not None:
                 self.store.drop(bad[2])
                 self.stats["crc_failures"] += len(bad[0])
@@ -897,7 +913,11 @@ class SwarmNode:
                                    np.zeros(k), offs[idx], eids[idx], delay=h.shaped_ms)
         if good is not None and len(good[0]):
             wids, srcs, eids, offs, lens, keys = good
+            winfo = wt.info(np.ascontiguousarray(wids[dgood])) if dgood is not None else None
             tok, idx, pf = wt.finish(wids)
+            exp_tok = None
+            if dgood is not None:
+                tok, idx, exp_tok = self._settle_deferred(h, good, dgood, exp_good, tok, idx, winfo)
             self._after_finish(wids, pf, keys, "p2p")
             k = len(tok)
             if k:
@@ -914,7 +934,7 @@ class SwarmNode:
                             p2p_ms[i] = max(p2p_ms[i], delay[i])
                     delay = delay[idx]
                 self._deliver_cols(tok, np.ones(k, dtype=np.int8), lens[idx], np.zeros(k), p2p_ms[idx], offs[idx],
-                                   eids[idx], peers=srcs[idx], delay=delay)
+                                   eids[idx], peers=srcs[idx], delay=delay, expect=exp_tok)
         if bad is not None and len(bad[0]):
             wt.requeue(bad[0], True)  # corrupted peer copy: from the CDN next round
         # planned but not served (a STAGE row, a CDN error already reported): waiting again
@@ -1150,11 +1170,20 @@ class SwarmNode:
             o, n = int(roff_a[0]), int(recv_rows[0, 4])
             if n:
                 self.arena[o + n // 2] ^= 0x5A
-        # verify against the senders' trailers; the combine kernel also scatters the computed
-        # CRCs into the per-entry table (ids ride the descriptor H2D): a mismatching entry is
-        # dropped in complete_round, so the table only ever serves verified values
-        _, ok = _crc.crc32_batch(self.arena, roff_a, recv_rows[:, 4], expect_dev=trailers,
-                                 scatter_to=self.crc_dev, scatter_idx=rid_a)
+        defer = None
+        if self.verify_deferred:  # rows whose consumer checks the CRC (no Python-side origin state)
+            wf = self._wt.info(np.ascontiguousarray(recv_rows[:, 7]))[:, 7]
+            d = (wf & (W_PY | W_PREFETCH)) == 0
+            defer = d if d.any() else None
+        if defer is None:
+            # verify against the senders' trailers; the combine kernel also scatters the
+            # computed CRCs into the per-entry table (ids ride the descriptor H2D): a
+            # mismatching entry is dropped in complete_round, so the table only ever serves
+            # verified values
+            _, ok = _crc.crc32_batch(self.arena, roff_a, recv_rows[:, 4], expect_dev=trailers,
+                                     scatter_to=self.crc_dev, scatter_idx=rid_a)
+        else:
+            ok = self._defer_verify(h, defer, trailers, roff_a, recv_rows, rid_a)
         if self.is_cuda:
             h.ok_host = torch.empty(ok.numel(), dtype=torch.uint8, pin_memory=True)
             h.ok_host.copy_(ok, non_blocking=True)
@@ -1164,13 +1193,135 @@ class SwarmNode:
         self.stats["p2p_segments"] += len(recv_rows)
         self.stats["p2p_links"] += len(rrun)
 
+    def _defer_verify(self, h: RoundHandle, defer: np.ndarray, trailers, roff_a: np.ndarray, recv_rows: np.ndarray,
+                      rid_a: np.ndarray):
+        """Received rows under deferred verification (``verify_deferred``): their trailers go
+        into the CRC table now (the entries are announced only after the check) and to the
+        host with the delivery; the other rows are CRC-read as usual.  Returns the per-row ok
+        flags on the node's device (deferred rows: provisionally 1)."""
+        dev = self.device
+        nd, dd = np.flatnonzero(~defer), np.flatnonzero(defer)
+        if self.is_cuda:
+            from ..ops.desc import pack_to_device
+
+            ix = pack_to_device({"nd": nd, "dd": dd, "rd": np.ascontiguousarray(rid_a[dd])}, dev)
+        else:
+            ix = {"nd": torch.from_numpy(nd), "dd": torch.from_numpy(dd), "rd": torch.from_numpy(rid_a[dd])}
+        ok = torch.ones(len(recv_rows), dtype=torch.uint8, device=dev)
+        if len(nd):
+            _, ok_nd = _crc.crc32_batch(self.arena, roff_a[nd], recv_rows[nd, 4],
+                                        expect_dev=torch.index_select(trailers, 0, ix["nd"]),
+                                        scatter_to=self.crc_dev, scatter_idx=rid_a[nd])
+            ok.index_copy_(0, ix["nd"], ok_nd)
+        self.crc_dev.index_copy_(0, ix["rd"], torch.index_select(trailers, 0, ix["dd"]))
+        h.defer = defer
+        if self.is_cuda:
+            h.expect_host = torch.empty(len(recv_rows), dtype=torch.int32, pin_memory=True)
+            h.expect_host.copy_(trailers, non_blocking=True)
+        else:
+            h.expect_host = trailers.clone()
+        return ok
+
+    def _settle_deferred(self, h: RoundHandle, good: tuple, dgood: np.ndarray, exp_good: np.ndarray,
+                         tok: np.ndarray, idx: np.ndarray, winfo: np.ndarray):
+        """Delivery-time bookkeeping of received rows whose CRC the consumer checks.  A row
+        only bulk (fleet) tokens wait for is delivered with its expected CRC and stays
+        pending (one extra pin) until :meth:`verify_done`; a row an in-process request (or
+        nobody) waits for is verified here, synchronously, as the loader contract delivers
+        checked bytes.  Returns the delivery's ``tok``, ``idx`` and per-token expected CRCs
+        (-1: none)."""
+        wids, _, eids, offs, lens, _ = good
+        drow = np.flatnonzero(dgood)
+        info_of = {int(r): winfo[k] for k, r in enumerate(drow)}
+        now = []
+        for r in drow.tolist():
+            t = tok[idx == r]
+            if not len(t) or (t < 0).any():
+                now.append(r)
+        keep = np.ones(len(tok), dtype=bool)
+        if now:
+            nr = np.asarray(now, dtype=np.int64)
+            exp = (exp_good[nr] & _M32).tolist()
+            if self.is_cuda:
+                with self._on_node_stream():
+                    _, okd = _crc.crc32_batch(self.arena, offs[nr], lens[nr], expect=exp)
+                    ok_now = okd.cpu().numpy().astype(bool)
+            else:
+                ok_now = _crc.crc32_batch(self.arena, offs[nr], lens[nr], expect=exp)[1].numpy().astype(bool)
+            if ok_now.any():
+                self.store.commit(eids[nr[ok_now]])
+            bad = nr[~ok_now]
+            if len(bad):
+                self.store.drop(eids[bad])
+                self.stats["crc_failures"] += len(bad)
+                for r in bad.tolist():
+                    sel = idx == r
+                    self._retry_cdn(info_of[r], tok[sel])
+                    keep &= ~sel
+            dgood = dgood.copy()
+            dgood[nr] = False
+        pend = np.flatnonzero(dgood)
+        if len(pend):
+            pe = eids[pend]
+            self.store.pin(pe)  # held until verify_done
+            for r, e in zip(pend.tolist(), pe.tolist()):
+                self._vpend[int(e)] = info_of[r]
+        exp_row = np.full(len(wids), -1, dtype=np.int64)
+        exp_row[pend] = exp_good[pend] & _M32
+        if not keep.all():
+            tok, idx = tok[keep], idx[keep]
+        return tok, idx, exp_row[idx]
+
+    def _retry_cdn(self, info: np.ndarray, tokens: np.ndarray) -> None:
+        """Ask again, from the CDN, for a segment whose peer copy failed its CRC."""
+        tokens = np.ascontiguousarray(tokens, dtype=np.int64)
+        if not len(tokens):
+            return
+        n = len(tokens)
+        rep = np.repeat(info.reshape(1, -1), n, axis=0)
+        self._wt.add(np.ascontiguousarray(rep[:, :4]), np.ascontiguousarray(rep[:, 4]), np.ascontiguousarray(rep[:, 5]),
+                     np.ascontiguousarray(rep[:, 6]), np.ascontiguousarray(rep[:, 7] | W_FORCE_CDN), tokens)
+        self._schedule()
+
+    def verify_done(self, eids: np.ndarray, ok: np.ndarray, tokens: np.ndarray) -> int:
+        """Outcome of deferred CRC checks (fragment columns: the entry each was read from,
+        passed, its token).  A passing entry is committed (announced next round, served to
+        peers); a failing one is detached (its readers' pins drain) and its tokens are asked
+        again from the CDN.  Returns the number of failed entries."""
+        eids = np.asarray(eids, dtype=np.int64)
+        ok = np.asarray(ok, dtype=bool)
+        tokens = np.asarray(tokens, dtype=np.int64)
+        if not len(eids):
+            return 0
+        ue, inv = np.unique(eids, return_inverse=True)
+        uok = np.ones(len(ue), dtype=bool)
+        np.logical_and.at(uok, inv, ok)
+        pend = self._vpend
+        good = [e for e, o in zip(ue.tolist(), uok.tolist()) if o and e in pend]
+        bad = [(k, e) for k, (e, o) in enumerate(zip(ue.tolist(), uok.tolist())) if not o and e in pend]
+        if good:
+            g = np.asarray(good, dtype=np.int64)
+            for e in good:
+                self._vpend.pop(e, None)
+            self.store.commit(g)
+            self.store.unpin(g)
+        for k, e in bad:
+            info = self._vpend.pop(e)
+            arr = np.array([e], dtype=np.int64)
+            self.store.detach(arr)
+            self.store.unpin(arr)
+            self.stats["crc_failures"] += 1
+            self._retry_cdn(info, tokens[inv == k])
+        return len(bad)
+
     # ------------------------------------------------------------------ delivery
     def _deliver_cols(self, tok: np.ndarray, src: np.ndarray, nbytes: np.ndarray, cdn_ms: np.ndarray,
                       p2p_ms: np.ndarray, offs: np.ndarray, eids: np.ndarray, peers: Optional[np.ndarray] = None,
-                      delay: Any = None) -> None:
+                      delay: Any = None, expect: Optional[np.ndarray] = None) -> None:
         """Answer waiting tokens.  Entries stay pinned ``PIN_DELAY_ROUNDS`` launches (their
         consumers read the arena asynchronously); shaped / slowed transfers are answered
-        after their modelled duration."""
+        after their modelled duration.  ``expect`` (bulk tokens only): the CRC the consumer
+        must find in the bytes (-1: already verified), see ``verify_deferred``."""
         if delay is not None and not (np.isscalar(delay) and delay <= 0):
             d = np.broadcast_to(np.asarray(delay, dtype=np.float64), tok.shape)
             later = d > 0
@@ -1182,13 +1333,15 @@ class SwarmNode:
                     self.store.pin(le)
                 self.loop.set_timeout(self._deliver_deferred, float(d[li].max()),
                                       (tok[li], src[li], nbytes[li], cdn_ms[li], p2p_ms[li], offs[li], eids[li],
-                                       None if peers is None else peers[li]), le)
+                                       None if peers is None else peers[li], None,
+                                       None if expect is None else expect[li]), le)
                 if later.all():
                     return
                 ni = np.flatnonzero(~later)
                 tok, src, nbytes, cdn_ms, p2p_ms, offs, eids = (tok[ni], src[ni], nbytes[ni], cdn_ms[ni], p2p_ms[ni],
                                                                 offs[ni], eids[ni])
                 peers = None if peers is None else peers[ni]
+                expect = None if expect is None else expect[ni]
         pin = eids[eids >= 0]
         if len(pin):
             self.store.pin(pin)
@@ -1198,11 +1351,12 @@ class SwarmNode:
         if nb:
             self.stats["segments"] += nb
             if self._bulk is not None:
+                ex = {} if expect is None else {"expect": expect if nb == len(tok) else expect[bulk]}
                 if nb == len(tok):
-                    self._bulk.deliver(tok, src, nbytes, cdn_ms, p2p_ms, offs, eids)
+                    self._bulk.deliver(tok, src, nbytes, cdn_ms, p2p_ms, offs, eids, **ex)
                 else:
                     self._bulk.deliver(tok[bulk], src[bulk], nbytes[bulk], cdn_ms[bulk], p2p_ms[bulk], offs[bulk],
-                                       eids[bulk])
+                                       eids[bulk], **ex)
         if nb == len(tok):
             return
         obj = np.flatnonzero(~bulk)

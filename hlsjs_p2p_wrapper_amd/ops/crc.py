@@ -45,6 +45,20 @@ def _device_consts(device: torch.device, variant: str):
     return c
 
 
+def fused_consts(device: torch.device):
+    """Device constants of the CRC fused into the AES decrypt (``kernels/aes_cbc.hip``
+    ``AesCrc``; ``transmux_launch(..., expect, crc_w, crc_tables)``): the chunk B fragments
+    (16 steps x 64 lanes x 16 bytes) and the shift tables P_0..P_39, Q_0..Q_11."""
+    k = (str(device), "chunk")
+    c = _consts.get(k)
+    if c is None:
+        w = torch.from_numpy(_rt().crc_chunk_weights_fp4()).to(device)
+        c = (w, _device_consts(device, "fp4")[1])
+        with _lock:
+            _consts[k] = c
+    return c
+
+
 def crc32_batch(buf: torch.Tensor, offs: Sequence[int], lens: Sequence[int],
                 expect: Optional[Sequence[int]] = None,
                 expect_dev: Optional[torch.Tensor] = None, scatter_to: Optional[torch.Tensor] = None,

@@ -40,6 +40,51 @@ constexpr int kAesThreads = kAesImageThreads;
 constexpr int kAesWgPerCu = 1;
 constexpr int kBlk = 4;  // blocks per lane per chunk (chunk = 64 * kBlk blocks): independent chains
 
+typedef int v4i __attribute__((ext_vector_type(4)));
+typedef int v8i __attribute__((ext_vector_type(8)));
+typedef float v16f __attribute__((ext_vector_type(16)));
+
+// Optional CRC-32 of the CIPHERTEXT, fused into the decrypt (SURVEY K12 on the receive path:
+// a segment that arrived from a peer is verified by the batch that decrypts it, instead of by a
+// separate read pass).  The ciphertext is already in VGPRs and the matrix cores sit idle
+// while the decrypt is VALU / LDS bound, so each flagged chunk adds 16 FP4 MFMAs
+// (v_mfma_scale_f32_32x32x64_f8f6f4, the operand scheme of crc32_mfma.hip): step 4j + d feeds
+// dword d of the lane's chain-j block.  Row r (lane & 31) collects the blocks r + 32m, m =
+// 2j + (lane >> 5), under weights that place every block at row 31's position
+// (crc_host.cpp: mfma_chunk_weights_fp4), so no data moves between lanes; the 32 row
+// accumulator parities go out as one 16-bit word per lane (`masks`: 64 per chunk, bit i =
+// parity of accumulator i: row (i & 3) + 8 (i >> 2) + 4 (lane >> 5), column lane & 31), and
+// crc32_rows_fold_kernel (crc32_mfma.hip) transposes them to row residues with ballots and
+// finishes the chunk -- no ballot SGPRs beside the 44 round keys here.
+struct AesCrc {
+  const int64_t* mask_off;  // [nseg] the segment's first mask word (64 per 4096-byte chunk), -1:
+                            // no CRC for it (nullptr: for no segment)
+  const v4i* wfrag;         // [16 steps][64 lanes] B fragments
+  uint16_t* masks;
+};
+
+__device__ __forceinline__ void crc_chunk_masks(const uint4 (&c)[kBlk], const v4i* __restrict__ wfrag, int lane,
+                                                uint16_t* __restrict__ out) {
+  v16f acc = {};
+#pragma unroll
+  for (int j = 0; j < kBlk; ++j) {
+    const uint32_t dw[4] = {c[j].x, c[j].y, c[j].z, c[j].w};
+#pragma unroll
+    for (int d = 0; d < 4; ++d) {
+      const uint32_t x = dw[d];
+      const v8i a = {static_cast<int>(x & 0x11111111u), static_cast<int>(x & 0x22222222u),
+                     static_cast<int>(x & 0x44444444u), static_cast<int>((x >> 1) & 0x44444444u), 0, 0, 0, 0};
+      const v4i b4 = wfrag[(4 * j + d) * 64 + lane];
+      const v8i b = {b4.x, b4.y, b4.z, b4.w, 0, 0, 0, 0};
+      acc = __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(a, b, acc, 4, 4, 0, 0, 0, 0);
+    }
+  }
+  uint32_t m = 0;  // exact counts: the parity is the GF(2) sum
+#pragma unroll
+  for (int i = 0; i < 16; ++i) m |= (static_cast<uint32_t>(static_cast<int>(acc[i])) & 1u) << i;
+  out[lane] = static_cast<uint16_t>(m);
+}
+
 // tdl: little-endian Td0 (256 words); isb: inverse S-box (256 bytes)
 // drk: per-segment little-endian equivalent-inverse-cipher round keys (44 words)
 // chunk_prefix: exclusive prefix of per-segment 256-block chunks (one chunk = one wave
@@ -50,7 +95,7 @@ __global__ __launch_bounds__(kAesThreads, 1) void aes128_cbc_decrypt_kernel(
     const int64_t* __restrict__ dst_off, const int64_t* __restrict__ blk_prefix,
     const int64_t* __restrict__ chunk_prefix, const uint32_t* __restrict__ drk, const uint32_t* __restrict__ ivw,
     const uint32_t* __restrict__ tdl_g, const uint8_t* __restrict__ isb_g, int64_t* __restrict__ out_len, int nseg,
-    int64_t total_chunks, int64_t per_wg) {
+    int64_t total_chunks, int64_t per_wg, AesCrc crc) {
   __shared__ uint32_t s_tab[kTdDwords + kIsDwords];  // 160 KiB (layout above)
   const int tid = threadIdx.x;
   aes_image_fill(s_tab, tdl_g, isb_g, tid);
@@ -67,7 +112,7 @@ __global__ __launch_bounds__(kAesThreads, 1) void aes128_cbc_decrypt_kernel(
   // segment state is wave-uniform (SGPRs): round keys come in by scalar loads
   int cur = -1;
   uint32_t rk[44];
-  int64_t so = 0, dof = 0, cstart = 0, cend = 0, nblk = 0;
+  int64_t so = 0, dof = 0, cstart = 0, cend = 0, nblk = 0, maskb = -1;
   for (int64_t ch = uniform64(begin + (tid >> 6)); ch < end; ch += kWaves) {
     if (cur < 0 || ch >= cend) {
       cur = cur < 0 ? find_seg_wave(chunk_prefix, nseg, ch)  // whole wave active: ch is uniform
@@ -79,6 +124,7 @@ __global__ __launch_bounds__(kAesThreads, 1) void aes128_cbc_decrypt_kernel(
       cstart = chunk_prefix[cur];
       cend = chunk_prefix[cur + 1];
       nblk = blk_prefix[cur + 1] - blk_prefix[cur];
+      maskb = crc.mask_off != nullptr ? crc.mask_off[cur] : -1;
     }
     const int64_t b0 = (ch - cstart) * (64 * kBlk) + lane;  // this lane's first block
     const uint4* cs = reinterpret_cast<const uint4*>(src + so);
@@ -93,6 +139,7 @@ __global__ __launch_bounds__(kAesThreads, 1) void aes128_cbc_decrypt_kernel(
       const int64_t b = b0 + 64 * j;
       pv[j] = b == 0 ? reinterpret_cast<const uint4*>(ivw)[cur] : (b < nblk ? cs[b - 1] : make_uint4(0, 0, 0, 0));
     }
+    if (maskb >= 0) crc_chunk_masks(c, crc.wfrag, lane, crc.masks + maskb + (ch - cstart) * 64);  // wave-uniform
     uint32_t st[kBlk][4];
 #pragma unroll
     for (int j = 0; j < kBlk; ++j) {
@@ -127,16 +174,19 @@ void aes_grid(int64_t total_chunks, int num_cu, int64_t& grid, int64_t& per_wg) 
 }
 }  // namespace
 
+// crc_mask_off / crc_wfrag / crc_masks: the fused ciphertext CRC (nullptr: off)
 hipError_t launch_aes128_cbc_decrypt(const uint8_t* src, uint8_t* dst, const int64_t* src_off, const int64_t* dst_off,
                                      const int64_t* blk_prefix, const int64_t* chunk_prefix, const uint32_t* drk,
                                      const uint32_t* ivw, const uint32_t* tdl, const uint8_t* isb, int64_t* out_len,
-                                     int nseg, int64_t total_chunks, int num_cu, hipStream_t stream) {
+                                     int nseg, int64_t total_chunks, int num_cu, hipStream_t stream,
+                                     const int64_t* crc_mask_off, const void* crc_wfrag, uint16_t* crc_masks) {
   if (total_chunks <= 0) return hipSuccess;
   int64_t grid, per_wg;
   aes_grid(total_chunks, num_cu, grid, per_wg);
+  const AesCrc crc{crc_mask_off, reinterpret_cast<const v4i*>(crc_wfrag), crc_masks};
   hipLaunchKernelGGL(aes128_cbc_decrypt_kernel, dim3(static_cast<unsigned>(grid)), dim3(kAesThreads), 0, stream,
                      src, dst, src_off, dst_off, blk_prefix, chunk_prefix, drk, ivw, tdl, isb, out_len, nseg,
-                     total_chunks, per_wg);
+                     total_chunks, per_wg, crc);
   return hipGetLastError();
 }
 

@@ -14,7 +14,8 @@ namespace dev {
 int aes_chunk_blocks();
 hipError_t launch_aes128_cbc_decrypt(const uint8_t*, uint8_t*, const int64_t*, const int64_t*, const int64_t*,
                                      const int64_t*, const uint32_t*, const uint32_t*, const uint32_t*,
-                                     const uint8_t*, int64_t*, int, int64_t, int, hipStream_t);
+                                     const uint8_t*, int64_t*, int, int64_t, int, hipStream_t, const int64_t*,
+                                     const void*, uint16_t*);
 hipError_t launch_crc32_batch(const uint8_t*, const int64_t*, const int64_t*, const int64_t*, const int64_t*,
                               const void*, const uint32_t*, uint32_t*, uint32_t*, const uint32_t*, uint8_t*,
                               const int64_t*, uint32_t*, int64_t, int, int64_t, int, bool, hipStream_t);
@@ -86,7 +87,8 @@ void aes128_cbc_decrypt(Tensor src, Tensor dst, Tensor src_off, Tensor dst_off, 
   ok(D::launch_aes128_cbc_decrypt(cptr<uint8_t>(src), mptr<uint8_t>(dst), cptr<int64_t>(src_off),
                                   cptr<int64_t>(dst_off), cptr<int64_t>(blk_prefix), cptr<int64_t>(chunk_prefix),
                                   cptr<uint32_t>(drk), cptr<uint32_t>(iv), cptr<uint32_t>(td0), cptr<uint8_t>(isb),
-                                  mptr<int64_t>(out_len), static_cast<int>(B), total_chunks, num_cus(src), stream()),
+                                  mptr<int64_t>(out_len), static_cast<int>(B), total_chunks, num_cus(src), stream(),
+                                  nullptr, nullptr, nullptr),
      "aes128_cbc_decrypt");
 }
 

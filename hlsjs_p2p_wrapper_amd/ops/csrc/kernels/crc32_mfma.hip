@@ -248,44 +248,49 @@ __device__ __forceinline__ uint32_t apply_tab(const uint32_t* __restrict__ t, ui
 
 constexpr int kCombineThreads = 1024;
 constexpr int kCombineLdsTables = 15;  // P_8 .. P_22
-constexpr int kNumQ = 8;               // Q_b = A^(-8 * 2^b): pad removal
-// Residue of the 256-byte group [FF FF FF FF 00 .. 00]: for n >= 4 the zlib init value
-// 0xFFFFFFFF equals XOR-ing FF into the message's first 4 bytes, so it folds into group 0's
-// residue (= zlib(FF^4 0^252) ^ zlib(0^256)) instead of a 20-step chain of dependent
-// global table lookups on one thread after the tree (that tail was most of the kernel).
-constexpr uint32_t kInitFold = 0xf2697aa7u;
+constexpr int kNumQ = 12;              // Q_b = A^(-8 * 2^b): pad removal (pad < 4096 bytes)
+// Residue of the group [FF FF FF FF 00 .. 00]: for n >= 4 the zlib init value 0xFFFFFFFF
+// equals XOR-ing FF into the message's first 4 bytes, so it folds into group 0's residue
+// (= zlib(FF^4 0^(G-4)) ^ zlib(0^G)) instead of a 20-step chain of dependent global table
+// lookups on one thread after the tree (that tail was most of the kernel).
+constexpr uint32_t kInitFold256 = 0xf2697aa7u;   // 256-byte groups (crc_host.cpp: init_fold)
+constexpr uint32_t kInitFold4096 = 0x38e3ffeeu;  // 4096-byte chunks of the fused decrypt CRC
 
-// One workgroup per segment.  tables: P_0..P_39 then Q_0..Q_7 (each kSlice u32).
+// One workgroup per segment.  tables: P_0..P_39 then Q_0..Q_11 (each kSlice u32).  Group
+// residues of 2^kLg bytes: 256-byte groups (the residue kernels above) or 4096-byte chunks
+// (the CRC fused into the decrypt, folded by crc32_rows_fold_kernel).
+template <int kLg>
 __global__ __launch_bounds__(kCombineThreads) void crc32_combine_kernel(
     const uint32_t* __restrict__ residues, const int64_t* __restrict__ res_off, const int64_t* __restrict__ seg_len,
     const uint32_t* __restrict__ tables, uint32_t* __restrict__ crc_out, const uint32_t* __restrict__ expect,
     uint8_t* __restrict__ ok_out, const int64_t* __restrict__ scatter_idx, uint32_t* __restrict__ scatter_out,
     int64_t scatter_n) {
   __shared__ __attribute__((aligned(16))) uint32_t s_tab[kCombineLdsTables * kSlice];  // 60 KiB
-  __shared__ __attribute__((aligned(16))) uint32_t s_q[kNumQ * kSlice];                // 32 KiB
+  __shared__ __attribute__((aligned(16))) uint32_t s_q[kLg * kSlice];                  // 32 / 48 KiB
   __shared__ uint32_t s_acc[kCombineThreads];
   const int seg = blockIdx.x;
   const int tid = threadIdx.x;
   const int64_t n = seg_len[seg];
-  const int64_t G = (n + 255) >> 8;
+  const int64_t G = (n + (int64_t(1) << kLg) - 1) >> kLg;
   // run length L = next pow2 of ceil(G / threads)
   int lgL = 0;
   while ((static_cast<int64_t>(kCombineThreads) << lgL) < G) ++lgL;
-  const int lds_tables = 1 + lgL + 10 <= kCombineLdsTables ? 1 + lgL + 10 : kCombineLdsTables;
+  const int need = kLg - 8 + 1 + lgL + 10;  // P_8 .. P_(kLg + lgL + 10) from LDS
+  const int lds_tables = need <= kCombineLdsTables ? need : kCombineLdsTables;
   lds_fill<kCombineLdsTables * kSlice / 4 / kCombineThreads + 1>(
       reinterpret_cast<uint4*>(s_tab), reinterpret_cast<const uint4*>(tables + 8 * kSlice), lds_tables * kSlice / 4,
       tid, kCombineThreads);
-  lds_fill<kNumQ * kSlice / 4 / kCombineThreads>(reinterpret_cast<uint4*>(s_q),
-                                                  reinterpret_cast<const uint4*>(tables + kNumP * kSlice),
-                                                  kNumQ * kSlice / 4, tid, kCombineThreads);
+  lds_fill<kLg * kSlice / 4 / kCombineThreads>(reinterpret_cast<uint4*>(s_q),
+                                                reinterpret_cast<const uint4*>(tables + kNumP * kSlice),
+                                                kLg * kSlice / 4, tid, kCombineThreads);
   __syncthreads();
   const int64_t L = int64_t(1) << lgL;
   const int64_t span = L * kCombineThreads;
   const int64_t front = span - G;  // virtual zero groups in front
   const uint32_t* __restrict__ res = residues + res_off[seg];
-  const uint32_t fold0 = n >= 4 ? kInitFold : 0u;
+  const uint32_t fold0 = n >= 4 ? (kLg == 8 ? kInitFold256 : kInitFold4096) : 0u;
   uint32_t acc = 0;
-  const uint32_t* p8 = s_tab;  // A^(8*256): one group
+  const uint32_t* pg = s_tab + (kLg - 8) * kSlice;  // A^(8 * 2^kLg): one group
   // Horner over this thread's run of L groups, 8 residues loaded ahead per step (a
   // load-per-iteration loop paid one global round trip per group: L of them in series)
   constexpr int kAhead = 8;
@@ -300,16 +305,16 @@ __global__ __launch_bounds__(kCombineThreads) void crc32_combine_kernel(
     for (int j = 0; j < kAhead; ++j) {
       if (k0 + j < L) {
         const int64_t g = static_cast<int64_t>(tid) * L + k0 + j - front;
-        acc = apply_tab(p8, acc) ^ rv[j] ^ (g == 0 ? fold0 : 0u);
+        acc = apply_tab(pg, acc) ^ rv[j] ^ (g == 0 ? fold0 : 0u);
       }
     }
   }
   s_acc[tid] = acc;
   __syncthreads();
-  // tree: level m merges runs of L*2^m groups: left = A^(8*256*L*2^m) left ^ right
+  // tree: level m merges runs of L*2^m groups: left = A^(8*2^kLg*L*2^m) left ^ right
   for (int m = 0; (1 << m) < kCombineThreads; ++m) {
     const int stride = 1 << m;
-    const int b = 8 + lgL + m;  // shift of 2^b bytes
+    const int b = kLg + lgL + m;  // shift of 2^b bytes
     if ((tid & (2 * stride - 1)) == 0) {
       const uint32_t* tab = (b - 8) < lds_tables ? s_tab + (b - 8) * kSlice : tables + static_cast<int64_t>(b) * kSlice;
       s_acc[tid] = apply_tab(tab, s_acc[tid]) ^ s_acc[tid + stride];
@@ -318,8 +323,8 @@ __global__ __launch_bounds__(kCombineThreads) void crc32_combine_kernel(
   }
   if (tid == 0) {
     uint32_t raw = s_acc[0];
-    const int64_t pad = G * 256 - n;
-    for (int b = 0; b < kNumQ; ++b)
+    const int64_t pad = (G << kLg) - n;
+    for (int b = 0; b < kLg; ++b)
       if ((pad >> b) & 1) raw = apply_tab(s_q + b * kSlice, raw);
     uint32_t init = 0;  // folded into group 0 (n >= 4)
     if (n < 4) {
@@ -337,6 +342,67 @@ __global__ __launch_bounds__(kCombineThreads) void crc32_combine_kernel(
       if (d >= 0 && d < scatter_n) scatter_out[d] = crc;
     }
   }
+}
+
+// The fused decrypt CRC's per-chunk fold (aes_cbc.hip: crc_chunk_masks).  A chunk's 64 lane
+// words carry the parity bits of the MFMA accumulators (bit i of lane l: row (i & 3) + 8 (i >> 2)
+// + 4 (l >> 5), column l & 31); 16 ballots turn them into the 32 row residues D[r] (lane r),
+// and the chunk residue XOR_r A^(8 * 16 (31 - r)) D[r] is a 5-level tree across the lanes with
+// the byte-slice tables P_4 .. P_8 (shifts of 16 .. 256 bytes, in LDS).  One wave per chunk.
+constexpr int kFoldThreads = 256;
+__global__ __launch_bounds__(kFoldThreads) void crc32_rows_fold_kernel(const uint16_t* __restrict__ masks,
+                                                                      const uint32_t* __restrict__ tables,
+                                                                      uint32_t* __restrict__ chunk_res,
+                                                                      int64_t total_chunks) {
+  __shared__ __attribute__((aligned(16))) uint32_t s_p[5 * kSlice];  // P_4 .. P_8
+  lds_fill<5 * kSlice / 4 / kFoldThreads>(reinterpret_cast<uint4*>(s_p), reinterpret_cast<const uint4*>(tables + 4 * kSlice),
+                                          5 * kSlice / 4, threadIdx.x, kFoldThreads);
+  __syncthreads();
+  const int lane = threadIdx.x & 63;
+  const int64_t waves = static_cast<int64_t>(gridDim.x) * (kFoldThreads / 64);
+  for (int64_t c = static_cast<int64_t>(blockIdx.x) * (kFoldThreads / 64) + (threadIdx.x >> 6); c < total_chunks;
+       c += waves) {
+    const uint32_t m = masks[64 * c + lane];
+    uint32_t res = 0;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+      const uint64_t b = __ballot((m >> i) & 1u);
+      const int row = (i & 3) + 8 * (i >> 2);
+      res = lane == row ? static_cast<uint32_t>(b) : res;
+      res = lane == row + 4 ? static_cast<uint32_t>(b >> 32) : res;
+    }
+    // tree over rows 0..31: level k merges runs of 2^k rows, the left run moved 16 * 2^k bytes
+#pragma unroll
+    for (int k = 0; k < 5; ++k) {
+      const uint32_t right = static_cast<uint32_t>(__shfl_down(static_cast<int>(res), 1 << k, 64));
+      if ((lane & ((2 << k) - 1)) == 0) res = apply_tab(s_p + k * kSlice, res) ^ right;
+    }
+    if (lane == 0) chunk_res[c] = res;
+  }
+}
+
+// masks: 64 words per 4096-byte chunk for each segment, the segment's chunks starting at
+// word 64 * chunk_off[seg]; chunk_res: scratch of total_chunks words.  Same outputs as
+// launch_crc32_batch.
+hipError_t launch_crc32_from_masks(const uint16_t* masks, const int64_t* chunk_off, const int64_t* seg_len,
+                                   const uint32_t* tables, uint32_t* chunk_res, uint32_t* crc_out,
+                                   const uint32_t* expect, uint8_t* ok_out, const int64_t* scatter_idx,
+                                   uint32_t* scatter_out, int64_t scatter_n, int nseg, int64_t total_chunks,
+                                   int num_cu, hipStream_t stream) {
+  if (nseg <= 0) return hipSuccess;
+  if (total_chunks > 0) {
+    const int64_t waves_max = static_cast<int64_t>(num_cu) * 16;
+    const int64_t waves = total_chunks < waves_max ? total_chunks : waves_max;
+    const int64_t grid = (waves + (kFoldThreads / 64) - 1) / (kFoldThreads / 64);
+    hipLaunchKernelGGL(crc32_rows_fold_kernel, dim3(static_cast<unsigned>(grid)), dim3(kFoldThreads), 0, stream, masks,
+                       tables, chunk_res, total_chunks);
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return e;
+  }
+  hipLaunchKernelGGL(crc32_combine_kernel<12>, dim3(static_cast<unsigned>(nseg)), dim3(kCombineThreads), 0, stream,
+                     chunk_res, chunk_off, seg_len, tables, crc_out, expect, ok_out, scatter_idx, scatter_out,
+                     scatter_n);
+  return hipGetLastError();
 }
 
 hipError_t launch_crc32_batch(const uint8_t* buf, const int64_t* seg_off, const int64_t* seg_len,
@@ -362,7 +428,7 @@ hipError_t launch_crc32_batch(const uint8_t* buf, const int64_t* seg_off, const 
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
   }
-  hipLaunchKernelGGL(crc32_combine_kernel, dim3(static_cast<unsigned>(nseg)), dim3(kCombineThreads), 0, stream,
+  hipLaunchKernelGGL(crc32_combine_kernel<8>, dim3(static_cast<unsigned>(nseg)), dim3(kCombineThreads), 0, stream,
                      residues, res_off, seg_len, tables, crc_out, expect, ok_out, scatter_idx, scatter_out, scatter_n);
   return hipGetLastError();
 }

@@ -25,9 +25,13 @@ namespace dev {
 int aes_chunk_blocks();
 hipError_t launch_aes128_cbc_decrypt(const uint8_t*, uint8_t*, const int64_t*, const int64_t*, const int64_t*,
                                      const int64_t*, const uint32_t*, const uint32_t*, const uint32_t*,
-                                     const uint8_t*, int64_t*, int, int64_t, int, hipStream_t);
+                                     const uint8_t*, int64_t*, int, int64_t, int, hipStream_t, const int64_t*,
+                                     const void*, uint16_t*);
 hipError_t launch_ts_demux(const uint8_t*, const int64_t*, const int64_t*, const int64_t*, int, int64_t, uint32_t*,
                            int64_t*, int32_t*, uint8_t*, const int64_t*, int64_t*, int64_t, int64_t*, hipStream_t);
+hipError_t launch_crc32_from_masks(const uint16_t*, const int64_t*, const int64_t*, const uint32_t*, uint32_t*, uint32_t*,
+                                   const uint32_t*, uint8_t*, const int64_t*, uint32_t*, int64_t, int, int64_t, int,
+                                   hipStream_t);
 }  // namespace dev
 }  // namespace hlsp2p
 
@@ -139,7 +143,8 @@ void hip_ok(hipError_t e, const char* what) { TORCH_CHECK(e == hipSuccess, what,
 py::tuple transmux_launch(Tensor src, I64 src_off, I64 nbytes, py::array_t<uint8_t, py::array::c_style> enc,
                           py::array_t<uint32_t, py::array::c_style | py::array::forcecast> drk,
                           py::array_t<uint8_t, py::array::c_style | py::array::forcecast> iv, Tensor td0, Tensor isb,
-                          int64_t max_pes) {
+                          int64_t max_pes, py::object expect_obj, c10::optional<Tensor> crc_w,
+                          c10::optional<Tensor> crc_tables) {
   TORCH_CHECK_VALUE(src.is_cuda() && src.is_contiguous() && src.scalar_type() == torch::kUInt8, "src: contiguous GPU uint8");
   TORCH_CHECK_VALUE((reinterpret_cast<uintptr_t>(src.data_ptr()) & 15) == 0, "src must be 16-byte aligned");
   const int64_t B = src_off.size();
@@ -160,9 +165,31 @@ py::tuple transmux_launch(Tensor src, I64 src_off, I64 nbytes, py::array_t<uint8
   }
   const auto dev_opts = torch::TensorOptions().device(torch::kCUDA, device);
   hipStream_t st = c10::hip::getCurrentHIPStream(device).stream();
+  // optional verify: expect[i] >= 0 is the CRC-32 the CIPHERTEXT of encrypted segment i must
+  // have (a peer's trailer); the decrypt computes it on the fly (aes_cbc.hip AesCrc)
+  std::vector<int64_t> v_exp;
+  if (!expect_obj.is_none()) {
+    I64 ex = expect_obj.cast<I64>();
+    TORCH_CHECK_VALUE(ex.size() == B, "expect must have one entry per segment");
+    v_exp.assign(ex.data(), ex.data() + B);
+    bool any = false;
+    for (int64_t i = 0; i < B; ++i) {
+      if (v_exp[i] < 0) continue;
+      TORCH_CHECK_VALUE(en[i], "fused CRC verify needs an encrypted segment (verify clear ones separately)");
+      any = true;
+    }
+    if (!any) v_exp.clear();
+    else
+      TORCH_CHECK_VALUE(crc_w.has_value() && crc_tables.has_value() && crc_w->is_cuda() &&
+                            crc_w->numel() * crc_w->element_size() >= 16 * 64 * 16 && crc_tables->is_cuda() &&
+                            crc_tables->numel() >= (40 + 12) * 1024,
+                        "fused CRC verify needs the chunk weights and shift tables on the device");
+  }
 
   // ---- plans: AES over the encrypted segments, demux per group
   std::vector<int64_t> a_so, a_do, a_bp{0}, a_cp{0};
+  std::vector<int64_t> a_mo, v_idx, v_coff, v_len, v_expw;  // fused CRC: mask offsets, verify columns
+  int64_t v_chunks = 0;
   std::vector<uint32_t> a_drk;
   std::vector<uint8_t> a_iv;
   DemuxPlan pe, pc;
@@ -179,6 +206,19 @@ py::tuple transmux_launch(Tensor src, I64 src_off, I64 nbytes, py::array_t<uint8
       const int64_t blocks = nb[i] / 16;
       a_bp.push_back(a_bp.back() + blocks);
       a_cp.push_back(a_cp.back() + (blocks + chunk - 1) / chunk);
+      if (!v_exp.empty()) {
+        const int64_t nch = (blocks + chunk - 1) / chunk;  // one 4096-byte CRC chunk per decrypt chunk
+        if (v_exp[i] >= 0) {
+          a_mo.push_back(64 * v_chunks);
+          v_idx.push_back(i);
+          v_coff.push_back(v_chunks);
+          v_len.push_back(nb[i]);
+          v_expw.push_back(v_exp[i] & 0xffffffffll);
+          v_chunks += nch;
+        } else {
+          a_mo.push_back(-1);
+        }
+      }
       a_drk.insert(a_drk.end(), drk.data(i, 0), drk.data(i, 0) + 44);
       a_iv.insert(a_iv.end(), iv.data(i, 0), iv.data(i, 0) + 16);
     } else {
@@ -194,7 +234,9 @@ py::tuple transmux_launch(Tensor src, I64 src_off, I64 nbytes, py::array_t<uint8
 
   // ---- every descriptor of the batch in one staging block, one H2D
   Desc desc;
-  int64_t d_so = -1, d_do = -1, d_bp = -1, d_cp = -1, d_drk = -1, d_iv = -1;
+  int64_t d_so = -1, d_do = -1, d_bp = -1, d_cp = -1, d_drk = -1, d_iv = -1, d_mo = -1, d_vco = -1, d_vl = -1,
+          d_vx = -1;
+  const int64_t nv = static_cast<int64_t>(v_idx.size());
   if (ne) {
     d_so = desc.add(a_so);
     d_do = desc.add(a_do);
@@ -205,6 +247,13 @@ py::tuple transmux_launch(Tensor src, I64 src_off, I64 nbytes, py::array_t<uint8
     pe.d_off = desc.add(pe.off);
     pe.d_bp = desc.add(pe.blk_prefix);
     pe.d_eo = desc.add(pe.es_off);
+    if (nv) {
+      std::vector<uint32_t> ex32(v_expw.begin(), v_expw.end());
+      d_mo = desc.add(a_mo);
+      d_vco = desc.add(v_coff);
+      d_vl = desc.add(v_len);
+      d_vx = desc.add(ex32);
+    }
   }
   if (nc) {
     pc.d_off = desc.add(pc.off);
@@ -218,6 +267,13 @@ py::tuple transmux_launch(Tensor src, I64 src_off, I64 nbytes, py::array_t<uint8
   Tensor host = torch::empty({(ne + nc) * kInfo + ne + 1}, torch::TensorOptions().dtype(torch::kInt64).pinned_memory(true));
   Tensor dec, out_len;
   if (ne) out_len = torch::empty({ne}, dev_opts.dtype(torch::kInt64));
+  Tensor masks, chunk_res, v_crc, v_ok, v_ok_host;
+  if (nv) {
+    masks = torch::empty({64 * v_chunks}, dev_opts.dtype(torch::kInt16));
+    chunk_res = torch::empty({std::max<int64_t>(1, v_chunks)}, dev_opts.dtype(torch::kInt32));
+    v_crc = torch::empty({nv}, dev_opts.dtype(torch::kInt32));
+    v_ok = torch::empty({nv}, dev_opts.dtype(torch::kUInt8));
+  }
   if (ne) {
     dec = torch::empty({dec_pos + kAlign}, dev_opts.dtype(torch::kUInt8));
     hip_ok(hlsp2p::dev::launch_aes128_cbc_decrypt(
@@ -225,8 +281,20 @@ py::tuple transmux_launch(Tensor src, I64 src_off, I64 nbytes, py::array_t<uint8
                desc.at<int64_t>(d_so), desc.at<int64_t>(d_do), desc.at<int64_t>(d_bp), desc.at<int64_t>(d_cp),
                desc.at<uint32_t>(d_drk), desc.at<uint32_t>(d_iv), static_cast<const uint32_t*>(td0.data_ptr()),
                static_cast<const uint8_t*>(isb.data_ptr()), out_len.data_ptr<int64_t>(), static_cast<int>(ne),
-               a_cp.back(), decrypt_cus(device), st),
+               a_cp.back(), decrypt_cus(device), st, nv ? desc.at<int64_t>(d_mo) : nullptr,
+               nv ? crc_w->data_ptr() : nullptr, nv ? reinterpret_cast<uint16_t*>(masks.data_ptr<int16_t>()) : nullptr),
            "aes128_cbc_decrypt");
+  }
+  if (nv) {  // fold the decrypt's CRC masks per chunk, combine per segment, compare
+    hip_ok(hlsp2p::dev::launch_crc32_from_masks(
+               reinterpret_cast<const uint16_t*>(masks.data_ptr<int16_t>()), desc.at<int64_t>(d_vco),
+               desc.at<int64_t>(d_vl), static_cast<const uint32_t*>(crc_tables->data_ptr()),
+               reinterpret_cast<uint32_t*>(chunk_res.data_ptr<int32_t>()),
+               reinterpret_cast<uint32_t*>(v_crc.data_ptr<int32_t>()), desc.at<uint32_t>(d_vx),
+               v_ok.data_ptr<uint8_t>(), nullptr, nullptr, 0, static_cast<int>(nv), v_chunks, cus(device), st),
+           "crc32_from_masks");
+    v_ok_host = torch::empty({nv}, torch::TensorOptions().dtype(torch::kUInt8).pinned_memory(true));
+    v_ok_host.copy_(v_ok, /*non_blocking=*/true);
   }
 
   py::list groups, keep;  // keep: scratch the kernels use until the batch completes
@@ -276,7 +344,14 @@ py::tuple transmux_launch(Tensor src, I64 src_off, I64 nbytes, py::array_t<uint8
   }
   keep.append(dec.defined() ? py::cast(dec) : py::none());
   keep.append(desc.device());
-  return py::make_tuple(groups, keep, host);
+  py::object verify = py::none();
+  if (nv) {
+    keep.append(py::make_tuple(masks, chunk_res, v_crc, v_ok));
+    I64 vi(static_cast<py::ssize_t>(nv));
+    std::memcpy(vi.mutable_data(), v_idx.data(), static_cast<size_t>(nv * 8));
+    verify = py::make_tuple(vi, v_ok_host);  // batch indices of the verified segments, ok flags (pinned)
+  }
+  return py::make_tuple(groups, keep, host, verify);
 }
 
 }  // namespace
@@ -286,5 +361,6 @@ void register_transmux(py::module& m) {
         "CUs the persistent decrypt grid leaves free for concurrent (RCCL) kernels");
   m.def("cu_reserve", [] { return g_cu_reserve; });
   m.def("transmux_launch", &transmux_launch, py::arg("src"), py::arg("src_off"), py::arg("nbytes"), py::arg("enc"),
-        py::arg("drk"), py::arg("iv"), py::arg("td0"), py::arg("isb"), py::arg("max_pes"));
+        py::arg("drk"), py::arg("iv"), py::arg("td0"), py::arg("isb"), py::arg("max_pes"),
+        py::arg("expect") = py::none(), py::arg("crc_w") = py::none(), py::arg("crc_tables") = py::none());
 }

@@ -203,6 +203,13 @@ PYBIND11_MODULE(_runtime, m) {
     std::memcpy(a.mutable_data(), w.data(), w.size());
     return a;
   });
+  m.def("crc_chunk_weights_fp4", [] {
+    auto w = crc::mfma_chunk_weights_fp4();
+    Arr<uint8_t> a(static_cast<py::ssize_t>(w.size()));
+    std::memcpy(a.mutable_data(), w.data(), w.size());
+    return a;
+  });
+  m.def("crc_init_fold", &crc::init_fold, py::arg("nbytes"));
   m.def("crc_shift_tables", [] {
     auto t = crc::shift_tables();
     Arr<uint32_t> a(static_cast<py::ssize_t>(t.size()));
@@ -212,6 +219,7 @@ PYBIND11_MODULE(_runtime, m) {
   m.attr("CRC_NUM_P") = crc::kNumP;
   m.attr("CRC_NUM_Q") = crc::kNumQ;
   m.attr("CRC_GROUP_BYTES") = crc::kGroupBytes;
+  m.attr("CRC_CHUNK_BYTES") = crc::kChunkBytes;
 
   // ------------------------------------------------------------------ TS
   m.def("mux_segment", [](double duration, double fps, int64_t target_bytes, int audio_kbps, bool with_id3,
@@ -418,6 +426,9 @@ PYBIND11_MODULE(_runtime, m) {
       })
       .def("pin", [](SegmentStore& s, Arr<int64_t> ids) {
         for (int64_t i = 0; i < ids.size(); ++i) s.pin(ids.data()[i]);
+      })
+      .def("detach", [](SegmentStore& s, Arr<int64_t> ids) {
+        for (int64_t i = 0; i < ids.size(); ++i) s.detach(ids.data()[i]);
       })
       .def("unpin", [](SegmentStore& s, Arr<int64_t> ids) {
         for (int64_t i = 0; i < ids.size(); ++i) s.unpin(ids.data()[i]);

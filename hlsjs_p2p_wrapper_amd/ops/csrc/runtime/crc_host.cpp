@@ -188,6 +188,48 @@ std::vector<uint8_t> mfma_group_weights_fp4() {
   return w;
 }
 
+std::vector<uint8_t> mfma_chunk_weights_fp4() {
+  const ByteTable& T = table();
+  const Mat a8 = zero_byte_op();
+  static const uint8_t kOne[4] = {0x4, 0x2, 0x1, 0x1};  // e2m1: 2.0, 1.0, 0.5, 0.5 (as the group form)
+  std::vector<uint8_t> w(16 * 64 * 16, 0);
+  // vec[m][y][bit] = A^(8 (512 (7 - m) + 15 - y)) t(bit)
+  static uint32_t vec[8][16][8];
+  for (int m = 0; m < 8; ++m) {
+    const Mat um = power(a8, uint64_t(512) * (7 - m));
+    for (int bit = 0; bit < 8; ++bit) {
+      uint32_t r = apply(um, T.t[0][1u << bit]);
+      for (int y = 15; y >= 0; --y) {
+        vec[m][y][bit] = r;
+        r = (r >> 8) ^ T.t[0][r & 0xff];  // one more zero byte after it
+      }
+    }
+  }
+  for (int s = 0; s < 16; ++s) {
+    const int j = s >> 2, d = s & 3;
+    for (int lane = 0; lane < 64; ++lane) {
+      const int col = lane & 31, h = lane >> 5, m = 2 * j + h;
+      uint8_t* frag = &w[(size_t(s) * 64 + lane) * 16];
+      for (int v = 0; v < 4; ++v)
+        for (int e = 0; e < 8; ++e) {
+          const int bit = 4 * e + v;  // bit of the data dword (element 8v + e)
+          const int y = 4 * d + (bit >> 3);
+          if (!((vec[m][y][bit & 7] >> col) & 1u)) continue;
+          frag[4 * v + (e >> 1)] |= static_cast<uint8_t>(kOne[v] << (4 * (e & 1)));
+        }
+    }
+  }
+  return w;
+}
+
+uint32_t init_fold(int64_t nbytes) {
+  if (nbytes < 4) return 0;
+  const ByteTable& T = table();
+  uint32_t r = 0;
+  for (int i = 0; i < 4; ++i) r = (r >> 8) ^ T.t[0][(r ^ 0xffu) & 0xff];
+  return apply(power(zero_byte_op(), static_cast<uint64_t>(nbytes - 4)), r);
+}
+
 std::vector<uint32_t> shift_tables() {
   std::vector<uint32_t> out(size_t(kNumP + kNumQ) * kSliceWords);
   Mat a8 = zero_byte_op();

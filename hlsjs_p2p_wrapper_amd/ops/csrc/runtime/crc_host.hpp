@@ -23,7 +23,8 @@ namespace crc {
 constexpr uint32_t kPoly = 0xEDB88320u;
 constexpr int kGroupBytes = 256;      // data bytes per MFMA output row
 constexpr int kNumP = 40;             // P_b tables, b = 0..39  (shift up to 2^39 bytes)
-constexpr int kNumQ = 8;              // Q_b tables, b = 0..7   (undo pad < 256 bytes)
+constexpr int kNumQ = 12;             // Q_b tables, b = 0..11  (undo pad < 4096 bytes)
+constexpr int kChunkBytes = 4096;     // data bytes per fused decrypt + CRC chunk (aes_cbc.hip)
 constexpr int kSliceWords = 4 * 256;  // one byte-slice table set (4 KiB)
 
 uint32_t crc32(const uint8_t* data, size_t n, uint32_t crc = 0);  // zlib-compatible update
@@ -44,8 +45,19 @@ std::vector<int8_t> mfma_group_weights();
 // FP4 (e2m1) variant for v_mfma_scale_f32_32x32x64_f8f6f4: [step s=0..31][lane][16 bytes of
 // packed nibbles] = 32768 bytes (see crc32_mfma.hip for the operand scheme).
 std::vector<uint8_t> mfma_group_weights_fp4();
-// Byte-slice tables: P_0..P_39 then Q_0..Q_7, each kSliceWords u32.
+// Byte-slice tables: P_0..P_39 then Q_0..Q_11, each kSliceWords u32.
 std::vector<uint32_t> shift_tables();
+// The CRC fused into the AES-CBC decrypt (aes_cbc.hip): a wave's 4096-byte chunk holds block
+// 64j + l in lane l, chain j.  Row r (= lane & 31) of the FP4 MFMA gets the blocks
+// r + 32m (m = 2j + (lane >> 5)); step s = 4j + d feeds dword d of the lane's chain-j block.
+// B fragments [s = 0..15][lane][16 bytes]: data bit (byte y, bit b) of a block of row-slot m
+// weighs A^(8 (512 (7 - m) + 15 - y)) t(b), so row r's residue is the chunk's contribution
+// with every block moved to row 31's position; the chunk residue is then
+// XOR_r A^(8 * 16 (31 - r)) D[r] (a Horner over the 32 rows with the 16-byte shift P_4).
+std::vector<uint8_t> mfma_chunk_weights_fp4();
+// Raw (zero-init) CRC of [FF FF FF FF 00 ...] of `nbytes` bytes: zlib's init value folded into
+// the first group's residue.
+uint32_t init_fold(int64_t nbytes);
 
 }  // namespace crc
 }  // namespace hlsp2p

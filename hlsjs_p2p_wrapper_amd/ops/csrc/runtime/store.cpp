@@ -167,6 +167,16 @@ void SegmentStore::drop(int64_t id) {
   release(id, true);
 }
 
+void SegmentStore::detach(int64_t id) {
+  if (id < 0 || id >= static_cast<int64_t>(entries_.size())) return;
+  Entry& e = entries_[id];
+  if (e.state == kFree) return;
+  auto it = index_.find(e.key);
+  if (it == index_.end() || it->second != id) return;  // already replaced / detached
+  if (e.state == kResident) delta_rm_.push_back(e.key);
+  index_.erase(it);
+}
+
 int64_t SegmentStore::evict_below(uint32_t swarm, uint32_t min_sn) {
   std::vector<int64_t> victims;
   for (const auto& kv : index_) {

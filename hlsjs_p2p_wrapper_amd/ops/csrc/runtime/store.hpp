@@ -88,6 +88,10 @@ class SegmentStore {
   }
   void commit(int64_t id);  // pending -> resident (+ "add" delta)
   void drop(int64_t id);    // remove now (+ "remove" delta if it was resident)
+  // Take the entry out of the index (+ "remove" delta if it was resident) but keep its bytes
+  // until its pins drop and the ring reaches it -- for a copy that readers still hold pins on
+  // and must not be found again (a received segment that failed its deferred CRC check).
+  void detach(int64_t id);
   void pin(int64_t id) { entries_[id].pins += 1; }
   void unpin(int64_t id) {
     if (entries_[id].pins > 0) entries_[id].pins -= 1;

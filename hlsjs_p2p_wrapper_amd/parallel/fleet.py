@@ -523,11 +523,20 @@ class FleetServer:
         self.batches_sent = [0] * W  # answer batches sent to each player ...
         self.batches_done = [0] * W  # ... and handled by it (reported back)
         node.set_bulk_sink(self)
+        # segments received from peers are CRC-checked by the transmux that decrypts them (the
+        # CRC fused into the AES kernel), not by a separate read in the node's round: results
+        # of a copy that fails go to no player, the node asks the CDN again (verify_done)
+        if hasattr(node, "verify_deferred") and os.environ.get("HLSP2P_DEFER_VERIFY", "1") != "0":
+            node.verify_deferred = True
+        self.verify_failures = 0
 
     # -------------------------------------------------------------- node sink
-    def deliver(self, tok, src, nbytes, cdn_ms, p2p_ms, offs, eids) -> None:
-        """Delivery columns of the node's round (``SwarmNode.set_bulk_sink``)."""
-        self._delivered.append((tok, src, nbytes, cdn_ms, p2p_ms, offs))
+    def deliver(self, tok, src, nbytes, cdn_ms, p2p_ms, offs, eids, expect=None) -> None:
+        """Delivery columns of the node's round (``SwarmNode.set_bulk_sink``); ``expect``: the
+        CRC each fragment's bytes must have (-1: verified by the node already)."""
+        if expect is None:
+            expect = np.full(len(tok), -1, dtype=np.int64)
+        self._delivered.append((tok, src, nbytes, cdn_ms, p2p_ms, offs, eids, expect))
 
     def fail(self, tok, status) -> None:
         """Requests the node could not serve (HTTP-like status per token)."""
@@ -627,9 +636,9 @@ class FleetServer:
         if not items:
             return None
         if len(items) == 1:
-            tok, src, nbytes, cdn_ms, p2p_ms, offs = items[0]
+            tok, src, nbytes, cdn_ms, p2p_ms, offs, eids, expect = items[0]
         else:
-            tok, src, nbytes, cdn_ms, p2p_ms, offs = (np.concatenate(c) for c in zip(*items))
+            tok, src, nbytes, cdn_ms, p2p_ms, offs, eids, expect = (np.concatenate(c) for c in zip(*items))
         w = tok >> TOKEN_SHIFT
         slot = (tok & _RID_MASK) % _RING
         gk = np.empty(len(tok), dtype=np.int32)
@@ -643,15 +652,25 @@ class FleetServer:
             drk, keys = self._drk[np.maximum(gk, 0)], self._rawkeys[np.maximum(gk, 0)]
         else:
             drk, keys = np.zeros((len(tok), 44), dtype=np.uint32), None
-        tag = (tok, src, nbytes, cdn_ms, p2p_ms, offs)
-        return self.pipe.launch_columns(self.node.arena, offs, nbytes, enc, drk, iv, tag, keys=keys)
+        verify = expect >= 0
+        tag = (tok, src, nbytes, cdn_ms, p2p_ms, offs, eids, expect if verify.any() else None)
+        return self.pipe.launch_columns(self.node.arena, offs, nbytes, enc, drk, iv, tag, keys=keys,
+                                        expect=expect if verify.any() else None)
 
     def complete_transmux(self, batch) -> None:
         """Wait for a launched transmux batch; its info rows go to the players as columns."""
         if batch is None:
             return
-        tag, rows, plain, has = self.pipe.complete_columns(batch)
-        tok, src, nbytes, cdn_ms, p2p_ms, offs = tag
+        tag, rows, plain, has, verified = self.pipe.complete_columns(batch)
+        tok, src, nbytes, cdn_ms, p2p_ms, offs, eids, expect = tag
+        if expect is not None:  # deferred receive checks: the node commits or re-fetches
+            chk = expect >= 0
+            self.verify_failures += self.node.verify_done(eids[chk], verified[chk], tok[chk])
+            if not verified.all():  # no answer for a corrupted copy: the CDN retry answers
+                keep = verified
+                tok, src, nbytes, cdn_ms, p2p_ms, offs = (tok[keep], src[keep], nbytes[keep], cdn_ms[keep],
+                                                          p2p_ms[keep], offs[keep])
+                rows, plain, has = rows[keep], plain[keep], has[keep]
         w = tok >> TOKEN_SHIFT
         rid = tok & _RID_MASK
         for p in np.unique(w).tolist():

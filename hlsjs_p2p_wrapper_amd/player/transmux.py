@@ -25,6 +25,7 @@ from ..net.event_loop import get_event_loop
 from ..ops import aes as _aes
 from ..ops import tsdemux as _ts
 from ..ops._native import device as _native_device
+from ..ops._native import runtime as _rt
 from ..utils.trace import PhaseTimer
 
 ALIGN = 256
@@ -257,8 +258,8 @@ class MediaPipeline:
         t2 = time.perf_counter()
         tm.add("decrypt_launch", t2 - t1)
         ev0 = self._event()
-        groups, dec, host_block = _native_device().transmux_launch(src, offs, nb, flags, drk, iv, td0, isb,
-                                                                   _ts.DEFAULT_MAX_PES)
+        groups, dec, host_block, _ = _native_device().transmux_launch(src, offs, nb, flags, drk, iv, td0, isb,
+                                                                      _ts.DEFAULT_MAX_PES)
         infos, host = [], []
         for gidx, info, pes, es, es_offs, hinfo, hlens in groups:
             batch_idx = [idx[k] for k in gidx.tolist()]
@@ -270,19 +271,27 @@ class MediaPipeline:
 
     # ------------------------------------------------------------------ columnar batch
     def launch_columns(self, src: torch.Tensor, offs: np.ndarray, nbytes: np.ndarray, enc: np.ndarray,
-                       drk: np.ndarray, iv: np.ndarray, tag: Any = None, keys: Optional[np.ndarray] = None
-                       ) -> Optional["_Batch"]:
+                       drk: np.ndarray, iv: np.ndarray, tag: Any = None, keys: Optional[np.ndarray] = None,
+                       expect: Optional[np.ndarray] = None) -> Optional["_Batch"]:
         """A batch given as columns (a fleet rank: no job object per fragment).  Fragment
         ``i`` is ``src[offs[i] : offs[i] + nbytes[i]]`` (the node's HBM arena, 16-byte aligned
         offsets); ``enc[i]``: AES-128-CBC with round keys ``drk[i]`` (44 little-endian words,
         ``ops.aes.round_keys_le``) and ``iv[i]``; ``keys[i]`` (raw 16-byte keys) is only read
-        by the CPU path.  ``tag`` comes back from :meth:`complete_columns`."""
+        by the CPU path.  ``expect[i] >= 0``: fragment i's bytes must have that CRC-32 (a
+        peer's trailer, verified here instead of by the node): an encrypted fragment is
+        checked by the decrypt itself (the CRC fused into ``aes_cbc.hip``), a clear one by the
+        CRC kernel; :meth:`complete_columns` reports the outcome.  ``tag`` comes back from
+        :meth:`complete_columns`."""
         n = len(offs)
         if n == 0:
             return None
         offs = np.ascontiguousarray(offs, dtype=np.int64)
         nb = np.ascontiguousarray(nbytes, dtype=np.int64)
         enc = np.asarray(enc, dtype=bool)
+        if expect is not None:
+            expect = np.ascontiguousarray(expect, dtype=np.int64)
+            if not (expect >= 0).any():
+                expect = None
         self.segments += n
         self.bytes_in += int(nb.sum())
         self.batches += 1
@@ -295,25 +304,50 @@ class MediaPipeline:
                 jobs.append(TransmuxJob(src[o:o + k], key, bytes(iv[i]) if key is not None else None, None))
             b = self.launch_jobs(jobs)
             b.tag = tag
+            if expect is not None:  # host CRC of the same bytes
+                vi = np.flatnonzero(expect >= 0)
+                got = _rt().crc32_batch(src.numpy(), offs[vi], nb[vi])
+                b.verify = [(vi, (got.astype(np.int64) & 0xFFFFFFFF) == (expect[vi] & 0xFFFFFFFF))]
             return b
         ok = ~(enc & ((nb <= 0) | (nb % 16 != 0)))  # encrypted payloads must be whole AES blocks
         idx_ok = np.flatnonzero(ok)
         if not len(idx_ok):
             return _Batch(None, infos=[], host=[], event=None, tag=tag, n=n)
+        verify = []
+        ex = None
+        if expect is not None:
+            clear_v = np.flatnonzero((expect >= 0) & ~enc)
+            if len(clear_v):  # clear fragments: the CRC kernel (no decrypt pass to fuse into)
+                from ..ops import crc as _crc
+
+                _, okd = _crc.crc32_batch(src, offs[clear_v], nb[clear_v],
+                                          expect=(expect[clear_v] & 0xFFFFFFFF).tolist())
+                okh = torch.empty(len(clear_v), dtype=torch.uint8, pin_memory=True)
+                okh.copy_(okd, non_blocking=True)
+                verify.append((clear_v, okh))
+            ex = np.where(enc, expect, -1)[ok] if (expect[enc] >= 0).any() else None
         if not ok.all():
             offs, nb, enc, drk, iv = offs[ok], nb[ok], enc[ok], drk[ok], iv[ok]
         td0, isb = _aes.device_tables(self.device)
+        cw, ctab = (None, None)
+        if ex is not None:
+            from ..ops import crc as _crc
+
+            cw, ctab = _crc.fused_consts(self.device)
         ev0 = self._event()
-        groups, dec, host_block = _native_device().transmux_launch(
+        groups, dec, host_block, fused = _native_device().transmux_launch(
             src, offs, nb, enc.astype(np.uint8), np.ascontiguousarray(drk, dtype=np.uint32),
-            np.ascontiguousarray(iv, dtype=np.uint8), td0, isb, _ts.DEFAULT_MAX_PES)
+            np.ascontiguousarray(iv, dtype=np.uint8), td0, isb, _ts.DEFAULT_MAX_PES, ex, cw, ctab)
         infos, host = [], []
         for gidx, info, pes, es, es_offs, hinfo, hlens in groups:
             infos.append((idx_ok[gidx], _ts.DemuxResult(info, pes, es, es_offs), es_offs, hlens))
             host.append((hinfo, hlens))
+        if fused is not None:
+            verify.append((idx_ok[fused[0]], fused[1]))
         ev = self._event()
         self.timer.add("launch_columns", time.perf_counter() - t1)
-        return _Batch(None, infos=infos, host=host, event=ev, keep=(dec, host_block), tag=tag, n=n, start=ev0)
+        return _Batch(None, infos=infos, host=host, event=ev, keep=(dec, host_block), tag=tag, n=n, start=ev0,
+                      verify=verify or None)
 
     def launch_jobs(self, jobs: List[TransmuxJob]) -> "_Batch":
         """:meth:`launch` for an explicit job list (the pipeline's own queue untouched)."""
@@ -324,10 +358,11 @@ class MediaPipeline:
 
     def complete_columns(self, batch: "_Batch"):
         """Wait for a :meth:`launch_columns` batch: ``(tag, rows int64[n, INFO_WORDS], plain
-        int64[n], has_row bool[n])`` aligned with the launch columns."""
+        int64[n], has_row bool[n], verified bool[n])`` aligned with the launch columns
+        (``verified[i]`` False: fragment i failed its ``expect`` CRC)."""
         if batch.jobs is not None:  # CPU job path
             _, rows, plain, has = self.complete_arrays(batch)
-            return batch.tag, rows, plain, has
+            return batch.tag, rows, plain, has, self._verified(batch, len(batch.jobs))
         n = batch.n
         rows = np.zeros((n, _ts.INFO_WORDS), dtype=np.int64)
         plain = np.full(n, -1, dtype=np.int64)
@@ -340,7 +375,15 @@ class MediaPipeline:
             rows[idx] = (hinfo.numpy() if isinstance(hinfo, torch.Tensor) else np.asarray(hinfo))[:k]
             plain[idx] = (hlens.numpy() if isinstance(hlens, torch.Tensor) else np.asarray(hlens))[:k]
             has[idx] = True
-        return batch.tag, rows, plain, has
+        return batch.tag, rows, plain, has, self._verified(batch, n)
+
+    @staticmethod
+    def _verified(batch: "_Batch", n: int) -> np.ndarray:
+        """Per fragment: passed its CRC check (True where none was asked); call after the wait."""
+        out = np.ones(n, dtype=bool)
+        for idx, ok in batch.verify or ():
+            out[idx] = (ok.numpy() if isinstance(ok, torch.Tensor) else np.asarray(ok)).astype(bool)
+        return out
 
     def complete_rows(self, batch: Optional["_Batch"]) -> List[Tuple["TransmuxJob", Optional[list], int]]:
         """Wait for a launched batch and return ``(job, info row, plaintext length)`` per job
@@ -485,6 +528,7 @@ class _Batch:
     tag: Any = None  # launch_columns: the caller's columns, handed back by complete_columns
     n: int = 0  # launch_columns: fragments in the batch
     start: Any = None  # timing event recorded before the batch's first launch
+    verify: Any = None  # [(fragment indices, ok flags (pinned uint8 / bool))] of expect-CRC checks
 
 
 _local = threading.local()

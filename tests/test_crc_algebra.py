@@ -96,3 +96,59 @@ def test_fp4_mfma_crc_formulation_matches_zlib(rt):
         assert np.all(acc == np.round(acc)) and acc.max() <= 2048  # exact in f32
         par = sum((int(acc[c]) & 1) << c for c in range(32))
         assert par == (~zlib.crc32(grp.tobytes(), 0xFFFFFFFF)) & 0xFFFFFFFF  # zero-init register
+
+
+def _chunk_rows(chunk: np.ndarray, wf: np.ndarray) -> list:
+    """The 32 row residues of one 4096-byte chunk, as the fused decrypt + CRC kernel forms
+    them (aes_cbc.hip): lane l holds block 64j + l (chain j); row r = l & 31 and half
+    h = l >> 5; step s = 4j + d feeds dword d of that block as four e2m1 operand dwords."""
+    words = chunk.view("<u4").reshape(256, 4).astype(np.uint64)
+    acc = np.zeros((32, 32))
+    for s in range(16):
+        j, d = s >> 2, s & 3
+        for h in range(2):
+            for r in range(32):
+                dw = int(words[64 * j + 32 * h + r, d])
+                a = _fp4_elements([dw & 0x11111111, dw & 0x22222222, dw & 0x44444444, (dw >> 1) & 0x44444444])
+                for col in range(32):
+                    b = _fp4_elements(wf[s, col + 32 * h].view("<u4"))
+                    acc[r, col] += float((a * b).sum())
+    rows = []
+    for r in range(32):
+        v = 0
+        for col in range(32):
+            v |= (int(acc[r, col]) & 1) << col
+        rows.append(v)
+    return rows
+
+
+def test_fused_chunk_crc_formulation_matches_zlib(rt):
+    """The CRC fused into the AES decrypt: per-chunk row residues (host weights from
+    crc_chunk_weights_fp4), folded per chunk with the 16-byte shift P_4 (Horner over the 32
+    rows), then a Horner over 4096-byte chunks (P_12), the pad removal Q_0..Q_11 and the
+    init term -- as crc32_rows_fold + crc32_combine(lg_group=12) compute them."""
+    wf = rt.crc_chunk_weights_fp4().reshape(16, 64, 16)
+    tab = rt.crc_shift_tables()
+    assert rt.CRC_NUM_Q == 12 and len(tab) == (40 + 12) * 1024
+    rng = np.random.default_rng(5)
+    for n in (16, 4096, 4096 + 48, 2 * 4096 + 4000):
+        data = rng.integers(0, 256, n, dtype=np.uint8).tobytes()
+        C = (n + 4095) // 4096
+        buf = np.zeros(C * 4096, np.uint8)
+        buf[:n] = np.frombuffer(data, np.uint8)
+        raw = 0
+        for c in range(C):
+            rows = _chunk_rows(buf[c * 4096:(c + 1) * 4096], wf)
+            chunk = 0
+            for v in rows:
+                chunk = _apply(tab, 4, chunk) ^ v
+            raw = _apply(tab, 12, raw) ^ chunk
+        pad = C * 4096 - n
+        for b in range(12):
+            if (pad >> b) & 1:
+                raw = _apply(tab, 40 + b, raw)
+        init = 0xFFFFFFFF
+        for b in range(40):
+            if (n >> b) & 1:
+                init = _apply(tab, b, init)
+        assert raw ^ init ^ 0xFFFFFFFF == zlib.crc32(data), n

@@ -103,6 +103,17 @@ def test_bench_two_ranks_abr_ladder_with_churn(players):
     _check_per_rank(calm, 2)
 
 
+def test_bench_fleet_corrupted_peer_copies_are_refetched():
+    """Fleet mode defers the receive-side CRC to the transmux that decrypts the segment
+    (FleetServer sets verify_deferred): a peer copy corrupted on arrival in each of the first
+    3 timed rounds is caught there, no player gets its result, the node re-fetches it from
+    the CDN, and every player still buffers its fragments without an error."""
+    res = _bench_cpu(_free_port(), "--players", "2", "--corrupt-recv", "3", "--steps", "10")
+    assert res["errors"] == 0 and res["value"] > 0
+    fails = sum(r["crc_failures"] for r in res["per_rank"])
+    assert 1 <= fails <= 6  # at most one per corrupted round on each rank
+
+
 def test_bench_eight_ranks_driver_shape():
     """The driver's N=8 launch (torchrun, 8 ranks, one bench.py each) rehearsed on CPU with
     gloo: shared-memory control plane across 8 processes with 4 player processes each,

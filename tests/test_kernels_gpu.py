@@ -197,3 +197,34 @@ def test_arena_views_share_storage(cuda):
     assert views[2].data_ptr() == arena.data_ptr() + 1000 and torch.equal(views[2], arena[1000:4000])
     with pytest.raises(ValueError):
         device().arena_views(arena, np.array([16000], np.int64), np.array([1000], np.int64))
+
+
+@pytest.mark.gpu
+def test_fused_decrypt_crc_matches_zlib_at_segment_sizes(cuda):
+    """The CRC fused into the AES decrypt (aes_cbc.hip AesCrc + crc32_rows_fold / combine<12>)
+    on bench-sized ciphertexts: 48 segments of 16 B .. 3 MB, every CRC equal to zlib's; one
+    corrupted byte fails exactly its segment."""
+    import zlib
+
+    from hlsjs_p2p_wrapper_amd.player.transmux import MediaPipeline
+    from hlsjs_p2p_wrapper_amd.net import new_event_loop
+
+    rng = np.random.default_rng(11)
+    sizes = [16, 4096, 4112] + [int(x) * 16 for x in rng.integers(1, 3_000_000 // 16, 45)]
+    offs, pos = [], 0
+    for n in sizes:
+        offs.append(pos)
+        pos += (n + 255) // 256 * 256
+    host = rng.integers(0, 256, pos, dtype=np.uint8)
+    arena = torch.from_numpy(host).to(cuda)
+    crcs = np.array([zlib.crc32(host[o:o + n].tobytes()) for o, n in zip(offs, sizes)], dtype=np.int64)
+    B = len(sizes)
+    drk = np.tile(aes.round_keys_le(bytes(16)), (B, 1)).astype(np.uint32)
+    iv = np.zeros((B, 16), dtype=np.uint8)
+    pipe = MediaPipeline(cuda, new_event_loop("virtual"))
+    o, nb, enc = np.asarray(offs, dtype=np.int64), np.asarray(sizes, dtype=np.int64), np.ones(B, dtype=bool)
+    *_, ok = pipe.complete_columns(pipe.launch_columns(arena, o, nb, enc, drk, iv, expect=crcs))
+    assert ok.all(), np.flatnonzero(~ok)
+    arena[offs[7] + sizes[7] // 2] ^= 0x40
+    *_, ok = pipe.complete_columns(pipe.launch_columns(arena, o, nb, enc, drk, iv, expect=crcs))
+    assert np.flatnonzero(~ok).tolist() == [7]

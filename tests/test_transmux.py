@@ -112,3 +112,59 @@ def test_complete_arrays_matches_per_job_results(device):
     for n in range(len(jobs)):
         assert has[n] and rows[n].tolist() == ref[n]["info"]._row and plain[n] == ref[n]["plain_bytes"]
     assert not has[-1] and plain[-1] == -1
+
+
+@pytest.mark.parametrize("device", ["cpu", pytest.param("cuda", marks=pytest.mark.gpu)])
+def test_launch_columns_verifies_expected_crcs(device, request):
+    """Fragments handed to the transmux with a peer's CRC (``expect``) are verified by the
+    batch that decrypts them: on the GPU the CRC is fused into the AES decrypt (encrypted
+    fragments) or run by the CRC kernel (clear ones).  A wrong expectation fails exactly that
+    fragment, the decrypt + demux results are the same as without verification, and the
+    fused CRC matches zlib for sizes around the 4096-byte chunk edges."""
+    import zlib
+
+    import numpy as np
+
+    if device == "cuda":
+        request.getfixturevalue("cuda")
+    jobs, arena, views, offs = _arena_jobs(device)
+    # extra encrypted fragments of awkward sizes: 16 B, one chunk, one chunk + 16, 3 chunks - 16
+    key = bytes(range(16))
+    extra = []
+    for i, n in enumerate((16, 4096, 4112, 3 * 4096 - 16)):
+        rng = np.random.default_rng(40 + i)
+        extra.append(rng.integers(0, 256, n, dtype=np.uint8))
+    pos = arena.numel()
+    big = torch.zeros(pos + sum((len(e) + 255) // 256 * 256 for e in extra), dtype=torch.uint8, device=device)
+    big[:pos] = arena
+    for e in extra:
+        big[pos:pos + len(e)] = torch.from_numpy(e).to(device)
+        offs = offs + [pos]
+        pos += (len(e) + 255) // 256 * 256
+    payloads = [p for _, p, _, _ in jobs] + extra
+    enc = np.array([k is not None for _, _, k, _ in jobs] + [True] * len(extra))
+    n = len(payloads)
+    drk = np.tile(aes.round_keys_le(key), (n, 1)).astype(np.uint32)
+    iv = np.stack([np.frombuffer(j[3] if j[3] is not None else bytes(16), dtype=np.uint8) for j in jobs]
+                  + [np.frombuffer(bytes(16), dtype=np.uint8)] * len(extra))
+    keys = np.tile(np.frombuffer(key, dtype=np.uint8), (n, 1))
+    nb = np.array([len(p) for p in payloads], dtype=np.int64)
+    crcs = np.array([zlib.crc32(bytes(p)) for p in payloads], dtype=np.int64)
+    expect = crcs.copy()
+    expect[1] ^= 0x10  # a clear fragment with a wrong trailer
+    expect[2] ^= 1     # an encrypted one
+    expect[3] = -1     # not verified
+    expect[-1] ^= 1 << 31
+    loop = new_event_loop("virtual")
+    pipe = MediaPipeline(torch.device(device), loop)
+    o = np.asarray(offs, dtype=np.int64)
+    tag, rows, plain, has, ok = pipe.complete_columns(pipe.launch_columns(big, o, nb, enc, drk, iv, "t", keys=keys,
+                                                                          expect=expect))
+    want = np.ones(n, dtype=bool)
+    want[[1, 2, n - 1]] = False
+    assert tag == "t" and ok.tolist() == want.tolist()
+    _, rows0, plain0, has0, ok0 = pipe.complete_columns(pipe.launch_columns(big, o, nb, enc, drk, iv, keys=keys))
+    assert ok0.all() and np.array_equal(rows, rows0) and np.array_equal(plain, plain0) and np.array_equal(has, has0)
+    # every fused CRC is exact: expecting the true values passes all of them
+    *_, ok_all = pipe.complete_columns(pipe.launch_columns(big, o, nb, enc, drk, iv, keys=keys, expect=crcs))
+    assert ok_all.all()

@@ -11,7 +11,8 @@ cd $R
 export PYTHONPATH=$R
 O=gpurun_out/r4_ab
 mkdir -p $O
-timeout -k 10 300 python -u -m pytest tests/test_stream_safety_gpu.py -v --timeout 120 --timeout-method thread > $O/stream_tests.log 2>&1
+timeout -k 10 300 python -u -m pytest tests/test_stream_safety_gpu.py tests/test_transmux.py tests/test_kernels_gpu.py tests/test_torch_ops.py -v --timeout 120 --timeout-method thread > $O/gpu_tests.log 2>&1
+timeout -k 10 300 python tools/transmux_bench.py --segs 256 --iters 10 > $O/transmux_bench.log 2>&1
 for i in 1 2; do
   timeout -k 10 300 python bench.py --inflight 64 --verbose > $O/head64_$i.log 2>&1
   timeout -k 10 300 python bench.py --inflight 128 --verbose > $O/head128_$i.log 2>&1
