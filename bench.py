@@ -327,11 +327,11 @@ def main() -> int:
         seg = max(max(pool.lengths) for pool in origin.pools)
         per_round = (world - 1) * K * max(1, W) * (seg + 512) + (1 << 20)
         os.environ.setdefault("HLSP2P_IPC_OUTBOX_BYTES", str(per_round))
-        if args.inflight > 64:
-            # host-side packing waits instead of interprocess events: at 128 in flight the event
-            # mode faulted on the device once, the host-wait mode ran clean
-            # (profiles/r3_validation/NOTES.md); events stay on at the validated 64
-            os.environ.setdefault("HLSP2P_IPC_EVENTS", "0")
+    if world > 1:
+        # the control all-gather's shared-memory slot: a round's message is ~16 + 6 words per
+        # want + 5 per add + 4 per remove (agent/node.py:_encode); size it for this step's
+        # wants with room for adds / removes of the same order, so no round falls back to gloo
+        os.environ.setdefault("HLSP2P_SHM_SLOT_WORDS", str(max(16384, 64 + 20 * K * max(1, W))))
     node = node_for_config(p2p_config)
     if W:
         return _fleet(args, world, rank, device, use_gpu, node, origin, players, desc, encrypted, seg_dur,

@@ -6,10 +6,15 @@ the four-kernel TS demux (ts_demux.hip), as one ``transmux_launch``.  Batches of
 against this sequence; all three were slower and were removed in round 4 -- their numbers
 stay in profiles/r3_transmux_fused_vs_split.md and profiles/r3_scatter/.)
 
-    PYTHONPATH=. python tools/transmux_bench.py [--segs 256] [--iters 10]
+    PYTHONPATH=. python tools/transmux_bench.py [--segs 256] [--iters 10] [--verify]
+
+``--verify`` also times the batch with every segment's ciphertext CRC checked by the decrypt
+(the CRC fused into aes_cbc.hip, as the fleet's deferred receive verification runs it), and
+adds the separate CRC kernel the node would otherwise run for comparison.
 """
 import argparse
 import json
+import zlib
 
 import numpy as np
 import torch
@@ -26,6 +31,7 @@ def main():
     ap.add_argument("--pool", type=int, default=64,
                     help="distinct segments (the batch cycles through them): 64 x 3 MB fits the 256 MB "
                          "Infinity Cache (MALL), 256 does not -- as in the pipeline, where every segment is new")
+    ap.add_argument("--verify", action="store_true")
     args = ap.parse_args()
     cuda = torch.device("cuda", 0)
     dev = device()
@@ -42,20 +48,36 @@ def main():
     td0, isb = aes.device_tables(cuda)
     total = int(lens.sum())
 
-    def launch():
-        return dev.transmux_launch(src, offs, lens, enc, drk, iv, td0, isb, tsdemux.DEFAULT_MAX_PES)
+    def launch(expect=None, cw=None, ctab=None):
+        return dev.transmux_launch(src, offs, lens, enc, drk, iv, td0, isb, tsdemux.DEFAULT_MAX_PES, expect, cw, ctab)
 
-    keep = [launch() for _ in range(2)]
-    torch.cuda.synchronize()
-    a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    a.record()
-    for _ in range(args.iters):
-        keep.append(launch())
-    b.record()
-    torch.cuda.synchronize()
-    us = a.elapsed_time(b) * 1e3 / args.iters
-    print(json.dumps({"segs": args.segs, "bytes": total, "us": round(us, 1), "us_per_seg": round(us / args.segs, 3),
-                      "GBps": round(total / (us * 1e-6) / 1e9, 1)}))
+    def timed(fn):
+        keep = [fn() for _ in range(2)]
+        torch.cuda.synchronize()
+        a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        a.record()
+        for _ in range(args.iters):
+            keep.append(fn())
+        b.record()
+        torch.cuda.synchronize()
+        return a.elapsed_time(b) * 1e3 / args.iters, keep
+
+    us, _ = timed(launch)
+    out = {"segs": args.segs, "bytes": total, "us": round(us, 1), "us_per_seg": round(us / args.segs, 3),
+           "GBps": round(total / (us * 1e-6) / 1e9, 1)}
+    if args.verify:
+        from hlsjs_p2p_wrapper_amd.ops import crc
+
+        host = pool.data.numpy()
+        expect = np.array([zlib.crc32(host[o:o + n].tobytes()) for o, n in zip(offs, lens)], dtype=np.int64)
+        cw, ctab = crc.fused_consts(cuda)
+        us_v, keep = timed(lambda: launch(expect, cw, ctab))
+        ok = all(bool(k[3][1].numpy().all()) for k in keep)
+        us_c, _ = timed(lambda: crc.crc32_batch(src, offs, lens, expect=(expect & 0xFFFFFFFF).tolist()))
+        out.update(fused_us=round(us_v, 1), fused_us_per_seg=round(us_v / args.segs, 3), fused_all_ok=ok,
+                   crc_kernel_us_per_seg=round(us_c / args.segs, 3),
+                   separate_us_per_seg=round((us + us_c) / args.segs, 3))
+    print(json.dumps(out))
 
 
 if __name__ == "__main__":
