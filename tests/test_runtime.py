@@ -25,6 +25,30 @@ def test_store_reserve_commit_lookup_delta(rt):
     assert len(add) == 0 and rm[:, 3].tolist() == [1]
 
 
+def test_store_detach_keeps_pinned_bytes_until_the_ring_reaches_them(rt):
+    """A received copy that failed its deferred CRC check is detached: no longer found (nor
+    announced: it was never committed), its id stays valid while readers hold pins, the key
+    can be reserved again at once, and the ring frees the old bytes only after the pins drop."""
+    st = rt.SegmentStore(4 * 1024, 256)
+    _, ids, _ = st.reserve_run(keys(1, 2), np.array([1024, 1024]), 0)
+    st.commit(ids[1:])
+    st.pin(ids[:1])
+    st.take_delta()
+    st.detach(ids[:1])
+    assert st.lookup(keys(1), True).tolist() == [-1]
+    add, rm = st.take_delta()
+    assert len(add) == 0 and len(rm) == 0  # pending: nobody was told about it
+    _, again, _ = st.reserve_run(keys(1), np.array([1024]), 1)
+    assert again[0] != ids[0] and st.lookup(keys(1), True).tolist() == again.tolist()
+    # the ring is full up to the detached, pinned entry: no room until it is unpinned
+    assert st.reserve_run(keys(9), np.array([2048]), 2) is None
+    st.unpin(ids[:1])
+    assert st.reserve_run(keys(9), np.array([2048]), 3) is not None
+    st.detach(np.array([ids[1]]))  # a resident one is announced as removed
+    _, rm = st.take_delta()
+    assert rm[:, 3].tolist() == [2]
+
+
 def _plan_rows(ks, lens, src, dst, seeded=0):
     rows = np.zeros((len(ks), 9), dtype=np.int64)
     rows[:, :4] = ks
