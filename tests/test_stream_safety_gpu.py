@@ -15,7 +15,21 @@ import pytest
 import torch
 
 SENTINEL = 0x5A5A5A5A
-SLEEP_CYCLES = 200_000_000  # ~0.1 s of device time: the default stream runs first
+LATE = 0x0F0F0F0F  # what the held-back node-stream write stores
+
+
+def _sleep_cycles(cuda, ms=200.0):
+    """``torch.cuda._sleep`` cycles for ~``ms`` of device time (calibrated: the counter it
+    spins on is not the shader clock on every part)."""
+    s = torch.cuda.Stream(cuda)
+    a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    with torch.cuda.stream(s):
+        a.record(s)
+        torch.cuda._sleep(10_000_000)
+        b.record(s)
+    b.synchronize()
+    per_cycle = max(a.elapsed_time(b), 1e-3) / 10_000_000
+    return int(min(ms / per_cycle, 2**31 - 1))
 
 
 def _segments(arena, n, seg=4096):
@@ -32,19 +46,16 @@ def test_old_crc_table_pattern_is_detected(cuda):
     replaced from the node stream without record_stream) lets a default-stream allocation
     take the table's block while a scatter into it is still queued -- the sentinel is
     overwritten.  Shows the check below can see the race."""
-    from hlsjs_p2p_wrapper_amd.ops import crc as _crc
-
     torch.cuda.synchronize()
     node_stream = torch.cuda.Stream(cuda)
-    arena = torch.zeros(1 << 20, dtype=torch.uint8, device=cuda)
-    offs, lens = _segments(arena, 64)
     size = 4100
     table = torch.zeros(size, dtype=torch.int32, device=cuda)  # default-stream allocation
     old_ptr = table.data_ptr()
     torch.cuda.synchronize()
+    cycles = _sleep_cycles(cuda)
     with torch.cuda.stream(node_stream):
-        torch.cuda._sleep(SLEEP_CYCLES)
-        _crc.crc32_batch(arena, offs, lens, scatter_to=table, scatter_idx=np.arange(64))
+        torch.cuda._sleep(cycles)
+        table[:64].fill_(LATE)  # stands for the queued CRC scatter (plain torch: no host sync)
         new = torch.zeros(2 * size, dtype=torch.int32, device=cuda)
         new[:size] = table
         table = new  # the old block goes back to the default stream's pool right now
@@ -55,8 +66,7 @@ def test_old_crc_table_pattern_is_detected(cuda):
     if probe is None:
         pytest.skip("no default-stream allocation received the freed block (control inconclusive)")
     p, off = probe
-    clobbered = int((p[off:off + 64] != SENTINEL).sum())
-    assert clobbered == 64  # exactly the scattered entries
+    assert (p[off:off + 64] == LATE).all()  # the late write landed in the new owner's memory
 
 
 def _covering_probe(cuda, size, ptr, tries=256):
@@ -87,8 +97,9 @@ def test_node_crc_table_grow_is_stream_safe(cuda):
     offs, lens = _segments(node.arena, 64)
     torch.cuda.synchronize()
     old_table_ptr = node.crc_dev.data_ptr()
+    cycles = _sleep_cycles(cuda)
     with torch.cuda.stream(node.stream):  # as launch_round's phases run
-        torch.cuda._sleep(SLEEP_CYCLES)
+        torch.cuda._sleep(cycles)
         _crc.crc32_batch(node.arena, offs, lens, scatter_to=node.crc_dev, scatter_idx=np.arange(64))
         node._grow_crc(size + 1)
     old_ptr = old_table_ptr
