@@ -80,9 +80,9 @@ def parse():
     p.add_argument("--warmup", type=int, default=5)
     p.add_argument("--config", default="1080p6m", choices=sorted(CONFIGS))
     p.add_argument("--inflight", type=int, default=None,
-                   help="fragments in flight per player (per step), default 64; 128 amortises the per-step "
-                        "device and host costs (+10-20 %% on the device-bound HBM-origin probe, flat on the "
-                        "PCIe-bound headline, profiles/r3_inflight) but is not validated with peers yet")
+                   help="fragments in flight per player (per step), default 64 -- chosen by measurement: 128 "
+                        "is flat on the PCIe-bound headline and was -4 %% to +20 %% on the device-bound "
+                        "HBM-origin probe across boxes (profiles/r3_inflight, profiles/r4_ab)")
     p.add_argument("--pool", type=int, default=64, help="distinct packaged segments per rendition")
     p.add_argument("--cache-gb", type=float, default=None,
                    help="segment-cache arena per GPU (default 8 GB)")
@@ -248,9 +248,9 @@ def _spawn_players(W, world, rank, origin_kwargs, hls_config, p2p_base, n_segmen
 def main() -> int:
     args = parse()
     if args.inflight is None:
-        # 64: the setting every N > 1 path (RCCL, HIP-IPC rehearsal) was validated with.  The
-        # device-bound HBM-origin probe gains 10-20 % at 128 (profiles/r3_inflight), but a 2-rank
-        # HIP-IPC rehearsal at 128 faulted on the device (open item), so bigger steps stay opt-in
+        # 64, by measurement (profiles/r4_ab): the headline is PCIe-bound and flat at 128; the
+        # HBM-origin probe was +10-20 % at 128 on round-3 boxes and -4 % on round 4's.  (The
+        # round-3 2-rank fault at 128 was the CRC-table lifetime bug, fixed: profiles/r4_uaf.)
         args.inflight = 64
     if args.cache_gb is None:
         args.cache_gb = 8.0
@@ -818,12 +818,12 @@ def _per_rank(node, pipe, s0, s1, elapsed, steps, inflight, fleet_total=None, ti
 def _per_rank_dicts(parts, steps) -> list:
     """Decode the gathered rows; add each rank's ``bound`` label.
 
-    Rule: the host waited on the device for more than 30 % of a step (``wait_device`` and
-    ``exchange`` per round x rounds per step + the transmux wait) -> device-bound, by the
-    busiest stream:
-    ``pcie`` (H2D copy stream), ``xgmi`` (the node stream's exchange), ``transmux`` (decrypt +
-    demux); otherwise ``players`` when the fleet wait exceeds the own host work, else
-    ``host``."""
+    Rule: the busiest device stream -- ``pcie`` (H2D copy stream), ``xgmi`` (the node
+    stream's exchange), ``transmux`` (decrypt + demux) -- when it is busy for >= 80 % of a
+    step (the pipeline keeps it saturated), or when the host waited on the device for more
+    than 30 % of a step (``wait_device`` and ``exchange`` per round x rounds per step + the
+    transmux wait); otherwise ``players`` when the fleet's wait on its players exceeds half a
+    step, else ``host``."""
     out = []
     for p in parts:
         d = {k: float(v) / 1000 for k, v in zip(PER_RANK_FIELDS, np.asarray(p).tolist())}
@@ -836,8 +836,9 @@ def _per_rank_dicts(parts, steps) -> list:
         rps = d["rounds"] / max(1, steps)
         waited = ((d["wait_device_us"] + d["exchange_us"]) * rps + d["transmux_wait_us"]) / 1e3
         busy = {"pcie": d["cdn_dev_ms"] * rps, "xgmi": d["p2p_dev_ms"] * rps, "transmux": d["transmux_dev_ms"]}
-        if waited > 0.3 * step:
-            d["bound"] = max(busy, key=busy.get)
+        top = max(busy, key=busy.get)
+        if busy[top] >= 0.8 * step or waited > 0.3 * step:
+            d["bound"] = top
         elif d["await_players_us"] / 1e3 > 0.5 * step:
             d["bound"] = "players"
         else:
