@@ -63,9 +63,11 @@ struct AesCrc {
   uint16_t* masks;
 };
 
+template <int kMode>
 __device__ __forceinline__ void crc_chunk_masks(const uint4 (&c)[kBlk], const v4i* __restrict__ wfrag, int lane,
                                                 uint16_t* __restrict__ out) {
   v16f acc = {};
+  uint32_t sink = 0;
 #pragma unroll
   for (int j = 0; j < kBlk; ++j) {
     const uint32_t dw[4] = {c[j].x, c[j].y, c[j].z, c[j].w};
@@ -74,11 +76,15 @@ __device__ __forceinline__ void crc_chunk_masks(const uint4 (&c)[kBlk], const v4
       const uint32_t x = dw[d];
       const v8i a = {static_cast<int>(x & 0x11111111u), static_cast<int>(x & 0x22222222u),
                      static_cast<int>(x & 0x44444444u), static_cast<int>((x >> 1) & 0x44444444u), 0, 0, 0, 0};
-      const v4i b4 = wfrag[(4 * j + d) * 64 + lane];
+      const v4i b4 = kMode == 2 ? v4i{lane, 0, 0, 0} : wfrag[(4 * j + d) * 64 + lane];
       const v8i b = {b4.x, b4.y, b4.z, b4.w, 0, 0, 0, 0};
-      acc = __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(a, b, acc, 4, 4, 0, 0, 0, 0);
+      if (kMode == 3)
+        sink ^= static_cast<uint32_t>(a[0] ^ a[1] ^ a[2] ^ a[3] ^ b[0] ^ b[1] ^ b[2] ^ b[3]);
+      else
+        acc = __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(a, b, acc, 4, 4, 0, 0, 0, 0);
     }
   }
+  if (kMode == 3) acc[0] = static_cast<float>(sink & 1u);
   uint32_t m = 0;  // exact counts: the parity is the GF(2) sum
 #pragma unroll
   for (int i = 0; i < 16; ++i) m |= (static_cast<uint32_t>(static_cast<int>(acc[i])) & 1u) << i;
@@ -90,6 +96,11 @@ __device__ __forceinline__ void crc_chunk_masks(const uint4 (&c)[kBlk], const v4
 // chunk_prefix: exclusive prefix of per-segment 256-block chunks (one chunk = one wave
 //   iteration: lane l decrypts blocks 64j + l, j < kBlk, so every load/store instruction
 //   moves 1 KB contiguous); waves never straddle segments
+// kCrc (A/B experiment, HLSP2P_AES_CRC_MODE): 0 no CRC code; 1 CRC before the rounds (the
+// ciphertext in VGPRs); 2 = 1 without the weight loads (timing only); 3 = 1 without the MFMAs
+// (timing only); 4 CRC steps interleaved with the rounds (two per round, data dwords re-read
+// from L1), branch-free.
+template <int kCrc>
 __global__ __launch_bounds__(kAesThreads, 1) void aes128_cbc_decrypt_kernel(
     const uint8_t* __restrict__ src, uint8_t* __restrict__ dst, const int64_t* __restrict__ src_off,
     const int64_t* __restrict__ dst_off, const int64_t* __restrict__ blk_prefix,
@@ -139,13 +150,50 @@ __global__ __launch_bounds__(kAesThreads, 1) void aes128_cbc_decrypt_kernel(
       const int64_t b = b0 + 64 * j;
       pv[j] = b == 0 ? reinterpret_cast<const uint4*>(ivw)[cur] : (b < nblk ? cs[b - 1] : make_uint4(0, 0, 0, 0));
     }
-    if (maskb >= 0) crc_chunk_masks(c, crc.wfrag, lane, crc.masks + maskb + (ch - cstart) * 64);  // wave-uniform
+    if constexpr (kCrc >= 1 && kCrc <= 3) {
+      if (maskb >= 0)  // wave-uniform
+        crc_chunk_masks<kCrc>(c, crc.wfrag, lane, crc.masks + maskb + (ch - cstart) * 64);
+    }
     uint32_t st[kBlk][4];
 #pragma unroll
     for (int j = 0; j < kBlk; ++j) {
       st[j][0] = c[j].x ^ rk[0]; st[j][1] = c[j].y ^ rk[1]; st[j][2] = c[j].z ^ rk[2]; st[j][3] = c[j].w ^ rk[3];
     }
-    AES_ROUNDS_PIPELINED(kBlk, st, rk)
+    if constexpr (kCrc == 4) {
+      v16f acc = {};
+      const uint32_t* cw = reinterpret_cast<const uint32_t*>(cs);
+      auto step = [&](int s) {  // s = 4j + d: dword d of the lane's chain-j block (an L1 hit)
+        const int64_t b = b0 + 64 * (s >> 2);
+        const uint32_t x = b < nblk ? cw[4 * b + (s & 3)] : 0u;
+        const v8i a = {static_cast<int>(x & 0x11111111u), static_cast<int>(x & 0x22222222u),
+                       static_cast<int>(x & 0x44444444u), static_cast<int>((x >> 1) & 0x44444444u), 0, 0, 0, 0};
+        const v4i b4 = crc.wfrag[s * 64 + lane];
+        const v8i bb = {b4.x, b4.y, b4.z, b4.w, 0, 0, 0, 0};
+        acc = __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(a, bb, acc, 4, 4, 0, 0, 0, 0);
+      };
+#pragma unroll
+      for (int r_ = 1; r_ < 10; ++r_) {
+        const uint32_t* k_ = rk + 4 * r_;
+        uint32_t v_[2][16];
+        if (r_ <= 8) step(2 * (r_ - 1));
+        AES_ROUND_READS(v_[0], st[0]);
+#pragma unroll
+        for (int j_ = 1; j_ < kBlk; ++j_) {
+          AES_ROUND_READS(v_[j_ & 1], st[j_]);
+          AES_ROUND_XORS(st[j_ - 1], v_[(j_ - 1) & 1], k_);
+          if (r_ <= 8 && j_ == 2) step(2 * (r_ - 1) + 1);
+        }
+        AES_ROUND_XORS(st[kBlk - 1], v_[(kBlk - 1) & 1], k_);
+      }
+      if (maskb >= 0) {
+        uint32_t m = 0;
+#pragma unroll
+        for (int i = 0; i < 16; ++i) m |= (static_cast<uint32_t>(static_cast<int>(acc[i])) & 1u) << i;
+        crc.masks[maskb + (ch - cstart) * 64 + lane] = static_cast<uint16_t>(m);
+      }
+    } else {
+      AES_ROUNDS_PIPELINED(kBlk, st, rk)
+    }
     uint4* ds = reinterpret_cast<uint4*>(dst + dof);
 #pragma unroll
     for (int j = 0; j < kBlk; ++j) {
@@ -161,6 +209,10 @@ __global__ __launch_bounds__(kAesThreads, 1) void aes128_cbc_decrypt_kernel(
 
 // 16-byte blocks per wave iteration (the host sizes its chunk index space with this)
 int aes_chunk_blocks() { return 64 * kBlk; }
+
+int g_aes_crc_mode = 1;  // the fused CRC's kernel form (kCrc above); set_aes_crc_mode
+int aes_crc_mode() { return g_aes_crc_mode; }
+void set_aes_crc_mode(int m) { g_aes_crc_mode = m; }
 
 namespace {
 void aes_grid(int64_t total_chunks, int num_cu, int64_t& grid, int64_t& per_wg) {
@@ -184,9 +236,19 @@ hipError_t launch_aes128_cbc_decrypt(const uint8_t* src, uint8_t* dst, const int
   int64_t grid, per_wg;
   aes_grid(total_chunks, num_cu, grid, per_wg);
   const AesCrc crc{crc_mask_off, reinterpret_cast<const v4i*>(crc_wfrag), crc_masks};
-  hipLaunchKernelGGL(aes128_cbc_decrypt_kernel, dim3(static_cast<unsigned>(grid)), dim3(kAesThreads), 0, stream,
-                     src, dst, src_off, dst_off, blk_prefix, chunk_prefix, drk, ivw, tdl, isb, out_len, nseg,
-                     total_chunks, per_wg, crc);
+  const int mode = crc_mask_off == nullptr ? 0 : aes_crc_mode();
+#define AES_LAUNCH(M)                                                                                             \
+  hipLaunchKernelGGL(aes128_cbc_decrypt_kernel<M>, dim3(static_cast<unsigned>(grid)), dim3(kAesThreads), 0, stream,  \
+                     src, dst, src_off, dst_off, blk_prefix, chunk_prefix, drk, ivw, tdl, isb, out_len, nseg,     \
+                     total_chunks, per_wg, crc)
+  switch (mode) {
+    case 0: AES_LAUNCH(0); break;
+    case 2: AES_LAUNCH(2); break;
+    case 3: AES_LAUNCH(3); break;
+    case 4: AES_LAUNCH(4); break;
+    default: AES_LAUNCH(1); break;
+  }
+#undef AES_LAUNCH
   return hipGetLastError();
 }
 

@@ -350,6 +350,7 @@ __global__ __launch_bounds__(kCombineThreads) void crc32_combine_kernel(
 // and the chunk residue XOR_r A^(8 * 16 (31 - r)) D[r] is a 5-level tree across the lanes with
 // the byte-slice tables P_4 .. P_8 (shifts of 16 .. 256 bytes, in LDS).  One wave per chunk.
 constexpr int kFoldThreads = 256;
+constexpr int kFoldIlp = 4;  // chunks per wave iteration: four independent trees hide the LDS latency
 __global__ __launch_bounds__(kFoldThreads) void crc32_rows_fold_kernel(const uint16_t* __restrict__ masks,
                                                                       const uint32_t* __restrict__ tables,
                                                                       uint32_t* __restrict__ chunk_res,
@@ -360,24 +361,41 @@ __global__ __launch_bounds__(kFoldThreads) void crc32_rows_fold_kernel(const uin
   __syncthreads();
   const int lane = threadIdx.x & 63;
   const int64_t waves = static_cast<int64_t>(gridDim.x) * (kFoldThreads / 64);
-  for (int64_t c = static_cast<int64_t>(blockIdx.x) * (kFoldThreads / 64) + (threadIdx.x >> 6); c < total_chunks;
-       c += waves) {
-    const uint32_t m = masks[64 * c + lane];
-    uint32_t res = 0;
+  const int64_t w0 = static_cast<int64_t>(blockIdx.x) * (kFoldThreads / 64) + (threadIdx.x >> 6);
+  for (int64_t c0 = w0 * kFoldIlp; c0 < total_chunks; c0 += waves * kFoldIlp) {
+    uint32_t m[kFoldIlp], res[kFoldIlp];
+#pragma unroll
+    for (int u = 0; u < kFoldIlp; ++u) {
+      const int64_t c = c0 + u < total_chunks ? c0 + u : total_chunks - 1;  // (a duplicate is not stored)
+      m[u] = masks[64 * c + lane];
+      res[u] = 0;
+    }
 #pragma unroll
     for (int i = 0; i < 16; ++i) {
-      const uint64_t b = __ballot((m >> i) & 1u);
       const int row = (i & 3) + 8 * (i >> 2);
-      res = lane == row ? static_cast<uint32_t>(b) : res;
-      res = lane == row + 4 ? static_cast<uint32_t>(b >> 32) : res;
+#pragma unroll
+      for (int u = 0; u < kFoldIlp; ++u) {
+        const uint64_t b = __ballot((m[u] >> i) & 1u);
+        res[u] = lane == row ? static_cast<uint32_t>(b) : res[u];
+        res[u] = lane == row + 4 ? static_cast<uint32_t>(b >> 32) : res[u];
+      }
     }
     // tree over rows 0..31: level k merges runs of 2^k rows, the left run moved 16 * 2^k bytes
 #pragma unroll
     for (int k = 0; k < 5; ++k) {
-      const uint32_t right = static_cast<uint32_t>(__shfl_down(static_cast<int>(res), 1 << k, 64));
-      if ((lane & ((2 << k) - 1)) == 0) res = apply_tab(s_p + k * kSlice, res) ^ right;
+      uint32_t right[kFoldIlp];
+#pragma unroll
+      for (int u = 0; u < kFoldIlp; ++u) right[u] = static_cast<uint32_t>(__shfl_down(static_cast<int>(res[u]), 1 << k, 64));
+      if ((lane & ((2 << k) - 1)) == 0) {
+#pragma unroll
+        for (int u = 0; u < kFoldIlp; ++u) res[u] = apply_tab(s_p + k * kSlice, res[u]) ^ right[u];
+      }
     }
-    if (lane == 0) chunk_res[c] = res;
+#pragma unroll
+    for (int u = 0; u < kFoldIlp; ++u) {  // chunk c0 + u's residue is lane 0's res[u]
+      const uint32_t v = static_cast<uint32_t>(__shfl(static_cast<int>(res[u]), 0, 64));
+      if (lane == u && c0 + u < total_chunks) chunk_res[c0 + u] = v;
+    }
   }
 }
 
@@ -391,8 +409,9 @@ hipError_t launch_crc32_from_masks(const uint16_t* masks, const int64_t* chunk_o
                                    int num_cu, hipStream_t stream) {
   if (nseg <= 0) return hipSuccess;
   if (total_chunks > 0) {
-    const int64_t waves_max = static_cast<int64_t>(num_cu) * 16;
-    const int64_t waves = total_chunks < waves_max ? total_chunks : waves_max;
+    const int64_t waves_max = static_cast<int64_t>(num_cu) * 32;
+    const int64_t need = (total_chunks + kFoldIlp - 1) / kFoldIlp;
+    const int64_t waves = need < waves_max ? need : waves_max;
     const int64_t grid = (waves + (kFoldThreads / 64) - 1) / (kFoldThreads / 64);
     hipLaunchKernelGGL(crc32_rows_fold_kernel, dim3(static_cast<unsigned>(grid)), dim3(kFoldThreads), 0, stream, masks,
                        tables, chunk_res, total_chunks);

@@ -23,6 +23,8 @@
 namespace hlsp2p {
 namespace dev {
 int aes_chunk_blocks();
+int aes_crc_mode();
+void set_aes_crc_mode(int);
 hipError_t launch_aes128_cbc_decrypt(const uint8_t*, uint8_t*, const int64_t*, const int64_t*, const int64_t*,
                                      const int64_t*, const uint32_t*, const uint32_t*, const uint32_t*,
                                      const uint8_t*, int64_t*, int, int64_t, int, hipStream_t, const int64_t*,
@@ -360,6 +362,9 @@ void register_transmux(py::module& m) {
   m.def("set_cu_reserve", [](int n) { g_cu_reserve = std::max(0, n); }, py::arg("n"),
         "CUs the persistent decrypt grid leaves free for concurrent (RCCL) kernels");
   m.def("cu_reserve", [] { return g_cu_reserve; });
+  m.def("set_aes_crc_mode", &hlsp2p::dev::set_aes_crc_mode, py::arg("mode"),
+        "kernel form of the CRC fused into the decrypt (A/B experiment; 1 = default)");
+  m.def("aes_crc_mode", &hlsp2p::dev::aes_crc_mode);
   m.def("transmux_launch", &transmux_launch, py::arg("src"), py::arg("src_off"), py::arg("nbytes"), py::arg("enc"),
         py::arg("drk"), py::arg("iv"), py::arg("td0"), py::arg("isb"), py::arg("max_pes"),
         py::arg("expect") = py::none(), py::arg("crc_w") = py::none(), py::arg("crc_tables") = py::none());
