@@ -47,8 +47,9 @@ def _device_consts(device: torch.device, variant: str):
 
 def fused_consts(device: torch.device):
     """Device constants of the CRC fused into the AES decrypt (``kernels/aes_cbc.hip``
-    ``AesCrc``; ``transmux_launch(..., expect, crc_w, crc_tables)``): the chunk B fragments
-    (16 steps x 64 lanes x 16 bytes) and the shift tables P_0..P_39, Q_0..Q_11."""
+    ``AesCrc``; ``transmux_launch(..., expect, crc_w, crc_tables)``): the decrypt's B fragments (4 steps x
+    64 lanes x 16 bytes) followed by the chunk fold's A fragments (64 steps), and the shift
+    tables P_0..P_39, Q_0..Q_11."""
     k = (str(device), "chunk")
     c = _consts.get(k)
     if c is None:

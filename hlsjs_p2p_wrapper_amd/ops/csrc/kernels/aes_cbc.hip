@@ -48,47 +48,55 @@ typedef float v16f __attribute__((ext_vector_type(16)));
 // a segment that arrived from a peer is verified by the batch that decrypts it, instead of by a
 // separate read pass).  The ciphertext is already in VGPRs and the matrix cores sit idle
 // while the decrypt is VALU / LDS bound, so each flagged chunk adds 16 FP4 MFMAs
-// (v_mfma_scale_f32_32x32x64_f8f6f4, the operand scheme of crc32_mfma.hip): step 4j + d feeds
-// dword d of the lane's chain-j block.  Row r (lane & 31) collects the blocks r + 32m, m =
-// 2j + (lane >> 5), under weights that place every block at row 31's position
-// (crc_host.cpp: mfma_chunk_weights_fp4), so no data moves between lanes; the 32 row
-// accumulator parities go out as one 16-bit word per lane (`masks`: 64 per chunk, bit i =
-// parity of accumulator i: row (i & 3) + 8 (i >> 2) + 4 (lane >> 5), column lane & 31), and
-// crc32_rows_fold_kernel (crc32_mfma.hip) transposes them to row residues with ballots and
-// finishes the chunk -- no ballot SGPRs beside the 44 round keys here.
+// (v_mfma_scale_f32_32x32x64_f8f6f4, the operand scheme of crc32_mfma.hip): chains 2p and 2p + 1
+// share accumulator set p; step (j & 1, d) feeds dword d of the lane's block 64j + l, row
+// rho = l & 31 collecting blocks 64j + rho and 64j + rho + 32 (k half l >> 5).  The 8 weight
+// steps are the same for both pairs (crc_host.cpp: mfma_chunk_weights_fp4), so they are loaded
+// once per wave and stay in 32 VGPRs; the pair's position moves to the fold.  The parities of
+// the 2 x 16 accumulators go out as one dword per lane (`masks`: 64 per chunk, bit 16 p + i =
+// row (i & 3) + 8 (i >> 2) + 4 (lane >> 5), column lane & 31); crc32_chunk_fold_kernel
+// (crc32_mfma.hip) turns them into the chunk residue with a second FP4 GEMM.
+//
+// (Round 4 measured a one-level form first -- 16 chain-specific weight steps re-read from L1
+// per chunk, one parity word per lane: +50 us per 256-segment batch in this kernel; then one
+// accumulator set per chain (4 steps in VGPRs): +76 us at +15.7 % VALU instructions and the
+// same clock -- the kernel is VALU + LDS co-bound, so every operand or parity instruction
+// costs time.  profiles/r4_fused.)
 struct AesCrc {
-  const int64_t* mask_off;  // [nseg] the segment's first mask word (64 per 4096-byte chunk), -1:
+  const int64_t* mask_off;  // [nseg] the segment's first mask dword (64 per 4096-byte chunk), -1:
                             // no CRC for it (nullptr: for no segment)
-  const v4i* wfrag;         // [16 steps][64 lanes] B fragments
-  uint16_t* masks;
+  const v4i* wfrag;         // [8 steps][64 lanes] B fragments
+  uint32_t* masks;
 };
+constexpr int kCrcSteps = 8;  // [chain parity jj][data dword d]
 
-template <int kMode>
-__device__ __forceinline__ void crc_chunk_masks(const uint4 (&c)[kBlk], const v4i* __restrict__ wfrag, int lane,
-                                                uint16_t* __restrict__ out) {
-  v16f acc = {};
-  uint32_t sink = 0;
+__device__ __forceinline__ void crc_chunk_masks(const uint4 (&c)[kBlk], const v4i (&w)[kCrcSteps], int lane,
+                                                uint32_t* __restrict__ out) {
+  // accumulators start at 2^23: the counts stay exact and the float's mantissa LSB is the parity,
+  // so one v_alignbit per accumulator moves it into the mask word (no float -> int conversion)
+  const v16f init = {8388608.f, 8388608.f, 8388608.f, 8388608.f, 8388608.f, 8388608.f, 8388608.f, 8388608.f,
+                     8388608.f, 8388608.f, 8388608.f, 8388608.f, 8388608.f, 8388608.f, 8388608.f, 8388608.f};
+  uint32_t m = 0;
+  v16f acc = init;
 #pragma unroll
-  for (int j = 0; j < kBlk; ++j) {
+  for (int j = 0; j < kBlk; ++j) {  // chains 2p and 2p + 1 share accumulator set p
     const uint32_t dw[4] = {c[j].x, c[j].y, c[j].z, c[j].w};
 #pragma unroll
     for (int d = 0; d < 4; ++d) {
       const uint32_t x = dw[d];
       const v8i a = {static_cast<int>(x & 0x11111111u), static_cast<int>(x & 0x22222222u),
                      static_cast<int>(x & 0x44444444u), static_cast<int>((x >> 1) & 0x44444444u), 0, 0, 0, 0};
-      const v4i b4 = kMode == 2 ? v4i{lane, 0, 0, 0} : wfrag[(4 * j + d) * 64 + lane];
-      const v8i b = {b4.x, b4.y, b4.z, b4.w, 0, 0, 0, 0};
-      if (kMode == 3)
-        sink ^= static_cast<uint32_t>(a[0] ^ a[1] ^ a[2] ^ a[3] ^ b[0] ^ b[1] ^ b[2] ^ b[3]);
-      else
-        acc = __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(a, b, acc, 4, 4, 0, 0, 0, 0);
+      const v4i& wv = w[4 * (j & 1) + d];
+      const v8i b = {wv.x, wv.y, wv.z, wv.w, 0, 0, 0, 0};
+      acc = __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(a, b, acc, 4, 4, 0, 0, 0, 0);
+    }
+    if (j & 1) {
+#pragma unroll
+      for (int i = 0; i < 16; ++i) m = __builtin_amdgcn_alignbit(__float_as_uint(acc[i]), m, 1);
+      acc = init;
     }
   }
-  if (kMode == 3) acc[0] = static_cast<float>(sink & 1u);
-  uint32_t m = 0;  // exact counts: the parity is the GF(2) sum
-#pragma unroll
-  for (int i = 0; i < 16; ++i) m |= (static_cast<uint32_t>(static_cast<int>(acc[i])) & 1u) << i;
-  out[lane] = static_cast<uint16_t>(m);
+  out[lane] = m;  // bits 16 p + i
 }
 
 // tdl: little-endian Td0 (256 words); isb: inverse S-box (256 bytes)
@@ -96,10 +104,7 @@ __device__ __forceinline__ void crc_chunk_masks(const uint4 (&c)[kBlk], const v4
 // chunk_prefix: exclusive prefix of per-segment 256-block chunks (one chunk = one wave
 //   iteration: lane l decrypts blocks 64j + l, j < kBlk, so every load/store instruction
 //   moves 1 KB contiguous); waves never straddle segments
-// kCrc (A/B experiment, HLSP2P_AES_CRC_MODE): 0 no CRC code; 1 CRC before the rounds (the
-// ciphertext in VGPRs); 2 = 1 without the weight loads (timing only); 3 = 1 without the MFMAs
-// (timing only); 4 CRC steps interleaved with the rounds (two per round, data dwords re-read
-// from L1), branch-free.
+// kCrc: 0 without the fused CRC code (its registers), 1 with it
 template <int kCrc>
 __global__ __launch_bounds__(kAesThreads, 1) void aes128_cbc_decrypt_kernel(
     const uint8_t* __restrict__ src, uint8_t* __restrict__ dst, const int64_t* __restrict__ src_off,
@@ -124,6 +129,11 @@ __global__ __launch_bounds__(kAesThreads, 1) void aes128_cbc_decrypt_kernel(
   int cur = -1;
   uint32_t rk[44];
   int64_t so = 0, dof = 0, cstart = 0, cend = 0, nblk = 0, maskb = -1;
+  v4i crc_w[kCrcSteps];
+  if constexpr (kCrc == 1) {
+#pragma unroll
+    for (int d = 0; d < kCrcSteps; ++d) crc_w[d] = crc.wfrag[d * 64 + lane];
+  }
   for (int64_t ch = uniform64(begin + (tid >> 6)); ch < end; ch += kWaves) {
     if (cur < 0 || ch >= cend) {
       cur = cur < 0 ? find_seg_wave(chunk_prefix, nseg, ch)  // whole wave active: ch is uniform
@@ -150,50 +160,16 @@ __global__ __launch_bounds__(kAesThreads, 1) void aes128_cbc_decrypt_kernel(
       const int64_t b = b0 + 64 * j;
       pv[j] = b == 0 ? reinterpret_cast<const uint4*>(ivw)[cur] : (b < nblk ? cs[b - 1] : make_uint4(0, 0, 0, 0));
     }
-    if constexpr (kCrc >= 1 && kCrc <= 3) {
+    if constexpr (kCrc == 1) {
       if (maskb >= 0)  // wave-uniform
-        crc_chunk_masks<kCrc>(c, crc.wfrag, lane, crc.masks + maskb + (ch - cstart) * 64);
+        crc_chunk_masks(c, crc_w, lane, crc.masks + maskb + (ch - cstart) * 64);
     }
     uint32_t st[kBlk][4];
 #pragma unroll
     for (int j = 0; j < kBlk; ++j) {
       st[j][0] = c[j].x ^ rk[0]; st[j][1] = c[j].y ^ rk[1]; st[j][2] = c[j].z ^ rk[2]; st[j][3] = c[j].w ^ rk[3];
     }
-    if constexpr (kCrc == 4) {
-      v16f acc = {};
-      const uint32_t* cw = reinterpret_cast<const uint32_t*>(cs);
-      auto step = [&](int s) {  // s = 4j + d: dword d of the lane's chain-j block (an L1 hit)
-        const int64_t b = b0 + 64 * (s >> 2);
-        const uint32_t x = b < nblk ? cw[4 * b + (s & 3)] : 0u;
-        const v8i a = {static_cast<int>(x & 0x11111111u), static_cast<int>(x & 0x22222222u),
-                       static_cast<int>(x & 0x44444444u), static_cast<int>((x >> 1) & 0x44444444u), 0, 0, 0, 0};
-        const v4i b4 = crc.wfrag[s * 64 + lane];
-        const v8i bb = {b4.x, b4.y, b4.z, b4.w, 0, 0, 0, 0};
-        acc = __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(a, bb, acc, 4, 4, 0, 0, 0, 0);
-      };
-#pragma unroll
-      for (int r_ = 1; r_ < 10; ++r_) {
-        const uint32_t* k_ = rk + 4 * r_;
-        uint32_t v_[2][16];
-        if (r_ <= 8) step(2 * (r_ - 1));
-        AES_ROUND_READS(v_[0], st[0]);
-#pragma unroll
-        for (int j_ = 1; j_ < kBlk; ++j_) {
-          AES_ROUND_READS(v_[j_ & 1], st[j_]);
-          AES_ROUND_XORS(st[j_ - 1], v_[(j_ - 1) & 1], k_);
-          if (r_ <= 8 && j_ == 2) step(2 * (r_ - 1) + 1);
-        }
-        AES_ROUND_XORS(st[kBlk - 1], v_[(kBlk - 1) & 1], k_);
-      }
-      if (maskb >= 0) {
-        uint32_t m = 0;
-#pragma unroll
-        for (int i = 0; i < 16; ++i) m |= (static_cast<uint32_t>(static_cast<int>(acc[i])) & 1u) << i;
-        crc.masks[maskb + (ch - cstart) * 64 + lane] = static_cast<uint16_t>(m);
-      }
-    } else {
-      AES_ROUNDS_PIPELINED(kBlk, st, rk)
-    }
+    AES_ROUNDS_PIPELINED(kBlk, st, rk)
     uint4* ds = reinterpret_cast<uint4*>(dst + dof);
 #pragma unroll
     for (int j = 0; j < kBlk; ++j) {
@@ -209,10 +185,6 @@ __global__ __launch_bounds__(kAesThreads, 1) void aes128_cbc_decrypt_kernel(
 
 // 16-byte blocks per wave iteration (the host sizes its chunk index space with this)
 int aes_chunk_blocks() { return 64 * kBlk; }
-
-int g_aes_crc_mode = 1;  // the fused CRC's kernel form (kCrc above); set_aes_crc_mode
-int aes_crc_mode() { return g_aes_crc_mode; }
-void set_aes_crc_mode(int m) { g_aes_crc_mode = m; }
 
 namespace {
 void aes_grid(int64_t total_chunks, int num_cu, int64_t& grid, int64_t& per_wg) {
@@ -231,23 +203,19 @@ hipError_t launch_aes128_cbc_decrypt(const uint8_t* src, uint8_t* dst, const int
                                      const int64_t* blk_prefix, const int64_t* chunk_prefix, const uint32_t* drk,
                                      const uint32_t* ivw, const uint32_t* tdl, const uint8_t* isb, int64_t* out_len,
                                      int nseg, int64_t total_chunks, int num_cu, hipStream_t stream,
-                                     const int64_t* crc_mask_off, const void* crc_wfrag, uint16_t* crc_masks) {
+                                     const int64_t* crc_mask_off, const void* crc_wfrag, uint32_t* crc_masks) {
   if (total_chunks <= 0) return hipSuccess;
   int64_t grid, per_wg;
   aes_grid(total_chunks, num_cu, grid, per_wg);
   const AesCrc crc{crc_mask_off, reinterpret_cast<const v4i*>(crc_wfrag), crc_masks};
-  const int mode = crc_mask_off == nullptr ? 0 : aes_crc_mode();
 #define AES_LAUNCH(M)                                                                                             \
   hipLaunchKernelGGL(aes128_cbc_decrypt_kernel<M>, dim3(static_cast<unsigned>(grid)), dim3(kAesThreads), 0, stream,  \
                      src, dst, src_off, dst_off, blk_prefix, chunk_prefix, drk, ivw, tdl, isb, out_len, nseg,     \
                      total_chunks, per_wg, crc)
-  switch (mode) {
-    case 0: AES_LAUNCH(0); break;
-    case 2: AES_LAUNCH(2); break;
-    case 3: AES_LAUNCH(3); break;
-    case 4: AES_LAUNCH(4); break;
-    default: AES_LAUNCH(1); break;
-  }
+  if (crc_mask_off == nullptr)
+    AES_LAUNCH(0);
+  else
+    AES_LAUNCH(1);
 #undef AES_LAUNCH
   return hipGetLastError();
 }

@@ -15,7 +15,7 @@ int aes_chunk_blocks();
 hipError_t launch_aes128_cbc_decrypt(const uint8_t*, uint8_t*, const int64_t*, const int64_t*, const int64_t*,
                                      const int64_t*, const uint32_t*, const uint32_t*, const uint32_t*,
                                      const uint8_t*, int64_t*, int, int64_t, int, hipStream_t, const int64_t*,
-                                     const void*, uint16_t*);
+                                     const void*, uint32_t*);
 hipError_t launch_crc32_batch(const uint8_t*, const int64_t*, const int64_t*, const int64_t*, const int64_t*,
                               const void*, const uint32_t*, uint32_t*, uint32_t*, const uint32_t*, uint8_t*,
                               const int64_t*, uint32_t*, int64_t, int, int64_t, int, bool, hipStream_t);

@@ -258,7 +258,7 @@ constexpr uint32_t kInitFold4096 = 0x38e3ffeeu;  // 4096-byte chunks of the fuse
 
 // One workgroup per segment.  tables: P_0..P_39 then Q_0..Q_11 (each kSlice u32).  Group
 // residues of 2^kLg bytes: 256-byte groups (the residue kernels above) or 4096-byte chunks
-// (the CRC fused into the decrypt, folded by crc32_rows_fold_kernel).
+// (the CRC fused into the decrypt, folded by crc32_chunk_fold_kernel).
 template <int kLg>
 __global__ __launch_bounds__(kCombineThreads) void crc32_combine_kernel(
     const uint32_t* __restrict__ residues, const int64_t* __restrict__ res_off, const int64_t* __restrict__ seg_len,
@@ -344,77 +344,80 @@ __global__ __launch_bounds__(kCombineThreads) void crc32_combine_kernel(
   }
 }
 
-// The fused decrypt CRC's per-chunk fold (aes_cbc.hip: crc_chunk_masks).  A chunk's 64 lane
-// words carry the parity bits of the MFMA accumulators (bit i of lane l: row (i & 3) + 8 (i >> 2)
-// + 4 (l >> 5), column l & 31); 16 ballots turn them into the 32 row residues D[r] (lane r),
-// and the chunk residue XOR_r A^(8 * 16 (31 - r)) D[r] is a 5-level tree across the lanes with
-// the byte-slice tables P_4 .. P_8 (shifts of 16 .. 256 bytes, in LDS).  One wave per chunk.
-constexpr int kFoldThreads = 256;
-constexpr int kFoldIlp = 4;  // chunks per wave iteration: four independent trees hide the LDS latency
-__global__ __launch_bounds__(kFoldThreads) void crc32_rows_fold_kernel(const uint16_t* __restrict__ masks,
-                                                                      const uint32_t* __restrict__ tables,
-                                                                      uint32_t* __restrict__ chunk_res,
-                                                                      int64_t total_chunks) {
-  __shared__ __attribute__((aligned(16))) uint32_t s_p[5 * kSlice];  // P_4 .. P_8
-  lds_fill<5 * kSlice / 4 / kFoldThreads>(reinterpret_cast<uint4*>(s_p), reinterpret_cast<const uint4*>(tables + 4 * kSlice),
-                                          5 * kSlice / 4, threadIdx.x, kFoldThreads);
+// The fused decrypt CRC's second level (aes_cbc.hip: crc_chunk_masks writes 64 mask dwords per
+// 4096-byte chunk, the accumulator parities of chain pairs p = 0, 1 in bits 16 p + i).  The
+// chunk residue is XOR_{p,rho} S[p][rho] D_p[rho] -- over GF(2) a [32 CRC bits x 2048] x
+// [2048 x chunks] GEMM, on the same FP4 MFMA: A = the host's S fragments (crc_host.cpp:
+// mfma_chunk_weights_fp4 after the 8 decrypt steps; 32 KiB, one ds_read_b128 per lane per step
+// from LDS), B = the chunk's mask dwords fed as e2m1 bit planes (k half hh of step s = mask
+// dword s + 32 hh), 32 chunks per wave tile, 32 MFMAs per tile.  Lane l ends with 16 residue
+// bits of chunk l & 31 (rows (i & 3) + 8 (i >> 2) + 4 (l >> 5)); one cross-half swap completes
+// the word.  (Round 4's first fold transposed one-level masks with 16 ballots per chunk and a
+// 5-level table tree: 45-50 us per 256-segment batch.)
+constexpr int kFoldThreads = 512;
+constexpr int kFoldSteps = 32;
+constexpr int kMaskDwords = 64;  // per chunk
+__global__ __launch_bounds__(kFoldThreads) void crc32_chunk_fold_kernel(const uint32_t* __restrict__ masks,
+                                                                       const v4i* __restrict__ wfold,
+                                                                       uint32_t* __restrict__ chunk_res,
+                                                                       int64_t total_chunks) {
+  __shared__ v4i s_w[kFoldSteps * 64];  // 32 KiB: [step][lane] A fragments
+  const int tid = threadIdx.x;
+  lds_fill<kFoldSteps * 64 / kFoldThreads>(s_w, wfold, kFoldSteps * 64, tid, kFoldThreads);
   __syncthreads();
-  const int lane = threadIdx.x & 63;
+  const int lane = tid & 63;
+  const int hh = lane >> 5;
+  const int64_t tiles = (total_chunks + 31) >> 5;
   const int64_t waves = static_cast<int64_t>(gridDim.x) * (kFoldThreads / 64);
-  const int64_t w0 = static_cast<int64_t>(blockIdx.x) * (kFoldThreads / 64) + (threadIdx.x >> 6);
-  for (int64_t c0 = w0 * kFoldIlp; c0 < total_chunks; c0 += waves * kFoldIlp) {
-    uint32_t m[kFoldIlp], res[kFoldIlp];
+  for (int64_t t = static_cast<int64_t>(blockIdx.x) * (kFoldThreads / 64) + (tid >> 6); t < tiles; t += waves) {
+    const int64_t c = t * 32 + (lane & 31);
+    const bool valid = c < total_chunks;
+    const uint4* src = reinterpret_cast<const uint4*>(masks + (valid ? c : 0) * kMaskDwords + 32 * hh);
+    uint4 x[kFoldSteps / 4];  // this lane's 32 mask dwords (128 contiguous bytes), all loads in flight
 #pragma unroll
-    for (int u = 0; u < kFoldIlp; ++u) {
-      const int64_t c = c0 + u < total_chunks ? c0 + u : total_chunks - 1;  // (a duplicate is not stored)
-      m[u] = masks[64 * c + lane];
-      res[u] = 0;
-    }
+    for (int k = 0; k < kFoldSteps / 4; ++k) x[k] = valid ? src[k] : make_uint4(0, 0, 0, 0);
+    v16f acc = {};
 #pragma unroll
-    for (int i = 0; i < 16; ++i) {
-      const int row = (i & 3) + 8 * (i >> 2);
+    for (int k = 0; k < kFoldSteps / 4; ++k) {
+      const uint32_t dw[4] = {x[k].x, x[k].y, x[k].z, x[k].w};
 #pragma unroll
-      for (int u = 0; u < kFoldIlp; ++u) {
-        const uint64_t b = __ballot((m[u] >> i) & 1u);
-        res[u] = lane == row ? static_cast<uint32_t>(b) : res[u];
-        res[u] = lane == row + 4 ? static_cast<uint32_t>(b >> 32) : res[u];
+      for (int u = 0; u < 4; ++u) {
+        const uint32_t d = dw[u];
+        const v8i b = {static_cast<int>(d & 0x11111111u), static_cast<int>(d & 0x22222222u),
+                       static_cast<int>(d & 0x44444444u), static_cast<int>((d >> 1) & 0x44444444u), 0, 0, 0, 0};
+        const v4i a4 = s_w[(4 * k + u) * 64 + lane];
+        const v8i a = {a4.x, a4.y, a4.z, a4.w, 0, 0, 0, 0};
+        acc = __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(a, b, acc, 4, 4, 0, 0, 0, 0);
       }
+      // keep the next group's LDS reads below this one (hoisting them all spills)
+      __builtin_amdgcn_sched_barrier(0);
     }
-    // tree over rows 0..31: level k merges runs of 2^k rows, the left run moved 16 * 2^k bytes
+    uint32_t part = 0;  // CRC bits (i & 3) + 8 (i >> 2) + 4 hh of chunk lane & 31
 #pragma unroll
-    for (int k = 0; k < 5; ++k) {
-      uint32_t right[kFoldIlp];
-#pragma unroll
-      for (int u = 0; u < kFoldIlp; ++u) right[u] = static_cast<uint32_t>(__shfl_down(static_cast<int>(res[u]), 1 << k, 64));
-      if ((lane & ((2 << k) - 1)) == 0) {
-#pragma unroll
-        for (int u = 0; u < kFoldIlp; ++u) res[u] = apply_tab(s_p + k * kSlice, res[u]) ^ right[u];
-      }
-    }
-#pragma unroll
-    for (int u = 0; u < kFoldIlp; ++u) {  // chunk c0 + u's residue is lane 0's res[u]
-      const uint32_t v = static_cast<uint32_t>(__shfl(static_cast<int>(res[u]), 0, 64));
-      if (lane == u && c0 + u < total_chunks) chunk_res[c0 + u] = v;
-    }
+    for (int i = 0; i < 16; ++i)
+      part |= (static_cast<uint32_t>(static_cast<int>(acc[i])) & 1u) << ((i & 3) + 8 * (i >> 2) + 4 * hh);
+    const uint32_t res = part | static_cast<uint32_t>(__shfl_xor(static_cast<int>(part), 32, 64));
+    if (lane < 32 && valid) chunk_res[c] = res;
   }
 }
 
-// masks: 64 words per 4096-byte chunk for each segment, the segment's chunks starting at
-// word 64 * chunk_off[seg]; chunk_res: scratch of total_chunks words.  Same outputs as
-// launch_crc32_batch.
-hipError_t launch_crc32_from_masks(const uint16_t* masks, const int64_t* chunk_off, const int64_t* seg_len,
-                                   const uint32_t* tables, uint32_t* chunk_res, uint32_t* crc_out,
-                                   const uint32_t* expect, uint8_t* ok_out, const int64_t* scatter_idx,
-                                   uint32_t* scatter_out, int64_t scatter_n, int nseg, int64_t total_chunks,
-                                   int num_cu, hipStream_t stream) {
+// masks: 64 dwords per 4096-byte chunk for each segment, the segment's chunks starting at
+// dword 64 * chunk_off[seg]; wfold: the fold's A fragments; chunk_res: scratch of total_chunks
+// words.  Same outputs as launch_crc32_batch.
+hipError_t launch_crc32_from_masks(const uint32_t* masks, const void* wfold, const int64_t* chunk_off,
+                                   const int64_t* seg_len, const uint32_t* tables, uint32_t* chunk_res,
+                                   uint32_t* crc_out, const uint32_t* expect, uint8_t* ok_out,
+                                   const int64_t* scatter_idx, uint32_t* scatter_out, int64_t scatter_n, int nseg,
+                                   int64_t total_chunks, int num_cu, hipStream_t stream) {
   if (nseg <= 0) return hipSuccess;
   if (total_chunks > 0) {
-    const int64_t waves_max = static_cast<int64_t>(num_cu) * 32;
-    const int64_t need = (total_chunks + kFoldIlp - 1) / kFoldIlp;
-    const int64_t waves = need < waves_max ? need : waves_max;
-    const int64_t grid = (waves + (kFoldThreads / 64) - 1) / (kFoldThreads / 64);
-    hipLaunchKernelGGL(crc32_rows_fold_kernel, dim3(static_cast<unsigned>(grid)), dim3(kFoldThreads), 0, stream, masks,
-                       tables, chunk_res, total_chunks);
+    const int64_t tiles = (total_chunks + 31) / 32;
+    const int64_t grid_max = static_cast<int64_t>(num_cu) * 4;  // 32 KiB LDS: up to 4 workgroups per CU
+    int64_t grid = (tiles + (kFoldThreads / 64) - 1) / (kFoldThreads / 64);
+    if (grid > grid_max) grid = grid_max;
+    hipLaunchKernelGGL(crc32_chunk_fold_kernel, dim3(static_cast<unsigned>(grid)), dim3(kFoldThreads), 0, stream,
+                       masks, reinterpret_cast<const v4i*>(wfold), chunk_res,
+                       total_chunks);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
   }

@@ -23,15 +23,13 @@
 namespace hlsp2p {
 namespace dev {
 int aes_chunk_blocks();
-int aes_crc_mode();
-void set_aes_crc_mode(int);
 hipError_t launch_aes128_cbc_decrypt(const uint8_t*, uint8_t*, const int64_t*, const int64_t*, const int64_t*,
                                      const int64_t*, const uint32_t*, const uint32_t*, const uint32_t*,
                                      const uint8_t*, int64_t*, int, int64_t, int, hipStream_t, const int64_t*,
-                                     const void*, uint16_t*);
+                                     const void*, uint32_t*);
 hipError_t launch_ts_demux(const uint8_t*, const int64_t*, const int64_t*, const int64_t*, int, int64_t, uint32_t*,
                            int64_t*, int32_t*, uint8_t*, const int64_t*, int64_t*, int64_t, int64_t*, hipStream_t);
-hipError_t launch_crc32_from_masks(const uint16_t*, const int64_t*, const int64_t*, const uint32_t*, uint32_t*, uint32_t*,
+hipError_t launch_crc32_from_masks(const uint32_t*, const void*, const int64_t*, const int64_t*, const uint32_t*, uint32_t*, uint32_t*,
                                    const uint32_t*, uint8_t*, const int64_t*, uint32_t*, int64_t, int, int64_t, int,
                                    hipStream_t);
 }  // namespace dev
@@ -183,7 +181,7 @@ py::tuple transmux_launch(Tensor src, I64 src_off, I64 nbytes, py::array_t<uint8
     if (!any) v_exp.clear();
     else
       TORCH_CHECK_VALUE(crc_w.has_value() && crc_tables.has_value() && crc_w->is_cuda() &&
-                            crc_w->numel() * crc_w->element_size() >= 16 * 64 * 16 && crc_tables->is_cuda() &&
+                            crc_w->numel() * crc_w->element_size() >= (8 + 32) * 64 * 16 && crc_tables->is_cuda() &&
                             crc_tables->numel() >= (40 + 12) * 1024,
                         "fused CRC verify needs the chunk weights and shift tables on the device");
   }
@@ -211,7 +209,7 @@ py::tuple transmux_launch(Tensor src, I64 src_off, I64 nbytes, py::array_t<uint8
       if (!v_exp.empty()) {
         const int64_t nch = (blocks + chunk - 1) / chunk;  // one 4096-byte CRC chunk per decrypt chunk
         if (v_exp[i] >= 0) {
-          a_mo.push_back(64 * v_chunks);
+          a_mo.push_back(64 * v_chunks);  // crc_host.hpp kFusedMaskDwords
           v_idx.push_back(i);
           v_coff.push_back(v_chunks);
           v_len.push_back(nb[i]);
@@ -271,7 +269,7 @@ py::tuple transmux_launch(Tensor src, I64 src_off, I64 nbytes, py::array_t<uint8
   if (ne) out_len = torch::empty({ne}, dev_opts.dtype(torch::kInt64));
   Tensor masks, chunk_res, v_crc, v_ok, v_ok_host;
   if (nv) {
-    masks = torch::empty({64 * v_chunks}, dev_opts.dtype(torch::kInt16));
+    masks = torch::empty({64 * v_chunks}, dev_opts.dtype(torch::kInt32));
     chunk_res = torch::empty({std::max<int64_t>(1, v_chunks)}, dev_opts.dtype(torch::kInt32));
     v_crc = torch::empty({nv}, dev_opts.dtype(torch::kInt32));
     v_ok = torch::empty({nv}, dev_opts.dtype(torch::kUInt8));
@@ -284,12 +282,13 @@ py::tuple transmux_launch(Tensor src, I64 src_off, I64 nbytes, py::array_t<uint8
                desc.at<uint32_t>(d_drk), desc.at<uint32_t>(d_iv), static_cast<const uint32_t*>(td0.data_ptr()),
                static_cast<const uint8_t*>(isb.data_ptr()), out_len.data_ptr<int64_t>(), static_cast<int>(ne),
                a_cp.back(), decrypt_cus(device), st, nv ? desc.at<int64_t>(d_mo) : nullptr,
-               nv ? crc_w->data_ptr() : nullptr, nv ? reinterpret_cast<uint16_t*>(masks.data_ptr<int16_t>()) : nullptr),
+               nv ? crc_w->data_ptr() : nullptr, nv ? reinterpret_cast<uint32_t*>(masks.data_ptr<int32_t>()) : nullptr),
            "aes128_cbc_decrypt");
   }
   if (nv) {  // fold the decrypt's CRC masks per chunk, combine per segment, compare
     hip_ok(hlsp2p::dev::launch_crc32_from_masks(
-               reinterpret_cast<const uint16_t*>(masks.data_ptr<int16_t>()), desc.at<int64_t>(d_vco),
+               reinterpret_cast<const uint32_t*>(masks.data_ptr<int32_t>()),
+               static_cast<const uint8_t*>(crc_w->data_ptr()) + 8 * 64 * 16, desc.at<int64_t>(d_vco),
                desc.at<int64_t>(d_vl), static_cast<const uint32_t*>(crc_tables->data_ptr()),
                reinterpret_cast<uint32_t*>(chunk_res.data_ptr<int32_t>()),
                reinterpret_cast<uint32_t*>(v_crc.data_ptr<int32_t>()), desc.at<uint32_t>(d_vx),
@@ -362,9 +361,6 @@ void register_transmux(py::module& m) {
   m.def("set_cu_reserve", [](int n) { g_cu_reserve = std::max(0, n); }, py::arg("n"),
         "CUs the persistent decrypt grid leaves free for concurrent (RCCL) kernels");
   m.def("cu_reserve", [] { return g_cu_reserve; });
-  m.def("set_aes_crc_mode", &hlsp2p::dev::set_aes_crc_mode, py::arg("mode"),
-        "kernel form of the CRC fused into the decrypt (A/B experiment; 1 = default)");
-  m.def("aes_crc_mode", &hlsp2p::dev::aes_crc_mode);
   m.def("transmux_launch", &transmux_launch, py::arg("src"), py::arg("src_off"), py::arg("nbytes"), py::arg("enc"),
         py::arg("drk"), py::arg("iv"), py::arg("td0"), py::arg("isb"), py::arg("max_pes"),
         py::arg("expect") = py::none(), py::arg("crc_w") = py::none(), py::arg("crc_tables") = py::none());

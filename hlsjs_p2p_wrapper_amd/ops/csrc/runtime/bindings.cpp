@@ -220,6 +220,9 @@ PYBIND11_MODULE(_runtime, m) {
   m.attr("CRC_NUM_Q") = crc::kNumQ;
   m.attr("CRC_GROUP_BYTES") = crc::kGroupBytes;
   m.attr("CRC_CHUNK_BYTES") = crc::kChunkBytes;
+  m.attr("CRC_FUSED_AES_STEPS") = crc::kFusedAesSteps;
+  m.attr("CRC_FUSED_FOLD_STEPS") = crc::kFusedFoldSteps;
+  m.attr("CRC_FUSED_MASK_DWORDS") = crc::kFusedMaskDwords;
 
   // ------------------------------------------------------------------ TS
   m.def("mux_segment", [](double duration, double fps, int64_t target_bytes, int audio_kbps, bool with_id3,

@@ -192,33 +192,51 @@ std::vector<uint8_t> mfma_chunk_weights_fp4() {
   const ByteTable& T = table();
   const Mat a8 = zero_byte_op();
   static const uint8_t kOne[4] = {0x4, 0x2, 0x1, 0x1};  // e2m1: 2.0, 1.0, 0.5, 0.5 (as the group form)
-  std::vector<uint8_t> w(16 * 64 * 16, 0);
-  // vec[m][y][bit] = A^(8 (512 (7 - m) + 15 - y)) t(bit)
-  static uint32_t vec[8][16][8];
-  for (int m = 0; m < 8; ++m) {
-    const Mat um = power(a8, uint64_t(512) * (7 - m));
-    for (int bit = 0; bit < 8; ++bit) {
-      uint32_t r = apply(um, T.t[0][1u << bit]);
-      for (int y = 15; y >= 0; --y) {
-        vec[m][y][bit] = r;
-        r = (r >> 8) ^ T.t[0][r & 0xff];  // one more zero byte after it
+  std::vector<uint8_t> w(size_t(kFusedAesSteps + kFusedFoldSteps) * 64 * 16, 0);
+  auto put = [&](uint8_t* frag, int v, int e) { frag[4 * v + (e >> 1)] |= static_cast<uint8_t>(kOne[v] << (4 * (e & 1))); };
+  // decrypt side: vec[jj][h][y][bit] = A^(8 (1024 (1 - jj) + 512 (1 - h) + 15 - y)) t(bit)
+  static uint32_t vec[2][2][16][8];
+  for (int jj = 0; jj < 2; ++jj)
+    for (int h = 0; h < 2; ++h) {
+      const Mat u = power(a8, uint64_t(1024) * (1 - jj) + uint64_t(512) * (1 - h));
+      for (int bit = 0; bit < 8; ++bit) {
+        uint32_t r = apply(u, T.t[0][1u << bit]);
+        for (int y = 15; y >= 0; --y) {
+          vec[jj][h][y][bit] = r;
+          r = (r >> 8) ^ T.t[0][r & 0xff];  // one more zero byte after it
+        }
       }
     }
-  }
-  for (int s = 0; s < 16; ++s) {
-    const int j = s >> 2, d = s & 3;
+  for (int st = 0; st < kFusedAesSteps; ++st) {
+    const int jj = st >> 2, d = st & 3;
     for (int lane = 0; lane < 64; ++lane) {
-      const int col = lane & 31, h = lane >> 5, m = 2 * j + h;
-      uint8_t* frag = &w[(size_t(s) * 64 + lane) * 16];
+      const int col = lane & 31, h = lane >> 5;
+      uint8_t* frag = &w[(size_t(st) * 64 + lane) * 16];
       for (int v = 0; v < 4; ++v)
         for (int e = 0; e < 8; ++e) {
           const int bit = 4 * e + v;  // bit of the data dword (element 8v + e)
-          const int y = 4 * d + (bit >> 3);
-          if (!((vec[m][y][bit & 7] >> col) & 1u)) continue;
-          frag[4 * v + (e >> 1)] |= static_cast<uint8_t>(kOne[v] << (4 * (e & 1)));
+          if ((vec[jj][h][4 * d + (bit >> 3)][bit & 7] >> col) & 1u) put(frag, v, e);
         }
     }
   }
+  // fold side: S[p][rho] = A^(8 * 16 (159 - 128 p - rho)) moves row rho of chain pair p to the chunk end
+  static Mat S[2][32];
+  const Mat m16 = power(a8, 16);
+  for (int p = 0; p < 2; ++p)
+    for (int rho = 0; rho < 32; ++rho) S[p][rho] = power(m16, uint64_t(159 - 128 * p - rho));
+  for (int s = 0; s < kFusedFoldSteps; ++s)
+    for (int lane = 0; lane < 64; ++lane) {
+      const int row = lane & 31, hh = lane >> 5;  // A row = output CRC bit; k half
+      const int lp = s + 32 * hh;                 // the chunk's mask dword this k half reads = its decrypt lane
+      uint8_t* frag = &w[(size_t(kFusedAesSteps + s) * 64 + lane) * 16];
+      for (int v = 0; v < 4; ++v)
+        for (int e = 0; e < 8; ++e) {
+          const int b = 4 * e + v;  // bit of the mask dword
+          const int p = b >> 4, i = b & 15;
+          const int rho = (i & 3) + 8 * (i >> 2) + 4 * (lp >> 5), n = lp & 31;
+          if ((S[p][rho].col[n] >> row) & 1u) put(frag, v, e);
+        }
+    }
   return w;
 }
 

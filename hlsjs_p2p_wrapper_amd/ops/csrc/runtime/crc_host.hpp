@@ -47,13 +47,22 @@ std::vector<int8_t> mfma_group_weights();
 std::vector<uint8_t> mfma_group_weights_fp4();
 // Byte-slice tables: P_0..P_39 then Q_0..Q_11, each kSliceWords u32.
 std::vector<uint32_t> shift_tables();
-// The CRC fused into the AES-CBC decrypt (aes_cbc.hip): a wave's 4096-byte chunk holds block
-// 64j + l in lane l, chain j.  Row r (= lane & 31) of the FP4 MFMA gets the blocks
-// r + 32m (m = 2j + (lane >> 5)); step s = 4j + d feeds dword d of the lane's chain-j block.
-// B fragments [s = 0..15][lane][16 bytes]: data bit (byte y, bit b) of a block of row-slot m
-// weighs A^(8 (512 (7 - m) + 15 - y)) t(b), so row r's residue is the chunk's contribution
-// with every block moved to row 31's position; the chunk residue is then
-// XOR_r A^(8 * 16 (31 - r)) D[r] (a Horner over the 32 rows with the 16-byte shift P_4).
+// The CRC fused into the AES-CBC decrypt (aes_cbc.hip), two FP4 MFMA levels:
+//  * decrypt side: a wave's 4096-byte chunk holds block 64j + l in lane l (chain j).  Chains 2p
+//    and 2p + 1 share accumulator set p: step (jj = j & 1, d = data dword) feeds dword d of the
+//    lane's chain-j block; row rho (= lane & 31) collects blocks 64j + rho and 64j + rho + 32
+//    (k half h = lane >> 5).  The B fragments [st = 4 jj + d][lane][16 bytes] weigh data bit
+//    (byte y, bit b) by A^(8 (1024 (1 - jj) + 512 (1 - h) + 15 - y)) t(b) -- the same for both
+//    pairs, so the 8 steps stay in VGPRs.  The accumulator parities go out as one dword per
+//    lane per chunk (bit 16 p + i = row (i & 3) + 8 (i >> 2) + 4 (lane >> 5), column lane & 31).
+//  * fold side (crc32_mfma.hip): chunk residue = XOR_{p,rho} S[p][rho] D_p[rho] with
+//    S[p][rho] = A^(8 * 16 (159 - 128 p - rho)) -- a [32 x 2048] x [2048 x chunks] GF(2) GEMM;
+//    A fragments [s = 0..31][lane][16 bytes] (row = CRC bit, k half hh reads mask dword
+//    s + 32 hh of the chunk).
+// Returns the decrypt fragments followed by the fold fragments.
+constexpr int kFusedAesSteps = 8;
+constexpr int kFusedFoldSteps = 32;
+constexpr int kFusedMaskDwords = 64;  // mask dwords per 4096-byte chunk
 std::vector<uint8_t> mfma_chunk_weights_fp4();
 // Raw (zero-init) CRC of [FF FF FF FF 00 ...] of `nbytes` bytes: zlib's init value folded into
 // the first group's residue.

@@ -98,51 +98,75 @@ def test_fp4_mfma_crc_formulation_matches_zlib(rt):
         assert par == (~zlib.crc32(grp.tobytes(), 0xFFFFFFFF)) & 0xFFFFFFFF  # zero-init register
 
 
-def _chunk_rows(chunk: np.ndarray, wf: np.ndarray) -> list:
-    """The 32 row residues of one 4096-byte chunk, as the fused decrypt + CRC kernel forms
-    them (aes_cbc.hip): lane l holds block 64j + l (chain j); row r = l & 31 and half
-    h = l >> 5; step s = 4j + d feeds dword d of that block as four e2m1 operand dwords."""
+def _planes(dw: int):
+    return [dw & 0x11111111, dw & 0x22222222, dw & 0x44444444, (dw >> 1) & 0x44444444]
+
+
+def _chunk_masks(chunk: np.ndarray, wa: np.ndarray) -> np.ndarray:
+    """The decrypt side (aes_cbc.hip: crc_chunk_masks): lane l holds block 64j + l (chain j);
+    chains 2p and 2p + 1 share accumulator set p, step (j & 1, d) feeding dword d of the
+    lane's block against the pair-independent B fragments wa[4 (j & 1) + d]; the accumulators
+    start at 2^23 (the mantissa LSB is then the parity) and lane l's 16 parities of set p go to
+    bits 16 p + i of its mask dword (i = row (i & 3) + 8 (i >> 2) + 4 (l >> 5), column l & 31)."""
     words = chunk.view("<u4").reshape(256, 4).astype(np.uint64)
-    acc = np.zeros((32, 32))
-    for s in range(16):
-        j, d = s >> 2, s & 3
-        for h in range(2):
-            for r in range(32):
-                dw = int(words[64 * j + 32 * h + r, d])
-                a = _fp4_elements([dw & 0x11111111, dw & 0x22222222, dw & 0x44444444, (dw >> 1) & 0x44444444])
-                for col in range(32):
-                    b = _fp4_elements(wf[s, col + 32 * h].view("<u4"))
-                    acc[r, col] += float((a * b).sum())
-    rows = []
-    for r in range(32):
-        v = 0
-        for col in range(32):
-            v |= (int(acc[r, col]) & 1) << col
-        rows.append(v)
-    return rows
+    b = np.stack([[_fp4_elements(wa[st, lane].view("<u4")) for lane in range(64)] for st in range(8)])
+    masks = np.zeros(64, np.uint32)
+    for p in range(2):
+        acc = np.full((32, 32), 2.0 ** 23, dtype=np.float32)  # [row][col], f32 as the MFMA accumulates
+        for jj in range(2):
+            j = 2 * p + jj
+            for d in range(4):
+                for h in range(2):
+                    for r in range(32):
+                        a = _fp4_elements(_planes(int(words[64 * j + 32 * h + r, d])))
+                        acc[r] += np.float32(b[4 * jj + d, 32 * h:32 * h + 32] @ a)
+        bits = acc.view(np.uint32) & 1
+        assert np.array_equal(bits, (acc.astype(np.int64) - 2 ** 23) & 1)
+        for lane in range(64):
+            for i in range(16):
+                row = (i & 3) + 8 * (i >> 2) + 4 * (lane >> 5)
+                masks[lane] |= int(bits[row, lane & 31]) << (16 * p + i)
+    return masks
+
+
+def _fold(masks: np.ndarray, wf: np.ndarray) -> int:
+    """The fold side (crc32_mfma.hip: crc32_chunk_fold_kernel): A = host fragments (row = CRC
+    bit), B = the chunk's mask dwords (k half hh of step s reads dword s + 32 hh)."""
+    acc = np.zeros(32)
+    for s in range(32):
+        for hh in range(2):
+            x = _fp4_elements(_planes(int(masks[s + 32 * hh])))
+            for row in range(32):
+                acc[row] += float(_fp4_elements(wf[s, row + 32 * hh].view("<u4")) @ x)
+    assert np.all(acc == np.round(acc)) and acc.max() <= 2048
+    return sum((int(acc[r]) & 1) << r for r in range(32))
 
 
 def test_fused_chunk_crc_formulation_matches_zlib(rt):
-    """The CRC fused into the AES decrypt: per-chunk row residues (host weights from
-    crc_chunk_weights_fp4), folded per chunk with the 16-byte shift P_4 (Horner over the 32
-    rows), then a Horner over 4096-byte chunks (P_12), the pad removal Q_0..Q_11 and the
-    init term -- as crc32_rows_fold + crc32_combine(lg_group=12) compute them."""
-    wf = rt.crc_chunk_weights_fp4().reshape(16, 64, 16)
+    """The CRC fused into the AES decrypt, two MFMA levels: row parities per chain pair in the
+    decrypt (8 pair-independent weight steps), a [32 x 2048] x [2048 x chunks] GF(2) GEMM
+    per chunk in the fold, then a Horner over 4096-byte chunks (P_12), the pad removal
+    Q_0..Q_11 and the init term -- as crc32_chunk_fold + crc32_combine(lg_group=12) do."""
+    na, nf = rt.CRC_FUSED_AES_STEPS, rt.CRC_FUSED_FOLD_STEPS
+    w = rt.crc_chunk_weights_fp4().reshape(na + nf, 64, 16)
+    wa, wf = w[:na], w[na:]
     tab = rt.crc_shift_tables()
-    assert rt.CRC_NUM_Q == 12 and len(tab) == (40 + 12) * 1024
+    assert rt.CRC_NUM_Q == 12 and len(tab) == (40 + 12) * 1024 and rt.CRC_FUSED_MASK_DWORDS == 64
     rng = np.random.default_rng(5)
-    for n in (16, 4096, 4096 + 48, 2 * 4096 + 4000):
+    for n in (16, 4096 + 48, 2 * 4096 + 4000):
         data = rng.integers(0, 256, n, dtype=np.uint8).tobytes()
         C = (n + 4095) // 4096
         buf = np.zeros(C * 4096, np.uint8)
         buf[:n] = np.frombuffer(data, np.uint8)
+        if n == 16:
+            buf[:16] = 0xFF  # every nibble bit set: the largest counts
+            data = bytes(buf[:16])
         raw = 0
         for c in range(C):
-            rows = _chunk_rows(buf[c * 4096:(c + 1) * 4096], wf)
-            chunk = 0
-            for v in rows:
-                chunk = _apply(tab, 4, chunk) ^ v
-            raw = _apply(tab, 12, raw) ^ chunk
+            chunk = buf[c * 4096:(c + 1) * 4096]
+            res = _fold(_chunk_masks(chunk, wa), wf)
+            assert res == (~zlib.crc32(chunk.tobytes(), 0xFFFFFFFF)) & 0xFFFFFFFF  # zero-init register
+            raw = _apply(tab, 12, raw) ^ res
         pad = C * 4096 - n
         for b in range(12):
             if (pad >> b) & 1:

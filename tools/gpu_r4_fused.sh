@@ -9,7 +9,7 @@ set -eo pipefail
 R=$GRAFT_REPO_ROOT
 cd $R
 export PYTHONPATH=$R
-O=gpurun_out/r4_fused
+O=gpurun_out/${FUSED_OUT:-r4_fused}
 mkdir -p $O
 reh() {  # $1 = HLSP2P_DEFER_VERIFY, $2 = port, rest: bench args
   HLSP2P_DEFER_VERIFY=$1 timeout -k 10 300 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 \

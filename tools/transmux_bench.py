@@ -32,8 +32,6 @@ def main():
                     help="distinct segments (the batch cycles through them): 64 x 3 MB fits the 256 MB "
                          "Infinity Cache (MALL), 256 does not -- as in the pipeline, where every segment is new")
     ap.add_argument("--verify", action="store_true")
-    ap.add_argument("--crc-modes", default="", help="with --verify: also time these kernel forms of the fused CRC "
-                                                       "(aes_cbc.hip kCrc: 2 no weight loads, 3 no MFMA, 4 interleaved)")
     args = ap.parse_args()
     cuda = torch.device("cuda", 0)
     dev = device()
@@ -80,13 +78,6 @@ def main():
         out.update(fused_us=round(us_v, 1), fused_us_per_seg=round(us_v / args.segs, 3), fused_all_ok=ok,
                    crc_kernel_us_per_seg=round(us_c / args.segs, 3),
                    separate_us_per_seg=round((us + us_c) / args.segs, 3))
-        base = dev.aes_crc_mode()
-        for m in [int(x) for x in args.crc_modes.split(",") if x]:
-            dev.set_aes_crc_mode(m)
-            us_m, keep = timed(lambda: launch(expect, cw, ctab))
-            out[f"mode{m}_us_per_seg"] = round(us_m / args.segs, 3)
-            out[f"mode{m}_ok"] = all(bool(k[3][1].numpy().all()) for k in keep)
-        dev.set_aes_crc_mode(base)
     print(json.dumps(out))
 
 
