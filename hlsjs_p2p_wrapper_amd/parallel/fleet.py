@@ -41,6 +41,7 @@ into a shared-memory ring the player maps.
 """
 from __future__ import annotations
 
+import collections
 import logging
 import os
 import time
@@ -78,7 +79,10 @@ class RemoteSegment:
         return self.nbytes
 
     def data(self) -> Optional[np.ndarray]:
-        """The fragment's bytes as a ``uint8`` array (``gpuSwarm.fleetPayload``), else None."""
+        """The fragment's bytes as a read-only ``uint8`` array (``gpuSwarm.fleetPayload``),
+        else None.  Zero-copy: a view into the rank's shared payload ring, valid while the
+        player handles this answer batch (the ``onSuccess`` callbacks); the ring region is
+        reused once the player acknowledges the batch, so ``.copy()`` what must outlive it."""
         return self._bytes
 
 
@@ -387,7 +391,10 @@ class RemoteNode:
             r = RemoteResult(status=int(info[0]) if info else -1, info=InfoRow(info), plain_bytes=plain)
             if plain < 0:
                 r["error"] = ValueError("decryption failed (bad PKCS#7 padding)")
-            data = buf[poff[i]:poff[i] + nbytes].copy() if buf is not None else None
+            data = None
+            if buf is not None:  # zero-copy: valid while this batch is handled (see RemoteSegment.data)
+                data = buf[poff[i]:poff[i] + nbytes]
+                data.flags.writeable = False
             on_success(RemoteSegment(nbytes, r, data))
             n += 1
         return n
@@ -460,30 +467,60 @@ class _Queue:
 
 
 class _PayloadRing:
-    """Rank side of the payload ring: a shared-memory segment the fragments' bytes are copied
-    into (device -> pinned host -> shared memory) for players that asked for them."""
+    """Rank side of the payload ring: a shared-memory segment the fragments' bytes go to for
+    players that asked for them.  On a GPU node the segment is registered with HIP (pinned),
+    so one asynchronous D2H per transmux batch lands the bytes where the players read them --
+    no host copy.  Regions are handed out in FIFO order; a region is reused only after every
+    player it was sent to has acknowledged that answer batch (players read their fragments as
+    zero-copy views while they handle the batch)."""
 
-    def __init__(self, nbytes: int) -> None:
+    def __init__(self, nbytes: int, pin: bool = False) -> None:
         from multiprocessing import shared_memory
 
         self.shm = shared_memory.SharedMemory(create=True, size=nbytes)
         self.buf = np.ndarray((nbytes,), dtype=np.uint8, buffer=self.shm.buf)
         self.head = 0
+        self.wraps = 0
+        self.live: "collections.deque" = collections.deque()  # [start, end, {player: batch no} | None]
+        self.tensor = None
+        self.pinned = False
+        if pin:
+            import torch
 
-    def place(self, lens: np.ndarray) -> np.ndarray:
-        """Offsets for a batch of ``lens`` bytes (wrapping; the oldest bytes are overwritten:
-        a player copies its fragments out when it handles the batch)."""
-        al = (lens + 63) // 64 * 64
-        total = int(al.sum())
-        if total > len(self.buf):
-            raise RuntimeError(f"payload ring of {len(self.buf)} bytes cannot hold a {total}-byte batch")
-        if self.head + total > len(self.buf):
-            self.head = 0
-        offs = self.head + np.concatenate([[0], np.cumsum(al)[:-1]]).astype(np.int64)
-        self.head += total
-        return offs
+            self.buf[::4096] = 0  # fault the pages in before pinning
+            err = torch._C._cudart.cudaHostRegister(self.buf.ctypes.data, nbytes, 0)
+            if int(err) != 0:
+                raise RuntimeError(f"hipHostRegister of the {nbytes}-byte payload ring failed: {err}")
+            self.pinned = True
+            self.tensor = torch.from_numpy(self.buf)
+
+    def place(self, total: int, released) -> int:
+        """Start of a ``total``-byte region (wrapping).  ``released(need)`` tells whether the
+        oldest live region may be reused; it is called (and may wait) until one frees."""
+        cap = len(self.buf)
+        if total > cap:
+            raise RuntimeError(f"payload ring of {cap} bytes cannot hold a {total}-byte batch "
+                               "(HLSP2P_FLEET_PAYLOAD_BYTES)")
+        start = self.head
+        if start + total > cap:
+            start = 0
+            self.wraps += 1
+        while any(s < start + total and start < e for s, e, _ in self.live):
+            released(self.live[0][2])  # the oldest first: waits for the players' acknowledgements
+            self.live.popleft()
+        region = [start, start + total, None]
+        self.live.append(region)
+        self.head = start + total
+        return start, region
 
     def close(self) -> None:
+        if self.pinned:
+            import torch
+
+            torch.cuda.synchronize()
+            torch._C._cudart.cudaHostUnregister(self.buf.ctypes.data)
+            self.pinned = False
+        self.tensor = None
         self.buf = None
         try:
             self.shm.close()
@@ -512,6 +549,7 @@ class FleetServer:
         self._down = [True] * W
         self._payload = [False] * W
         self._ring: Optional[_PayloadRing] = None
+        self._pstream = None  # side stream of the payload gathers + D2H
         self._delivered: List[tuple] = []  # delivery columns from the node, not transmuxed yet
         self._chunks: List[List[tuple]] = [[] for _ in range(W)]  # answer columns per player
         self._errors: List[List[Tuple[int, int]]] = [[] for _ in range(W)]
@@ -653,7 +691,8 @@ class FleetServer:
         else:
             drk, keys = np.zeros((len(tok), 44), dtype=np.uint32), None
         verify = expect >= 0
-        tag = (tok, src, nbytes, cdn_ms, p2p_ms, offs, eids, expect if verify.any() else None)
+        pay = self._payload_stage(w, offs, nbytes) if any(self._payload) else None
+        tag = (tok, src, nbytes, cdn_ms, p2p_ms, offs, eids, expect if verify.any() else None, pay)
         return self.pipe.launch_columns(self.node.arena, offs, nbytes, enc, drk, iv, tag, keys=keys,
                                         expect=expect if verify.any() else None)
 
@@ -662,7 +701,12 @@ class FleetServer:
         if batch is None:
             return
         tag, rows, plain, has, verified = self.pipe.complete_columns(batch)
-        tok, src, nbytes, cdn_ms, p2p_ms, offs, eids, expect = tag
+        tok, src, nbytes, cdn_ms, p2p_ms, offs, eids, expect, pay = tag
+        ring_off = None
+        if pay is not None:
+            ring_off, region, ev = pay
+            if ev is not None:
+                ev.synchronize()  # the batch's D2H into the ring (queued at launch, long done)
         if expect is not None:  # deferred receive checks: the node commits or re-fetches
             chk = expect >= 0
             self.verify_failures += self.node.verify_done(eids[chk], verified[chk], tok[chk])
@@ -671,41 +715,79 @@ class FleetServer:
                 tok, src, nbytes, cdn_ms, p2p_ms, offs = (tok[keep], src[keep], nbytes[keep], cdn_ms[keep],
                                                           p2p_ms[keep], offs[keep])
                 rows, plain, has = rows[keep], plain[keep], has[keep]
+                if ring_off is not None:
+                    ring_off = ring_off[keep]
         w = tok >> TOKEN_SHIFT
         rid = tok & _RID_MASK
+        need = {}
         for p in np.unique(w).tolist():
             sel = np.flatnonzero(w == p)
             chunk = (rid[sel], src[sel].astype(np.int8), nbytes[sel], cdn_ms[sel], p2p_ms[sel], plain[sel],
                      has[sel], rows[sel])
-            if self._payload[p]:
-                chunk = chunk + (self._payload_copy(offs[sel], nbytes[sel]),)
+            if ring_off is not None and self._payload[p]:
+                chunk = chunk + ((self._ring.shm.name, ring_off[sel], nbytes[sel]),)
+                need[p] = self.batches_sent[p] + 1  # the answer batch the next send() carries
             self._chunks[p].append(chunk)
+        if pay is not None:
+            region[2] = need
 
-    def _payload_copy(self, offs: np.ndarray, lens: np.ndarray) -> tuple:
-        """Copy fragments' bytes from the HBM arena into the shared payload ring (one gather on
-        the device, one D2H, one host copy); returns ``(ring name, offsets, lengths)``."""
-        import torch
-
-        from ..ops import segment as _seg
-
-        if self._ring is None:
-            self._ring = _PayloadRing(int(os.environ.get("HLSP2P_FLEET_PAYLOAD_BYTES", str(1 << 30))))
-        ring_off = self._ring.place(lens)
+    def _payload_stage(self, w: np.ndarray, offs: np.ndarray, lens: np.ndarray):
+        """Queue the copy of the payload players' fragments from the HBM arena into the shared
+        ring: one gather kernel into a packed staging block and one asynchronous D2H into the
+        pinned ring, on a side stream (they overlap the transmux).  Returns ``(ring offset per
+        fragment or -1, ring region, done event)``."""
+        want = np.fromiter((self._payload[p] for p in w.tolist()), dtype=bool, count=len(w))
+        if not want.any():
+            return None
         arena = self.node.arena
-        al = (lens + 63) // 64 * 64
+        if self._ring is None:
+            self._ring = _PayloadRing(int(os.environ.get("HLSP2P_FLEET_PAYLOAD_BYTES", str(4 << 30))),
+                                      pin=arena.is_cuda)
+        idx = np.flatnonzero(want)
+        n = lens[idx]
+        al = (n + 63) // 64 * 64
         pack = np.concatenate([[0], np.cumsum(al)[:-1]]).astype(np.int64)
         total = int(al.sum())
+        start, region = self._ring.place(total, self._ring_released)
+        ring_off = np.full(len(w), -1, dtype=np.int64)
+        ring_off[idx] = start + pack
+        ev = None
         if arena.is_cuda:
-            staged = torch.empty(max(total, 1), dtype=torch.uint8, device=arena.device)
-            _seg.copy_segments(arena, staged, offs, pack, lens)
-            host = staged.cpu().numpy()
+            import torch
+
+            from ..ops import segment as _seg
+
+            if self._pstream is None:
+                self._pstream = torch.cuda.Stream(device=arena.device)
+            ps = self._pstream
+            ps.wait_stream(torch.cuda.current_stream(arena.device))
+            with torch.cuda.stream(ps):  # staging allocated, used and freed in ps's stream order
+                staged = torch.empty(max(total, 1), dtype=torch.uint8, device=arena.device)
+                _seg.copy_segments(arena, staged, offs[idx], pack, n)
+                self._ring.tensor[start:start + total].copy_(staged[:total], non_blocking=True)
+                ev = torch.cuda.Event()
+                ev.record(ps)
         else:
-            host = arena.numpy()
-            pack = offs
-        buf = self._ring.buf
-        for o, p, n in zip(ring_off.tolist(), pack.tolist(), lens.tolist()):
-            buf[o:o + n] = host[p:p + n]
-        return (self._ring.shm.name, ring_off, lens)
+            host, buf = arena.numpy(), self._ring.buf
+            for o, p, k in zip(offs[idx].tolist(), (start + pack).tolist(), n.tolist()):
+                buf[p:p + k] = host[o:o + k]
+        return ring_off, region, ev
+
+    def _ring_released(self, need) -> None:
+        """Wait until every player a ring region was sent to has acknowledged that batch."""
+        if need is None:
+            raise RuntimeError("payload ring too small for the transmux batches in flight "
+                               "(raise HLSP2P_FLEET_PAYLOAD_BYTES)")
+        from multiprocessing.connection import wait
+
+        end = time.monotonic() + 60.0
+        while not all(not self.open[p] or self.batches_done[p] >= k for p, k in need.items()):
+            if time.monotonic() > end:
+                raise RuntimeError("fleet players did not acknowledge their payload batches in 60 s")
+            conns = [c for p, c in enumerate(self.conns) if self.open[p]]
+            if conns:
+                wait(conns, timeout=0.005)
+            self.poll()
 
     def send(self) -> int:
         """One answer batch per player (plus the swarm state the agents' stats read)."""

@@ -139,6 +139,111 @@ def test_remote_node_delivers_result_rows_and_errors():
     assert b.recv() == ("ack", 1)
 
 
+def test_payload_ring_reuses_regions_only_after_acknowledgement(monkeypatch):
+    """The rank's payload ring hands out FIFO regions; one is reused only once the players it
+    was sent to acknowledged that batch (they read zero-copy views while handling it)."""
+    from hlsjs_p2p_wrapper_amd.parallel.fleet import _PayloadRing
+
+    ring = _PayloadRing(1000)
+    waited = []
+    try:
+        s0, r0 = ring.place(400, lambda need: waited.append(need))
+        r0[2] = {0: 1}
+        s1, r1 = ring.place(400, lambda need: waited.append(need))
+        r1[2] = {0: 2}
+        assert (s0, s1) == (0, 400) and not waited
+        s2, _ = ring.place(400, lambda need: waited.append(need))  # wraps: must free region 0 first
+        assert s2 == 0 and waited == [{0: 1}]
+        with pytest.raises(RuntimeError):
+            ring.place(2000, lambda need: None)
+        ring.live[0][2] = None  # a region queued but not sent yet cannot be freed
+
+        def refuse(need):
+            if need is None:
+                raise RuntimeError("ring too small")
+
+        with pytest.raises(RuntimeError):
+            ring.place(900, refuse)
+    finally:
+        ring.close()
+
+
+def test_fleet_payload_bytes_through_a_wrapping_ring(monkeypatch):
+    """``gpuSwarm.fleetPayload`` on the CPU node: a player thread reads every fragment's bytes
+    in ``onSuccess`` (zero-copy views into the rank's shared ring) while the ring, sized for a
+    few answer batches, wraps; each view matches the origin's bytes."""
+    import zlib
+
+    monkeypatch.setenv("HLSP2P_FLEET_PAYLOAD_BYTES", str(5 << 20))
+    clear_origins()
+    set_current_node(None)
+    loop = new_event_loop("real")
+    spec = dict(ORIGIN, encrypted=False, base_url="http://fleet.ring/live/", pool_size=8)
+    origin = SyntheticHlsOrigin(**spec, pin_memory=False)
+    node = node_for_config({"gpuSwarm": {"backend": "local", "device": "cpu", "cacheBytes": 64 << 20,
+                                         "autoTick": False}})
+    a, b = mp.Pipe()
+    sns = list(range(0, 40))
+    got, errs = {}, []
+
+    def player():
+        rn = RemoteNode(b, payload=True)
+
+        class Cb:
+            def __init__(self, sn):
+                self.sn = sn
+
+            def onProgress(self, ev):  # noqa: N802
+                pass
+
+            def onSuccess(self, seg):  # noqa: N802
+                got[self.sn] = zlib.crc32(seg.data().tobytes())  # inside the callback: the view is valid
+
+            def onError(self, err):  # noqa: N802
+                errs.append((self.sn, err.status))
+
+        for sn in sns:
+            rn.request((9, 0, 0, sn), spec["base_url"] + origin.segment_path(0, sn), None, Cb(sn))
+        rn.flush()
+        end = time.monotonic() + 60
+        while len(got) + len(errs) < len(sns) and time.monotonic() < end:
+            rn.poll(0.002)
+            rn.flush()
+        rn.close()
+
+    pipe = pipeline_for(torch.device("cpu"), loop)
+    pipe.auto_flush = False
+    server = FleetServer(node, pipe, [a])
+    t = threading.Thread(target=player, daemon=True)
+    t.start()
+    try:
+        hs, tb = collections.deque(), None
+        end = time.monotonic() + 60
+        while t.is_alive():
+            assert time.monotonic() < end, f"fleet did not deliver: {len(got)} / {len(sns)}"
+            while loop._ready:
+                loop.run_once(block=False)
+            server.poll()
+            server.admit(6)
+            hs.append(node.launch_round())
+            if len(hs) > 1:
+                node.complete_round(hs.popleft())
+            nb = server.launch_transmux()
+            server.complete_transmux(tb)
+            tb = nb
+            server.send()
+        t.join(5)
+        assert not errs and sorted(got) == sns
+        for sn in sns:
+            assert got[sn] == origin.resource(origin.segment_path(0, sn))[3]
+        assert server._ring is not None and server._ring.wraps >= 1
+    finally:
+        server.close()
+        node.close()
+        set_current_node(None)
+        clear_origins()
+
+
 @pytest.mark.gpu
 def test_bench_fleet_on_the_gpu():
     """``bench.py`` in its default fleet shape on one MI355X, tiny segments: the players are
@@ -190,7 +295,7 @@ def test_fleet_player_reads_fragment_bytes_on_the_gpu(cuda):
                 pass
 
             def onSuccess(self, seg):  # noqa: N802
-                got[self.sn] = seg
+                got[self.sn] = (seg, seg.data().copy())  # the view is valid during the callback
 
             def onError(self, err):  # noqa: N802
                 errs.append((self.sn, err.status))
@@ -217,9 +322,8 @@ def test_fleet_player_reads_fragment_bytes_on_the_gpu(cuda):
             player.poll(0.002)
         assert not errs
         for sn in sns:
-            seg = got[sn]
-            assert isinstance(seg, RemoteSegment)
-            data = seg.data()
+            seg, data = got[sn]
+            assert isinstance(seg, RemoteSegment) and not seg.data().flags.writeable
             assert data is not None and data.dtype == np.uint8 and len(data) == seg.numel()
             pool_data, off, n, crc = origin.resource(origin.segment_path(0, sn))
             assert n == seg.numel()
