@@ -623,6 +623,7 @@ def _fleet(args, world, rank, device, use_gpu, node, origin, players, desc, encr
         pipe.timer.reset()
         fleet_timer.reset()
         s0 = dict(node.stats)
+        pay0 = (server.payload_bytes, server.payload_wait_s)
         node.corrupt_next_recv = args.corrupt_recv
         calib0 = cpu_calibration_us() if args.verbose else 0.0
         mark("t0")
@@ -642,6 +643,8 @@ def _fleet(args, world, rank, device, use_gpu, node, origin, players, desc, encr
         fleet_ms = fleet_timer.summary_ms(args.steps)
         node_ms, tm_ms = node.timer.summary_ms(args.steps), pipe.timer.summary_ms(args.steps)
         win_fleet = dict(fleet_timer.total)
+        win_fleet["payload_bytes"] = server.payload_bytes - pay0[0]
+        win_fleet["payload_wait"] = server.payload_wait_s - pay0[1]
         s1_timers = (dict(node.timer.total), dict(pipe.timer.total))
         if _PROF is not None:
             _PROF.disable()
@@ -763,7 +766,7 @@ PER_RANK_FIELDS = ("rank", "rounds", "step_ms", "wait_device_us", "exchange_us",
                    "host_round_us",
                    "cdn_GBps", "cdn_dev_ms", "p2p_recv_MB", "p2p_sent_MB", "p2p_dev_ms", "p2p_GBps",
                    "p2p_links", "p2p_link_GBps", "transmux_dev_ms", "transmux_wait_us", "await_players_us",
-                   "crc_failures", "control_fallbacks", "deferred", "inflight", "cu_reserve")
+                   "payload_GBps", "payload_wait_us", "crc_failures", "control_fallbacks", "deferred", "inflight", "cu_reserve")
 
 
 def _per_rank(node, pipe, s0, s1, elapsed, steps, inflight, fleet_total=None, timers=None) -> np.ndarray:
@@ -776,7 +779,9 @@ def _per_rank(node, pipe, s0, s1, elapsed, steps, inflight, fleet_total=None, ti
     the node-stream exchange device ms per round (a peer's stall included), the received
     GB/s over that time, the source links per round and the GB/s per link (bytes per link
     over the exchange time: a lower bound on each xGMI link's rate); transmux device ms per
-    step (default stream) and the host wait for it; fleet: per-step wait on the players."""
+    step (default stream) and the host wait for it; fleet: per-step wait on the players, and
+    with ``fleetPayload`` the D2H rate of the fragments' bytes into the players' ring and the
+    per-step host wait on it."""
     rounds = max(1, s1["rounds"] - s0["rounds"])
     tm, pt = timers if timers is not None else (node.timer.total, pipe.timer.total)
     recv = s1["p2p"] - s0["p2p"]
@@ -807,6 +812,8 @@ def _per_rank(node, pipe, s0, s1, elapsed, steps, inflight, fleet_total=None, ti
         "transmux_dev_ms": pt.get("dev_transmux", 0.0) * 1e3 / max(1, steps),
         "transmux_wait_us": pt.get("wait_device", 0.0) * 1e6 / max(1, steps),
         "await_players_us": (fleet_total or {}).get("await_players", 0.0) * 1e6 / max(1, steps),
+        "payload_GBps": (fleet_total or {}).get("payload_bytes", 0) / max(elapsed, 1e-9) / 1e9,
+        "payload_wait_us": (fleet_total or {}).get("payload_wait", 0.0) * 1e6 / max(1, steps),
         "crc_failures": s1["crc_failures"] - s0["crc_failures"],
         "control_fallbacks": getattr(node.comm, "control_fallbacks", 0),
         "deferred": s1.get("deferred", 0) - s0.get("deferred", 0),
@@ -819,10 +826,11 @@ def _per_rank_dicts(parts, steps) -> list:
     """Decode the gathered rows; add each rank's ``bound`` label.
 
     Rule: the busiest device stream -- ``pcie`` (H2D copy stream), ``xgmi`` (the node
-    stream's exchange), ``transmux`` (decrypt + demux) -- when it is busy for >= 80 % of a
-    step (the pipeline keeps it saturated), or when the host waited on the device for more
-    than 30 % of a step (``wait_device`` and ``exchange`` per round x rounds per step + the
-    transmux wait); otherwise ``players`` when the fleet's wait on its players exceeds half a
+    stream's exchange), ``transmux`` (decrypt + demux), ``pcie_d2h`` (the fleet payload copy;
+    its host wait stands for its busy time) -- when it is busy for >= 80 % of a step (the
+    pipeline keeps it saturated), or when the host waited on the device for more than 30 % of
+    a step (``wait_device`` and ``exchange`` per round x rounds per step + the transmux and
+    payload waits); otherwise ``players`` when the fleet's wait on its players exceeds half a
     step, else ``host``."""
     out = []
     for p in parts:
@@ -834,8 +842,9 @@ def _per_rank_dicts(parts, steps) -> list:
                 d[k] = round(v, 3)
         step = max(d["step_ms"], 1e-9)
         rps = d["rounds"] / max(1, steps)
-        waited = ((d["wait_device_us"] + d["exchange_us"]) * rps + d["transmux_wait_us"]) / 1e3
-        busy = {"pcie": d["cdn_dev_ms"] * rps, "xgmi": d["p2p_dev_ms"] * rps, "transmux": d["transmux_dev_ms"]}
+        waited = ((d["wait_device_us"] + d["exchange_us"]) * rps + d["transmux_wait_us"] + d["payload_wait_us"]) / 1e3
+        busy = {"pcie": d["cdn_dev_ms"] * rps, "xgmi": d["p2p_dev_ms"] * rps, "transmux": d["transmux_dev_ms"],
+                "pcie_d2h": d["payload_wait_us"] / 1e3}
         top = max(busy, key=busy.get)
         if busy[top] >= 0.8 * step or waited > 0.3 * step:
             d["bound"] = top

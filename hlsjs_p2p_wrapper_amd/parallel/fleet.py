@@ -550,6 +550,8 @@ class FleetServer:
         self._payload = [False] * W
         self._ring: Optional[_PayloadRing] = None
         self._pstream = None  # side stream of the payload gathers + D2H
+        self.payload_bytes = 0  # copied into the payload ring
+        self.payload_wait_s = 0.0  # host time blocked on a batch's payload D2H
         self._delivered: List[tuple] = []  # delivery columns from the node, not transmuxed yet
         self._chunks: List[List[tuple]] = [[] for _ in range(W)]  # answer columns per player
         self._errors: List[List[Tuple[int, int]]] = [[] for _ in range(W)]
@@ -706,7 +708,9 @@ class FleetServer:
         if pay is not None:
             ring_off, region, ev = pay
             if ev is not None:
-                ev.synchronize()  # the batch's D2H into the ring (queued at launch, long done)
+                t0 = time.perf_counter()
+                ev.synchronize()  # the batch's D2H into the ring (queued at launch)
+                self.payload_wait_s += time.perf_counter() - t0
         if expect is not None:  # deferred receive checks: the node commits or re-fetches
             chk = expect >= 0
             self.verify_failures += self.node.verify_done(eids[chk], verified[chk], tok[chk])
@@ -749,6 +753,7 @@ class FleetServer:
         pack = np.concatenate([[0], np.cumsum(al)[:-1]]).astype(np.int64)
         total = int(al.sum())
         start, region = self._ring.place(total, self._ring_released)
+        self.payload_bytes += total
         ring_off = np.full(len(w), -1, dtype=np.int64)
         ring_off[idx] = start + pack
         ev = None

@@ -133,7 +133,8 @@ def test_bench_eight_ranks_driver_shape():
 PER_RANK_KEYS = {"rank", "rounds", "step_ms", "wait_device_us", "exchange_us", "control_us", "plan_us",
                  "host_round_us", "cdn_GBps", "cdn_dev_ms", "p2p_recv_MB", "p2p_sent_MB", "p2p_dev_ms", "p2p_GBps",
                  "p2p_links", "p2p_link_GBps",
-                 "transmux_dev_ms", "transmux_wait_us", "await_players_us", "crc_failures", "control_fallbacks",
+                 "transmux_dev_ms", "transmux_wait_us", "await_players_us", "payload_GBps", "payload_wait_us",
+                 "crc_failures", "control_fallbacks",
                  "deferred", "inflight", "cu_reserve", "bound"}
 
 
@@ -145,7 +146,7 @@ def _check_per_rank(res, world):
     for r in rows:
         assert set(r) == PER_RANK_KEYS
         assert r["rounds"] >= res["steps"] and r["crc_failures"] == 0 and r["control_fallbacks"] == 0
-        assert r["bound"] in ("pcie", "xgmi", "transmux", "players", "host")
+        assert r["bound"] in ("pcie", "xgmi", "transmux", "pcie_d2h", "players", "host")
         assert 0 <= r["p2p_links"] <= world - 1
     # (which rank receives depends on the players' relative pace: the swarm as a whole does)
     assert sum(r["p2p_recv_MB"] for r in rows) > 0 and sum(r["p2p_sent_MB"] for r in rows) > 0
@@ -223,6 +224,16 @@ def test_bench_fleet_two_ranks_two_players():
     # window the rank ahead fetches segments its peer only receives after it (GPU rehearsals,
     # profiles/r2_fleet_validation: exactly 0.50 / 0.75 at 2 / 4 ranks)
     assert 0.3 < res["offload_ratio"] <= 0.52
+
+
+def test_bench_fleet_payloads_two_ranks():
+    """``--fleet-payload`` (``gpuSwarm.fleetPayload``: bytes in every player's ``onSuccess``)
+    through the driver's launch path: the fragments' bytes go through each rank's shared
+    payload ring, the players finish without errors, and the record shows the payload rate."""
+    res = _bench_cpu(_free_port(), "--players", "2", "--fleet-payload", config="hostcost-micro")
+    assert res["errors"] == 0 and res["value"] > 0
+    _check_per_rank(res, 2)
+    assert all(r["payload_GBps"] > 0 for r in res["per_rank"])
 
 
 def test_ipc_outbox_slots_follow_the_packing_order():
