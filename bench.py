@@ -766,7 +766,8 @@ PER_RANK_FIELDS = ("rank", "rounds", "step_ms", "wait_device_us", "exchange_us",
                    "host_round_us",
                    "cdn_GBps", "cdn_dev_ms", "p2p_recv_MB", "p2p_sent_MB", "p2p_dev_ms", "p2p_GBps",
                    "p2p_links", "p2p_link_GBps", "transmux_dev_ms", "transmux_wait_us", "await_players_us",
-                   "payload_GBps", "payload_wait_us", "crc_failures", "control_fallbacks", "deferred", "inflight", "cu_reserve")
+                   "payload_GBps", "payload_wait_us", "crc_failures", "control_fallbacks", "deferred", "inflight",
+                   "cu_reserve")
 
 
 def _per_rank(node, pipe, s0, s1, elapsed, steps, inflight, fleet_total=None, timers=None) -> np.ndarray:
