@@ -9,8 +9,6 @@
 // packs, argument checks, six pybind launches, two pinned allocations) cost ~0.2 ms of host
 // time per 64-segment batch -- the host path bounds the per-GPU segment rate once peers
 // share the CDN work (N > 1); here it is tens of microseconds.
-#include <c10/hip/HIPCachingAllocator.h>
-#include <c10/hip/HIPGuard.h>
 #include <c10/hip/HIPStream.h>
 #include <hip/hip_runtime_api.h>
 #include <torch/extension.h>
@@ -20,7 +18,6 @@
 #include <algorithm>
 #include <cstdlib>
 #include <cstring>
-#include <optional>
 #include <vector>
 
 namespace hlsp2p {
@@ -124,33 +121,14 @@ int g_cu_reserve = 0;
 // memory-bound kernels of the other streams (ingest copies, CRC, the previous batch's demux):
 // one 160 KiB decrypt workgroup fills a CU's LDS, so nothing that needs LDS co-resides with it
 int g_decrypt_cap = -1;
-// split batches (a demux stream given): the decrypt grid leaves this many CUs to the demux of
-// the previous batch, which then runs beside it instead of after it (set_split_reserve)
-int g_split_reserve = 64;
-int decrypt_cus(int device, bool split) {
+int decrypt_cus(int device) {
   if (g_decrypt_cap < 0) {
     const char* v = std::getenv("HLSP2P_DECRYPT_CUS");
     g_decrypt_cap = v != nullptr ? std::max(0, std::atoi(v)) : 0;
   }
-  int n = cus(device) - (split ? std::max(g_cu_reserve, g_split_reserve) : g_cu_reserve);
+  int n = cus(device) - g_cu_reserve;
   if (g_decrypt_cap > 0) n = std::min(n, g_decrypt_cap);
   return std::max(8, n);
-}
-
-// Decrypt -> demux handoff events (split batches): a wait captures the event's state when it
-// is enqueued, so a small ring per device is reused safely
-hipEvent_t handoff_event(int device) {
-  constexpr int kRing = 16;
-  static std::vector<hipEvent_t> ring[64];
-  static int next[64] = {0};
-  std::vector<hipEvent_t>& r = ring[device & 63];
-  if (r.empty()) {
-    r.resize(kRing);
-    for (auto& e : r) TORCH_CHECK(hipEventCreateWithFlags(&e, hipEventDisableTiming) == hipSuccess, "hipEventCreate");
-  }
-  hipEvent_t e = r[next[device & 63]];
-  next[device & 63] = (next[device & 63] + 1) % kRing;
-  return e;
 }
 
 void hip_ok(hipError_t e, const char* what) { TORCH_CHECK(e == hipSuccess, what, " failed: ", hipGetErrorString(e)); }
@@ -162,15 +140,11 @@ void hip_ok(hipError_t e, const char* what) { TORCH_CHECK(e == hipSuccess, what,
 // (indices into the batch, info [B,24] device, pes device, es buffer, es offsets,
 // info rows in pinned host memory, plaintext lengths in pinned host memory (enc) or a
 // host array (clear)); plus the decrypt buffer to keep alive until the batch completes.
-// demux_stream != 0 (a hipStream_t): SPLIT batch -- the decrypt runs on the current stream
-// with `g_split_reserve` CUs left free, everything after it (fused-verify fold, demux, D2H)
-// on demux_stream behind a handoff event, so this batch's demux overlaps the NEXT batch's
-// decrypt; the caller records its completion event on demux_stream.
 py::tuple transmux_launch(Tensor src, I64 src_off, I64 nbytes, py::array_t<uint8_t, py::array::c_style> enc,
                           py::array_t<uint32_t, py::array::c_style | py::array::forcecast> drk,
                           py::array_t<uint8_t, py::array::c_style | py::array::forcecast> iv, Tensor td0, Tensor isb,
                           int64_t max_pes, py::object expect_obj, c10::optional<Tensor> crc_w,
-                          c10::optional<Tensor> crc_tables, int64_t demux_stream) {
+                          c10::optional<Tensor> crc_tables) {
   TORCH_CHECK_VALUE(src.is_cuda() && src.is_contiguous() && src.scalar_type() == torch::kUInt8, "src: contiguous GPU uint8");
   TORCH_CHECK_VALUE((reinterpret_cast<uintptr_t>(src.data_ptr()) & 15) == 0, "src must be 16-byte aligned");
   const int64_t B = src_off.size();
@@ -294,7 +268,12 @@ py::tuple transmux_launch(Tensor src, I64 src_off, I64 nbytes, py::array_t<uint8
   Tensor dec, out_len;
   if (ne) out_len = torch::empty({ne}, dev_opts.dtype(torch::kInt64));
   Tensor masks, chunk_res, v_crc, v_ok, v_ok_host;
-  if (nv) masks = torch::empty({64 * v_chunks}, dev_opts.dtype(torch::kInt32));
+  if (nv) {
+    masks = torch::empty({64 * v_chunks}, dev_opts.dtype(torch::kInt32));
+    chunk_res = torch::empty({std::max<int64_t>(1, v_chunks)}, dev_opts.dtype(torch::kInt32));
+    v_crc = torch::empty({nv}, dev_opts.dtype(torch::kInt32));
+    v_ok = torch::empty({nv}, dev_opts.dtype(torch::kUInt8));
+  }
   if (ne) {
     dec = torch::empty({dec_pos + kAlign}, dev_opts.dtype(torch::kUInt8));
     hip_ok(hlsp2p::dev::launch_aes128_cbc_decrypt(
@@ -302,30 +281,9 @@ py::tuple transmux_launch(Tensor src, I64 src_off, I64 nbytes, py::array_t<uint8
                desc.at<int64_t>(d_so), desc.at<int64_t>(d_do), desc.at<int64_t>(d_bp), desc.at<int64_t>(d_cp),
                desc.at<uint32_t>(d_drk), desc.at<uint32_t>(d_iv), static_cast<const uint32_t*>(td0.data_ptr()),
                static_cast<const uint8_t*>(isb.data_ptr()), out_len.data_ptr<int64_t>(), static_cast<int>(ne),
-               a_cp.back(), decrypt_cus(device, demux_stream != 0), st, nv ? desc.at<int64_t>(d_mo) : nullptr,
+               a_cp.back(), decrypt_cus(device), st, nv ? desc.at<int64_t>(d_mo) : nullptr,
                nv ? crc_w->data_ptr() : nullptr, nv ? reinterpret_cast<uint32_t*>(masks.data_ptr<int32_t>()) : nullptr),
            "aes128_cbc_decrypt");
-  }
-  // split batch: the rest runs on the demux stream behind the decrypt; the st-allocated
-  // buffers it reads are recorded on it (never handed out again before it has used them)
-  std::optional<c10::hip::HIPStreamGuard> on_demux;
-  hipStream_t dst = st;
-  if (demux_stream != 0) {
-    c10::hip::HIPStream ds = c10::hip::getStreamFromExternal(reinterpret_cast<hipStream_t>(demux_stream),
-                                                            static_cast<c10::DeviceIndex>(device));
-    hipEvent_t ev = handoff_event(device);
-    hip_ok(hipEventRecord(ev, st), "hipEventRecord");
-    hip_ok(hipStreamWaitEvent(ds.stream(), ev, 0), "hipStreamWaitEvent");
-    for (const Tensor* t : {&dec, &out_len, &masks})
-      if (t->defined()) c10::hip::HIPCachingAllocator::recordStream(t->storage().data_ptr(), ds);
-    c10::hip::HIPCachingAllocator::recordStream(desc.device().storage().data_ptr(), ds);
-    on_demux.emplace(ds);  // current stream from here on: allocations and torch copies go to ds
-    dst = ds.stream();
-  }
-  if (nv) {
-    chunk_res = torch::empty({std::max<int64_t>(1, v_chunks)}, dev_opts.dtype(torch::kInt32));
-    v_crc = torch::empty({nv}, dev_opts.dtype(torch::kInt32));
-    v_ok = torch::empty({nv}, dev_opts.dtype(torch::kUInt8));
   }
   if (nv) {  // fold the decrypt's CRC masks per chunk, combine per segment, compare
     hip_ok(hlsp2p::dev::launch_crc32_from_masks(
@@ -334,7 +292,7 @@ py::tuple transmux_launch(Tensor src, I64 src_off, I64 nbytes, py::array_t<uint8
                desc.at<int64_t>(d_vl), static_cast<const uint32_t*>(crc_tables->data_ptr()),
                reinterpret_cast<uint32_t*>(chunk_res.data_ptr<int32_t>()),
                reinterpret_cast<uint32_t*>(v_crc.data_ptr<int32_t>()), desc.at<uint32_t>(d_vx),
-               v_ok.data_ptr<uint8_t>(), nullptr, nullptr, 0, static_cast<int>(nv), v_chunks, cus(device), dst),
+               v_ok.data_ptr<uint8_t>(), nullptr, nullptr, 0, static_cast<int>(nv), v_chunks, cus(device), st),
            "crc32_from_masks");
     v_ok_host = torch::empty({nv}, torch::TensorOptions().dtype(torch::kUInt8).pinned_memory(true));
     v_ok_host.copy_(v_ok, /*non_blocking=*/true);
@@ -361,7 +319,7 @@ py::tuple transmux_launch(Tensor src, I64 src_off, I64 nbytes, py::array_t<uint8
                                         reinterpret_cast<uint32_t*>(meta.data_ptr<int32_t>()),
                                         pts.data_ptr<int64_t>(), aux.data_ptr<int32_t>(), es.data_ptr<uint8_t>(),
                                         desc.at<int64_t>(p.d_eo), pes.data_ptr<int64_t>(), max_pes,
-                                        info.data_ptr<int64_t>(), dst),
+                                        info.data_ptr<int64_t>(), st),
            "ts_demux");
     keep.append(py::make_tuple(meta, pts, aux));
     // D2H through torch's copy so the caching host allocator records the use of the pinned
@@ -387,7 +345,6 @@ py::tuple transmux_launch(Tensor src, I64 src_off, I64 nbytes, py::array_t<uint8
   }
   keep.append(dec.defined() ? py::cast(dec) : py::none());
   keep.append(desc.device());
-  if (out_len.defined()) keep.append(out_len);
   py::object verify = py::none();
   if (nv) {
     keep.append(py::make_tuple(masks, chunk_res, v_crc, v_ok));
@@ -404,11 +361,7 @@ void register_transmux(py::module& m) {
   m.def("set_cu_reserve", [](int n) { g_cu_reserve = std::max(0, n); }, py::arg("n"),
         "CUs the persistent decrypt grid leaves free for concurrent (RCCL) kernels");
   m.def("cu_reserve", [] { return g_cu_reserve; });
-  m.def("set_split_reserve", [](int n) { g_split_reserve = std::max(0, n); }, py::arg("n"),
-        "CUs a split batch's decrypt leaves free for the previous batch's demux");
-  m.def("split_reserve", [] { return g_split_reserve; });
   m.def("transmux_launch", &transmux_launch, py::arg("src"), py::arg("src_off"), py::arg("nbytes"), py::arg("enc"),
         py::arg("drk"), py::arg("iv"), py::arg("td0"), py::arg("isb"), py::arg("max_pes"),
-        py::arg("expect") = py::none(), py::arg("crc_w") = py::none(), py::arg("crc_tables") = py::none(),
-        py::arg("demux_stream") = 0);
+        py::arg("expect") = py::none(), py::arg("crc_w") = py::none(), py::arg("crc_tables") = py::none());
 }

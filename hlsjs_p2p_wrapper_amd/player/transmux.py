@@ -13,7 +13,6 @@ get their own pipeline.
 """
 from __future__ import annotations
 
-import os
 import threading
 import time
 from dataclasses import dataclass
@@ -83,11 +82,6 @@ class MediaPipeline:
         # event-loop players flush at the end of the loop iteration; a throughput driver
         # sets auto_flush=False and overlaps launch() / complete() of consecutive batches
         self.auto_flush = True
-        # columnar (fleet) batches split over two streams: the decrypt on the current stream
-        # with CUs left free, everything after it on a demux stream, so batch k's demux runs
-        # beside batch k+1's decrypt (kernels/transmux.cpp; HLSP2P_TRANSMUX_SPLIT=0: one stream)
-        self.split = self.device.type == "cuda" and os.environ.get("HLSP2P_TRANSMUX_SPLIT", "1") != "0"
-        self._demux_stream = None
 
     def submit(self, job: TransmuxJob) -> None:
         self._jobs.append(job)
@@ -340,27 +334,17 @@ class MediaPipeline:
             from ..ops import crc as _crc
 
             cw, ctab = _crc.fused_consts(self.device)
-        ds = None
-        if self.split:
-            if self._demux_stream is None:
-                self._demux_stream = torch.cuda.Stream(device=self.device)
-            ds = self._demux_stream
         ev0 = self._event()
         groups, dec, host_block, fused = _native_device().transmux_launch(
             src, offs, nb, enc.astype(np.uint8), np.ascontiguousarray(drk, dtype=np.uint32),
-            np.ascontiguousarray(iv, dtype=np.uint8), td0, isb, _ts.DEFAULT_MAX_PES, ex, cw, ctab,
-            ds.cuda_stream if ds is not None else 0)
+            np.ascontiguousarray(iv, dtype=np.uint8), td0, isb, _ts.DEFAULT_MAX_PES, ex, cw, ctab)
         infos, host = [], []
         for gidx, info, pes, es, es_offs, hinfo, hlens in groups:
             infos.append((idx_ok[gidx], _ts.DemuxResult(info, pes, es, es_offs), es_offs, hlens))
             host.append((hinfo, hlens))
         if fused is not None:
             verify.append((idx_ok[fused[0]], fused[1]))
-        if ds is not None:
-            with torch.cuda.stream(ds):  # the batch completes on the demux stream
-                ev = self._event()
-        else:
-            ev = self._event()
+        ev = self._event()
         self.timer.add("launch_columns", time.perf_counter() - t1)
         return _Batch(None, infos=infos, host=host, event=ev, keep=(dec, host_block), tag=tag, n=n, start=ev0,
                       verify=verify or None)

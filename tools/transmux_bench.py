@@ -14,7 +14,6 @@ adds the separate CRC kernel the node would otherwise run for comparison.
 """
 import argparse
 import json
-import time
 import zlib
 
 import numpy as np
@@ -33,11 +32,6 @@ def main():
                     help="distinct segments (the batch cycles through them): 64 x 3 MB fits the 256 MB "
                          "Infinity Cache (MALL), 256 does not -- as in the pipeline, where every segment is new")
     ap.add_argument("--verify", action="store_true")
-    ap.add_argument("--split", default="", help="split batches (decrypt on the current stream, demux on a second "
-                                                 "one) with these CU reserves for the decrypt grid, e.g. 32,64,96")
-    ap.add_argument("--overlap", default="", help="streams:reserve pairs, e.g. 1:0,2:0,2:64 -- consecutive batches "
-                                                   "alternate over that many streams with the decrypt grid leaving "
-                                                   "`reserve` CUs free (does batch k's demux overlap batch k+1's decrypt?)")
     args = ap.parse_args()
     cuda = torch.device("cuda", 0)
     dev = device()
@@ -54,19 +48,20 @@ def main():
     td0, isb = aes.device_tables(cuda)
     total = int(lens.sum())
 
-    def launch(expect=None, cw=None, ctab=None, ds=0):
-        return dev.transmux_launch(src, offs, lens, enc, drk, iv, td0, isb, tsdemux.DEFAULT_MAX_PES, expect, cw, ctab,
-                                   ds)
+    def launch(expect=None, cw=None, ctab=None):
+        return dev.transmux_launch(src, offs, lens, enc, drk, iv, td0, isb, tsdemux.DEFAULT_MAX_PES, expect, cw, ctab)
 
     def timed(fn):
         keep = [fn() for _ in range(args.iters + 2)]  # warm the caching allocator: no hipMalloc in the timed loop
         torch.cuda.synchronize()
         keep = keep[:2]
-        t0 = time.perf_counter()
+        a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        a.record()
         for _ in range(args.iters):
             keep.append(fn())
-        torch.cuda.synchronize()  # wall clock: launches on several streams
-        return (time.perf_counter() - t0) * 1e6 / args.iters, keep
+        b.record()
+        torch.cuda.synchronize()
+        return a.elapsed_time(b) * 1e3 / args.iters, keep
 
     us, _ = timed(launch)
     out = {"segs": args.segs, "bytes": total, "us": round(us, 1), "us_per_seg": round(us / args.segs, 3),
@@ -83,32 +78,6 @@ def main():
         out.update(fused_us=round(us_v, 1), fused_us_per_seg=round(us_v / args.segs, 3), fused_all_ok=ok,
                    crc_kernel_us_per_seg=round(us_c / args.segs, 3),
                    separate_us_per_seg=round((us + us_c) / args.segs, 3))
-    if args.split:
-        ds = torch.cuda.Stream()
-        base = dev.split_reserve()
-        for r in [int(x) for x in args.split.split(",") if x]:
-            dev.set_split_reserve(r)
-            us_s, _ = timed(lambda: launch(ds=ds.cuda_stream))
-            out[f"split_r{r}_us_per_seg"] = round(us_s / args.segs, 3)
-            if args.verify:
-                us_sv, keep = timed(lambda: launch(expect, cw, ctab, ds=ds.cuda_stream))
-                out[f"split_r{r}_fused_us_per_seg"] = round(us_sv / args.segs, 3)
-                out[f"split_r{r}_fused_ok"] = all(bool(k[3][1].numpy().all()) for k in keep)
-        dev.set_split_reserve(base)
-    for pair in [x for x in args.overlap.split(",") if x]:
-        ns, res = (int(v) for v in pair.split(":"))
-        streams = [torch.cuda.Stream() for _ in range(ns)]
-        dev.set_cu_reserve(res)
-
-        def alt(it=[0]):
-            st = streams[it[0] % ns]
-            it[0] += 1
-            with torch.cuda.stream(st):
-                return launch()
-
-        us_o, _ = timed(lambda: alt())
-        out[f"s{ns}_r{res}_us_per_seg"] = round(us_o / args.segs, 3)
-        dev.set_cu_reserve(0)
     print(json.dumps(out))
 
 
