@@ -494,9 +494,10 @@ class _PayloadRing:
             self.pinned = True
             self.tensor = torch.from_numpy(self.buf)
 
-    def place(self, total: int, released) -> int:
-        """Start of a ``total``-byte region (wrapping).  ``released(need)`` tells whether the
-        oldest live region may be reused; it is called (and may wait) until one frees."""
+    def place(self, total: int, released) -> Tuple[int, list]:
+        """``(start, region)`` of a ``total``-byte region (wrapping); ``region[2]`` takes the
+        players' batch numbers once sent.  ``released(need)`` returns once the oldest live
+        region may be reused (it may wait); it is called until the new region is free."""
         cap = len(self.buf)
         if total > cap:
             raise RuntimeError(f"payload ring of {cap} bytes cannot hold a {total}-byte batch "
