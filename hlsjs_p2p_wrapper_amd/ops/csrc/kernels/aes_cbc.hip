@@ -99,19 +99,31 @@ __device__ __forceinline__ void crc_chunk_masks(const uint4 (&c)[kBlk], const v4
   out[lane] = m;  // bits 16 p + i
 }
 
+// Optional packet-header records for the demux scan (ts_demux.hip: ts_scan_kernel): the block
+// holding packet q's 4-byte TS header (byte 188 q; 188 q mod 16 is 0, 4, 8 or 12, so the header
+// never straddles blocks) is also stored, whole, as record q of the segment.  The scan then
+// reads 16 dense bytes per packet instead of one 128-byte line of plaintext per packet (0.68 of
+// a pass).  Per block: one multiply-high division by 188 and a compare; one masked 16-byte
+// store in ~1 of 12 lanes.
+struct AesHdr {
+  const int64_t* off;  // [nseg] the segment's first record (nullptr: no records)
+  uint4* rec;
+};
+constexpr uint32_t kDiv188Magic = 2924233053u;  // floor(x / 188) = umulhi(x, M) >> 7 for all 32-bit x
+
 // tdl: little-endian Td0 (256 words); isb: inverse S-box (256 bytes)
 // drk: per-segment little-endian equivalent-inverse-cipher round keys (44 words)
 // chunk_prefix: exclusive prefix of per-segment 256-block chunks (one chunk = one wave
 //   iteration: lane l decrypts blocks 64j + l, j < kBlk, so every load/store instruction
 //   moves 1 KB contiguous); waves never straddle segments
-// kCrc: 0 without the fused CRC code (its registers), 1 with it
-template <int kCrc>
+// kCrc: 0 without the fused CRC code (its registers), 1 with it; kHdr: packet-header records
+template <int kCrc, int kHdr>
 __global__ __launch_bounds__(kAesThreads, 1) void aes128_cbc_decrypt_kernel(
     const uint8_t* __restrict__ src, uint8_t* __restrict__ dst, const int64_t* __restrict__ src_off,
     const int64_t* __restrict__ dst_off, const int64_t* __restrict__ blk_prefix,
     const int64_t* __restrict__ chunk_prefix, const uint32_t* __restrict__ drk, const uint32_t* __restrict__ ivw,
     const uint32_t* __restrict__ tdl_g, const uint8_t* __restrict__ isb_g, int64_t* __restrict__ out_len, int nseg,
-    int64_t total_chunks, int64_t per_wg, AesCrc crc) {
+    int64_t total_chunks, int64_t per_wg, AesCrc crc, AesHdr hdr) {
   __shared__ uint32_t s_tab[kTdDwords + kIsDwords];  // 160 KiB (layout above)
   const int tid = threadIdx.x;
   aes_image_fill(s_tab, tdl_g, isb_g, tid);
@@ -128,7 +140,7 @@ __global__ __launch_bounds__(kAesThreads, 1) void aes128_cbc_decrypt_kernel(
   // segment state is wave-uniform (SGPRs): round keys come in by scalar loads
   int cur = -1;
   uint32_t rk[44];
-  int64_t so = 0, dof = 0, cstart = 0, cend = 0, nblk = 0, maskb = -1;
+  int64_t so = 0, dof = 0, cstart = 0, cend = 0, nblk = 0, maskb = -1, hdrb = 0;
   v4i crc_w[kCrcSteps];
   if constexpr (kCrc == 1) {
 #pragma unroll
@@ -146,6 +158,7 @@ __global__ __launch_bounds__(kAesThreads, 1) void aes128_cbc_decrypt_kernel(
       cend = chunk_prefix[cur + 1];
       nblk = blk_prefix[cur + 1] - blk_prefix[cur];
       maskb = crc.mask_off != nullptr ? crc.mask_off[cur] : -1;
+      if constexpr (kHdr == 1) hdrb = hdr.off[cur];
     }
     const int64_t b0 = (ch - cstart) * (64 * kBlk) + lane;  // this lane's first block
     const uint4* cs = reinterpret_cast<const uint4*>(src + so);
@@ -178,6 +191,11 @@ __global__ __launch_bounds__(kAesThreads, 1) void aes128_cbc_decrypt_kernel(
       const uint4 p = make_uint4(o0, o1, o2, o3);
       const int64_t b = b0 + 64 * j;
       if (b < nblk) ds[b] = p;
+      if constexpr (kHdr == 1) {  // does packet q = ceil(16 b / 188) start in this block?
+        const uint32_t b16 = static_cast<uint32_t>(b) << 4;
+        const uint32_t q = __umulhi(b16 + 187u, kDiv188Magic) >> 7;
+        if (q * 188u - b16 < 16u && b < nblk) hdr.rec[hdrb + q] = p;
+      }
       if (b == nblk - 1) out_len[cur] = pkcs7_len(p, nblk * 16);
     }
   }
@@ -198,24 +216,29 @@ void aes_grid(int64_t total_chunks, int num_cu, int64_t& grid, int64_t& per_wg) 
 }
 }  // namespace
 
-// crc_mask_off / crc_wfrag / crc_masks: the fused ciphertext CRC (nullptr: off)
+// crc_mask_off / crc_wfrag / crc_masks: the fused ciphertext CRC (nullptr: off);
+// hdr_off / hdr_rec: packet-header records for the demux scan (nullptr: off)
 hipError_t launch_aes128_cbc_decrypt(const uint8_t* src, uint8_t* dst, const int64_t* src_off, const int64_t* dst_off,
                                      const int64_t* blk_prefix, const int64_t* chunk_prefix, const uint32_t* drk,
                                      const uint32_t* ivw, const uint32_t* tdl, const uint8_t* isb, int64_t* out_len,
                                      int nseg, int64_t total_chunks, int num_cu, hipStream_t stream,
-                                     const int64_t* crc_mask_off, const void* crc_wfrag, uint32_t* crc_masks) {
+                                     const int64_t* crc_mask_off, const void* crc_wfrag, uint32_t* crc_masks,
+                                     const int64_t* hdr_off, void* hdr_rec) {
   if (total_chunks <= 0) return hipSuccess;
   int64_t grid, per_wg;
   aes_grid(total_chunks, num_cu, grid, per_wg);
   const AesCrc crc{crc_mask_off, reinterpret_cast<const v4i*>(crc_wfrag), crc_masks};
-#define AES_LAUNCH(M)                                                                                             \
-  hipLaunchKernelGGL(aes128_cbc_decrypt_kernel<M>, dim3(static_cast<unsigned>(grid)), dim3(kAesThreads), 0, stream,  \
-                     src, dst, src_off, dst_off, blk_prefix, chunk_prefix, drk, ivw, tdl, isb, out_len, nseg,     \
-                     total_chunks, per_wg, crc)
-  if (crc_mask_off == nullptr)
-    AES_LAUNCH(0);
-  else
-    AES_LAUNCH(1);
+#define AES_LAUNCH(M, H)                                                                                          \
+  hipLaunchKernelGGL((aes128_cbc_decrypt_kernel<M, H>), dim3(static_cast<unsigned>(grid)), dim3(kAesThreads), 0,     \
+                     stream, src, dst, src_off, dst_off, blk_prefix, chunk_prefix, drk, ivw, tdl, isb, out_len, nseg, \
+                     total_chunks, per_wg, crc, hdr)
+  const AesHdr hdr{hdr_off, reinterpret_cast<uint4*>(hdr_rec)};
+  const bool with_hdr = hdr_off != nullptr && hdr_rec != nullptr;
+  if (crc_mask_off == nullptr) {
+    if (with_hdr) AES_LAUNCH(0, 1); else AES_LAUNCH(0, 0);
+  } else {
+    if (with_hdr) AES_LAUNCH(1, 1); else AES_LAUNCH(1, 0);
+  }
 #undef AES_LAUNCH
   return hipGetLastError();
 }

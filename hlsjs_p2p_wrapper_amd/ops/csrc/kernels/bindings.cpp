@@ -15,12 +15,13 @@ int aes_chunk_blocks();
 hipError_t launch_aes128_cbc_decrypt(const uint8_t*, uint8_t*, const int64_t*, const int64_t*, const int64_t*,
                                      const int64_t*, const uint32_t*, const uint32_t*, const uint32_t*,
                                      const uint8_t*, int64_t*, int, int64_t, int, hipStream_t, const int64_t*,
-                                     const void*, uint32_t*);
+                                     const void*, uint32_t*, const int64_t*, void*);
 hipError_t launch_crc32_batch(const uint8_t*, const int64_t*, const int64_t*, const int64_t*, const int64_t*,
                               const void*, const uint32_t*, uint32_t*, uint32_t*, const uint32_t*, uint8_t*,
                               const int64_t*, uint32_t*, int64_t, int, int64_t, int, bool, hipStream_t);
 hipError_t launch_ts_demux(const uint8_t*, const int64_t*, const int64_t*, const int64_t*, int, int64_t, uint32_t*,
-                           int64_t*, int32_t*, uint8_t*, const int64_t*, int64_t*, int64_t, int64_t*, hipStream_t);
+                           int64_t*, int32_t*, uint8_t*, const int64_t*, int64_t*, int64_t, int64_t*, hipStream_t,
+                           const void*, const int64_t*);
 hipError_t launch_segment_copy(const uint8_t*, uint8_t*, const int64_t*, const int64_t*, const int64_t*,
                                const int64_t*, int, int64_t, hipStream_t);
 }  // namespace dev
@@ -88,7 +89,7 @@ void aes128_cbc_decrypt(Tensor src, Tensor dst, Tensor src_off, Tensor dst_off, 
                                   cptr<int64_t>(dst_off), cptr<int64_t>(blk_prefix), cptr<int64_t>(chunk_prefix),
                                   cptr<uint32_t>(drk), cptr<uint32_t>(iv), cptr<uint32_t>(td0), cptr<uint8_t>(isb),
                                   mptr<int64_t>(out_len), static_cast<int>(B), total_chunks, num_cus(src), stream(),
-                                  nullptr, nullptr, nullptr),
+                                  nullptr, nullptr, nullptr, nullptr, nullptr),
      "aes128_cbc_decrypt");
 }
 
@@ -156,7 +157,7 @@ void ts_demux(Tensor buf, Tensor seg_off, Tensor seg_len, Tensor blk_prefix, int
   ok(D::launch_ts_demux(cptr<uint8_t>(buf), cptr<int64_t>(seg_off), cptr<int64_t>(seg_len),
                         cptr<int64_t>(blk_prefix), static_cast<int>(B), total_blocks, mptr<uint32_t>(meta),
                         mptr<int64_t>(pts_dts), mptr<int32_t>(blk_sums), mptr<uint8_t>(es), cptr<int64_t>(es_off),
-                        mptr<int64_t>(pes), max_pes, mptr<int64_t>(info), stream()),
+                        mptr<int64_t>(pes), max_pes, mptr<int64_t>(info), stream(), nullptr, nullptr),
      "ts_demux");
 }
 

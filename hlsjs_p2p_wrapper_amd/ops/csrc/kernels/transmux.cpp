@@ -26,9 +26,10 @@ int aes_chunk_blocks();
 hipError_t launch_aes128_cbc_decrypt(const uint8_t*, uint8_t*, const int64_t*, const int64_t*, const int64_t*,
                                      const int64_t*, const uint32_t*, const uint32_t*, const uint32_t*,
                                      const uint8_t*, int64_t*, int, int64_t, int, hipStream_t, const int64_t*,
-                                     const void*, uint32_t*);
+                                     const void*, uint32_t*, const int64_t*, void*);
 hipError_t launch_ts_demux(const uint8_t*, const int64_t*, const int64_t*, const int64_t*, int, int64_t, uint32_t*,
-                           int64_t*, int32_t*, uint8_t*, const int64_t*, int64_t*, int64_t, int64_t*, hipStream_t);
+                           int64_t*, int32_t*, uint8_t*, const int64_t*, int64_t*, int64_t, int64_t*, hipStream_t,
+                           const void*, const int64_t*);
 hipError_t launch_crc32_from_masks(const uint32_t*, const void*, const int64_t*, const int64_t*, const uint32_t*, uint32_t*, uint32_t*,
                                    const uint32_t*, uint8_t*, const int64_t*, uint32_t*, int64_t, int, int64_t, int,
                                    hipStream_t);
@@ -190,6 +191,15 @@ py::tuple transmux_launch(Tensor src, I64 src_off, I64 nbytes, py::array_t<uint8
   std::vector<int64_t> a_so, a_do, a_bp{0}, a_cp{0};
   std::vector<int64_t> a_mo, v_idx, v_coff, v_len, v_expw;  // fused CRC: mask offsets, verify columns
   int64_t v_chunks = 0;
+  // packet-header records for the demux scan, written by the decrypt (aes_cbc.hip AesHdr):
+  // per encrypted segment nb / 188 + 2 16-byte records (HLSP2P_HDR_RECORDS=0: off, the scan
+  // reads the plaintext)
+  static const bool hdr_on = [] {
+    const char* v = std::getenv("HLSP2P_HDR_RECORDS");
+    return v == nullptr || std::strcmp(v, "0") != 0;
+  }();
+  std::vector<int64_t> a_ho;
+  int64_t hdr_pos = 0;
   std::vector<uint32_t> a_drk;
   std::vector<uint8_t> a_iv;
   DemuxPlan pe, pc;
@@ -206,6 +216,8 @@ py::tuple transmux_launch(Tensor src, I64 src_off, I64 nbytes, py::array_t<uint8
       const int64_t blocks = nb[i] / 16;
       a_bp.push_back(a_bp.back() + blocks);
       a_cp.push_back(a_cp.back() + (blocks + chunk - 1) / chunk);
+      a_ho.push_back(hdr_pos);
+      hdr_pos += nb[i] / kPacket + 2;
       if (!v_exp.empty()) {
         const int64_t nch = (blocks + chunk - 1) / chunk;  // one 4096-byte CRC chunk per decrypt chunk
         if (v_exp[i] >= 0) {
@@ -235,7 +247,7 @@ py::tuple transmux_launch(Tensor src, I64 src_off, I64 nbytes, py::array_t<uint8
   // ---- every descriptor of the batch in one staging block, one H2D
   Desc desc;
   int64_t d_so = -1, d_do = -1, d_bp = -1, d_cp = -1, d_drk = -1, d_iv = -1, d_mo = -1, d_vco = -1, d_vl = -1,
-          d_vx = -1;
+          d_vx = -1, d_ho = -1;
   const int64_t nv = static_cast<int64_t>(v_idx.size());
   if (ne) {
     d_so = desc.add(a_so);
@@ -247,6 +259,7 @@ py::tuple transmux_launch(Tensor src, I64 src_off, I64 nbytes, py::array_t<uint8
     pe.d_off = desc.add(pe.off);
     pe.d_bp = desc.add(pe.blk_prefix);
     pe.d_eo = desc.add(pe.es_off);
+    if (hdr_on) d_ho = desc.add(a_ho);
     if (nv) {
       std::vector<uint32_t> ex32(v_expw.begin(), v_expw.end());
       d_mo = desc.add(a_mo);
@@ -274,6 +287,8 @@ py::tuple transmux_launch(Tensor src, I64 src_off, I64 nbytes, py::array_t<uint8
     v_crc = torch::empty({nv}, dev_opts.dtype(torch::kInt32));
     v_ok = torch::empty({nv}, dev_opts.dtype(torch::kUInt8));
   }
+  Tensor hdr_rec;
+  if (ne && hdr_on) hdr_rec = torch::empty({std::max<int64_t>(1, hdr_pos) * 16}, dev_opts.dtype(torch::kUInt8));
   if (ne) {
     dec = torch::empty({dec_pos + kAlign}, dev_opts.dtype(torch::kUInt8));
     hip_ok(hlsp2p::dev::launch_aes128_cbc_decrypt(
@@ -282,7 +297,8 @@ py::tuple transmux_launch(Tensor src, I64 src_off, I64 nbytes, py::array_t<uint8
                desc.at<uint32_t>(d_drk), desc.at<uint32_t>(d_iv), static_cast<const uint32_t*>(td0.data_ptr()),
                static_cast<const uint8_t*>(isb.data_ptr()), out_len.data_ptr<int64_t>(), static_cast<int>(ne),
                a_cp.back(), decrypt_cus(device), st, nv ? desc.at<int64_t>(d_mo) : nullptr,
-               nv ? crc_w->data_ptr() : nullptr, nv ? reinterpret_cast<uint32_t*>(masks.data_ptr<int32_t>()) : nullptr),
+               nv ? crc_w->data_ptr() : nullptr, nv ? reinterpret_cast<uint32_t*>(masks.data_ptr<int32_t>()) : nullptr,
+               hdr_on ? desc.at<int64_t>(d_ho) : nullptr, hdr_on ? hdr_rec.data_ptr() : nullptr),
            "aes128_cbc_decrypt");
   }
   if (nv) {  // fold the decrypt's CRC masks per chunk, combine per segment, compare
@@ -319,7 +335,9 @@ py::tuple transmux_launch(Tensor src, I64 src_off, I64 nbytes, py::array_t<uint8
                                         reinterpret_cast<uint32_t*>(meta.data_ptr<int32_t>()),
                                         pts.data_ptr<int64_t>(), aux.data_ptr<int32_t>(), es.data_ptr<uint8_t>(),
                                         desc.at<int64_t>(p.d_eo), pes.data_ptr<int64_t>(), max_pes,
-                                        info.data_ptr<int64_t>(), st),
+                                        info.data_ptr<int64_t>(), st,
+                                        g == 0 && hdr_on ? hdr_rec.data_ptr() : nullptr,
+                                        g == 0 && hdr_on ? desc.at<int64_t>(d_ho) : nullptr),
            "ts_demux");
     keep.append(py::make_tuple(meta, pts, aux));
     // D2H through torch's copy so the caching host allocator records the use of the pinned
@@ -345,6 +363,7 @@ py::tuple transmux_launch(Tensor src, I64 src_off, I64 nbytes, py::array_t<uint8
   }
   keep.append(dec.defined() ? py::cast(dec) : py::none());
   keep.append(desc.device());
+  if (hdr_rec.defined()) keep.append(hdr_rec);
   py::object verify = py::none();
   if (nv) {
     keep.append(py::make_tuple(masks, chunk_res, v_crc, v_ok));

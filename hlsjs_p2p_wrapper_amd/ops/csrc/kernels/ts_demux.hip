@@ -147,10 +147,15 @@ __device__ __forceinline__ int wave_incl_scan(int v, int lane) {
   return v;
 }
 
+// hdr_rec / hdr_off (optional, from the decrypt: aes_cbc.hip AesHdr): record p of a segment is
+// the 16-byte block holding packet p's header at byte (188 p) mod 16 -- read densely instead of
+// one plaintext line per packet; byte 4 (adaptation-field length) comes from it too unless the
+// header sits at byte 12, and PES headers still come from the plaintext (a few % of packets).
 __global__ __launch_bounds__(kTsThreads) void ts_scan_kernel(
     const uint8_t* __restrict__ buf, const int64_t* __restrict__ seg_off, const int64_t* __restrict__ seg_len,
     const int64_t* __restrict__ blk_prefix, int nseg, int64_t* __restrict__ info, uint32_t* __restrict__ meta,
-    int64_t* __restrict__ pts_dts, int32_t* __restrict__ blk_sums) {
+    int64_t* __restrict__ pts_dts, int32_t* __restrict__ blk_sums, const uint4* __restrict__ hdr_rec,
+    const int64_t* __restrict__ hdr_off) {
   __shared__ int32_t s_sum[2 * kClasses];
   __shared__ int32_t s_err;
   const int64_t gblk = blockIdx.x;
@@ -170,7 +175,16 @@ __global__ __launch_bounds__(kTsThreads) void ts_scan_kernel(
   int err = 0;
   if (pk < np) {
     const uint8_t* p = buf + seg_off[seg] + pk * kPkt;
-    const uint32_t hdr = *reinterpret_cast<const uint32_t*>(p);  // packets are 4-byte aligned
+    uint32_t hdr;
+    int b4 = -1;  // byte 4 when the record holds it
+    if (hdr_rec != nullptr) {
+      const uint4 r = hdr_rec[hdr_off[seg] + pk];
+      const int o = static_cast<int>((pk * kPkt) & 15);  // 0, 4, 8 or 12
+      hdr = o == 0 ? r.x : o == 4 ? r.y : o == 8 ? r.z : r.w;
+      if (o < 12) b4 = static_cast<int>((o == 0 ? r.y : o == 4 ? r.z : r.w) & 0xff);
+    } else {
+      hdr = *reinterpret_cast<const uint32_t*>(p);  // packets are 4-byte aligned
+    }
     const int sync = hdr & 0xff;
     const int b1 = (hdr >> 8) & 0xff, b2 = (hdr >> 16) & 0xff, b3 = hdr >> 24;
     if (sync != 0x47) {
@@ -180,7 +194,7 @@ __global__ __launch_bounds__(kTsThreads) void ts_scan_kernel(
       const int cls = (cpid0 >= 0 && pid == cpid0) ? 0 : (cpid1 >= 0 && pid == cpid1) ? 1 : (cpid2 >= 0 && pid == cpid2) ? 2 : 3;
       const int afc = (b3 >> 4) & 3;
       if (cls < 3 && (afc & 1)) {
-        int s = 4 + ((afc & 2) ? 1 + p[4] : 0);
+        int s = 4 + ((afc & 2) ? 1 + (b4 >= 0 ? b4 : p[4]) : 0);
         if (s > kPkt) {
           err |= static_cast<int>(kBadLength);
         } else {
@@ -444,7 +458,8 @@ __global__ __launch_bounds__(kTsThreads) void ts_gather_kernel(
 hipError_t launch_ts_demux(const uint8_t* buf, const int64_t* seg_off, const int64_t* seg_len,
                            const int64_t* blk_prefix, int nseg, int64_t total_blocks, uint32_t* meta,
                            int64_t* pts_dts, int32_t* aux, uint8_t* es, const int64_t* es_off, int64_t* pes,
-                           int64_t max_pes, int64_t* info, hipStream_t stream) {
+                           int64_t max_pes, int64_t* info, hipStream_t stream, const void* hdr_rec,
+                           const int64_t* hdr_off) {
   if (nseg <= 0) return hipSuccess;
   // aux (int32): [blk_sums: blocks x 6 | blk_pre: blocks x 6 | seg_tot: nseg x 6 | spare: nseg]
   int32_t* blk_sums = aux;
@@ -454,7 +469,8 @@ hipError_t launch_ts_demux(const uint8_t* buf, const int64_t* seg_off, const int
   hipError_t e = hipGetLastError();
   if (e != hipSuccess || total_blocks <= 0) return e;
   hipLaunchKernelGGL(ts_scan_kernel, dim3(static_cast<unsigned>(total_blocks)), dim3(kTsThreads), 0, stream, buf,
-                     seg_off, seg_len, blk_prefix, nseg, info, meta, pts_dts, blk_sums);
+                     seg_off, seg_len, blk_prefix, nseg, info, meta, pts_dts, blk_sums,
+                     reinterpret_cast<const uint4*>(hdr_rec), hdr_rec != nullptr ? hdr_off : nullptr);
   e = hipGetLastError();
   if (e != hipSuccess) return e;
   hipLaunchKernelGGL(ts_prefix_kernel, dim3(nseg), dim3(64), 0, stream, blk_prefix, blk_sums, blk_pre, seg_tot, info,
