@@ -151,100 +151,151 @@ __device__ __forceinline__ int wave_incl_scan(int v, int lane) {
 // the 16-byte block holding packet p's header at byte (188 p) mod 16 -- read densely instead of
 // one plaintext line per packet; byte 4 (adaptation-field length) comes from it too unless the
 // header sits at byte 12, and PES headers still come from the plaintext (a few % of packets).
+//
+// One workgroup scans kScanBlocks consecutive 256-packet blocks (the unit of blk_sums): the
+// segment lookup and PID loads are paid once, and every block's header loads are issued before
+// the first block is parsed (a workgroup per block was a chain of dependent loads per 256
+// packets: latency, not bandwidth, set the scan's time).
+constexpr int kScanBlocks = 4;
+
+struct ScanPkt {
+  uint32_t hdr;
+  int b4;  // byte 4 when known (-1: read it from the plaintext)
+};
+
+__device__ __forceinline__ ScanPkt scan_load(const uint8_t* __restrict__ p, const uint4* __restrict__ rec, int64_t pk) {
+  ScanPkt r;
+  r.b4 = -1;
+  if (rec != nullptr) {
+    const uint4 v = *rec;
+    const int o = static_cast<int>((pk * kPkt) & 15);  // 0, 4, 8 or 12
+    r.hdr = o == 0 ? v.x : o == 4 ? v.y : o == 8 ? v.z : v.w;
+    if (o < 12) r.b4 = static_cast<int>((o == 0 ? v.y : o == 4 ? v.z : v.w) & 0xff);
+  } else {
+    r.hdr = *reinterpret_cast<const uint32_t*>(p);  // packets are 4-byte aligned
+  }
+  return r;
+}
+
 __global__ __launch_bounds__(kTsThreads) void ts_scan_kernel(
     const uint8_t* __restrict__ buf, const int64_t* __restrict__ seg_off, const int64_t* __restrict__ seg_len,
-    const int64_t* __restrict__ blk_prefix, int nseg, int64_t* __restrict__ info, uint32_t* __restrict__ meta,
-    int64_t* __restrict__ pts_dts, int32_t* __restrict__ blk_sums, const uint4* __restrict__ hdr_rec,
-    const int64_t* __restrict__ hdr_off) {
-  __shared__ int32_t s_sum[2 * kClasses];
-  __shared__ int32_t s_err;
-  const int64_t gblk = blockIdx.x;
-  const int seg = find_seg_wave(blk_prefix, nseg, gblk);
-  const int64_t blk = gblk - blk_prefix[seg];
+    const int64_t* __restrict__ blk_prefix, int nseg, int64_t total_blocks, int64_t* __restrict__ info,
+    uint32_t* __restrict__ meta, int64_t* __restrict__ pts_dts, int32_t* __restrict__ blk_sums,
+    const uint4* __restrict__ hdr_rec, const int64_t* __restrict__ hdr_off) {
+  __shared__ int32_t s_sum[kScanBlocks][2 * kClasses];
+  __shared__ int32_t s_err[kScanBlocks];
   const int tid = threadIdx.x;
-  if (tid < 2 * kClasses) s_sum[tid] = 0;
-  if (tid == 0) s_err = 0;
-  __syncthreads();
-  const int64_t* inf = info + static_cast<int64_t>(seg) * kInfo;
-  const int cpid0 = static_cast<int>(inf[kVideoPid]), cpid1 = static_cast<int>(inf[kVideoPid + 1]),
-            cpid2 = static_cast<int>(inf[kVideoPid + 2]);
-  const int64_t np = seg_length(seg_len, seg) / kPkt;
-  const int64_t pk = blk * kTsThreads + tid;
-  const int64_t gpk = gblk * kTsThreads + tid;  // global packet slot (meta index)
-  int c = 3, ps = 0, len = 0, pes = 0;
-  int err = 0;
-  if (pk < np) {
-    const uint8_t* p = buf + seg_off[seg] + pk * kPkt;
-    uint32_t hdr;
-    int b4 = -1;  // byte 4 when the record holds it
-    if (hdr_rec != nullptr) {
-      const uint4 r = hdr_rec[hdr_off[seg] + pk];
-      const int o = static_cast<int>((pk * kPkt) & 15);  // 0, 4, 8 or 12
-      hdr = o == 0 ? r.x : o == 4 ? r.y : o == 8 ? r.z : r.w;
-      if (o < 12) b4 = static_cast<int>((o == 0 ? r.y : o == 4 ? r.z : r.w) & 0xff);
-    } else {
-      hdr = *reinterpret_cast<const uint32_t*>(p);  // packets are 4-byte aligned
+  const int64_t gb0 = static_cast<int64_t>(blockIdx.x) * kScanBlocks;
+  const int nb = static_cast<int>(total_blocks - gb0 < kScanBlocks ? total_blocks - gb0 : kScanBlocks);
+  if (tid < kScanBlocks * 2 * kClasses) (&s_sum[0][0])[tid] = 0;
+  if (tid < kScanBlocks) s_err[tid] = 0;
+  // the segment of each block (uniform), then every block's header load in flight at once
+  int segs[kScanBlocks];
+  int seg = find_seg_wave(blk_prefix, nseg, gb0);
+  ScanPkt pkt[kScanBlocks];
+  int64_t pks[kScanBlocks];
+  const uint8_t* pp[kScanBlocks];
+#pragma unroll
+  for (int u = 0; u < kScanBlocks; ++u) {
+    segs[u] = seg;
+    pks[u] = -1;
+    if (u < nb) {
+      if (u > 0) {
+        seg = __builtin_amdgcn_readfirstlane(advance_seg(blk_prefix, seg, gb0 + u));
+        segs[u] = seg;
+      }
+      const int64_t np = seg_length(seg_len, seg) / kPkt;
+      const int64_t pk = (gb0 + u - blk_prefix[seg]) * kTsThreads + tid;
+      if (pk < np) {
+        pks[u] = pk;
+        pp[u] = buf + seg_off[seg] + pk * kPkt;
+        pkt[u] = scan_load(pp[u], hdr_rec != nullptr ? hdr_rec + hdr_off[seg] + pk : nullptr, pk);
+      }
     }
-    const int sync = hdr & 0xff;
-    const int b1 = (hdr >> 8) & 0xff, b2 = (hdr >> 16) & 0xff, b3 = hdr >> 24;
-    if (sync != 0x47) {
-      err |= static_cast<int>(kBadSync);
-    } else {
-      const int pid = ((b1 & 0x1f) << 8) | b2;
-      const int cls = (cpid0 >= 0 && pid == cpid0) ? 0 : (cpid1 >= 0 && pid == cpid1) ? 1 : (cpid2 >= 0 && pid == cpid2) ? 2 : 3;
-      const int afc = (b3 >> 4) & 3;
-      if (cls < 3 && (afc & 1)) {
-        int s = 4 + ((afc & 2) ? 1 + (b4 >= 0 ? b4 : p[4]) : 0);
-        if (s > kPkt) {
-          err |= static_cast<int>(kBadLength);
-        } else {
-          int l = kPkt - s;
-          bool ok = true;
-          if (b1 & 0x40) {
-            const uint8_t* h = p + s;
-            if (l < 9 || h[0] != 0 || h[1] != 0 || h[2] != 1 || 9 + h[8] > l) {
-              err |= static_cast<int>(kPesHeaderError);
-              ok = false;
-            } else {
-              const int64_t pts = ((h[7] & 0x80) && l >= 14) ? read_pts(h + 9) : -1;
-              const int64_t dts = ((h[7] & 0xC0) == 0xC0 && l >= 19) ? read_pts(h + 14) : -1;
-              pts_dts[2 * gpk] = pts;
-              pts_dts[2 * gpk + 1] = dts;
-              pes = 1;
-              s += 9 + h[8];
-              l -= 9 + h[8];
+  }
+  __syncthreads();
+  int cur = -1, cpid0 = -1, cpid1 = -1, cpid2 = -1;
+#pragma unroll
+  for (int u = 0; u < kScanBlocks; ++u) {
+    if (u >= nb) break;
+    if (segs[u] != cur) {
+      cur = segs[u];
+      const int64_t* inf = info + static_cast<int64_t>(cur) * kInfo;
+      cpid0 = static_cast<int>(inf[kVideoPid]);
+      cpid1 = static_cast<int>(inf[kVideoPid + 1]);
+      cpid2 = static_cast<int>(inf[kVideoPid + 2]);
+    }
+    const int64_t gpk = (gb0 + u) * kTsThreads + tid;  // global packet slot (meta index)
+    int c = 3, ps = 0, len = 0, pes = 0;
+    int err = 0;
+    if (pks[u] >= 0) {
+      const uint8_t* p = pp[u];
+      const uint32_t hdr = pkt[u].hdr;
+      const int sync = hdr & 0xff;
+      const int b1 = (hdr >> 8) & 0xff, b2 = (hdr >> 16) & 0xff, b3 = hdr >> 24;
+      if (sync != 0x47) {
+        err |= static_cast<int>(kBadSync);
+      } else {
+        const int pid = ((b1 & 0x1f) << 8) | b2;
+        const int cls = (cpid0 >= 0 && pid == cpid0) ? 0 : (cpid1 >= 0 && pid == cpid1) ? 1 : (cpid2 >= 0 && pid == cpid2) ? 2 : 3;
+        const int afc = (b3 >> 4) & 3;
+        if (cls < 3 && (afc & 1)) {
+          int s = 4 + ((afc & 2) ? 1 + (pkt[u].b4 >= 0 ? pkt[u].b4 : p[4]) : 0);
+          if (s > kPkt) {
+            err |= static_cast<int>(kBadLength);
+          } else {
+            int l = kPkt - s;
+            bool ok = true;
+            if (b1 & 0x40) {
+              const uint8_t* h = p + s;
+              if (l < 9 || h[0] != 0 || h[1] != 0 || h[2] != 1 || 9 + h[8] > l) {
+                err |= static_cast<int>(kPesHeaderError);
+                ok = false;
+              } else {
+                const int64_t pts = ((h[7] & 0x80) && l >= 14) ? read_pts(h + 9) : -1;
+                const int64_t dts = ((h[7] & 0xC0) == 0xC0 && l >= 19) ? read_pts(h + 14) : -1;
+                pts_dts[2 * gpk] = pts;
+                pts_dts[2 * gpk + 1] = dts;
+                pes = 1;
+                s += 9 + h[8];
+                l -= 9 + h[8];
+              }
             }
-          }
-          if (ok) {
-            c = cls;
-            ps = s;
-            len = l;
+            if (ok) {
+              c = cls;
+              ps = s;
+              len = l;
+            }
           }
         }
       }
     }
-  }
-  meta[gpk] = pack_meta(c, ps, len, pes);
-  // wave-level sums per class, then one LDS atomic per wave per class
+    meta[gpk] = pack_meta(c, ps, len, pes);
+    // wave-level sums per class (bytes < 2^16 and PES starts packed in one word), then one
+    // LDS atomic per wave per class
 #pragma unroll
-  for (int k = 0; k < kClasses; ++k) {
-    int vb = (c == k) ? len : 0;
-    int vp = (c == k) ? pes : 0;
+    for (int k = 0; k < kClasses; ++k) {
+      int v = (c == k) ? (len | (pes << 16)) : 0;
 #pragma unroll
-    for (int o = 32; o > 0; o >>= 1) {
-      vb += __shfl_xor(vb, o);
-      vp += __shfl_xor(vp, o);
+      for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
+      if ((tid & 63) == 0 && v) {
+        atomicAdd(&s_sum[u][2 * k], v & 0xffff);
+        atomicAdd(&s_sum[u][2 * k + 1], v >> 16);
+      }
     }
-    if ((tid & 63) == 0) {
-      if (vb) atomicAdd(&s_sum[2 * k], vb);
-      if (vp) atomicAdd(&s_sum[2 * k + 1], vp);
-    }
+    if (err) atomicOr(&s_err[u], err);
   }
-  if (err) atomicOr(&s_err, err);
   __syncthreads();
-  if (tid < 2 * kClasses) blk_sums[gblk * 2 * kClasses + tid] = s_sum[tid];
-  if (tid == 0 && s_err) atomicOr(reinterpret_cast<unsigned long long*>(info + static_cast<int64_t>(seg) * kInfo + kStatus),
-                                  static_cast<unsigned long long>(s_err));
+  if (tid < nb * 2 * kClasses) {
+    const int u = tid / (2 * kClasses), k = tid % (2 * kClasses);
+    blk_sums[(gb0 + u) * 2 * kClasses + k] = s_sum[u][k];
+  }
+  if (tid == 0) {
+    for (int u = 0; u < nb; ++u)
+      if (s_err[u])
+        atomicOr(reinterpret_cast<unsigned long long*>(info + static_cast<int64_t>(segs[u]) * kInfo + kStatus),
+                 static_cast<unsigned long long>(s_err[u]));
+  }
 }
 
 // ---------------------------------------------------------------- 2b. block prefix
@@ -468,8 +519,9 @@ hipError_t launch_ts_demux(const uint8_t* buf, const int64_t* seg_off, const int
   hipLaunchKernelGGL(ts_psi_kernel, dim3(nseg), dim3(64), 0, stream, buf, seg_off, seg_len, info, pes, max_pes);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess || total_blocks <= 0) return e;
-  hipLaunchKernelGGL(ts_scan_kernel, dim3(static_cast<unsigned>(total_blocks)), dim3(kTsThreads), 0, stream, buf,
-                     seg_off, seg_len, blk_prefix, nseg, info, meta, pts_dts, blk_sums,
+  hipLaunchKernelGGL(ts_scan_kernel, dim3(static_cast<unsigned>((total_blocks + kScanBlocks - 1) / kScanBlocks)),
+                     dim3(kTsThreads), 0, stream, buf, seg_off, seg_len, blk_prefix, nseg, total_blocks, info, meta,
+                     pts_dts, blk_sums,
                      reinterpret_cast<const uint4*>(hdr_rec), hdr_rec != nullptr ? hdr_off : nullptr);
   e = hipGetLastError();
   if (e != hipSuccess) return e;
