@@ -682,6 +682,9 @@ def _fleet(args, world, rank, device, use_gpu, node, origin, players, desc, encr
         result = _result(args, world, tot, max_ns / 1e9, origin, K, desc, encrypted, seg_dur, use_gpu, numa_node,
                          dist, players=W, transport=getattr(node.comm, "data_transport", None))
         result["per_rank"] = _per_rank_dicts(per_parts, args.steps)
+        # how received segments were checked: by the CRC fused into the transmux decrypt
+        # (deferred, fleet default) or by the node's own verify pass before delivery
+        result["config"]["receive_verify"] = "fused-decrypt" if getattr(node, "verify_deferred", False) else "node"
         result["data_plane"] = _plane_info(node)
         if live:
             result["config"].update(live=True, live_speed=args.live_speed, live_window=args.live_window,
