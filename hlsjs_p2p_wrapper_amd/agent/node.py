@@ -274,6 +274,7 @@ class SwarmNode:
         # batch that decrypts it computes the CRC on the way (kernels/aes_cbc.hip AesCrc).  The
         # entry stays pending -- pinned, not announced, not served -- until verify_done.
         self.verify_deferred = False
+        self.cdn_balance = os.environ.get("HLSP2P_CDN_BALANCE", "1") != "0"  # planner CDN balance (plan_round_into)
         # entries waiting for a deferred check, by entry id: flag + want info row (a CDN retry's source)
         self._vflag = np.zeros(0, dtype=bool)
         self._vinfo = np.zeros((0, 10), dtype=np.int64)
@@ -803,7 +804,11 @@ class SwarmNode:
         # only the rows this rank sends, receives or fetches (the full plan is identical on
         # every rank; any_p2p says whether the round has transfers at all)
         me = self.rank
-        plan, any_p2p = rt.plan_round_for(self.directory, all_wants, flags, self.world, me)
+        # each rank's cumulative CDN bytes (header word 7): the planner's CDN balance holds a
+        # lone want of a rank over its share back once when another rank is about to want it
+        cdn_bytes = np.fromiter((int(p[7]) for p in parts), dtype=np.int64, count=len(parts)) \
+            if self.cdn_balance and self.world > 1 else None
+        plan, any_p2p = rt.plan_round_for(self.directory, all_wants, flags, self.world, me, cdn_bytes)
         h.n_wants = len(all_wants)
         cdn_rows = plan[(plan[:, 5] == -1) & (plan[:, 6] == me)]
         if self._net_wants and self._wx:  # network-origin wants this rank must download first (STAGE rows)

@@ -470,7 +470,7 @@ PYBIND11_MODULE(_runtime, m) {
       });
   // One round's gathered control messages (agent/node.py:_encode layout: header[hdr_words] =
   // magic, flags, #wants, #adds, #removes, leaving, round, cdn, p2p, upload, ...; then wants
-  // [key4, size, want_id | force_cdn << 62 | not_staged << 61 | staging << 60], adds [key4, len], removes
+  // [key4, size, want_id | force_cdn << 62 | not_staged << 61 | staging << 60 | held << 59], adds [key4, len], removes
   // [key4]) in one call:
   // applies every rank's cache delta to the directory and returns (want rows int64[n, 8] for
   // plan_round, per-rank flags, all-leaving, swarm byte totals [cdn, p2p, upload]).
@@ -509,16 +509,17 @@ PYBIND11_MODULE(_runtime, m) {
       for (int64_t i = 0; i < nr; ++i) d.apply_remove(r, key_from(rm + 4 * i));
       for (int64_t i = 0; i < nw; ++i, o += 8) {
         const int64_t* x = w + 6 * i;
-        // want word: want_id | force_cdn << 62 | not_staged << 61 | staging << 60 -> WantFlag bits
+        // want word: want_id | force_cdn << 62 | not_staged << 61 | staging << 60 | held << 59
+        // -> WantFlag bits
         o[0] = x[0];
         o[1] = x[1];
         o[2] = x[2];
         o[3] = x[3];
         o[4] = x[4];
-        o[5] = x[5] & ((int64_t(1) << 60) - 1);
+        o[5] = x[5] & ((int64_t(1) << 59) - 1);
         o[6] = r;
         o[7] = ((x[5] >> 62) & 1 ? kForceCdn : 0) | ((x[5] >> 61) & 1 ? kNotStaged : 0) |
-               ((x[5] >> 60) & 1 ? kStaging : 0);
+               ((x[5] >> 60) & 1 ? kStaging : 0) | ((x[5] >> 59) & 1 ? kHeld : 0);
       }
     }
     Arr<int64_t> totals(3);
@@ -533,7 +534,7 @@ PYBIND11_MODULE(_runtime, m) {
   // (every rank enters the exchange then).  At 8 ranks a rank needs ~1/4 of the rows: the
   // rest would be built into numpy and masked away in Python every round.
   auto plan_rows = [](const Directory& d, const Arr<int64_t>& wants, const Arr<int64_t>& flags, int world,
-                      int me) {
+                      int me, const py::object& cdn_obj) {
     const int64_t n = wants.size() / 8;
     if (flags.size() != world) throw std::invalid_argument("flags must have world entries");
     std::vector<Want> w(n);
@@ -549,7 +550,13 @@ PYBIND11_MODULE(_runtime, m) {
       if (w[i].rank < 0 || w[i].rank >= world) throw std::invalid_argument("want rank out of range");
     }
     f.assign(flags.data(), flags.data() + world);
-    plan_round_into(d, w.data(), w.size(), f, world, &t);
+    std::vector<int64_t> cdn;
+    if (!cdn_obj.is_none()) {  // each rank's cumulative CDN bytes: the planner's CDN balance
+      Arr<int64_t> c = cdn_obj.cast<Arr<int64_t>>();
+      if (c.size() != world) throw std::invalid_argument("cdn_bytes must have world entries");
+      cdn.assign(c.data(), c.data() + world);
+    }
+    plan_round_into(d, w.data(), w.size(), f, world, &t, cdn.empty() ? nullptr : cdn.data());
     bool any_p2p = false;
     int64_t m = 0;
     for (const Transfer& x : t) {
@@ -566,15 +573,17 @@ PYBIND11_MODULE(_runtime, m) {
     }
     return std::make_pair(out, any_p2p);
   };
-  m.def("plan_round", [plan_rows](const Directory& d, Arr<int64_t> wants, Arr<int64_t> flags, int world) {
-    return plan_rows(d, wants, flags, world, -1).first;
-  });
+  m.def("plan_round", [plan_rows](const Directory& d, Arr<int64_t> wants, Arr<int64_t> flags, int world,
+                                  py::object cdn_bytes) {
+    return plan_rows(d, wants, flags, world, -1, cdn_bytes).first;
+  }, py::arg("directory"), py::arg("wants"), py::arg("flags"), py::arg("world"), py::arg("cdn_bytes") = py::none());
   m.def("plan_round_for", [plan_rows](const Directory& d, Arr<int64_t> wants, Arr<int64_t> flags, int world,
-                                      int me) {
+                                      int me, py::object cdn_bytes) {
     if (me < 0 || me >= world) throw std::invalid_argument("rank out of range");
-    auto r = plan_rows(d, wants, flags, world, me);
+    auto r = plan_rows(d, wants, flags, world, me, cdn_bytes);
     return py::make_tuple(r.first, r.second);
-  });
+  }, py::arg("directory"), py::arg("wants"), py::arg("flags"), py::arg("world"), py::arg("me"),
+     py::arg("cdn_bytes") = py::none());
   // CPU-mode CDN phase: copy origin byte ranges (raw host addresses, as the want table holds
   // them) into the node's host arena at `dst_base + dst_off[i]` (bounds-checked against cap)
   m.def("host_copy_batch", [](int64_t dst_base, int64_t dst_cap, Arr<int64_t> dst_off, Arr<int64_t> src_ptr,

@@ -105,7 +105,7 @@ std::mutex g_scratch_mu;
 }  // namespace
 
 void plan_round_into(const Directory& dir, const Want* wants_in, size_t n_in, const std::vector<int64_t>& flags,
-                     int world, std::vector<Transfer>* out_rows) {
+                     int world, std::vector<Transfer>* out_rows, const int64_t* cdn_bytes) {
   if (world <= 0 || world > kMaxRanks) throw std::invalid_argument("world size out of range");
   if (flags.size() < size_t(world)) throw std::invalid_argument("flags must have world entries");
   std::lock_guard<std::mutex> lock(g_scratch_mu);
@@ -204,11 +204,48 @@ void plan_round_into(const Directory& dir, const Want* wants_in, size_t n_in, co
   std::vector<size_t>& unserved = S.unserved;  // reused per key
   members.clear();
 
+  // CDN balance (see planner.hpp): is rank d over its share of the swarm's CDN bytes?
+  constexpr int64_t kBalanceMinBytes = int64_t(256) << 20;  // no decisions on start-up noise
+  constexpr uint32_t kFollowSns = 4096;                      // "about to want": within this many sns
+  uint64_t over_share = 0;
+  if (cdn_bytes != nullptr && world > 1) {
+    int64_t total = 0;
+    int active = 0;
+    for (int r = 0; r < world; ++r)
+      if (flag(r, kOnline) && flag(r, kCdnDedup)) {
+        total += cdn_bytes[r];
+        ++active;
+      }
+    if (active > 1 && total >= kBalanceMinBytes)
+      for (int r = 0; r < world; ++r)  // share > 1.1 / active
+        if (flag(r, kOnline) && cdn_bytes[r] * 10 * active > total * 11) over_share |= uint64_t(1) << r;
+  }
+  // per track (swarm, level, url_id): each rank's first wanted sn this round (wants are in key
+  // order, so the first want of a rank inside a track run has its smallest sn)
+  uint32_t track_first[kMaxRanks];
+  uint64_t track_ranks = 0;
+  size_t track_end = 0;
+  auto same_track = [](const SegKey& a, const SegKey& b) {
+    return a.swarm == b.swarm && a.level == b.level && a.url_id == b.url_id;
+  };
+
   size_t i = 0;
   while (i < wants.size()) {
     size_t j = i;
     while (j < wants.size() && wants[j].key == wants[i].key) ++j;
     const SegKey key = wants[i].key;
+    if (over_share && i >= track_end) {  // entering a new track: scan its wants once
+      track_ranks = 0;
+      track_end = i;
+      while (track_end < wants.size() && same_track(wants[track_end].key, key)) {
+        const int r = wants[track_end].rank;
+        if (!((track_ranks >> r) & 1u)) {
+          track_ranks |= uint64_t(1) << r;
+          track_first[r] = wants[track_end].key.sn;
+        }
+        ++track_end;
+      }
+    }
     const DirEntry* de = dir.find(key);
     uint64_t holders = 0;
     if (de) {
@@ -267,7 +304,18 @@ void plan_round_into(const Directory& dir, const Want* wants_in, size_t n_in, co
                            (cands & ready) != 0});  // seeder chosen below
         }
       } else {
-        for (size_t w : unserved) cdn_or_stage(wants[w], key);
+        for (size_t w : unserved) {
+          const Want& wt = wants[w];
+          if (unserved.size() == 1 && ((over_share >> wt.rank) & 1u) && !(wt.flags & (kHeld | kForceCdn)) &&
+              flag(wt.rank, kCdnDedup)) {
+            bool follower = false;  // another rank that will want it: online, in the swarm, behind
+            for (int r = 0; r < world && !follower; ++r)
+              follower = r != wt.rank && ((track_ranks >> r) & 1u) && flag(r, kOnline) && flag(r, kCdnDedup) &&
+                         flag(r, kDownloadOn) && track_first[r] <= key.sn && key.sn - track_first[r] <= kFollowSns;
+            if (follower) continue;  // held back one announcement (kHeld next time)
+          }
+          cdn_or_stage(wt, key);
+        }
       }
     }
     i = j;

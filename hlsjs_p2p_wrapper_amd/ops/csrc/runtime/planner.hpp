@@ -42,8 +42,10 @@ struct DirEntry {
   int64_t length = 0;
 };
 
-// kNotStaged: the body is not in host memory yet; kStaging: this rank is downloading it now
-enum WantFlag : int64_t { kForceCdn = 1, kNotStaged = 2, kStaging = 4 };
+// kNotStaged: the body is not in host memory yet; kStaging: this rank is downloading it now;
+// kHeld: announced before without being served (a want is held back at most once, see
+// plan_round_into's CDN balance)
+enum WantFlag : int64_t { kForceCdn = 1, kNotStaged = 2, kStaging = 4, kHeld = 8 };
 
 constexpr int32_t kCdn = -1;    // Transfer.src: CDN fetch (body in host memory) by dst
 constexpr int32_t kStage = -2;  // Transfer.src: dst downloads the body from its network origin
@@ -110,7 +112,14 @@ class Directory {
 std::vector<Transfer> plan_round(const Directory& dir, const std::vector<Want>& wants,
                                  const std::vector<int64_t>& rank_flags, int world);
 // The same plan written into `out` (cleared first; its capacity is reused round to round).
+// `cdn_bytes` (optional, one entry per rank: each rank's cumulative CDN bytes, from the
+// round's control headers): CDN balance -- a segment only one rank wants, no peer holds and
+// another rank is about to want (it already asks for an earlier segment of the same track),
+// is held back one announcement when its wanter has fetched more than its share from the
+// CDN; the follower then fetches it alone and the leader takes the copy.  Ranks whose players
+// run a round apart never co-want a segment, so without this the rank ahead would seed the
+// whole swarm (every other rank's copy crosses its PCIe link once).
 void plan_round_into(const Directory& dir, const Want* wants, size_t n, const std::vector<int64_t>& rank_flags,
-                     int world, std::vector<Transfer>* out);
+                     int world, std::vector<Transfer>* out, const int64_t* cdn_bytes = nullptr);
 
 }  // namespace hlsp2p

@@ -170,7 +170,7 @@ void WantTable::encode(const int64_t* ids, int64_t n, int64_t* rows) const {
     o[3] = r.key.sn;
     o[4] = r.size;
     o[5] = r.id | (int64_t(r.flags & kWForceCdn ? 1 : 0) << 62) | (int64_t(r.flags & kWNotStaged ? 1 : 0) << 61) |
-           (int64_t(r.flags & kWStaging ? 1 : 0) << 60);
+           (int64_t(r.flags & kWStaging ? 1 : 0) << 60) | (int64_t(r.flags & kWHeld ? 1 : 0) << 59);
   }
 }
 
@@ -197,6 +197,7 @@ void WantTable::requeue(const int64_t* ids, int64_t n, bool force_cdn) {
     auto it = recs_.find(ids[i]);
     if (it == recs_.end()) continue;
     it->second.round = -1;
+    it->second.flags |= kWHeld;
     if (force_cdn) {
       it->second.flags |= kWForceCdn;
       it->second.attempts += 1;

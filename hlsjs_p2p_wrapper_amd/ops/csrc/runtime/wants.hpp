@@ -29,6 +29,7 @@ enum WantBits : int32_t {
   kWPrefetch = 8,   // issued by an agent's prefetch planner (may have no waiter)
   kWPy = 16,        // the node keeps Python-side state for it (network / live origin)
   kWCorrupt = 32,   // fault injection: corrupt the CDN copy on ingest
+  kWHeld = 64,      // announced before and not served (the planner holds a want back at most once)
 };
 
 constexpr int64_t kNoToken = -1;
@@ -68,13 +69,15 @@ class WantTable {
   void select(const SegmentStore& store, const Directory* dir, int64_t cap, int32_t round,
               std::vector<int64_t>* admitted, std::vector<int64_t>* dropped, std::vector<int64_t>* too_big,
               int64_t* deferred);
-  // Control rows of wants: [key x4, size, id | force_cdn << 62 | not_staged << 61 | staging << 60].
+  // Control rows of wants: [key x4, size, id | force_cdn << 62 | not_staged << 61 | staging << 60 |
+  // held << 59].
   void encode(const int64_t* ids, int64_t n, int64_t* rows) const;
   // Remove served (or failed) wants; appends their live tokens, the index of each token's
   // want in `ids`, and per want whether it was a prefetch with nobody waiting.
   void finish(const int64_t* ids, int64_t n, std::vector<int64_t>* tokens, std::vector<int64_t>* index,
               std::vector<uint8_t>* prefetch_only);
-  // Back to waiting (planned but not served); `force_cdn`: next time from the CDN (+1 attempt).
+  // Back to waiting (announced but not served: kWHeld from now on); `force_cdn`: next time
+  // from the CDN (+1 attempt).
   void requeue(const int64_t* ids, int64_t n, bool force_cdn);
 
   int64_t size() const { return static_cast<int64_t>(recs_.size()); }
