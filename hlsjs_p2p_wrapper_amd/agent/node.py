@@ -274,7 +274,7 @@ class SwarmNode:
         # batch that decrypts it computes the CRC on the way (kernels/aes_cbc.hip AesCrc).  The
         # entry stays pending -- pinned, not announced, not served -- until verify_done.
         self.verify_deferred = False
-        self.cdn_balance = os.environ.get("HLSP2P_CDN_BALANCE", "1") != "0"  # planner CDN balance (plan_round_into)
+        self.cdn_balance = os.environ.get("HLSP2P_CDN_BALANCE", "0") == "1"  # opt-in (plan_round_into)
         # entries waiting for a deferred check, by entry id: flag + want info row (a CDN retry's source)
         self._vflag = np.zeros(0, dtype=bool)
         self._vinfo = np.zeros((0, 10), dtype=np.int64)

@@ -117,8 +117,12 @@ std::vector<Transfer> plan_round(const Directory& dir, const std::vector<Want>& 
 // another rank is about to want (it already asks for an earlier segment of the same track),
 // is held back one announcement when its wanter has fetched more than its share from the
 // CDN; the follower then fetches it alone and the leader takes the copy.  Ranks whose players
-// run a round apart never co-want a segment, so without this the rank ahead would seed the
-// whole swarm (every other rank's copy crosses its PCIe link once).
+// run a round apart never co-want a segment, so without this the rank ahead seeds the whole
+// swarm.  Opt-in (HLSP2P_CDN_BALANCE=1 on the node): a held want arrives a round later, and
+// measured on the rehearsal plane that latency cost 18.5 % with cheap ingest while the
+// PCIe-origin run gained nothing outside the spread; a leader that does become PCIe-bound
+// slows, its followers catch up and co-want, and the seeding quota splits the bytes anyway
+// (profiles/r4_balance/NOTES.md).
 void plan_round_into(const Directory& dir, const Want* wants, size_t n, const std::vector<int64_t>& rank_flags,
                      int world, std::vector<Transfer>* out, const int64_t* cdn_bytes = nullptr);
 
