@@ -32,6 +32,8 @@ def main():
                     help="distinct segments (the batch cycles through them): 64 x 3 MB fits the 256 MB "
                          "Infinity Cache (MALL), 256 does not -- as in the pipeline, where every segment is new")
     ap.add_argument("--verify", action="store_true")
+    ap.add_argument("--sub", type=int, default=0,
+                    help="launch the batch as back-to-back sub-batches of this many segments (0: one launch)")
     args = ap.parse_args()
     cuda = torch.device("cuda", 0)
     dev = device()
@@ -48,8 +50,16 @@ def main():
     td0, isb = aes.device_tables(cuda)
     total = int(lens.sum())
 
+    def launch_one(sl, expect=None, cw=None, ctab=None):
+        return dev.transmux_launch(src, offs[sl], lens[sl], enc[sl], drk[sl], iv[sl], td0, isb, tsdemux.DEFAULT_MAX_PES,
+                                   None if expect is None else expect[sl], cw, ctab)
+
+    step = args.sub if 0 < args.sub < args.segs else args.segs
+    slices = [slice(a, min(a + step, args.segs)) for a in range(0, args.segs, step)]
+
     def launch(expect=None, cw=None, ctab=None):
-        return dev.transmux_launch(src, offs, lens, enc, drk, iv, td0, isb, tsdemux.DEFAULT_MAX_PES, expect, cw, ctab)
+        outs = [launch_one(sl, expect, cw, ctab) for sl in slices]
+        return outs[0] if len(outs) == 1 else outs
 
     def timed(fn):
         keep = [fn() for _ in range(args.iters + 2)]  # warm the caching allocator: no hipMalloc in the timed loop
@@ -64,7 +74,7 @@ def main():
         return a.elapsed_time(b) * 1e3 / args.iters, keep
 
     us, _ = timed(launch)
-    out = {"segs": args.segs, "bytes": total, "us": round(us, 1), "us_per_seg": round(us / args.segs, 3),
+    out = {"segs": args.segs, "sub": step, "bytes": total, "us": round(us, 1), "us_per_seg": round(us / args.segs, 3),
            "GBps": round(total / (us * 1e-6) / 1e9, 1)}
     if args.verify:
         from hlsjs_p2p_wrapper_amd.ops import crc
@@ -73,7 +83,7 @@ def main():
         expect = np.array([zlib.crc32(host[o:o + n].tobytes()) for o, n in zip(offs, lens)], dtype=np.int64)
         cw, ctab = crc.fused_consts(cuda)
         us_v, keep = timed(lambda: launch(expect, cw, ctab))
-        ok = all(bool(k[3][1].numpy().all()) for k in keep)
+        ok = all(bool(o[3][1].numpy().all()) for k in keep for o in (k if isinstance(k, list) else [k]))
         us_c, _ = timed(lambda: crc.crc32_batch(src, offs, lens, expect=(expect & 0xFFFFFFFF).tolist()))
         out.update(fused_us=round(us_v, 1), fused_us_per_seg=round(us_v / args.segs, 3), fused_all_ok=ok,
                    crc_kernel_us_per_seg=round(us_c / args.segs, 3),
