@@ -81,6 +81,8 @@ def cbc_decrypt_batch(src: torch.Tensor, src_offs: Sequence[int], nbytes: Sequen
         return torch.empty(0, dtype=torch.int64, device=src.device)
     if np.any(nb % 16) or np.any(nb < 16):
         raise ValueError("AES-CBC segments must be non-empty multiples of 16 bytes")
+    if np.any(nb >= 1 << 31):
+        raise ValueError("AES-CBC segments must be under 2 GiB (the kernel's buffer ranges)")
     so = np.asarray(src_offs, dtype=np.int64)
     do = np.asarray(dst_offs, dtype=np.int64)
     if np.any(so % 16) or np.any(do % 16):

@@ -41,6 +41,8 @@ constexpr int kAesWgPerCu = 1;
 constexpr int kBlk = 4;  // blocks per lane per chunk (chunk = 64 * kBlk blocks): independent chains
 
 typedef int v4i __attribute__((ext_vector_type(4)));
+typedef unsigned int v4u __attribute__((ext_vector_type(4)));
+constexpr uint32_t kOutOfRange = 0x80000000u;  // a buffer offset past every segment (reads 0)
 typedef int v8i __attribute__((ext_vector_type(8)));
 typedef float v16f __attribute__((ext_vector_type(16)));
 
@@ -141,6 +143,9 @@ __global__ __launch_bounds__(kAesThreads, 1) void aes128_cbc_decrypt_kernel(
   int cur = -1;
   uint32_t rk[44];
   int64_t so = 0, dof = 0, cstart = 0, cend = 0, nblk = 0, maskb = -1, hdrb = 0;
+  // the current segment's ciphertext / plaintext as buffer ranges (empty until the first segment)
+  __amdgpu_buffer_rsrc_t s_rsrc = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint8_t*>(src), 0, 0, 0x00020000);
+  __amdgpu_buffer_rsrc_t d_rsrc = __builtin_amdgcn_make_buffer_rsrc(dst, 0, 0, 0x00020000);
   v4i crc_w[kCrcSteps];
   if constexpr (kCrc == 1) {
 #pragma unroll
@@ -159,20 +164,27 @@ __global__ __launch_bounds__(kAesThreads, 1) void aes128_cbc_decrypt_kernel(
       nblk = blk_prefix[cur + 1] - blk_prefix[cur];
       maskb = crc.mask_off != nullptr ? crc.mask_off[cur] : -1;
       if constexpr (kHdr == 1) hdrb = hdr.off[cur];
+      s_rsrc = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint8_t*>(src + so), 0, static_cast<int>(nblk * 16),
+                                                 0x00020000);
+      d_rsrc = __builtin_amdgcn_make_buffer_rsrc(dst + dof, 0, static_cast<int>(nblk * 16), 0x00020000);
     }
     const int64_t b0 = (ch - cstart) * (64 * kBlk) + lane;  // this lane's first block
-    const uint4* cs = reinterpret_cast<const uint4*>(src + so);
+    // buffer loads over the segment: blocks past its end read as 0 (no per-block predicate, no
+    // zero fill); the chaining input of block 0 is the IV
     uint4 c[kBlk], pv[kBlk];
+    const uint32_t boff = static_cast<uint32_t>(b0) << 4;  // segments are < 2 GiB (host-checked)
 #pragma unroll
     for (int j = 0; j < kBlk; ++j) {
-      const int64_t b = b0 + 64 * j;
-      c[j] = b < nblk ? cs[b] : make_uint4(0, 0, 0, 0);
+      const v4u q = __builtin_amdgcn_raw_buffer_load_b128(s_rsrc, boff + 1024u * j, 0, 0);
+      c[j] = make_uint4(q[0], q[1], q[2], q[3]);
     }
 #pragma unroll
     for (int j = 0; j < kBlk; ++j) {  // CBC chaining input: the previous block (an L1 hit)
-      const int64_t b = b0 + 64 * j;
-      pv[j] = b == 0 ? reinterpret_cast<const uint4*>(ivw)[cur] : (b < nblk ? cs[b - 1] : make_uint4(0, 0, 0, 0));
+      const uint32_t o = boff + 1024u * j;
+      const v4u q = __builtin_amdgcn_raw_buffer_load_b128(s_rsrc, j == 0 && o == 0 ? kOutOfRange : o - 16u, 0, 0);
+      pv[j] = make_uint4(q[0], q[1], q[2], q[3]);
     }
+    if (ch == cstart && lane == 0) pv[0] = reinterpret_cast<const uint4*>(ivw)[cur];
     if constexpr (kCrc == 1) {
       if (maskb >= 0)  // wave-uniform
         crc_chunk_masks(c, crc_w, lane, crc.masks + maskb + (ch - cstart) * 64);
@@ -183,14 +195,14 @@ __global__ __launch_bounds__(kAesThreads, 1) void aes128_cbc_decrypt_kernel(
       st[j][0] = c[j].x ^ rk[0]; st[j][1] = c[j].y ^ rk[1]; st[j][2] = c[j].z ^ rk[2]; st[j][3] = c[j].w ^ rk[3];
     }
     AES_ROUNDS_PIPELINED(kBlk, st, rk)
-    uint4* ds = reinterpret_cast<uint4*>(dst + dof);
 #pragma unroll
     for (int j = 0; j < kBlk; ++j) {
       uint32_t o0, o1, o2, o3;
       AES_FINAL(st[j][0], st[j][1], st[j][2], st[j][3], o0, o1, o2, o3, rk + 40, pv[j])
       const uint4 p = make_uint4(o0, o1, o2, o3);
       const int64_t b = b0 + 64 * j;
-      if (b < nblk) ds[b] = p;
+      const v4u pw = {o0, o1, o2, o3};  // a store past the segment's end is dropped by the range check
+      __builtin_amdgcn_raw_buffer_store_b128(pw, d_rsrc, static_cast<uint32_t>(b) << 4, 0, 0);
       if constexpr (kHdr == 1) {  // does packet q = ceil(16 b / 188) start in this block?
         const uint32_t b16 = static_cast<uint32_t>(b) << 4;
         const uint32_t q = __umulhi(b16 + 187u, kDiv188Magic) >> 7;

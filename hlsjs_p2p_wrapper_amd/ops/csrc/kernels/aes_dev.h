@@ -50,12 +50,22 @@ constexpr uint32_t kIsRegion = 0x20000u;
     s[3] = AES_XOR3(AES_XOR3(v[12], v[13], v[14]), v[15], (k)[3]);                                                \
   } while (0)
 
-// final round fused with the CBC chaining: o = InvShiftRows/InvSubBytes(s) ^ k ^ px
-#define AES_FINAL(s0, s1, s2, s3, o0, o1, o2, o3, k, px)                                                          \
-  o0 = AES_XOR3(AES_IS(s0, 0) | (AES_IS(s3, 1) << 8) | (AES_IS(s2, 2) << 16) | (AES_IS(s1, 3) << 24), (k)[0], (px).x); \
-  o1 = AES_XOR3(AES_IS(s1, 0) | (AES_IS(s0, 1) << 8) | (AES_IS(s3, 2) << 16) | (AES_IS(s2, 3) << 24), (k)[1], (px).y); \
-  o2 = AES_XOR3(AES_IS(s2, 0) | (AES_IS(s1, 1) << 8) | (AES_IS(s0, 2) << 16) | (AES_IS(s3, 3) << 24), (k)[2], (px).z); \
-  o3 = AES_XOR3(AES_IS(s3, 0) | (AES_IS(s2, 1) << 8) | (AES_IS(s1, 2) << 16) | (AES_IS(s0, 3) << 24), (k)[3], (px).w);
+// final round fused with the CBC chaining: o = InvShiftRows/InvSubBytes(s) ^ k ^ px.  The
+// InvSbox image is replicated (every byte of a row's dwords holds InvSbox[x]): two v_perm pick the four output bytes into disjoint byte lanes, one
+// 3-input XOR merges them with the round key, one XOR applies the CBC chaining input
+#define AES_FINAL(s0, s1, s2, s3, o0, o1, o2, o3, k, px)                                                      \
+  o0 = __builtin_amdgcn_bitop3_b32(__builtin_amdgcn_perm(AES_IS(s3, 1), AES_IS(s0, 0), 0x0c0c0500u),               \
+                                   __builtin_amdgcn_perm(AES_IS(s1, 3), AES_IS(s2, 2), 0x07020c0cu), (k)[0], 0x96) ^ \
+       (px).x;                                                                                                    \
+  o1 = __builtin_amdgcn_bitop3_b32(__builtin_amdgcn_perm(AES_IS(s0, 1), AES_IS(s1, 0), 0x0c0c0500u),               \
+                                   __builtin_amdgcn_perm(AES_IS(s2, 3), AES_IS(s3, 2), 0x07020c0cu), (k)[1], 0x96) ^ \
+       (px).y;                                                                                                    \
+  o2 = __builtin_amdgcn_bitop3_b32(__builtin_amdgcn_perm(AES_IS(s1, 1), AES_IS(s2, 0), 0x0c0c0500u),               \
+                                   __builtin_amdgcn_perm(AES_IS(s3, 3), AES_IS(s0, 2), 0x07020c0cu), (k)[2], 0x96) ^ \
+       (px).z;                                                                                                    \
+  o3 = __builtin_amdgcn_bitop3_b32(__builtin_amdgcn_perm(AES_IS(s2, 1), AES_IS(s3, 0), 0x0c0c0500u),               \
+                                   __builtin_amdgcn_perm(AES_IS(s0, 3), AES_IS(s1, 2), 0x07020c0cu), (k)[3], 0x96) ^ \
+       (px).w;
 
 // Rounds 1..9 of N independent chains, software-pipelined IN SOURCE ORDER (the backend keeps
 // the unrolled block in emission order): chain j's 16 LDS reads are issued before chain
@@ -92,7 +102,7 @@ __device__ __forceinline__ void aes_image_fill(uint32_t* s_tab, const uint32_t* 
     s_tab[tid + k * kAesImageThreads] = rot ? __builtin_amdgcn_alignbit(v, v, 32 - rot) : v;
   }
 #pragma unroll
-  for (int k = 0; k < 8; ++k) s_tab[kTdDwords + tid + k * kAesImageThreads] = is[k];
+  for (int k = 0; k < 8; ++k) s_tab[kTdDwords + tid + k * kAesImageThreads] = is[k] * 0x01010101u;
 }
 
 // Per-lane image bases: Td address of entry x for lane l = (region << 16) | (x << 8) |

@@ -162,7 +162,10 @@ py::tuple transmux_launch(Tensor src, I64 src_off, I64 nbytes, py::array_t<uint8
   for (int64_t i = 0; i < B; ++i) {
     TORCH_CHECK_VALUE(so[i] >= 0 && nb[i] >= 0 && so[i] + nb[i] <= cap_src, "payload out of bounds");
     TORCH_CHECK_VALUE(so[i] % 16 == 0, "payload offsets must be 16-byte aligned");
-    if (en[i]) TORCH_CHECK_VALUE(nb[i] >= 16 && nb[i] % 16 == 0, "encrypted payload is not a positive multiple of 16");
+    if (en[i]) {
+      TORCH_CHECK_VALUE(nb[i] >= 16 && nb[i] % 16 == 0, "encrypted payload is not a positive multiple of 16");
+      TORCH_CHECK_VALUE(nb[i] < (int64_t(1) << 31), "encrypted payload over 2 GiB (the decrypt's buffer ranges)");
+    }
   }
   const auto dev_opts = torch::TensorOptions().device(torch::kCUDA, device);
   hipStream_t st = c10::hip::getCurrentHIPStream(device).stream();
