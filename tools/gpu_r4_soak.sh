@@ -5,7 +5,7 @@ set -eo pipefail
 R=$GRAFT_REPO_ROOT
 cd $R
 export PYTHONPATH=$R
-O=gpurun_out/r4_soak
+O=gpurun_out/${SOAK_OUT:-r4_soak}
 mkdir -p $O
 timeout -k 10 300 python bench.py --steps 2000 --warmup 10 --verbose > $O/headline_2000.log 2>&1
 timeout -k 10 400 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 \
