@@ -53,6 +53,10 @@ log = logging.getLogger("hlsjs_p2p_wrapper_amd.node")
 
 MAGIC = 0x48505032  # "HPP2"
 HDR = 16
+# a rank whose CDN copies keep its ingest link busy for more than this share of its rounds
+# reports FLAG_CDN_BOUND (the planner's CDN balance relieves only such ranks): a PCIe-origin
+# leader measures ~0.96, the HBM-origin rehearsal's leader ~0.2 (profiles/r4_balance)
+CDN_BOUND_BUSY = 0.6
 ALIGN = 256
 SLACK = 4096
 PIN_DELAY_ROUNDS = 2  # delivered segments stay pinned this many launches (consumers run async)
@@ -274,7 +278,14 @@ class SwarmNode:
         # batch that decrypts it computes the CRC on the way (kernels/aes_cbc.hip AesCrc).  The
         # entry stays pending -- pinned, not announced, not served -- until verify_done.
         self.verify_deferred = False
-        self.cdn_balance = os.environ.get("HLSP2P_CDN_BALANCE", "0") == "1"  # opt-in (plan_round_into)
+        # planner CDN balance (plan_round_into), opt-in (HLSP2P_CDN_BALANCE=1; measured in
+        # profiles/r4_balance): this rank reports FLAG_CDN_BOUND while its CDN copies keep its
+        # ingest link busy (`_cdn_busy`, an average over rounds of the copy time per round
+        # interval), and the plan then holds its lone wants back once when another rank is about
+        # to want them
+        self.cdn_balance = os.environ.get("HLSP2P_CDN_BALANCE", "0") == "1"
+        self._cdn_busy = 0.0
+        self._cdn_t = None
         # entries waiting for a deferred check, by entry id: flag + want info row (a CDN retry's source)
         self._vflag = np.zeros(0, dtype=bool)
         self._vinfo = np.zeros((0, 10), dtype=np.int64)
@@ -346,6 +357,8 @@ class SwarmNode:
             f |= self.rt.FLAG_DOWNLOAD
         if self.cdn_dedup:
             f |= self.rt.FLAG_CDN_DEDUP
+        if self.cdn_balance and self._cdn_busy > CDN_BOUND_BUSY:
+            f |= self.rt.FLAG_CDN_BOUND
         return f
 
     def pending(self) -> int:
@@ -957,6 +970,11 @@ class SwarmNode:
         self.timer.add("commit", t2 - t1)
         self.timer.add("deliver", time.perf_counter() - t2)
         self.timer.add("dev_cdn_ms", h.cdn_ms / 1e3)
+        now = time.perf_counter()
+        if self._cdn_t is not None and now > self._cdn_t:  # busy share of the ingest link, averaged
+            busy = min(1.0, h.cdn_ms / 1e3 / (now - self._cdn_t))
+            self._cdn_busy += 0.2 * (busy - self._cdn_busy)
+        self._cdn_t = now
         self.timer.add("dev_p2p_ms", h.p2p_ms / 1e3)
         self.last_round = {"wants": h.n_wants, "cdn": 0 if h.cdn is None else len(h.cdn[0]), "send": h.n_send,
                            "recv": 0 if h.recv is None else len(h.recv[0]), "cdn_ms": h.cdn_ms, "dmas": h.dmas,

@@ -787,4 +787,5 @@ PYBIND11_MODULE(_runtime, m) {
   m.attr("FLAG_UPLOAD") = int64_t(kUploadOn);
   m.attr("FLAG_DOWNLOAD") = int64_t(kDownloadOn);
   m.attr("FLAG_CDN_DEDUP") = int64_t(kCdnDedup);
+  m.attr("FLAG_CDN_BOUND") = int64_t(kCdnBound);
 }

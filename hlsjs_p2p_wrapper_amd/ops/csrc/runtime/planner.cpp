@@ -217,8 +217,9 @@ void plan_round_into(const Directory& dir, const Want* wants_in, size_t n_in, co
         ++active;
       }
     if (active > 1 && total >= kBalanceMinBytes)
-      for (int r = 0; r < world; ++r)  // share > 1.1 / active
-        if (flag(r, kOnline) && cdn_bytes[r] * 10 * active > total * 11) over_share |= uint64_t(1) << r;
+      for (int r = 0; r < world; ++r)  // share > 1.1 / active, and the rank's link is its bound
+        if (flag(r, kOnline) && flag(r, kCdnBound) && cdn_bytes[r] * 10 * active > total * 11)
+          over_share |= uint64_t(1) << r;
   }
   // per track (swarm, level, url_id): each rank's first wanted sn this round (wants are in key
   // order, so the first want of a rank inside a track run has its smallest sn)

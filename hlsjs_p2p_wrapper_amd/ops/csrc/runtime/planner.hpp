@@ -35,7 +35,9 @@ namespace hlsp2p {
 
 constexpr int kMaxRanks = 64;
 
-enum RankFlag : int64_t { kOnline = 1, kUploadOn = 2, kDownloadOn = 4, kCdnDedup = 8 };
+// kCdnBound: the rank's CDN copies keep its ingest link busy most of the time (its link is the
+// bottleneck); only such a rank is relieved by the CDN balance (plan_round_into)
+enum RankFlag : int64_t { kOnline = 1, kUploadOn = 2, kDownloadOn = 4, kCdnDedup = 8, kCdnBound = 16 };
 
 struct DirEntry {
   uint64_t holders = 0;
@@ -118,11 +120,11 @@ std::vector<Transfer> plan_round(const Directory& dir, const std::vector<Want>& 
 // is held back one announcement when its wanter has fetched more than its share from the
 // CDN; the follower then fetches it alone and the leader takes the copy.  Ranks whose players
 // run a round apart never co-want a segment, so without this the rank ahead seeds the whole
-// swarm.  Opt-in (HLSP2P_CDN_BALANCE=1 on the node): a held want arrives a round later, and
-// measured on the rehearsal plane that latency cost 18.5 % with cheap ingest while the
-// PCIe-origin run gained nothing outside the spread; a leader that does become PCIe-bound
-// slows, its followers catch up and co-want, and the seeding quota splits the bytes anyway
-// (profiles/r4_balance/NOTES.md).
+// swarm.  Only a rank flagged kCdnBound is relieved: a held want arrives a round later, which
+// measured -18.5 % on the rehearsal plane when the leader's ingest was cheap (HBM origin).  The
+// node keeps the balance opt-in (HLSP2P_CDN_BALANCE=1): with the gate, the one-GPU rehearsals
+// still lost 7-13 % with a PCIe origin, where all ranks share one link and spreading the
+// fetches cannot add bandwidth (profiles/r4_balance/NOTES.md).
 void plan_round_into(const Directory& dir, const Want* wants, size_t n, const std::vector<int64_t>& rank_flags,
                      int world, std::vector<Transfer>* out, const int64_t* cdn_bytes = nullptr);
 

@@ -168,29 +168,32 @@ def test_planner_is_deterministic_and_balances_links(rt):
 def test_planner_cdn_balance_holds_a_leaders_lone_want_once(rt):
     """Ranks whose players run a round apart never want a segment in the same round, so the
     rank ahead would fetch every segment from the CDN and the others take its copies.  The
-    planner's CDN balance holds a lone, unheld want back once when its rank is over its share
-    of the swarm's CDN bytes and another rank already asks for an earlier segment of the same
-    track; the follower then fetches it itself, and the leader's copy comes from the follower."""
+    planner's CDN balance holds a lone, unheld want back once when its rank reports its ingest
+    link as its bound (FLAG_CDN_BOUND), is over its share of the swarm's CDN bytes, and another
+    rank already asks for an earlier segment of the same track; the follower then fetches it
+    itself, and the leader's copy comes from the follower."""
     d = rt.Directory()
     mb = 1 << 20
     w = wants([(10, 1000, 1, 0, 0), (9, 1000, 2, 1, 0)])  # rank 0 one segment ahead of rank 1
     cdn = lambda plan: sorted((int(r[3]), int(r[6])) for r in plan if r[5] == -1)  # noqa: E731
     assert cdn(rt.plan_round(d, w, flags(rt, 2), 2)) == [(9, 1), (10, 0)]  # no balance input
     skew = np.array([600 * mb, 100 * mb], dtype=np.int64)
-    assert cdn(rt.plan_round(d, w, flags(rt, 2), 2, skew)) == [(9, 1)]  # rank 0's sn 10 held
+    assert cdn(rt.plan_round(d, w, flags(rt, 2), 2, skew)) == [(9, 1), (10, 0)]  # rank 0's link is not its bound
+    full = rt.FLAG_ONLINE | rt.FLAG_UPLOAD | rt.FLAG_DOWNLOAD | rt.FLAG_CDN_DEDUP
+    bound = flags(rt, 2, r0=full | rt.FLAG_CDN_BOUND)
+    assert cdn(rt.plan_round(d, w, bound, 2, skew)) == [(9, 1)]  # CDN-bound and over its share: sn 10 held
     held = wants([(10, 1000, 1, 0, 8), (9, 1000, 2, 1, 0)])
-    assert cdn(rt.plan_round(d, held, flags(rt, 2), 2, skew)) == [(9, 1), (10, 0)]  # kHeld (8): at most once
+    assert cdn(rt.plan_round(d, held, bound, 2, skew)) == [(9, 1), (10, 0)]  # kHeld (8): at most once
     even = np.array([300 * mb, 290 * mb], dtype=np.int64)
-    assert cdn(rt.plan_round(d, w, flags(rt, 2), 2, even)) == [(9, 1), (10, 0)]  # within its share
+    assert cdn(rt.plan_round(d, w, bound, 2, even)) == [(9, 1), (10, 0)]  # within its share
     small = np.array([60 * mb, 10 * mb], dtype=np.int64)
-    assert cdn(rt.plan_round(d, w, flags(rt, 2), 2, small)) == [(9, 1), (10, 0)]  # start-up: no decision
+    assert cdn(rt.plan_round(d, w, bound, 2, small)) == [(9, 1), (10, 0)]  # start-up: no decision
     ahead = wants([(10, 1000, 1, 0, 0), (11, 1000, 2, 1, 0)])  # rank 1 is ahead, not following sn 10
-    assert cdn(rt.plan_round(d, ahead, flags(rt, 2), 2, skew)) == [(10, 0), (11, 1)]
-    assert cdn(rt.plan_round(d, w, flags(rt, 2, r1=rt.FLAG_ONLINE | rt.FLAG_UPLOAD | rt.FLAG_DOWNLOAD), 2,
-                             skew)) == [(9, 1), (10, 0)]  # follower not in the CDN dedup swarm
-    # rank flags, want order and the rest of the plan stay identical on every rank
-    assert np.array_equal(rt.plan_round(d, w, flags(rt, 2), 2, skew), rt.plan_round(d, w[::-1].copy(), flags(rt, 2), 2,
-                                                                                     skew))
+    assert cdn(rt.plan_round(d, ahead, bound, 2, skew)) == [(10, 0), (11, 1)]
+    nodedup = flags(rt, 2, r0=full | rt.FLAG_CDN_BOUND, r1=rt.FLAG_ONLINE | rt.FLAG_UPLOAD | rt.FLAG_DOWNLOAD)
+    assert cdn(rt.plan_round(d, w, nodedup, 2, skew)) == [(9, 1), (10, 0)]  # follower not in the CDN dedup swarm
+    # want order does not change the plan (every rank computes the same one)
+    assert np.array_equal(rt.plan_round(d, w, bound, 2, skew), rt.plan_round(d, w[::-1].copy(), bound, 2, skew))
 
 
 def test_planner_respects_flags(rt):

@@ -467,3 +467,35 @@ def test_agent_negotiates_the_live_buffer_margin():
     agent = _agent_of(seen[0])
     assert out[0]["ok"] and agent.is_live is False and agent.live_buffer_level is None
     assert agent.player.hls.config.maxBufferLength == 30  # the wrapper default, untouched
+
+
+def test_node_reports_a_saturated_ingest_link_to_the_planner(monkeypatch):
+    """FLAG_CDN_BOUND (the planner's CDN balance relieves only such ranks) follows the share of
+    the rank's rounds its CDN copies keep the ingest link busy, averaged over rounds, and is
+    only ever set with the balance on (HLSP2P_CDN_BALANCE=1; off by default)."""
+    from hlsjs_p2p_wrapper_amd.agent import node as node_mod
+    from hlsjs_p2p_wrapper_amd.agent.node import RoundHandle, SwarmNode
+
+    assert not SwarmNode(device="cpu", cache_bytes=64 << 10, loop=new_event_loop("virtual"),
+                         auto_tick=False).cdn_balance
+    monkeypatch.setenv("HLSP2P_CDN_BALANCE", "1")
+    node = SwarmNode(device="cpu", cache_bytes=64 << 10, loop=new_event_loop("virtual"), auto_tick=False)
+    bound = node.rt.FLAG_CDN_BOUND
+    assert not node.flags & bound
+    clock = [100.0]
+    monkeypatch.setattr(node_mod.time, "perf_counter", lambda: clock[0])
+    for _ in range(20):  # 10 ms rounds, 9.6 ms of CDN copies each: a saturated link
+        clock[0] += 0.010
+        h = RoundHandle(node.round, np.zeros(0, dtype=np.int64), t0=clock[0])
+        h.empty, h.cdn_ms = False, 9.6
+        node.complete_round(h)
+    assert node._cdn_busy > node_mod.CDN_BOUND_BUSY and node.flags & bound
+    for _ in range(20):  # 2 ms of copies per 10 ms round (an HBM origin): the flag clears
+        clock[0] += 0.010
+        h = RoundHandle(node.round, np.zeros(0, dtype=np.int64), t0=clock[0])
+        h.empty, h.cdn_ms = False, 2.0
+        node.complete_round(h)
+    assert not node.flags & bound
+    node._cdn_busy = 0.95
+    node.cdn_balance = False
+    assert not node.flags & bound

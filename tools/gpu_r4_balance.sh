@@ -5,7 +5,7 @@ set -eo pipefail
 R=$GRAFT_REPO_ROOT
 cd $R
 export PYTHONPATH=$R
-O=gpurun_out/r4_balance
+O=gpurun_out/${BAL_OUT:-r4_balance}
 mkdir -p $O
 run() {  # name, nproc, port, balance, extra args...
   local name=$1 n=$2 port=$3 bal=$4; shift 4
