@@ -52,7 +52,12 @@ def save_cache(node, path: str) -> Dict[str, int]:
 
         _seg.copy_segments(node.arena, staged, offs_src, offs, lens)
         data.copy_(staged)
-        crcs = node.crc_dev[torch.from_numpy(ids).to(node.device)].cpu()
+        if getattr(node, "ingest_crc", True):
+            crcs = node.crc_dev[torch.from_numpy(ids).to(node.device)].cpu()
+        else:  # a one-rank node keeps no CRC table: compute the CRCs the restore verifies
+            from ..ops import crc as _crc
+
+            crcs = _crc.crc32_batch(staged, offs.tolist(), lens.tolist())[0].cpu()
     else:
         crcs = torch.zeros(0, dtype=torch.int32)
     save_file({"keys": torch.from_numpy(np.ascontiguousarray(keys, dtype=np.int64)),

@@ -184,6 +184,10 @@ class SwarmNode:
         self.comm = comm or LocalComm()
         self.rank = self.comm.rank
         self.world = self.comm.world_size
+        # The ingest CRC of a CDN fetch only produces the trailer a peer's receive check compares
+        # against (the CDN sends none).  A one-rank swarm never sends, so it skips that pass
+        # (HLSP2P_INGEST_CRC=1 forces it; agent/checkpoint.py computes the CRCs it saves then).
+        self.ingest_crc = self.world > 1 or os.environ.get("HLSP2P_INGEST_CRC", "0") == "1"
         if device in (None, "auto"):
             device = torch.device("cuda", torch.cuda.current_device()) if torch.cuda.is_available() else "cpu"
         self.device = torch.device(device)
@@ -1118,7 +1122,8 @@ class SwarmNode:
         for i in corrupt.tolist():
             if lens[i]:
                 self.arena[int(offs[i]) + int(lens[i]) // 2] ^= 0xFF
-        _crc.crc32_batch(self.arena, offs, lens, scatter_to=self.crc_dev, scatter_idx=eids)  # ingest CRCs
+        if self.ingest_crc:  # the trailers this rank's sends carry
+            _crc.crc32_batch(self.arena, offs, lens, scatter_to=self.crc_dev, scatter_idx=eids)
         self.store.commit(eids)  # announced next round; peers' reads are stream-ordered after the H2D
         # CDN bandwidth shaping (xhr-shaper analog): completions are deferred by the modelled
         # transfer time of this round's CDN bytes

@@ -72,3 +72,17 @@ def test_checkpoint_rejects_foreign_files(tmp_path):
     node = SwarmNode(device="cpu", cache_bytes=1 << 20, loop=new_event_loop("virtual"))
     with pytest.raises(ValueError, match="not a segment-cache checkpoint"):
         node.load_cache(p)
+
+
+def test_one_rank_node_skips_the_ingest_crc(monkeypatch):
+    """The ingest CRC only produces the trailers peers check; a one-rank swarm never sends, so
+    it skips the pass (the checkpoint above then computes the CRCs it saves), a multi-rank
+    node keeps it, and HLSP2P_INGEST_CRC=1 forces it."""
+    from hlsjs_p2p_wrapper_amd.parallel import ThreadHub
+
+    loop = new_event_loop("virtual")
+    assert not SwarmNode(device="cpu", cache_bytes=1 << 20, loop=loop, auto_tick=False).ingest_crc
+    hub = ThreadHub(2)
+    assert SwarmNode(hub.comm(0), device="cpu", cache_bytes=1 << 20, loop=loop, auto_tick=False).ingest_crc
+    monkeypatch.setenv("HLSP2P_INGEST_CRC", "1")
+    assert SwarmNode(device="cpu", cache_bytes=1 << 20, loop=loop, auto_tick=False).ingest_crc
