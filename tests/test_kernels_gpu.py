@@ -83,6 +83,11 @@ def test_aes_cbc_decrypt_matches_host(cuda):
     for i, p in enumerate(plains):
         assert out_len[i] == len(p)
         assert np.array_equal(host[offs[i]:offs[i] + len(p)], p)
+    # nothing written past a segment's ciphertext: the kernel's buffer ranges drop the stores of
+    # the blocks beyond each segment's end (the last chunk of a segment is partial)
+    ends = [o + len(c) for o, c in zip(offs, cts)]
+    for e, nxt in zip(ends, offs[1:] + [pos]):
+        assert not host[e:nxt].any()
     # wrong key -> padding check fails (overwhelmingly likely)
     bad = aes.cbc_decrypt_batch(s, offs[-1:], [len(cts[-1])], [bytes(16)], ivs[-1:], d, offs[-1:])
     assert int(bad.cpu()[0]) == -1 or not np.array_equal(d.cpu().numpy()[offs[-1]:offs[-1] + 64], plains[-1][:64])
