@@ -685,6 +685,9 @@ def _fleet(args, world, rank, device, use_gpu, node, origin, players, desc, encr
         # how received segments were checked: by the CRC fused into the transmux decrypt
         # (deferred, fleet default) or by the node's own verify pass before delivery
         result["config"]["receive_verify"] = "fused-decrypt" if getattr(node, "verify_deferred", False) else "node"
+        # whether CDN fetches get the CRC trailer peers check (a one-rank swarm sends nothing, so
+        # it skips that pass; the headline is the same with it forced: profiles/r4_ingestcrc)
+        result["config"]["ingest_crc"] = bool(getattr(node, "ingest_crc", True))
         result["data_plane"] = _plane_info(node)
         if live:
             result["config"].update(live=True, live_speed=args.live_speed, live_window=args.live_window,

@@ -240,6 +240,7 @@ def test_bench_fleet_payloads_two_ranks():
     assert res["errors"] == 0 and res["value"] > 0
     _check_per_rank(res, 2)
     assert all(r["payload_GBps"] > 0 for r in res["per_rank"])
+    assert res["config"]["ingest_crc"]  # ranks with peers compute the trailers their sends carry
 
 
 def test_ipc_outbox_slots_follow_the_packing_order():
