@@ -33,9 +33,21 @@ def tune_gc(gen0_threshold: int = 50_000) -> Tuple[int, int, int]:
     # no cyclic garbage (host peak is the same with the GC off over 3000 steps,
     # profiles/r2_soak), so run them 10x less often than the default
     gc.set_threshold(gen0_threshold, prev[1], max(prev[2], 100))
+    # State that builds up while a peer runs (buffered fragments, delivered-segment records)
+    # would make every later full pass longer: over 3,000 HBM-origin bench steps the step time
+    # drifted +16 % with the GC on and stayed flat with it off (profiles/r4_gc).  Freezing what
+    # survives each full pass keeps the next one proportional to what is new since.
+    if _freeze_after_full not in gc.callbacks:
+        gc.callbacks.append(_freeze_after_full)
     if os.environ.get("HLSP2P_GC_DISABLE") == "1":  # diagnostic: no cyclic GC after start-up at all
         gc.disable()
     return prev
+
+
+def _freeze_after_full(phase: str, info: dict) -> None:
+    """gc callback: move the survivors of a full (gen-2) collection to the permanent generation."""
+    if phase == "stop" and info.get("generation") == 2:
+        gc.freeze()
 
 
 def cpu_calibration_us(n: int = 20_000, reps: int = 3) -> float:

@@ -12,7 +12,19 @@ def test_tune_gc_freezes_and_raises_gen0():
     try:
         out = rt.tune_gc(12345)
         assert out == prev and gc.get_threshold()[0] == 12345 and gc.get_freeze_count() > 0
+        # survivors of every later full collection are frozen too (long runs stay flat)
+        kept = [[i] for i in range(1000)]
+        before = gc.get_freeze_count()
+        gc.collect(2)
+        assert gc.get_freeze_count() >= before + len(kept)
+        # cyclic garbage is still collected
+        a = []
+        a.append(a)
+        del a
+        assert gc.collect(0) >= 1
     finally:
+        if rt._freeze_after_full in gc.callbacks:
+            gc.callbacks.remove(rt._freeze_after_full)
         gc.unfreeze()
         gc.set_threshold(*prev)
 
