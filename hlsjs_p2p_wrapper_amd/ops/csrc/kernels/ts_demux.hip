@@ -137,14 +137,25 @@ __device__ __forceinline__ uint32_t pack_meta(int c, int ps, int len, int pes) {
 }
 
 // ---------------------------------------------------------------- 2. scan
-// inclusive wave prefix sum (wave64)
-__device__ __forceinline__ int wave_incl_scan(int v, int lane) {
-#pragma unroll
-  for (int o = 1; o < 64; o <<= 1) {
-    const int t = __shfl_up(v, o);
-    if (lane >= o) v += t;
-  }
+// Inclusive prefix sum over the wave64 in six DPP-modified moves and adds, no LDS traffic
+// (a __shfl_up ladder is six ds_bpermute round trips): row_shr:1/2/4/8 scan each 16-lane row
+// (bound_ctrl fills 0 past the row start), row_bcast:15 adds row 0's / row 2's total to rows 1
+// and 3, row_bcast:31 adds rows 0-1's total to rows 2 and 3.
+__device__ __forceinline__ uint32_t wave_scan_dpp(uint32_t v) {
+  v += static_cast<uint32_t>(__builtin_amdgcn_update_dpp(0, static_cast<int>(v), 0x111, 0xf, 0xf, true));
+  v += static_cast<uint32_t>(__builtin_amdgcn_update_dpp(0, static_cast<int>(v), 0x112, 0xf, 0xf, true));
+  v += static_cast<uint32_t>(__builtin_amdgcn_update_dpp(0, static_cast<int>(v), 0x114, 0xf, 0xf, true));
+  v += static_cast<uint32_t>(__builtin_amdgcn_update_dpp(0, static_cast<int>(v), 0x118, 0xf, 0xf, true));
+  v += static_cast<uint32_t>(__builtin_amdgcn_update_dpp(0, static_cast<int>(v), 0x142, 0xa, 0xf, false));
+  v += static_cast<uint32_t>(__builtin_amdgcn_update_dpp(0, static_cast<int>(v), 0x143, 0xc, 0xf, false));
   return v;
+}
+// the wave's total (lane 63 of the inclusive scan), wave-uniform
+__device__ __forceinline__ uint32_t wave_sum_dpp(uint32_t v) {
+  return static_cast<uint32_t>(__builtin_amdgcn_readlane(static_cast<int>(wave_scan_dpp(v)), 63));
+}
+__device__ __forceinline__ int wave_incl_scan(int v, int /*lane*/) {
+  return static_cast<int>(wave_scan_dpp(static_cast<uint32_t>(v)));
 }
 
 // hdr_rec / hdr_off (optional, from the decrypt: aes_cbc.hip AesHdr): record p of a segment is
@@ -275,12 +286,10 @@ __global__ __launch_bounds__(kTsThreads) void ts_scan_kernel(
     // LDS atomic per wave per class
 #pragma unroll
     for (int k = 0; k < kClasses; ++k) {
-      int v = (c == k) ? (len | (pes << 16)) : 0;
-#pragma unroll
-      for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
+      const uint32_t v = wave_sum_dpp((c == k) ? static_cast<uint32_t>(len | (pes << 16)) : 0u);
       if ((tid & 63) == 0 && v) {
-        atomicAdd(&s_sum[u][2 * k], v & 0xffff);
-        atomicAdd(&s_sum[u][2 * k + 1], v >> 16);
+        atomicAdd(&s_sum[u][2 * k], static_cast<int>(v & 0xffff));
+        atomicAdd(&s_sum[u][2 * k + 1], static_cast<int>(v >> 16));
       }
     }
     if (err) atomicOr(&s_err[u], err);
@@ -398,15 +407,9 @@ __global__ __launch_bounds__(kTsThreads) void ts_gather_kernel(
   uint32_t sA = (c == 0 ? lb : 0u) | ((c == 1 ? lb : 0u) << 16);
   uint32_t sB = (c == 2 ? lb : 0u) | ((c == 0 ? pf : 0u) << 16) | ((c == 1 ? pf : 0u) << 24);
   uint32_t sC = c == 2 ? pf : 0u;
-#pragma unroll
-  for (int o = 1; o < 64; o <<= 1) {
-    const uint32_t tA = __shfl_up(sA, o), tB = __shfl_up(sB, o), tC = __shfl_up(sC, o);
-    if (lane >= o) {
-      sA += tA;
-      sB += tB;
-      sC += tC;
-    }
-  }
+  sA = wave_scan_dpp(sA);
+  sB = wave_scan_dpp(sB);
+  sC = wave_scan_dpp(sC);
   if (lane == 63) {
     s_wave[wave][0] = sA;
     s_wave[wave][1] = sB;
