@@ -224,6 +224,43 @@ __global__ __launch_bounds__(kTsThreads) void ts_scan_kernel(
       }
     }
   }
+  // The bytes a packet's parse needs beyond its header record, loaded for every block before the
+  // first block is parsed (issued per block inside the parse they were 2-3 dependent round trips
+  // per block): byte 4 when the record does not hold it and an adaptation field is present,
+  // then, for a payload-unit start, the PES header's first 20 bytes as 6 dwords realigned in
+  // registers (dwords past the packet read as 0; the parse never uses bytes past its length).
+  int b4v[kScanBlocks];
+#pragma unroll
+  for (int u = 0; u < kScanBlocks; ++u) {
+    b4v[u] = 0;
+    if (pks[u] >= 0) {
+      const uint32_t hdr = pkt[u].hdr;
+      const int afc = (hdr >> 28) & 3;
+      b4v[u] = pkt[u].b4 >= 0 ? pkt[u].b4 : ((afc & 2) ? static_cast<int>(pp[u][4]) : 0);
+    }
+  }
+  uint32_t hw[kScanBlocks][5];
+#pragma unroll
+  for (int u = 0; u < kScanBlocks; ++u) {
+#pragma unroll
+    for (int k = 0; k < 5; ++k) hw[u][k] = 0;
+    if (pks[u] >= 0) {
+      const uint32_t hdr = pkt[u].hdr;
+      const int afc = (hdr >> 28) & 3, b1 = (hdr >> 8) & 0xff;
+      const int s0 = 4 + ((afc & 2) ? 1 + b4v[u] : 0);
+      if ((hdr & 0xff) == 0x47 && (b1 & 0x40) && (afc & 1) && s0 + 9 <= kPkt) {
+        const uint8_t* h = pp[u] + s0;
+        const uint32_t* w = reinterpret_cast<const uint32_t*>(reinterpret_cast<uintptr_t>(h) & ~uintptr_t(3));
+        const uint32_t* wend = reinterpret_cast<const uint32_t*>(pp[u] + kPkt);  // packets are 4-byte aligned
+        uint32_t d[6];
+#pragma unroll
+        for (int k = 0; k < 6; ++k) d[k] = w + k < wend ? w[k] : 0u;
+        const uint32_t mis = static_cast<uint32_t>(reinterpret_cast<uintptr_t>(h) & 3);
+#pragma unroll
+        for (int k = 0; k < 5; ++k) hw[u][k] = __builtin_amdgcn_alignbyte(d[k + 1], d[k], mis);
+      }
+    }
+  }
   __syncthreads();
   int cur = -1, cpid0 = -1, cpid1 = -1, cpid2 = -1;
 #pragma unroll
@@ -240,7 +277,6 @@ __global__ __launch_bounds__(kTsThreads) void ts_scan_kernel(
     int c = 3, ps = 0, len = 0, pes = 0;
     int err = 0;
     if (pks[u] >= 0) {
-      const uint8_t* p = pp[u];
       const uint32_t hdr = pkt[u].hdr;
       const int sync = hdr & 0xff;
       const int b1 = (hdr >> 8) & 0xff, b2 = (hdr >> 16) & 0xff, b3 = hdr >> 24;
@@ -251,26 +287,34 @@ __global__ __launch_bounds__(kTsThreads) void ts_scan_kernel(
         const int cls = (cpid0 >= 0 && pid == cpid0) ? 0 : (cpid1 >= 0 && pid == cpid1) ? 1 : (cpid2 >= 0 && pid == cpid2) ? 2 : 3;
         const int afc = (b3 >> 4) & 3;
         if (cls < 3 && (afc & 1)) {
-          int s = 4 + ((afc & 2) ? 1 + (pkt[u].b4 >= 0 ? pkt[u].b4 : p[4]) : 0);
+          int s = 4 + ((afc & 2) ? 1 + b4v[u] : 0);
           if (s > kPkt) {
             err |= static_cast<int>(kBadLength);
           } else {
             int l = kPkt - s;
             bool ok = true;
             if (b1 & 0x40) {
-              const uint8_t* h = p + s;
-              if (l < 9 || h[0] != 0 || h[1] != 0 || h[2] != 1 || 9 + h[8] > l) {
+#define HB(i) static_cast<int>((hw[u][(i) >> 2] >> (8 * ((i) & 3))) & 0xffu)
+              if (l < 9 || HB(0) != 0 || HB(1) != 0 || HB(2) != 1 || 9 + HB(8) > l) {
                 err |= static_cast<int>(kPesHeaderError);
                 ok = false;
               } else {
-                const int64_t pts = ((h[7] & 0x80) && l >= 14) ? read_pts(h + 9) : -1;
-                const int64_t dts = ((h[7] & 0xC0) == 0xC0 && l >= 19) ? read_pts(h + 14) : -1;
+                const int f7 = HB(7);
+                const int64_t pts = ((f7 & 0x80) && l >= 14)
+                                        ? (int64_t((HB(9) >> 1) & 0x07) << 30) | (int64_t(HB(10)) << 22) |
+                                              (int64_t(HB(11) >> 1) << 15) | (int64_t(HB(12)) << 7) | int64_t(HB(13) >> 1)
+                                        : -1;
+                const int64_t dts = ((f7 & 0xC0) == 0xC0 && l >= 19)
+                                        ? (int64_t((HB(14) >> 1) & 0x07) << 30) | (int64_t(HB(15)) << 22) |
+                                              (int64_t(HB(16) >> 1) << 15) | (int64_t(HB(17)) << 7) | int64_t(HB(18) >> 1)
+                                        : -1;
                 pts_dts[2 * gpk] = pts;
                 pts_dts[2 * gpk + 1] = dts;
                 pes = 1;
-                s += 9 + h[8];
-                l -= 9 + h[8];
+                s += 9 + HB(8);
+                l -= 9 + HB(8);
               }
+#undef HB
             }
             if (ok) {
               c = cls;

@@ -5,7 +5,7 @@ set -eo pipefail
 R=$GRAFT_REPO_ROOT
 cd $R
 export PYTHONPATH=$R
-O=gpurun_out/r4_dpp
+O=gpurun_out/${DPP_OUT:-r4_dpp}
 mkdir -p $O
 timeout -k 10 300 python -u -m pytest tests/test_transmux.py tests/test_kernels_gpu.py tests/test_torch_ops.py tests/test_fleet.py -x -v -m gpu --timeout 200 --timeout-method thread -p no:cacheprovider > $O/tests.log 2>&1
 for i in 1 2; do
