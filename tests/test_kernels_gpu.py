@@ -119,6 +119,108 @@ def test_ts_demux_matches_cpu_oracle(cuda):
         assert ci[i, 0] == 0
 
 
+def _damaged_segments():
+    """TS segments with damage on the parse's error paths: adaptation-field lengths (byte 4) up
+    to past the packet, broken PES start codes and header lengths, PES headers that run to the
+    packet end, and lost sync bytes."""
+    rng = np.random.default_rng(7)
+    segs = []
+    for i in range(6):
+        seg, _ = tsdemux.mux_segment(target_bytes=300_000, with_id3=bool(i & 1), seed=40 + i, sn=i, start_time=4.0 * i)
+        seg = np.frombuffer(seg, np.uint8).copy()
+        pk = seg.reshape(-1, 188)
+        n = len(pk)
+        adapt = np.flatnonzero((pk[:, 3] & 0x20) != 0)
+        pusi = np.flatnonzero((pk[:, 1] & 0x40) != 0)
+        if i >= 1 and len(adapt):  # adaptation lengths: random, the largest legal, past the packet
+            for j in rng.choice(adapt, min(20, len(adapt)), replace=False):
+                pk[j, 4] = rng.choice([0, 1, 182, 183, 184, 200, int(rng.integers(0, 256))])
+        if i >= 2 and len(pusi):  # PES start code / header length damaged
+            for j in rng.choice(pusi, min(12, len(pusi)), replace=False):
+                s0 = 4 + (1 + int(pk[j, 4]) if pk[j, 3] & 0x20 else 0)
+                if s0 + 9 <= 188:
+                    pk[j, s0 + int(rng.integers(0, 3))] ^= 0xFF if rng.random() < 0.5 else 0
+                    if rng.random() < 0.5:
+                        pk[j, s0 + 8] = int(rng.integers(0, 256))
+        if i >= 3:  # PES headers pushed to the end of their packet
+            for j in rng.choice(pusi, min(8, len(pusi)), replace=False) if len(pusi) else []:
+                pk[j, 3] |= 0x20
+                pk[j, 4] = int(rng.integers(160, 184))
+        if i >= 4:  # lost sync
+            for j in rng.choice(n, 5, replace=False):
+                pk[j, 0] = 0x46
+        segs.append(seg.tobytes())
+    return segs
+
+
+def test_ts_demux_matches_cpu_oracle_on_damaged_streams(cuda):
+    """Damaged packets take the kernels' error paths exactly as the CPU oracle does."""
+    segs = _damaged_segments()
+    offs, pos = [], 0
+    for sg in segs:
+        offs.append(pos)
+        pos += (len(sg) + 255) // 256 * 256
+    buf = np.zeros(pos + 256, np.uint8)
+    for o, sg in zip(offs, segs):
+        buf[o:o + len(sg)] = np.frombuffer(sg, np.uint8)
+    lens = [len(sg) for sg in segs]
+    cpu = tsdemux.demux_batch(torch.from_numpy(buf), offs, lens, torch.zeros(pos + 256, dtype=torch.uint8), offs)
+    g_es = torch.zeros(pos + 256, dtype=torch.uint8, device=cuda)
+    gpu = tsdemux.demux_batch(torch.from_numpy(buf).to(cuda), offs, lens, g_es, offs)
+    assert torch.equal(gpu.info.cpu(), cpu.info)
+    assert torch.equal(gpu.pes.cpu(), cpu.pes)
+    ci = cpu.info.numpy()
+    assert (ci[1:, 0] != 0).any()  # the damage reached the error paths
+    for i, o in enumerate(offs):
+        n = int(ci[i, 14])
+        assert torch.equal(g_es[o:o + n].cpu(), cpu.es[o:o + n])
+
+
+def test_transmux_with_header_records_matches_cpu_oracle_on_damaged_streams(cuda):
+    """The same damage through the encrypted transmux batch, where the scan takes its packet
+    headers (and byte 4, unless the header sits at byte 12 of its block) from the records the
+    decrypt writes: info rows, PES tables and ES bytes equal the CPU oracle on the plaintext."""
+    from hlsjs_p2p_wrapper_amd.ops._native import device
+
+    segs = _damaged_segments()
+    key = bytes(range(16, 32))
+    cts = [aes.cbc_encrypt(key, aes.iv_from_sn(100 + i), np.frombuffer(sg, np.uint8)) for i, sg in enumerate(segs)]
+    offs, pos = [], 0
+    for c in cts:
+        offs.append(pos)
+        pos += (len(c) + 255) // 256 * 256
+    src = np.zeros(pos + 256, np.uint8)
+    for o, c in zip(offs, cts):
+        src[o:o + len(c)] = c
+    B = len(cts)
+    td0, isb = aes.device_tables(cuda)
+    drk = np.tile(aes.round_keys_le(key), (B, 1)).astype(np.uint32)
+    iv = np.stack([np.frombuffer(aes.iv_from_sn(100 + i), np.uint8) for i in range(B)])
+    groups, keep, _, _ = device().transmux_launch(torch.from_numpy(src).to(cuda), np.asarray(offs, np.int64),
+                                                  np.asarray([len(c) for c in cts], np.int64), np.ones(B, np.uint8),
+                                                  drk, iv, td0, isb, tsdemux.DEFAULT_MAX_PES)
+    torch.cuda.synchronize()
+    idx, info, pes, es, eo, _, _ = groups[0]
+    assert list(idx) == list(range(B))
+    plain_offs, ppos = [], 0
+    for sg in segs:
+        plain_offs.append(ppos)
+        ppos += (len(sg) + 255) // 256 * 256
+    pbuf = np.zeros(ppos + 256, np.uint8)
+    for o, sg in zip(plain_offs, segs):
+        pbuf[o:o + len(sg)] = np.frombuffer(sg, np.uint8)
+    cpu = tsdemux.demux_batch(torch.from_numpy(pbuf), plain_offs, [len(sg) for sg in segs],
+                              torch.zeros(ppos + 256, dtype=torch.uint8), plain_offs)
+    assert torch.equal(info.cpu(), cpu.info)
+    assert torch.equal(pes.cpu(), cpu.pes)
+    ci = cpu.info.numpy()
+    assert (ci[1:, 0] != 0).any()
+    es_h = es.cpu()
+    for i in range(B):
+        n = int(ci[i, 14])
+        assert torch.equal(es_h[int(eo[i]):int(eo[i]) + n], cpu.es[plain_offs[i]:plain_offs[i] + n])
+
+
 def test_decrypt_then_demux_on_device(cuda):
     seg, st = tsdemux.mux_segment(target_bytes=1_500_000, seed=5, sn=42, start_time=168.0)
     key = bytes(range(16))
