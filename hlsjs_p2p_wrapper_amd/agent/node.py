@@ -289,6 +289,7 @@ class SwarmNode:
         # to want them
         self.cdn_balance = os.environ.get("HLSP2P_CDN_BALANCE", "0") == "1"
         self._cdn_busy = 0.0
+        self._cdn_num = self._cdn_den = 0.0
         self._cdn_t = None
         # entries waiting for a deferred check, by entry id: flag + want info row (a CDN retry's source)
         self._vflag = np.zeros(0, dtype=bool)
@@ -975,9 +976,12 @@ class SwarmNode:
         self.timer.add("deliver", time.perf_counter() - t2)
         self.timer.add("dev_cdn_ms", h.cdn_ms / 1e3)
         now = time.perf_counter()
-        if self._cdn_t is not None and now > self._cdn_t:  # busy share of the ingest link, averaged
-            busy = min(1.0, h.cdn_ms / 1e3 / (now - self._cdn_t))
-            self._cdn_busy += 0.2 * (busy - self._cdn_busy)
+        if self._cdn_t is not None:  # busy share of the ingest link: copy time over wall time, both
+            # averaged over rounds (rounds in flight can complete back to back: a per-round ratio
+            # would read a burst as a saturated link)
+            self._cdn_num += 0.2 * (h.cdn_ms / 1e3 - self._cdn_num)
+            self._cdn_den += 0.2 * ((now - self._cdn_t) - self._cdn_den)
+            self._cdn_busy = min(1.0, self._cdn_num / self._cdn_den) if self._cdn_den > 0 else 0.0
         self._cdn_t = now
         self.timer.add("dev_p2p_ms", h.p2p_ms / 1e3)
         self.last_round = {"wants": h.n_wants, "cdn": 0 if h.cdn is None else len(h.cdn[0]), "send": h.n_send,

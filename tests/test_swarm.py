@@ -496,6 +496,14 @@ def test_node_reports_a_saturated_ingest_link_to_the_planner(monkeypatch):
         h.empty, h.cdn_ms = False, 2.0
         node.complete_round(h)
     assert not node.flags & bound
+    for _ in range(40):  # bursts: rounds completing back to back after a long gap do not read as saturated
+        clock[0] += 0.020
+        for dt in (0.0, 0.0001):
+            clock[0] += dt
+            h = RoundHandle(node.round, np.zeros(0, dtype=np.int64), t0=clock[0])
+            h.empty, h.cdn_ms = False, 2.0
+            node.complete_round(h)
+    assert node._cdn_busy < 0.3 and not node.flags & bound
     node._cdn_busy = 0.95
     node.cdn_balance = False
     assert not node.flags & bound
