@@ -56,7 +56,7 @@ typedef float v16f __attribute__((ext_vector_type(16)));
 // steps are the same for both pairs (crc_host.cpp: mfma_chunk_weights_fp4), so they are loaded
 // once per wave and stay in 32 VGPRs; the pair's position moves to the fold.  The parities of
 // the 2 x 16 accumulators go out as one dword per lane (`masks`: 64 per chunk, bit 16 p + i =
-// row (i & 3) + 8 (i >> 2) + 4 (lane >> 5), column lane & 31); crc32_chunk_fold_kernel
+// row (i & 3) + 8 (i >> 2) + 4 (lane >> 5), column lane & 31); crc32_fold_combine_kernel
 // (crc32_mfma.hip) turns them into the chunk residue with a second FP4 GEMM.
 //
 // (Round 4 measured a one-level form first -- 16 chain-specific weight steps re-read from L1

@@ -258,18 +258,14 @@ constexpr uint32_t kInitFold4096 = 0x38e3ffeeu;  // 4096-byte chunks of the fuse
 
 // One workgroup per segment.  tables: P_0..P_39 then Q_0..Q_11 (each kSlice u32).  Group
 // residues of 2^kLg bytes: 256-byte groups (the residue kernels above) or 4096-byte chunks
-// (the CRC fused into the decrypt, folded by crc32_chunk_fold_kernel).
+// (the CRC fused into the decrypt, folded by crc32_fold_combine_kernel).
 template <int kLg>
-__global__ __launch_bounds__(kCombineThreads) void crc32_combine_kernel(
+__device__ __forceinline__ void combine_segment(
+    int seg, int tid, uint32_t* __restrict__ s_tab, uint32_t* __restrict__ s_q, uint32_t* __restrict__ s_acc,
     const uint32_t* __restrict__ residues, const int64_t* __restrict__ res_off, const int64_t* __restrict__ seg_len,
     const uint32_t* __restrict__ tables, uint32_t* __restrict__ crc_out, const uint32_t* __restrict__ expect,
     uint8_t* __restrict__ ok_out, const int64_t* __restrict__ scatter_idx, uint32_t* __restrict__ scatter_out,
     int64_t scatter_n) {
-  __shared__ __attribute__((aligned(16))) uint32_t s_tab[kCombineLdsTables * kSlice];  // 60 KiB
-  __shared__ __attribute__((aligned(16))) uint32_t s_q[kLg * kSlice];                  // 32 / 48 KiB
-  __shared__ uint32_t s_acc[kCombineThreads];
-  const int seg = blockIdx.x;
-  const int tid = threadIdx.x;
   const int64_t n = seg_len[seg];
   const int64_t G = (n + (int64_t(1) << kLg) - 1) >> kLg;
   // run length L = next pow2 of ceil(G / threads)
@@ -344,6 +340,19 @@ __global__ __launch_bounds__(kCombineThreads) void crc32_combine_kernel(
   }
 }
 
+template <int kLg>
+__global__ __launch_bounds__(kCombineThreads) void crc32_combine_kernel(
+    const uint32_t* __restrict__ residues, const int64_t* __restrict__ res_off, const int64_t* __restrict__ seg_len,
+    const uint32_t* __restrict__ tables, uint32_t* __restrict__ crc_out, const uint32_t* __restrict__ expect,
+    uint8_t* __restrict__ ok_out, const int64_t* __restrict__ scatter_idx, uint32_t* __restrict__ scatter_out,
+    int64_t scatter_n) {
+  __shared__ __attribute__((aligned(16))) uint32_t s_tab[kCombineLdsTables * kSlice];  // 60 KiB
+  __shared__ __attribute__((aligned(16))) uint32_t s_q[kLg * kSlice];                  // 32 / 48 KiB
+  __shared__ uint32_t s_acc[kCombineThreads];
+  combine_segment<kLg>(blockIdx.x, threadIdx.x, s_tab, s_q, s_acc, residues, res_off, seg_len, tables, crc_out, expect,
+                       ok_out, scatter_idx, scatter_out, scatter_n);
+}
+
 // The fused decrypt CRC's second level (aes_cbc.hip: crc_chunk_masks writes 64 mask dwords per
 // 4096-byte chunk, the accumulator parities of chain pairs p = 0, 1 in bits 16 p + i).  The
 // chunk residue is XOR_{p,rho} S[p][rho] D_p[rho] -- over GF(2) a [32 CRC bits x 2048] x
@@ -354,51 +363,69 @@ __global__ __launch_bounds__(kCombineThreads) void crc32_combine_kernel(
 // bits of chunk l & 31 (rows (i & 3) + 8 (i >> 2) + 4 (l >> 5)); one cross-half swap completes
 // the word.  (Round 4's first fold transposed one-level masks with 16 ballots per chunk and a
 // 5-level table tree: 45-50 us per 256-segment batch.)
-constexpr int kFoldThreads = 512;
 constexpr int kFoldSteps = 32;
 constexpr int kMaskDwords = 64;  // per chunk
-__global__ __launch_bounds__(kFoldThreads) void crc32_chunk_fold_kernel(const uint32_t* __restrict__ masks,
-                                                                       const v4i* __restrict__ wfold,
-                                                                       uint32_t* __restrict__ chunk_res,
-                                                                       int64_t total_chunks) {
-  __shared__ v4i s_w[kFoldSteps * 64];  // 32 KiB: [step][lane] A fragments
-  const int tid = threadIdx.x;
-  lds_fill<kFoldSteps * 64 / kFoldThreads>(s_w, wfold, kFoldSteps * 64, tid, kFoldThreads);
-  __syncthreads();
-  const int lane = tid & 63;
+// One 32-chunk tile of the fold: chunks [cbase, cbase + 32) below cend, one wave.
+__device__ __forceinline__ void fold_tile(const uint32_t* __restrict__ masks, const v4i* __restrict__ s_w,
+                                          uint32_t* __restrict__ chunk_res, int64_t cbase, int64_t cend, int lane) {
+  // the weight reads below are the same for every tile: without this barrier the compiler
+  // hoists all 32 of them out of the caller's tile loop (128 VGPRs held live, spills)
+  __asm__ volatile("" ::: "memory");
   const int hh = lane >> 5;
-  const int64_t tiles = (total_chunks + 31) >> 5;
-  const int64_t waves = static_cast<int64_t>(gridDim.x) * (kFoldThreads / 64);
-  for (int64_t t = static_cast<int64_t>(blockIdx.x) * (kFoldThreads / 64) + (tid >> 6); t < tiles; t += waves) {
-    const int64_t c = t * 32 + (lane & 31);
-    const bool valid = c < total_chunks;
-    const uint4* src = reinterpret_cast<const uint4*>(masks + (valid ? c : 0) * kMaskDwords + 32 * hh);
-    uint4 x[kFoldSteps / 4];  // this lane's 32 mask dwords (128 contiguous bytes), all loads in flight
+  const int64_t c = cbase + (lane & 31);
+  const bool valid = c < cend;
+  const uint4* src = reinterpret_cast<const uint4*>(masks + (valid ? c : 0) * kMaskDwords + 32 * hh);
+  uint4 x[kFoldSteps / 4];  // this lane's 32 mask dwords (128 contiguous bytes), all loads in flight
 #pragma unroll
-    for (int k = 0; k < kFoldSteps / 4; ++k) x[k] = valid ? src[k] : make_uint4(0, 0, 0, 0);
-    v16f acc = {};
+  for (int k = 0; k < kFoldSteps / 4; ++k) x[k] = valid ? src[k] : make_uint4(0, 0, 0, 0);
+  v16f acc = {};
 #pragma unroll
-    for (int k = 0; k < kFoldSteps / 4; ++k) {
-      const uint32_t dw[4] = {x[k].x, x[k].y, x[k].z, x[k].w};
+  for (int k = 0; k < kFoldSteps / 4; ++k) {
+    const uint32_t dw[4] = {x[k].x, x[k].y, x[k].z, x[k].w};
 #pragma unroll
-      for (int u = 0; u < 4; ++u) {
-        const uint32_t d = dw[u];
-        const v8i b = {static_cast<int>(d & 0x11111111u), static_cast<int>(d & 0x22222222u),
-                       static_cast<int>(d & 0x44444444u), static_cast<int>((d >> 1) & 0x44444444u), 0, 0, 0, 0};
-        const v4i a4 = s_w[(4 * k + u) * 64 + lane];
-        const v8i a = {a4.x, a4.y, a4.z, a4.w, 0, 0, 0, 0};
-        acc = __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(a, b, acc, 4, 4, 0, 0, 0, 0);
-      }
-      // keep the next group's LDS reads below this one (hoisting them all spills)
-      __builtin_amdgcn_sched_barrier(0);
+    for (int u = 0; u < 4; ++u) {
+      const uint32_t d = dw[u];
+      const v8i b = {static_cast<int>(d & 0x11111111u), static_cast<int>(d & 0x22222222u),
+                     static_cast<int>(d & 0x44444444u), static_cast<int>((d >> 1) & 0x44444444u), 0, 0, 0, 0};
+      const v4i a4 = s_w[(4 * k + u) * 64 + lane];
+      const v8i a = {a4.x, a4.y, a4.z, a4.w, 0, 0, 0, 0};
+      acc = __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(a, b, acc, 4, 4, 0, 0, 0, 0);
     }
-    uint32_t part = 0;  // CRC bits (i & 3) + 8 (i >> 2) + 4 hh of chunk lane & 31
-#pragma unroll
-    for (int i = 0; i < 16; ++i)
-      part |= (static_cast<uint32_t>(static_cast<int>(acc[i])) & 1u) << ((i & 3) + 8 * (i >> 2) + 4 * hh);
-    const uint32_t res = part | static_cast<uint32_t>(__shfl_xor(static_cast<int>(part), 32, 64));
-    if (lane < 32 && valid) chunk_res[c] = res;
+    // keep the next group's LDS reads below this one (hoisting them all spills)
+    __builtin_amdgcn_sched_barrier(0);
   }
+  uint32_t part = 0;  // CRC bits (i & 3) + 8 (i >> 2) + 4 hh of chunk lane & 31
+#pragma unroll
+  for (int i = 0; i < 16; ++i)
+    part |= (static_cast<uint32_t>(static_cast<int>(acc[i])) & 1u) << ((i & 3) + 8 * (i >> 2) + 4 * hh);
+  const uint32_t res = part | static_cast<uint32_t>(__shfl_xor(static_cast<int>(part), 32, 64));
+  if (lane < 32 && valid) chunk_res[c] = res;
+}
+
+// Fold + combine in one workgroup per segment: the segment's chunk tiles over its 16 waves,
+// then the combine over the residues it just wrote (L2-resident).  144 KiB of LDS: the fold's
+// A fragments beside the combine's tables.  (A separate fold kernel over all chunks followed by
+// the combine kernel took 19.1 + 8.4 us per 256-segment batch and two launches; this one takes
+// 25.9 us, profiles/r4_dpp/NOTES.md.)
+__global__ __launch_bounds__(kCombineThreads) void crc32_fold_combine_kernel(
+    const uint32_t* __restrict__ masks, const v4i* __restrict__ wfold, const int64_t* __restrict__ chunk_off,
+    const int64_t* __restrict__ seg_len, const uint32_t* __restrict__ tables, uint32_t* __restrict__ chunk_res,
+    uint32_t* __restrict__ crc_out, const uint32_t* __restrict__ expect, uint8_t* __restrict__ ok_out,
+    const int64_t* __restrict__ scatter_idx, uint32_t* __restrict__ scatter_out, int64_t scatter_n) {
+  __shared__ v4i s_w[kFoldSteps * 64];                                                  // 32 KiB
+  __shared__ __attribute__((aligned(16))) uint32_t s_tab[kCombineLdsTables * kSlice];  // 60 KiB
+  __shared__ __attribute__((aligned(16))) uint32_t s_q[12 * kSlice];                   // 48 KiB
+  __shared__ uint32_t s_acc[kCombineThreads];
+  const int seg = blockIdx.x, tid = threadIdx.x, lane = tid & 63;
+  lds_fill<kFoldSteps * 64 / kCombineThreads>(s_w, wfold, kFoldSteps * 64, tid, kCombineThreads);
+  __syncthreads();
+  const int64_t n = seg_len[seg] < 0 ? 0 : seg_len[seg];
+  const int64_t c0 = chunk_off[seg], cend = c0 + ((n + 4095) >> 12);
+  const int64_t tiles = (cend - c0 + 31) >> 5;
+  for (int64_t t = tid >> 6; t < tiles; t += kCombineThreads / 64) fold_tile(masks, s_w, chunk_res, c0 + 32 * t, cend, lane);
+  __syncthreads();  // the segment's chunk residues, written by its own waves, before the combine reads them
+  combine_segment<12>(seg, tid, s_tab, s_q, s_acc, chunk_res, chunk_off, seg_len, tables, crc_out, expect, ok_out,
+                      scatter_idx, scatter_out, scatter_n);
 }
 
 // masks: 64 dwords per 4096-byte chunk for each segment, the segment's chunks starting at
@@ -408,22 +435,11 @@ hipError_t launch_crc32_from_masks(const uint32_t* masks, const void* wfold, con
                                    const int64_t* seg_len, const uint32_t* tables, uint32_t* chunk_res,
                                    uint32_t* crc_out, const uint32_t* expect, uint8_t* ok_out,
                                    const int64_t* scatter_idx, uint32_t* scatter_out, int64_t scatter_n, int nseg,
-                                   int64_t total_chunks, int num_cu, hipStream_t stream) {
+                                   int64_t /*total_chunks*/, int /*num_cu*/, hipStream_t stream) {
   if (nseg <= 0) return hipSuccess;
-  if (total_chunks > 0) {
-    const int64_t tiles = (total_chunks + 31) / 32;
-    const int64_t grid_max = static_cast<int64_t>(num_cu) * 4;  // 32 KiB LDS: up to 4 workgroups per CU
-    int64_t grid = (tiles + (kFoldThreads / 64) - 1) / (kFoldThreads / 64);
-    if (grid > grid_max) grid = grid_max;
-    hipLaunchKernelGGL(crc32_chunk_fold_kernel, dim3(static_cast<unsigned>(grid)), dim3(kFoldThreads), 0, stream,
-                       masks, reinterpret_cast<const v4i*>(wfold), chunk_res,
-                       total_chunks);
-    hipError_t e = hipGetLastError();
-    if (e != hipSuccess) return e;
-  }
-  hipLaunchKernelGGL(crc32_combine_kernel<12>, dim3(static_cast<unsigned>(nseg)), dim3(kCombineThreads), 0, stream,
-                     chunk_res, chunk_off, seg_len, tables, crc_out, expect, ok_out, scatter_idx, scatter_out,
-                     scatter_n);
+  hipLaunchKernelGGL(crc32_fold_combine_kernel, dim3(static_cast<unsigned>(nseg)), dim3(kCombineThreads), 0, stream,
+                     masks, reinterpret_cast<const v4i*>(wfold), chunk_off, seg_len, tables, chunk_res, crc_out, expect,
+                     ok_out, scatter_idx, scatter_out, scatter_n);
   return hipGetLastError();
 }
 

@@ -130,7 +130,7 @@ def _chunk_masks(chunk: np.ndarray, wa: np.ndarray) -> np.ndarray:
 
 
 def _fold(masks: np.ndarray, wf: np.ndarray) -> int:
-    """The fold side (crc32_mfma.hip: crc32_chunk_fold_kernel): A = host fragments (row = CRC
+    """The fold side (crc32_mfma.hip: fold_tile in crc32_fold_combine_kernel): A = host fragments (row = CRC
     bit), B = the chunk's mask dwords (k half hh of step s reads dword s + 32 hh)."""
     acc = np.zeros(32)
     for s in range(32):
@@ -146,7 +146,7 @@ def test_fused_chunk_crc_formulation_matches_zlib(rt):
     """The CRC fused into the AES decrypt, two MFMA levels: row parities per chain pair in the
     decrypt (8 pair-independent weight steps), a [32 x 2048] x [2048 x chunks] GF(2) GEMM
     per chunk in the fold, then a Horner over 4096-byte chunks (P_12), the pad removal
-    Q_0..Q_11 and the init term -- as crc32_chunk_fold + crc32_combine(lg_group=12) do."""
+    Q_0..Q_11 and the init term -- as crc32_fold_combine_kernel (fold_tile + combine_segment<12>) does."""
     na, nf = rt.CRC_FUSED_AES_STEPS, rt.CRC_FUSED_FOLD_STEPS
     w = rt.crc_chunk_weights_fp4().reshape(na + nf, 64, 16)
     wa, wf = w[:na], w[na:]

@@ -308,7 +308,7 @@ def test_arena_views_share_storage(cuda):
 
 @pytest.mark.gpu
 def test_fused_decrypt_crc_matches_zlib_at_segment_sizes(cuda):
-    """The CRC fused into the AES decrypt (aes_cbc.hip AesCrc + crc32_chunk_fold / combine<12>)
+    """The CRC fused into the AES decrypt (aes_cbc.hip AesCrc + crc32_fold_combine_kernel)
     on bench-sized ciphertexts: 48 segments of 16 B .. 3 MB, every CRC equal to zlib's; one
     corrupted byte fails exactly its segment."""
     import zlib
