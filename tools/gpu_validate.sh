@@ -1,6 +1,6 @@
 # Round validation on one MI355X (what the driver runs, plus the two probes):
 #   GPU tests, smoke(), the headline bench, the host-cost probe and the HBM-origin probe.
-#   bash tools/gpu_validate.sh            -> gpurun_out/validate/*.log
+#   bash tools/gpu_validate.sh            -> gpurun_out/validate/*.log (VAL_OUT=<dir> to keep runs apart)
 set -eo pipefail
 R=$GRAFT_REPO_ROOT
 cd $R
