@@ -309,15 +309,17 @@ def test_arena_views_share_storage(cuda):
 @pytest.mark.gpu
 def test_fused_decrypt_crc_matches_zlib_at_segment_sizes(cuda):
     """The CRC fused into the AES decrypt (aes_cbc.hip AesCrc + crc32_fold_combine_kernel)
-    on bench-sized ciphertexts: 48 segments of 16 B .. 3 MB, every CRC equal to zlib's; one
-    corrupted byte fails exactly its segment."""
+    on bench-sized ciphertexts: 50 segments of 16 B .. 3 MB plus a 4K-sized 12.5 MB and a 40 MB
+    one (the fold's per-segment workgroup then walks many chunk tiles per wave), every CRC equal
+    to zlib's; one corrupted byte fails exactly its segment."""
     import zlib
 
     from hlsjs_p2p_wrapper_amd.player.transmux import MediaPipeline
     from hlsjs_p2p_wrapper_amd.net import new_event_loop
 
     rng = np.random.default_rng(11)
-    sizes = [16, 4096, 4112] + [int(x) * 16 for x in rng.integers(1, 3_000_000 // 16, 45)]
+    sizes = [16, 4096, 4112] + [int(x) * 16 for x in rng.integers(1, 3_000_000 // 16, 45)] + [12_500_000 // 16 * 16,
+                                                                                                40_000_016]
     offs, pos = [], 0
     for n in sizes:
         offs.append(pos)
