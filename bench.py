@@ -75,7 +75,13 @@ LIVE = {"1080p6m-live"}
 
 def parse():
     p = argparse.ArgumentParser(description=__doc__, formatter_class=argparse.RawDescriptionHelpFormatter)
-    p.add_argument("--gpus", type=int, default=1)
+    p.add_argument("--gpus", type=int, default=None,
+                   help="ranks (one per GPU); without a launcher, N > 1 starts N rank processes itself "
+                        "(a torch.distributed.run child) and forwards rank 0's JSON line; under a launcher "
+                        "it must equal WORLD_SIZE (default: the launcher's world, else 1)")
+    p.add_argument("--launch-timeout", type=float, default=float(os.environ.get("HLSP2P_LAUNCH_TIMEOUT", "1500")),
+                   help="self-launch (--gpus N > 1 without a launcher): kill the rank processes and exit "
+                        "non-zero after this many seconds")
     p.add_argument("--steps", type=int, default=20)
     p.add_argument("--warmup", type=int, default=5)
     p.add_argument("--config", default="1080p6m", choices=sorted(CONFIGS))
@@ -245,8 +251,116 @@ def _spawn_players(W, world, rank, origin_kwargs, hls_config, p2p_base, n_segmen
     return conns, procs
 
 
+def _launcher_world():
+    """The world size a launcher (torchrun / torch.distributed.run, an MPI-style wrapper that
+    exports the same variables) gave this process, or None when started directly."""
+    if "WORLD_SIZE" in os.environ and "RANK" in os.environ:
+        return int(os.environ["WORLD_SIZE"])
+    return None
+
+
+def _self_launch(args) -> int:
+    """``--gpus N > 1`` without a launcher: run the N ranks as children of a
+    ``torch.distributed.run`` process (one rank per GPU, rendezvous on 127.0.0.1), forward
+    rank 0's JSON line, and exit non-zero if any rank fails, the job overruns
+    ``--launch-timeout`` or the record does not report N ranks.  Runs before this process
+    touches the GPU (``torch.cuda.device_count`` does not initialise it) and never execs:
+    the launcher is a child process in its own process group."""
+    import signal
+    import socket
+    import subprocess
+    import threading
+
+    n = args.gpus
+    if not args.cpu and args.dist_backend in ("auto", "nccl"):
+        avail = torch.cuda.device_count()
+        if 0 < avail < n:
+            print(f"bench.py: --gpus {n} needs {n} visible GPUs for the RCCL data plane (one rank per GPU); "
+                  f"{avail} visible.  Rehearse ranks that share a GPU with --dist-backend ipc.", file=sys.stderr)
+            return 2
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+           "--master-addr=127.0.0.1", f"--master-port={port}", os.path.abspath(__file__), *sys.argv[1:]]
+    env = dict(os.environ, HLSP2P_LAUNCHER="self")
+    env.setdefault("OMP_NUM_THREADS", "1")
+    print(f"# bench.py: launching {n} ranks: {' '.join(cmd)}", file=sys.stderr, flush=True)
+    proc = subprocess.Popen(cmd, env=env, stdout=subprocess.PIPE, text=True, start_new_session=True)
+    lines = []
+
+    def pump():  # rank 0's JSON line is kept for the parent's stdout; the rest goes to stderr
+        for ln in proc.stdout:
+            if ln.startswith("{"):
+                lines.append(ln.strip())
+            else:
+                sys.stderr.write(ln)
+                sys.stderr.flush()
+
+    reader = threading.Thread(target=pump, daemon=True)
+    reader.start()
+
+    def kill_group(sig=signal.SIGTERM):
+        try:
+            os.killpg(proc.pid, sig)
+        except ProcessLookupError:
+            pass
+
+    def on_signal(signum, frame):  # the driver stopping this process stops every rank
+        kill_group()
+        raise SystemExit(128 + signum)
+
+    prev = {sg: signal.signal(sg, on_signal) for sg in (signal.SIGTERM, signal.SIGINT)}
+    try:
+        try:
+            rc = proc.wait(timeout=args.launch_timeout)
+        except subprocess.TimeoutExpired:
+            print(f"bench.py: {n}-rank job overran --launch-timeout {args.launch_timeout:.0f} s; killing it",
+                  file=sys.stderr, flush=True)
+            kill_group()
+            try:
+                proc.wait(timeout=15)
+            except subprocess.TimeoutExpired:
+                kill_group(signal.SIGKILL)
+                proc.wait()
+            return 124
+    finally:
+        for sg, h in prev.items():
+            signal.signal(sg, h)
+    reader.join(timeout=10)
+    if rc != 0:
+        print(f"bench.py: the {n}-rank job failed (exit {rc})", file=sys.stderr)
+        return rc if rc > 0 else 1
+    if not lines:
+        print("bench.py: the rank processes printed no result line", file=sys.stderr)
+        return 3
+    rec = json.loads(lines[-1])
+    if rec.get("n_gpus") != n:
+        print(f"bench.py: asked for {n} ranks, the record reports n_gpus={rec.get('n_gpus')}", file=sys.stderr)
+        return 4
+    print(lines[-1], flush=True)
+    return 0
+
+
 def main() -> int:
     args = parse()
+    launched = _launcher_world()
+    if launched is None:
+        if args.gpus is None:
+            args.gpus = 1
+        if args.gpus < 1:
+            raise SystemExit("--gpus must be >= 1")
+        if args.gpus > 1:
+            return _self_launch(args)
+    elif args.gpus is None:
+        args.gpus = launched
+    elif args.gpus != launched:
+        raise SystemExit(f"bench.py: --gpus {args.gpus} but the launcher started {launched} ranks "
+                         f"(WORLD_SIZE={launched}); they must agree")
+    # a round whose transfers are never matched (a dead or diverged peer) fails the job in a
+    # minute, with the rank's plan in the error, instead of at the 600 s library default
+    os.environ.setdefault("HLSP2P_ROUND_TIMEOUT", "60")
     if args.inflight is None:
         # 64, by measurement (profiles/r4_ab): the headline is PCIe-bound and flat at 128; the
         # HBM-origin probe was +10-20 % at 128 on round-3 boxes and -4 % on round 4's.  (The
@@ -268,8 +382,14 @@ def main() -> int:
     players = _spawn_players(W, world, rank, origin_kwargs, hls_config, p2p_base, n_segments, seg_dur) \
         if W else None
     use_gpu = torch.cuda.is_available() and not args.cpu
+    rccl_plane = use_gpu and world > 1 and args.dist_backend in ("auto", "nccl")
     if use_gpu:
-        local_dev = local_rank % torch.cuda.device_count()  # rehearsals may share one GPU
+        n_dev = torch.cuda.device_count()
+        if rccl_plane and local_rank >= n_dev:  # before any stream, event or communicator exists
+            raise SystemExit(f"bench.py: rank {rank} (local rank {local_rank}) has no GPU of its own: {n_dev} "
+                             f"visible for {os.environ.get('LOCAL_WORLD_SIZE', world)} local ranks.  The RCCL "
+                             "data plane needs one GPU per rank; rehearse shared-GPU ranks with --dist-backend ipc.")
+        local_dev = local_rank % n_dev  # the ipc / gloo rehearsals may share one GPU
         torch.cuda.set_device(local_dev)
         device = torch.device("cuda", local_dev)
         numa_node = _numa(args.numa, local_dev, world, W)  # before the pinned CDN buffers are allocated
@@ -447,6 +567,7 @@ def main() -> int:
     node.timer.reset()
     pipe.timer.reset()
     b0, s0 = counters["buffered"], dict(node.stats)
+    pf0 = node.p2p_from.copy()
     node.corrupt_next_recv = args.corrupt_recv
     t0 = time.perf_counter()
     if _PROF is not None and not _PROF_C3:
@@ -474,7 +595,7 @@ def main() -> int:
     result = _result(args, world, tot, max_s, origin, K, desc, encrypted, seg_dur, use_gpu, numa_node, dist,
                      transport=getattr(node.comm, "data_transport", None))
     result["per_rank"] = _per_rank_dicts(per_parts, args.steps)
-    result["data_plane"] = _plane_info(node)
+    result["data_plane"] = _plane_info(node, dist, world, device, node.p2p_from - pf0)
     if args.verbose:
         print(f"# rank {rank} pack {t_pack:.2f}s {_mem(use_gpu, device)} counters {counters} level {hls.currentLevel}\n"
               f"#   node stats {node.stats} last round {node.last_round}\n"
@@ -623,6 +744,7 @@ def _fleet(args, world, rank, device, use_gpu, node, origin, players, desc, encr
         pipe.timer.reset()
         fleet_timer.reset()
         s0 = dict(node.stats)
+        pf0 = node.p2p_from.copy()
         pay0 = (server.payload_bytes, server.payload_wait_s)
         node.corrupt_next_recv = args.corrupt_recv
         calib0 = cpu_calibration_us() if args.verbose else 0.0
@@ -652,6 +774,7 @@ def _fleet(args, world, rank, device, use_gpu, node, origin, players, desc, encr
         calib1 = cpu_calibration_us() if args.verbose else 0.0
         mark("t1")
         s1 = dict(node.stats)
+        pf1 = node.p2p_from.copy()
         # keep serving until every player has acknowledged both marks (collective rounds)
         t_end = time.perf_counter() + 120
         while True:
@@ -688,7 +811,7 @@ def _fleet(args, world, rank, device, use_gpu, node, origin, players, desc, encr
         # whether CDN fetches get the CRC trailer peers check (a one-rank swarm sends nothing, so
         # it skips that pass; the headline is the same with it forced: profiles/r4_ingestcrc)
         result["config"]["ingest_crc"] = bool(getattr(node, "ingest_crc", True))
-        result["data_plane"] = _plane_info(node)
+        result["data_plane"] = _plane_info(node, dist, world, device, pf1 - pf0)
         if live:
             result["config"].update(live=True, live_speed=args.live_speed, live_window=args.live_window,
                                     round_ms=args.round_ms, evicted_segments=server.evicted)
@@ -863,18 +986,55 @@ def _per_rank_dicts(parts, steps) -> list:
     return out
 
 
-def _plane_info(node) -> dict:
+def _plane_info(node, dist, world: int, device, recv_from=None) -> dict:
     """Which transports the run actually used (the data plane may fall back; see
-    parallel/comm.py).  ``hsa_ipc_legacy``: the HSA IPC mode the process started with
+    parallel/comm.py) and the topology that proves an N > 1 record: per rank (all-gathered,
+    collective) its host, local rank, device index and PCI address, what the data plane
+    reports about itself (for RCCL: ``ncclCommCount`` / ``ncclCommUserRank`` /
+    ``ncclCommCuDevice``, rounds posted, version) and the bytes it received from each source
+    peer over the timed window (``recv_from``: the fan-in over the point-to-point links).
+    ``distinct_devices``: no two ranks drive the same GPU (required on the RCCL plane: the
+    run fails otherwise).  ``hsa_ipc_legacy``: the HSA IPC mode the process started with
     (``0`` = dmabuf: RCCL's intra-node P2P transport and the HIP-IPC rehearsal export device
     buffers with ``hipIpcGetMemHandle``, which fails with ``invalid argument`` under the
     legacy mode on this host driver, ``tools/ipc_probe.py``)."""
+    import socket
+
     comm = node.comm
     ipc = getattr(comm, "_ipc", None)
-    return {"data": getattr(comm, "data_transport", "local"), "control": getattr(comm, "control_transport", "local"),
+    transport = getattr(comm, "data_transport", "local")
+    bus = None
+    if device.type == "cuda":
+        try:
+            from hlsjs_p2p_wrapper_amd.ops._native import device as _dev
+
+            bus = _dev().pci_bus_id(device.index)
+        except Exception:  # noqa: BLE001 - reported as unknown
+            bus = None
+    me = {"rank": node.rank, "local_rank": int(os.environ.get("LOCAL_RANK", "0")), "host": socket.gethostname(),
+          "device": device.index if device.type == "cuda" else None, "pci_bus_id": bus,
+          "rounds": int(node.stats["rounds"]),
+          "recv_bytes_from": [int(x) for x in (recv_from if recv_from is not None else node.p2p_from)]}
+    topo = getattr(comm, "topology", None)
+    if topo is not None:
+        me["comm"] = topo()
+    ranks = [me]
+    if world > 1:
+        ranks = [None] * world
+        dist.all_gather_object(ranks, me)
+    devs = [(r["host"], r["pci_bus_id"]) for r in ranks if r["pci_bus_id"] is not None]
+    distinct = len(set(devs)) == len(devs) if len(devs) == len(ranks) else None
+    if transport.startswith("rccl") and distinct is not True:
+        raise RuntimeError(f"RCCL data plane without one GPU per rank: {[(r['rank'], r['pci_bus_id']) for r in ranks]}")
+    rccl = next((r["comm"]["rccl"] for r in ranks if "rccl" in r.get("comm", {})), None)
+    return {"data": transport, "control": getattr(comm, "control_transport", "local"),
             "ipc_events": bool(ipc is not None and ipc._peer_ev is not None),
             "shm_slot_words": getattr(comm, "shm_slot_words", None),
-            "hsa_ipc_legacy": os.environ.get("HSA_ENABLE_IPC_MODE_LEGACY")}
+            "hsa_ipc_legacy": os.environ.get("HSA_ENABLE_IPC_MODE_LEGACY"),
+            "launcher": os.environ.get("HLSP2P_LAUNCHER") or ("torchrun" if "TORCHELASTIC_RUN_ID" in os.environ
+                                                              else "env" if world > 1 else "none"),
+            "world": world, "distinct_devices": distinct,
+            "rccl_version": rccl["version"] if rccl else None, "ranks": ranks}
 
 
 def _mem(use_gpu, device) -> str:

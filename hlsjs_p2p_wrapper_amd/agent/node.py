@@ -53,6 +53,7 @@ log = logging.getLogger("hlsjs_p2p_wrapper_amd.node")
 
 MAGIC = 0x48505032  # "HPP2"
 HDR = 16
+CHECK_WORD = 10  # header words 10..12: directory digest, previous plan digest, its round (ingest_control)
 # a rank whose CDN copies keep its ingest link busy for more than this share of its rounds
 # reports FLAG_CDN_BOUND (the planner's CDN balance relieves only such ranks): a PCIe-origin
 # leader measures ~0.96, the HBM-origin rehearsal's leader ~0.2 (profiles/r4_balance)
@@ -147,6 +148,7 @@ class RoundHandle:
     ok_host: Any = None
     defer: Any = None  # bool per received row: its CRC is checked by the consumer's decrypt (fleet)
     expect_host: Any = None  # the senders' CRC trailers of the received rows (host copy)
+    plan: Any = None  # (send rows, recv rows) of this rank's plan
     done: Any = None
     n_wants: int = 0
     n_send: int = 0
@@ -277,6 +279,16 @@ class SwarmNode:
         self.swarm_stats = {"cdn": 0, "p2p": 0, "upload": 0}
         self.last_round: Dict[str, Any] = {}
         self.corrupt_next_recv = 0  # fault injection: flip a byte in the next N received rounds
+        # cross-rank consistency (SURVEY 5.2 state-machine assertions): every rank replays the
+        # same control messages into its own directory and plans every round independently; a
+        # two-sided data plane (RCCL send / recv) then needs the plans to match exactly.  The
+        # directory digest and the previous plan's digest ride every control message and are
+        # compared before anything is applied (HLSP2P_DIVERGENCE_CHECK=0 turns it off)
+        self.divergence_check = self.world > 1 and os.environ.get("HLSP2P_DIVERGENCE_CHECK", "1") != "0"
+        self._plan_digest = 0
+        self._plan_round = 0
+        # bytes received from each source peer (the fan-in over the point-to-point links)
+        self.p2p_from = np.zeros(self.world, dtype=np.int64)
         # Deferred receive verification (set by a fleet server, parallel/fleet.py): a segment a
         # peer sent is not CRC-read by the node; its trailer travels with the delivery and the
         # batch that decrypts it computes the CRC on the way (kernels/aes_cbc.hip AesCrc).  The
@@ -737,6 +749,11 @@ class SwarmNode:
         hdr[7] = self.stats["cdn"]
         hdr[8] = self.stats["p2p"]
         hdr[9] = self.stats["upload"]
+        # consistency words (checked by every rank in ingest_control): this replica's directory
+        # digest before the round's deltas, and the digest of the previous round's full plan
+        hdr[CHECK_WORD] = self.directory.digest
+        hdr[CHECK_WORD + 1] = self._plan_digest
+        hdr[CHECK_WORD + 2] = self._plan_round
         return np.concatenate([hdr, rows.reshape(-1), adds.reshape(-1).astype(np.int64),
                                rms.reshape(-1).astype(np.int64)])
 
@@ -809,14 +826,21 @@ class SwarmNode:
         adds, rms = self.store.take_delta()
         parts = self.comm.allgather_control(self._encode(rows, adds, rms))
         # every rank's deltas into the directory + the round's want rows, in one native call
-        all_wants, flags, all_leaving, swarm_tot = rt.ingest_control(self.directory, parts, MAGIC, HDR)
+        # (after checking that every replica and the last plans agree)
+        try:
+            all_wants, flags, all_leaving, swarm_tot = rt.ingest_control(
+                self.directory, parts, MAGIC, HDR, CHECK_WORD if self.divergence_check else -1)
+        except rt.SwarmDivergence as e:
+            self._diverged(str(e))
+            raise
         self.peer_online = (flags & rt.FLAG_ONLINE) != 0
         self.swarm_stats = {"cdn": int(swarm_tot[0]), "p2p": int(swarm_tot[1]), "upload": int(swarm_tot[2])}
         h = RoundHandle(self.round, all_leaving, t0=t0)
         h.ids = ids
         t_ctrl = time.perf_counter()
         self.timer.add("control", t_ctrl - t0)
-        if not len(all_wants):
+        if not len(all_wants):  # (every rank sees the same want rows: all skip planning alike)
+            self._plan_digest, self._plan_round = 0, self.round
             return h
         h.empty = False
         # only the rows this rank sends, receives or fetches (the full plan is identical on
@@ -826,7 +850,9 @@ class SwarmNode:
         # lone want of a rank over its share back once when another rank is about to want it
         cdn_bytes = np.fromiter((int(p[7]) for p in parts), dtype=np.int64, count=len(parts)) \
             if self.cdn_balance and self.world > 1 else None
-        plan, any_p2p = rt.plan_round_for(self.directory, all_wants, flags, self.world, me, cdn_bytes)
+        plan, any_p2p, self._plan_digest = rt.plan_round_for(self.directory, all_wants, flags, self.world, me,
+                                                             cdn_bytes)
+        self._plan_round = self.round
         h.n_wants = len(all_wants)
         cdn_rows = plan[(plan[:, 5] == -1) & (plan[:, 6] == me)]
         if self._net_wants and self._wx:  # network-origin wants this rank must download first (STAGE rows)
@@ -837,6 +863,7 @@ class SwarmNode:
         send_rows = plan[plan[:, 5] == me]
         recv_rows = plan[(plan[:, 6] == me) & (plan[:, 5] >= 0)]
         h.n_send = len(send_rows)
+        h.plan = (send_rows, recv_rows)  # kept for the diagnostic of a round that never completes
         # ---------------- 2. pin what we send from cache (seeded rows come from the CDN phase)
         # send_eids[i]: store entry of send row i (-1: missing), aligned with send_rows
         send_eids = np.full(len(send_rows), -1, dtype=np.int64)
@@ -1026,9 +1053,52 @@ class SwarmNode:
             if err:
                 raise RuntimeError(f"rank {self.rank}: swarm round {h.round} failed in the data plane: {err}")
             if time.perf_counter() > deadline:
+                summary = self.plan_summary(h)
+                log.error("rank %d: swarm round %d did not complete; this rank's plan: %s", self.rank, h.round,
+                          summary)
+                self._dump_plan(h)
                 raise TimeoutError(f"rank {self.rank}: swarm round {h.round} did not complete on the device "
-                                   "(HLSP2P_ROUND_TIMEOUT); a peer may have stopped")
+                                   f"(HLSP2P_ROUND_TIMEOUT); a peer may have stopped.  Plan: {summary}")
             time.sleep(1e-3)
+
+    @staticmethod
+    def plan_summary(h: RoundHandle) -> Dict[str, Any]:
+        """Per peer: the rows and bytes this rank was to send / receive in round ``h`` (what its
+        data-plane group posted), for the diagnostic of a round that does not complete."""
+        out: Dict[str, Any] = {"round": h.round, "send": {}, "recv": {}}
+        if h.plan is None:
+            return out
+        for name, rows, col in (("send", h.plan[0], 6), ("recv", h.plan[1], 5)):
+            if len(rows):
+                peers, inv = np.unique(rows[:, col], return_inverse=True)
+                nbytes = np.bincount(inv, weights=rows[:, 4])
+                count = np.bincount(inv)
+                out[name] = {int(p): [int(c), int(b)] for p, c, b in zip(peers, count, nbytes)}
+        return out
+
+    def _dump_plan(self, h: RoundHandle) -> None:
+        """Write this rank's plan rows of round ``h`` under ``HLSP2P_PLAN_DUMP`` (a directory;
+        one ``plan.r<round>.rank<rank>.npz`` per rank), so the ranks' views can be compared."""
+        d = os.environ.get("HLSP2P_PLAN_DUMP")
+        if not d or h.plan is None:
+            return
+        try:
+            os.makedirs(d, exist_ok=True)
+            np.savez(os.path.join(d, f"plan.r{h.round}.rank{self.rank}.npz"), send=h.plan[0], recv=h.plan[1],
+                     directory_digest=np.int64(self.directory.digest))
+        except OSError as e:  # a diagnostic must not mask the timeout itself
+            log.warning("rank %d: plan dump failed: %s", self.rank, e)
+
+    def _diverged(self, what: str) -> None:
+        """Replicated state differs across ranks: no rank may post another data-plane group.
+        Abort the communicator (transfers already posted would never be matched) and log."""
+        log.error("rank %d: %s", self.rank, what)
+        abort = getattr(self.comm, "abort", None)
+        if abort is not None:
+            try:
+                abort()
+            except Exception as e:  # noqa: BLE001 - the divergence is the error to report
+                log.warning("rank %d: communicator abort failed: %s", self.rank, e)
 
     def _views(self, offs: List[int], lens: List[int]) -> List[torch.Tensor]:
         """Zero-copy uint8 views of the arena for a round's deliveries (one native call on
@@ -1182,6 +1252,8 @@ class SwarmNode:
                 recvs.append((src, view))
                 recvs.append((src, trailers[a:b]))
             h.hold.append(rid_a)  # pinned by p2p_layout until complete_round
+            # segment bytes per source run (a run's span also holds alignment gaps)
+            np.add.at(self.p2p_from, rrun[:, 0], np.add.reduceat(recv_rows[:, 4], rrun[:, 1]))
             self._grow_crc(int(rid_a.max()) + 1)
             h.recv = (np.ascontiguousarray(recv_rows[:, 7]), np.ascontiguousarray(recv_rows[:, 5]), rid_a, roff_a,
                       np.ascontiguousarray(recv_rows[:, 4]), np.ascontiguousarray(recv_rows[:, :4]))

@@ -119,6 +119,25 @@ class RcclComm {
     ncclCommAbort(c);
   }
 
+  // What RCCL itself reports for this communicator (the topology record of an N > 1 run
+  // proves the group RCCL built, not the one the caller asked for): its rank count, this
+  // rank's index in it, and the HIP device it runs on.
+  int comm_count() const {
+    int n = 0;
+    nccl_ok(ncclCommCount(live(), &n), "ncclCommCount");
+    return n;
+  }
+  int comm_user_rank() const {
+    int r = -1;
+    nccl_ok(ncclCommUserRank(live(), &r), "ncclCommUserRank");
+    return r;
+  }
+  int comm_device() const {
+    int d = -1;
+    nccl_ok(ncclCommCuDevice(live(), &d), "ncclCommCuDevice");
+    return d;
+  }
+
   bool closed() const { return comm_ == nullptr; }
   int world() const { return world_; }
   int rank() const { return rank_; }
@@ -126,6 +145,10 @@ class RcclComm {
   int64_t rounds() const { return rounds_; }
 
  private:
+  ncclComm_t live() const {
+    if (comm_ == nullptr) throw std::runtime_error("RcclComm: communicator is closed");
+    return comm_;
+  }
   ncclComm_t comm_ = nullptr;
   int world_, rank_, device_;
   int64_t rounds_ = 0;
@@ -143,11 +166,21 @@ std::string version() {
   return std::to_string(v);
 }
 
+// PCI address ("dddd:bb:dd.f") of a HIP device: the identity two ranks compare to prove they
+// drive different GPUs (a device index is only meaningful inside one process's visible set).
+std::string pci_bus_id(int device) {
+  char buf[64] = {0};
+  if (hipDeviceGetPCIBusId(buf, sizeof(buf), device) != hipSuccess)
+    throw std::runtime_error("hipDeviceGetPCIBusId failed for device " + std::to_string(device));
+  return std::string(buf);
+}
+
 }  // namespace
 
 void register_rccl(py::module& m) {
   m.def("rccl_unique_id", &unique_id, "ncclGetUniqueId (rank 0 of a new communicator)");
   m.def("rccl_version", &version);
+  m.def("pci_bus_id", &pci_bus_id, py::arg("device"));
   py::class_<RcclComm, std::shared_ptr<RcclComm>>(m, "RcclComm")
       .def(py::init<const py::bytes&, int, int, int>(), py::arg("unique_id"), py::arg("world"), py::arg("rank"),
            py::arg("device"))
@@ -160,5 +193,8 @@ void register_rccl(py::module& m) {
       .def_property_readonly("world", &RcclComm::world)
       .def_property_readonly("rank", &RcclComm::rank)
       .def_property_readonly("device", &RcclComm::device)
-      .def_property_readonly("rounds", &RcclComm::rounds);
+      .def_property_readonly("rounds", &RcclComm::rounds)
+      .def("comm_count", &RcclComm::comm_count)
+      .def("comm_user_rank", &RcclComm::comm_user_rank)
+      .def("comm_device", &RcclComm::comm_device);
 }

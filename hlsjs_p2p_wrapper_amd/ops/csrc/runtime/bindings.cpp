@@ -10,8 +10,11 @@
 
 #include <algorithm>
 #include <cstring>
+#include <map>
+#include <sstream>
 #include <stdexcept>
 #include <thread>
+#include <tuple>
 #include <vector>
 
 #include "aes_host.hpp"
@@ -69,7 +72,30 @@ py::array_t<uint8_t> to_u8(const std::vector<uint8_t>& v) {
 
 }  // namespace
 
+namespace {
+// Replicated swarm state that differs across ranks (directory content or a round's plan).
+struct SwarmDivergence : std::runtime_error {
+  using std::runtime_error::runtime_error;
+};
+
+// "digest A: ranks [0, 1, 2]; digest B: ranks [3]" for one header word of every rank
+std::string group_ranks(const std::vector<Arr<int64_t>>& parts, int64_t word) {
+  std::map<int64_t, std::vector<int>> by;
+  for (size_t r = 0; r < parts.size(); ++r) by[parts[r].data()[word]].push_back(int(r));
+  std::ostringstream o;
+  bool first = true;
+  for (const auto& kv : by) {
+    o << (first ? "" : "; ") << std::hex << "0x" << uint64_t(kv.first) << std::dec << ": ranks [";
+    for (size_t i = 0; i < kv.second.size(); ++i) o << (i ? ", " : "") << kv.second[i];
+    o << "]";
+    first = false;
+  }
+  return o.str();
+}
+}  // namespace
+
 PYBIND11_MODULE(_runtime, m) {
+  py::register_exception<SwarmDivergence>(m, "SwarmDivergence", PyExc_RuntimeError);
   m.doc() = "hlsjs-p2p-wrapper-amd host runtime (store, planner, packager, CPU oracles)";
 
   // ------------------------------------------------------------------ AES
@@ -458,6 +484,8 @@ PYBIND11_MODULE(_runtime, m) {
   py::class_<Directory>(m, "Directory")
       .def(py::init<>())
       .def_property_readonly("size", &Directory::size)
+      // the content digest as a signed 64-bit word (it travels in an int64 control header)
+      .def_property_readonly("digest", [](const Directory& d) { return static_cast<int64_t>(d.digest()); })
       .def("apply", [](Directory& d, int rank, Arr<int64_t> adds, Arr<int64_t> removes) {
         // adds int64[n,5] (key4, len); removes int64[m,4]
         for (int64_t i = 0; i < adds.size() / 5; ++i) d.apply_add(rank, key_from(adds.data() + 5 * i), adds.data()[5 * i + 4]);
@@ -474,8 +502,14 @@ PYBIND11_MODULE(_runtime, m) {
   // [key4]) in one call:
   // applies every rank's cache delta to the directory and returns (want rows int64[n, 8] for
   // plan_round, per-rank flags, all-leaving, swarm byte totals [cdn, p2p, upload]).
+  //
+  // check_word >= 0: header words [check_word, check_word + 3) carry each rank's directory
+  // digest taken before this ingest, the digest of the previous round's full plan and that
+  // round's number.  They must agree on every rank: otherwise SwarmDivergence is raised
+  // before anything is applied, naming the ranks behind each value, so no rank goes on to
+  // post a send / receive group its peers do not match (a hang on a two-sided transport).
   m.def("ingest_control", [](Directory& d, const std::vector<Arr<int64_t>>& parts, int64_t magic,
-                             int64_t hdr_words) {
+                             int64_t hdr_words, int64_t check_word) {
     const int world = static_cast<int>(parts.size());
     Arr<int64_t> flags(world);
     int64_t tot[3] = {0, 0, 0};
@@ -491,6 +525,25 @@ PYBIND11_MODULE(_runtime, m) {
       if (nw < 0 || na < 0 || nr < 0 || hdr_words + 6 * nw + 5 * na + 4 * nr > size)
         throw std::runtime_error("truncated swarm control message");
       n += nw;
+    }
+    if (check_word >= 0 && check_word + 3 <= hdr_words && world > 1) {
+      const int64_t* p0 = parts[0].data();
+      for (int r = 1; r < world; ++r) {
+        const int64_t* p = parts[r].data();
+        if (p[check_word] != p0[check_word]) {
+          std::ostringstream o;
+          o << "swarm directory diverged before round " << p0[6] << " (replica digests "
+            << group_ranks(parts, check_word) << ")";
+          throw SwarmDivergence(o.str());
+        }
+        if (p[check_word + 1] != p0[check_word + 1] || p[check_word + 2] != p0[check_word + 2]) {
+          std::ostringstream o;
+          o << "swarm plans diverged in round " << p0[check_word + 2] << " (plan digests "
+            << group_ranks(parts, check_word + 1) << "; planned rounds " << group_ranks(parts, check_word + 2)
+            << ")";
+          throw SwarmDivergence(o.str());
+        }
+      }
     }
     Arr<int64_t> out({n, int64_t(8)});
     int64_t* o = out.mutable_data();
@@ -525,14 +578,16 @@ PYBIND11_MODULE(_runtime, m) {
     Arr<int64_t> totals(3);
     std::memcpy(totals.mutable_data(), tot, sizeof(tot));
     return py::make_tuple(out, flags, all_leaving, totals);
-  });
+  }, py::arg("directory"), py::arg("parts"), py::arg("magic"), py::arg("hdr_words"), py::arg("check_word") = -1);
   // wants: int64[n, 8] = (key4, size, want_id, rank, want_flags); flags int64[world]
   // -> int64[m, 10] = (key4, size, src, dst, want_id, seeded, reserved); src -1 = CDN fetch,
   // -2 = stage (download from a network origin into host memory for a later round)
   // plan_round_for: the same plan, but only the rows this rank takes part in (src == me or
   // dst == me, canonical order kept) plus whether the round has any P2P transfer at all
-  // (every rank enters the exchange then).  At 8 ranks a rank needs ~1/4 of the rows: the
-  // rest would be built into numpy and masked away in Python every round.
+  // (every rank enters the exchange then) and the 64-bit digest of the full plan (ranks
+  // compare it in the next round's control all-gather, see ingest_control).  At 8 ranks a
+  // rank needs ~1/4 of the rows: the rest would be built into numpy and masked away in
+  // Python every round.
   auto plan_rows = [](const Directory& d, const Arr<int64_t>& wants, const Arr<int64_t>& flags, int world,
                       int me, const py::object& cdn_obj) {
     const int64_t n = wants.size() / 8;
@@ -557,6 +612,7 @@ PYBIND11_MODULE(_runtime, m) {
       cdn.assign(c.data(), c.data() + world);
     }
     plan_round_into(d, w.data(), w.size(), f, world, &t, cdn.empty() ? nullptr : cdn.data());
+    const int64_t digest = static_cast<int64_t>(plan_digest(t));  // of the FULL plan, before filtering
     bool any_p2p = false;
     int64_t m = 0;
     for (const Transfer& x : t) {
@@ -571,17 +627,17 @@ PYBIND11_MODULE(_runtime, m) {
       o[4] = x.size; o[5] = x.src; o[6] = x.dst; o[7] = x.want_id; o[8] = x.seeded; o[9] = 0;
       o += 10;
     }
-    return std::make_pair(out, any_p2p);
+    return std::make_tuple(out, any_p2p, digest);
   };
   m.def("plan_round", [plan_rows](const Directory& d, Arr<int64_t> wants, Arr<int64_t> flags, int world,
                                   py::object cdn_bytes) {
-    return plan_rows(d, wants, flags, world, -1, cdn_bytes).first;
+    return std::get<0>(plan_rows(d, wants, flags, world, -1, cdn_bytes));
   }, py::arg("directory"), py::arg("wants"), py::arg("flags"), py::arg("world"), py::arg("cdn_bytes") = py::none());
   m.def("plan_round_for", [plan_rows](const Directory& d, Arr<int64_t> wants, Arr<int64_t> flags, int world,
                                       int me, py::object cdn_bytes) {
     if (me < 0 || me >= world) throw std::invalid_argument("rank out of range");
     auto r = plan_rows(d, wants, flags, world, me, cdn_bytes);
-    return py::make_tuple(r.first, r.second);
+    return py::make_tuple(std::get<0>(r), std::get<1>(r), std::get<2>(r));
   }, py::arg("directory"), py::arg("wants"), py::arg("flags"), py::arg("world"), py::arg("me"),
      py::arg("cdn_bytes") = py::none());
   // CPU-mode CDN phase: copy origin byte ranges (raw host addresses, as the want table holds

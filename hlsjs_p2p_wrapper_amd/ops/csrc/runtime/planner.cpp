@@ -8,14 +8,33 @@ namespace hlsp2p {
 
 Directory::Directory() { rehash(1024); }
 
+namespace {
+inline uint64_t fmix64(uint64_t x) {  // murmur3 finalizer: full avalanche of every input bit
+  x ^= x >> 33;
+  x *= 0xFF51AFD7ED558CCDull;
+  x ^= x >> 33;
+  x *= 0xC4CEB9FE1A85EC53ull;
+  return x ^ (x >> 33);
+}
+}  // namespace
+
+uint64_t Directory::entry_terms(const Slot& s) {
+  const uint64_t hk = DirKeyHash{}(s.key);
+  uint64_t d = length_term(hk, s.e.length);
+  for (uint64_t m = s.e.holders; m; m &= m - 1) d += holder_term(hk, __builtin_ctzll(m));
+  return d;
+}
+
 void Directory::rehash(size_t cap) {
   std::vector<Slot> old;
   old.swap(slots_);
   slots_.assign(cap, Slot{});
   mask_ = cap - 1;
   size_ = 0;
+  digest_ = 0;  // recomputed: drop_rank edits holder masks in place before re-packing
   for (const Slot& s : old) {
     if (s.e.holders == 0) continue;
+    digest_ += entry_terms(s);
     size_t i = home(s.key);
     while (slots_[i].e.holders != 0) i = (i + 1) & mask_;
     slots_[i] = s;
@@ -25,14 +44,20 @@ void Directory::rehash(size_t cap) {
 
 void Directory::apply_add(int rank, const SegKey& k, int64_t length) {
   if (size_t(size_ + 1) * 2 > slots_.size()) rehash(slots_.size() * 2);
-  size_t i = home(k);
+  const uint64_t hk = DirKeyHash{}(k);
+  size_t i = hk & mask_;
   while (slots_[i].e.holders != 0 && !(slots_[i].key == k)) i = (i + 1) & mask_;
   Slot& s = slots_[i];
+  const uint64_t bit = uint64_t(1) << rank;
   if (s.e.holders == 0) {
     s.key = k;
     ++size_;
+    digest_ += length_term(hk, length);
+  } else if (s.e.length != length) {
+    digest_ += length_term(hk, length) - length_term(hk, s.e.length);
   }
-  s.e.holders |= (uint64_t(1) << rank);
+  if (!(s.e.holders & bit)) digest_ += holder_term(hk, rank);
+  s.e.holders |= bit;
   s.e.length = length;
 }
 
@@ -55,11 +80,15 @@ void Directory::erase_at(size_t i) {
 }
 
 void Directory::apply_remove(int rank, const SegKey& k) {
-  size_t i = home(k);
+  const uint64_t hk = DirKeyHash{}(k);
+  size_t i = hk & mask_;
   while (slots_[i].e.holders != 0) {
     if (slots_[i].key == k) {
-      slots_[i].e.holders &= ~(uint64_t(1) << rank);
+      const uint64_t bit = uint64_t(1) << rank;
+      if (slots_[i].e.holders & bit) digest_ -= holder_term(hk, rank);
+      slots_[i].e.holders &= ~bit;
       if (slots_[i].e.holders == 0) {
+        digest_ -= length_term(hk, slots_[i].e.length);
         slots_[i].e.holders = 1;  // still occupied while erase_at shifts the run
         erase_at(i);
       }
@@ -422,6 +451,18 @@ void plan_round_into(const Directory& dir, const Want* wants_in, size_t n_in, co
   out.reserve(cdn.size() + p2p.size());
   out.insert(out.end(), cdn.begin(), cdn.end());
   out.insert(out.end(), p2p.begin(), p2p.end());
+}
+
+uint64_t plan_digest(const std::vector<Transfer>& plan) {
+  uint64_t h = 0x243F6A8885A308D3ull ^ plan.size();
+  for (const Transfer& t : plan) {
+    h = fmix64(h ^ ((uint64_t(t.key.swarm) << 32 | t.key.level) + 0x9E3779B97F4A7C15ull));
+    h = fmix64(h ^ (uint64_t(t.key.url_id) << 32 | t.key.sn));
+    h = fmix64(h ^ uint64_t(t.size));
+    h = fmix64(h ^ (uint64_t(uint32_t(t.src)) << 32 | uint32_t(t.dst)));
+    h = fmix64(h ^ uint64_t(t.want_id) ^ (uint64_t(t.seeded) << 63));
+  }
+  return h;
 }
 
 std::vector<Transfer> plan_round(const Directory& dir, const std::vector<Want>& wants_in,

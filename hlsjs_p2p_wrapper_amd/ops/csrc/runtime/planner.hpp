@@ -94,6 +94,12 @@ class Directory {
   void drop_rank(int rank);  // a rank left: forget everything it held
   const DirEntry* find(const SegKey& k) const;
   int64_t size() const { return size_; }
+  // Order-independent 64-bit digest of the whole content (every key with its holder mask
+  // and length), kept up to date by every add / remove in O(1).  Every rank replays the same
+  // deltas into its replica, so the replicas' digests must agree at every round; ranks
+  // compare them in the control all-gather and stop before planning on a divergent state
+  // (a two-sided transport would otherwise hang in a send/recv group nobody matches).
+  uint64_t digest() const { return digest_; }
 
  private:
   struct Slot {
@@ -103,7 +109,18 @@ class Directory {
   size_t home(const SegKey& k) const { return DirKeyHash{}(k) & mask_; }
   void rehash(size_t cap);
   void erase_at(size_t i);
+  // digest terms: one per (key, holder rank) and one per (key, length), summed mod 2^64 --
+  // an add or remove changes one or two terms (one multiply each), so the digest costs
+  // ~1 ns per delta on the control path instead of re-hashing the entry
+  static uint64_t holder_term(uint64_t hk, int rank) {
+    return (hk + uint64_t(rank + 1) * 0x9E3779B97F4A7C15ull) * 0xD6E8FEB86659FD93ull;
+  }
+  static uint64_t length_term(uint64_t hk, int64_t length) {
+    return (hk ^ (uint64_t(length) * 0xA0761D6478BD642Full)) * 0xE7037ED1A0B428DBull;
+  }
+  static uint64_t entry_terms(const Slot& s);
   std::vector<Slot> slots_;
+  uint64_t digest_ = 0;
   size_t mask_ = 0;
   int64_t size_ = 0;
 };
@@ -111,6 +128,11 @@ class Directory {
 // Returns every transfer of the round (CDN fetches have src = -1), in a canonical order:
 // all CDN fetches first, then P2P transfers grouped by (src, dst) in key order — the order
 // in which both sides pack / unpack their per-pair buffers.
+// Order-sensitive 64-bit digest of a plan (every row's key, size, src, dst, want id,
+// seeded): identical inputs give identical plans, so every rank's digest of a round's FULL
+// plan must agree; a rank that planned differently would post sends or receives nobody matches.
+uint64_t plan_digest(const std::vector<Transfer>& plan);
+
 std::vector<Transfer> plan_round(const Directory& dir, const std::vector<Want>& wants,
                                  const std::vector<int64_t>& rank_flags, int world);
 // The same plan written into `out` (cleared first; its capacity is reused round to round).

@@ -65,6 +65,9 @@ class SwarmComm:
     def close(self) -> None:
         pass
 
+    def abort(self) -> None:
+        """Error path: stop the data plane without waiting on peers (no-op by default)."""
+
 
 class LocalComm(SwarmComm):
     def __init__(self) -> None:
@@ -207,19 +210,31 @@ class DistComm(SwarmComm):
         dev = None
         ok = True
         uid: List[object] = [None]
+        gpu = None
         try:
             from ..ops._native import device as _dev
 
             dev = _dev()
             dev.rccl_version()
+            gpu = dev.pci_bus_id(torch.cuda.current_device())
             if self.rank == 0:  # a failure here is reported through the all-gather below
                 uid[0] = dev.rccl_unique_id()
         except Exception:  # noqa: BLE001 - no native module / RCCL: torch's path
             ok = False
         flags: List[object] = [None] * self.world_size
-        dist.all_gather_object(flags, ok, group=g)
-        if not all(flags):
+        dist.all_gather_object(flags, (ok, _host_id(), gpu), group=g)
+        if not all(f[0] for f in flags):  # type: ignore[index]
             return None
+        # one GPU per rank: RCCL cannot place two ranks of a communicator on one device (it
+        # fails deep inside ncclCommInitRank, or worse, a launcher mapped ranks onto a shared
+        # card silently); every rank sees the same table, so every rank raises here together
+        seen: dict = {}
+        for r, (_, host, bus) in enumerate(flags):  # type: ignore[misc]
+            if (host, bus) in seen:
+                raise RuntimeError(f"RCCL data plane: ranks {seen[(host, bus)]} and {r} would share GPU {bus} on "
+                                   f"host {host[0]}; RCCL needs one GPU per rank (rehearse ranks that share a "
+                                   "GPU with --dist-backend ipc or gloo)")
+            seen[(host, bus)] = r
         dist.broadcast_object_list(uid, src=0, group=g)
         comm, err = None, ""
         try:
@@ -245,13 +260,8 @@ class DistComm(SwarmComm):
         if os.environ.get("HLSP2P_CONTROL", "auto") == "gloo":
             return None
         dist, g = self.dist, self.control_group
-        try:
-            with open("/proc/sys/kernel/random/boot_id") as f:
-                boot = f.read().strip()
-        except OSError:
-            boot = ""
         hosts: List[object] = [None] * self.world_size
-        dist.all_gather_object(hosts, (socket.gethostname(), boot), group=g)
+        dist.all_gather_object(hosts, _host_id(), group=g)
         if any(h != hosts[0] for h in hosts):
             return None
         from ..ops._native import runtime as _rt
@@ -373,6 +383,29 @@ class DistComm(SwarmComm):
         if self._ipc is not None:
             self._ipc.close()
 
+    def abort(self) -> None:
+        """Error path (e.g. replicated state diverged): abort the native RCCL communicator
+        without synchronising the device -- transfers already posted may never be matched, so
+        waiting for them would hang; ``ncclCommAbort`` returns regardless.  The IPC rehearsal
+        plane's buffers stay mapped until the process exits (peers may still be copying)."""
+        if self._rccl is not None:
+            self._rccl.abort()
+
+    def topology(self) -> dict:
+        """What the data plane reports about itself: for the native RCCL communicator, the
+        rank count and rank RCCL holds (``ncclCommCount`` / ``ncclCommUserRank``), the HIP
+        device it runs on (``ncclCommCuDevice``), the rounds posted and the RCCL version."""
+        out = {"transport": self.data_transport, "world": self.world_size, "rank": self.rank}
+        if self._rccl is not None and not self._rccl.closed:
+            from ..ops._native import device as _dev
+
+            out["rccl"] = {"count": int(self._rccl.comm_count()), "rank": int(self._rccl.comm_user_rank()),
+                           "device": int(self._rccl.comm_device()), "rounds": int(self._rccl.rounds),
+                           "version": _dev().rccl_version()}
+        if self._ipc is not None:
+            out["ipc_exchanges"] = int(self._ipc.exchanges)
+        return out
+
     def _exchange_staged(self, sends, recvs) -> None:
         """gloo data plane with GPU tensors (several ranks sharing one GPU, e.g. rehearsing
         the multi-rank path on a single MI355X): stage through host memory.  Synchronous
@@ -404,6 +437,16 @@ class DistComm(SwarmComm):
             self._shm.barrier(self.control_timeout_s)
             return
         self.dist.barrier(group=self.control_group)
+
+
+def _host_id() -> Tuple[str, str]:
+    """``(hostname, boot id)``: ranks with equal ids share a host (and its /dev/shm)."""
+    try:
+        with open("/proc/sys/kernel/random/boot_id") as f:
+            boot = f.read().strip()
+    except OSError:
+        boot = ""
+    return socket.gethostname(), boot
 
 
 def _as_bytes(t: torch.Tensor) -> torch.Tensor:
@@ -485,13 +528,8 @@ class _IpcOutbox:
     @classmethod
     def open(cls, comm: "DistComm") -> Optional["_IpcOutbox"]:
         dist, g = comm.dist, comm.control_group
-        try:
-            with open("/proc/sys/kernel/random/boot_id") as f:
-                boot = f.read().strip()
-        except OSError:
-            boot = ""
         hosts: List[object] = [None] * comm.world_size
-        dist.all_gather_object(hosts, (socket.gethostname(), boot), group=g)
+        dist.all_gather_object(hosts, _host_id(), group=g)
         if any(h != hosts[0] for h in hosts):
             return None
         box = cls(comm)

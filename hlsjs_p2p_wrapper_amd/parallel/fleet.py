@@ -197,6 +197,7 @@ class RemoteNode:
         self.batches = 0  # answer batches handled (reported to the node, which paces on it)
         self._reported = 0
         self._ring = _ShmRing()
+        self.payload_revoked = False
         if payload:
             self._out.append(("payload", True))
 
@@ -327,6 +328,10 @@ class RemoteNode:
                     self.stats["upload"] = st["upload"]
                     self.swarm_stats = st["swarm"]
                     self.peer_online = np.asarray(st["online"], dtype=bool)
+            elif msg[0] == "revoke":  # the node stopped this player's payloads (it stalled on its acks)
+                log.warning("fleet player (rank %d): the node stopped sending fragment bytes to this player; "
+                            "onSuccess payloads arrive without data from now on", self.rank)
+                self.payload_revoked = True
             else:  # a control message ("mark", "stop"): the player acts on it before reading on
                 self.control.append(msg)
                 return n
@@ -472,12 +477,27 @@ class _PayloadRing:
     so one asynchronous D2H per transmux batch lands the bytes where the players read them --
     no host copy.  Regions are handed out in FIFO order; a region is reused only after every
     player it was sent to has acknowledged that answer batch (players read their fragments as
-    zero-copy views while they handle the batch)."""
+    zero-copy views while they handle the batch).
+
+    The segment's pages are reserved up front (``posix_fallocate``: a /dev/shm too small for
+    it fails here with a clear error instead of a SIGBUS on first touch), and a failed HIP
+    registration leaves the ring unpinned: the rank then stages each batch through a pinned
+    bounce buffer and copies it in on the host (``pinned`` False)."""
 
     def __init__(self, nbytes: int, pin: bool = False) -> None:
         from multiprocessing import shared_memory
 
         self.shm = shared_memory.SharedMemory(create=True, size=nbytes)
+        try:
+            fd = getattr(self.shm, "_fd", -1)
+            if fd >= 0:
+                os.posix_fallocate(fd, 0, nbytes)
+        except OSError as e:
+            self.shm.close()
+            self.shm.unlink()
+            raise RuntimeError(f"cannot reserve a {nbytes}-byte payload ring in /dev/shm ({e}); lower "
+                               "HLSP2P_FLEET_PAYLOAD_BYTES or the fragments in flight") from e
+        self.cap = nbytes
         self.buf = np.ndarray((nbytes,), dtype=np.uint8, buffer=self.shm.buf)
         self.head = 0
         self.wraps = 0
@@ -487,28 +507,33 @@ class _PayloadRing:
         if pin:
             import torch
 
-            self.buf[::4096] = 0  # fault the pages in before pinning
             err = torch._C._cudart.cudaHostRegister(self.buf.ctypes.data, nbytes, 0)
-            if int(err) != 0:
-                raise RuntimeError(f"hipHostRegister of the {nbytes}-byte payload ring failed: {err}")
-            self.pinned = True
-            self.tensor = torch.from_numpy(self.buf)
+            if int(err) == 0:
+                self.pinned = True
+                self.tensor = torch.from_numpy(self.buf)
+            else:
+                log.warning("hipHostRegister of the %d-byte payload ring failed (%s): staging payloads through a "
+                            "pinned bounce buffer instead", nbytes, err)
 
-    def place(self, total: int, released) -> Tuple[int, list]:
-        """``(start, region)`` of a ``total``-byte region (wrapping); ``region[2]`` takes the
-        players' batch numbers once sent.  ``released(need)`` returns once the oldest live
-        region may be reused (it may wait); it is called until the new region is free."""
-        cap = len(self.buf)
-        if total > cap:
-            raise RuntimeError(f"payload ring of {cap} bytes cannot hold a {total}-byte batch "
-                               "(HLSP2P_FLEET_PAYLOAD_BYTES)")
-        start = self.head
-        if start + total > cap:
-            start = 0
-            self.wraps += 1
-        while any(s < start + total and start < e for s, e, _ in self.live):
-            released(self.live[0][2])  # the oldest first: waits for the players' acknowledgements
+    def release_done(self, acked) -> None:
+        """Drop the oldest regions whose players have all acknowledged them (no waiting)."""
+        while self.live and self.live[0][2] is not None and acked(self.live[0][2]):
             self.live.popleft()
+
+    def try_place(self, total: int) -> Optional[Tuple[int, list]]:
+        """``(start, region)`` of a free ``total``-byte region after the head (wrapping), or
+        None while it would overlap a live region; ``region[2]`` takes the players' batch
+        numbers once the batch is sent."""
+        if total > self.cap:
+            return None
+        start = self.head
+        wrapped = start + total > self.cap
+        if wrapped:
+            start = 0
+        if any(s < start + total and start < e for s, e, _ in self.live):
+            return None
+        if wrapped:
+            self.wraps += 1
         region = [start, start + total, None]
         self.live.append(region)
         self.head = start + total
@@ -528,6 +553,14 @@ class _PayloadRing:
             self.shm.unlink()
         except (BufferError, FileNotFoundError):
             pass
+
+
+def _shm_free_bytes() -> Optional[int]:
+    try:
+        st = os.statvfs("/dev/shm")
+    except OSError:
+        return None
+    return st.f_bavail * st.f_frsize
 
 
 class FleetServer:
@@ -550,7 +583,11 @@ class FleetServer:
         self._down = [True] * W
         self._payload = [False] * W
         self._ring: Optional[_PayloadRing] = None
+        self._retired: List[_PayloadRing] = []  # replaced rings, closed once their regions are released
+        self._bounce = None  # pinned staging of an unpinned ring's batches
         self._pstream = None  # side stream of the payload gathers + D2H
+        self.ring_ack_timeout_s = float(os.environ.get("HLSP2P_FLEET_ACK_TIMEOUT", "10"))
+        self.revoked: set = set()  # players whose payloads were stopped (stalled on their acks)
         self.payload_bytes = 0  # copied into the payload ring
         self.payload_wait_s = 0.0  # host time blocked on a batch's payload D2H
         self._delivered: List[tuple] = []  # delivery columns from the node, not transmuxed yet
@@ -707,10 +744,12 @@ class FleetServer:
         tok, src, nbytes, cdn_ms, p2p_ms, offs, eids, expect, pay = tag
         ring_off = None
         if pay is not None:
-            ring_off, region, ev = pay
+            ring_off, region, ev, post = pay
             if ev is not None:
                 t0 = time.perf_counter()
                 ev.synchronize()  # the batch's D2H into the ring (queued at launch)
+                if post is not None:  # unpinned ring: the bounce buffer's bytes go in on the host
+                    post()
                 self.payload_wait_s += time.perf_counter() - t0
         if expect is not None:  # deferred receive checks: the node commits or re-fetches
             chk = expect >= 0
@@ -745,19 +784,17 @@ class FleetServer:
         if not want.any():
             return None
         arena = self.node.arena
-        if self._ring is None:
-            self._ring = _PayloadRing(int(os.environ.get("HLSP2P_FLEET_PAYLOAD_BYTES", str(4 << 30))),
-                                      pin=arena.is_cuda)
         idx = np.flatnonzero(want)
         n = lens[idx]
         al = (n + 63) // 64 * 64
         pack = np.concatenate([[0], np.cumsum(al)[:-1]]).astype(np.int64)
         total = int(al.sum())
-        start, region = self._ring.place(total, self._ring_released)
+        self._reap_retired()
+        ring, (start, region) = self._place(total)
         self.payload_bytes += total
         ring_off = np.full(len(w), -1, dtype=np.int64)
         ring_off[idx] = start + pack
-        ev = None
+        ev = post = None
         if arena.is_cuda:
             import torch
 
@@ -770,30 +807,114 @@ class FleetServer:
             with torch.cuda.stream(ps):  # staging allocated, used and freed in ps's stream order
                 staged = torch.empty(max(total, 1), dtype=torch.uint8, device=arena.device)
                 _seg.copy_segments(arena, staged, offs[idx], pack, n)
-                self._ring.tensor[start:start + total].copy_(staged[:total], non_blocking=True)
+                if ring.pinned:
+                    ring.tensor[start:start + total].copy_(staged[:total], non_blocking=True)
+                else:  # registration failed: D2H into a pinned bounce buffer, host copy at completion
+                    if self._bounce is None or self._bounce.numel() < total:
+                        self._bounce = torch.empty(max(total, 64 << 20), dtype=torch.uint8, pin_memory=True)
+                    bounce = self._bounce
+                    bounce[:total].copy_(staged[:total], non_blocking=True)
+
+                    def post(buf=ring.buf, bounce=bounce, start=start, total=total):
+                        buf[start:start + total] = bounce[:total].numpy()
                 ev = torch.cuda.Event()
                 ev.record(ps)
         else:
-            host, buf = arena.numpy(), self._ring.buf
+            host, buf = arena.numpy(), ring.buf
             for o, p, k in zip(offs[idx].tolist(), (start + pack).tolist(), n.tolist()):
                 buf[p:p + k] = host[o:o + k]
-        return ring_off, region, ev
+        return ring_off, region, ev, post
 
-    def _ring_released(self, need) -> None:
-        """Wait until every player a ring region was sent to has acknowledged that batch."""
-        if need is None:
-            raise RuntimeError("payload ring too small for the transmux batches in flight "
-                               "(raise HLSP2P_FLEET_PAYLOAD_BYTES)")
+    # -------------------------------------------------------------- payload ring
+    def _acked(self, need) -> bool:
+        return all(not self.open[p] or self.batches_done[p] >= k for p, k in need.items())
+
+    RING_MIN = 256 << 20  # smallest automatic payload ring
+
+    def _new_ring(self, total: int) -> _PayloadRing:
+        """A (bigger) payload ring; the current one is retired, kept until every region on it
+        is acknowledged.  Size: ``HLSP2P_FLEET_PAYLOAD_BYTES`` for the first ring, else room
+        for 4 batches of this size (>= 256 MiB, doubling on growth), capped to half of the
+        free /dev/shm, and never below 2 batches."""
+        old = self._ring
+        env = os.environ.get("HLSP2P_FLEET_PAYLOAD_BYTES")
+        if old is None and env:
+            size = int(env)
+        else:
+            size = max(self.RING_MIN, 4 * total, 2 * old.cap if old is not None else 0)
+            size = (size + (1 << 20) - 1) // (1 << 20) * (1 << 20)
+            free = _shm_free_bytes()
+            if free is not None:
+                size = min(size, free // 2)
+            if size < 2 * total:
+                raise RuntimeError(f"/dev/shm has {free} bytes free: too little for a payload ring of two "
+                                   f"{total}-byte batches (lower the fragments in flight)")
+        ring = _PayloadRing(size, pin=self.node.arena.is_cuda)
+        if old is not None:
+            if old.live:
+                self._retired.append(old)
+            else:
+                old.close()
+        self._ring = ring
+        return ring
+
+    def _reap_retired(self) -> None:
+        for ring in list(self._retired):
+            ring.release_done(self._acked)
+            if not ring.live:
+                ring.close()
+                self._retired.remove(ring)
+
+    def _place(self, total: int):
+        """A ring region for a ``total``-byte batch.  Regions free in FIFO order once their
+        players acknowledged them; when the next region is still held by a batch in flight
+        (the ring is too small for the batches in flight) or by players that do not
+        acknowledge within ``HLSP2P_FLEET_ACK_TIMEOUT`` s, the rank moves to a bigger ring
+        instead of failing -- and stops sending payloads to the stalled players (their
+        regions stay valid on the retired ring until they acknowledge or leave)."""
+        ring = self._ring
+        if ring is None or total > ring.cap:
+            ring = self._new_ring(total)
+        while True:
+            ring.release_done(self._acked)
+            got = ring.try_place(total)
+            if got is not None:
+                return ring, got
+            need = ring.live[0][2]
+            if need is None or not self._wait_acks(need):
+                if need is not None:
+                    self._revoke([p for p, k in need.items() if self.open[p] and self.batches_done[p] < k])
+                ring = self._new_ring(total)
+
+    def _wait_acks(self, need) -> bool:
+        """Wait up to ``ring_ack_timeout_s`` for the players of a region to acknowledge it."""
         from multiprocessing.connection import wait
 
-        end = time.monotonic() + 60.0
-        while not all(not self.open[p] or self.batches_done[p] >= k for p, k in need.items()):
+        end = time.monotonic() + self.ring_ack_timeout_s
+        while not self._acked(need):
             if time.monotonic() > end:
-                raise RuntimeError("fleet players did not acknowledge their payload batches in 60 s")
+                return False
             conns = [c for p, c in enumerate(self.conns) if self.open[p]]
             if conns:
                 wait(conns, timeout=0.005)
             self.poll()
+        return True
+
+    def _revoke(self, players: List[int]) -> None:
+        """Stop sending payloads to players that stopped acknowledging their answer batches:
+        one stalled player must not stall (or fail) the rank's other players.  The player is
+        told (``("revoke",)``): its later fragments arrive without bytes."""
+        for p in players:
+            if p in self.revoked:
+                continue
+            self.revoked.add(p)
+            self._payload[p] = False
+            log.warning("fleet player %d did not acknowledge its payload batches in %.0f s: no more payloads for "
+                        "it", p, self.ring_ack_timeout_s)
+            try:
+                self.conns[p].send(("revoke",))
+            except (OSError, BrokenPipeError):
+                self.open[p] = False
 
     def send(self) -> int:
         """One answer batch per player (plus the swarm state the agents' stats read)."""
@@ -851,7 +972,10 @@ class FleetServer:
             self.poll()
 
     def close(self) -> None:
-        """Release the payload ring (after the players stopped)."""
+        """Release the payload rings (after the players stopped)."""
+        for ring in self._retired:
+            ring.close()
+        self._retired = []
         if self._ring is not None:
             self._ring.close()
             self._ring = None

@@ -308,24 +308,28 @@ class MediaPipeline:
                 vi = np.flatnonzero(expect >= 0)
                 got = _rt().crc32_batch(src.numpy(), offs[vi], nb[vi])
                 b.verify = [(vi, (got.astype(np.int64) & 0xFFFFFFFF) == (expect[vi] & 0xFFFFFFFF))]
+                b.expect_mask = expect >= 0
             return b
         ok = ~(enc & ((nb <= 0) | (nb % 16 != 0)))  # encrypted payloads must be whole AES blocks
         idx_ok = np.flatnonzero(ok)
-        if not len(idx_ok):
-            return _Batch(None, infos=[], host=[], event=None, tag=tag, n=n)
         verify = []
         ex = None
         if expect is not None:
-            clear_v = np.flatnonzero((expect >= 0) & ~enc)
-            if len(clear_v):  # clear fragments: the CRC kernel (no decrypt pass to fuse into)
+            # bytes with an expected CRC that no decrypt pass reads -- clear fragments, and
+            # encrypted ones rejected for their length -- go through the CRC kernel: every
+            # fragment that asked for a check gets one (complete_columns reports the rest False)
+            crc_v = np.flatnonzero((expect >= 0) & (~enc | ~ok))
+            if len(crc_v):
                 from ..ops import crc as _crc
 
-                _, okd = _crc.crc32_batch(src, offs[clear_v], nb[clear_v],
-                                          expect=(expect[clear_v] & 0xFFFFFFFF).tolist())
-                okh = torch.empty(len(clear_v), dtype=torch.uint8, pin_memory=True)
+                _, okd = _crc.crc32_batch(src, offs[crc_v], nb[crc_v], expect=(expect[crc_v] & 0xFFFFFFFF).tolist())
+                okh = torch.empty(len(crc_v), dtype=torch.uint8, pin_memory=True)
                 okh.copy_(okd, non_blocking=True)
-                verify.append((clear_v, okh))
-            ex = np.where(enc, expect, -1)[ok] if (expect[enc] >= 0).any() else None
+                verify.append((crc_v, okh))
+            ex = np.where(enc, expect, -1)[ok] if (expect[enc & ok] >= 0).any() else None
+        if not len(idx_ok):  # nothing to decrypt or demux (the CRC checks above still run)
+            return _Batch(None, infos=[], host=[], event=self._event() if verify else None, tag=tag, n=n,
+                          verify=verify or None, expect_mask=None if expect is None else expect >= 0)
         if not ok.all():
             offs, nb, enc, drk, iv = offs[ok], nb[ok], enc[ok], drk[ok], iv[ok]
         td0, isb = _aes.device_tables(self.device)
@@ -347,7 +351,7 @@ class MediaPipeline:
         ev = self._event()
         self.timer.add("launch_columns", time.perf_counter() - t1)
         return _Batch(None, infos=infos, host=host, event=ev, keep=(dec, host_block), tag=tag, n=n, start=ev0,
-                      verify=verify or None)
+                      verify=verify or None, expect_mask=None if expect is None else expect >= 0)
 
     def launch_jobs(self, jobs: List[TransmuxJob]) -> "_Batch":
         """:meth:`launch` for an explicit job list (the pipeline's own queue untouched)."""
@@ -379,8 +383,11 @@ class MediaPipeline:
 
     @staticmethod
     def _verified(batch: "_Batch", n: int) -> np.ndarray:
-        """Per fragment: passed its CRC check (True where none was asked); call after the wait."""
+        """Per fragment: passed its CRC check (True where none was asked); call after the wait.
+        A fragment that asked for a check is True only if a check actually ran and passed."""
         out = np.ones(n, dtype=bool)
+        if batch.expect_mask is not None:
+            out[batch.expect_mask] = False
         for idx, ok in batch.verify or ():
             out[idx] = (ok.numpy() if isinstance(ok, torch.Tensor) else np.asarray(ok)).astype(bool)
         return out
@@ -529,6 +536,7 @@ class _Batch:
     n: int = 0  # launch_columns: fragments in the batch
     start: Any = None  # timing event recorded before the batch's first launch
     verify: Any = None  # [(fragment indices, ok flags (pinned uint8 / bool))] of expect-CRC checks
+    expect_mask: Any = None  # bool[n]: fragments that asked for a CRC check (unchecked ones fail)
 
 
 _local = threading.local()

@@ -7,7 +7,8 @@ and lands in the middle of a swarm round.  After start-up, :func:`tune_gc` moves
 everything alive into the permanent generation (``gc.freeze``) and raises the gen-0
 threshold, so collections only look at young objects.  The per-fragment churn (loader
 stats, event payloads, closures) is mostly freed by reference counting anyway.  GC stays
-enabled: new cycles are still collected.
+enabled: new cycles are still collected, and every few full passes one of them traverses the
+whole (thawed) heap, so a cycle that formed among frozen objects is reclaimed too.
 
 :func:`bind_to_gpu_numa` keeps a peer's host side on the NUMA node its GPU hangs off: the
 CPUs it runs on (the host path is one Python thread per GPU) and, through first touch, the
@@ -21,11 +22,14 @@ import time
 from typing import List, Optional, Tuple
 
 
-def tune_gc(gen0_threshold: int = 50_000) -> Tuple[int, int, int]:
+def tune_gc(gen0_threshold: int = 50_000, thaw_every: int = 4) -> Tuple[int, int, int]:
     """Collect once, freeze the surviving heap, raise the gen-0 threshold.
 
-    Call it after the player / node / origin are set up (``bench.py`` does).  Returns the
-    previous thresholds."""
+    Call it after the player / node / origin are set up (``bench.py`` does).  Every
+    ``thaw_every``-th full collection first thaws the frozen heap, so objects that were alive
+    at a freeze and became cyclic garbage since (a request, a loader context or a round handle
+    in flight when a full pass ran) are reclaimed instead of leaking.  Returns the previous
+    thresholds."""
     prev = gc.get_threshold()
     gc.collect()
     gc.freeze()
@@ -37,6 +41,7 @@ def tune_gc(gen0_threshold: int = 50_000) -> Tuple[int, int, int]:
     # would make every later full pass longer: over 3,000 HBM-origin bench steps the step time
     # drifted +16 % with the GC on and stayed flat with it off (profiles/r4_gc).  Freezing what
     # survives each full pass keeps the next one proportional to what is new since.
+    _freeze_after_full.thaw_every = max(1, int(thaw_every))
     if _freeze_after_full not in gc.callbacks:
         gc.callbacks.append(_freeze_after_full)
     if os.environ.get("HLSP2P_GC_DISABLE") == "1":  # diagnostic: no cyclic GC after start-up at all
@@ -44,10 +49,30 @@ def tune_gc(gen0_threshold: int = 50_000) -> Tuple[int, int, int]:
     return prev
 
 
-def _freeze_after_full(phase: str, info: dict) -> None:
-    """gc callback: move the survivors of a full (gen-2) collection to the permanent generation."""
-    if phase == "stop" and info.get("generation") == 2:
-        gc.freeze()
+class _FullPassFreezer:
+    """gc callback: move the survivors of a full (gen-2) collection to the permanent
+    generation; every ``thaw_every``-th full pass starts by thawing it (``gc.unfreeze`` merges
+    the permanent generation into gen 2 before the pass runs), so that pass traverses the
+    whole heap once and frees cycles among formerly frozen objects."""
+
+    def __init__(self) -> None:
+        self.thaw_every = 4
+        self.full_passes = 0
+        self.thaws = 0
+
+    def __call__(self, phase: str, info: dict) -> None:
+        if info.get("generation") != 2:
+            return
+        if phase == "start":
+            self.full_passes += 1
+            if self.full_passes % self.thaw_every == 0:
+                gc.unfreeze()
+                self.thaws += 1
+        elif phase == "stop":
+            gc.freeze()
+
+
+_freeze_after_full = _FullPassFreezer()
 
 
 def cpu_calibration_us(n: int = 20_000, reps: int = 3) -> float:

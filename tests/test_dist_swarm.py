@@ -156,7 +156,80 @@ def _check_per_rank(res, world):
         assert 0 <= r["p2p_links"] <= world - 1
     # (which rank receives depends on the players' relative pace: the swarm as a whole does)
     assert sum(r["p2p_recv_MB"] for r in rows) > 0 and sum(r["p2p_sent_MB"] for r in rows) > 0
-    assert res["data_plane"]["data"] == "gloo" and res["data_plane"]["control"] == "shm"
+    dp = res["data_plane"]
+    assert dp["data"] == "gloo" and dp["control"] == "shm"
+    # topology proof: every rank's row, its data plane's own view of the
+    # world, and the bytes it received per source peer (matching the per-rank P2P totals)
+    assert dp["world"] == world and [r["rank"] for r in dp["ranks"]] == list(range(world))
+    for r, pr in zip(dp["ranks"], rows):
+        assert r["comm"]["world"] == world and r["comm"]["rank"] == r["rank"]
+        assert len(r["recv_bytes_from"]) == world and r["recv_bytes_from"][r["rank"]] == 0
+        assert r["rounds"] >= res["steps"]
+        assert sum(r["recv_bytes_from"]) / 1e6 == pytest.approx(pr["p2p_recv_MB"] * pr["rounds"], rel=0.01, abs=0.01)
+
+
+def _bench_plain(*extra: str, timeout: int = 300):
+    """``python bench.py ...`` with NO launcher (the driver's BENCH command shape)."""
+    import subprocess
+    import sys
+    from pathlib import Path
+
+    repo = Path(__file__).resolve().parents[1]
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    env["PYTHONPATH"] = str(repo)
+    return subprocess.run([sys.executable, str(repo / "bench.py"), *extra], cwd=repo, env=env, capture_output=True,
+                          text=True, timeout=timeout)
+
+
+def test_bench_gpus_n_self_launches_n_ranks():
+    """a plain ``python bench.py --gpus 4`` (no torchrun) runs 4 ranks --
+    the parent starts them as a torch.distributed.run child before touching any device,
+    forwards rank 0's JSON line, and the record proves the world it ran: n_gpus 4, four rank
+    rows, 3/4 offload, each rank's bytes received per source peer."""
+    p = _bench_plain("--cpu", "--gpus", "4", "--players", "2", "--config", "hostcost-micro", "--steps", "8",
+                     "--warmup", "2", "--inflight", "8", "--pool", "8", "--cache-gb", "0.5")
+    assert p.returncode == 0, p.stderr[-4000:]
+    lines = [ln for ln in p.stdout.splitlines() if ln.strip()]
+    assert len(lines) == 1  # exactly the result line on stdout
+    import json
+
+    res = json.loads(lines[0])
+    assert res["n_gpus"] == 4 and res["errors"] == 0 and res["value"] > 0
+    assert 0.6 < res["offload_ratio"] <= 0.8
+    dp = res["data_plane"]
+    assert dp["launcher"] == "self" and dp["world"] == 4
+    assert [r["rank"] for r in dp["ranks"]] == [0, 1, 2, 3]
+    for r in dp["ranks"]:
+        assert r["comm"]["world"] == 4 and r["comm"]["rank"] == r["rank"]
+        assert len(r["recv_bytes_from"]) == 4 and r["recv_bytes_from"][r["rank"]] == 0
+    recv = sum(sum(r["recv_bytes_from"]) for r in dp["ranks"])
+    assert recv > 0
+    _check_per_rank(res, 4)
+
+
+def test_bench_gpus_must_match_the_launcher_world():
+    import subprocess
+    import sys
+    from pathlib import Path
+
+    repo = Path(__file__).resolve().parents[1]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "4", "--master-addr",
+           "127.0.0.1", "--master-port", str(_free_port()), str(repo / "bench.py"), "--cpu", "--gpus", "2",
+           "--steps", "2", "--warmup", "1", "--players", "0", "--config", "hostcost-micro"]
+    p = subprocess.run(cmd, cwd=repo, env=dict(os.environ, PYTHONPATH=str(repo)), capture_output=True, text=True,
+                       timeout=300)
+    assert p.returncode != 0
+    assert "--gpus 2 but the launcher started 4 ranks" in p.stderr
+    assert not [ln for ln in p.stdout.splitlines() if ln.startswith("{")]
+
+
+def test_bench_self_launch_reports_a_failing_rank():
+    """A rank that fails makes the self-launched job exit non-zero with no result line."""
+    p = _bench_plain("--cpu", "--gpus", "2", "--players", "0", "--config", "hostcost-micro", "--steps", "2",
+                     "--warmup", "1", "--live-window", "3", "--cache-gb", "-1")
+    assert p.returncode != 0
+    assert not [ln for ln in p.stdout.splitlines() if ln.startswith("{")]
+    assert "failed" in p.stderr
 
 
 def _peer4(rank: int, world: int, port: int, q) -> None:

@@ -145,27 +145,76 @@ def test_payload_ring_reuses_regions_only_after_acknowledgement(monkeypatch):
     from hlsjs_p2p_wrapper_amd.parallel.fleet import _PayloadRing
 
     ring = _PayloadRing(1000)
-    waited = []
+    done = {0: 0}
+
+    def acked(need):
+        return all(done[p] >= k for p, k in need.items())
+
     try:
-        s0, r0 = ring.place(400, lambda need: waited.append(need))
+        s0, r0 = ring.try_place(400)
         r0[2] = {0: 1}
-        s1, r1 = ring.place(400, lambda need: waited.append(need))
+        s1, r1 = ring.try_place(400)
         r1[2] = {0: 2}
-        assert (s0, s1) == (0, 400) and not waited
-        s2, _ = ring.place(400, lambda need: waited.append(need))  # wraps: must free region 0 first
-        assert s2 == 0 and waited == [{0: 1}]
-        with pytest.raises(RuntimeError):
-            ring.place(2000, lambda need: None)
-        ring.live[0][2] = None  # a region queued but not sent yet cannot be freed
-
-        def refuse(need):
-            if need is None:
-                raise RuntimeError("ring too small")
-
-        with pytest.raises(RuntimeError):
-            ring.place(900, refuse)
+        assert (s0, s1) == (0, 400)
+        assert ring.try_place(400) is None  # wraps onto region 0: not acknowledged yet
+        ring.release_done(acked)
+        assert len(ring.live) == 2
+        done[0] = 1
+        ring.release_done(acked)
+        s2, r2 = ring.try_place(400)
+        assert s2 == 0 and ring.wraps == 1 and len(ring.live) == 2
+        assert ring.try_place(2000) is None  # larger than the ring
+        done[0] = 5
+        ring.release_done(acked)  # region 2 was never sent (need None): it stays
+        assert ring.live[0] is r2
     finally:
         ring.close()
+
+
+class _StubNode:
+    def __init__(self):
+        self.arena = torch.zeros(1 << 20, dtype=torch.uint8)
+        self.verify_deferred = False
+
+    def set_bulk_sink(self, sink):
+        pass
+
+
+def test_payload_ring_grows_instead_of_failing_and_revokes_stalled_players(monkeypatch):
+    """a ring too small for the batches in flight, or a player that stops
+    acknowledging, must not raise inside the rank (one stalled player would take down every
+    other player of the rank).  The rank moves to a bigger ring -- the old one stays mapped
+    until its regions are acknowledged -- and stops sending payloads to the stalled player,
+    telling it so."""
+    monkeypatch.setenv("HLSP2P_FLEET_PAYLOAD_BYTES", str(1 << 20))
+    monkeypatch.setattr(FleetServer, "RING_MIN", 2 << 20)
+    a0, b0 = mp.Pipe()
+    a1, b1 = mp.Pipe()
+    server = FleetServer(_StubNode(), None, [a0, a1])
+    server.ring_ack_timeout_s = 0.05
+    server._payload = [True, True]
+    try:
+        first, (s, r) = server._place(600_000)
+        assert first.cap == 1 << 20 and s == 0
+        # the batch is still in flight (need None) when the next one needs its space: grow
+        second, (s2, r2) = server._place(600_000)
+        assert second is not first and second.cap >= 4 * 600_000 and first in server._retired
+        r[2] = {0: 1, 1: 1}
+        server.batches_done = [1, 1]
+        server._reap_retired()
+        assert first not in server._retired  # released once acknowledged: closed
+        # player 1 stops acknowledging: the rank keeps going on a new ring without it
+        r2[2] = {0: 2, 1: 2}
+        server.batches_done = [2, 1]
+        third, (s3, _) = server._place(second.cap - 300_000)  # must wrap onto r2
+        assert third is not second and server.revoked == {1} and server._payload == [True, False]
+        assert b1.recv() == ("revoke",)
+        rn = RemoteNode(b1)
+        a1.send(("revoke",))
+        rn.poll(1.0)
+        assert rn.payload_revoked
+    finally:
+        server.close()
 
 
 def test_fleet_payload_bytes_through_a_wrapping_ring(monkeypatch):

@@ -241,7 +241,7 @@ def test_planner_stage_rows():
 
 
 def test_player_plays_from_an_http_cdn(cdn):
-    out = run_swarm(1, cdn.origin, until=30.0, cfg_extra={"network": {"pin_memory": False, "workers": 4}})
+    out = run_swarm(1, cdn.origin, until=39.0, cfg_extra={"network": {"pin_memory": False, "workers": 4}})
     assert out[0]["ok"]
     seg_total = sum(cdn.origin.pools[0].lengths)
     assert cdn.ts_bytes() == seg_total and out[0]["stats"]["cdn"] == seg_total
@@ -249,7 +249,7 @@ def test_player_plays_from_an_http_cdn(cdn):
 
 
 def test_swarm_downloads_each_segment_once(cdn):
-    out = run_swarm(3, cdn.origin, until=30.0, cfg_extra={"network": {"pin_memory": False, "workers": 4}})
+    out = run_swarm(3, cdn.origin, until=39.0, cfg_extra={"network": {"pin_memory": False, "workers": 4}})
     assert all(o["ok"] for o in out.values())
     seg_total = sum(cdn.origin.pools[0].lengths)
     assert cdn.ts_bytes() == seg_total  # the network carried every segment once

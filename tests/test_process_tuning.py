@@ -29,6 +29,39 @@ def test_tune_gc_freezes_and_raises_gen0():
         gc.set_threshold(*prev)
 
 
+def test_frozen_objects_that_become_cyclic_garbage_are_reclaimed():
+    """an object alive at a freeze (e.g. a request in flight when a full pass
+    ran) that later becomes part of a garbage cycle must not leak: every ``thaw_every``-th
+    full pass thaws the permanent generation first and reclaims it."""
+    import weakref
+
+    class Node:
+        pass
+
+    prev = gc.get_threshold()
+    holder = []
+    try:
+        a, b = Node(), Node()
+        a.peer, b.peer = b, a  # a cycle, kept alive from outside for now
+        holder.append(a)
+        ref = weakref.ref(a)
+        del a, b
+        rt.tune_gc(12345, thaw_every=3)
+        assert gc.get_freeze_count() > 0
+        holder.clear()  # now cyclic garbage, inside the frozen generation
+        passes = rt._freeze_after_full.full_passes
+        while rt._freeze_after_full.full_passes < passes + 3 and ref() is not None:
+            gc.collect(2)
+        assert ref() is None
+        assert rt._freeze_after_full.thaws >= 1
+        assert gc.get_freeze_count() > 0  # the survivors are frozen again after the pass
+    finally:
+        if rt._freeze_after_full in gc.callbacks:
+            gc.callbacks.remove(rt._freeze_after_full)
+        gc.unfreeze()
+        gc.set_threshold(*prev)
+
+
 def test_parse_cpulist():
     assert rt._parse_cpulist("0-3,8,10-11\n") == [0, 1, 2, 3, 8, 10, 11]
     assert rt._parse_cpulist("") == []

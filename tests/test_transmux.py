@@ -168,3 +168,47 @@ def test_launch_columns_verifies_expected_crcs(device, request):
     # every fused CRC is exact: expecting the true values passes all of them
     *_, ok_all = pipe.complete_columns(pipe.launch_columns(big, o, nb, enc, drk, iv, keys=keys, expect=crcs))
     assert ok_all.all()
+
+
+@pytest.mark.parametrize("device", ["cpu", pytest.param("cuda", marks=pytest.mark.gpu)])
+def test_rejected_fragments_with_an_expected_crc_are_still_checked(device, request):
+    """an encrypted fragment whose length is not a whole number of AES blocks is
+    rejected before the decrypt, so the fused CRC never reads it.  Its expected CRC is checked
+    by the CRC kernel instead -- a fragment that asked for a check is reported as passed only
+    when a check ran and passed -- also when the whole batch is rejected (no decrypt launch)."""
+    import zlib
+
+    import numpy as np
+
+    from hlsjs_p2p_wrapper_amd.player.transmux import _Batch
+
+    if device == "cuda":
+        request.getfixturevalue("cuda")
+    rng = np.random.default_rng(3)
+    payloads = [rng.integers(0, 256, n, dtype=np.uint8) for n in (100, 4004, 33)]  # none a multiple of 16
+    offs, pos = [], 0
+    for p in payloads:
+        offs.append(pos)
+        pos += (len(p) + 255) // 256 * 256
+    arena = torch.zeros(pos + 256, dtype=torch.uint8)
+    for o, p in zip(offs, payloads):
+        arena[o:o + len(p)] = torch.from_numpy(p)
+    arena = arena.to(device)
+    n = len(payloads)
+    o = np.asarray(offs, dtype=np.int64)
+    nb = np.array([len(p) for p in payloads], dtype=np.int64)
+    enc = np.ones(n, dtype=bool)
+    key = bytes(range(16))
+    drk = np.tile(aes.round_keys_le(key), (n, 1)).astype(np.uint32)
+    iv = np.zeros((n, 16), dtype=np.uint8)
+    keys = np.tile(np.frombuffer(key, dtype=np.uint8), (n, 1))
+    crcs = np.array([zlib.crc32(bytes(p)) for p in payloads], dtype=np.int64)
+    expect = crcs.copy()
+    expect[1] ^= 4  # the middle one's trailer is wrong
+    pipe = MediaPipeline(torch.device(device), new_event_loop("virtual"))
+    *_, has, ok = pipe.complete_columns(pipe.launch_columns(arena, o, nb, enc, drk, iv, keys=keys, expect=expect))
+    assert ok.tolist() == [True, False, True]
+    assert not has.any()  # no decrypt / demux result for a rejected fragment
+    # the default is "not verified": a fragment that asked for a check no check covered fails
+    b = _Batch(None, n=3, expect_mask=np.array([True, False, True]))
+    assert MediaPipeline._verified(b, 3).tolist() == [False, True, False]
