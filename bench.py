@@ -442,6 +442,10 @@ def main() -> int:
                                "cdnDedup": not args.no_dedup, "maxWantsPerRound": K}}
     if args.metrics_port is not None:
         p2p_config["gpuSwarm"]["metricsPort"] = args.metrics_port
+    if not W and os.environ.get("HLSP2P_DEFER_VERIFY", "1") != "0":
+        # the in-process player verifies received segments in its transmux batch (the CRC fused
+        # into the decrypt), as the fleet's rank does for its players: no separate CRC pass
+        p2p_config["gpuSwarm"]["deferVerify"] = True
     if os.environ.get("HLSP2P_DATA_PLANE") == "ipc" and world > 1:
         # rehearsal outbox (fixed size): a rank forwards at most every peer's wants of a round
         seg = max(max(pool.lengths) for pool in origin.pools)
@@ -595,6 +599,7 @@ def main() -> int:
     result = _result(args, world, tot, max_s, origin, K, desc, encrypted, seg_dur, use_gpu, numa_node, dist,
                      transport=getattr(node.comm, "data_transport", None))
     result["per_rank"] = _per_rank_dicts(per_parts, args.steps)
+    result["config"]["receive_verify"] = "fused-decrypt" if getattr(node, "verify_deferred", False) else "node"
     result["data_plane"] = _plane_info(node, dist, world, device, node.p2p_from - pf0)
     if args.verbose:
         print(f"# rank {rank} pack {t_pack:.2f}s {_mem(use_gpu, device)} counters {counters} level {hls.currentLevel}\n"
@@ -891,7 +896,8 @@ def _result(args, world, tot, max_s, origin, K, desc, encrypted, seg_dur, use_gp
 
 
 # per-rank diagnostics of the timed window, all-gathered as int64 milli-units (fixed order)
-PER_RANK_FIELDS = ("rank", "rounds", "step_ms", "wait_device_us", "exchange_us", "control_us", "plan_us",
+PER_RANK_FIELDS = ("rank", "rounds", "step_ms", "wait_device_us", "exchange_us", "exchange_queued_us", "control_us",
+                   "plan_us",
                    "host_round_us",
                    "cdn_GBps", "cdn_dev_ms", "p2p_recv_MB", "p2p_sent_MB", "p2p_dev_ms", "p2p_GBps",
                    "p2p_links", "p2p_link_GBps", "transmux_dev_ms", "transmux_wait_us", "await_players_us",
@@ -903,7 +909,10 @@ def _per_rank(node, pipe, s0, s1, elapsed, steps, inflight, fleet_total=None, ti
     """This rank's timed-window diagnostics (``PER_RANK_FIELDS``): per ROUND host phases in
     us (``wait_device`` = host blocked on the round's device event, ``exchange`` = posting
     the data plane: microseconds for RCCL, which only enqueues, but the HIP-IPC rehearsal
-    plane blocks there on its peers' packing, ``control`` = control all-gather + directory
+    plane blocks there on its peers' packing, ``exchange_queued`` = host time from posting the
+    exchange to the node stream reaching it (device event times mapped to host time through
+    the last round the host waited on; average over the rounds measured), ``control`` =
+    control all-gather + directory
     ingest, ``plan`` = plan_round + pins); the CDN rate over the
     window and the copy-stream (H2D) device ms per round; P2P received / sent MB per round,
     the node-stream exchange device ms per round (a peer's stall included), the received
@@ -929,6 +938,7 @@ def _per_rank(node, pipe, s0, s1, elapsed, steps, inflight, fleet_total=None, ti
         "rank": node.rank, "rounds": rounds, "step_ms": elapsed * 1e3 / max(1, steps),
         "wait_device_us": tm.get("wait_device", 0.0) * 1e6 / rounds,
         "exchange_us": tm.get("p2p_enqueue", 0.0) * 1e6 / rounds,
+        "exchange_queued_us": tm.get("exchange_queued", 0.0) * 1e6 / max(1.0, tm.get("exchange_queued_n", 0.0)),
         "control_us": tm.get("control", 0.0) * 1e6 / rounds,
         "plan_us": tm.get("plan", 0.0) * 1e6 / rounds,
         "host_round_us": host_round * 1e6 / rounds,

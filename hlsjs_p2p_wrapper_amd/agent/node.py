@@ -149,11 +149,38 @@ class RoundHandle:
     defer: Any = None  # bool per received row: its CRC is checked by the consumer's decrypt (fleet)
     expect_host: Any = None  # the senders' CRC trailers of the received rows (host copy)
     plan: Any = None  # (send rows, recv rows) of this rank's plan
+    t_post: float = 0.0  # host time the exchange was posted
     done: Any = None
     n_wants: int = 0
     n_send: int = 0
     t0: float = 0.0
     completed: bool = False
+
+
+class VerifyTicket:
+    """A received segment delivered before its CRC check (``SwarmNode.defer_inproc``): its
+    consumer -- the player's transmux batch, which computes the CRC inside the decrypt --
+    passes ``expect`` to the check and calls :meth:`report` with the outcome.  Until then the
+    node keeps the entry pinned and does not announce it to peers; a failed check detaches it
+    and the player's next request for the key goes to the CDN."""
+
+    __slots__ = ("node", "eid", "expect", "token", "done")
+
+    def __init__(self, node: "SwarmNode", eid: int, expect: int, token: int) -> None:
+        self.node = node
+        self.eid = eid
+        self.expect = expect
+        self.token = token
+        self.done = False
+
+    def report(self, ok: bool) -> None:
+        if not self.done:
+            self.done = True
+            self.node.verify_done(np.array([self.eid], dtype=np.int64), np.array([bool(ok)]),
+                                  np.array([self.token], dtype=np.int64))
+
+    def __repr__(self) -> str:
+        return f"VerifyTicket(eid={self.eid}, expect={self.expect:#010x}, done={self.done})"
 
 
 class _EventPool:
@@ -233,6 +260,7 @@ class SwarmNode:
         with self._on_node_stream():
             self.crc_dev = torch.zeros(self._crc_capacity(), dtype=torch.int32, device=self.device)
         self._events = _EventPool()
+        self._clk = None  # (timing event, host time it completed): node-stream clock -> host clock
         self.online = True
         self._upload_default = True
         self._download_default = True
@@ -306,6 +334,16 @@ class SwarmNode:
         # entries waiting for a deferred check, by entry id: flag + want info row (a CDN retry's source)
         self._vflag = np.zeros(0, dtype=bool)
         self._vinfo = np.zeros((0, 10), dtype=np.int64)
+        self._vround = np.zeros(0, dtype=np.int64)  # round each pending entry was delivered in
+        self._vexp = np.zeros(0, dtype=np.int64)  # its expected CRC (the sender's trailer)
+        # in-process requests join the deferred check too (gpuSwarm.deferVerify): their bytes
+        # reach the loader with a VerifyTicket, the player's transmux batch verifies them (the
+        # CRC fused into its decrypt) and reports back; a copy that fails is detached and the
+        # player's re-request goes to the CDN (_force_cdn_keys).  Entries whose ticket never comes
+        # back (a fragment dropped before its transmux) are checked by the node after
+        # VERIFY_STALE_ROUNDS rounds
+        self.defer_inproc = False
+        self._force_cdn_keys: set = set()
         self.link_kbps: Dict[int, float] = {}  # fault injection: slow link from peer -> kbit/s
         self.timer = PhaseTimer()
         # per-request trace records {key, trequest, tfirst, tload, source, bytes, peer, round}
@@ -495,6 +533,9 @@ class SwarmNode:
         flags = 0
         if agent is not None and self._sessions and not self.session_flags(agent)[0]:
             flags = W_FORCE_CDN  # this session does not download from peers
+        if self._force_cdn_keys and k in self._force_cdn_keys:
+            self._force_cdn_keys.discard(k)
+            flags |= W_FORCE_CDN  # its peer copy failed the player's check: from the CDN
         size = ptr = base = 0
         x = None
         if wt.lookup1(*k) < 0:
@@ -796,6 +837,8 @@ class SwarmNode:
         t0 = time.perf_counter()
         self.round += 1
         self.stats["rounds"] += 1
+        if self.verify_deferred and self.round % 8 == 0 and len(self._vflag):
+            self._sweep_pending()
         if self._pins:
             keep = []
             for rel, ids in self._pins:
@@ -894,7 +937,7 @@ class SwarmNode:
                 self._p2p_phase(h, send_rows, recv_rows, send_eids)
             h.sent_bytes = int(send_rows[:, 4].sum()) if len(send_rows) else 0
             if self.is_cuda:
-                h.done = self._events.get()
+                h.done = self._events.get(True)  # timing: it also calibrates the device clock (_clock_sync)
                 h.done.record(self.stream)  # explicit stream: skips torch's current_stream() lookup
         self.timer.add("p2p_enqueue", time.perf_counter() - t_p2p0)
         return h
@@ -912,6 +955,9 @@ class SwarmNode:
         t0 = time.perf_counter()
         if h.done is not None and not h.done.query():
             self._wait_round(h)
+            # the host saw the round's last event complete just now: a (device, host) time pair
+            self._clock_sync(h.done, time.perf_counter())
+            h.done = None
         t1 = time.perf_counter()
         self.timer.add("wait_device", t1 - t0)
         if h.ev_cdn is not None:
@@ -919,9 +965,16 @@ class SwarmNode:
             self._events.put(True, *h.ev_cdn)
         if h.ev_p2p is not None:
             h.p2p_ms = h.ev_p2p[0].elapsed_time(h.ev_p2p[1])
+            if self._clk is not None:
+                # host time the node stream reached the exchange minus the host time it was
+                # posted: how long the round's transfers waited behind earlier node-stream work
+                ev, t_host = self._clk
+                q = t_host + ev.elapsed_time(h.ev_p2p[0]) / 1e3 - h.t_post
+                self.timer.add("exchange_queued", max(0.0, q))
+                self.timer.add("exchange_queued_n", 1.0)
             self._events.put(True, *h.ev_p2p)
         if h.done is not None:
-            self._events.put(False, h.done)
+            self._events.put(True, h.done)
             h.done = None
         wt = self._wt
         recv = h.recv
@@ -1029,6 +1082,16 @@ class SwarmNode:
         if prefetch_only.any():
             for i in np.flatnonzero(prefetch_only).tolist():
                 self._prefetched[tuple(int(v) for v in keys[i])] = source
+
+    def _clock_sync(self, ev, t_host: float) -> None:
+        """Keep ``ev`` (a timing event the host just saw complete at ``t_host``) as the
+        reference that maps node-stream event times to host time (the previous reference goes
+        back to the pool).  Error: one event query (~µs); refreshed at every waited round, so
+        device / host clock drift never accumulates."""
+        old = self._clk
+        self._clk = (ev, t_host)
+        if old is not None:
+            self._events.put(True, old[0])
 
     ROUND_SPIN_S = 0.02  # busy-poll a round's completion this long before checking for peer failures
 
@@ -1259,6 +1322,7 @@ class SwarmNode:
                       np.ascontiguousarray(recv_rows[:, 4]), np.ascontiguousarray(recv_rows[:, :4]))
         self.timer.add("p2p_prep", time.perf_counter() - t_prep)
         t = time.perf_counter()
+        h.t_post = t
         if self.is_cuda:
             start = self._events.get(True)
             end = self._events.get(True)
@@ -1342,7 +1406,7 @@ class SwarmNode:
         info[dgood] = winfo
         now = dgood & (np.bincount(idx, minlength=n) == 0)
         neg = tok < 0
-        if neg.any():
+        if neg.any() and not self.defer_inproc:
             now |= dgood & (np.bincount(idx[neg], minlength=n) > 0)
         keep = None
         if now.any():
@@ -1370,14 +1434,14 @@ class SwarmNode:
         if len(pend):
             pe = eids[pend]
             self.store.pin(pe)  # held until verify_done
-            self._vpend_add(pe, info[pend])
+            self._vpend_add(pe, info[pend], exp_good[pend])
         exp_row = np.full(n, -1, dtype=np.int64)
         exp_row[pend] = exp_good[pend] & _M32
         if keep is not None:
             tok, idx = tok[keep], idx[keep]
         return tok, idx, exp_row[idx]
 
-    def _vpend_add(self, eids: np.ndarray, info: np.ndarray) -> None:
+    def _vpend_add(self, eids: np.ndarray, info: np.ndarray, expect: np.ndarray) -> None:
         need = int(eids.max()) + 1
         if need > len(self._vflag):
             cap = max(need, 2 * len(self._vflag), 1024)
@@ -1385,9 +1449,37 @@ class SwarmNode:
             flag[:len(self._vflag)] = self._vflag
             vinfo = np.zeros((cap, self._vinfo.shape[1]), dtype=np.int64)
             vinfo[:len(self._vinfo)] = self._vinfo
-            self._vflag, self._vinfo = flag, vinfo
+            vround = np.zeros(cap, dtype=np.int64)
+            vround[:len(self._vround)] = self._vround
+            vexp = np.zeros(cap, dtype=np.int64)
+            vexp[:len(self._vexp)] = self._vexp
+            self._vflag, self._vinfo, self._vround, self._vexp = flag, vinfo, vround, vexp
         self._vflag[eids] = True
         self._vinfo[eids] = info
+        self._vround[eids] = self.round
+        self._vexp[eids] = expect
+
+    VERIFY_STALE_ROUNDS = 32  # a pending entry nobody reported on for this long is checked by the node
+
+    def _sweep_pending(self) -> int:
+        """Check, on the node, deferred entries whose consumer never reported (an in-process
+        fragment dropped before its transmux: a seek, an abort, a stale level); their entries
+        would otherwise stay pinned and unannounced.  Synchronous CRC kernel; rare."""
+        stale = np.flatnonzero(self._vflag & (self._vround < self.round - self.VERIFY_STALE_ROUNDS))
+        if not len(stale):
+            return 0
+        ent = self.store.entries(stale)
+        offs, lens = ent[:, 0].copy(), ent[:, 1].copy()
+        exp = (self._vexp[stale] & _M32).tolist()
+        if self.is_cuda:
+            with self._on_node_stream():
+                _, okd = _crc.crc32_batch(self.arena, offs, lens, expect=exp)
+                ok = okd.cpu().numpy().astype(bool)
+        else:
+            ok = _crc.crc32_batch(self.arena, offs, lens, expect=exp)[1].numpy().astype(bool)
+        self.verify_done(stale, ok, np.full(len(stale), self.rt.NO_TOKEN, dtype=np.int64))
+        self.stats["verify_swept"] = self.stats.get("verify_swept", 0) + len(stale)
+        return len(stale)
 
     def pending_verify(self) -> int:
         """Entries delivered under deferred verification whose check has not come back."""
@@ -1433,7 +1525,10 @@ class SwarmNode:
             self.store.detach(arr)
             self.store.unpin(arr)
             self.stats["crc_failures"] += 1
-            self._retry_cdn(self._vinfo[e], tokens[inv == k])
+            toks = tokens[inv == k]
+            self._retry_cdn(self._vinfo[e], toks[toks >= 0])  # bulk (fleet) tokens: asked again here
+            # in-process requests were answered already: their players ask again, from the CDN
+            self._force_cdn_keys.add(tuple(int(v) & _M32 for v in self._vinfo[e][:4]))
         return len(bad)
 
     # ------------------------------------------------------------------ delivery
@@ -1488,6 +1583,8 @@ class SwarmNode:
             return
         views = self._views(offs[live].tolist(), nbytes[live].tolist())
         for i, r, view in zip(live, [r for r in reqs if r is not None], views):
+            if expect is not None and expect[i] >= 0:  # deferred check: the consumer's transmux verifies
+                view.swarm_verify = VerifyTicket(self, int(eids[i]), int(expect[i]), r.token)
             self._deliver_req(r, SOURCE_NAMES[int(src[i])], int(nbytes[i]), float(cdn_ms[i]), float(p2p_ms[i]), view,
                               self.rank if peers is None else int(peers[i]), int(eids[i]), pin=False)
 
@@ -1621,7 +1718,9 @@ def node_for_config(p2p_config: Any) -> SwarmNode:
     ``GET /metrics`` on port + rank, 0 = ephemeral; ``metricsHost`` defaults to
     127.0.0.1), ``network`` (``True`` or ``HttpOrigin`` options: fetch ``http(s)://`` URLs
     no in-process origin serves from the real CDN, :mod:`..net.network`); the agent reads
-    ``prefetchSeconds`` / ``prefetchMaxSegments``.  ``numaBind``: run this process on the CPUs
+    ``prefetchSeconds`` / ``prefetchMaxSegments``.  ``deferVerify``: segments received from
+    peers reach in-process players before their CRC check, which the player's transmux batch
+    runs fused into its decrypt (:class:`VerifyTicket`).  ``numaBind``: run this process on the CPUs
     local to the node's GPU (``utils.runtime.bind_to_gpu_numa``; ``bench.py --numa auto``).
     """
     apply_network_config(p2p_config)
@@ -1661,6 +1760,8 @@ def node_for_config(p2p_config: Any) -> SwarmNode:
         from ..utils.runtime import bind_to_gpu_numa
 
         bind_to_gpu_numa(node.device.index if node.device.index is not None else torch.cuda.current_device())
+    if cfg.get("deferVerify"):  # in-process players verify received segments in their transmux
+        node.verify_deferred = node.defer_inproc = True
     if cfg.get("trace"):
         node.enable_trace()
     for peer, kbps in (cfg.get("linkKbps") or {}).items():

@@ -611,13 +611,23 @@ class StreamController:
             self.loop.call_soon(self._on_parsed, frag, stats, payload.transmux_result)
             return
         dev = self.hls.transmux_device(payload)
+        # a segment a peer sent, delivered before its CRC check (gpuSwarm.deferVerify): the
+        # transmux batch verifies it on the way through the decrypt
+        ticket = getattr(payload, "swarm_verify", None)
         pipeline_for(dev, self.loop).submit(
-            TransmuxJob(payload, key, iv, lambda r: self._on_parsed(frag, stats, r), frag))
+            TransmuxJob(payload, key, iv, lambda r: self._on_parsed(frag, stats, r), frag, ticket))
 
     def _on_parsed(self, frag: Fragment, stats: Any, r: Any) -> None:  # r: dict-like transmux result
         hls = self.hls
         key = (frag.level, frag.sn)
         if self.inflight.get(key) is not frag:
+            return
+        if r.get("verify_failed"):
+            # the peer's copy was corrupted: nothing was buffered, the node detached the copy and
+            # this fragment's next load goes to the CDN -- a transport retry, not a media error
+            self.inflight.pop(key, None)
+            log.warning("fragment sn=%s level=%s: peer copy failed its CRC check; reloading", frag.sn, frag.level)
+            self._kick()
             return
         if r.get("error") is not None or r.get("status", 0) & 0b111111:
             self.inflight.pop(key, None)

@@ -37,15 +37,19 @@ class TransmuxJob:
     slotted class: one is built per fragment, and a dataclass ``__init__`` stays interpreted
     code inside the compiled module."""
 
-    __slots__ = ("payload", "key", "iv", "callback", "frag")
+    __slots__ = ("payload", "key", "iv", "callback", "frag", "verify")
 
     def __init__(self, payload: Any, key: Optional[bytes], iv: Optional[bytes],
-                 callback: Callable[[Dict[str, Any]], None], frag: Any = None) -> None:
+                 callback: Callable[[Dict[str, Any]], None], frag: Any = None, verify: Any = None) -> None:
         self.payload = payload
         self.key = key
         self.iv = iv
         self.callback = callback
         self.frag = frag
+        self.verify = verify
+        # a received segment's pending CRC check (agent/node.py VerifyTicket: ``expect``,
+        # ``report(ok)``): the batch verifies the bytes -- fused into the decrypt -- reports the
+        # outcome, and a fragment that fails gets a ``verify_failed`` error result
 
     def __repr__(self) -> str:
         return f"TransmuxJob(key={'set' if self.key else None}, frag={self.frag!r})"
@@ -109,10 +113,17 @@ class MediaPipeline:
         if batch is None:
             return
         if batch.error is not None:
-            for j in batch.jobs:
+            for j in batch.jobs:  # (a pending receive check is left to the node's own sweep)
                 j.callback({"error": batch.error})
             return
         results = self._complete(batch)
+        if batch.expect_mask is not None:  # deferred receive checks: report, drop failed results
+            ok = self._verified(batch, len(batch.jobs))
+            for i in np.flatnonzero(batch.expect_mask).tolist():
+                batch.jobs[i].verify.report(bool(ok[i]))
+                if not ok[i]:
+                    results[i] = {"error": ValueError("received segment failed its CRC check"), "status": -1,
+                                  "verify_failed": True}
         t = time.perf_counter()
         for j, r in zip(batch.jobs, results):
             j.callback(r)
@@ -186,8 +197,16 @@ class MediaPipeline:
                 results[i] = {"error": ValueError("encrypted payload is not a multiple of 16 bytes"), "status": -1}
             if bad:
                 enc = [i for i in enc if i not in bad]
+        vjobs = [i for i, j in enumerate(jobs) if j.verify is not None]
         if dev.type == "cuda":
-            return self._launch_native(jobs, src, src_offs, sizes, enc, clear, results, t1)
+            return self._launch_native(jobs, src, src_offs, sizes, enc, clear, results, t1, vjobs)
+        host_verify = None
+        if vjobs:  # CPU: a host CRC of the received bytes (the GPU fuses it into the decrypt)
+            vi = np.asarray(vjobs, dtype=np.int64)
+            got = _rt().crc32_batch(src.numpy(), np.asarray([src_offs[i] for i in vjobs], dtype=np.int64),
+                                    np.asarray([sizes[i] for i in vjobs], dtype=np.int64))
+            exp = np.asarray([jobs[i].verify.expect for i in vjobs], dtype=np.int64)
+            host_verify = [(vi, (got.astype(np.int64) & 0xFFFFFFFF) == (exp & 0xFFFFFFFF))]
         if enc:
             dec_offs, pos = [], 0
             for i in enc:
@@ -230,16 +249,42 @@ class MediaPipeline:
         if dev.type != "cpu":
             ev = self._event()
         tm.add("demux_launch", time.perf_counter() - t2)
-        return _Batch(jobs, infos=infos, host=host, event=ev, results=results)
+        return _Batch(jobs, infos=infos, host=host, event=ev, results=results, verify=host_verify,
+                      expect_mask=_mask(len(jobs), vjobs))
 
-    def _launch_native(self, jobs, src, src_offs, sizes, enc, clear, results, t1) -> "_Batch":
+    def _launch_native(self, jobs, src, src_offs, sizes, enc, clear, results, t1, vjobs=()) -> "_Batch":
         """GPU batch in ONE native call (``kernels/transmux.cpp``): descriptor math, one
-        staging H2D, AES-CBC decrypt, demux per group, D2H of the info rows."""
+        staging H2D, AES-CBC decrypt (with the receive CRC of ``vjobs`` fused in), demux per
+        group, D2H of the info rows.  Received segments the decrypt does not read (clear
+        ones, rejected ones) are checked by the CRC kernel."""
         tm = self.timer
         idx = enc + clear
         n = len(idx)
+        verify = []
+        ex = cw = ctab = None
+        if vjobs:
+            in_dec = set(enc)
+            side = [i for i in vjobs if i not in in_dec]
+            if side:
+                from ..ops import crc as _crc
+
+                _, okd = _crc.crc32_batch(src, [src_offs[i] for i in side], [sizes[i] for i in side],
+                                          expect=[jobs[i].verify.expect & 0xFFFFFFFF for i in side])
+                okh = torch.empty(len(side), dtype=torch.uint8, pin_memory=True)
+                okh.copy_(okd, non_blocking=True)
+                verify.append((np.asarray(side, dtype=np.int64), okh))
+            if len(side) < len(vjobs):
+                from ..ops import crc as _crc
+
+                ex = np.full(n, -1, dtype=np.int64)
+                for r, i in enumerate(enc):
+                    if jobs[i].verify is not None:
+                        ex[r] = jobs[i].verify.expect & 0xFFFFFFFF
+                cw, ctab = _crc.fused_consts(self.device)
+        mask = _mask(len(jobs), vjobs)
         if n == 0:  # every job was rejected above
-            return _Batch(jobs, infos=[], host=[], event=None, results=results)
+            return _Batch(jobs, infos=[], host=[], event=self._event() if verify else None, results=results,
+                          verify=verify or None, expect_mask=mask)
         offs = np.fromiter((src_offs[i] for i in idx), dtype=np.int64, count=n)
         nb = np.fromiter((sizes[i] for i in idx), dtype=np.int64, count=n)
         flags = np.zeros(n, dtype=np.uint8)
@@ -258,16 +303,19 @@ class MediaPipeline:
         t2 = time.perf_counter()
         tm.add("decrypt_launch", t2 - t1)
         ev0 = self._event()
-        groups, dec, host_block, _ = _native_device().transmux_launch(src, offs, nb, flags, drk, iv, td0, isb,
-                                                                      _ts.DEFAULT_MAX_PES)
+        groups, dec, host_block, fused = _native_device().transmux_launch(src, offs, nb, flags, drk, iv, td0, isb,
+                                                                          _ts.DEFAULT_MAX_PES, ex, cw, ctab)
         infos, host = [], []
         for gidx, info, pes, es, es_offs, hinfo, hlens in groups:
             batch_idx = [idx[k] for k in gidx.tolist()]
             infos.append((batch_idx, _ts.DemuxResult(info, pes, es, es_offs), es_offs, hlens))
             host.append((hinfo, hlens))
+        if fused is not None:  # rows of the launch -> job indices
+            verify.append((np.asarray(idx, dtype=np.int64)[fused[0]], fused[1]))
         ev = self._event()
         tm.add("demux_launch", time.perf_counter() - t2)
-        return _Batch(jobs, infos=infos, host=host, event=ev, results=results, keep=(dec, host_block), start=ev0)
+        return _Batch(jobs, infos=infos, host=host, event=ev, results=results, keep=(dec, host_block), start=ev0,
+                      verify=verify or None, expect_mask=mask)
 
     # ------------------------------------------------------------------ columnar batch
     def launch_columns(self, src: torch.Tensor, offs: np.ndarray, nbytes: np.ndarray, enc: np.ndarray,
@@ -460,6 +508,15 @@ class MediaPipeline:
                 results[i] = r
         tm.add("results", time.perf_counter() - t4)
         return results  # type: ignore[return-value]
+
+
+def _mask(n: int, idx) -> Optional[np.ndarray]:
+    """bool[n] with ``idx`` set (None when ``idx`` is empty)."""
+    if not len(idx):
+        return None
+    m = np.zeros(n, dtype=bool)
+    m[np.asarray(idx, dtype=np.int64)] = True
+    return m
 
 
 _VB, _AB, _IB = _ts.INFO["video_bytes"], _ts.INFO["audio_bytes"], _ts.INFO["id3_bytes"]

@@ -109,13 +109,16 @@ def test_bench_two_ranks_abr_ladder_with_churn(players):
     _check_per_rank(calm, 2)
 
 
-def test_bench_fleet_corrupted_peer_copies_are_refetched():
-    """Fleet mode defers the receive-side CRC to the transmux that decrypts the segment
-    (FleetServer sets verify_deferred): a peer copy corrupted on arrival in each of the first
-    3 timed rounds is caught there, no player gets its result, the node re-fetches it from
-    the CDN, and every player still buffers its fragments without an error."""
-    res = _bench_cpu(_free_port(), "--players", "2", "--corrupt-recv", "3", "--steps", "10")
+@pytest.mark.parametrize("players", ["2", "0"])
+def test_bench_fleet_corrupted_peer_copies_are_refetched(players):
+    """Both player modes defer the receive-side CRC to the transmux that decrypts the
+    segment (fleet: FleetServer sets verify_deferred; in-process: gpuSwarm.deferVerify, the
+    player's batch reports through a VerifyTicket): a peer copy corrupted on arrival in each
+    of the first 3 timed rounds is caught there, nothing is buffered from it, the copy is
+    re-fetched from the CDN, and every player still buffers its fragments without an error."""
+    res = _bench_cpu(_free_port(), "--players", players, "--corrupt-recv", "3", "--steps", "10")
     assert res["errors"] == 0 and res["value"] > 0
+    assert res["config"]["receive_verify"] == "fused-decrypt"
     fails = sum(r["crc_failures"] for r in res["per_rank"])
     assert 1 <= fails <= 6  # at most one per corrupted round on each rank
 
@@ -136,7 +139,8 @@ def test_bench_eight_ranks_driver_shape():
     _check_per_rank(res, 8)
 
 
-PER_RANK_KEYS = {"rank", "rounds", "step_ms", "wait_device_us", "exchange_us", "control_us", "plan_us",
+PER_RANK_KEYS = {"rank", "rounds", "step_ms", "wait_device_us", "exchange_us", "exchange_queued_us", "control_us",
+                 "plan_us",
                  "host_round_us", "cdn_GBps", "cdn_dev_ms", "p2p_recv_MB", "p2p_sent_MB", "p2p_dev_ms", "p2p_GBps",
                  "p2p_links", "p2p_link_GBps",
                  "transmux_dev_ms", "transmux_wait_us", "await_players_us", "payload_GBps", "payload_wait_us",

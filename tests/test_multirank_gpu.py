@@ -63,19 +63,22 @@ def test_two_ranks_ipc_events_bench_scale(cuda):
 
 
 @pytest.mark.gpu
-def test_two_ranks_corrupted_peer_copies_caught_by_the_fused_verify(cuda):
-    """Fleet mode on the GPU: received segments are verified by the CRC fused into the
-    decrypt (profiles/r4_fused).  A peer copy corrupted on arrival in each of the first 3
-    timed rounds must be caught there, detached and re-fetched from the CDN, and no player
-    may see an error."""
+@pytest.mark.parametrize("players", ["2", "0"])
+def test_two_ranks_corrupted_peer_copies_caught_by_the_fused_verify(cuda, players):
+    """Both player modes on the GPU: received segments are verified by the CRC fused into the
+    decrypt (profiles/r4_fused) -- the fleet rank's batch for its players, or the in-process
+    player's own batch (gpuSwarm.deferVerify).  A peer copy corrupted on arrival in each of
+    the first 3 timed rounds must be caught there, detached and re-fetched from the CDN, and
+    no player may see an error."""
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2", "--master-addr",
            "127.0.0.1", "--master-port", str(_free_port()), str(REPO / "bench.py"), "--gpus", "2", "--steps", "20",
-           "--warmup", "4", "--inflight", "16", "--players", "2", "--cache-gb", "2", "--dist-backend", "ipc",
+           "--warmup", "4", "--inflight", "16", "--players", players, "--cache-gb", "2", "--dist-backend", "ipc",
            "--ingest", "hbm", "--corrupt-recv", "3"]
     env = dict(os.environ, PYTHONPATH=str(REPO))
     p = subprocess.run(cmd, cwd=REPO, env=env, capture_output=True, text=True, timeout=420)
     assert p.returncode == 0, p.stderr[-4000:]
     res = json.loads([ln for ln in p.stdout.splitlines() if ln.startswith("{")][-1])
     assert res["errors"] == 0 and res["value"] > 0
+    assert res["config"]["receive_verify"] == "fused-decrypt"
     fails = sum(r["crc_failures"] for r in res["per_rank"])
     assert 1 <= fails <= 6  # at most one per corrupted round on each rank

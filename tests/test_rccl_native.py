@@ -74,6 +74,11 @@ def test_native_rccl_self_exchange_on_stream(cuda):
         done.synchronize()
         assert torch.equal(out_seg, seg) and torch.equal(out_tr, trailer)
         assert comm.rounds == 1 and comm.async_error() == ""
+        # what RCCL itself reports (the topology record of an N > 1 bench run)
+        assert comm.comm_count() == 1 and comm.comm_user_rank() == 0
+        assert comm.comm_device() == torch.cuda.current_device()
+        bus = dev.pci_bus_id(torch.cuda.current_device())
+        assert len(bus.split(":")) == 3 and bus.endswith(".0"), bus
         with pytest.raises(ValueError):  # peer out of range for a world of one
             comm.exchange(np.array([seg.data_ptr()]), np.array([16]), np.array([1]), np.zeros(0, np.int64),
                           np.zeros(0, np.int64), np.zeros(0, np.int64), s.cuda_stream)
@@ -113,6 +118,10 @@ with torch.cuda.stream(s):
     c.exchange([(0, buf), (0, tr)], [(0, rb), (0, rt)])
 torch.cuda.synchronize()
 assert torch.equal(rb, buf) and torch.equal(rt, tr)
+t = c.topology()
+assert t['transport'] == 'rccl-native' and t['world'] == 1, t
+assert t['rccl']['count'] == 1 and t['rccl']['rank'] == 0 and t['rccl']['device'] == 0, t
+assert t['rccl']['rounds'] == 1 and int(t['rccl']['version']) >= 21800, t
 c.close()
 dist.destroy_process_group()
 print('NATIVE_OK')
@@ -123,3 +132,18 @@ print('NATIVE_OK')
     p = subprocess.run([sys.executable, "-c", code], cwd=REPO, capture_output=True, text=True, timeout=180,
                        env=env)
     assert p.returncode == 0 and "NATIVE_OK" in p.stdout, (p.stdout[-2000:], p.stderr[-4000:])
+
+
+@pytest.mark.gpu
+def test_bench_refuses_more_rccl_ranks_than_gpus(cuda):
+    """``bench.py --gpus N`` on a box with fewer than N GPUs: the RCCL plane needs one GPU per
+    rank, so the self-launch refuses before starting any rank (exit 2, a clear message) --
+    it never runs ranks that share a card, or fewer ranks than asked."""
+    n = torch.cuda.device_count() + 1
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    env["PYTHONPATH"] = str(REPO)
+    p = subprocess.run([sys.executable, str(REPO / "bench.py"), "--gpus", str(n), "--steps", "2", "--warmup", "1"],
+                       cwd=REPO, env=env, capture_output=True, text=True, timeout=120)
+    assert p.returncode == 2, (p.stdout[-2000:], p.stderr[-2000:])
+    assert f"--gpus {n} needs {n} visible GPUs" in p.stderr
+    assert not [ln for ln in p.stdout.splitlines() if ln.startswith("{")]

@@ -113,6 +113,63 @@ def test_crc_failure_falls_back_to_cdn(vod):
     assert out[1]["stats"]["cdn"] > 0  # refetched from the CDN after the bad peer copy
 
 
+def test_deferred_receive_check_in_the_players_transmux(vod):
+    """gpuSwarm.deferVerify: a peer copy reaches the in-process player before its CRC check;
+    the player's transmux batch verifies it and reports back (VerifyTicket).  Corrupted copies
+    are dropped before anything is buffered, the node detaches them, the player reloads the
+    fragment from the CDN -- no player error -- and good copies are committed and announced."""
+    errors = {}
+
+    def corrupt(r, node, w):
+        assert node.verify_deferred and node.defer_inproc
+        if r == 1:
+            node.corrupt_next_recv = 2
+        hls = w._wrapper.hls
+        errors[r] = []
+        hls.on(Hls.Events.ERROR, lambda e, d: errors[r].append(d.get("details")))
+
+    out = run_swarm(2, vod, before=corrupt, cfg_extra={"deferVerify": True})
+    assert all(o["ok"] for o in out.values())
+    assert errors == {0: [], 1: []}
+    assert out[1]["node"]["crc_failures"] >= 1
+    assert out[1]["stats"]["cdn"] > 0  # the corrupted fragments came again from the CDN
+    seg_total = sum(vod.pools[0].lengths)
+    assert out[0]["stats"]["p2p"] + out[1]["stats"]["p2p"] > 0
+    assert sum(o["stats"]["cdn"] + o["stats"]["p2p"] for o in out.values()) >= 2 * seg_total
+
+
+def test_deferred_check_of_a_dropped_fragment_is_swept_by_the_node():
+    """A received segment whose consumer never reports (dropped before its transmux) is
+    checked by the node after VERIFY_STALE_ROUNDS rounds: committed when good, detached when
+    not -- never left pinned and unannounced."""
+    import zlib
+
+    from hlsjs_p2p_wrapper_amd.agent.node import SwarmNode
+
+    node = SwarmNode(device="cpu", cache_bytes=1 << 20, loop=new_event_loop("virtual"), auto_tick=False)
+    data = np.arange(3000, dtype=np.uint8)
+    keys = np.array([[3, 0, 0, 1, 3000], [3, 0, 0, 2, 3000]], dtype=np.int64)
+    res = node.store.reserve_run(np.ascontiguousarray(keys[:, :4]), keys[:, 4], 1)
+    _, eids, offs = res
+    for o in offs.tolist():
+        node.arena[o:o + 3000] = torch_from(data)
+    good = zlib.crc32(data.tobytes())
+    node.store.pin(eids)
+    node._vpend_add(eids, np.zeros((2, 10), dtype=np.int64), np.array([good, good ^ 1], dtype=np.int64))
+    node.verify_deferred = True
+    node.round = 100
+    assert node.pending_verify() == 2
+    assert node._sweep_pending() == 2
+    assert node.pending_verify() == 0 and node.stats["crc_failures"] == 1
+    assert node.store.lookup1(3, 0, 0, 1) >= 0 and node.store.lookup1(3, 0, 0, 2) < 0
+
+
+def torch_from(a):
+    import torch
+
+    return torch.from_numpy(a)
+
+
 def test_offline_peer_neither_serves_nor_receives(vod):
     def offline(r, node, w):
         if r == 1:

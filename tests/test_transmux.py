@@ -212,3 +212,48 @@ def test_rejected_fragments_with_an_expected_crc_are_still_checked(device, reque
     # the default is "not verified": a fragment that asked for a check no check covered fails
     b = _Batch(None, n=3, expect_mask=np.array([True, False, True]))
     assert MediaPipeline._verified(b, 3).tolist() == [False, True, False]
+
+
+class _Ticket:
+    def __init__(self, expect):
+        self.expect = expect
+        self.got = None
+
+    def report(self, ok):
+        self.got = ok
+
+
+@pytest.mark.parametrize("device", ["cpu", pytest.param("cuda", marks=pytest.mark.gpu)])
+def test_jobs_with_verify_tickets_are_checked_by_their_batch(device, request):
+    """In-process deferred receive checks (agent/node.py VerifyTicket): a job carrying a
+    ticket is verified by the batch that transmuxes it -- on the GPU the CRC is fused into the
+    AES decrypt -- the outcome is reported to the ticket, and a failed fragment's result is a
+    ``verify_failed`` error (nothing of it reaches the buffer).  Jobs without a ticket are
+    untouched."""
+    import zlib
+
+    if device == "cuda":
+        request.getfixturevalue("cuda")
+    jobs, arena, views, offs = _arena_jobs(device)
+    tickets = []
+    subs = []
+    out = {}
+    for n, ((_, payload, key, iv), v) in enumerate(zip(jobs, views)):
+        t = None
+        if n % 2 == 0:  # every other fragment arrived from a peer
+            crc = zlib.crc32(bytes(payload))
+            t = _Ticket(crc ^ (1 if n == 2 else 0))  # fragment 2's copy is "corrupted"
+            tickets.append((n, t))
+        subs.append(TransmuxJob(v, key, iv, lambda r, n=n: out.__setitem__(n, r), n, t))
+    loop = new_event_loop("virtual")
+    pipe = MediaPipeline(torch.device(device), loop)
+    pipe.auto_flush = False
+    for j in subs:
+        pipe.submit(j)
+    pipe.complete(pipe.launch())
+    for n, t in tickets:
+        assert t.got is (n != 2), (n, t.got)
+    assert out[2].get("verify_failed") and out[2]["error"] is not None
+    for n in range(len(subs)):
+        if n != 2:
+            assert out[n].get("error") is None and not out[n].get("verify_failed"), (n, out[n])
