@@ -221,3 +221,29 @@ def test_round_timeout_reports_and_dumps_the_plan(tmp_path, monkeypatch):
         node._wait_round(h)
     dump = np.load(tmp_path / "plan.r9.rank0.npz")
     assert (dump["send"] == send).all() and (dump["recv"] == recv).all()
+
+
+def test_planner_grouping_fast_path_matches_the_general_path():
+    """The planner groups wants by key with a counting sort over the sn window when the input
+    is rank-major (as ingest_control emits it) and with a hash table otherwise; both must give
+    the identical plan (and digest) for the same set of wants."""
+    rng = np.random.default_rng(11)
+    flags = np.full(4, rt.FLAG_ONLINE | rt.FLAG_UPLOAD | rt.FLAG_DOWNLOAD | rt.FLAG_CDN_DEDUP, dtype=np.int64)
+    for trial in range(20):
+        d = rt.Directory()
+        held = [(7, lvl, 0, sn) for lvl in range(3) for sn in range(100, 140) if rng.random() < 0.3]
+        for k in held:
+            d.apply(int(rng.integers(0, 4)), _adds([k], length=int(rng.integers(1000, 5000))), _rms([]))
+        rows = []
+        for r in range(4):
+            lvl = int(rng.integers(0, 3))
+            sns = rng.choice(np.arange(100, 160), size=int(rng.integers(5, 40)), replace=False)
+            for i, sn in enumerate(sorted(sns.tolist())):
+                rows.append([7, (lvl + i) % 3, 0, sn, int(rng.integers(1000, 5000)), 1000 * r + i, r, 0])
+        wants = np.array(rows, dtype=np.int64)
+        shuffled = wants[rng.permutation(len(wants))]  # not rank-major: the hash path
+        a = rt.plan_round_for(d, wants, flags, 4, 0)
+        b = rt.plan_round_for(d, np.ascontiguousarray(shuffled), flags, 4, 0)
+        assert np.array_equal(a[0], b[0]) and a[1] == b[1] and a[2] == b[2], trial
+        assert np.array_equal(rt.plan_round(d, wants, flags, 4), rt.plan_round(d, np.ascontiguousarray(shuffled),
+                                                                               flags, 4))

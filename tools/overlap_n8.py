@@ -9,10 +9,10 @@ that cadence for each mitigation, one option per run:
 
   base        CU reserve 8 (the default), RCCL on a default-priority stream
   prio        the RCCL stream at the highest stream priority
-  r16 / r32   CU reserve 16 / 32 (the decrypt grid leaves more CUs free)
+  rN          CU reserve N (the decrypt grid leaves N CUs free; r16, r32, r64, ...)
   split       every transmux batch as two launches of half the segments (RCCL kernels can
               dispatch between the two decrypt grids)
-  prio+split  both
+  a+b         options combined (prio+split, r32+split, ...)
 
 Per option (median of --iters), from a common start event:
   rccl_alone_us / tm_alone_us      one exchange round / one transmux batch, alone
@@ -122,9 +122,11 @@ def main():
         timed([("r", rround, streams["default"])])
         timed([("t", batch, s_tm)])
     for opt in args.options.split(","):
-        state["split"] = "split" in opt
-        state["rccl"] = streams["high" if "prio" in opt else "default"]
-        dev.set_cu_reserve(32 if "r32" in opt else 16 if "r16" in opt else 8)
+        parts = opt.split("+")
+        state["split"] = "split" in parts
+        state["rccl"] = streams["high" if "prio" in parts else "default"]
+        reserve = [int(p[1:]) for p in parts if p[:1] == "r" and p[1:].isdigit()]
+        dev.set_cu_reserve(reserve[0] if reserve else 8)
         rs = state["rccl"]
         ra, ta, cad = [], [], []
         for _ in range(args.iters):

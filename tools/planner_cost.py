@@ -72,7 +72,7 @@ def run(world: int, W: int, rounds: int, resident: int) -> dict:
         t0 = time.perf_counter()
         all_wants, flags, _, _ = rt.ingest_control(d, parts, MAGIC, HDR)
         t1 = time.perf_counter()
-        plan, _ = rt.plan_round_for(d, all_wants, flags, world, rnd % world)  # as agent/node.py calls it
+        plan, _, _ = rt.plan_round_for(d, all_wants, flags, world, rnd % world)  # as agent/node.py calls it
         t2 = time.perf_counter()
         if rnd >= rounds // 10:  # skip the first tenth (allocator / cache warm-up)
             t_ing += t1 - t0
