@@ -45,6 +45,9 @@ import torch
 log = logging.getLogger("hlsjs_p2p_wrapper_amd.comm")
 
 
+RCCL_CU_RESERVE = 64  # CUs the decrypt grid leaves free while the native RCCL plane is live
+
+
 class SwarmComm:
     rank: int = 0
     world_size: int = 1
@@ -190,11 +193,14 @@ class DistComm(SwarmComm):
             dist.all_reduce(t, group=self.data_group)
             torch.cuda.synchronize()
         if self._rccl is not None and torch.cuda.is_available():
-            # the persistent decrypt grid leaves one CU per XCD to the node stream's RCCL kernels
+            # the persistent decrypt grid leaves CUs to the node stream's RCCL kernels: 64 (8 per
+            # XCD) measured best for the bench's lag-2 pipeline of a 7-peer round beside the
+            # transmux batches (1,330 us a step against 1,409 at 8; the round completes 2.5x
+            # sooner; profiles/r5_overlap)
             try:
                 from ..ops._native import device as _dev
 
-                _dev().set_cu_reserve(int(os.environ.get("HLSP2P_RCCL_CU_RESERVE", "8")))
+                _dev().set_cu_reserve(int(os.environ.get("HLSP2P_RCCL_CU_RESERVE", str(RCCL_CU_RESERVE))))
             except Exception:  # noqa: BLE001 - older extension without the knob: full grid
                 pass
         self.data_transport = ("rccl-native" if self._rccl is not None else

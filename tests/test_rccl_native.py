@@ -108,7 +108,7 @@ c = DistComm()
 assert c.data_transport == 'rccl-native', c.data_transport
 if '{group}' != 'nccl':
     assert c.data_backend == 'gloo' and c.data_group is None  # no torch RCCL communicator
-    assert _dev().cu_reserve() == 8
+    assert _dev().cu_reserve() == 64  # parallel/comm.py RCCL_CU_RESERVE (profiles/r5_overlap)
 buf = torch.arange(1 << 20, dtype=torch.int32, device=dev).view(torch.uint8)
 tr = torch.tensor([7, 8, 9], dtype=torch.int32, device=dev)
 rb, rt = torch.empty_like(buf), torch.empty_like(tr)

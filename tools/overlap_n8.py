@@ -7,7 +7,7 @@ right behind it.  Round 3 measured (``profiles/r3_rccl_overlap``) that RCCL make
 beside the decrypt grid but most of a round queues until the grid drains.  This tool times
 that cadence for each mitigation, one option per run:
 
-  base        CU reserve 8 (the default), RCCL on a default-priority stream
+  base        CU reserve 8 (round 4's default; 64 since this rehearsal), RCCL on a default-priority stream
   prio        the RCCL stream at the highest stream priority
   rN          CU reserve N (the decrypt grid leaves N CUs free; r16, r32, r64, ...)
   split       every transmux batch as two launches of half the segments (RCCL kernels can
@@ -19,6 +19,10 @@ Per option (median of --iters), from a common start event:
   cadence: batch A, then the exchange round R, then batch B (A and B on one stream, R on
   another, enqueued in that order): rccl_done_us, a_done_us, b_done_us, total_us
   serial_us = rccl_alone + 2 x tm_alone;  saved = 1 - total / serial
+  steady_step_us (--steady K): the bench's pipeline for K steps -- round t+2 posted, then
+  batch t, which consumes round t's deliveries (its stream waits on round t's end event) --
+  total time / K: the device time per step when exchange and transmux overlap in steady
+  state; steady_saved = 1 - steady_step / (rccl_alone + tm_alone)
 
 A one-rank communicator sends to itself: the same ncclGroupStart / ncclSend x 7 + ncclRecv x 7
 / ncclGroupEnd path as a round between peers, but an HBM-to-HBM copy (more CU work per byte
@@ -45,6 +49,7 @@ def main():
     ap.add_argument("--segs", type=int, default=256, help="segments per transmux batch (64 in flight x 4 players)")
     ap.add_argument("--options", default="base,prio,r16,r32,split,prio+split")
     ap.add_argument("--iters", type=int, default=5)
+    ap.add_argument("--steady", type=int, default=0, help="also time K steps of the bench's lag-2 pipeline")
     args = ap.parse_args()
     cuda = torch.device("cuda", 0)
     dev = device()
@@ -116,6 +121,29 @@ def main():
         keep.clear()
         return {k: start.elapsed_time(e) * 1e3 for k, e in ends.items()}
 
+    def steady(rs, k, lag=2):
+        """k steps of the bench's pipeline; returns the total device time in us."""
+        torch.cuda.synchronize()
+        start = torch.cuda.Event(enable_timing=True)
+        start.record()
+        s_tm.wait_event(start)
+        rs.wait_event(start)
+        done = []
+        for t in range(k + lag):
+            if t < k:
+                rround()
+                e = torch.cuda.Event()
+                e.record(rs)
+                done.append(e)
+            if t >= lag:
+                s_tm.wait_event(done[t - lag])  # batch t-lag decrypts round t-lag's deliveries
+                batch()
+        end = torch.cuda.Event(enable_timing=True)
+        end.record(s_tm)
+        torch.cuda.synchronize()
+        keep.clear()
+        return start.elapsed_time(end) * 1e3
+
     out = {"peers": args.peers, "per_peer": args.per_peer, "round_MB": round(args.peers * per / 1e6, 1),
            "segs": args.segs, "rccl_version": int(dev.rccl_version()), "priority_range": [lo, hi], "runs": []}
     for _ in range(2):  # warm-up (RCCL channels, allocator, code objects)
@@ -133,12 +161,18 @@ def main():
             ra.append(timed([("r", rround, rs)])["r"])
             ta.append(timed([("t", batch, s_tm)])["t"])
             cad.append(timed([("a", batch, s_tm), ("r", rround, rs), ("b", batch, s_tm)]))
+        st = []
+        for _ in range(args.iters if args.steady else 0):
+            st.append(steady(rs, args.steady) / args.steady)
         med = lambda xs: round(float(np.median(xs)), 1)  # noqa: E731
         row = {"option": opt, "cu_reserve": dev.cu_reserve(), "rccl_alone_us": med(ra), "tm_alone_us": med(ta),
                "rccl_done_us": med([c["r"] for c in cad]), "a_done_us": med([c["a"] for c in cad]),
                "b_done_us": med([c["b"] for c in cad]), "total_us": med([max(c.values()) for c in cad])}
         row["serial_us"] = round(row["rccl_alone_us"] + 2 * row["tm_alone_us"], 1)
         row["saved"] = round(1 - row["total_us"] / row["serial_us"], 3)
+        if st:
+            row["steady_step_us"] = med(st)
+            row["steady_saved"] = round(1 - row["steady_step_us"] / (row["rccl_alone_us"] + row["tm_alone_us"]), 3)
         out["runs"].append(row)
         print(json.dumps(row), flush=True)
     dev.set_cu_reserve(8)
