@@ -1287,6 +1287,12 @@ class SwarmNode:
         srun, gath, rrun, rid_a, roff_a = self.store.p2p_layout(
             np.ascontiguousarray(send_rows), np.ascontiguousarray(send_eids, dtype=np.int64),
             np.ascontiguousarray(recv_rows), self.round)
+        # the native RCCL plane takes the round as pointer columns: with every send run a
+        # contiguous arena span, no tensor view or Python object is built per peer
+        spans_plane = getattr(self.comm, "exchange_spans", None) if self.is_cuda else None
+        if spans_plane is not None and len(srun) and not (srun[:, 3] == 0).all():
+            spans_plane = None  # a gathered run needs its staging tensor: the general path
+        trailer_all = trailers = None
         # --- sends: one buffer (+ CRC trailer slice) per destination
         if len(send_rows):
             present_all = send_eids >= 0
@@ -1294,9 +1300,9 @@ class SwarmNode:
             trailer_all = torch.index_select(self.crc_dev, 0, idx)
             if not present_all.all():  # missing entry: a bad CRC, the receiver re-fetches from the CDN
                 trailer_all[torch.from_numpy(np.flatnonzero(~present_all)).to(dev)] = -1
-            spans = self._views(srun[:, 4].tolist(), srun[:, 5].tolist()) if len(srun) and (srun[:, 3] == 0).all() \
-                else None
-            for k, (dst, a, b, mode, off, total) in enumerate(srun.tolist()):
+            spans = self._views(srun[:, 4].tolist(), srun[:, 5].tolist()) \
+                if spans_plane is None and len(srun) and (srun[:, 3] == 0).all() else None
+            for k, (dst, a, b, mode, off, total) in enumerate(srun.tolist() if spans_plane is None else ()):
                 if mode == 0:
                     buf = spans[k] if spans is not None else self.arena[off:off + total]
                 else:  # entries not back to back in the arena: gather into a staging buffer
@@ -1307,13 +1313,13 @@ class SwarmNode:
                 sends.append((dst, buf))
                 sends.append((dst, trailer_all[a:b]))
         # --- recvs: the reserved runs; one trailer buffer for all of them
-        trailers = None
         if len(rrun):
             trailers = torch.empty(len(recv_rows), dtype=torch.int32, device=dev)
-            views = self._views(rrun[:, 3].tolist(), rrun[:, 4].tolist())
-            for (src, a, b, _, _), view in zip(rrun.tolist(), views):
-                recvs.append((src, view))
-                recvs.append((src, trailers[a:b]))
+            if spans_plane is None:
+                views = self._views(rrun[:, 3].tolist(), rrun[:, 4].tolist())
+                for (src, a, b, _, _), view in zip(rrun.tolist(), views):
+                    recvs.append((src, view))
+                    recvs.append((src, trailers[a:b]))
             h.hold.append(rid_a)  # pinned by p2p_layout until complete_round
             # segment bytes per source run (a run's span also holds alignment gaps)
             np.add.at(self.p2p_from, rrun[:, 0], np.add.reduceat(recv_rows[:, 4], rrun[:, 1]))
@@ -1327,7 +1333,10 @@ class SwarmNode:
             start = self._events.get(True)
             end = self._events.get(True)
             start.record(self.stream)  # launch_round runs this phase on the node stream
-        self.comm.exchange(sends, recvs)
+        if spans_plane is not None:
+            spans_plane(*_span_columns(self.arena.data_ptr(), srun, trailer_all, rrun, trailers))
+        else:
+            self.comm.exchange(sends, recvs)
         if self.is_cuda:
             end.record(self.stream)
             h.ev_p2p = (start, end)
@@ -1685,6 +1694,30 @@ class SwarmNode:
         """P2P bytes / (P2P + CDN bytes) over the whole swarm."""
         c, p = self.swarm_stats["cdn"], self.swarm_stats["p2p"]
         return p / (p + c) if (p + c) else 0.0
+
+
+def _span_columns(arena_ptr: int, srun: np.ndarray, trailer_all, rrun: np.ndarray, trailers):
+    """A round's transfers as pointer columns ``(send_ptr, send_bytes, send_peer, recv_ptr,
+    recv_bytes, recv_peer)`` for the native RCCL group call: per peer its arena span, then
+    its CRC-trailer slice -- the same per-pair order on both sides, as RCCL point-to-point
+    matches the i-th send with the i-th receive.  ``srun`` rows: (dst, a, b, mode 0, arena
+    offset, bytes); ``rrun`` rows: (src, a, b, arena offset, bytes); trailers are int32."""
+    def cols(runs, span_off, span_len, tr):
+        n = len(runs)
+        ptr = np.empty(2 * n, dtype=np.int64)
+        nb = np.empty(2 * n, dtype=np.int64)
+        peer = np.empty(2 * n, dtype=np.int64)
+        if n:
+            ptr[0::2] = arena_ptr + runs[:, span_off]
+            nb[0::2] = runs[:, span_len]
+            ptr[1::2] = tr.data_ptr() + 4 * runs[:, 1]
+            nb[1::2] = 4 * (runs[:, 2] - runs[:, 1])
+            peer[0::2] = peer[1::2] = runs[:, 0]
+        return ptr, nb, peer
+
+    sp, sb, sd = cols(srun, 4, 5, trailer_all)
+    rp, rb, rs = cols(rrun, 3, 4, trailers)
+    return sp, sb, sd, rp, rb, rs
 
 
 def _dev_index(idx: np.ndarray, dev: torch.device) -> torch.Tensor:

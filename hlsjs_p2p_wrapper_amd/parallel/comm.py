@@ -353,6 +353,20 @@ class DistComm(SwarmComm):
         for r in reqs:
             r.wait()
 
+    @property
+    def exchange_spans(self):
+        """Pointer-column form of :meth:`exchange` for the native RCCL plane (None on the
+        other planes): ``(send_ptr, send_bytes, send_peer, recv_ptr, recv_bytes, recv_peer)``
+        int64 columns, one RCCL group call on the current stream.  The caller keeps the
+        buffers alive and stream-ordered, as for :meth:`exchange`."""
+        if self._rccl is None:
+            return None
+        return self._exchange_spans
+
+    def _exchange_spans(self, sp, sb, sd, rp, rb, rs) -> None:
+        if len(sp) or len(rp):
+            self._rccl.exchange(sp, sb, sd, rp, rb, rs, torch.cuda.current_stream().cuda_stream)
+
     def _exchange_native(self, sends, recvs) -> None:
         """One RCCL group call on the current stream (the swarm node's stream)."""
         if not sends and not recvs:

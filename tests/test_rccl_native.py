@@ -147,3 +147,63 @@ def test_bench_refuses_more_rccl_ranks_than_gpus(cuda):
     assert p.returncode == 2, (p.stdout[-2000:], p.stderr[-2000:])
     assert f"--gpus {n} needs {n} visible GPUs" in p.stderr
     assert not [ln for ln in p.stdout.splitlines() if ln.startswith("{")]
+
+
+def test_span_columns_pair_each_span_with_its_trailer():
+    """The node hands the native RCCL plane a round as pointer columns: per peer its arena span
+    then its CRC-trailer slice, on both sides (RCCL matches the i-th send with the i-th
+    receive of a pair)."""
+    from hlsjs_p2p_wrapper_amd.agent.node import _span_columns
+
+    class T:  # a trailer buffer at a fixed address
+        def __init__(self, p):
+            self.p = p
+
+        def data_ptr(self):
+            return self.p
+
+    srun = np.array([[1, 0, 3, 0, 4096, 9000], [3, 3, 4, 0, 65536, 100]], dtype=np.int64)
+    rrun = np.array([[2, 0, 2, 8192, 6000]], dtype=np.int64)
+    sp, sb, sd, rp, rb, rs = _span_columns(1 << 40, srun, T(5000), rrun, T(7000))
+    assert sp.tolist() == [(1 << 40) + 4096, 5000, (1 << 40) + 65536, 5000 + 12]
+    assert sb.tolist() == [9000, 12, 100, 4] and sd.tolist() == [1, 1, 3, 3]
+    assert rp.tolist() == [(1 << 40) + 8192, 7000] and rb.tolist() == [6000, 8] and rs.tolist() == [2, 2]
+    empty = _span_columns(0, np.zeros((0, 6), dtype=np.int64), None, np.zeros((0, 5), dtype=np.int64), None)
+    assert all(len(c) == 0 for c in empty)
+
+
+@pytest.mark.gpu
+def test_exchange_spans_moves_arena_runs_and_trailers(cuda):
+    """The pointer-column exchange on a one-rank native communicator: two arena runs and
+    their trailer slices sent to self land in the receive runs, byte for byte."""
+    code = """
+import numpy as np, torch, torch.distributed as dist
+from hlsjs_p2p_wrapper_amd.parallel.comm import DistComm
+from hlsjs_p2p_wrapper_amd.agent.node import _span_columns
+dev = torch.device('cuda', 0)
+torch.cuda.set_device(dev)
+dist.init_process_group('gloo', init_method='tcp://127.0.0.1:%d', world_size=1, rank=0)
+c = DistComm()
+assert c.exchange_spans is not None
+g = torch.Generator().manual_seed(5)
+arena = torch.zeros(1 << 23, dtype=torch.uint8, device=dev)  # 8 MiB: sources + both receive runs
+arena[:3_000_000] = torch.randint(0, 256, (3_000_000,), dtype=torch.uint8, generator=g).to(dev)
+tr = torch.tensor([11, 22, 33], dtype=torch.int32, device=dev)
+rt = torch.zeros(3, dtype=torch.int32, device=dev)
+srun = np.array([[0, 0, 2, 0, 0, 2_000_000], [0, 2, 3, 0, 2_000_000, 1_000_000]], dtype=np.int64)
+rrun = np.array([[0, 0, 2, 3_000_064, 2_000_000], [0, 2, 3, 6_000_128, 1_000_000]], dtype=np.int64)
+s = torch.cuda.Stream(dev)
+s.wait_stream(torch.cuda.current_stream())
+with torch.cuda.stream(s):
+    c.exchange_spans(*_span_columns(arena.data_ptr(), srun, tr, rrun, rt))
+torch.cuda.synchronize()
+assert torch.equal(arena[3_000_064:5_000_064], arena[:2_000_000])
+assert torch.equal(arena[6_000_128:7_000_128], arena[2_000_000:3_000_000])
+assert rt.tolist() == [11, 22, 33]
+c.close()
+dist.destroy_process_group()
+print('SPANS_OK')
+""" % _free_port()
+    env = dict(os.environ, PYTHONPATH=str(REPO), HLSP2P_DATA_PLANE="rccl")
+    p = subprocess.run([sys.executable, "-c", code], cwd=REPO, capture_output=True, text=True, timeout=180, env=env)
+    assert p.returncode == 0 and "SPANS_OK" in p.stdout, (p.stdout[-2000:], p.stderr[-4000:])
