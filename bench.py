@@ -272,7 +272,7 @@ def _self_launch(args) -> int:
     import threading
 
     n = args.gpus
-    if not args.cpu and args.dist_backend in ("auto", "nccl"):
+    if not args.cpu and args.dist_backend in ("auto", "nccl") and not os.environ.get("HLSP2P_RCCL_REHEARSAL"):
         avail = torch.cuda.device_count()
         if 0 < avail < n:
             print(f"bench.py: --gpus {n} needs {n} visible GPUs for the RCCL data plane (one rank per GPU); "
@@ -383,6 +383,8 @@ def main() -> int:
         if W else None
     use_gpu = torch.cuda.is_available() and not args.cpu
     rccl_plane = use_gpu and world > 1 and args.dist_backend in ("auto", "nccl")
+    if os.environ.get("HLSP2P_RCCL_REHEARSAL"):  # RCCL ranks sharing a GPU over its socket transport
+        rccl_plane = False
     if use_gpu:
         n_dev = torch.cuda.device_count()
         if rccl_plane and local_rank >= n_dev:  # before any stream, event or communicator exists
@@ -1034,7 +1036,8 @@ def _plane_info(node, dist, world: int, device, recv_from=None) -> dict:
         dist.all_gather_object(ranks, me)
     devs = [(r["host"], r["pci_bus_id"]) for r in ranks if r["pci_bus_id"] is not None]
     distinct = len(set(devs)) == len(devs) if len(devs) == len(ranks) else None
-    if transport.startswith("rccl") and distinct is not True:
+    rehearsal = next((r["comm"].get("rehearsal") for r in ranks if r.get("comm", {}).get("rehearsal")), None)
+    if transport.startswith("rccl") and distinct is not True and rehearsal is None:
         raise RuntimeError(f"RCCL data plane without one GPU per rank: {[(r['rank'], r['pci_bus_id']) for r in ranks]}")
     rccl = next((r["comm"]["rccl"] for r in ranks if "rccl" in r.get("comm", {})), None)
     return {"data": transport, "control": getattr(comm, "control_transport", "local"),
@@ -1043,7 +1046,7 @@ def _plane_info(node, dist, world: int, device, recv_from=None) -> dict:
             "hsa_ipc_legacy": os.environ.get("HSA_ENABLE_IPC_MODE_LEGACY"),
             "launcher": os.environ.get("HLSP2P_LAUNCHER") or ("torchrun" if "TORCHELASTIC_RUN_ID" in os.environ
                                                               else "env" if world > 1 else "none"),
-            "world": world, "distinct_devices": distinct,
+            "world": world, "distinct_devices": distinct, "rccl_rehearsal": rehearsal,
             "rccl_version": rccl["version"] if rccl else None, "ranks": ranks}
 
 

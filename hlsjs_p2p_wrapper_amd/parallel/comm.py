@@ -172,6 +172,7 @@ class DistComm(SwarmComm):
         self._shm = self._open_shm_control() if self.world_size > 1 else None
         self.control_transport = "shm" if self._shm is not None else "gloo"
         self._rccl = None
+        self.rehearsal = None
         self._ipc: Optional[_IpcOutbox] = None
         if backend == "gloo" and plane == "ipc" and self.world_size > 1 and torch.cuda.is_available():
             self._ipc = _IpcOutbox.open(self)
@@ -211,12 +212,26 @@ class DistComm(SwarmComm):
         """The node's own RCCL communicator (collective).  Every rank first reports whether
         the native module and RCCL are usable; only if all are does any rank enter
         ``ncclCommInitRank`` (a rank that cannot join would leave the others blocked in it).
-        Otherwise every rank stays on torch's ``batch_isend_irecv``."""
+        Otherwise every rank stays on torch's ``batch_isend_irecv``.
+
+        ``HLSP2P_RCCL_REHEARSAL=socket``: ranks that share one GPU still get the real native
+        RCCL plane -- each rank presents RCCL a host id of its own (``NCCL_HOSTID``), so RCCL
+        sees N "hosts" and connects them over its socket transport on the loopback instead
+        of refusing duplicate devices.  Everything above the wire (one group call per round,
+        send / recv matching, the pointer columns, async-error polling) is the production
+        path; only the transport differs from xGMI.  For one-GPU rehearsals only."""
         dist, g = self.dist, self.control_group
         dev = None
         ok = True
         uid: List[object] = [None]
         gpu = None
+        self.rehearsal = os.environ.get("HLSP2P_RCCL_REHEARSAL") or None
+        if self.rehearsal == "socket":  # before any RCCL call: the host hash is computed once
+            os.environ["NCCL_HOSTID"] = f"hlsp2p-rehearsal-{os.getpid()}-{self.rank}"
+            os.environ.setdefault("NCCL_SOCKET_IFNAME", "lo")
+            os.environ.setdefault("NCCL_IB_DISABLE", "1")
+        elif self.rehearsal is not None:
+            raise ValueError(f"unknown HLSP2P_RCCL_REHEARSAL {self.rehearsal!r} (expected 'socket')")
         try:
             from ..ops._native import device as _dev
 
@@ -236,7 +251,7 @@ class DistComm(SwarmComm):
         # card silently); every rank sees the same table, so every rank raises here together
         seen: dict = {}
         for r, (_, host, bus) in enumerate(flags):  # type: ignore[misc]
-            if (host, bus) in seen:
+            if (host, bus) in seen and self.rehearsal is None:
                 raise RuntimeError(f"RCCL data plane: ranks {seen[(host, bus)]} and {r} would share GPU {bus} on "
                                    f"host {host[0]}; RCCL needs one GPU per rank (rehearse ranks that share a "
                                    "GPU with --dist-backend ipc or gloo)")
@@ -416,6 +431,8 @@ class DistComm(SwarmComm):
         rank count and rank RCCL holds (``ncclCommCount`` / ``ncclCommUserRank``), the HIP
         device it runs on (``ncclCommCuDevice``), the rounds posted and the RCCL version."""
         out = {"transport": self.data_transport, "world": self.world_size, "rank": self.rank}
+        if getattr(self, "rehearsal", None):
+            out["rehearsal"] = self.rehearsal  # RCCL's socket transport between ranks sharing a GPU
         if self._rccl is not None and not self._rccl.closed:
             from ..ops._native import device as _dev
 
