@@ -603,6 +603,7 @@ def main() -> int:
     result["per_rank"] = _per_rank_dicts(per_parts, args.steps)
     result["config"]["receive_verify"] = "fused-decrypt" if getattr(node, "verify_deferred", False) else "node"
     result["data_plane"] = _plane_info(node, dist, world, device, node.p2p_from - pf0)
+    _label_rehearsal(result)
     if args.verbose:
         print(f"# rank {rank} pack {t_pack:.2f}s {_mem(use_gpu, device)} counters {counters} level {hls.currentLevel}\n"
               f"#   node stats {node.stats} last round {node.last_round}\n"
@@ -819,6 +820,7 @@ def _fleet(args, world, rank, device, use_gpu, node, origin, players, desc, encr
         # it skips that pass; the headline is the same with it forced: profiles/r4_ingestcrc)
         result["config"]["ingest_crc"] = bool(getattr(node, "ingest_crc", True))
         result["data_plane"] = _plane_info(node, dist, world, device, pf1 - pf0)
+        _label_rehearsal(result)
         if live:
             result["config"].update(live=True, live_speed=args.live_speed, live_window=args.live_window,
                                     round_ms=args.round_ms, evicted_segments=server.evicted)
@@ -1048,6 +1050,23 @@ def _plane_info(node, dist, world: int, device, recv_from=None) -> dict:
                                                               else "env" if world > 1 else "none"),
             "world": world, "distinct_devices": distinct, "rccl_rehearsal": rehearsal,
             "rccl_version": rccl["version"] if rccl else None, "ranks": ranks}
+
+
+def _label_rehearsal(result: dict) -> None:
+    """A run whose RCCL ranks share GPUs (``HLSP2P_RCCL_REHEARSAL``) says so in its config:
+    the model names the devices actually used and the parallelism the transport."""
+    dp = result.get("data_plane") or {}
+    if not dp.get("rccl_rehearsal"):
+        return
+    devs = {(r["host"], r["pci_bus_id"]) for r in dp.get("ranks", [])}
+    cfg = result["config"]
+    cfg["model"] = cfg["model"].split(", ")[0] + (f", {result['n_gpus']} peers sharing {len(devs)} MI355X "
+                                                  f"(native RCCL over its {dp['rccl_rehearsal']} transport: "
+                                                  "a rehearsal, not an xGMI run)")
+    cfg["parallelism"] += f"-{dp['rccl_rehearsal']}"
+    for r in result.get("per_rank", []):  # the exchange ran over the rehearsal transport, not xGMI
+        if r.get("bound") == "xgmi":
+            r["bound"] = f"exchange-{dp['rccl_rehearsal']}"
 
 
 def _mem(use_gpu, device) -> str:

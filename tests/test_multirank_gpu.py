@@ -82,3 +82,30 @@ def test_two_ranks_corrupted_peer_copies_caught_by_the_fused_verify(cuda, player
     assert res["config"]["receive_verify"] == "fused-decrypt"
     fails = sum(r["crc_failures"] for r in res["per_rank"])
     assert 1 <= fails <= 6  # at most one per corrupted round on each rank
+
+
+@pytest.mark.gpu
+def test_native_rccl_plane_with_ranks_sharing_the_gpu(cuda):
+    """The production native RCCL data plane at N=2 on the one GPU: each rank presents RCCL a
+    host id of its own (HLSP2P_RCCL_REHEARSAL=socket), so RCCL connects the ranks over its
+    socket transport instead of refusing duplicate devices.  bench.py self-launches the ranks
+    (no torchrun); the round's group calls go through the pointer-column path; a corrupted
+    peer copy in each of the first 3 timed rounds is caught by the in-process player's fused
+    verify and re-fetched; the record shows RCCL's own view (2 ranks, rounds posted)."""
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    env.update(PYTHONPATH=str(REPO), HLSP2P_RCCL_REHEARSAL="socket")
+    p = subprocess.run([sys.executable, str(REPO / "bench.py"), "--gpus", "2", "--steps", "10", "--warmup", "3",
+                        "--cache-gb", "2", "--inflight", "16", "--players", "0", "--ingest", "hbm",
+                        "--corrupt-recv", "3"], cwd=REPO, env=env, capture_output=True, text=True, timeout=400)
+    assert p.returncode == 0, p.stderr[-4000:]
+    res = json.loads([ln for ln in p.stdout.splitlines() if ln.startswith("{")][-1])
+    assert res["n_gpus"] == 2 and res["errors"] == 0 and res["value"] > 0
+    assert res["config"]["receive_verify"] == "fused-decrypt"
+    assert res["config"]["parallelism"] == "swarm2-rccl-socket" and "rehearsal" in res["config"]["model"]
+    dp = res["data_plane"]
+    assert dp["data"] == "rccl-native" and dp["rccl_rehearsal"] == "socket" and dp["launcher"] == "self"
+    for r in dp["ranks"]:
+        rc = r["comm"]["rccl"]
+        assert rc["count"] == 2 and rc["rank"] == r["rank"] and rc["rounds"] > 0
+        assert sum(r["recv_bytes_from"]) > 0
+    assert 1 <= sum(r["crc_failures"] for r in res["per_rank"]) <= 6
