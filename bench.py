@@ -1060,7 +1060,7 @@ def _label_rehearsal(result: dict) -> None:
         return
     devs = {(r["host"], r["pci_bus_id"]) for r in dp.get("ranks", [])}
     cfg = result["config"]
-    cfg["model"] = cfg["model"].split(", ")[0] + (f", {result['n_gpus']} peers sharing {len(devs)} MI355X "
+    cfg["model"] = cfg["model"].rsplit(", ", 1)[0] + (f", {result['n_gpus']} peers sharing {len(devs)} MI355X "
                                                   f"(native RCCL over its {dp['rccl_rehearsal']} transport: "
                                                   "a rehearsal, not an xGMI run)")
     cfg["parallelism"] += f"-{dp['rccl_rehearsal']}"
