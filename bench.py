@@ -819,6 +819,9 @@ def _fleet(args, world, rank, device, use_gpu, node, origin, players, desc, encr
         # whether CDN fetches get the CRC trailer peers check (a one-rank swarm sends nothing, so
         # it skips that pass; the headline is the same with it forced: profiles/r4_ingestcrc)
         result["config"]["ingest_crc"] = bool(getattr(node, "ingest_crc", True))
+        # how a player's onSuccess payload reaches its bytes (RemoteSegment.data()): copied for
+        # every fragment into the shared ring, or fetched from the HBM cache when read
+        result["config"]["player_bytes"] = "ring" if args.fleet_payload else "on-demand"
         result["data_plane"] = _plane_info(node, dist, world, device, pf1 - pf0)
         _label_rehearsal(result)
         if live:

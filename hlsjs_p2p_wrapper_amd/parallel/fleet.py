@@ -23,7 +23,8 @@ Protocol (one ``multiprocessing`` pipe per player process, batched per loop iter
   IV the GPU transmux needs (each distinct key crosses the pipe once);
   ``("abort", [rid, ...])``; ``("evict", swarm, sn)``; ``("flags", down, up)`` (this
   player's ``p2pDownloadOn`` / ``p2pUploadOn``); ``("mark", tag, counters)`` (bench window
-  markers); ``("payload", on)``; ``("bye",)``.
+  markers); ``("payload", on)``; ``("fetch", id, key)`` (one segment's bytes on demand,
+  answered by ``("bytes", id, array or None)``); ``("bye",)``.
 * node -> player: ``("done", chunks, errors, swarm_state)``.  Each chunk holds the fragments
   of one transmux batch as columns: ``rid``, ``source`` code (:data:`SOURCES`), ``nbytes``,
   ``cdn_ms``, ``p2p_ms``, ``plain`` bytes, ``has_row``, the transmux info ``rows`` ``[n,
@@ -33,11 +34,12 @@ Protocol (one ``multiprocessing`` pipe per player process, batched per loop iter
 Player side, :class:`RemoteNode` stands in for the ``SwarmNode`` behind the unchanged
 ``PeerAgent`` (``gpuSwarm.backend = "remote"``): the loader's ``onSuccess`` gets a
 :class:`RemoteSegment` whose ``transmux_result`` the stream controller uses instead of
-transmuxing itself (it holds the info row: durations, PTS, ES byte counts).  With
-``gpuSwarm.fleetPayload`` the segment also carries its bytes (``RemoteSegment.data()``, the
+transmuxing itself (it holds the info row: durations, PTS, ES byte counts).  Its bytes (the
 reference ``onSuccess`` contract ``{currentTarget: {response: ArrayBuffer}}``,
-``lib/integration/p2p-loader-generator.js:92-99``): the rank copies them device-to-host
-into a shared-memory ring the player maps.
+``lib/integration/p2p-loader-generator.js:92-99``) are ``RemoteSegment.data()``: fetched from
+the rank's HBM cache on demand by default (nothing moves for a player that does not read
+them), or, with ``gpuSwarm.fleetPayload``, copied device-to-host for every fragment into a
+shared-memory ring the player maps (one batched D2H per transmux batch).
 """
 from __future__ import annotations
 
@@ -62,15 +64,17 @@ _RING = 1 << 16  # per-player request slots (rid % _RING): far above the fragmen
 
 # ============================================================================ player side
 class RemoteSegment:
-    """``onSuccess`` payload of a remotely served fragment: its size, its transmux result and,
-    when the player asked for payloads, its bytes (:meth:`data`)."""
+    """``onSuccess`` payload of a remotely served fragment: its size, its transmux result and
+    its bytes (:meth:`data`) -- the reference hands the player the response bytes
+    (``lib/integration/p2p-loader-generator.js:92-99``)."""
 
-    __slots__ = ("nbytes", "transmux_result", "_bytes")
+    __slots__ = ("nbytes", "transmux_result", "_bytes", "_src")
 
-    def __init__(self, nbytes: int, transmux_result: Any, data: Any = None) -> None:
+    def __init__(self, nbytes: int, transmux_result: Any, data: Any = None, src: Any = None) -> None:
         self.nbytes = nbytes
         self.transmux_result = transmux_result
         self._bytes = data
+        self._src = src  # (RemoteNode, key): where data() fetches the bytes on demand
 
     def numel(self) -> int:
         return self.nbytes
@@ -79,10 +83,19 @@ class RemoteSegment:
         return self.nbytes
 
     def data(self) -> Optional[np.ndarray]:
-        """The fragment's bytes as a read-only ``uint8`` array (``gpuSwarm.fleetPayload``),
-        else None.  Zero-copy: a view into the rank's shared payload ring, valid while the
-        player handles this answer batch (the ``onSuccess`` callbacks); the ring region is
-        reused once the player acknowledges the batch, so ``.copy()`` what must outlive it."""
+        """The fragment's bytes as a read-only ``uint8`` array.
+
+        With ``gpuSwarm.fleetPayload`` they arrived with the answer batch: a zero-copy view into
+        the rank's shared payload ring, valid while the player handles the batch (the
+        ``onSuccess`` callbacks) -- ``.copy()`` what must outlive it.  Otherwise they are
+        fetched on demand, the first time this is called: the rank copies the segment out of
+        its HBM cache (one D2H) and sends it over the player's pipe, so a player that never
+        reads bytes pays nothing and one that reads some pays per segment read.  None when
+        the rank no longer holds the segment (evicted from its cache)."""
+        if self._bytes is None and self._src is not None:
+            node, key = self._src
+            self._src = None
+            self._bytes = node.fetch_bytes(key)
         return self._bytes
 
 
@@ -198,6 +211,9 @@ class RemoteNode:
         self._reported = 0
         self._ring = _ShmRing()
         self.payload_revoked = False
+        self._stash: List[tuple] = []  # messages read while waiting for fetched bytes
+        self._fetch_id = 0
+        self.bytes_fetched = 0
         if payload:
             self._out.append(("payload", True))
 
@@ -309,14 +325,33 @@ class RemoteNode:
             self.conn.send(("abort", self._aborts))
             self._aborts = []
 
+    def fetch_bytes(self, key) -> Optional[np.ndarray]:
+        """One segment's bytes from the node (:meth:`RemoteSegment.data` on demand): a
+        ``("fetch", id, key)`` request, answered by ``("bytes", id, array or None)``.  Other
+        messages that arrive meanwhile are kept for :meth:`poll` (this runs inside an
+        ``onSuccess`` callback, i.e. inside the delivery of an earlier message)."""
+        self._fetch_id += 1
+        fid = self._fetch_id
+        self.conn.send(("fetch", fid, tuple(int(k) for k in key)))
+        while True:
+            msg = self.conn.recv()
+            if msg[0] == "bytes" and msg[1] == fid:
+                data = msg[2]
+                if data is not None:
+                    data.flags.writeable = False
+                self.bytes_fetched += 0 if data is None else len(data)
+                return data
+            self._stash.append(msg)
+
     def poll(self, timeout: float = 0.0) -> int:
         """Deliver every answer that has arrived (waiting up to ``timeout`` s for the first)."""
         n = 0
         conn = self.conn
-        if not conn.poll(timeout):
+        stash = self._stash
+        if not stash and not conn.poll(timeout):
             return 0
         while True:
-            msg = conn.recv()
+            msg = stash.pop(0) if stash else conn.recv()
             if msg[0] == "done":
                 for chunk in msg[1]:
                     n += self._deliver(chunk)
@@ -335,7 +370,7 @@ class RemoteNode:
             else:  # a control message ("mark", "stop"): the player acts on it before reading on
                 self.control.append(msg)
                 return n
-            if not conn.poll(0):
+            if not stash and not conn.poll(0):
                 return n
 
     def _fail(self, errors: List[Tuple[int, int]]) -> None:
@@ -400,7 +435,7 @@ class RemoteNode:
             if buf is not None:  # zero-copy: valid while this batch is handled (see RemoteSegment.data)
                 data = buf[poff[i]:poff[i] + nbytes]
                 data.flags.writeable = False
-            on_success(RemoteSegment(nbytes, r, data))
+            on_success(RemoteSegment(nbytes, r, data, None if data is not None else (self, req.key)))
             n += 1
         return n
 
@@ -607,6 +642,7 @@ class FleetServer:
         if hasattr(node, "verify_deferred") and os.environ.get("HLSP2P_DEFER_VERIFY", "1") != "0":
             node.verify_deferred = True
         self.verify_failures = 0
+        self.bytes_fetched = 0  # segment bytes sent to players on demand (RemoteSegment.data)
 
     # -------------------------------------------------------------- node sink
     def deliver(self, tok, src, nbytes, cdn_ms, p2p_ms, offs, eids, expect=None) -> None:
@@ -681,6 +717,8 @@ class FleetServer:
                         node.set_session_flags(("fleet", w), bool(msg[1]), bool(msg[2]))
                     elif kind == "payload":
                         self._payload[w] = bool(msg[1])
+                    elif kind == "fetch":  # RemoteSegment.data() on demand
+                        conn.send(("bytes", msg[1], self._segment_bytes(msg[2])))
                     elif kind == "mark":
                         self.marks.setdefault(msg[1], {})[w] = msg[2]
                     elif kind == "ready":
@@ -691,6 +729,25 @@ class FleetServer:
             except (EOFError, OSError):
                 self.open[w] = False
         return n
+
+    def _segment_bytes(self, key) -> Optional[np.ndarray]:
+        """A cached segment's bytes on the host (one D2H on a GPU node), or None when the
+        cache no longer holds it.  Entries the host delivered are resident (their round was
+        waited on), so the copy needs no stream ordering beyond the default stream's."""
+        store = self.node.store
+        eid = store.lookup1(*(int(k) & 0xFFFFFFFF for k in key))
+        if eid < 0:
+            return None
+        ids = np.array([eid], dtype=np.int64)
+        store.pin(ids)
+        try:
+            off, n = (int(x) for x in store.entries(ids)[0][:2])
+            view = self.node.arena[off:off + n]
+            out = view.cpu().numpy() if view.is_cuda else view.numpy().copy()  # a copy either way
+        finally:
+            store.unpin(ids)
+        self.bytes_fetched += n
+        return out
 
     def admit(self, per_player: int) -> int:
         """Hand up to ``per_player`` queued requests of every player to the node (call right

@@ -293,6 +293,96 @@ def test_fleet_payload_bytes_through_a_wrapping_ring(monkeypatch):
         clear_origins()
 
 
+@pytest.mark.parametrize("device", ["cpu", pytest.param("cuda", marks=pytest.mark.gpu)])
+def test_fleet_player_reads_bytes_on_demand_without_payload_mode(device, request):
+    """The default fleet contract: every onSuccess payload exposes the fragment's bytes
+    (``RemoteSegment.data()``, ``lib/integration/p2p-loader-generator.js:92-99``) without the
+    payload ring -- the first data() call fetches the segment from the rank's cache over the
+    player's pipe; answers that arrive meanwhile are delivered afterwards, in order; a player
+    that never calls data() moves no bytes."""
+    import zlib
+
+    if device == "cuda":
+        request.getfixturevalue("cuda")
+    clear_origins()
+    set_current_node(None)
+    loop = new_event_loop("real")
+    spec = dict(ORIGIN, encrypted=False, base_url="http://fleet.demand/live/", pool_size=8)
+    origin = SyntheticHlsOrigin(**spec, pin_memory=device == "cuda")
+    node = node_for_config({"gpuSwarm": {"backend": "local", "device": device, "cacheBytes": 64 << 20,
+                                         "autoTick": False}})
+    a, b = mp.Pipe()
+    sns = list(range(0, 24))
+    got, order, errs = {}, [], []
+    fetched = {}
+
+    def player():
+        rn = RemoteNode(b)  # payload mode off
+
+        class Cb:
+            def __init__(self, sn):
+                self.sn = sn
+
+            def onProgress(self, ev):  # noqa: N802
+                pass
+
+            def onSuccess(self, seg):  # noqa: N802
+                order.append(self.sn)
+                if self.sn % 3 == 0:  # only some fragments are read
+                    d = seg.data()
+                    got[self.sn] = zlib.crc32(d.tobytes()) if d is not None else None
+                    assert seg.data() is d  # fetched once
+
+            def onError(self, err):  # noqa: N802
+                errs.append((self.sn, err.status))
+
+        for sn in sns:
+            rn.request((9, 0, 0, sn), spec["base_url"] + origin.segment_path(0, sn), None, Cb(sn))
+        rn.flush()
+        end = time.monotonic() + 60
+        while len(order) + len(errs) < len(sns) and time.monotonic() < end:
+            rn.poll(0.002)
+            rn.flush()
+        fetched["bytes"] = rn.bytes_fetched
+        rn.close()
+
+    pipe = pipeline_for(torch.device(device) if device == "cpu" else node.device, loop)
+    pipe.auto_flush = False
+    server = FleetServer(node, pipe, [a])
+    t = threading.Thread(target=player, daemon=True)
+    t.start()
+    try:
+        hs, tb = collections.deque(), None
+        end = time.monotonic() + 60
+        while t.is_alive():
+            assert time.monotonic() < end, f"fleet did not deliver: {len(order)} / {len(sns)}"
+            while loop._ready:
+                loop.run_once(block=False)
+            server.poll()
+            server.admit(4)
+            hs.append(node.launch_round())
+            if len(hs) > 1:
+                node.complete_round(hs.popleft())
+            nb = server.launch_transmux()
+            server.complete_transmux(tb)
+            tb = nb
+            server.send()
+        t.join(5)
+        assert not errs and sorted(order) == sns
+        read = [sn for sn in sns if sn % 3 == 0]
+        assert sorted(got) == read
+        for sn in read:
+            assert got[sn] == origin.resource(origin.segment_path(0, sn))[3]
+        seg_bytes = sum(origin.resource(origin.segment_path(0, sn))[2] for sn in read)
+        assert server.bytes_fetched == seg_bytes == fetched["bytes"]  # only what was read moved
+        assert server._ring is None  # no payload ring
+    finally:
+        server.close()
+        node.close()
+        set_current_node(None)
+        clear_origins()
+
+
 @pytest.mark.gpu
 def test_bench_fleet_on_the_gpu():
     """``bench.py`` in its default fleet shape on one MI355X, tiny segments: the players are
