@@ -50,6 +50,8 @@ def main():
     ap.add_argument("--options", default="base,prio,r16,r32,split,prio+split")
     ap.add_argument("--iters", type=int, default=5)
     ap.add_argument("--steady", type=int, default=0, help="also time K steps of the bench's lag-2 pipeline")
+    ap.add_argument("--only-steady", action="store_true", help="time the steady pipeline only (A/B runs)")
+    ap.add_argument("--repeat", type=int, default=1, help="run the option list this many times, interleaved")
     args = ap.parse_args()
     cuda = torch.device("cuda", 0)
     dev = device()
@@ -149,22 +151,28 @@ def main():
     for _ in range(2):  # warm-up (RCCL channels, allocator, code objects)
         timed([("r", rround, streams["default"])])
         timed([("t", batch, s_tm)])
-    for opt in args.options.split(","):
+    for opt in args.options.split(",") * args.repeat:
         parts = opt.split("+")
         state["split"] = "split" in parts
         state["rccl"] = streams["high" if "prio" in parts else "default"]
         reserve = [int(p[1:]) for p in parts if p[:1] == "r" and p[1:].isdigit()]
         dev.set_cu_reserve(reserve[0] if reserve else 8)
         rs = state["rccl"]
+        med = lambda xs: round(float(np.median(xs)), 1)  # noqa: E731
+        st = []
+        for _ in range(args.iters if args.steady else 0):
+            st.append(steady(rs, args.steady) / args.steady)
+        if args.only_steady:
+            row = {"option": opt, "cu_reserve": dev.cu_reserve(), "steady_step_us": med(st),
+                   "steady_all_us": [round(x, 1) for x in st]}
+            out["runs"].append(row)
+            print(json.dumps(row), flush=True)
+            continue
         ra, ta, cad = [], [], []
         for _ in range(args.iters):
             ra.append(timed([("r", rround, rs)])["r"])
             ta.append(timed([("t", batch, s_tm)])["t"])
             cad.append(timed([("a", batch, s_tm), ("r", rround, rs), ("b", batch, s_tm)]))
-        st = []
-        for _ in range(args.iters if args.steady else 0):
-            st.append(steady(rs, args.steady) / args.steady)
-        med = lambda xs: round(float(np.median(xs)), 1)  # noqa: E731
         row = {"option": opt, "cu_reserve": dev.cu_reserve(), "rccl_alone_us": med(ra), "tm_alone_us": med(ta),
                "rccl_done_us": med([c["r"] for c in cad]), "a_done_us": med([c["a"] for c in cad]),
                "b_done_us": med([c["b"] for c in cad]), "total_us": med([max(c.values()) for c in cad])}
