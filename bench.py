@@ -361,6 +361,8 @@ def main() -> int:
     # a round whose transfers are never matched (a dead or diverged peer) fails the job in a
     # minute, with the rank's plan in the error, instead of at the 600 s library default
     os.environ.setdefault("HLSP2P_ROUND_TIMEOUT", "60")
+    # likewise a control all-gather whose peer died (the launcher also stops the job then)
+    os.environ.setdefault("HLSP2P_CONTROL_TIMEOUT", "300")  # start-up skew of a cold box stays well inside
     if args.inflight is None:
         # 64, by measurement (profiles/r4_ab): the headline is PCIe-bound and flat at 128; the
         # HBM-origin probe was +10-20 % at 128 on round-3 boxes and -4 % on round 4's.  (The
