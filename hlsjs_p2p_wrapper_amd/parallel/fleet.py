@@ -23,8 +23,8 @@ Protocol (one ``multiprocessing`` pipe per player process, batched per loop iter
   IV the GPU transmux needs (each distinct key crosses the pipe once);
   ``("abort", [rid, ...])``; ``("evict", swarm, sn)``; ``("flags", down, up)`` (this
   player's ``p2pDownloadOn`` / ``p2pUploadOn``); ``("mark", tag, counters)`` (bench window
-  markers); ``("payload", on)``; ``("fetch", id, key)`` (one segment's bytes on demand,
-  answered by ``("bytes", id, array or None)``); ``("bye",)``.
+  markers); ``("payload", on)``; ``("fetch", id, keys int64[n, 4])`` (an answer chunk's
+  bytes on demand, answered by ``("bytes", id, [array or None per key])``); ``("bye",)``.
 * node -> player: ``("done", chunks, errors, swarm_state)``.  Each chunk holds the fragments
   of one transmux batch as columns: ``rid``, ``source`` code (:data:`SOURCES`), ``nbytes``,
   ``cdn_ms``, ``p2p_ms``, ``plain`` bytes, ``has_row``, the transmux info ``rows`` ``[n,
@@ -93,10 +93,29 @@ class RemoteSegment:
         reads bytes pays nothing and one that reads some pays per segment read.  None when
         the rank no longer holds the segment (evicted from its cache)."""
         if self._bytes is None and self._src is not None:
-            node, key = self._src
+            batch, i = self._src
             self._src = None
-            self._bytes = node.fetch_bytes(key)
+            self._bytes = batch.get(i)
         return self._bytes
+
+
+class _BatchFetch:
+    """The keys of one answer chunk whose bytes were not shipped with it: the first
+    ``RemoteSegment.data()`` of the chunk fetches every one of them in ONE request (one
+    gather + D2H on the rank, one pipe message), so a player that reads all bytes pays a
+    round trip per batch, not per fragment; one that reads none pays nothing."""
+
+    __slots__ = ("node", "keys", "data")
+
+    def __init__(self, node: "RemoteNode") -> None:
+        self.node = node
+        self.keys: List[Tuple[int, int, int, int]] = []
+        self.data: Optional[list] = None
+
+    def get(self, i: int) -> Optional[np.ndarray]:
+        if self.data is None:
+            self.data = self.node.fetch_bytes_many(self.keys)
+        return self.data[i]
 
 
 class RemoteResult(dict):
@@ -325,22 +344,23 @@ class RemoteNode:
             self.conn.send(("abort", self._aborts))
             self._aborts = []
 
-    def fetch_bytes(self, key) -> Optional[np.ndarray]:
-        """One segment's bytes from the node (:meth:`RemoteSegment.data` on demand): a
-        ``("fetch", id, key)`` request, answered by ``("bytes", id, array or None)``.  Other
+    def fetch_bytes_many(self, keys) -> list:
+        """Segments' bytes from the node (:meth:`RemoteSegment.data` on demand): a ``("fetch",
+        id, keys)`` request, answered by ``("bytes", id, [array or None per key])``.  Other
         messages that arrive meanwhile are kept for :meth:`poll` (this runs inside an
         ``onSuccess`` callback, i.e. inside the delivery of an earlier message)."""
         self._fetch_id += 1
         fid = self._fetch_id
-        self.conn.send(("fetch", fid, tuple(int(k) for k in key)))
+        self.conn.send(("fetch", fid, np.asarray(keys, dtype=np.int64).reshape(-1, 4)))
         while True:
             msg = self.conn.recv()
             if msg[0] == "bytes" and msg[1] == fid:
-                data = msg[2]
-                if data is not None:
-                    data.flags.writeable = False
-                self.bytes_fetched += 0 if data is None else len(data)
-                return data
+                out = msg[2]
+                for d in out:
+                    if d is not None:
+                        d.flags.writeable = False
+                        self.bytes_fetched += len(d)
+                return out
             self._stash.append(msg)
 
     def poll(self, timeout: float = 0.0) -> int:
@@ -394,10 +414,15 @@ class RemoteNode:
         rid_a, src_a, nbytes_a, cdn_a, p2p_a, plain_a, has_a, rows_a = chunk[:8]
         payload = chunk[8] if len(chunk) > 8 else None
         buf = poff = None
+        lazy = None
         if payload is not None:
             buf = self._ring.view(payload[0])
             poff = payload[1].tolist()
         pending = self._pending
+        if payload is None:  # this chunk's bytes, fetched together on the first data()
+            lazy = _BatchFetch(self)
+            gone = (0xFFFFFFFF, 0xFFFFFFFF, 0xFFFFFFFF, 0xFFFFFFFF)  # an answer nobody waits for
+            lazy.keys = [pending[r].key if r in pending else gone for r in rid_a.tolist()]
         stats = self.stats
         n = 0
         for i, (rid, code, nbytes, cdn_ms, p2p_ms, plain, has, info) in enumerate(zip(
@@ -435,7 +460,7 @@ class RemoteNode:
             if buf is not None:  # zero-copy: valid while this batch is handled (see RemoteSegment.data)
                 data = buf[poff[i]:poff[i] + nbytes]
                 data.flags.writeable = False
-            on_success(RemoteSegment(nbytes, r, data, None if data is not None else (self, req.key)))
+            on_success(RemoteSegment(nbytes, r, data, None if lazy is None else (lazy, i)))
             n += 1
         return n
 
@@ -717,7 +742,7 @@ class FleetServer:
                         node.set_session_flags(("fleet", w), bool(msg[1]), bool(msg[2]))
                     elif kind == "payload":
                         self._payload[w] = bool(msg[1])
-                    elif kind == "fetch":  # RemoteSegment.data() on demand
+                    elif kind == "fetch":  # RemoteSegment.data() on demand (one answer chunk's keys)
                         conn.send(("bytes", msg[1], self._segment_bytes(msg[2])))
                     elif kind == "mark":
                         self.marks.setdefault(msg[1], {})[w] = msg[2]
@@ -730,23 +755,43 @@ class FleetServer:
                 self.open[w] = False
         return n
 
-    def _segment_bytes(self, key) -> Optional[np.ndarray]:
-        """A cached segment's bytes on the host (one D2H on a GPU node), or None when the
-        cache no longer holds it.  Entries the host delivered are resident (their round was
-        waited on), so the copy needs no stream ordering beyond the default stream's."""
+    def _segment_bytes(self, keys: np.ndarray) -> list:
+        """Cached segments' bytes on the host, one array per key (None: the cache no longer
+        holds it): on a GPU node one gather kernel into a packed block and ONE D2H.  Entries the
+        host delivered are resident (their round was waited on), so the copies need no stream
+        ordering beyond the default stream's."""
         store = self.node.store
-        eid = store.lookup1(*(int(k) & 0xFFFFFFFF for k in key))
-        if eid < 0:
-            return None
-        ids = np.array([eid], dtype=np.int64)
+        keys = np.ascontiguousarray(np.asarray(keys, dtype=np.int64).reshape(-1, 4) & 0xFFFFFFFF)
+        eids = store.lookup(keys, False)
+        out: list = [None] * len(keys)
+        hit = np.flatnonzero(eids >= 0)
+        if not len(hit):
+            return out
+        ids = np.ascontiguousarray(eids[hit])
         store.pin(ids)
         try:
-            off, n = (int(x) for x in store.entries(ids)[0][:2])
-            view = self.node.arena[off:off + n]
-            out = view.cpu().numpy() if view.is_cuda else view.numpy().copy()  # a copy either way
+            ent = store.entries(ids)
+            offs, lens = ent[:, 0].copy(), ent[:, 1].copy()
+            arena = self.node.arena
+            pack = np.concatenate([[0], np.cumsum(lens)[:-1]]).astype(np.int64)
+            total = int(lens.sum())
+            if arena.is_cuda:
+                import torch
+
+                from ..ops import segment as _seg
+
+                staged = torch.empty(max(total, 1), dtype=torch.uint8, device=arena.device)
+                _seg.copy_segments(arena, staged, offs, pack, lens)
+                host = staged[:total].cpu().numpy()
+            else:
+                a = arena.numpy()
+                host = np.concatenate([a[o:o + n] for o, n in zip(offs.tolist(), lens.tolist())]) if total else \
+                    np.zeros(0, dtype=np.uint8)
         finally:
             store.unpin(ids)
-        self.bytes_fetched += n
+        for j, p, n in zip(hit.tolist(), pack.tolist(), lens.tolist()):
+            out[j] = host[p:p + n]
+        self.bytes_fetched += total
         return out
 
     def admit(self, per_player: int) -> int:

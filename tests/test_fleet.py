@@ -374,7 +374,10 @@ def test_fleet_player_reads_bytes_on_demand_without_payload_mode(device, request
         for sn in read:
             assert got[sn] == origin.resource(origin.segment_path(0, sn))[3]
         seg_bytes = sum(origin.resource(origin.segment_path(0, sn))[2] for sn in read)
-        assert server.bytes_fetched == seg_bytes == fetched["bytes"]  # only what was read moved
+        # the first data() of an answer chunk fetched the whole chunk (one round trip per batch):
+        # at least what was read moved, at most the fragments of the chunks read from
+        assert server.bytes_fetched == fetched["bytes"] >= seg_bytes
+        assert server.bytes_fetched <= sum(origin.resource(origin.segment_path(0, sn))[2] for sn in sns)
         assert server._ring is None  # no payload ring
     finally:
         server.close()
