@@ -668,6 +668,7 @@ class FleetServer:
             node.verify_deferred = True
         self.verify_failures = 0
         self.bytes_fetched = 0  # segment bytes sent to players on demand (RemoteSegment.data)
+        self._fetches: List[tuple] = []  # on-demand copies in flight, answered in order
 
     # -------------------------------------------------------------- node sink
     def deliver(self, tok, src, nbytes, cdn_ms, p2p_ms, offs, eids, expect=None) -> None:
@@ -718,6 +719,8 @@ class FleetServer:
         """Take every queued player message; returns the number of new requests."""
         n = 0
         node = self.node
+        if self._fetches:
+            self._finish_fetches()
         for w, conn in enumerate(self.conns):
             if not self.open[w]:
                 continue
@@ -743,7 +746,7 @@ class FleetServer:
                     elif kind == "payload":
                         self._payload[w] = bool(msg[1])
                     elif kind == "fetch":  # RemoteSegment.data() on demand (one answer chunk's keys)
-                        conn.send(("bytes", msg[1], self._segment_bytes(msg[2])))
+                        self._start_fetch(w, msg[1], msg[2])
                     elif kind == "mark":
                         self.marks.setdefault(msg[1], {})[w] = msg[2]
                     elif kind == "ready":
@@ -755,44 +758,72 @@ class FleetServer:
                 self.open[w] = False
         return n
 
-    def _segment_bytes(self, keys: np.ndarray) -> list:
-        """Cached segments' bytes on the host, one array per key (None: the cache no longer
-        holds it): on a GPU node one gather kernel into a packed block and ONE D2H.  Entries the
-        host delivered are resident (their round was waited on), so the copies need no stream
-        ordering beyond the default stream's."""
+    def _start_fetch(self, w: int, fid: int, keys) -> None:
+        """Start copying an answer chunk's cached segments to the host for player ``w``
+        (``RemoteSegment.data()`` on demand): on a GPU node one gather kernel into a packed
+        block and ONE asynchronous D2H into pinned memory on the payload side stream; the
+        answer goes out from a later :meth:`poll` once the copy has landed, so the rank never
+        blocks on it.  A key the cache no longer holds answers None.  Entries the host
+        delivered are resident (their round was waited on); they stay pinned until the copy
+        is done."""
         store = self.node.store
         keys = np.ascontiguousarray(np.asarray(keys, dtype=np.int64).reshape(-1, 4) & 0xFFFFFFFF)
         eids = store.lookup(keys, False)
-        out: list = [None] * len(keys)
         hit = np.flatnonzero(eids >= 0)
-        if not len(hit):
-            return out
         ids = np.ascontiguousarray(eids[hit])
-        store.pin(ids)
-        try:
+        lens = np.zeros(0, dtype=np.int64)
+        pack = lens
+        host = ev = None
+        if len(hit):
+            store.pin(ids)
             ent = store.entries(ids)
             offs, lens = ent[:, 0].copy(), ent[:, 1].copy()
-            arena = self.node.arena
             pack = np.concatenate([[0], np.cumsum(lens)[:-1]]).astype(np.int64)
             total = int(lens.sum())
+            arena = self.node.arena
             if arena.is_cuda:
                 import torch
 
                 from ..ops import segment as _seg
 
-                staged = torch.empty(max(total, 1), dtype=torch.uint8, device=arena.device)
-                _seg.copy_segments(arena, staged, offs, pack, lens)
-                host = staged[:total].cpu().numpy()
+                if self._pstream is None:
+                    self._pstream = torch.cuda.Stream(device=arena.device)
+                ps = self._pstream
+                ps.wait_stream(torch.cuda.current_stream(arena.device))
+                with torch.cuda.stream(ps):  # staging allocated, used and freed in ps's stream order
+                    staged = torch.empty(max(total, 1), dtype=torch.uint8, device=arena.device)
+                    _seg.copy_segments(arena, staged, offs, pack, lens)
+                    host = torch.empty(max(total, 1), dtype=torch.uint8, pin_memory=True)
+                    host.copy_(staged, non_blocking=True)
+                    ev = torch.cuda.Event()
+                    ev.record(ps)
             else:
                 a = arena.numpy()
                 host = np.concatenate([a[o:o + n] for o, n in zip(offs.tolist(), lens.tolist())]) if total else \
                     np.zeros(0, dtype=np.uint8)
-        finally:
-            store.unpin(ids)
-        for j, p, n in zip(hit.tolist(), pack.tolist(), lens.tolist()):
-            out[j] = host[p:p + n]
-        self.bytes_fetched += total
-        return out
+        self._fetches.append((w, fid, len(keys), hit, ids, pack, lens, host, ev))
+        self._finish_fetches()
+
+    def _finish_fetches(self) -> None:
+        """Answer every on-demand fetch whose copy has landed (in request order)."""
+        while self._fetches:
+            w, fid, n, hit, ids, pack, lens, host, ev = self._fetches[0]
+            if ev is not None and not ev.query():
+                return
+            self._fetches.pop(0)
+            if len(ids):
+                self.node.store.unpin(ids)
+            out: list = [None] * n
+            if host is not None:
+                h = host.numpy() if not isinstance(host, np.ndarray) else host
+                for j, p, k in zip(hit.tolist(), pack.tolist(), lens.tolist()):
+                    out[j] = h[p:p + k]
+                self.bytes_fetched += int(lens.sum())
+            if self.open[w]:
+                try:
+                    self.conns[w].send(("bytes", fid, out))
+                except (OSError, BrokenPipeError):
+                    self.open[w] = False
 
     def admit(self, per_player: int) -> int:
         """Hand up to ``per_player`` queued requests of every player to the node (call right
