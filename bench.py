@@ -265,7 +265,8 @@ def _self_launch(args) -> int:
     rank 0's JSON line, and exit non-zero if any rank fails, the job overruns
     ``--launch-timeout`` or the record does not report N ranks.  Runs before this process
     touches the GPU (``torch.cuda.device_count`` does not initialise it) and never execs:
-    the launcher is a child process in its own process group."""
+    the launcher is a child process in this process group, and dies with this process
+    (``PR_SET_PDEATHSIG``), so no rank outlives a killed bench."""
     import signal
     import socket
     import subprocess
@@ -287,7 +288,17 @@ def _self_launch(args) -> int:
     env = dict(os.environ, HLSP2P_LAUNCHER="self")
     env.setdefault("OMP_NUM_THREADS", "1")
     print(f"# bench.py: launching {n} ranks: {' '.join(cmd)}", file=sys.stderr, flush=True)
-    proc = subprocess.Popen(cmd, env=env, stdout=subprocess.PIPE, text=True, start_new_session=True)
+
+    def die_with_parent():  # the launcher (and through it every rank) ends if this process is killed
+        try:
+            import ctypes
+
+            ctypes.CDLL("libc.so.6", use_errno=True).prctl(1, signal.SIGTERM)  # PR_SET_PDEATHSIG
+        except OSError:
+            pass
+
+    # same process group as this one: whatever stops the bench stops its ranks too
+    proc = subprocess.Popen(cmd, env=env, stdout=subprocess.PIPE, text=True, preexec_fn=die_with_parent)
     lines = []
 
     def pump():  # rank 0's JSON line is kept for the parent's stdout; the rest goes to stderr
@@ -301,9 +312,9 @@ def _self_launch(args) -> int:
     reader = threading.Thread(target=pump, daemon=True)
     reader.start()
 
-    def kill_group(sig=signal.SIGTERM):
+    def kill_group(sig=signal.SIGTERM):  # torch.distributed.run stops its workers on SIGTERM
         try:
-            os.killpg(proc.pid, sig)
+            proc.send_signal(sig)
         except ProcessLookupError:
             pass
 

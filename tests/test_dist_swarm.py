@@ -349,3 +349,23 @@ def test_bench_live_edge_two_ranks():
     assert cfg["live"] is True and "live" in cfg["model"] and cfg["evicted_segments"] > 0
     assert 0.3 < res["offload_ratio"] <= 0.52  # each segment crosses the CDN once per swarm of 2
     assert res["live_latency_s"]["p50"] < 30.0  # well ahead of the 30 s live sync point
+
+
+def test_bench_self_launch_deadline_stops_the_ranks():
+    """A self-launched job that overruns ``--launch-timeout`` is stopped -- launcher and ranks
+    -- and the bench exits 124 with no result line."""
+    import time
+
+    import psutil
+
+    t0 = time.monotonic()
+    p = _bench_plain("--cpu", "--gpus", "2", "--players", "0", "--config", "hostcost-micro", "--steps", "100000",
+                     "--warmup", "1", "--inflight", "8", "--pool", "8", "--cache-gb", "0.5", "--launch-timeout", "8")
+    assert p.returncode == 124, p.stderr[-2000:]
+    assert "overran --launch-timeout" in p.stderr
+    assert not [ln for ln in p.stdout.splitlines() if ln.startswith("{")]
+    assert time.monotonic() - t0 < 60
+    time.sleep(1.0)
+    left = [q for q in psutil.process_iter(["cmdline"])
+            if q.info["cmdline"] and "--launch-timeout" in q.info["cmdline"] and "100000" in q.info["cmdline"]]
+    assert not left, [q.info["cmdline"] for q in left]
