@@ -87,3 +87,33 @@ def test_wheel_ships_every_compiled_module(tmp_path):
     built = {str(so.relative_to(pkg)) for so in pkg.rglob("*.so")}
     assert built and built <= shipped, sorted(built - shipped)
     assert "_accel.json" in shipped and "ops/csrc/kernels/aes_cbc.hip" in shipped
+
+
+def test_scale_report_runs_each_n_and_tabulates(tmp_path):
+    """SURVEY §5.5's bench reporter (``tools/scale_report.py``): one self-launched bench per N,
+    a row each with segments/s, offload and weak-scaling efficiency against N x the 1-rank
+    rate (CPU rehearsal here; on a node of MI355X the same command runs RCCL ranks)."""
+    out = tmp_path / "scale.md"
+    p = subprocess.run([sys.executable, str(REPO / "tools" / "scale_report.py"), "--gpus", "1", "2", "--cpu", "--out",
+                        str(out), "--", "--players", "0", "--config", "hostcost-micro", "--steps", "4", "--warmup", "1",
+                        "--inflight", "8", "--pool", "8", "--cache-gb", "0.5"], cwd=REPO, capture_output=True,
+                       text=True, timeout=300)
+    assert p.returncode == 0, p.stderr[-3000:]
+    rows = [ln for ln in p.stdout.splitlines() if ln.startswith("| 1 |") or ln.startswith("| 2 |")]
+    assert len(rows) == 2 and "| 1.00 |" in rows[0] and "| 0.500 |" in rows[1]
+    text = out.read_text()
+    assert text.count('"n_gpus": ') == 2
+
+
+def test_scale_report_table_marks_failures():
+    import scale_report
+
+    rec = {"value": 100.0, "offload_ratio": 0.0, "goodput_GBps": 1.0, "ms_per_step": 2.0, "per_rank": [],
+           "data_plane": {"data": "local"}}
+    rec2 = dict(rec, value=350.0, offload_ratio=0.5, per_rank=[{"bound": "pcie"}, {"bound": "xgmi"}],
+                data_plane={"data": "rccl-native"})
+    t = scale_report.table([{"n": 1, "ok": True, "record": rec}, {"n": 2, "ok": True, "record": rec2},
+                            {"n": 4, "ok": False, "error": "exit 1: boom"}])
+    lines = t.splitlines()
+    assert "| 1.75 |" in lines[3] and "pcie,xgmi" in lines[3] and "rccl-native" in lines[3]
+    assert lines[4].startswith("| 4 | failed |") and "boom" in lines[4]
