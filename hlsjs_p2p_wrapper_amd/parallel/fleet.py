@@ -74,7 +74,7 @@ class RemoteSegment:
         self.nbytes = nbytes
         self.transmux_result = transmux_result
         self._bytes = data
-        self._src = src  # (RemoteNode, key): where data() fetches the bytes on demand
+        self._src = src  # (_BatchFetch, index): where data() fetches the bytes on demand
 
     def numel(self) -> int:
         return self.nbytes
