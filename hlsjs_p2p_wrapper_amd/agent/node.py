@@ -162,22 +162,29 @@ class VerifyTicket:
     consumer -- the player's transmux batch, which computes the CRC inside the decrypt --
     passes ``expect`` to the check and calls :meth:`report` with the outcome.  Until then the
     node keeps the entry pinned and does not announce it to peers; a failed check detaches it
-    and the player's next request for the key goes to the CDN."""
+    and the player's next request for the key goes to the CDN.
 
-    __slots__ = ("node", "eid", "expect", "token", "done")
+    A report that comes after the node swept the entry (``VERIFY_STALE_ROUNDS``) is ignored:
+    the ticket remembers the round its entry went pending, and by then the entry id may hold
+    another segment that is pending on its own check."""
+
+    __slots__ = ("node", "eid", "expect", "token", "stamp", "done")
 
     def __init__(self, node: "SwarmNode", eid: int, expect: int, token: int) -> None:
         self.node = node
         self.eid = eid
         self.expect = expect
         self.token = token
+        self.stamp = int(node._vround[eid])
         self.done = False
 
     def report(self, ok: bool) -> None:
         if not self.done:
             self.done = True
-            self.node.verify_done(np.array([self.eid], dtype=np.int64), np.array([bool(ok)]),
-                                  np.array([self.token], dtype=np.int64))
+            node, e = self.node, self.eid
+            if node._vflag[e] and node._vround[e] == self.stamp:
+                node.verify_done(np.array([e], dtype=np.int64), np.array([bool(ok)]),
+                                 np.array([self.token], dtype=np.int64))
 
     def __repr__(self) -> str:
         return f"VerifyTicket(eid={self.eid}, expect={self.expect:#010x}, done={self.done})"

@@ -164,6 +164,29 @@ def test_deferred_check_of_a_dropped_fragment_is_swept_by_the_node():
     assert node.store.lookup1(3, 0, 0, 1) >= 0 and node.store.lookup1(3, 0, 0, 2) < 0
 
 
+def test_a_late_ticket_report_after_the_sweep_is_ignored():
+    """A consumer that reports after the node swept its entry must not decide the check of
+    whatever segment the entry id holds by then."""
+    from hlsjs_p2p_wrapper_amd.agent.node import SwarmNode, VerifyTicket
+
+    node = SwarmNode(device="cpu", cache_bytes=1 << 20, loop=new_event_loop("virtual"), auto_tick=False)
+    keys = np.array([[3, 0, 0, 1]], dtype=np.int64)
+    _, eids, _ = node.store.reserve_run(keys, np.array([3000]), 1)
+    node.store.pin(eids)
+    node.round = 5
+    node._vpend_add(eids, np.zeros((1, 10), dtype=np.int64), np.array([0], dtype=np.int64))
+    late = VerifyTicket(node, int(eids[0]), 0, 7)
+    node.round = 200  # swept, then (as if evicted and reused) pending again on a newer delivery
+    node.verify_done(eids, np.array([True]), np.array([node.rt.NO_TOKEN]))
+    node.store.pin(eids)
+    node._vpend_add(eids, np.zeros((1, 10), dtype=np.int64), np.array([0], dtype=np.int64))
+    late.report(False)
+    assert node.pending_verify() == 1 and node.stats["crc_failures"] == 0
+    fresh = VerifyTicket(node, int(eids[0]), 0, 8)
+    fresh.report(True)
+    assert node.pending_verify() == 0
+
+
 def torch_from(a):
     import torch
 
