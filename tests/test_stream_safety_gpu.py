@@ -32,6 +32,32 @@ def _sleep_cycles(cuda, ms=200.0):
     return int(min(ms / per_cycle, 2**31 - 1))
 
 
+def _concurrent_stream(cuda, tries=8):
+    """A new stream the device runs beside the default stream, plus the streams tried (kept
+    alive).  HIP maps streams onto a few hardware queues (``GPU_MAX_HW_QUEUES``); a stream
+    that shares the default stream's queue runs in order with it, and the race the positive
+    control provokes cannot happen there."""
+    keep = []
+    cycles = _sleep_cycles(cuda, 30.0)
+    for _ in range(tries):
+        s = torch.cuda.Stream(cuda)
+        keep.append(s)
+        done = torch.cuda.Event()
+        with torch.cuda.stream(s):
+            torch.cuda._sleep(cycles)
+            done.record(s)
+        x = torch.empty(1, dtype=torch.int32, device=cuda)
+        x.fill_(1)  # default stream
+        mark = torch.cuda.Event()
+        mark.record()
+        mark.synchronize()
+        concurrent = not done.query()  # the default stream finished while s still slept
+        torch.cuda.synchronize()
+        if concurrent:
+            return s, keep
+    return None, keep
+
+
 def _segments(arena, n, seg=4096):
     gen = torch.Generator().manual_seed(3)
     data = torch.randint(0, 256, (n * seg,), dtype=torch.uint8, generator=gen)
@@ -47,7 +73,9 @@ def test_old_crc_table_pattern_is_detected(cuda):
     take the table's block while a scatter into it is still queued -- the sentinel is
     overwritten.  Shows the check below can see the race."""
     torch.cuda.synchronize()
-    node_stream = torch.cuda.Stream(cuda)
+    node_stream, _streams = _concurrent_stream(cuda)
+    if node_stream is None:
+        pytest.skip("every new stream ran in order with the default stream (control inconclusive)")
     size = 4100
     table = torch.zeros(size, dtype=torch.int32, device=cuda)  # default-stream allocation
     old_ptr = table.data_ptr()
