@@ -1233,8 +1233,10 @@ def player_main(conn: Any, spec: Dict[str, Any]) -> None:
             prof.disable()
             out = io.StringIO()
             pstats.Stats(prof, stream=out).sort_stats("tottime").print_stats(40)
-            with open(f"{os.environ['HLSP2P_PLAYER_PROFILE']}.player{spec.get('rank', 0)}_{os.getpid()}.txt", "w") as f:
+            stem = f"{os.environ['HLSP2P_PLAYER_PROFILE']}.player{spec.get('rank', 0)}_{os.getpid()}"
+            with open(stem + ".txt", "w") as f:
                 f.write(f"buffered {counters['buffered']}\n" + out.getvalue())
+            prof.dump_stats(stem + ".prof")  # for pstats' callers / callees views
         try:
             hls.destroy()
         finally:

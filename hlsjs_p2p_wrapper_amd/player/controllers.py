@@ -18,7 +18,7 @@ import logging
 from typing import Any, Dict, List, Optional, Tuple
 
 from .events import ErrorDetails, ErrorTypes, Events
-from .level import Fragment, Level, LevelDetails
+from .level import _START_GENERATION, Fragment, Level, LevelDetails
 from .playlist import PlaylistError, is_master, parse_master, parse_media
 from ..parallel.fleet import RemoteSegment
 from .transmux import TransmuxJob, pipeline_for
@@ -379,6 +379,48 @@ def _byte_length(payload: Any) -> int:
 
 
 # ---------------------------------------------------------------------------- stream
+class _Inflight(dict):
+    """The fragments in flight, keyed by ``(level, sn)``, in load order -- and whether they
+    form one chain in that order (each starts within 0.5 s of the previous one's end and ends
+    after it), kept up to date as fragments are added and removed.  ``tick`` needs the end of
+    the in-flight run that continues the buffer; for a chain that is the last fragment's end
+    (O(1)), where the scan over every fragment in flight (256 per player at the bench's depth)
+    cost ~5 µs of each fragment's player CPU."""
+
+    __slots__ = ("chain_ok", "tail")
+
+    def __init__(self) -> None:
+        super().__init__()
+        self.chain_ok = True
+        self.tail: Optional[Fragment] = None
+
+    def __setitem__(self, key, frag) -> None:
+        t = self.tail
+        if not self:
+            ok = True
+        elif key in self or t is None or not self.chain_ok:
+            ok = False  # a re-inserted key keeps its old position in the order
+        else:
+            te = t._start + t.duration
+            ok = frag._start <= te + 0.5 and frag._start + frag.duration > te
+        dict.__setitem__(self, key, frag)
+        self.tail = frag
+        self.chain_ok = ok
+
+    def pop(self, key, *default):
+        if self.chain_ok and key in self and key != next(iter(self)):
+            self.chain_ok = False  # removing a fragment other than the oldest may open a gap
+        return dict.pop(self, key, *default)
+
+    def __delitem__(self, key) -> None:
+        self.pop(key)
+
+    def clear(self) -> None:
+        dict.clear(self)
+        self.chain_ok = True
+        self.tail = None
+
+
 class StreamController:
     STOPPED, IDLE, ERROR, ENDED = "STOPPED", "IDLE", "ERROR", "ENDED"
 
@@ -386,7 +428,9 @@ class StreamController:
         self.hls = hls
         self.loop = hls.loop
         self.state = self.STOPPED
-        self.inflight: Dict[Tuple[int, int], Fragment] = {}
+        self.inflight: Dict[Tuple[int, int], Fragment] = _Inflight()
+        self._chain_gen = -1  # fragment_generation() when the chain flag was last checked by a scan
+        self.run_scans = 0  # _run_end calls that scanned every fragment in flight
         self.fragPrevious: Optional[Fragment] = None
         self.fragLastKbps = 0
         self.stats = None
@@ -542,12 +586,7 @@ class StreamController:
         max_buf = max(8.0 * (cfg.maxBufferSize or 0) / bitrate, float(cfg.maxBufferLength))
         max_buf = min(max_buf, float(cfg.maxMaxBufferLength))
         max_inflight = max(1, int(cfg.get("maxFragLoadsInFlight", 1) or 1))
-        nxt = buf_end
-        for f in self.inflight.values():
-            fs = f.start
-            fe = fs + f.duration  # f.end, without the property call (runs per in-flight fragment per tick)
-            if fe > nxt and fs <= nxt + 0.5:
-                nxt = fe
+        nxt = self._run_end(buf_end)
         while len(self.inflight) < max_inflight and nxt - pos < max_buf:
             frag = self._frag_at(details, nxt)
             if frag is None:
@@ -562,6 +601,36 @@ class StreamController:
                 continue
             self._load(frag)
             nxt = frag.end
+
+    def _run_end(self, nxt: float) -> float:
+        """The end of the in-flight run that continues the buffer (which ends at ``nxt``): one
+        pass in load order, each fragment starting within 0.5 s of the covered end extends
+        it.  For a chain (:class:`_Inflight`) whose oldest fragment extends the buffer that is
+        the newest fragment's end."""
+        inflight = self.inflight
+        if not inflight:
+            return nxt
+        gen = _START_GENERATION[0]
+        first = next(iter(inflight.values()))
+        fs = first._start
+        fe = fs + first.duration
+        if inflight.chain_ok and self._chain_gen == gen and fe > nxt and fs <= nxt + 0.5:
+            t = inflight.tail
+            return t._start + t.duration
+        self.run_scans += 1
+        ok, prev = True, None
+        for f in inflight.values():
+            fs = f._start
+            fe = fs + f.duration
+            if prev is not None and not (fs <= prev + 0.5 and fe > prev):
+                ok = False
+            prev = fe
+            if fe > nxt and fs <= nxt + 0.5:
+                nxt = fe
+        inflight.chain_ok = ok
+        inflight.tail = f
+        self._chain_gen = gen
+        return nxt
 
     def _load(self, frag: Fragment) -> None:
         frag.loadCounter += 1
