@@ -283,22 +283,25 @@ def _self_launch(args) -> int:
     s.bind(("127.0.0.1", 0))
     port = s.getsockname()[1]
     s.close()
-    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
-           "--master-addr=127.0.0.1", f"--master-port={port}", os.path.abspath(__file__), *sys.argv[1:]]
+    args_run = ["--nnodes=1", f"--nproc-per-node={n}", "--master-addr=127.0.0.1", f"--master-port={port}",
+                os.path.abspath(__file__), *sys.argv[1:]]
+    # The launcher ends if this process is killed, even by SIGKILL (and through it every rank):
+    # it asks for SIGTERM on its parent's death (PR_SET_PDEATHSIG) first thing, then checks
+    # that parent is still this process, then runs torch.distributed.run as __main__.  Done
+    # in the child itself rather than in a preexec_fn, which is unsafe in a process with threads.
+    boot = ("import ctypes, os, runpy, signal, sys\n"
+            "ctypes.CDLL(None, use_errno=True).prctl(1, signal.SIGTERM)\n"
+            "if os.getppid() != int(sys.argv[1]):\n"
+            "    sys.exit(125)\n"
+            "sys.argv = ['torch.distributed.run'] + sys.argv[2:]\n"
+            "runpy.run_module('torch.distributed.run', run_name='__main__', alter_sys=True)\n")
+    cmd = [sys.executable, "-c", boot, str(os.getpid()), *args_run]
     env = dict(os.environ, HLSP2P_LAUNCHER="self")
     env.setdefault("OMP_NUM_THREADS", "1")
-    print(f"# bench.py: launching {n} ranks: {' '.join(cmd)}", file=sys.stderr, flush=True)
-
-    def die_with_parent():  # the launcher (and through it every rank) ends if this process is killed
-        try:
-            import ctypes
-
-            ctypes.CDLL("libc.so.6", use_errno=True).prctl(1, signal.SIGTERM)  # PR_SET_PDEATHSIG
-        except OSError:
-            pass
-
+    print(f"# bench.py: launching {n} ranks: {sys.executable} -m torch.distributed.run {' '.join(args_run)}",
+          file=sys.stderr, flush=True)
     # same process group as this one: whatever stops the bench stops its ranks too
-    proc = subprocess.Popen(cmd, env=env, stdout=subprocess.PIPE, text=True, preexec_fn=die_with_parent)
+    proc = subprocess.Popen(cmd, env=env, stdout=subprocess.PIPE, text=True)
     lines = []
 
     def pump():  # rank 0's JSON line is kept for the parent's stdout; the rest goes to stderr

@@ -369,3 +369,44 @@ def test_bench_self_launch_deadline_stops_the_ranks():
     left = [q for q in psutil.process_iter(["cmdline"])
             if q.info["cmdline"] and "--launch-timeout" in q.info["cmdline"] and "100000" in q.info["cmdline"]]
     assert not left, [q.info["cmdline"] for q in left]
+
+
+def test_killing_the_self_launching_bench_stops_its_ranks():
+    """SIGKILL of ``bench.py --gpus 2`` (no signal handler runs): the launcher it started gets
+    SIGTERM from the kernel on its parent's death and stops the ranks."""
+    import signal
+    import subprocess
+    import sys
+    import time
+    from pathlib import Path
+
+    import psutil
+
+    repo = Path(__file__).resolve().parents[1]
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    env["PYTHONPATH"] = str(repo)
+    p = subprocess.Popen([sys.executable, str(repo / "bench.py"), "--cpu", "--gpus", "2", "--players", "0", "--config",
+                          "hostcost-micro", "--steps", "100000", "--warmup", "1", "--inflight", "8", "--pool", "8",
+                          "--cache-gb", "0.5"], cwd=repo, env=env, stdout=subprocess.DEVNULL,
+                         stderr=subprocess.DEVNULL)
+    kids = []
+    try:
+        parent = psutil.Process(p.pid)
+        deadline = time.monotonic() + 120
+        while time.monotonic() < deadline and len(kids) < 3:  # the launcher and its two ranks
+            time.sleep(0.5)
+            kids = parent.children(recursive=True)
+        assert len(kids) >= 3, [k.cmdline() for k in kids]
+        time.sleep(2.0)
+        p.send_signal(signal.SIGKILL)
+        p.wait(timeout=30)
+        gone, alive = psutil.wait_procs(kids, timeout=60)
+        assert not alive, [a.pid for a in alive]
+    finally:
+        if p.poll() is None:
+            p.kill()
+        for k in kids:  # a failed check leaves no process behind (exact PIDs of this test's tree)
+            try:
+                k.kill()
+            except psutil.NoSuchProcess:
+                pass
