@@ -3,9 +3,10 @@
 Statics: ``Hls.Events``, ``Hls.ErrorTypes``, ``Hls.ErrorDetails``, ``Hls.DefaultConfig``,
 ``Hls.isSupported()``, ``Hls.version``.  Instance: ``config``, ``on/off/once/trigger``,
 ``url``, ``media``, ``levels``, ``loadSource``, ``attachMedia``, ``detachMedia``,
-``startLoad``, ``stopLoad``, ``destroy``, ``currentLevel``, ``loadLevel``,
-``nextLoadLevel``, ``nextLevel``, ``autoLevelEnabled``, ``levelController._levels``,
-``abrController.bwEstimator.getEstimate()``.
+``startLoad``, ``stopLoad``, ``destroy``, ``recoverMediaError``, ``swapAudioCodec``,
+``currentLevel``, ``loadLevel``, ``nextLoadLevel``, ``nextLevel``, ``firstLevel``,
+``startLevel``, ``autoLevelCapping``, ``autoLevelEnabled``, ``manualLevel``,
+``levelController._levels``, ``abrController.bwEstimator.getEstimate()``.
 """
 from __future__ import annotations
 
@@ -208,6 +209,40 @@ class Hls:
     def startLevel(self) -> int:
         """First level loaded."""
         return self.levelController.firstLevel
+
+    @startLevel.setter
+    def startLevel(self, v: int) -> None:
+        # hls.js: the level the next manifest starts on (config.startLevel); -1 = automatic
+        self.config.startLevel = v
+
+    @property
+    def firstLevel(self) -> int:
+        """First level of the manifest (``startLevel`` when it names a level, else 0)."""
+        return self.levelController.firstLevel
+
+    @firstLevel.setter
+    def firstLevel(self, v: int) -> None:
+        self.levelController.firstLevel = v
+
+    def recoverMediaError(self) -> None:
+        """hls.js's recovery for a fatal media error: detach the media element and attach it
+        again, which restarts buffering at its current position."""
+        media = self.media
+        if media is None:
+            return
+        self.detachMedia()
+        self.attachMedia(media)
+        restart = getattr(media, "restart", None)
+        if restart is not None:
+            restart()
+
+    def swapAudioCodec(self) -> None:
+        """hls.js toggles the audio codec string (``mp4a.40.2`` / ``mp4a.40.5``) it hands to
+        MSE on the next init segment, to recover from a decoder that rejects one.  The
+        elementary streams here go to :class:`MediaElement`, which takes no codec string,
+        so the flag is kept (``audioCodecSwap``) for callers that read it and changes no
+        output."""
+        self.audioCodecSwap = not getattr(self, "audioCodecSwap", False)
 
     @property
     def bandwidthEstimate(self) -> float:

@@ -233,5 +233,12 @@ class MediaElement(EventEmitter):
             self._timer.cancel()
             self._timer = None
 
+    def restart(self) -> None:
+        """Restart the playback clock after :meth:`stop` (the engine re-attaching this element)
+        unless playback is paused."""
+        if not self.paused and self._timer is None:
+            self._last_tick = self.loop.now()
+            self._ensure_timer()
+
 
 HTMLVideoElement = MediaElement

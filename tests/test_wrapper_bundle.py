@@ -197,6 +197,24 @@ def test_bundle_plays_from_start(vod):
     assert loop.run_until(lambda: media.currentTime > 1.0, timeout_ms=30_000)
 
 
+def test_bundle_recovers_from_a_media_error_and_keeps_playing(vod):
+    """hls.js's ``recoverMediaError()`` (detach + re-attach the media element) mid-playback:
+    buffering and the playback clock resume; the level statics of hls.js answer."""
+    loop = new_event_loop("virtual")
+    hls = Hls({"debug": True}, P2P)
+    media = MediaElement()
+    _start(hls, media, vod.master_url())
+    assert loop.run_until(lambda: media.currentTime > 5.0, timeout_ms=30_000)
+    assert hls.firstLevel == 0 and hls.startLevel == 0
+    hls.startLevel = 0
+    hls.recoverMediaError()
+    assert hls.media is media
+    assert loop.run_until(lambda: media.currentTime > 20.0, timeout_ms=60_000)
+    hls.swapAudioCodec()
+    assert hls.audioCodecSwap
+    hls.destroy()
+
+
 def test_bundle_seeks_to_30s(vod):
     loop = new_event_loop("virtual")
     hls = Hls({"debug": True}, P2P)
