@@ -873,6 +873,12 @@ class SwarmNode:
             self._finish_failed(too_big, http.HttpError(507, "", f"segment exceeds the {self.cache_bytes}-byte cache"))
         if deferred:
             self.stats["deferred"] = self.stats.get("deferred", 0) + int(deferred)
+        if len(rows):
+            # the entries this round's reservations overwrite leave the directory in this
+            # round's control message, so no peer plans a transfer from them: a send would pin
+            # them after admission and the reservation would find them pinned
+            need = np.maximum((rows[:, 4] + (ALIGN - 1)) // ALIGN * ALIGN, ALIGN)
+            self.store.retire_region(int(need.sum()))
         adds, rms = self.store.take_delta()
         parts = self.comm.allgather_control(self._encode(rows, adds, rms))
         # every rank's deltas into the directory + the round's want rows, in one native call

@@ -101,6 +101,36 @@ bool SegmentStore::fits(int64_t total) const {
   return true;
 }
 
+int64_t SegmentStore::retire_region(int64_t total) {
+  if (total <= 0) return 0;
+  if (total > capacity_) total = capacity_;
+  int64_t start = head_;
+  bool wrapped = false;
+  if (start + total > capacity_) {
+    start = 0;
+    wrapped = true;
+  }
+  const int64_t end = start + total;
+  std::vector<int64_t> victims;
+  for (const auto& fe : fifo_) {  // the walk of fits() / make_room()
+    const Entry& e = entries_[fe.first];
+    if (e.state == kFree || e.gen != fe.second) continue;
+    const bool in_skip = wrapped && e.offset >= head_;
+    const bool overlaps = e.offset < end && e.offset + e.alloc_bytes > start;
+    if (!in_skip && !overlaps) break;
+    victims.push_back(fe.first);
+  }
+  int64_t n = 0;
+  for (int64_t id : victims) {
+    const Entry& e = entries_[id];
+    auto it = index_.find(e.key);
+    if (it == index_.end() || it->second != id) continue;  // already detached / replaced
+    detach(id);
+    ++n;
+  }
+  return n;
+}
+
 int64_t SegmentStore::reserve_run(const SegKey* keys, const int64_t* lens, int64_t n, int64_t tick, int64_t* ids,
                                   int64_t* offsets) {
   int64_t total = 0;

@@ -82,6 +82,12 @@ class SegmentStore {
   // Would a run of `total` aligned bytes fit at the head now (no pinned entry in its way)?
   // Non-mutating; consecutive smaller runs of the same total then fit too (backpressure).
   bool fits(int64_t total) const;
+  // Detach (and announce the removal of) every entry a reservation of `total` bytes at the
+  // head would overwrite -- the entries `fits(total)` walks.  A round calls it for the bytes
+  // it admitted, before its control message goes out: no peer then plans a transfer from an
+  // entry this rank overwrites in the same round (the send would pin it after admission and
+  // the reservation would find it pinned).  Returns the number detached.
+  int64_t retire_region(int64_t total);
   int64_t aligned(int64_t len) const {
     const int64_t a = (len + align_ - 1) & ~(align_ - 1);
     return a == 0 ? align_ : a;
