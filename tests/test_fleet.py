@@ -99,6 +99,53 @@ def test_two_players_are_served_their_slices(node_side):
         assert not t.is_alive()
 
 
+def test_a_killed_player_process_does_not_stop_the_other_players(node_side):
+    """A player process that dies mid-run (SIGKILL: no goodbye on its pipe) is dropped by the
+    rank -- its pipe reads EOF, nothing more is sent to it -- and the other player keeps
+    being served."""
+    loop, node = node_side
+    ctx = mp.get_context("spawn")
+    pairs = [ctx.Pipe() for _ in range(2)]
+    procs = []
+    for w, (_, child) in enumerate(pairs):
+        spec = {"origin": dict(ORIGIN, pin_memory=False),
+                "hls_config": {"maxFragLoadsInFlight": 8, "maxBufferLength": 1e9, "maxMaxBufferLength": 1e9,
+                               "startPosition": w * 60.0, "startLevel": 0, "tickInterval": 1e9},
+                "p2p_config": {"streamrootKey": "t", "contentId": "fleet-test"}, "world": 1, "rank": 0}
+        pr = ctx.Process(target=player_main, args=(child, spec), daemon=True)
+        pr.start()
+        child.close()
+        procs.append(pr)
+    conns = [parent for parent, _ in pairs]
+    state = {"killed_at": None}
+
+    def until(s):
+        if state["killed_at"] is None and s.sent >= 8:
+            procs[1].kill()
+            procs[1].join(10)
+            state["killed_at"] = s.requests[0]
+        return state["killed_at"] is not None and not s.open[1] and s.requests[0] >= state["killed_at"] + 16
+
+    try:
+        server = _serve(loop, node, conns, until, timeout_s=120.0)
+        assert server.open[0] and not server.open[1]
+        conns[0].send(("mark", "end"))
+        end = time.monotonic() + 30
+        while 0 not in server.marks.get("end", {}):
+            server.poll()
+            time.sleep(0.002)
+            assert time.monotonic() < end
+        m = server.marks["end"][0]
+        assert m["buffered"] > 0 and m["errors"] == 0
+        conns[0].send(("stop",))
+        procs[0].join(30)
+        assert procs[0].exitcode == 0
+    finally:
+        for pr in procs:
+            if pr.is_alive():
+                pr.kill()
+
+
 def test_remote_node_delivers_result_rows_and_errors():
     a, b = mp.Pipe()
     node = RemoteNode(a)
