@@ -96,6 +96,21 @@ def test_four_peers_offload(vod):
     assert p2p / (p2p + cdn) == pytest.approx(0.75)  # (N-1)/N with de-duplication
 
 
+def test_staggered_peers_with_tiny_caches_play_through():
+    """Four peers whose caches hold ~5 segments each, started 16 s apart: a lagging peer keeps
+    wanting the segments a leader is about to overwrite (the ring-retire path,
+    tests/test_ring_pressure.py; without it this run failed with "cannot make room"),
+    in-flight windows of 4, 30 segments -- everyone plays to the end, nothing fails."""
+    origin = SyntheticHlsOrigin("http://cdn.test/tiny/", renditions=[Rendition(1_000_000, 640, 360)],
+                                num_segments=30, encrypted=True)
+    seg = max(origin.pools[0].lengths)
+    out = run_swarm(4, origin, until=110.0, cfg_extra={"cacheBytes": 5 * ((seg + 255) // 256 * 256)},
+                    hls_cfg={"maxFragLoadsInFlight": 4, "maxBufferLength": 12},
+                    start_delay=lambda r: 16000.0 * r, timeout=400_000)
+    assert all(o["ok"] for o in out.values()), {r: o["t"] for r, o in out.items()}
+    assert sum(o["stats"]["p2p"] for o in out.values()) > 0
+
+
 def test_late_joiner_served_from_peers_cache(vod):
     # peer 1 starts 60 s later: everything it needs is already cached on peer 0
     out = run_swarm(2, vod, start_delay=lambda r: 60_000 if r == 1 else 0, timeout=400_000)
