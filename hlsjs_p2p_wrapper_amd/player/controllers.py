@@ -587,6 +587,7 @@ class StreamController:
         max_buf = min(max_buf, float(cfg.maxMaxBufferLength))
         max_inflight = max(1, int(cfg.get("maxFragLoadsInFlight", 1) or 1))
         nxt = self._run_end(buf_end)
+        ranges = None
         while len(self.inflight) < max_inflight and nxt - pos < max_buf:
             frag = self._frag_at(details, nxt)
             if frag is None:
@@ -598,6 +599,16 @@ class StreamController:
             key = (frag.level, frag.sn)
             if key in self.inflight:
                 nxt = frag.end
+                continue
+            # a fragment already in the buffer past the run being loaded (after a seek to just
+            # before a buffered range, with fragments in flight) is skipped, not loaded again:
+            # reloading it from the cache would complete at once and re-kick this loop forever
+            if ranges is None:
+                ranges = list(media.buffered)
+                hole = cfg.maxBufferHole
+            fs, fe = frag.start, frag.end
+            if any(s - hole <= fs + 1e-3 and e >= fe - hole for s, e in ranges):
+                nxt = fe
                 continue
             self._load(frag)
             nxt = frag.end
