@@ -604,6 +604,13 @@ class SwarmNode:
         if force_cdn is not None:
             fc = np.asarray(force_cdn, dtype=bool)
             flags[:] = np.where(fc if miss is None else fc[miss], W_FORCE_CDN, 0)
+        if self._force_cdn_keys:  # keys whose copy a consumer rejected (invalidate / verify): from the CDN
+            fk = self._force_cdn_keys
+            for j, row in enumerate((keys if miss is None else keys[miss]).tolist()):
+                t = tuple(row)
+                if t in fk:
+                    fk.discard(t)
+                    flags[j] |= W_FORCE_CDN
         xs: Dict[int, _WantX] = {}
         bad: List[Tuple[int, int]] = []
         resolve = self._resolve
@@ -877,8 +884,12 @@ class SwarmNode:
             # the entries this round's reservations overwrite leave the directory in this
             # round's control message, so no peer plans a transfer from them: a send would pin
             # them after admission and the reservation would find them pinned
-            need = np.maximum((rows[:, 4] + (ALIGN - 1)) // ALIGN * ALIGN, ALIGN)
-            self.store.retire_region(int(need.sum()))
+            need = int(np.maximum((rows[:, 4] + (ALIGN - 1)) // ALIGN * ALIGN, ALIGN).sum())
+            self.store.retire_region(need)
+            # the round's runs (CDN + one per source peer) all land in the region admission
+            # checked: if they would cross the ring's end, the ring wraps before the first
+            if not self.store.wrap_for(need):
+                raise RuntimeError("segment cache cannot wrap for the round (pinned entries block eviction)")
         adds, rms = self.store.take_delta()
         parts = self.comm.allgather_control(self._encode(rows, adds, rms))
         # every rank's deltas into the directory + the round's want rows, in one native call
@@ -1517,6 +1528,24 @@ class SwarmNode:
         self._wt.add(np.ascontiguousarray(rep[:, :4]), np.ascontiguousarray(rep[:, 4]), np.ascontiguousarray(rep[:, 5]),
                      np.ascontiguousarray(rep[:, 6]), np.ascontiguousarray(rep[:, 7] | W_FORCE_CDN), tokens)
         self._schedule()
+
+    def invalidate(self, keys) -> int:
+        """A consumer found the cached copy of these segments unusable (its decrypt or demux
+        failed): detach each from the cache -- the removal goes out with the next round's
+        control message, so peers stop asking this rank for it -- and take the next request
+        for the key from the CDN.  ``keys``: int64[n, 4] ``(swarm, level, urlId, sn)``.
+        Returns the number of cached copies detached."""
+        keys = np.ascontiguousarray(np.asarray(keys, dtype=np.int64).reshape(-1, 4) & _M32)
+        if not len(keys):
+            return 0
+        eids = self.store.lookup(keys, False)
+        held = eids[eids >= 0]
+        if len(held):
+            self.store.detach(held)
+        for row in keys.tolist():
+            self._force_cdn_keys.add(tuple(row))
+        self.stats["invalidated"] = self.stats.get("invalidated", 0) + len(held)
+        return len(held)
 
     def verify_done(self, eids: np.ndarray, ok: np.ndarray, tokens: np.ndarray) -> int:
         """Outcome of deferred CRC checks (fragment columns: the entry each was read from,

@@ -19,6 +19,8 @@ from __future__ import annotations
 import logging
 from typing import Any, Dict, Optional
 
+import numpy as np
+
 from ..utils.events import JsObject
 from .node import SwarmNode, node_for_config, swarm_id_for
 
@@ -96,6 +98,19 @@ class PeerAgent:
         return req
 
     get_segment = getSegment
+
+    def invalidateSegment(self, segmentView: Any) -> None:
+        """The player could not decrypt or demux the bytes it got for ``segmentView``: the
+        node drops its cached copy and fetches the segment from the CDN when it is asked
+        again (an extension of the reference's agent contract; the wrapper calls it on
+        ``FRAG_DECRYPT_ERROR`` / ``FRAG_PARSING_ERROR``)."""
+        if self.disposed:
+            return
+        tv = segmentView.trackView
+        key = (self.swarm_id, int(tv.level or 0), int(tv.urlId or 0), int(segmentView.sn or 0))
+        invalidate = getattr(self.node, "invalidate", None)
+        if invalidate is not None:
+            invalidate(np.array([key], dtype=np.int64))
 
     def setMediaElement(self, media: Any) -> None:
         """The media element whose playhead drives prefetch and eviction."""

@@ -24,6 +24,7 @@ from ..integration.p2p_loader import p2p_loader_generator
 from ..integration.player_interface import PlayerInterface
 from ..models.media_map import MediaMap
 from ..models.segment_view import SegmentView
+from ..models.track_view import TrackView
 from ..utils.js import truthy
 
 log = logging.getLogger("hlsjs_p2p_wrapper_amd.wrapper")
@@ -156,11 +157,28 @@ class HlsjsP2PWrapperPrivate:
         if not truthy(hlsEventsEnum):
             raise Exception("Need valid Hls.js Events enumeration")
         hlsjs.on(hlsEventsEnum.ERROR, self.onMediaEngineError)
+        hlsjs.on(hlsEventsEnum.ERROR, self._invalidateUnusableFragment)
         playerBridge = PlayerInterface(hlsjs, hlsEventsEnum, self.onDispose)
         mediaMap = MediaMap(hlsjs)
         self.peerAgentModule = StreamrootPeerAgentModule(playerBridge, contentUrl, mediaMap, p2pConfig, SegmentView,
                                                          streamType, integrationVersion)
         self._setMediaElement(hlsjs, hlsEventsEnum)
+
+    def _invalidateUnusableFragment(self, event: str, data: Any) -> None:
+        """A fragment the engine could not decrypt or demux: the agent drops the cached copy
+        it served, so the engine's retry fetches the segment from the CDN instead of getting
+        the same bytes again (extension; the reference's agent contract has no such call)."""
+        details = data.get("details") if isinstance(data, dict) else getattr(data, "details", None)
+        if details not in ("fragDecryptError", "fragParsingError"):
+            return
+        frag = data.get("frag") if isinstance(data, dict) else getattr(data, "frag", None)
+        invalidate = getattr(self.peerAgentModule, "invalidateSegment", None)
+        if frag is None or invalidate is None or self.hls is None:
+            return
+        levels = self.hls.levels or []
+        lvl = levels[frag.level] if 0 <= frag.level < len(levels) else None
+        invalidate(SegmentView._owning(frag.sn, TrackView(level=frag.level, urlId=getattr(lvl, "urlId", 0)),
+                                       frag.start))
 
     @staticmethod
     def onMediaEngineError(event: str, data: Any) -> None:

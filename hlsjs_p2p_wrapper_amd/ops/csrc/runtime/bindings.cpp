@@ -432,6 +432,7 @@ PYBIND11_MODULE(_runtime, m) {
         return py::make_tuple(as2d(srun, 6), as2d(gath, 4), as2d(rrun, 5), rid, roff);
       })
       .def("fits", &SegmentStore::fits)
+      .def("wrap_for", &SegmentStore::wrap_for)
       .def("retire_region", &SegmentStore::retire_region)
       .def("resident", [](const SegmentStore& s) {
         // -> (ids int64[n], keys int64[n,4]) of resident entries, oldest first

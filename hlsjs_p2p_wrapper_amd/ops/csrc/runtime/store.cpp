@@ -101,6 +101,13 @@ bool SegmentStore::fits(int64_t total) const {
   return true;
 }
 
+bool SegmentStore::wrap_for(int64_t total) {
+  if (total <= 0 || head_ + total <= capacity_) return true;
+  if (!make_room(0, 0, true)) return false;  // len 0: only the tail entries (offset >= head) go
+  head_ = 0;
+  return true;
+}
+
 int64_t SegmentStore::retire_region(int64_t total) {
   if (total <= 0) return 0;
   if (total > capacity_) total = capacity_;

@@ -82,6 +82,13 @@ class SegmentStore {
   // Would a run of `total` aligned bytes fit at the head now (no pinned entry in its way)?
   // Non-mutating; consecutive smaller runs of the same total then fit too (backpressure).
   bool fits(int64_t total) const;
+  // A round about to reserve several runs totalling `total` (a CDN run, one run per source
+  // peer): when they would cross the ring's end, wrap NOW -- evict the tail past the head and
+  // continue at 0 -- so every run of the round lands in [0, total), the region fits(total)
+  // checked.  (Runs wrapping one by one skip the tail in the middle of the round, and the
+  // runs after the wrap can reach the round's own earlier, pinned, runs.)  False if a pinned
+  // entry is in the tail (admission rules that out).
+  bool wrap_for(int64_t total);
   // Detach (and announce the removal of) every entry a reservation of `total` bytes at the
   // head would overwrite -- the entries `fits(total)` walks.  A round calls it for the bytes
   // it admitted, before its control message goes out: no peer then plans a transfer from an

@@ -344,6 +344,12 @@ class RemoteNode:
             self.conn.send(("abort", self._aborts))
             self._aborts = []
 
+    def invalidate(self, keys) -> int:
+        """Ask the rank to drop its cached copies of ``keys`` (int64[n, 4]) and take them from
+        the CDN next time (:meth:`SwarmNode.invalidate`); sent before the next requests."""
+        self._out.append(("invalidate", np.asarray(keys, dtype=np.int64).reshape(-1, 4)))
+        return 0
+
     def fetch_bytes_many(self, keys) -> list:
         """Segments' bytes from the node (:meth:`RemoteSegment.data` on demand): a ``("fetch",
         id, keys)`` request, answered by ``("bytes", id, [array or None per key])``.  Other
@@ -745,6 +751,8 @@ class FleetServer:
                         node.set_session_flags(("fleet", w), bool(msg[1]), bool(msg[2]))
                     elif kind == "payload":
                         self._payload[w] = bool(msg[1])
+                    elif kind == "invalidate":  # the player could not decrypt / demux these copies
+                        node.invalidate(msg[1])
                     elif kind == "fetch":  # RemoteSegment.data() on demand (one answer chunk's keys)
                         self._start_fetch(w, msg[1], msg[2])
                     elif kind == "mark":

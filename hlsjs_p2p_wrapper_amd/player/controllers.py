@@ -607,7 +607,9 @@ class StreamController:
                 ranges = list(media.buffered)
                 hole = cfg.maxBufferHole
             fs, fe = frag.start, frag.end
-            if any(s - hole <= fs + 1e-3 and e >= fe - hole for s, e in ranges):
+            # covered: one range from the fragment's start (a range evicted up to just past it
+            # leaves a hole to fill) to within a hole of its end (ranges end at the media end)
+            if any(s <= fs + 1e-3 and e >= fe - hole for s, e in ranges):
                 nxt = fe
                 continue
             self._load(frag)
@@ -681,7 +683,6 @@ class StreamController:
         if self.inflight.get((frag.level, frag.sn)) is not frag:
             return  # aborted / stale
         self.stats = data["stats"]
-        self._retry.pop((frag.level, frag.sn), None)
         dd = frag.decryptdata
         key = dd.key if (dd is not None and dd.method == "AES-128") else None
         iv = frag.iv_for_decrypt() if key is not None else None
@@ -713,9 +714,22 @@ class StreamController:
             self.inflight.pop(key, None)
             details = (ErrorDetails.FRAG_DECRYPT_ERROR if r.get("plain_bytes", 0) < 0
                        else ErrorDetails.FRAG_PARSING_ERROR)
-            hls.trigger(Events.ERROR, {"type": ErrorTypes.MEDIA_ERROR, "details": details, "fatal": False,
-                                       "frag": frag, "reason": str(r.get("error") or r.get("status"))})
-            self._kick()
+            # retried like a load error: back-off, up to fragLoadingMaxRetry, then fatal.  An
+            # immediate reload of bytes that fail the same way (a cached copy) would spin this
+            # loop without time advancing; the wrapper drops the cached copy on this event
+            cfg = hls.config
+            n = self._retry.get(key, 0) + 1
+            data = {"type": ErrorTypes.MEDIA_ERROR, "details": details, "fatal": n > cfg.fragLoadingMaxRetry,
+                    "frag": frag, "reason": str(r.get("error") or r.get("status"))}
+            hls.trigger(Events.ERROR, data)
+            if data["fatal"]:
+                log.error("fragment sn=%s level=%s failed: %s", frag.sn, frag.level, details)
+                self.state = self.ERROR
+                return
+            self._retry[key] = n
+            delay = min(2 ** (n - 1) * cfg.fragLoadingRetryDelay, 64000)
+            self._retry_until = self.loop.now() + delay
+            self.loop.set_timeout(self._kick, delay)
             return
         info = r["info"]
         if frag.level not in self._init_levels:
@@ -768,6 +782,8 @@ class StreamController:
         dt = max(now - tfirst, 1e-3)
         self.fragLastKbps = round(8 * length / dt)
         self.inflight.pop(key, None)
+        if self._retry:
+            self._retry.pop(key, None)  # loaded, decrypted and demuxed: its retry count starts over
         self.fragPrevious = frag
         self.fragments_buffered += 1
         self.bytes_buffered += int(length)

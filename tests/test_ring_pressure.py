@@ -84,3 +84,35 @@ def test_a_peer_wanting_the_segments_a_rank_overwrites_this_round():
         assert nodes[0].directory.digest == nodes[1].directory.digest
     finally:
         clear_origins()
+
+
+def test_a_rounds_several_runs_wrap_together():
+    """A round reserves a CDN run and one run per source peer.  Runs that wrapped one by one
+    skipped the ring's tail in the middle of the round, and the runs after the wrap could land
+    on the round's own, pinned, earlier runs: admission's single-run check passed and the third
+    reservation failed (a 3-segment cache in tests/swarm_chaos.py, seed 153).  The round now
+    wraps before its first run when its admitted total would cross the end (``wrap_for``)."""
+    from hlsjs_p2p_wrapper_amd.ops._native import runtime
+
+    rt = runtime()
+
+    def fresh():
+        st = rt.SegmentStore(1024, 16)
+        _, ids, _ = st.reserve_run(np.array([[9, 0, 0, 0]], dtype=np.int64), np.array([320]), 0)
+        st.commit(ids)  # head -> 320; the entry stays unpinned (evictable)
+        return st
+
+    def run(st, sn, n):
+        r = st.reserve_run(np.array([[9, 0, 0, sn]], dtype=np.int64), np.array([n], dtype=np.int64), 0)
+        if r is not None:
+            st.pin(r[1])  # in flight: pinned until its round completes
+        return r
+
+    st = fresh()
+    assert st.fits(896)  # admission: 896 bytes, wrapping past the 320-byte head
+    # runs placed one by one: 512 before the end, 320 wraps to 0, 64 lands on the first run
+    assert run(st, 1, 512) is not None and run(st, 2, 320) is not None and run(st, 3, 64) is None
+    st = fresh()
+    assert st.wrap_for(896)  # the round wraps first: its runs fill [0, 896)
+    assert all(run(st, sn, n) is not None for sn, n in ((1, 512), (2, 320), (3, 64)))
+    assert st.wrap_for(64) and st.wrap_for(0)  # (no-ops: 64 fits before the end)

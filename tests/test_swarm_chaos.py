@@ -8,12 +8,16 @@ Seed 80 found a stream-loop livelock: after a seek to just before a buffered ran
 fragments in flight, the loop re-loaded the already-buffered fragments past the in-flight
 run; each reload completed at once from the cache and re-kicked the loop, so (on the
 virtual clock) time never advanced and the fragment under the playhead never arrived.
-The loop now skips fragments already in the buffer."""
+The loop now skips fragments already in the buffer.  Seed 119: that skip must not treat a
+fragment as buffered when back-buffer eviction cut the range just past its start (a hole
+the playhead stalls at).  Seed 153: a round's several ring reservations (CDN run, one run
+per source peer) overlapped their own earlier runs when the total wrapped the ring; the
+rank failed with "cannot make room" (a round now wraps before its first run: ``wrap_for``)."""
 import pytest
 
 from swarm_chaos import check, scenario
 
 
-@pytest.mark.parametrize("seed", [2, 9, 26, 29, 80])
+@pytest.mark.parametrize("seed", [2, 9, 26, 29, 80, 119, 153])
 def test_chaos_scenario(seed):
     check(scenario(seed))

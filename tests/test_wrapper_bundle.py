@@ -197,6 +197,34 @@ def test_bundle_plays_from_start(vod):
     assert loop.run_until(lambda: media.currentTime > 1.0, timeout_ms=30_000)
 
 
+def test_a_fragment_that_never_decrypts_is_retried_with_backoff_then_fatal(vod):
+    """Bytes that fail to decrypt (here: a wrong key) are retried like a load error -- back-off,
+    up to fragLoadingMaxRetry, then a fatal FRAG_DECRYPT_ERROR -- instead of being reloaded at
+    once forever; on each failure the wrapper has the node drop its cached copy, so every retry
+    is a fresh CDN fetch."""
+    loop = new_event_loop("virtual")
+    hls = Hls({"debug": True, "fragLoadingMaxRetry": 2, "fragLoadingRetryDelay": 100}, P2P)
+    media = MediaElement()
+    errors = []
+    hls.on(Hls.Events.ERROR, lambda e, d: errors.append((d.get("details"), d.get("fatal"))))
+
+    def wrong_key(e, d):
+        for uri in list(hls.keyLoader.keys):
+            hls.keyLoader.keys[uri] = bytes(16)
+    hls.on(Hls.Events.KEY_LOADED, wrong_key)
+    _start(hls, media, vod.master_url())
+    t0 = loop.now()
+    assert loop.run_until(lambda: any(f for _, f in errors), timeout_ms=60_000)
+    assert errors[-1] == ("fragDecryptError", True) and len(errors) == 3
+    assert [f for _, f in errors] == [False, False, True]
+    assert loop.now() - t0 >= 300  # two back-offs: 100 ms, then 200 ms
+    from hlsjs_p2p_wrapper_amd.agent import current_node
+
+    node = current_node()
+    assert node.stats["invalidated"] >= 2 and node.stats["cdn_segments"] >= 3
+    hls.destroy()
+
+
 def test_bundle_recovers_from_a_media_error_and_keeps_playing(vod):
     """hls.js's ``recoverMediaError()`` (detach + re-attach the media element) mid-playback:
     buffering and the playback clock resume; the level statics of hls.js answer."""
