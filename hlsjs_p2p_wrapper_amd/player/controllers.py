@@ -576,6 +576,7 @@ class StreamController:
             if abs(media.currentTime - pos0) > 1e-9:
                 media.currentTime = pos0
         cfg = hls.config
+        self._seek_over_hole(media, cfg)
         pos = media.currentTime
         buf_end = pos
         for s, e in media.buffered:
@@ -614,6 +615,30 @@ class StreamController:
                 continue
             self._load(frag)
             nxt = frag.end
+
+    def _seek_over_hole(self, media: Any, cfg: Any) -> None:
+        """hls.js ``_checkBuffer``: no media at the playhead but a buffered range starts less
+        than ``maxSeekHole`` ahead (a seek that landed just before a range, a range evicted up
+        to just past a fragment's start, a gap between appends) -> jump to that range's start +
+        ``seekHoleNudgeDuration`` and report ``BUFFER_SEEK_OVER_HOLE`` (non-fatal).  The stream
+        loop counts the playhead as inside a range that starts within ``maxBufferHole``, so it
+        never loads that hole; without the jump the playhead waits there forever."""
+        if media.paused and not media.seeking:
+            return
+        pos = media.currentTime
+        nxt = None
+        for s, e in media.buffered:
+            if s <= pos < e:
+                return  # media at the playhead
+            if s > pos:
+                nxt = s
+                break
+        if nxt is None or nxt - pos >= float(cfg.get("maxSeekHole", 2) or 0):
+            return
+        target = nxt + float(cfg.get("seekHoleNudgeDuration", 0.01) or 0)
+        media.currentTime = target
+        self.hls.trigger(Events.ERROR, {"type": ErrorTypes.MEDIA_ERROR, "details": ErrorDetails.BUFFER_SEEK_OVER_HOLE,
+                                        "fatal": False, "hole": target - pos})
 
     def _run_end(self, nxt: float) -> float:
         """The end of the in-flight run that continues the buffer (which ends at ``nxt``): one

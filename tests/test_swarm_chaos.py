@@ -12,12 +12,16 @@ The loop now skips fragments already in the buffer.  Seed 119: that skip must no
 fragment as buffered when back-buffer eviction cut the range just past its start (a hole
 the playhead stalls at).  Seed 153: a round's several ring reservations (CDN run, one run
 per source peer) overlapped their own earlier runs when the total wrapped the ring; the
-rank failed with "cannot make room" (a round now wraps before its first run: ``wrap_for``)."""
+rank failed with "cannot make room" (a round now wraps before its first run: ``wrap_for``).
+Seed 271: a seek that lands 0.2 s before a buffered range never completed -- the stream loop
+counts the playhead as inside a range that starts within ``maxBufferHole`` and loads nothing,
+the media has no data at the playhead; the loop now jumps such holes as hls.js does
+(``BUFFER_SEEK_OVER_HOLE``)."""
 import pytest
 
 from swarm_chaos import check, scenario
 
 
-@pytest.mark.parametrize("seed", [2, 9, 26, 29, 80, 119, 153])
+@pytest.mark.parametrize("seed", [2, 9, 26, 29, 80, 119, 153, 208, 271])
 def test_chaos_scenario(seed):
     check(scenario(seed))
