@@ -4,7 +4,7 @@ offline periods, P2P download toggles, corrupted peer copies and deferred verifi
 scenario passes when every peer plays to the end without an exception or a media error.
 
 Used by ``tests/test_swarm_chaos.py`` (a few fixed seeds) and runnable directly for a wider
-sweep: ``python tests/swarm_chaos.py 0 200``.
+sweep: ``python tests/swarm_chaos.py 0 200 [--extras]``.
 """
 from __future__ import annotations
 
@@ -23,7 +23,9 @@ from hlsjs_p2p_wrapper_amd.player import MediaElement
 from hlsjs_p2p_wrapper_amd.player.hls import Hls as Engine
 
 
-def scenario(seed: int) -> dict:
+def scenario(seed: int, extras: bool = False) -> dict:
+    """``extras``: also pause / resume playback and stop / restart loading at random times
+    (drawn from a second generator, so the base scenario of a seed does not change)."""
     rng = np.random.default_rng(seed)
     n = int(rng.integers(2, 5))
     nseg = int(rng.integers(12, 30))
@@ -49,6 +51,12 @@ def scenario(seed: int) -> dict:
             t = float(rng.uniform(2_000, duration * 1000 * 0.7))
             kind = str(rng.choice(["seek", "offline", "nodl", "corrupt", "level"]))
             peers[r]["events"].append((t, kind, float(rng.uniform(0, duration * 0.8))))
+    if extras:
+        rng2 = np.random.default_rng(seed + 1_000_003)
+        for r in range(n):
+            for _ in range(int(rng2.integers(0, 3))):
+                t = float(rng2.uniform(2_000, duration * 1000 * 0.7))
+                peers[r]["events"].append((t, str(rng2.choice(["pause", "restart"])), float(rng2.uniform(500, 4_000))))
     hub = ThreadHub(n)
     out, errs = {}, []
 
@@ -87,6 +95,12 @@ def scenario(seed: int) -> dict:
                     loop.set_timeout(lambda: setattr(node, "corrupt_next_recv", 2), t)
                 elif kind == "level" and ladder:
                     loop.set_timeout(lambda a=arg: setattr(hls, "nextLevel", int(a) % 3), t)
+                elif kind == "pause":
+                    loop.set_timeout(media.pause, t)
+                    loop.set_timeout(media.play, t + arg)
+                elif kind == "restart":
+                    loop.set_timeout(hls.stopLoad, t)
+                    loop.set_timeout(lambda: hls.startLoad(media.currentTime), t + arg)
             ok = loop.run_until(lambda: media.currentTime >= duration - 4.5, timeout_ms=900_000)
             out[r] = {"ok": ok, "t": media.currentTime, "fatal": media_errors, "stats": dict(w.stats)}
             node.close()
@@ -112,9 +126,10 @@ def check(res: dict) -> None:
 
 if __name__ == "__main__":
     lo, hi = (int(sys.argv[1]), int(sys.argv[2])) if len(sys.argv) > 2 else (0, 20)
+    extras = "--extras" in sys.argv
     bad = []
     for s in range(lo, hi):
-        res = scenario(s)
+        res = scenario(s, extras)
         try:
             check(res)
             print(f"seed {s}: ok ({res['n']} peers)", flush=True)
