@@ -576,19 +576,26 @@ class StreamController:
             if abs(media.currentTime - pos0) > 1e-9:
                 media.currentTime = pos0
         cfg = hls.config
-        self._seek_over_hole(media, cfg)
+        ranges = list(media.buffered)  # one walk of the buffered ranges per tick
+        if ranges and (media.seeking or not media.paused):
+            self._seek_over_hole(media, cfg, ranges)
         pos = media.currentTime
+        hole = cfg.maxBufferHole
         buf_end = pos
-        for s, e in media.buffered:
-            if s - cfg.maxBufferHole <= pos < e:
+        later = None  # buffered ranges past the one the playhead is in
+        for i, (s, e) in enumerate(ranges):
+            if s - hole <= pos < e:
                 buf_end = e
+                later = ranges[i + 1:]
+                break
+            if s > pos:
+                later = ranges[i:]
                 break
         bitrate = level.bitrate or 1
         max_buf = max(8.0 * (cfg.maxBufferSize or 0) / bitrate, float(cfg.maxBufferLength))
         max_buf = min(max_buf, float(cfg.maxMaxBufferLength))
         max_inflight = max(1, int(cfg.get("maxFragLoadsInFlight", 1) or 1))
         nxt = self._run_end(buf_end)
-        ranges = None
         while len(self.inflight) < max_inflight and nxt - pos < max_buf:
             frag = self._frag_at(details, nxt)
             if frag is None:
@@ -601,33 +608,30 @@ class StreamController:
             if key in self.inflight:
                 nxt = frag.end
                 continue
-            # a fragment already in the buffer past the run being loaded (after a seek to just
-            # before a buffered range, with fragments in flight) is skipped, not loaded again:
-            # reloading it from the cache would complete at once and re-kick this loop forever
-            if ranges is None:
-                ranges = list(media.buffered)
-                hole = cfg.maxBufferHole
-            fs, fe = frag.start, frag.end
-            # covered: one range from the fragment's start (a range evicted up to just past it
-            # leaves a hole to fill) to within a hole of its end (ranges end at the media end)
-            if any(s <= fs + 1e-3 and e >= fe - hole for s, e in ranges):
-                nxt = fe
-                continue
+            if later:
+                # a fragment already in a later buffered range (after a seek to just before
+                # it, with fragments in flight) is skipped, not loaded again: reloading it from
+                # the cache would complete at once and re-kick this loop forever.  Covered: one
+                # range from the fragment's start (a range evicted up to just past it leaves a
+                # hole to fill) to within a hole of its end (ranges end at the media end)
+                fs = frag._start
+                fe = fs + frag.duration
+                if any(s <= fs + 1e-3 and e >= fe - hole for s, e in later):
+                    nxt = fe
+                    continue
             self._load(frag)
             nxt = frag.end
 
-    def _seek_over_hole(self, media: Any, cfg: Any) -> None:
+    def _seek_over_hole(self, media: Any, cfg: Any, ranges: List[Tuple[float, float]]) -> None:
         """hls.js ``_checkBuffer``: no media at the playhead but a buffered range starts less
         than ``maxSeekHole`` ahead (a seek that landed just before a range, a range evicted up
         to just past a fragment's start, a gap between appends) -> jump to that range's start +
         ``seekHoleNudgeDuration`` and report ``BUFFER_SEEK_OVER_HOLE`` (non-fatal).  The stream
         loop counts the playhead as inside a range that starts within ``maxBufferHole``, so it
         never loads that hole; without the jump the playhead waits there forever."""
-        if media.paused and not media.seeking:
-            return
         pos = media.currentTime
         nxt = None
-        for s, e in media.buffered:
+        for s, e in ranges:
             if s <= pos < e:
                 return  # media at the playhead
             if s > pos:
