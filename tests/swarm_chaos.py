@@ -4,7 +4,7 @@ offline periods, P2P download toggles, corrupted peer copies and deferred verifi
 scenario passes when every peer plays to the end without an exception or a media error.
 
 Used by ``tests/test_swarm_chaos.py`` (a few fixed seeds) and runnable directly for a wider
-sweep: ``python tests/swarm_chaos.py 0 200 [--extras]``.
+sweep: ``python tests/swarm_chaos.py 0 200 [--extras] [--gpu]``.
 """
 from __future__ import annotations
 
@@ -23,9 +23,11 @@ from hlsjs_p2p_wrapper_amd.player import MediaElement
 from hlsjs_p2p_wrapper_amd.player.hls import Hls as Engine
 
 
-def scenario(seed: int, extras: bool = False) -> dict:
+def scenario(seed: int, extras: bool = False, device: str = "cpu") -> dict:
     """``extras``: also pause / resume playback and stop / restart loading at random times
-    (drawn from a second generator, so the base scenario of a seed does not change)."""
+    (drawn from a second generator, so the base scenario of a seed does not change).
+    ``device``: where the peers' caches and the transmux live (``cuda:0``: every peer on the
+    one GPU, with its streams, events and asynchronous copies)."""
     rng = np.random.default_rng(seed)
     n = int(rng.integers(2, 5))
     nseg = int(rng.integers(12, 30))
@@ -65,7 +67,7 @@ def scenario(seed: int, extras: bool = False) -> dict:
         try:
             set_current_node(None)
             loop = new_event_loop("virtual")
-            gs = {"backend": "thread", "hub": hub, "rank": r, "device": "cpu",
+            gs = {"backend": "thread", "hub": hub, "rank": r, "device": device,
                   "cacheBytes": p["cache_segs"] * ((seg + 255) // 256 * 256), "roundIntervalMs": 20,
                   "deferVerify": p["defer"]}
             node = node_for_config({"gpuSwarm": gs})
@@ -127,9 +129,10 @@ def check(res: dict) -> None:
 if __name__ == "__main__":
     lo, hi = (int(sys.argv[1]), int(sys.argv[2])) if len(sys.argv) > 2 else (0, 20)
     extras = "--extras" in sys.argv
+    device = "cuda:0" if "--gpu" in sys.argv else "cpu"
     bad = []
     for s in range(lo, hi):
-        res = scenario(s, extras)
+        res = scenario(s, extras, device)
         try:
             check(res)
             print(f"seed {s}: ok ({res['n']} peers)", flush=True)

@@ -25,3 +25,11 @@ from swarm_chaos import check, scenario
 @pytest.mark.parametrize("seed", [2, 9, 26, 29, 80, 119, 153, 208, 271])
 def test_chaos_scenario(seed):
     check(scenario(seed))
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("seed", [80, 153, 271])
+def test_chaos_scenario_on_the_gpu(cuda, seed):
+    """The same scenarios with every peer's cache and transmux on the MI355X (streams, events
+    and asynchronous copies under seeks, aborts, evictions and corrupted copies)."""
+    check(scenario(seed, device="cuda:0"))
