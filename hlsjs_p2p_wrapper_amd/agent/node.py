@@ -71,7 +71,10 @@ _M32 = 0xFFFFFFFF
 
 
 W_FORCE_CDN, W_NOT_STAGED, W_STAGING, W_PREFETCH, W_PY, W_CORRUPT = 1, 2, 4, 8, 16, 32
-W_ON_DEV = 64  # the origin bytes live in device memory (diagnostic HBM origin): D2D copies
+# the origin bytes live in device memory (diagnostic HBM origin): D2D copies.  (Was 64, the
+# want table's own "held" bit: a requeued want -- a corrupted peer copy -- then looked
+# device-resident to the CDN phase.)
+W_ON_DEV = 128
 SRC_CDN, SRC_P2P, SRC_CACHE = 0, 1, 2  # source codes of delivery columns (parallel/fleet.SOURCES)
 SOURCE_NAMES = ("cdn", "p2p", "cache")
 

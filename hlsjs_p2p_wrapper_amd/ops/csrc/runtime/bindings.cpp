@@ -804,6 +804,8 @@ PYBIND11_MODULE(_runtime, m) {
   m.attr("WANT_PREFETCH") = int64_t(kWPrefetch);
   m.attr("WANT_PY") = int64_t(kWPy);
   m.attr("WANT_CORRUPT") = int64_t(kWCorrupt);
+  m.attr("WANT_HELD") = int64_t(kWHeld);
+  m.attr("WANT_ON_DEV") = int64_t(kWOnDev);
   m.attr("NO_TOKEN") = kNoToken;
 
   // ------------------------------------------------------------------ intra-node control plane

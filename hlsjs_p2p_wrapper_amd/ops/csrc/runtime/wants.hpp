@@ -30,6 +30,7 @@ enum WantBits : int32_t {
   kWPy = 16,        // the node keeps Python-side state for it (network / live origin)
   kWCorrupt = 32,   // fault injection: corrupt the CDN copy on ingest
   kWHeld = 64,      // announced before and not served (the planner holds a want back at most once)
+  kWOnDev = 128,    // the node's: the origin bytes live in device memory (D2D ingest copies)
 };
 
 constexpr int64_t kNoToken = -1;

@@ -362,3 +362,22 @@ def test_want_table_unstaged_size_from_directory(rt):
     st.unpin(e)
     adm, rows, _, _, _ = wt.select(st, d, -1, 3)
     assert adm.tolist() == ids.tolist() and rows[0, 4] == 3000
+
+
+def test_the_nodes_want_flags_match_the_want_table_bits(rt):
+    """The node ORs its own flags into the want table's (requests, locator, CDN phase): each
+    must be the table's bit of that name and none may alias another.  W_ON_DEV once shared
+    bit 64 with the table's "held" bit, so a requeued want looked device-resident to the GPU
+    CDN phase."""
+    from hlsjs_p2p_wrapper_amd.agent import node as n
+
+    assert (n.W_FORCE_CDN, n.W_NOT_STAGED, n.W_STAGING, n.W_PREFETCH, n.W_PY, n.W_CORRUPT, n.W_ON_DEV) == (
+        rt.WANT_FORCE_CDN, rt.WANT_NOT_STAGED, rt.WANT_STAGING, rt.WANT_PREFETCH, rt.WANT_PY, rt.WANT_CORRUPT,
+        rt.WANT_ON_DEV)
+    bits = [rt.WANT_FORCE_CDN, rt.WANT_NOT_STAGED, rt.WANT_STAGING, rt.WANT_PREFETCH, rt.WANT_PY, rt.WANT_CORRUPT,
+            rt.WANT_HELD, rt.WANT_ON_DEV]
+    assert len(set(bits)) == len(bits) and all(b & (b - 1) == 0 for b in bits)
+    wt = rt.WantTable()
+    ids, _ = _add(wt, keys(3), size=100, flags=0, tokens=[1])
+    wt.requeue(ids, False)
+    assert not (wt.info(ids)[0, 7] & n.W_ON_DEV)  # held, not device-resident
