@@ -1581,8 +1581,11 @@ class SwarmNode:
             self.stats["crc_failures"] += 1
             toks = tokens[inv == k]
             self._retry_cdn(self._vinfo[e], toks[toks >= 0])  # bulk (fleet) tokens: asked again here
-            # in-process requests were answered already: their players ask again, from the CDN
-            self._force_cdn_keys.add(tuple(int(v) & _M32 for v in self._vinfo[e][:4]))
+            if (toks < 0).any():
+                # in-process requests were answered already: their players ask again, from the
+                # CDN.  (Bulk-only entries are re-fetched above; a key nobody will ask for again
+                # must not sit in the set: request_batch checks every key while it is non-empty)
+                self._force_cdn_keys.add(tuple(int(v) & _M32 for v in self._vinfo[e][:4]))
         return len(bad)
 
     # ------------------------------------------------------------------ delivery
