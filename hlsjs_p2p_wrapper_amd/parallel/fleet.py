@@ -666,6 +666,10 @@ class FleetServer:
         self.evicted = 0  # cache entries dropped by the players' live-window eviction
         self.batches_sent = [0] * W  # answer batches sent to each player ...
         self.batches_done = [0] * W  # ... and handled by it (reported back)
+        # entries answered to an on-demand player stay pinned until it handled their answer
+        # batch, so RemoteSegment.data() in its onSuccess finds them cached: per player
+        # (answer batch number, time sent, entry ids)
+        self._holds: List["collections.deque"] = [collections.deque() for _ in range(W)]
         node.set_bulk_sink(self)
         # segments received from peers are CRC-checked by the transmux that decrypts them (the
         # CRC fused into the AES kernel), not by a separate read in the node's round: results
@@ -682,6 +686,11 @@ class FleetServer:
         CRC each fragment's bytes must have (-1: verified by the node already)."""
         if expect is None:
             expect = np.full(len(tok), -1, dtype=np.int64)
+        # pinned from here until the answer is out: through the transmux that reads them, and
+        # for an on-demand player until it handled the answer (see complete_transmux)
+        he = eids[eids >= 0]
+        if len(he):
+            self.node.store.pin(he)
         self._delivered.append((tok, src, nbytes, cdn_ms, p2p_ms, offs, eids, expect))
 
     def fail(self, tok, status) -> None:
@@ -729,6 +738,8 @@ class FleetServer:
             self._finish_fetches()
         for w, conn in enumerate(self.conns):
             if not self.open[w]:
+                if self._holds[w]:
+                    self._release_holds(w)
                 continue
             try:
                 while conn.poll(0):
@@ -764,7 +775,18 @@ class FleetServer:
                         break
             except (EOFError, OSError):
                 self.open[w] = False
+            if self._holds[w]:
+                self._release_holds(w)
         return n
+
+    def _release_holds(self, w: int) -> None:
+        """Unpin the entries of answer batches player ``w`` has handled -- or that it did not
+        acknowledge within ``ring_ack_timeout_s``, or all of them once it left."""
+        q = self._holds[w]
+        done, stale, gone = self.batches_done[w], time.monotonic() - self.ring_ack_timeout_s, not self.open[w]
+        store = self.node.store
+        while q and (gone or q[0][0] <= done or q[0][1] < stale):
+            store.unpin(q.popleft()[2])
 
     def _start_fetch(self, w: int, fid: int, keys) -> None:
         """Start copying an answer chunk's cached segments to the host for player ``w``
@@ -897,8 +919,12 @@ class FleetServer:
             self.verify_failures += self.node.verify_done(eids[chk], verified[chk], tok[chk])
             if not verified.all():  # no answer for a corrupted copy: the CDN retry answers
                 keep = verified
-                tok, src, nbytes, cdn_ms, p2p_ms, offs = (tok[keep], src[keep], nbytes[keep], cdn_ms[keep],
-                                                          p2p_ms[keep], offs[keep])
+                dropped = eids[~keep]
+                dropped = dropped[dropped >= 0]
+                if len(dropped):
+                    self.node.store.unpin(dropped)  # (deliver's pin)
+                tok, src, nbytes, cdn_ms, p2p_ms, offs, eids = (tok[keep], src[keep], nbytes[keep], cdn_ms[keep],
+                                                                p2p_ms[keep], offs[keep], eids[keep])
                 rows, plain, has = rows[keep], plain[keep], has[keep]
                 if ring_off is not None:
                     ring_off = ring_off[keep]
@@ -912,6 +938,13 @@ class FleetServer:
             if ring_off is not None and self._payload[p]:
                 chunk = chunk + ((self._ring.shm.name, ring_off[sel], nbytes[sel]),)
                 need[p] = self.batches_sent[p] + 1  # the answer batch the next send() carries
+            he = eids[sel]
+            he = he[he >= 0]
+            if len(he):  # deliver's pin: kept for an on-demand player until it handled this batch
+                if self.open[p] and not (ring_off is not None and self._payload[p]):
+                    self._holds[p].append((self.batches_sent[p] + 1, time.monotonic(), he))
+                else:
+                    self.node.store.unpin(he)
             self._chunks[p].append(chunk)
         if pay is not None:
             region[2] = need
@@ -1123,11 +1156,30 @@ class FleetServer:
 
 
 # ============================================================================ player process
+def _script_action(hls: Any, media: Any, loop: Any, action: str, arg: Any) -> None:
+    """One scripted player action (``player_main`` ``spec["script"]``)."""
+    if action == "seek":
+        media.currentTime = float(arg)
+    elif action == "pause":
+        media.pause()
+        loop.set_timeout(media.play, float(arg))
+    elif action == "level":
+        if hls.levels:
+            hls.nextLevel = int(arg) % len(hls.levels)
+    elif action == "restart":
+        hls.stopLoad()
+        loop.set_timeout(lambda: hls.startLoad(media.currentTime), float(arg))
+    else:
+        raise ValueError(f"unknown scripted action {action!r}")
+
+
 def player_main(conn: Any, spec: Dict[str, Any]) -> None:
     """A fleet player process: the bundle ``Hls`` over a :class:`RemoteNode`, drained as fast
     as the node answers (the throughput bench's player).  ``spec``: ``origin`` (keyword
     arguments of ``SyntheticHlsOrigin``: the player reads playlists and keys from it, the
-    node process serves the segments), ``hls_config``, ``p2p_config``, ``world``, ``rank``.
+    node process serves the segments), ``hls_config``, ``p2p_config``, ``world``, ``rank``;
+    for tests, ``script`` (scheduled seeks, pauses, level switches, load restarts) and
+    ``read_bytes`` (read every fragment's bytes back through ``RemoteSegment.data()``).
     Control from the node: ``("mark", tag)`` -> reply ``("mark", tag, counters)`` once every
     answer sent before it is buffered; ``("stop",)`` -> close and exit."""
     import copy
@@ -1168,6 +1220,18 @@ def player_main(conn: Any, spec: Dict[str, Any]) -> None:
 
     hls.on(Hls.Events.FRAG_BUFFERED, on_buffered)
     hls.on(Hls.Events.ERROR, lambda e, d: counters.__setitem__("errors", counters["errors"] + 1))
+    hls.on(Hls.Events.ERROR,
+           lambda e, d: counters.__setitem__("fatal", counters.get("fatal", 0) + bool(d.get("fatal"))))
+    if spec.get("read_bytes"):  # every fragment's bytes read back through RemoteSegment.data()
+
+        def read_back(e, d):
+            seg = d.get("payload")
+            data = seg.data() if isinstance(seg, RemoteSegment) else None
+            if data is None or len(data) != seg.nbytes:
+                counters["byte_errors"] = counters.get("byte_errors", 0) + 1
+            else:
+                counters["bytes_read"] = counters.get("bytes_read", 0) + len(data)
+        hls.on(Hls.Events.FRAG_LOADED, read_back)
     hls.on(Hls.Events.LEVEL_SWITCH, lambda e, d: counters.__setitem__("level_switches",
                                                                      counters["level_switches"] + 1))
     # start together: a player that started early would run ahead into the next one's slice
@@ -1186,6 +1250,9 @@ def player_main(conn: Any, spec: Dict[str, Any]) -> None:
     hls.attachMedia(media)
     hls.on(Hls.Events.MANIFEST_PARSED, lambda e, d: media.play())
     sc = hls.streamController
+    # tests / diagnostics: scripted player actions, (ms after start, action, argument)
+    for t_ms, action, arg in spec.get("script") or ():
+        loop.set_timeout(_script_action, float(t_ms), hls, media, loop, action, arg)
 
     def drain():
         loop.run_once(block=False)  # due timers too (live playlist reloads, the playback clock)
@@ -1225,6 +1292,7 @@ def player_main(conn: Any, spec: Dict[str, Any]) -> None:
                     counters["bytes"] = node.stats.get("cdn", 0) + node.stats.get("p2p", 0)
                     out = dict(counters)
                     out["cpu_s"] = time.process_time()
+                    out["t"] = media.currentTime
                     if len(msg) > 2 and msg[2].get("calib"):  # soak analysis: core speed at the mark
                         out["calib_us"] = cpu_calibration_us()
                     if live_lat:  # live latency behind the edge since the previous mark
