@@ -1179,7 +1179,8 @@ def player_main(conn: Any, spec: Dict[str, Any]) -> None:
     arguments of ``SyntheticHlsOrigin``: the player reads playlists and keys from it, the
     node process serves the segments), ``hls_config``, ``p2p_config``, ``world``, ``rank``;
     for tests, ``script`` (scheduled seeks, pauses, level switches, load restarts) and
-    ``read_bytes`` (read every fragment's bytes back through ``RemoteSegment.data()``).
+    ``read_bytes`` (read every fragment's bytes back through ``RemoteSegment.data()``) and
+    ``in_process`` (a thread in the node's process: leave its torch threads and GPU alone).
     Control from the node: ``("mark", tag)`` -> reply ``("mark", tag, counters)`` once every
     answer sent before it is buffered; ``("stop",)`` -> close and exit."""
     import copy
@@ -1193,8 +1194,10 @@ def player_main(conn: Any, spec: Dict[str, Any]) -> None:
 
     import torch
 
-    torch.set_num_threads(1)  # a player does no tensor math: no intra-op pool competing for cores
-    if torch.cuda.device_count():
+    in_process = bool(spec.get("in_process"))  # a thread beside the node (tests/fleet_chaos.py)
+    if not in_process:
+        torch.set_num_threads(1)  # a player does no tensor math: no intra-op pool competing for cores
+    if torch.cuda.device_count() and not in_process:
         log.warning("fleet player sees %d GPU(s); it should not (HIP_VISIBLE_DEVICES)", torch.cuda.device_count())
     set_current_node(None)
     speed = float(spec.get("clock_speed", 1.0))

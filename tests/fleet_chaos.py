@@ -69,7 +69,7 @@ def scenario(seed: int, timeout_s: float = 120.0, device: str = "cpu") -> dict:
                                "tickInterval": 1e9},
                 "p2p_config": {"streamrootKey": "t", "contentId": f"fleet-chaos-{seed}",
                                "gpuSwarm": {"fleetPayload": p["payload"]}},
-                "world": 1, "rank": 0, "script": p["script"], "read_bytes": p["read"]}
+                "world": 1, "rank": 0, "script": p["script"], "read_bytes": p["read"], "in_process": True}
 
         def run(c=child, s=spec):
             try:
