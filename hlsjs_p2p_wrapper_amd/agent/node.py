@@ -346,6 +346,10 @@ class SwarmNode:
         self._vinfo = np.zeros((0, 10), dtype=np.int64)
         self._vround = np.zeros(0, dtype=np.int64)  # round each pending entry was delivered in
         self._vexp = np.zeros(0, dtype=np.int64)  # its expected CRC (the sender's trailer)
+        # bulk tokens asking for a segment whose received copy awaits its check: answered from
+        # that copy once it passes (another fetch of the segment would replace the copy in the
+        # index while its first consumers still read it), or from the CDN if it fails
+        self._vwait: Dict[int, List[np.ndarray]] = {}
         # in-process requests join the deferred check too (gpuSwarm.deferVerify): their bytes
         # reach the loader with a VerifyTicket, the player's transmux batch verifies them (the
         # CRC fused into its decrypt) and reports back; a copy that fails is detached and the
@@ -598,6 +602,10 @@ class SwarmNode:
                 return
         else:
             miss = None
+        if self._vflag.any():  # (a flag per entry id: small)
+            miss = self._park_on_pending(keys, tokens, miss)
+            if miss is not None and not len(miss):
+                return
         idx = range(n) if miss is None else miss.tolist()
         m = n if miss is None else len(miss)
         sizes = np.zeros(m, dtype=np.int64)
@@ -748,6 +756,35 @@ class SwarmNode:
             self._deliver_req(req, src or "cache", n, 0.0, 0.0, self.arena[off:off + n], -1, eid)
         finally:
             self.store.unpin(np.array([eid], dtype=np.int64))
+
+    def _park_on_pending(self, keys: np.ndarray, tokens: np.ndarray, miss: Optional[np.ndarray]) -> np.ndarray:
+        """Requests (rows ``miss`` of ``keys``; all when None) for segments whose received copy
+        is delivered and awaits its deferred check wait for that check (:meth:`verify_done`)
+        instead of fetching the segment again.  Returns the rows still to fetch."""
+        rows = np.arange(len(tokens)) if miss is None else miss
+        pe = self.store.lookup(np.ascontiguousarray(keys[rows]), True)
+        park = pe >= 0
+        park[park] = pe[park] < len(self._vflag)
+        park[park] = self._vflag[pe[park]]
+        if not park.any():
+            return rows if miss is not None else None
+        for e, t in zip(pe[park].tolist(), tokens[rows[park]].tolist()):
+            self._vwait.setdefault(e, []).append(t)
+        self.stats["parked"] = self.stats.get("parked", 0) + int(park.sum())
+        return rows[~park]
+
+    def _release_parked(self, e: int, ok: bool) -> None:
+        toks = np.asarray(self._vwait.pop(e), dtype=np.int64)
+        if ok:  # the copy is committed: a cache hit
+            arr = np.array([e], dtype=np.int64)
+            ids = np.repeat(arr, len(toks))
+            self.store.pin(ids)
+            self._bulk_hits.append((toks, ids))
+            if not self._bulk_hits_scheduled:
+                self._bulk_hits_scheduled = True
+                self.loop.call_soon(self._serve_bulk_hits)
+        else:
+            self._retry_cdn(self._vinfo[e], toks)
 
     def _serve_bulk_hits(self) -> None:
         """Answer the bulk requests that hit the cache (pinned at request time)."""
@@ -1571,6 +1608,10 @@ class SwarmNode:
             self._vflag[good] = False
             self.store.commit(good)
             self.store.unpin(good)
+            if self._vwait:
+                for e in good.tolist():
+                    if e in self._vwait:
+                        self._release_parked(e, True)
         bad = np.flatnonzero(pend & ~uok)
         for k in bad.tolist():
             e = int(ue[k])
@@ -1581,6 +1622,8 @@ class SwarmNode:
             self.stats["crc_failures"] += 1
             toks = tokens[inv == k]
             self._retry_cdn(self._vinfo[e], toks[toks >= 0])  # bulk (fleet) tokens: asked again here
+            if e in self._vwait:
+                self._release_parked(e, False)
             if (toks < 0).any():
                 # in-process requests were answered already: their players ask again, from the
                 # CDN.  (Bulk-only entries are re-fetched above; a key nobody will ask for again

@@ -195,6 +195,10 @@ void SegmentStore::commit(int64_t id) {
   Entry& e = entries_[id];
   if (e.state != kPending) return;
   e.state = kResident;
+  // a copy detached meanwhile (a newer copy of the key took its index slot) serves only the
+  // readers holding it: announcing it would let peers plan transfers this rank cannot look up
+  auto it = index_.find(e.key);
+  if (it == index_.end() || it->second != id) return;
   delta_add_.push_back(e.key);
   delta_add_len_.push_back(e.length);
 }

@@ -642,6 +642,7 @@ class FleetServer:
         # per player request slots (rid % _RING): AES key index (global, -1 = clear) and IV
         self._gkey = [np.full(_RING, -1, dtype=np.int32) for _ in range(W)]
         self._iv = [np.zeros((_RING, 16), dtype=np.uint8) for _ in range(W)]
+        self._skey = [np.zeros((_RING, 4), dtype=np.int64) for _ in range(W)]  # segment key (32-bit fields)
         self._kmap: List[Dict[int, int]] = [{} for _ in range(W)]  # player key id -> global key index
         self._gk: Dict[bytes, int] = {}
         self._drk = np.zeros((0, 44), dtype=np.uint32)  # round keys per global key index
@@ -668,7 +669,7 @@ class FleetServer:
         self.batches_done = [0] * W  # ... and handled by it (reported back)
         # entries answered to an on-demand player stay pinned until it handled their answer
         # batch, so RemoteSegment.data() in its onSuccess finds them cached: per player
-        # (answer batch number, time sent, entry ids)
+        # (answer batch number, time sent, entry ids, their keys)
         self._holds: List["collections.deque"] = [collections.deque() for _ in range(W)]
         node.set_bulk_sink(self)
         # segments received from peers are CRC-checked by the transmux that decrypts them (the
@@ -725,6 +726,7 @@ class FleetServer:
         else:
             self._gkey[w][slot] = -1
         self._iv[w][slot] = iv
+        self._skey[w][slot] = np.asarray(key, dtype=np.int64).reshape(-1, 4) & 0xFFFFFFFF
         force = np.full(len(rid), not self._down[w], dtype=bool)
         self._q[w].push(rid, key, urls, hdr, force)
         self.requests[w] += len(rid)
@@ -799,6 +801,17 @@ class FleetServer:
         store = self.node.store
         keys = np.ascontiguousarray(np.asarray(keys, dtype=np.int64).reshape(-1, 4) & 0xFFFFFFFF)
         eids = store.lookup(keys, False)
+        if self._holds[w]:
+            # the copies this player was answered with, while its batches hold them: the cache's
+            # index may name another copy by now (a second request for a segment whose peer copy
+            # awaited its check fetched it again) or none (detached), the held bytes stay put
+            held = {}
+            for _, _, he, hk in self._holds[w]:
+                held.update(zip(map(tuple, hk.tolist()), he.tolist()))
+            for i, k in enumerate(map(tuple, keys.tolist())):
+                e = held.get(k)
+                if e is not None:
+                    eids[i] = e
         hit = np.flatnonzero(eids >= 0)
         ids = np.ascontiguousarray(eids[hit])
         lens = np.zeros(0, dtype=np.int64)
@@ -939,10 +952,12 @@ class FleetServer:
                 chunk = chunk + ((self._ring.shm.name, ring_off[sel], nbytes[sel]),)
                 need[p] = self.batches_sent[p] + 1  # the answer batch the next send() carries
             he = eids[sel]
-            he = he[he >= 0]
+            cached = he >= 0
+            he = he[cached]
             if len(he):  # deliver's pin: kept for an on-demand player until it handled this batch
                 if self.open[p] and not (ring_off is not None and self._payload[p]):
-                    self._holds[p].append((self.batches_sent[p] + 1, time.monotonic(), he))
+                    hk = self._skey[p][rid[sel][cached] % _RING]
+                    self._holds[p].append((self.batches_sent[p] + 1, time.monotonic(), he, hk))
                 else:
                     self.node.store.unpin(he)
             self._chunks[p].append(chunk)
@@ -1298,6 +1313,12 @@ def player_main(conn: Any, spec: Dict[str, Any]) -> None:
                     out["t"] = media.currentTime
                     if len(msg) > 2 and msg[2].get("calib"):  # soak analysis: core speed at the mark
                         out["calib_us"] = cpu_calibration_us()
+                    if len(msg) > 2 and msg[2].get("state"):  # a stalled player says what it waits on
+                        sc = hls.streamController
+                        out["state"] = {"buffered": [tuple(r) for r in media.buffered], "paused": media.paused,
+                                        "seeking": media.seeking, "stream": sc.state, "level": hls.currentLevel,
+                                        "inflight": sorted(sc.inflight), "pending": len(node._pending),
+                                        "node_inflight": node.inflight}
                     if live_lat:  # live latency behind the edge since the previous mark
                         out["live_latency_s"] = live_lat[:]
                         live_lat.clear()

@@ -1,12 +1,14 @@
-"""Randomized fleet scenarios: one rank (a CPU ``SwarmNode`` + ``FleetServer``, the bench's
-node-side loop) serving 2-3 player threads running ``player_main`` -- the process layout of
-``bench.py`` in one process -- with random caches, in-flight windows, payload modes, byte
-read-back through ``RemoteSegment.data()`` and scripted seeks, pauses, level switches and
-load restarts.  A scenario passes when every player plays to the end of the VOD with no
-fatal error, no failed byte read and no exception on either side.
+"""Randomized fleet scenarios: ranks (a CPU or GPU ``SwarmNode`` + ``FleetServer`` each, the
+bench's node-side loop) serving 2-3 player threads running ``player_main`` -- the process
+layout of ``bench.py`` in one process -- with random caches, in-flight windows, payload modes,
+byte read-back through ``RemoteSegment.data()`` and scripted seeks, pauses, level switches and
+load restarts.  With ``ranks`` > 1 the ranks are threads on a ``ThreadHub``: they share one
+content, plan peer transfers between their caches each round, and a rank's players are
+answered from its peers' caches too.  A scenario passes when every player plays to the end of
+the VOD with no fatal error, no failed byte read and no exception on any side.
 
 Used by ``tests/test_fleet_chaos.py`` (fixed seeds) and runnable directly for a sweep:
-``python tests/fleet_chaos.py 0 100`` (``--gpu``: the node on ``cuda:0``).
+``python tests/fleet_chaos.py 0 100`` (``--gpu``: the nodes on ``cuda:0``; ``--ranks=N``).
 """
 from __future__ import annotations
 
@@ -19,36 +21,21 @@ import time
 import numpy as np
 import torch
 
-from hlsjs_p2p_wrapper_amd.agent import node_for_config, set_current_node
+from hlsjs_p2p_wrapper_amd.agent.node import SwarmNode
+from hlsjs_p2p_wrapper_amd.agent import set_current_node
 from hlsjs_p2p_wrapper_amd.net import clear_origins, new_event_loop
 from hlsjs_p2p_wrapper_amd.net.origin import Rendition, SyntheticHlsOrigin
+from hlsjs_p2p_wrapper_amd.parallel import LocalComm, ThreadHub
 from hlsjs_p2p_wrapper_amd.parallel.fleet import FleetServer, player_main
 from hlsjs_p2p_wrapper_amd.player.transmux import pipeline_for
 
 
-def scenario(seed: int, timeout_s: float = 120.0, device: str = "cpu") -> dict:
-    """``device``: where the node's segment cache and the transmux live (``cuda:0``: the HBM
-    ring, the GPU transmux and the on-demand bytes copied back from the device)."""
-    rng = np.random.default_rng(seed)
-    nseg = int(rng.integers(10, 24))
-    ladder = rng.random() < 0.4
-    rends = ([Rendition(300_000, 480, 270), Rendition(700_000, 640, 360), Rendition(1_200_000, 960, 540)]
-             if ladder else [Rendition(int(rng.integers(300_000, 1_200_000)), 640, 360)])
-    origin_kw = dict(base_url=f"http://fleet.chaos{seed}/vod/", renditions=rends, num_segments=nseg,
-                     segment_duration=4.0, encrypted=bool(rng.random() < 0.7), pool_size=min(nseg, 8), seed=seed)
-    duration = nseg * 4.0
+def _draw_rank(rng, duration):
+    """One rank's draws: its player count, its cache (in segments) and its players."""
     W = int(rng.integers(2, 4))
-    clear_origins()
-    set_current_node(None)
-    loop = new_event_loop("real")
-    pinned = device != "cpu"  # the GPU CDN phase copies from pinned host buffers
-    origin = SyntheticHlsOrigin(**origin_kw, pin_memory=pinned)
-    seg = max(max(p.lengths) for p in origin.pools)
-    cache = int(rng.integers(4, 24)) * ((seg + 255) // 256 * 256)
-    node = node_for_config({"gpuSwarm": {"backend": "local", "device": device, "cacheBytes": cache,
-                                         "autoTick": False}})
+    cache_segs = int(rng.integers(4, 24))
     players = []
-    for w in range(W):
+    for _ in range(W):
         script = []
         for _ in range(int(rng.integers(0, 4))):
             t = float(rng.uniform(200, 3000))  # real milliseconds: the fleet runs on the real clock
@@ -58,88 +45,146 @@ def scenario(seed: int, timeout_s: float = 120.0, device: str = "cpu") -> dict:
             script.append((t, kind, arg))
         players.append({"inflight": int(rng.choice([1, 2, 4, 8])), "payload": bool(rng.random() < 0.3),
                         "read": bool(rng.random() < 0.5), "script": script})
-    pairs = [mp.Pipe() for _ in range(W)]
-    errs: list = []
-    threads = []
-    for w, (_, child) in enumerate(pairs):
-        p = players[w]
-        spec = {"origin": dict(origin_kw, pin_memory=pinned),
-                "hls_config": {"maxFragLoadsInFlight": p["inflight"], "maxBufferLength": 1e9,
-                               "maxMaxBufferLength": 1e9, "startPosition": 0, "startLevel": 0,
-                               "tickInterval": 1e9},
-                "p2p_config": {"streamrootKey": "t", "contentId": f"fleet-chaos-{seed}",
-                               "gpuSwarm": {"fleetPayload": p["payload"]}},
-                "world": 1, "rank": 0, "script": p["script"], "read_bytes": p["read"], "in_process": True}
+    return W, cache_segs, players
 
-        def run(c=child, s=spec):
-            try:
-                player_main(c, s)
-            except BaseException as e:  # noqa: BLE001
-                errs.append(("player", e))
-        t = threading.Thread(target=run, daemon=True)
-        t.start()
-        threads.append(t)
-    conns = [parent for parent, _ in pairs]
-    pipe = pipeline_for(torch.device(device), loop)
-    pipe.auto_flush = False
-    server = None
-    result = {"seed": seed, "players": players, "cache_segs": cache // ((seg + 255) // 256 * 256), "W": W,
-              "errors": errs, "marks": {}, "duration": duration}
-    try:
-        server = FleetServer(node, pipe, conns)
-        end = time.monotonic() + 30
-        while len(server.ready) < W:
-            server.poll()
-            time.sleep(0.002)
-            if time.monotonic() > end:
-                raise RuntimeError("players did not start")
-        for c in conns:
-            c.send(("go",))
-        hs, b = collections.deque(), None
-        deadline = time.monotonic() + timeout_s
-        next_mark, tag = time.monotonic() + 0.5, 0
-        while True:
-            while loop._ready:
-                loop.run_once(block=False)
-            server.await_players(timeout_s=0.005)
-            server.poll()
-            server.admit(8)
-            hs.append(node.launch_round())
-            if len(hs) > 1:
-                node.complete_round(hs.popleft())
-            nb = server.launch_transmux()
-            server.complete_transmux(b)
-            server.send()
-            b = nb
-            if time.monotonic() > next_mark:  # ask every player where it is
-                tag += 1
-                for w, c in enumerate(conns):
-                    if server.open[w]:
-                        c.send(("mark", tag))
-                next_mark = time.monotonic() + 0.5
-            marks = {}
-            for t_ in sorted(server.marks):
-                marks.update(server.marks[t_])
-            result["marks"] = marks
-            if len(marks) == W and all(m["t"] >= duration - 4.5 for m in marks.values()):
-                break
-            if errs or time.monotonic() > deadline:
-                break
-    except BaseException as e:  # noqa: BLE001
-        errs.append(("node", e))
-    finally:
-        for w, c in enumerate(conns):
-            try:
-                c.send(("stop",))
-            except (OSError, BrokenPipeError):
-                pass
-        for t in threads:
-            t.join(10)
-        if server is not None:
-            server.close()
-        node.close()
-        clear_origins()
+
+def scenario(seed: int, timeout_s: float = 120.0, device: str = "cpu", ranks: int = 1) -> dict:
+    """``device``: where the nodes' segment caches and the transmux live (``cuda:0``: the HBM
+    ring, the GPU transmux and the on-demand bytes copied back from the device).  ``ranks``:
+    rank 0 draws what the single-rank scenario of the seed draws; later ranks draw after it."""
+    rng = np.random.default_rng(seed)
+    nseg = int(rng.integers(10, 24))
+    ladder = rng.random() < 0.4
+    rends = ([Rendition(300_000, 480, 270), Rendition(700_000, 640, 360), Rendition(1_200_000, 960, 540)]
+             if ladder else [Rendition(int(rng.integers(300_000, 1_200_000)), 640, 360)])
+    origin_kw = dict(base_url=f"http://fleet.chaos{seed}/vod/", renditions=rends, num_segments=nseg,
+                     segment_duration=4.0, encrypted=bool(rng.random() < 0.7), pool_size=min(nseg, 8), seed=seed)
+    duration = nseg * 4.0
+    draws = [_draw_rank(rng, duration) for _ in range(ranks)]
+    clear_origins()
+    pinned = device != "cpu"  # the GPU CDN phase copies from pinned host buffers
+    origin = SyntheticHlsOrigin(**origin_kw, pin_memory=pinned)
+    seg_al = (max(max(p.lengths) for p in origin.pools) + 255) // 256 * 256
+    hub = ThreadHub(ranks, timeout=60) if ranks > 1 else None
+    errs: list = []
+    result = {"seed": seed, "ranks": ranks, "duration": duration, "errors": errs,
+              "players": [p for _, _, ps in draws for p in ps], "W": sum(d[0] for d in draws),
+              "cache_segs": [c for _, c, _ in draws], "marks": {}}
+    # the ranks stop together: a collective round needs every rank, so once rank 0 sees every
+    # player done it names a step a few rounds ahead (ranks run at most a round apart)
+    stop = {"step": None}
+    done = [False] * ranks
+    marks_all: list = [{} for _ in range(ranks)]
+    base = [sum(d[0] for d in draws[:r]) for r in range(ranks)]
+
+    def rank_main(r):
+        W, cache_segs, players = draws[r]
         set_current_node(None)
+        loop = new_event_loop("real")
+        comm = hub.comm(r) if hub is not None else LocalComm()
+        node = SwarmNode(comm, device=device, cache_bytes=cache_segs * seg_al, auto_tick=False)
+        set_current_node(node)
+        pairs = [mp.Pipe() for _ in range(W)]
+        threads = []
+        for w, (_, child) in enumerate(pairs):
+            p = players[w]
+            spec = {"origin": dict(origin_kw, pin_memory=pinned),
+                    "hls_config": {"maxFragLoadsInFlight": p["inflight"], "maxBufferLength": 1e9,
+                                   "maxMaxBufferLength": 1e9, "startPosition": 0, "startLevel": 0,
+                                   "tickInterval": 1e9},
+                    "p2p_config": {"streamrootKey": "t", "contentId": f"fleet-chaos-{seed}",
+                                   "gpuSwarm": {"fleetPayload": p["payload"]}},
+                    "world": ranks, "rank": r, "script": p["script"], "read_bytes": p["read"],
+                    "in_process": True}
+
+            def run(c=child, s=spec):
+                try:
+                    player_main(c, s)
+                except BaseException as e:  # noqa: BLE001
+                    errs.append((f"player {r}", e))
+            t = threading.Thread(target=run, daemon=True)
+            t.start()
+            threads.append(t)
+        conns = [parent for parent, _ in pairs]
+        pipe = pipeline_for(torch.device(device), loop)
+        pipe.auto_flush = False
+        server = None
+        try:
+            server = FleetServer(node, pipe, conns)
+            end = time.monotonic() + 30
+            while len(server.ready) < W:
+                server.poll()
+                time.sleep(0.002)
+                if time.monotonic() > end:
+                    raise RuntimeError("players did not start")
+            for c in conns:
+                c.send(("go",))
+            hs, b = collections.deque(), None
+            deadline = time.monotonic() + timeout_s
+            next_mark, tag, step = time.monotonic() + 0.5, 0, 0
+            while True:
+                while loop._ready:
+                    loop.run_once(block=False)
+                server.await_players(timeout_s=0.005)
+                server.poll()
+                server.admit(8)
+                hs.append(node.launch_round())
+                if len(hs) > 1:
+                    node.complete_round(hs.popleft())
+                nb = server.launch_transmux()
+                server.complete_transmux(b)
+                server.send()
+                b = nb
+                step += 1
+                if time.monotonic() > next_mark:  # ask every player where it is
+                    tag += 1
+                    for w, c in enumerate(conns):
+                        if server.open[w]:
+                            c.send(("mark", tag, {"state": True}))
+                    next_mark = time.monotonic() + 0.5
+                marks = {}
+                for t_ in sorted(server.marks):
+                    marks.update(server.marks[t_])
+                marks_all[r] = {base[r] + w: m for w, m in marks.items()}
+                done[r] = len(marks) == W and all(m["t"] >= duration - 4.5 for m in marks.values())
+                if r == 0 and stop["step"] is None and (all(done) or errs or time.monotonic() > deadline):
+                    stop["step"] = step + 4
+                if stop["step"] is not None and step >= stop["step"]:
+                    break
+                if hub is None and (errs or time.monotonic() > deadline):
+                    break
+        except BaseException as e:  # noqa: BLE001
+            errs.append((f"rank {r}", e))
+        finally:
+            result.setdefault("nodes", {})[r] = {"wants": len(node._wt), "parked": len(node._vwait),
+                                                 "pending_verify": node.pending_verify(),
+                                                 "stats": {k: v for k, v in node.stats.items()
+                                                           if isinstance(v, (int, float))}}
+            for c in conns:
+                try:
+                    c.send(("stop",))
+                except (OSError, BrokenPipeError):
+                    pass
+            for t in threads:
+                t.join(10)
+            if server is not None:
+                server.close()
+            node.close()
+            set_current_node(None)
+
+    try:
+        if ranks == 1:
+            rank_main(0)
+        else:
+            ts = [threading.Thread(target=rank_main, args=(r,), daemon=True) for r in range(ranks)]
+            [t.start() for t in ts]
+            [t.join(timeout_s + 90) for t in ts]
+            if any(t.is_alive() for t in ts):
+                errs.append(("scenario", TimeoutError("a rank did not stop")))
+    finally:
+        clear_origins()
+    for m in marks_all:
+        result["marks"].update(m)
     return result
 
 
@@ -151,20 +196,21 @@ def check(res: dict) -> None:
     for w, m in marks.items():
         assert m.get("fatal", 0) == 0 and m.get("byte_errors", 0) == 0, (res["seed"], w, m, res["players"][w])
         assert m["t"] >= res["duration"] - 4.5, (res["seed"], w, "stopped at", m["t"], res["players"][w],
-                                                 res["cache_segs"])
+                                                 res["cache_segs"], m.get("state"), res.get("nodes"))
 
 
 if __name__ == "__main__":
     device = "cuda:0" if "--gpu" in sys.argv else "cpu"
+    nranks = next((int(a.split("=", 1)[1]) for a in sys.argv if a.startswith("--ranks=")), 1)
     argv = [a for a in sys.argv[1:] if not a.startswith("--")]
     lo, hi = (int(argv[0]), int(argv[1])) if len(argv) > 1 else (0, 20)
     bad = []
     for s in range(lo, hi):
-        res = scenario(s, device=device)
+        res = scenario(s, device=device, ranks=nranks)
         try:
             check(res)
             ends = sorted(round(m["t"], 1) for m in res["marks"].values())
-            print(f"seed {s}: ok ({res['W']} players, t {ends})", flush=True)
+            print(f"seed {s}: ok ({res['ranks']} ranks, {res['W']} players, t {ends})", flush=True)
         except AssertionError as e:
             print(f"seed {s}: FAIL {str(e)[:400]}", flush=True)
             bad.append(s)

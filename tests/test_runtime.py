@@ -25,6 +25,23 @@ def test_store_reserve_commit_lookup_delta(rt):
     assert len(add) == 0 and rm[:, 3].tolist() == [1]
 
 
+def test_store_commit_of_a_replaced_copy_is_not_announced(rt):
+    """A received copy awaiting its deferred check (pending, pinned by its readers) is replaced
+    in the index when the key is fetched again.  Its check passing later commits it for those
+    readers only: announcing it would tell peers this rank holds a key its index maps to a
+    copy still in flight (fleet chaos, 3 ranks)."""
+    st = rt.SegmentStore(1 << 20, 256)
+    _, old, _ = st.reserve_run(keys(1), np.array([1000]), 0)
+    st.pin(old)
+    _, new, _ = st.reserve_run(keys(1), np.array([1000]), 1)
+    st.commit(old)
+    add, _ = st.take_delta()
+    assert len(add) == 0
+    st.commit(new)
+    add, _ = st.take_delta()
+    assert add[:, 3].tolist() == [1]
+
+
 def test_store_detach_keeps_pinned_bytes_until_the_ring_reaches_them(rt):
     """A received copy that failed its deferred CRC check is detached: no longer found (nor
     announced: it was never committed), its id stays valid while readers hold pins, the key

@@ -202,6 +202,48 @@ def test_a_late_ticket_report_after_the_sweep_is_ignored():
     assert node.pending_verify() == 0
 
 
+class _ColSink:
+    def __init__(self):
+        self.got = []
+
+    def deliver(self, tok, src, *a, **k):
+        self.got.extend(zip(np.asarray(tok).tolist(), np.asarray(src).tolist()))
+
+    def fail(self, *a):
+        pass
+
+
+@pytest.mark.parametrize("passes", [True, False])
+def test_a_request_for_a_copy_awaiting_its_check_waits_for_the_check(passes):
+    """A fleet request for a segment whose received copy was delivered and awaits its deferred
+    check waits for that check instead of fetching the segment again (the second fetch
+    replaced the copy in the index while the first players still read it; their on-demand
+    bytes came back empty): answered from the copy when it passes, from the CDN when not."""
+    from hlsjs_p2p_wrapper_amd.agent.node import SRC_CACHE, SwarmNode
+
+    loop = new_event_loop("virtual")
+    node = SwarmNode(device="cpu", cache_bytes=1 << 20, loop=loop, auto_tick=False)
+    sink = _ColSink()
+    node.set_bulk_sink(sink)
+    node.verify_deferred = True
+    key = np.array([[3, 0, 0, 1]], dtype=np.int64)
+    _, eids, _ = node.store.reserve_run(key, np.array([3000]), 1)
+    node.store.pin(eids)
+    info = np.zeros((1, 10), dtype=np.int64)
+    info[0, :4] = key[0]
+    info[0, 4] = 3000
+    node._vpend_add(eids, info, np.array([0], dtype=np.int64))
+    node.request_batch(key, ["http://cdn.test/vod/x.ts"], None, np.array([42], dtype=np.int64))
+    assert node.stats["parked"] == 1 and len(node._wt) == 0
+    node.verify_done(eids, np.array([passes]), np.array([7], dtype=np.int64))
+    loop.run_until(lambda: False, timeout_ms=10)
+    if passes:
+        assert (42, SRC_CACHE) in sink.got and len(node._wt) == 0
+    else:
+        assert not any(t == 42 for t, _ in sink.got) and len(node._wt) == 1  # asked again, from the CDN
+    assert not node._vwait
+
+
 def torch_from(a):
     import torch
 
