@@ -8,7 +8,8 @@ answered from its peers' caches too.  A scenario passes when every player plays 
 the VOD with no fatal error, no failed byte read and no exception on any side.
 
 Used by ``tests/test_fleet_chaos.py`` (fixed seeds) and runnable directly for a sweep:
-``python tests/fleet_chaos.py 0 100`` (``--gpu``: the nodes on ``cuda:0``; ``--ranks=N``).
+``python tests/fleet_chaos.py 0 100`` (``--gpu``: the nodes on ``cuda:0``; ``--ranks=N``;
+``--faults``: corrupted receives and offline periods).
 """
 from __future__ import annotations
 
@@ -48,10 +49,12 @@ def _draw_rank(rng, duration):
     return W, cache_segs, players
 
 
-def scenario(seed: int, timeout_s: float = 120.0, device: str = "cpu", ranks: int = 1) -> dict:
+def scenario(seed: int, timeout_s: float = 120.0, device: str = "cpu", ranks: int = 1, faults: bool = False) -> dict:
     """``device``: where the nodes' segment caches and the transmux live (``cuda:0``: the HBM
     ring, the GPU transmux and the on-demand bytes copied back from the device).  ``ranks``:
-    rank 0 draws what the single-rank scenario of the seed draws; later ranks draw after it."""
+    rank 0 draws what the single-rank scenario of the seed draws; later ranks draw after it.
+    ``faults`` (ranks > 1): each rank also corrupts received rounds and goes offline for a
+    while at random times (drawn from a second generator: the base scenario does not change)."""
     rng = np.random.default_rng(seed)
     nseg = int(rng.integers(10, 24))
     ladder = rng.random() < 0.4
@@ -61,13 +64,18 @@ def scenario(seed: int, timeout_s: float = 120.0, device: str = "cpu", ranks: in
                      segment_duration=4.0, encrypted=bool(rng.random() < 0.7), pool_size=min(nseg, 8), seed=seed)
     duration = nseg * 4.0
     draws = [_draw_rank(rng, duration) for _ in range(ranks)]
+    frng = np.random.default_rng(seed + 5_000_011)
+    faults_at = [sorted((float(frng.uniform(0.2, 3.0)), str(frng.choice(["corrupt", "offline"])),
+                         int(frng.integers(1, 4)), float(frng.uniform(0.1, 1.0)))
+                        for _ in range(int(frng.integers(1, 4)))) if faults and ranks > 1 else []
+                 for _ in range(ranks)]
     clear_origins()
     pinned = device != "cpu"  # the GPU CDN phase copies from pinned host buffers
     origin = SyntheticHlsOrigin(**origin_kw, pin_memory=pinned)
     seg_al = (max(max(p.lengths) for p in origin.pools) + 255) // 256 * 256
     hub = ThreadHub(ranks, timeout=60) if ranks > 1 else None
     errs: list = []
-    result = {"seed": seed, "ranks": ranks, "duration": duration, "errors": errs,
+    result = {"seed": seed, "ranks": ranks, "duration": duration, "errors": errs, "faults": faults_at,
               "players": [p for _, _, ps in draws for p in ps], "W": sum(d[0] for d in draws),
               "cache_segs": [c for _, c, _ in draws], "marks": {}}
     # the ranks stop together: a collective round needs every rank, so once rank 0 sees every
@@ -122,7 +130,19 @@ def scenario(seed: int, timeout_s: float = 120.0, device: str = "cpu", ranks: in
             hs, b = collections.deque(), None
             deadline = time.monotonic() + timeout_s
             next_mark, tag, step = time.monotonic() + 0.5, 0, 0
+            t0, todo, back_online = time.monotonic(), list(faults_at[r]), None
             while True:
+                now = time.monotonic() - t0
+                while todo and todo[0][0] <= now:  # (at s, kind, rounds to corrupt, offline s)
+                    _, kind, k, off_s = todo.pop(0)
+                    if kind == "corrupt":
+                        node.corrupt_next_recv += k
+                    elif back_online is None:
+                        node.set_online(False)
+                        back_online = now + off_s
+                if back_online is not None and now >= back_online:
+                    node.set_online(True)
+                    back_online = None
                 while loop._ready:
                     loop.run_once(block=False)
                 server.await_players(timeout_s=0.005)
@@ -202,15 +222,19 @@ def check(res: dict) -> None:
 if __name__ == "__main__":
     device = "cuda:0" if "--gpu" in sys.argv else "cpu"
     nranks = next((int(a.split("=", 1)[1]) for a in sys.argv if a.startswith("--ranks=")), 1)
+    faults = "--faults" in sys.argv
     argv = [a for a in sys.argv[1:] if not a.startswith("--")]
     lo, hi = (int(argv[0]), int(argv[1])) if len(argv) > 1 else (0, 20)
     bad = []
     for s in range(lo, hi):
-        res = scenario(s, device=device, ranks=nranks)
+        res = scenario(s, device=device, ranks=nranks, faults=faults)
         try:
             check(res)
             ends = sorted(round(m["t"], 1) for m in res["marks"].values())
-            print(f"seed {s}: ok ({res['ranks']} ranks, {res['W']} players, t {ends})", flush=True)
+            st = [n["stats"] for n in res.get("nodes", {}).values()]
+            crc, parked = sum(x.get("crc_failures", 0) for x in st), sum(x.get("parked", 0) for x in st)
+            print(f"seed {s}: ok ({res['ranks']} ranks, {res['W']} players, t {ends}, crc failures {crc}, "
+                  f"parked {parked})", flush=True)
         except AssertionError as e:
             print(f"seed {s}: FAIL {str(e)[:400]}", flush=True)
             bad.append(s)

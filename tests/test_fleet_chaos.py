@@ -24,6 +24,15 @@ def test_fleet_chaos_seed(seed, ranks):
     fleet_chaos.check(fleet_chaos.scenario(seed, ranks=ranks))
 
 
+@pytest.mark.parametrize("seed", [3, 15])
+def test_fleet_chaos_with_faults(seed):
+    """Three ranks that corrupt received rounds and go offline at random times (the two seeds
+    hit CRC failures with requests parked on copies awaiting their check)."""
+    res = fleet_chaos.scenario(seed, ranks=3, faults=True)
+    fleet_chaos.check(res)
+    assert any(f for f in res["faults"])
+
+
 @pytest.mark.gpu
 @pytest.mark.parametrize("seed,ranks", [(4, 1), (5, 1), (11, 1), (4, 2), (32, 2)])
 def test_fleet_chaos_seed_gpu(seed, ranks):
