@@ -1175,6 +1175,8 @@ def _script_action(hls: Any, media: Any, loop: Any, action: str, arg: Any) -> No
     """One scripted player action (``player_main`` ``spec["script"]``)."""
     if action == "seek":
         media.currentTime = float(arg)
+    elif action == "seek_rel":  # (live: back into the DVR window)
+        media.currentTime = max(0.0, media.currentTime + float(arg))
     elif action == "pause":
         media.pause()
         loop.set_timeout(media.play, float(arg))
@@ -1319,6 +1321,15 @@ def player_main(conn: Any, spec: Dict[str, Any]) -> None:
                                         "seeking": media.seeking, "stream": sc.state, "level": hls.currentLevel,
                                         "inflight": sorted(sc.inflight), "pending": len(node._pending),
                                         "node_inflight": node.inflight}
+                        lc = hls.levelController
+                        lv = hls.levels[lc.level] if hls.levels and 0 <= lc.level < len(hls.levels) else None
+                        det = lv.details if lv is not None else None
+                        if det is not None and det.fragments:
+                            out["state"].update(last_sn=det.fragments[-1].sn, last_end=det.fragments[-1].end,
+                                                reload_timer=lc._reload_timer is not None,
+                                                playlist_loaders=sorted(hls.playlistLoader.loaders))
+                            if origin.live:
+                                out["state"]["edge_sn"] = origin.live_edge()
                     if live_lat:  # live latency behind the edge since the previous mark
                         out["live_latency_s"] = live_lat[:]
                         live_lat.clear()

@@ -114,6 +114,18 @@ class PlaylistLoader:
 
 
 # ---------------------------------------------------------------------------- levels
+def _sn_delta(ref: List[Fragment], frags: List[Fragment], targetduration: Optional[float]) -> float:
+    """Shift that puts ``frags`` on the timeline of ``ref`` (playlists of one live stream):
+    through the first sn both hold, else by the sn distance from ``ref``'s last fragment."""
+    by_sn = {f.sn: f for f in ref}
+    for f in frags:
+        o = by_sn.get(f.sn)
+        if o is not None:
+            return o.start - f.start
+    gap = frags[0].sn - ref[-1].sn - 1
+    return ref[-1].end + gap * (targetduration or 0) - frags[0].start
+
+
 class LevelController:
     def __init__(self, hls) -> None:
         self.hls = hls
@@ -192,20 +204,23 @@ class LevelController:
         lvl = levels[idx]
         details: LevelDetails = data["details"]
         old = lvl.details
+        if (old is None or not old.fragments) and details.live and details.fragments:
+            # a live level's first playlist starts its own timeline at 0: put it on the timeline
+            # playback is on, through the sn the levels share (hls.js alignStream / adjustSliding),
+            # or a switch lands the playhead segments away from the fragments it needs
+            ref = self._timeline_ref(idx)
+            if ref is not None:
+                delta = _sn_delta(ref.fragments, details.fragments, details.targetduration)
+                if delta:
+                    for f in details.fragments:
+                        f.start += delta
+                    details.totalduration = details.fragments[-1].end
         if old is not None and old.fragments and details.fragments:
             # live reload: a refreshed playlist restarts its timeline at 0; align it on the
             # previous one through a common sn (hls.js mergeDetails) and keep Fragment
             # identity for sn present in both (in-flight loads refer to them)
             by_sn = {f.sn: f for f in old.fragments}
-            delta = None
-            for f in details.fragments:
-                o = by_sn.get(f.sn)
-                if o is not None:
-                    delta = o.start - f.start
-                    break
-            if delta is None:  # no overlap: continue after the old playlist's end
-                gap = details.fragments[0].sn - old.fragments[-1].sn - 1
-                delta = old.fragments[-1].end + gap * (details.targetduration or 0) - details.fragments[0].start
+            delta = _sn_delta(old.fragments, details.fragments, details.targetduration)
             merged = []
             for f in details.fragments:
                 o = by_sn.get(f.sn)
@@ -222,6 +237,16 @@ class LevelController:
         if details.live and idx == self._level:
             interval = 1000.0 * (details.averagetargetduration or details.targetduration or 1.0)
             self._reload_timer = self.hls.loop.set_timeout(self._reload, interval, idx)
+
+    def _timeline_ref(self, idx: int) -> Optional["LevelDetails"]:
+        """Details of another level already on the playback timeline (the current one first)."""
+        order = [self._level] + [i for i in range(len(self._levels or ())) if i != self._level]
+        for i in order:
+            if i != idx and 0 <= i < len(self._levels or ()):
+                d = self._levels[i].details  # type: ignore[index]
+                if d is not None and d.fragments:
+                    return d
+        return None
 
     def _reload(self, idx: int) -> None:
         self._reload_timer = None
@@ -547,6 +572,22 @@ class StreamController:
         start = details.fragments[0].start if details.fragments else 0.0
         return max(start, details.totalduration - back)
 
+    def _ensure_in_live_window(self, media: Any, cfg: Any, details: LevelDetails) -> None:
+        """A live playhead whose buffer ends before the sliding window's first fragment (a
+        seek back past the DVR window, a long pause) can never be fed: reset it to the live
+        sync position (hls.js stream-controller ``_ensureFragmentAtLivePoint``)."""
+        first = details.fragments[0].start - float(cfg.get("maxFragLookUpTolerance", 0.2))
+        pos = media.currentTime
+        if pos >= first:
+            return
+        hole = cfg.maxBufferHole
+        for s, e in media.buffered:
+            if s - hole <= pos < e:
+                pos = e
+                break
+        if pos < first:
+            media.currentTime = self._live_start(details)
+
     def tick(self) -> None:
         hls = self.hls
         if self.state in (self.STOPPED, self.ERROR):
@@ -576,6 +617,8 @@ class StreamController:
             if abs(media.currentTime - pos0) > 1e-9:
                 media.currentTime = pos0
         cfg = hls.config
+        if details.live and details.fragments:
+            self._ensure_in_live_window(media, cfg, details)
         ranges = list(media.buffered)  # one walk of the buffered ranges per tick
         if ranges and (media.seeking or not media.paused):
             self._seek_over_hole(media, cfg, ranges)

@@ -9,7 +9,7 @@ the VOD with no fatal error, no failed byte read and no exception on any side.
 
 Used by ``tests/test_fleet_chaos.py`` (fixed seeds) and runnable directly for a sweep:
 ``python tests/fleet_chaos.py 0 100`` (``--gpu``: the nodes on ``cuda:0``; ``--ranks=N``;
-``--faults``: corrupted receives and offline periods).
+``--faults``: corrupted receives and offline periods; ``--live``: a live channel).
 """
 from __future__ import annotations
 
@@ -31,6 +31,10 @@ from hlsjs_p2p_wrapper_amd.parallel.fleet import FleetServer, player_main
 from hlsjs_p2p_wrapper_amd.player.transmux import pipeline_for
 
 
+LIVE_SPEED = 20.0  # live scenarios: media seconds per wall second
+LIVE_WALL_S = 6.0  # ... and their wall time
+
+
 def _draw_rank(rng, duration):
     """One rank's draws: its player count, its cache (in segments) and its players."""
     W = int(rng.integers(2, 4))
@@ -49,12 +53,18 @@ def _draw_rank(rng, duration):
     return W, cache_segs, players
 
 
-def scenario(seed: int, timeout_s: float = 120.0, device: str = "cpu", ranks: int = 1, faults: bool = False) -> dict:
+def scenario(seed: int, timeout_s: float = 120.0, device: str = "cpu", ranks: int = 1, faults: bool = False,
+             live: bool = False) -> dict:
     """``device``: where the nodes' segment caches and the transmux live (``cuda:0``: the HBM
     ring, the GPU transmux and the on-demand bytes copied back from the device).  ``ranks``:
     rank 0 draws what the single-rank scenario of the seed draws; later ranks draw after it.
     ``faults`` (ranks > 1): each rank also corrupts received rounds and goes offline for a
-    while at random times (drawn from a second generator: the base scenario does not change)."""
+    while at random times (drawn from a second generator: the base scenario does not change).
+    ``live``: the channel is live (a sliding window of 6-15 segments published 20x faster than
+    real time, players at the live sync point on the channel's clock, live-window eviction on
+    the nodes); the scripts' times and pauses are scaled to the channel's clock and their seeks
+    go back into the window.  A live scenario runs ``LIVE_WALL_S`` and passes when every player
+    is still playing at the end (its media clock advanced over the last second)."""
     rng = np.random.default_rng(seed)
     nseg = int(rng.integers(10, 24))
     ladder = rng.random() < 0.4
@@ -64,6 +74,16 @@ def scenario(seed: int, timeout_s: float = 120.0, device: str = "cpu", ranks: in
                      segment_duration=4.0, encrypted=bool(rng.random() < 0.7), pool_size=min(nseg, 8), seed=seed)
     duration = nseg * 4.0
     draws = [_draw_rank(rng, duration) for _ in range(ranks)]
+    speed = LIVE_SPEED
+    if live:
+        lrng = np.random.default_rng(seed + 9_000_017)
+        window = int(lrng.integers(6, 16))
+        origin_kw.update(live=True, window=window, num_segments=None, live_speed=speed, pool_size=8)
+        for _, _, ps in draws:  # the scripts on the channel's clock (player loop ms = media ms)
+            for p in ps:
+                p["script"] = [(t * speed, "seek_rel", -float(a % (window * 4.0 * 0.6))) if k == "seek" else
+                               (t * speed, k, a * speed if k in ("pause", "restart") else a)
+                               for t, k, a in p["script"]]
     frng = np.random.default_rng(seed + 5_000_011)
     faults_at = [sorted((float(frng.uniform(0.2, 3.0)), str(frng.choice(["corrupt", "offline"])),
                          int(frng.integers(1, 4)), float(frng.uniform(0.1, 1.0)))
@@ -84,6 +104,12 @@ def scenario(seed: int, timeout_s: float = 120.0, device: str = "cpu", ranks: in
     done = [False] * ranks
     marks_all: list = [{} for _ in range(ranks)]
     base = [sum(d[0] for d in draws[:r]) for r in range(ranks)]
+    epoch = time.time() + 0.5  # live: the channel's clock, shared by the nodes and players
+    if live:
+        origin.live_epoch = epoch
+    trail = collections.defaultdict(dict)  # live: player -> {mark tag: media t}
+    result["live"] = live
+    result["trail"] = trail
 
     def rank_main(r):
         W, cache_segs, players = draws[r]
@@ -96,14 +122,17 @@ def scenario(seed: int, timeout_s: float = 120.0, device: str = "cpu", ranks: in
         threads = []
         for w, (_, child) in enumerate(pairs):
             p = players[w]
-            spec = {"origin": dict(origin_kw, pin_memory=pinned),
-                    "hls_config": {"maxFragLoadsInFlight": p["inflight"], "maxBufferLength": 1e9,
-                                   "maxMaxBufferLength": 1e9, "startPosition": 0, "startLevel": 0,
-                                   "tickInterval": 1e9},
+            hcfg = ({"maxFragLoadsInFlight": p["inflight"], "fragLoadingTimeOut": 60_000, "startLevel": 0}
+                    if live else
+                    {"maxFragLoadsInFlight": p["inflight"], "maxBufferLength": 1e9, "maxMaxBufferLength": 1e9,
+                     "startPosition": 0, "startLevel": 0, "tickInterval": 1e9})
+            spec = {"origin": dict(origin_kw, pin_memory=pinned), "hls_config": hcfg,
                     "p2p_config": {"streamrootKey": "t", "contentId": f"fleet-chaos-{seed}",
                                    "gpuSwarm": {"fleetPayload": p["payload"]}},
                     "world": ranks, "rank": r, "script": p["script"], "read_bytes": p["read"],
                     "in_process": True}
+            if live:
+                spec.update(clock_speed=speed, media_mode="realtime")
 
             def run(c=child, s=spec):
                 try:
@@ -126,10 +155,11 @@ def scenario(seed: int, timeout_s: float = 120.0, device: str = "cpu", ranks: in
                 if time.monotonic() > end:
                     raise RuntimeError("players did not start")
             for c in conns:
-                c.send(("go",))
+                c.send(("go", {"live_epoch": epoch} if live else {}))
             hs, b = collections.deque(), None
             deadline = time.monotonic() + timeout_s
             next_mark, tag, step = time.monotonic() + 0.5, 0, 0
+            live_end = time.monotonic() + LIVE_WALL_S
             t0, todo, back_online = time.monotonic(), list(faults_at[r]), None
             while True:
                 now = time.monotonic() - t0
@@ -166,7 +196,13 @@ def scenario(seed: int, timeout_s: float = 120.0, device: str = "cpu", ranks: in
                 for t_ in sorted(server.marks):
                     marks.update(server.marks[t_])
                 marks_all[r] = {base[r] + w: m for w, m in marks.items()}
-                done[r] = len(marks) == W and all(m["t"] >= duration - 4.5 for m in marks.values())
+                if live:  # every mark's t per player, for the end check
+                    for t_ in sorted(server.marks)[-3:]:
+                        for w, m in server.marks[t_].items():
+                            trail[base[r] + w][t_] = m["t"]
+                    done[r] = time.monotonic() > live_end
+                else:
+                    done[r] = len(marks) == W and all(m["t"] >= duration - 4.5 for m in marks.values())
                 if r == 0 and stop["step"] is None and (all(done) or errs or time.monotonic() > deadline):
                     stop["step"] = step + 4
                 if stop["step"] is not None and step >= stop["step"]:
@@ -177,6 +213,7 @@ def scenario(seed: int, timeout_s: float = 120.0, device: str = "cpu", ranks: in
             errs.append((f"rank {r}", e))
         finally:
             result.setdefault("nodes", {})[r] = {"wants": len(node._wt), "parked": len(node._vwait),
+                                                 "evicted": server.evicted if server is not None else 0,
                                                  "pending_verify": node.pending_verify(),
                                                  "stats": {k: v for k, v in node.stats.items()
                                                            if isinstance(v, (int, float))}}
@@ -215,6 +252,11 @@ def check(res: dict) -> None:
     assert len(marks) == res["W"], (res["seed"], "not every player reported", marks)
     for w, m in marks.items():
         assert m.get("fatal", 0) == 0 and m.get("byte_errors", 0) == 0, (res["seed"], w, m, res["players"][w])
+        if res["live"]:  # still playing: its clock advanced over the last two marks (1 s of wall)
+            ts = [t for _, t in sorted(res["trail"][w].items())][-3:]
+            assert len(ts) == 3 and ts[-1] - ts[0] >= 0.25 * LIVE_SPEED, (res["seed"], w, "stalled", ts, m,
+                                                                           res["players"][w])
+            continue
         assert m["t"] >= res["duration"] - 4.5, (res["seed"], w, "stopped at", m["t"], res["players"][w],
                                                  res["cache_segs"], m.get("state"), res.get("nodes"))
 
@@ -223,18 +265,20 @@ if __name__ == "__main__":
     device = "cuda:0" if "--gpu" in sys.argv else "cpu"
     nranks = next((int(a.split("=", 1)[1]) for a in sys.argv if a.startswith("--ranks=")), 1)
     faults = "--faults" in sys.argv
+    live = "--live" in sys.argv
     argv = [a for a in sys.argv[1:] if not a.startswith("--")]
     lo, hi = (int(argv[0]), int(argv[1])) if len(argv) > 1 else (0, 20)
     bad = []
     for s in range(lo, hi):
-        res = scenario(s, device=device, ranks=nranks, faults=faults)
+        res = scenario(s, device=device, ranks=nranks, faults=faults, live=live)
         try:
             check(res)
             ends = sorted(round(m["t"], 1) for m in res["marks"].values())
             st = [n["stats"] for n in res.get("nodes", {}).values()]
             crc, parked = sum(x.get("crc_failures", 0) for x in st), sum(x.get("parked", 0) for x in st)
+            ev = sum(n.get("evicted", 0) for n in res.get("nodes", {}).values())
             print(f"seed {s}: ok ({res['ranks']} ranks, {res['W']} players, t {ends}, crc failures {crc}, "
-                  f"parked {parked})", flush=True)
+                  f"parked {parked}, evicted {ev})", flush=True)
         except AssertionError as e:
             print(f"seed {s}: FAIL {str(e)[:400]}", flush=True)
             bad.append(s)

@@ -13,7 +13,9 @@ byte read-back and scripted seeks / pauses / level switches / restarts.
   nothing.  The request now waits for the check (``SwarmNode._park_on_pending``), and a fetch
   reads the exact copy the player was answered with while its batch holds it.
 * Seed 8 (three ranks) stalled a player once on a fragment never answered, not reproduced
-  since (kept)."""
+  since (kept).
+* Live (``live=True``): a switched-to level's first playlist off the playback timeline and a
+  seek behind the sliding window stalled players (see ``test_fleet_chaos_live``)."""
 import pytest
 
 import fleet_chaos
@@ -33,9 +35,18 @@ def test_fleet_chaos_with_faults(seed):
     assert any(f for f in res["faults"])
 
 
+@pytest.mark.parametrize("seed,ranks", [(10, 1), (3, 2), (8, 2), (18, 2)])
+def test_fleet_chaos_live(seed, ranks):
+    """A live channel (sliding window, live-window eviction, seeks back into the window).  Seed 10
+    stalled on a switched-to level's unaligned first playlist, seeds 8 and 18 on a seek behind
+    the window (two ranks, with faults)."""
+    fleet_chaos.check(fleet_chaos.scenario(seed, ranks=ranks, faults=ranks > 1, live=True))
+
+
 @pytest.mark.gpu
-@pytest.mark.parametrize("seed,ranks", [(4, 1), (5, 1), (11, 1), (4, 2), (32, 2)])
-def test_fleet_chaos_seed_gpu(seed, ranks):
+@pytest.mark.parametrize("seed,ranks,live", [(4, 1, False), (5, 1, False), (11, 1, False), (4, 2, False),
+                                             (32, 2, False), (3, 2, True)])
+def test_fleet_chaos_seed_gpu(seed, ranks, live):
     """The nodes' caches are HBM rings and the transmux runs on the GPU: the on-demand bytes a
     player reads back come off the device (two ranks: both on the one GPU)."""
-    fleet_chaos.check(fleet_chaos.scenario(seed, device="cuda:0", ranks=ranks))
+    fleet_chaos.check(fleet_chaos.scenario(seed, device="cuda:0", ranks=ranks, live=live))

@@ -644,3 +644,63 @@ def test_node_reports_a_saturated_ingest_link_to_the_planner(monkeypatch):
     node._cdn_busy = 0.95
     node.cdn_balance = False
     assert not node.flags & bound
+
+
+def test_live_level_switch_lands_on_the_playback_timeline():
+    """A live level's first playlist starts its own timeline at 0.  Loaded for the first time
+    after the window slid (a level switch), it must be put on the timeline playback is on
+    through the sn the levels share (hls.js alignStream): unaligned, the switched-to level's
+    fragments sat 8 segments early and the player stalled at its buffer end waiting for them
+    (tests/fleet_chaos.py --live, seed 10)."""
+    from hlsjs_p2p_wrapper_amd.agent import SwarmNode
+
+    set_current_node(None)
+    loop = new_event_loop("virtual")
+    origin = SyntheticHlsOrigin("http://cdn.test/lsw/", renditions=[Rendition(400_000, 320, 180),
+                                                                    Rendition(800_000, 640, 360)],
+                                live=True, window=5, num_segments=None, pool_size=8, encrypted=True, loop=loop)
+    node = SwarmNode(device="cpu", cache_bytes=256 << 20, loop=loop)
+    set_current_node(node)
+    w = HlsjsP2PWrapper(Engine)
+    hls = w.createPlayer({"liveSyncDurationCount": 2, "startLevel": 0}, {})
+    media = MediaElement()
+    hls.loadSource(origin.master_url())
+    hls.attachMedia(media)
+    hls.on(Hls.Events.MANIFEST_PARSED, lambda e, d: media.play())
+    hls.currentLevel = 0
+    assert loop.run_until(lambda: media.currentTime > 40.0, timeout_ms=400_000)
+    assert hls.levels[1].details is None  # never loaded: its first playlist comes after the slide
+    hls.currentLevel = 1
+    t = media.currentTime
+    assert loop.run_until(lambda: media.currentTime > t + 40.0, timeout_ms=400_000), media.currentTime
+    off = {lv: {round(f.start - 4.0 * f.sn, 6) for f in hls.levels[lv].details.fragments} for lv in (0, 1)}
+    assert off[0] == off[1] and len(off[0]) == 1
+    hls.destroy()
+    set_current_node(None)
+
+
+def test_live_seek_behind_the_window_resets_to_the_live_sync_point():
+    """A live playhead seeked back past the sliding window (or paused until the window left
+    it) cannot be fed: it is reset to the live sync position, as hls.js does; before, it sat
+    seeking forever in front of the buffered window (tests/fleet_chaos.py --live, seeds 8, 18)."""
+    from hlsjs_p2p_wrapper_amd.agent import SwarmNode
+
+    set_current_node(None)
+    loop = new_event_loop("virtual")
+    origin = SyntheticHlsOrigin("http://cdn.test/lsk/", renditions=[Rendition(400_000, 320, 180)],
+                                live=True, window=5, num_segments=None, pool_size=8, encrypted=True, loop=loop)
+    node = SwarmNode(device="cpu", cache_bytes=256 << 20, loop=loop)
+    set_current_node(node)
+    w = HlsjsP2PWrapper(Engine)
+    hls = w.createPlayer({"liveSyncDurationCount": 2}, {})
+    media = MediaElement()
+    hls.loadSource(origin.master_url())
+    hls.attachMedia(media)
+    hls.on(Hls.Events.MANIFEST_PARSED, lambda e, d: media.play())
+    assert loop.run_until(lambda: media.currentTime > 60.0, timeout_ms=400_000)
+    first = hls.levels[0].details.fragments[0].start
+    assert first > 10.0
+    media.currentTime = 1.0  # behind the window
+    assert loop.run_until(lambda: media.currentTime > first + 30.0, timeout_ms=400_000), media.currentTime
+    hls.destroy()
+    set_current_node(None)
