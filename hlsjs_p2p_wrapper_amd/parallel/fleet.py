@@ -1022,13 +1022,14 @@ class FleetServer:
 
     def _new_ring(self, total: int) -> _PayloadRing:
         """A (bigger) payload ring; the current one is retired, kept until every region on it
-        is acknowledged.  Size: ``HLSP2P_FLEET_PAYLOAD_BYTES`` for the first ring, else room
+        is acknowledged.  Size: ``HLSP2P_FLEET_PAYLOAD_BYTES`` for the first ring (at least this
+        batch), else room
         for 4 batches of this size (>= 256 MiB, doubling on growth), capped to half of the
         free /dev/shm, and never below 2 batches."""
         old = self._ring
         env = os.environ.get("HLSP2P_FLEET_PAYLOAD_BYTES")
         if old is None and env:
-            size = int(env)
+            size = max(int(env), total)  # (never below the batch asking for it)
         else:
             size = max(self.RING_MIN, 4 * total, 2 * old.cap if old is not None else 0)
             size = (size + (1 << 20) - 1) // (1 << 20) * (1 << 20)
@@ -1069,6 +1070,9 @@ class FleetServer:
             got = ring.try_place(total)
             if got is not None:
                 return ring, got
+            if not ring.live:  # empty and still too small for this batch
+                ring = self._new_ring(total)
+                continue
             need = ring.live[0][2]
             if need is None or not self._wait_acks(need):
                 if need is not None:

@@ -9,12 +9,14 @@ the VOD with no fatal error, no failed byte read and no exception on any side.
 
 Used by ``tests/test_fleet_chaos.py`` (fixed seeds) and runnable directly for a sweep:
 ``python tests/fleet_chaos.py 0 100`` (``--gpu``: the nodes on ``cuda:0``; ``--ranks=N``;
-``--faults``: corrupted receives and offline periods; ``--live``: a live channel).
+``--faults``: corrupted receives and offline periods; ``--live``: a live channel; ``--ring``:
+payloads through a small, growing payload ring).
 """
 from __future__ import annotations
 
 import collections
 import multiprocessing as mp
+import os
 import sys
 import threading
 import time
@@ -54,7 +56,7 @@ def _draw_rank(rng, duration):
 
 
 def scenario(seed: int, timeout_s: float = 120.0, device: str = "cpu", ranks: int = 1, faults: bool = False,
-             live: bool = False) -> dict:
+             live: bool = False, ring: bool = False) -> dict:
     """``device``: where the nodes' segment caches and the transmux live (``cuda:0``: the HBM
     ring, the GPU transmux and the on-demand bytes copied back from the device).  ``ranks``:
     rank 0 draws what the single-rank scenario of the seed draws; later ranks draw after it.
@@ -64,7 +66,10 @@ def scenario(seed: int, timeout_s: float = 120.0, device: str = "cpu", ranks: in
     real time, players at the live sync point on the channel's clock, live-window eviction on
     the nodes); the scripts' times and pauses are scaled to the channel's clock and their seeks
     go back into the window.  A live scenario runs ``LIVE_WALL_S`` and passes when every player
-    is still playing at the end (its media clock advanced over the last second)."""
+    is still playing at the end (its media clock advanced over the last second).
+    ``ring``: every player takes payloads, through a payload ring that starts at 1 MiB and
+    grows by at least 1 MiB (``FleetServer._new_ring``): the ring fills, grows and retires
+    rings whose regions players still hold, all through the scenario."""
     rng = np.random.default_rng(seed)
     nseg = int(rng.integers(10, 24))
     ladder = rng.random() < 0.4
@@ -74,6 +79,10 @@ def scenario(seed: int, timeout_s: float = 120.0, device: str = "cpu", ranks: in
                      segment_duration=4.0, encrypted=bool(rng.random() < 0.7), pool_size=min(nseg, 8), seed=seed)
     duration = nseg * 4.0
     draws = [_draw_rank(rng, duration) for _ in range(ranks)]
+    if ring:
+        for _, _, ps in draws:
+            for p in ps:
+                p["payload"] = True
     speed = LIVE_SPEED
     if live:
         lrng = np.random.default_rng(seed + 9_000_017)
@@ -148,6 +157,9 @@ def scenario(seed: int, timeout_s: float = 120.0, device: str = "cpu", ranks: in
         server = None
         try:
             server = FleetServer(node, pipe, conns)
+            if ring:
+                server.RING_MIN = 1 << 20
+                server.ring_ack_timeout_s = 0.5  # a player behind by half a second loses its payloads
             end = time.monotonic() + 30
             while len(server.ready) < W:
                 server.poll()
@@ -214,6 +226,9 @@ def scenario(seed: int, timeout_s: float = 120.0, device: str = "cpu", ranks: in
         finally:
             result.setdefault("nodes", {})[r] = {"wants": len(node._wt), "parked": len(node._vwait),
                                                  "evicted": server.evicted if server is not None else 0,
+                                                 "ring_cap": server._ring.cap if server is not None and
+                                                 server._ring is not None else 0,
+                                                 "revoked": len(server.revoked) if server is not None else 0,
                                                  "pending_verify": node.pending_verify(),
                                                  "stats": {k: v for k, v in node.stats.items()
                                                            if isinstance(v, (int, float))}}
@@ -229,6 +244,9 @@ def scenario(seed: int, timeout_s: float = 120.0, device: str = "cpu", ranks: in
             node.close()
             set_current_node(None)
 
+    saved_ring = os.environ.get("HLSP2P_FLEET_PAYLOAD_BYTES")
+    if ring:
+        os.environ["HLSP2P_FLEET_PAYLOAD_BYTES"] = str(1 << 20)
     try:
         if ranks == 1:
             rank_main(0)
@@ -240,6 +258,11 @@ def scenario(seed: int, timeout_s: float = 120.0, device: str = "cpu", ranks: in
                 errs.append(("scenario", TimeoutError("a rank did not stop")))
     finally:
         clear_origins()
+        if ring:
+            if saved_ring is None:
+                os.environ.pop("HLSP2P_FLEET_PAYLOAD_BYTES", None)
+            else:
+                os.environ["HLSP2P_FLEET_PAYLOAD_BYTES"] = saved_ring
     for m in marks_all:
         result["marks"].update(m)
     return result
@@ -266,11 +289,12 @@ if __name__ == "__main__":
     nranks = next((int(a.split("=", 1)[1]) for a in sys.argv if a.startswith("--ranks=")), 1)
     faults = "--faults" in sys.argv
     live = "--live" in sys.argv
+    ring = "--ring" in sys.argv
     argv = [a for a in sys.argv[1:] if not a.startswith("--")]
     lo, hi = (int(argv[0]), int(argv[1])) if len(argv) > 1 else (0, 20)
     bad = []
     for s in range(lo, hi):
-        res = scenario(s, device=device, ranks=nranks, faults=faults, live=live)
+        res = scenario(s, device=device, ranks=nranks, faults=faults, live=live, ring=ring)
         try:
             check(res)
             ends = sorted(round(m["t"], 1) for m in res["marks"].values())

@@ -264,6 +264,24 @@ def test_payload_ring_grows_instead_of_failing_and_revokes_stalled_players(monke
         server.close()
 
 
+def test_a_first_batch_bigger_than_the_configured_ring(monkeypatch):
+    """``HLSP2P_FLEET_PAYLOAD_BYTES`` smaller than the first payload batch: the first ring
+    still holds that batch (it was sized exactly and the rank failed with an IndexError,
+    tests/fleet_chaos.py --ring); an empty ring too small for a batch is replaced."""
+    monkeypatch.setenv("HLSP2P_FLEET_PAYLOAD_BYTES", str(1 << 20))
+    monkeypatch.setattr(FleetServer, "RING_MIN", 1 << 20)
+    a0, _ = mp.Pipe()
+    server = FleetServer(_StubNode(), None, [a0])
+    server._payload = [True]
+    try:
+        ring, (s, _) = server._place(3 << 20)
+        assert ring.cap >= 3 << 20 and s == 0
+        ring2, _ = server._place(ring.cap + 1)  # larger than the ring: a new one, no error
+        assert ring2 is not ring and ring2.cap > ring.cap
+    finally:
+        server.close()
+
+
 def test_fleet_payload_bytes_through_a_wrapping_ring(monkeypatch):
     """``gpuSwarm.fleetPayload`` on the CPU node: a player thread reads every fragment's bytes
     in ``onSuccess`` (zero-copy views into the rank's shared ring) while the ring, sized for a

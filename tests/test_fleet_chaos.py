@@ -43,6 +43,13 @@ def test_fleet_chaos_live(seed, ranks):
     fleet_chaos.check(fleet_chaos.scenario(seed, ranks=ranks, faults=ranks > 1, live=True))
 
 
+@pytest.mark.parametrize("seed,ranks", [(1, 1), (2, 1), (5, 2)])
+def test_fleet_chaos_payload_ring(seed, ranks):
+    """Every player on payloads through a ring that starts at 1 MiB and grows (a first batch
+    bigger than the configured ring raised inside the rank: seeds 1 and 2)."""
+    fleet_chaos.check(fleet_chaos.scenario(seed, ranks=ranks, faults=ranks > 1, ring=True))
+
+
 @pytest.mark.gpu
 @pytest.mark.parametrize("seed,ranks,live", [(4, 1, False), (5, 1, False), (11, 1, False), (4, 2, False),
                                              (32, 2, False), (3, 2, True)])
