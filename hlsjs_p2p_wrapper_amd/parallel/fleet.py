@@ -1201,7 +1201,7 @@ def player_main(conn: Any, spec: Dict[str, Any]) -> None:
     node process serves the segments), ``hls_config``, ``p2p_config``, ``world``, ``rank``;
     for tests, ``script`` (scheduled seeks, pauses, level switches, load restarts) and
     ``read_bytes`` (read every fragment's bytes back through ``RemoteSegment.data()``) and
-    ``in_process`` (a thread in the node's process: leave its torch threads and GPU alone).
+    ``in_process`` (a thread in the node's process: leave its torch threads, GPU and GC alone).
     Control from the node: ``("mark", tag)`` -> reply ``("mark", tag, counters)`` once every
     answer sent before it is buffered; ``("stop",)`` -> close and exit."""
     import copy
@@ -1306,7 +1306,8 @@ def player_main(conn: Any, spec: Dict[str, Any]) -> None:
             drain()
             node.flush()
             if not gc_tuned and node.inflight:  # started: freeze the start-up heap
-                tune_gc()
+                if not in_process:  # (the process's GC is its owner's to tune)
+                    tune_gc()
                 gc_tuned = True
                 if prof is not None:
                     prof.enable()

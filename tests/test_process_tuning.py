@@ -9,6 +9,7 @@ from hlsjs_p2p_wrapper_amd.utils import runtime as rt
 
 def test_tune_gc_freezes_and_raises_gen0():
     prev = gc.get_threshold()
+    rt._freeze_after_full.full_passes = 0  # (the thawing pass is every 4th: not the one below)
     try:
         out = rt.tune_gc(12345)
         assert out == prev and gc.get_threshold()[0] == 12345 and gc.get_freeze_count() > 0
