@@ -1326,6 +1326,14 @@ def player_main(conn: Any, spec: Dict[str, Any]) -> None:
                                         "seeking": media.seeking, "stream": sc.state, "level": hls.currentLevel,
                                         "inflight": sorted(sc.inflight), "pending": len(node._pending),
                                         "node_inflight": node.inflight}
+                        fl = hls.fragmentLoader.loaders
+                        out["state"]["loaders"] = [
+                            (k, id(f) in fl, getattr(fl.get(id(f)), "requestTimeout", None) is not None,
+                             getattr(fl.get(id(f)), "peerAgentLoader", None) is not None)
+                            for k, f in sc.inflight.items()]
+                        out["state"]["n_loaders"] = len(fl)
+                        out["state"]["remote_pending"] = [(rid, q.key[3], q.aborted, q.done)
+                                                          for rid, q in node._pending.items()]
                         lc = hls.levelController
                         lv = hls.levels[lc.level] if hls.levels and 0 <= lc.level < len(hls.levels) else None
                         det = lv.details if lv is not None else None

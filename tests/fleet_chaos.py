@@ -37,6 +37,28 @@ LIVE_SPEED = 20.0  # live scenarios: media seconds per wall second
 LIVE_WALL_S = 6.0  # ... and their wall time
 
 
+def _want_rows(node) -> list:
+    """The node's live wants (diagnostics of a stalled scenario): info row + waiters."""
+    if not len(node._wt):
+        return []
+    ids = np.arange(1, 1 << 16, dtype=np.int64)
+    info = node._wt.info(ids)
+    live = np.flatnonzero(info[:, 0] >= 0)[:8]
+    out = [(int(ids[i]), info[i].tolist(), list(node._wt.waiters(int(ids[i])))) for i in live]
+    try:  # where the planner routes them now (src -1: CDN; a rank: that rank's cache)
+        rt = node.rt
+        w = np.zeros((len(live), 8), dtype=np.int64)
+        w[:, :5] = info[live, :5]
+        w[:, 5] = ids[live]
+        w[:, 6] = node.rank
+        flags = np.where(np.asarray(node.peer_online, dtype=bool), rt.FLAG_ONLINE, 0).astype(np.int64)
+        plan, _, _ = rt.plan_round_for(node.directory, w, flags, node.world, node.rank, None)
+        out.append(("plan", plan.tolist()))
+    except Exception as e:  # noqa: BLE001
+        out.append(("plan error", repr(e)))
+    return out
+
+
 def _draw_rank(rng, duration):
     """One rank's draws: its player count, its cache (in segments) and its players."""
     W = int(rng.integers(2, 4))
@@ -113,6 +135,12 @@ def scenario(seed: int, timeout_s: float = 120.0, device: str = "cpu", ranks: in
     done = [False] * ranks
     marks_all: list = [{} for _ in range(ranks)]
     base = [sum(d[0] for d in draws[:r]) for r in range(ranks)]
+    # no rank is done before every scripted action ran (a player at the end that a late
+    # seek sends back is not done; the scripts' times are on the players' clocks)
+    script_end_s = max([t for _, _, ps in draws for p in ps for t, _, _ in p["script"]] or [0.0]) / 1000.0
+    if live:
+        script_end_s /= speed
+    script_end_s += 0.5
     epoch = time.time() + 0.5  # live: the channel's clock, shared by the nodes and players
     if live:
         origin.live_epoch = epoch
@@ -208,15 +236,23 @@ def scenario(seed: int, timeout_s: float = 120.0, device: str = "cpu", ranks: in
                 for t_ in sorted(server.marks):
                     marks.update(server.marks[t_])
                 marks_all[r] = {base[r] + w: m for w, m in marks.items()}
+                settled = time.monotonic() - t0 > script_end_s
                 if live:  # every mark's t per player, for the end check
                     for t_ in sorted(server.marks)[-3:]:
                         for w, m in server.marks[t_].items():
                             trail[base[r] + w][t_] = m["t"]
                     done[r] = time.monotonic() > live_end
                 else:
-                    done[r] = len(marks) == W and all(m["t"] >= duration - 4.5 for m in marks.values())
+                    done[r] = settled and len(marks) == W and all(m["t"] >= duration - 4.5 for m in marks.values())
                 if r == 0 and stop["step"] is None and (all(done) or errs or time.monotonic() > deadline):
                     stop["step"] = step + 4
+                    result["stop"] = ("done" if all(done) else "errors" if errs else "deadline", list(done),
+                                      round(time.monotonic() - t0, 1))
+                    if not all(done) and not errs:  # a stall: where is every thread?
+                        import traceback
+                        names = {t.ident: t.name for t in threading.enumerate()}
+                        result["stacks"] = {names.get(i, i): "".join(traceback.format_stack(f)[-6:])
+                                            for i, f in sys._current_frames().items()}
                 if stop["step"] is not None and step >= stop["step"]:
                     break
                 if hub is None and (errs or time.monotonic() > deadline):
@@ -230,6 +266,11 @@ def scenario(seed: int, timeout_s: float = 120.0, device: str = "cpu", ranks: in
                                                  server._ring is not None else 0,
                                                  "revoked": len(server.revoked) if server is not None else 0,
                                                  "pending_verify": node.pending_verify(),
+                                                 "round": node.round,
+                                                 "pending_rows": [(int(e), node._vinfo[e][:4].tolist(),
+                                                                   int(node._vround[e]))
+                                                                  for e in np.flatnonzero(node._vflag)[:8]],
+                                                 "want_rows": _want_rows(node),
                                                  "stats": {k: v for k, v in node.stats.items()
                                                            if isinstance(v, (int, float))}}
             for c in conns:

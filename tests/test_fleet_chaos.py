@@ -12,8 +12,9 @@ byte read-back and scripted seeks / pauses / level switches / restarts.
   again, and the new copy took the index slot -- pending, so the first player's fetch found
   nothing.  The request now waits for the check (``SwarmNode._park_on_pending``), and a fetch
   reads the exact copy the player was answered with while its batch holds it.
-* Seed 8 (three ranks) stalled a player once on a fragment never answered, not reproduced
-  since (kept).
+* Seed 8 (three ranks) looked like a player stalled on an unanswered fragment (about 1 run in
+  7): the harness had stopped the scenario once every player was at the end, before a
+  scripted seek sent one back.  Scenarios now end only after every script ran.
 * Live (``live=True``): a switched-to level's first playlist off the playback timeline and a
   seek behind the sliding window stalled players (see ``test_fleet_chaos_live``)."""
 import pytest
