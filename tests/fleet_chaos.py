@@ -83,7 +83,8 @@ def scenario(seed: int, timeout_s: float = 120.0, device: str = "cpu", ranks: in
     ring, the GPU transmux and the on-demand bytes copied back from the device).  ``ranks``:
     rank 0 draws what the single-rank scenario of the seed draws; later ranks draw after it.
     ``faults`` (ranks > 1): each rank also corrupts received rounds and goes offline for a
-    while at random times (drawn from a second generator: the base scenario does not change).
+    while at random times, and the CDN serves one corrupted copy of 1-2 segments (drawn from a
+    second generator: the base scenario does not change).
     ``live``: the channel is live (a sliding window of 6-15 segments published 20x faster than
     real time, players at the live sync point on the channel's clock, live-window eviction on
     the nodes); the scripts' times and pauses are scaled to the channel's clock and their seeks
@@ -120,6 +121,11 @@ def scenario(seed: int, timeout_s: float = 120.0, device: str = "cpu", ranks: in
                          int(frng.integers(1, 4)), float(frng.uniform(0.1, 1.0)))
                         for _ in range(int(frng.integers(1, 4)))) if faults and ranks > 1 else []
                  for _ in range(ranks)]
+    # ... and the CDN serves one corrupted copy of 1-2 segments (a flipped byte mid-segment:
+    # the decrypt / demux may reject it -> the wrapper drops the cached copy, the retry is a
+    # fresh CDN fetch)
+    cdn_corrupt = [int(x) for x in frng.integers(0, nseg, size=int(frng.integers(1, 3)))] \
+        if faults and ranks > 1 else []
     clear_origins()
     pinned = device != "cpu"  # the GPU CDN phase copies from pinned host buffers
     origin = SyntheticHlsOrigin(**origin_kw, pin_memory=pinned)
@@ -127,6 +133,7 @@ def scenario(seed: int, timeout_s: float = 120.0, device: str = "cpu", ranks: in
     hub = ThreadHub(ranks, timeout=60) if ranks > 1 else None
     errs: list = []
     result = {"seed": seed, "ranks": ranks, "duration": duration, "errors": errs, "faults": faults_at,
+              "cdn_corrupt": cdn_corrupt,
               "players": [p for _, _, ps in draws for p in ps], "W": sum(d[0] for d in draws),
               "cache_segs": [c for _, c, _ in draws], "marks": {}}
     # the ranks stop together: a collective round needs every rank, so once rank 0 sees every
@@ -194,6 +201,11 @@ def scenario(seed: int, timeout_s: float = 120.0, device: str = "cpu", ranks: in
                 time.sleep(0.002)
                 if time.monotonic() > end:
                     raise RuntimeError("players did not start")
+            if cdn_corrupt and r == 0:  # (on the origin instance the URLs resolve to)
+                from hlsjs_p2p_wrapper_amd.net import http as _http
+                served = _http.resolve(origin.base_url + origin.segment_path(0, 0))[0]
+                for sn in cdn_corrupt:
+                    served.corrupt(rf"r\d+/seg{sn}\.ts$", 1)
             for c in conns:
                 c.send(("go", {"live_epoch": epoch} if live else {}))
             hs, b = collections.deque(), None
@@ -342,8 +354,9 @@ if __name__ == "__main__":
             st = [n["stats"] for n in res.get("nodes", {}).values()]
             crc, parked = sum(x.get("crc_failures", 0) for x in st), sum(x.get("parked", 0) for x in st)
             ev = sum(n.get("evicted", 0) for n in res.get("nodes", {}).values())
+            inv = sum(x.get("invalidated", 0) for x in st)
             print(f"seed {s}: ok ({res['ranks']} ranks, {res['W']} players, t {ends}, crc failures {crc}, "
-                  f"parked {parked}, evicted {ev})", flush=True)
+                  f"parked {parked}, evicted {ev}, invalidated {inv})", flush=True)
         except AssertionError as e:
             print(f"seed {s}: FAIL {str(e)[:400]}", flush=True)
             bad.append(s)
