@@ -6,7 +6,7 @@ set -eo pipefail
 R=$GRAFT_REPO_ROOT
 cd $R
 export PYTHONPATH=$R HLSP2P_RCCL_REHEARSAL=socket GPU_MAX_HW_QUEUES=1
-O=gpurun_out/r5_rccl_stress
+O=gpurun_out/${STRESS_OUT:-r5_rccl_stress}
 mkdir -p $O
 timeout -k 10 400 python -u bench.py --gpus 8 > $O/n8_default.log 2>&1
 timeout -k 10 400 python -u bench.py --gpus 8 --steps 40 --warmup 3 --cache-gb 2 > $O/n8_tight.log 2>&1
