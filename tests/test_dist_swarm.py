@@ -401,7 +401,13 @@ def test_killing_the_self_launching_bench_stops_its_ranks():
         p.send_signal(signal.SIGKILL)
         p.wait(timeout=30)
         gone, alive = psutil.wait_procs(kids, timeout=60)
-        assert not alive, [a.pid for a in alive]
+
+        def desc(a):
+            try:
+                return a.pid, a.cmdline()[:4], a.ppid()
+            except psutil.Error:
+                return a.pid, None, None
+        assert not alive, [desc(a) for a in alive]
     finally:
         if p.poll() is None:
             p.kill()
