@@ -52,9 +52,12 @@ def test_fleet_chaos_payload_ring(seed, ranks):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("seed,ranks,live", [(4, 1, False), (5, 1, False), (11, 1, False), (4, 2, False),
-                                             (32, 2, False), (3, 2, True)])
-def test_fleet_chaos_seed_gpu(seed, ranks, live):
+@pytest.mark.parametrize("seed,ranks,live,faults", [(4, 1, False, False), (5, 1, False, False),
+                                                    (11, 1, False, False), (4, 2, False, False),
+                                                    (32, 2, False, False), (3, 2, True, False),
+                                                    (7, 2, False, True)])
+def test_fleet_chaos_seed_gpu(seed, ranks, live, faults):
     """The nodes' caches are HBM rings and the transmux runs on the GPU: the on-demand bytes a
-    player reads back come off the device (two ranks: both on the one GPU)."""
-    fleet_chaos.check(fleet_chaos.scenario(seed, device="cuda:0", ranks=ranks, live=live))
+    player reads back come off the device (two ranks: both on the one GPU; with faults, the GPU
+    decrypt / demux rejects corrupted CDN copies and the players invalidate them)."""
+    fleet_chaos.check(fleet_chaos.scenario(seed, device="cuda:0", ranks=ranks, live=live, faults=faults))
