@@ -264,7 +264,9 @@ def _self_launch(args) -> int:
     ``torch.distributed.run`` process (one rank per GPU, rendezvous on 127.0.0.1), forward
     rank 0's JSON line, and exit non-zero if any rank fails, the job overruns
     ``--launch-timeout`` or the record does not report N ranks.  Runs before this process
-    touches the GPU (``torch.cuda.device_count`` does not initialise it) and never execs:
+    touches the GPU -- GPUs are counted from the KFD topology (``visible_gpu_count``), and
+    right before the launcher starts, ``gpu_touched`` must report no HIP context and no
+    ``/dev/kfd`` mapping or descriptor (exit 5 otherwise) -- and never execs:
     the launcher is a child process in this process group, and dies with this process
     (``PR_SET_PDEATHSIG``), so no rank outlives a killed bench."""
     import signal
@@ -272,13 +274,28 @@ def _self_launch(args) -> int:
     import subprocess
     import threading
 
+    from hlsjs_p2p_wrapper_amd.utils.runtime import gpu_touched, visible_gpu_count
+
     n = args.gpus
+    dry = os.environ.get("HLSP2P_LAUNCH_DRYRUN") == "1"  # GPU test of this path: everything but the Popen
+    avail = None
     if not args.cpu and args.dist_backend in ("auto", "nccl") and not os.environ.get("HLSP2P_RCCL_REHEARSAL"):
-        avail = torch.cuda.device_count()
-        if 0 < avail < n:
+        # counted from the KFD topology, not torch.cuda.device_count(): on this torch that may
+        # fall back to hipGetDeviceCount, which starts the HIP runtime in this process, and a
+        # process that initialised the GPU must not fork-and-exec the launcher
+        avail = visible_gpu_count()
+        if 0 < avail < n and not dry:
             print(f"bench.py: --gpus {n} needs {n} visible GPUs for the RCCL data plane (one rank per GPU); "
                   f"{avail} visible.  Rehearse ranks that share a GPU with --dist-backend ipc.", file=sys.stderr)
             return 2
+    touched = gpu_touched()
+    if any(touched.values()):  # checked right before the fork + exec of the launcher
+        print(f"bench.py: refusing to start the launcher from a process that initialised the GPU: {touched}",
+              file=sys.stderr)
+        return 5
+    if dry:
+        print(json.dumps({"launch": "dry-run", "gpus": n, "visible_gpus": avail, **touched}), flush=True)
+        return 0
     s = socket.socket()
     s.bind(("127.0.0.1", 0))
     port = s.getsockname()[1]
@@ -372,11 +389,9 @@ def main() -> int:
     elif args.gpus != launched:
         raise SystemExit(f"bench.py: --gpus {args.gpus} but the launcher started {launched} ranks "
                          f"(WORLD_SIZE={launched}); they must agree")
-    # a round whose transfers are never matched (a dead or diverged peer) fails the job in a
-    # minute, with the rank's plan in the error, instead of at the 600 s library default
-    os.environ.setdefault("HLSP2P_ROUND_TIMEOUT", "60")
-    # likewise a control all-gather whose peer died (the launcher also stops the job then)
-    os.environ.setdefault("HLSP2P_CONTROL_TIMEOUT", "300")  # start-up skew of a cold box stays well inside
+    # a round whose transfers are never matched (a dead or diverged peer), or a control
+    # all-gather a peer never joins, fails the job with the rank's plan in the error: the
+    # library's own deadlines (60 s / 300 s: gpuSwarm.roundTimeoutMs / controlTimeoutMs)
     if args.inflight is None:
         # 64, by measurement (profiles/r4_ab): the headline is PCIe-bound and flat at 128; the
         # HBM-origin probe was +10-20 % at 128 on round-3 boxes and -4 % on round 4's.  (The
@@ -925,7 +940,7 @@ PER_RANK_FIELDS = ("rank", "rounds", "step_ms", "wait_device_us", "exchange_us",
                    "cdn_GBps", "cdn_dev_ms", "p2p_recv_MB", "p2p_sent_MB", "p2p_dev_ms", "p2p_GBps",
                    "p2p_links", "p2p_link_GBps", "transmux_dev_ms", "transmux_wait_us", "await_players_us",
                    "payload_GBps", "payload_wait_us", "crc_failures", "control_fallbacks", "deferred", "inflight",
-                   "cu_reserve")
+                   "cu_reserve", "p2p_rejected_MB")
 
 
 def _per_rank(node, pipe, s0, s1, elapsed, steps, inflight, fleet_total=None, timers=None) -> np.ndarray:
@@ -946,7 +961,7 @@ def _per_rank(node, pipe, s0, s1, elapsed, steps, inflight, fleet_total=None, ti
     per-step host wait on it."""
     rounds = max(1, s1["rounds"] - s0["rounds"])
     tm, pt = timers if timers is not None else (node.timer.total, pipe.timer.total)
-    recv = s1["p2p"] - s0["p2p"]
+    recv = s1.get("p2p_wire", s1["p2p"]) - s0.get("p2p_wire", s0["p2p"])  # wire bytes (checked or not): link rates
     sent = s1["upload"] - s0["upload"]
     links = s1.get("p2p_links", 0) - s0.get("p2p_links", 0)
     p2p_dev_s = tm.get("dev_p2p_ms", 0.0)  # seconds (PhaseTimer totals)
@@ -981,6 +996,8 @@ def _per_rank(node, pipe, s0, s1, elapsed, steps, inflight, fleet_total=None, ti
         "control_fallbacks": getattr(node.comm, "control_fallbacks", 0),
         "deferred": s1.get("deferred", 0) - s0.get("deferred", 0),
         "inflight": inflight, "cu_reserve": cu_reserve,
+        # peer bytes whose CRC check failed (re-fetched from the CDN; not in offload_ratio)
+        "p2p_rejected_MB": (s1.get("p2p_rejected", 0) - s0.get("p2p_rejected", 0)) / 1e6,
     }
     return np.array([int(round(float(vals[k]) * 1000)) for k in PER_RANK_FIELDS], dtype=np.int64)
 
@@ -1061,6 +1078,13 @@ def _plane_info(node, dist, world: int, device, recv_from=None) -> dict:
     if transport.startswith("rccl") and distinct is not True and rehearsal is None:
         raise RuntimeError(f"RCCL data plane without one GPU per rank: {[(r['rank'], r['pci_bus_id']) for r in ranks]}")
     rccl = next((r["comm"]["rccl"] for r in ranks if "rccl" in r.get("comm", {})), None)
+    # the wire each rank's RCCL connections actually use (RCCL's own connection log: P2P over
+    # xGMI, or a NET fallback) and HIP's link type to its peers (parallel/wire.py)
+    from hlsjs_p2p_wrapper_amd.parallel.wire import degraded
+    for r in ranks:
+        w = r.get("comm", {}).get("wire")
+        r["transport"] = w.get("transport") if w else None
+    wires = sorted({r["transport"] for r in ranks if r["transport"]})
     return {"data": transport, "control": getattr(comm, "control_transport", "local"),
             "ipc_events": bool(ipc is not None and ipc._peer_ev is not None),
             "shm_slot_words": getattr(comm, "shm_slot_words", None),
@@ -1068,13 +1092,24 @@ def _plane_info(node, dist, world: int, device, recv_from=None) -> dict:
             "launcher": os.environ.get("HLSP2P_LAUNCHER") or ("torchrun" if "TORCHELASTIC_RUN_ID" in os.environ
                                                               else "env" if world > 1 else "none"),
             "world": world, "distinct_devices": distinct, "rccl_rehearsal": rehearsal,
-            "rccl_version": rccl["version"] if rccl else None, "ranks": ranks}
+            "rccl_version": rccl["version"] if rccl else None, "wire": wires,
+            "transport_degraded": degraded(transport, distinct, rehearsal, wires), "ranks": ranks}
 
 
 def _label_rehearsal(result: dict) -> None:
     """A run whose RCCL ranks share GPUs (``HLSP2P_RCCL_REHEARSAL``) says so in its config:
     the model names the devices actually used and the parallelism the transport."""
     dp = result.get("data_plane") or {}
+    if dp.get("transport_degraded"):
+        # one GPU per rank, yet RCCL connected some pair over a network transport: the number
+        # is real but it is not an xGMI number, and the record says so where it is read first
+        cfg = result["config"]
+        cfg["model"] += f" [RCCL fell back to {'/'.join(dp.get('wire') or [])}: NOT an xGMI run]"
+        cfg["parallelism"] += "-degraded"
+        print(f"bench.py: WARNING: RCCL transport degraded on a one-GPU-per-rank run: {dp.get('wire')}; "
+              "see data_plane.ranks[*].comm.wire", file=sys.stderr, flush=True)
+        if os.environ.get("HLSP2P_REQUIRE_XGMI") == "1":
+            raise RuntimeError(f"RCCL data plane did not use its P2P transport: {dp.get('wire')}")
     if not dp.get("rccl_rehearsal"):
         return
     devs = {(r["host"], r["pci_bus_id"]) for r in dp.get("ranks", [])}

@@ -79,6 +79,12 @@ SRC_CDN, SRC_P2P, SRC_CACHE = 0, 1, 2  # source codes of delivery columns (paral
 SOURCE_NAMES = ("cdn", "p2p", "cache")
 
 
+class SwarmPeerLost(TimeoutError):
+    """A swarm collective did not complete: a peer died, or stopped answering within the
+    round / control deadline (``gpuSwarm.roundTimeoutMs`` / ``controlTimeoutMs``).  The
+    message carries this rank's plan of the last round it posted."""
+
+
 class Request:
     """One in-process ``getSegment`` request: the loader handle (``abort()``) and its
     delivery state.  Its want-table token is negative (fleet tokens are >= 0)."""
@@ -281,6 +287,18 @@ class SwarmNode:
         self.cdn_dedup = cdn_dedup
         self.round = 0
         self.round_interval_ms = round_interval_ms
+        # fail-fast deadlines (gpuSwarm.roundTimeoutMs; the control all-gather's is the comm's
+        # control_timeout_s, gpuSwarm.controlTimeoutMs): None = HLSP2P_ROUND_TIMEOUT or 60 s
+        self.round_timeout_s: Optional[float] = None
+        self._last_posted: Optional[RoundHandle] = None  # for the diagnostic of a lost peer
+        # fault injection (SURVEY 5.3 "drop peer"): HLSP2P_FAULT_EXIT=<rank>:<round> makes that
+        # rank's process die abruptly (os._exit) when it starts that round, as a crashed peer
+        self._exit_at = None
+        fe = os.environ.get("HLSP2P_FAULT_EXIT")
+        if fe:
+            fr, _, fk = fe.partition(":")
+            if int(fr) == self.rank:
+                self._exit_at = int(fk)
         self.auto_tick = auto_tick
         self.max_wants_per_round = max_wants_per_round
         self.leaving = False
@@ -311,9 +329,15 @@ class SwarmNode:
         self._prefetched: Dict[Tuple[int, int, int, int], str] = {}  # key -> "cdn" | "p2p"
         self._net_wants = False  # some want came from a network origin (plans may carry STAGE rows)
         self.peer_online = np.ones(self.world, dtype=bool)
+        # "p2p" / "p2p_segments": peer bytes / segments that PASSED their CRC check (counted when
+        # the check ran: in complete_round, or in verify_done for a check deferred to the
+        # consumer's decrypt); a rejected copy counts in "p2p_rejected" and its CDN re-fetch in
+        # "cdn", so cdn + p2p is what the players were served, and offload = p2p / (cdn + p2p)
+        # stays exact under corruption.  Wire-level: "p2p_wire" (every byte received, checked or
+        # not) and "p2p_links" ((round, source peer) pairs received from): link rates
         self.stats = {"cdn": 0, "p2p": 0, "upload": 0, "cache": 0, "rounds": 0, "crc_failures": 0,
                       "segments": 0, "cdn_segments": 0, "p2p_segments": 0, "prefetched": 0,
-                      "p2p_links": 0}  # p2p_links: (round, source peer) pairs received from
+                      "p2p_links": 0, "p2p_wire": 0, "p2p_rejected": 0, "p2p_rejected_segments": 0}
         self.swarm_stats = {"cdn": 0, "p2p": 0, "upload": 0}
         self.last_round: Dict[str, Any] = {}
         self.corrupt_next_recv = 0  # fault injection: flip a byte in the next N received rounds
@@ -891,6 +915,9 @@ class SwarmNode:
         t0 = time.perf_counter()
         self.round += 1
         self.stats["rounds"] += 1
+        if self._exit_at is not None and self.round >= self._exit_at:
+            log.error("rank %d: injected crash at round %d (HLSP2P_FAULT_EXIT)", self.rank, self.round)
+            os._exit(17)
         if self.verify_deferred and self.round % 8 == 0 and len(self._vflag):
             self._sweep_pending()
         if self._pins:
@@ -931,7 +958,10 @@ class SwarmNode:
             if not self.store.wrap_for(need):
                 raise RuntimeError("segment cache cannot wrap for the round (pinned entries block eviction)")
         adds, rms = self.store.take_delta()
-        parts = self.comm.allgather_control(self._encode(rows, adds, rms))
+        try:
+            parts = self.comm.allgather_control(self._encode(rows, adds, rms))
+        except Exception as e:  # noqa: BLE001 - a dead or stalled peer (deadline: comm.control_timeout_s)
+            raise self._peer_lost("control all-gather", e) from e
         # every rank's deltas into the directory + the round's want rows, in one native call
         # (after checking that every replica and the last plans agree)
         try:
@@ -971,6 +1001,7 @@ class SwarmNode:
         recv_rows = plan[(plan[:, 6] == me) & (plan[:, 5] >= 0)]
         h.n_send = len(send_rows)
         h.plan = (send_rows, recv_rows)  # kept for the diagnostic of a round that never completes
+        self._last_posted = h
         # ---------------- 2. pin what we send from cache (seeded rows come from the CDN phase)
         # send_eids[i]: store entry of send row i (-1: missing), aligned with send_rows
         send_eids = np.full(len(send_rows), -1, dtype=np.int64)
@@ -1060,9 +1091,13 @@ class SwarmNode:
             commit = good[2] if dgood is None else good[2][~dgood]
             if len(commit):
                 self.store.commit(commit)
+                # checked by the node's verify CRC (rows deferred to their consumer count when
+                # their check comes back: _settle_deferred / verify_done)
+                self._count_p2p(good[4] if dgood is None else good[4][~dgood], True)
             if bad is not None:
                 self.store.drop(bad[2])
                 self.stats["crc_failures"] += len(bad[0])
+                self._count_p2p(bad[4], False)
         if h.send_pins is not None:
             self.store.unpin(h.send_pins)
         for x in h.release:  # the round's DMAs are done: drop the staged host copies
@@ -1166,15 +1201,16 @@ class SwarmNode:
         ``hipEventSynchronize`` would block forever.  Instead: poll the round's event (the
         common case finishes within the first ``ROUND_SPIN_S``), then poll it every
         millisecond while asking the communicator for an asynchronous error
-        (``ncclCommGetAsyncError``) and watching the ``HLSP2P_ROUND_TIMEOUT`` deadline
-        (default 600 s); either one raises instead of hanging the rank."""
+        (``ncclCommGetAsyncError``) and watching the round deadline (``gpuSwarm.roundTimeoutMs``,
+        else ``HLSP2P_ROUND_TIMEOUT`` seconds, else 60 s: :meth:`round_deadline_s`); either one
+        raises instead of hanging the rank."""
         ev = h.done
         spin_end = time.perf_counter() + self.ROUND_SPIN_S
         while time.perf_counter() < spin_end:
             if ev.query():
                 return
         check = getattr(self.comm, "async_error", None)
-        deadline = time.perf_counter() + float(os.environ.get("HLSP2P_ROUND_TIMEOUT", "600"))
+        deadline = time.perf_counter() + self.round_deadline_s()
         while not ev.query():
             err = check() if check is not None else ""
             if err:
@@ -1184,9 +1220,31 @@ class SwarmNode:
                 log.error("rank %d: swarm round %d did not complete; this rank's plan: %s", self.rank, h.round,
                           summary)
                 self._dump_plan(h)
-                raise TimeoutError(f"rank {self.rank}: swarm round {h.round} did not complete on the device "
-                                   f"(HLSP2P_ROUND_TIMEOUT); a peer may have stopped.  Plan: {summary}")
+                raise SwarmPeerLost(f"rank {self.rank}: swarm round {h.round} did not complete on the device "
+                                    f"within {self.round_deadline_s():g} s (gpuSwarm.roundTimeoutMs); a peer may have "
+                                    f"stopped.  Plan: {summary}")
             time.sleep(1e-3)
+
+    ROUND_TIMEOUT_S = 60.0  # library default of the round deadline (was 600 s outside bench.py)
+
+    def round_deadline_s(self) -> float:
+        """Seconds a round may wait for its transfers: ``gpuSwarm.roundTimeoutMs`` when set,
+        else ``HLSP2P_ROUND_TIMEOUT`` (read at each wait), else :attr:`ROUND_TIMEOUT_S`."""
+        if self.round_timeout_s is not None:
+            return float(self.round_timeout_s)
+        return float(os.environ.get("HLSP2P_ROUND_TIMEOUT", str(self.ROUND_TIMEOUT_S)))
+
+    def _peer_lost(self, where: str, err: BaseException) -> "SwarmPeerLost":
+        """A collective of the swarm failed (a peer died or stopped answering within the
+        deadline): stop the data plane without waiting on peers, and build the error with this
+        rank's plan of the last round it posted (what its peers were to send / receive)."""
+        summary = self.plan_summary(self._last_posted) if self._last_posted is not None else {}
+        log.error("rank %d: swarm %s failed in round %d: %s; last posted plan: %s", self.rank, where, self.round,
+                  err, summary)
+        self._diverged(f"{where} failed: {err}")
+        return SwarmPeerLost(f"rank {self.rank}: swarm {where} failed in round {self.round} ({type(err).__name__}: "
+                             f"{err}); a peer may have stopped.  Plan of round "
+                             f"{summary.get('round', '-')}: {summary}")
 
     @staticmethod
     def plan_summary(h: RoundHandle) -> Dict[str, Any]:
@@ -1397,10 +1455,13 @@ class SwarmNode:
             start = self._events.get(True)
             end = self._events.get(True)
             start.record(self.stream)  # launch_round runs this phase on the node stream
-        if spans_plane is not None:
-            spans_plane(*_span_columns(self.arena.data_ptr(), srun, trailer_all, rrun, trailers))
-        else:
-            self.comm.exchange(sends, recvs)
+        try:
+            if spans_plane is not None:
+                spans_plane(*_span_columns(self.arena.data_ptr(), srun, trailer_all, rrun, trailers))
+            else:
+                self.comm.exchange(sends, recvs)
+        except Exception as e:  # noqa: BLE001 - e.g. gloo's "connection closed by peer"
+            raise self._peer_lost("data-plane exchange", e) from e
         if self.is_cuda:
             end.record(self.stream)
             h.ev_p2p = (start, end)
@@ -1432,8 +1493,8 @@ class SwarmNode:
             h.ok_host.copy_(ok, non_blocking=True)
         else:
             h.ok_host = ok
-        self.stats["p2p"] += int(recv_rows[:, 4].sum())
-        self.stats["p2p_segments"] += len(recv_rows)
+        # wire-level only: peer bytes count as delivered P2P once their CRC check passed
+        self.stats["p2p_wire"] += int(recv_rows[:, 4].sum())
         self.stats["p2p_links"] += len(rrun)
 
     def _defer_verify(self, h: RoundHandle, defer: np.ndarray, trailers, roff_a: np.ndarray, recv_rows: np.ndarray,
@@ -1493,10 +1554,12 @@ class SwarmNode:
                 ok_now = _crc.crc32_batch(self.arena, offs[nr], lens[nr], expect=exp)[1].numpy().astype(bool)
             if ok_now.any():
                 self.store.commit(eids[nr[ok_now]])
+                self._count_p2p(lens[nr[ok_now]], True)
             bad = nr[~ok_now]
             if len(bad):
                 self.store.drop(eids[bad])
                 self.stats["crc_failures"] += len(bad)
+                self._count_p2p(lens[bad], False)
                 keep = np.ones(len(tok), dtype=bool)
                 for r in bad.tolist():
                     sel = idx == r
@@ -1513,6 +1576,21 @@ class SwarmNode:
         if keep is not None:
             tok, idx = tok[keep], idx[keep]
         return tok, idx, exp_row[idx]
+
+    def _count_p2p(self, lens: np.ndarray, passed: bool) -> None:
+        """Account peer copies whose CRC check just ran: delivered P2P bytes when it passed,
+        rejected bytes when it failed (the segment is then re-fetched, and counted, from the
+        CDN)."""
+        n = len(lens)
+        if not n:
+            return
+        b = int(np.asarray(lens, dtype=np.int64).sum())
+        if passed:
+            self.stats["p2p"] += b
+            self.stats["p2p_segments"] += n
+        else:
+            self.stats["p2p_rejected"] += b
+            self.stats["p2p_rejected_segments"] += n
 
     def _vpend_add(self, eids: np.ndarray, info: np.ndarray, expect: np.ndarray) -> None:
         need = int(eids.max()) + 1
@@ -1608,6 +1686,7 @@ class SwarmNode:
             self._vflag[good] = False
             self.store.commit(good)
             self.store.unpin(good)
+            self._count_p2p(self._vinfo[good, 4], True)
             if self._vwait:
                 for e in good.tolist():
                     if e in self._vwait:
@@ -1620,6 +1699,7 @@ class SwarmNode:
             self.store.detach(arr)
             self.store.unpin(arr)
             self.stats["crc_failures"] += 1
+            self._count_p2p(self._vinfo[e:e + 1, 4], False)
             toks = tokens[inv == k]
             self._retry_cdn(self._vinfo[e], toks[toks >= 0])  # bulk (fleet) tokens: asked again here
             if e in self._vwait:
@@ -1842,7 +1922,10 @@ def node_for_config(p2p_config: Any) -> SwarmNode:
     ``GET /metrics`` on port + rank, 0 = ephemeral; ``metricsHost`` defaults to
     127.0.0.1), ``network`` (``True`` or ``HttpOrigin`` options: fetch ``http(s)://`` URLs
     no in-process origin serves from the real CDN, :mod:`..net.network`); the agent reads
-    ``prefetchSeconds`` / ``prefetchMaxSegments``.  ``deferVerify``: segments received from
+    ``prefetchSeconds`` / ``prefetchMaxSegments``.  ``roundTimeoutMs`` (default 60 000) /
+    ``controlTimeoutMs`` (default 300 000): how long a round may wait for its transfers and the
+    control all-gather for every peer before the rank raises :class:`SwarmPeerLost` with its
+    plan (a dead peer fails the job in a minute instead of hanging it).  ``deferVerify``: segments received from
     peers reach in-process players before their CRC check, which the player's transmux batch
     runs fused into its decrypt (:class:`VerifyTicket`).  ``numaBind``: run this process on the CPUs
     local to the node's GPU (``utils.runtime.bind_to_gpu_numa``; ``bench.py --numa auto``).
@@ -1884,6 +1967,10 @@ def node_for_config(p2p_config: Any) -> SwarmNode:
         from ..utils.runtime import bind_to_gpu_numa
 
         bind_to_gpu_numa(node.device.index if node.device.index is not None else torch.cuda.current_device())
+    if cfg.get("roundTimeoutMs") is not None:
+        node.round_timeout_s = float(cfg["roundTimeoutMs"]) / 1e3
+    if cfg.get("controlTimeoutMs") is not None and hasattr(comm, "control_timeout_s"):
+        comm.control_timeout_s = float(cfg["controlTimeoutMs"]) / 1e3
     if cfg.get("deferVerify"):  # in-process players verify received segments in their transmux
         node.verify_deferred = node.defer_inproc = True
     if cfg.get("trace"):

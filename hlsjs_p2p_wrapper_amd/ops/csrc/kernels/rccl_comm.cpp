@@ -175,12 +175,24 @@ std::string pci_bus_id(int device) {
   return std::string(buf);
 }
 
+// HIP's view of the link between two devices of this process (HSA_AMD_LINK_INFO_TYPE_*:
+// 2 = PCIe, 4 = xGMI) and its hop count: the second, RCCL-independent proof of the wire an
+// N > 1 record ran on (parallel/wire.py).
+py::tuple link_type(int dev_a, int dev_b) {
+  uint32_t type = 0, hops = 0;
+  const hipError_t e = hipExtGetLinkTypeAndHopCount(dev_a, dev_b, &type, &hops);
+  if (e != hipSuccess)
+    throw std::runtime_error(std::string("hipExtGetLinkTypeAndHopCount: ") + hipGetErrorString(e));
+  return py::make_tuple(type, hops);
+}
+
 }  // namespace
 
 void register_rccl(py::module& m) {
   m.def("rccl_unique_id", &unique_id, "ncclGetUniqueId (rank 0 of a new communicator)");
   m.def("rccl_version", &version);
   m.def("pci_bus_id", &pci_bus_id, py::arg("device"));
+  m.def("link_type", &link_type, py::arg("dev_a"), py::arg("dev_b"));
   py::class_<RcclComm, std::shared_ptr<RcclComm>>(m, "RcclComm")
       .def(py::init<const py::bytes&, int, int, int>(), py::arg("unique_id"), py::arg("world"), py::arg("rank"),
            py::arg("device"))

@@ -163,7 +163,10 @@ class DistComm(SwarmComm):
         self.data_group = data_group
         self.data_backend = backend
         self._cap = 64  # int64 words per rank in the one-shot control all-gather
-        self.control_timeout_s = float(os.environ.get("HLSP2P_CONTROL_TIMEOUT", "600"))
+        # a control all-gather waits this long for every peer before raising (gpuSwarm.
+        # controlTimeoutMs; HLSP2P_CONTROL_TIMEOUT seconds): long enough for a cold box's start-up
+        # skew, short enough that a dead peer fails the job instead of hanging it
+        self.control_timeout_s = float(os.environ.get("HLSP2P_CONTROL_TIMEOUT", str(self.CONTROL_TIMEOUT_S)))
         # shared-memory slot per rank and round: a message larger than it makes every rank
         # take the gloo all-gather for that round (~3.4 ms at 8 ranks instead of ~10 us):
         # counted, and warned about once, never silent (bench.py sizes the slot)
@@ -173,6 +176,8 @@ class DistComm(SwarmComm):
         self.control_transport = "shm" if self._shm is not None else "gloo"
         self._rccl = None
         self.rehearsal = None
+        self.rccl_log: Optional[str] = None  # RCCL's connection log of this rank (parallel/wire.py)
+        self.peer_devices: dict = {}  # rank -> (host id, PCI bus id, device index), native RCCL plane
         self._ipc: Optional[_IpcOutbox] = None
         if backend == "gloo" and plane == "ipc" and self.world_size > 1 and torch.cuda.is_available():
             self._ipc = _IpcOutbox.open(self)
@@ -226,31 +231,49 @@ class DistComm(SwarmComm):
         uid: List[object] = [None]
         gpu = None
         self.rehearsal = os.environ.get("HLSP2P_RCCL_REHEARSAL") or None
+        if self.rehearsal is not None and self.data_backend != "gloo":
+            # the rehearsal's per-rank host id must reach RCCL before its first call; an nccl
+            # default group may have initialised RCCL (and hashed the real host id) already.
+            # The default group's backend is the same on every rank: all raise here together
+            raise RuntimeError("HLSP2P_RCCL_REHEARSAL needs a gloo default group with HLSP2P_DATA_PLANE=rccl "
+                               "(bench.py's GPU launch), not an nccl one")
         if self.rehearsal == "socket":  # before any RCCL call: the host hash is computed once
             os.environ["NCCL_HOSTID"] = f"hlsp2p-rehearsal-{os.getpid()}-{self.rank}"
             os.environ.setdefault("NCCL_SOCKET_IFNAME", "lo")
             os.environ.setdefault("NCCL_IB_DISABLE", "1")
         elif self.rehearsal is not None:
             raise ValueError(f"unknown HLSP2P_RCCL_REHEARSAL {self.rehearsal!r} (expected 'socket')")
+        # RCCL's per-peer connection log (which wire each pair runs on: parallel/wire.py), set
+        # before the process's first RCCL call, which reads the debug variables once
+        from .wire import configure_rccl_log
+
+        self.rccl_log = configure_rccl_log(self.rank)
+        dev_index = torch.cuda.current_device()
         try:
             from ..ops._native import device as _dev
 
             dev = _dev()
             dev.rccl_version()
-            gpu = dev.pci_bus_id(torch.cuda.current_device())
+            gpu = dev.pci_bus_id(dev_index)
             if self.rank == 0:  # a failure here is reported through the all-gather below
                 uid[0] = dev.rccl_unique_id()
         except Exception:  # noqa: BLE001 - no native module / RCCL: torch's path
             ok = False
         flags: List[object] = [None] * self.world_size
-        dist.all_gather_object(flags, (ok, _host_id(), gpu), group=g)
+        dist.all_gather_object(flags, (ok, _host_id(), gpu, self.rehearsal, dev_index), group=g)
         if not all(f[0] for f in flags):  # type: ignore[index]
             return None
+        # every rank must agree on the rehearsal mode: a rank that skips the duplicate-device
+        # check below while another raises would leave the others blocked in the next collective
+        modes = sorted({str(f[3]) for f in flags})  # type: ignore[index]
+        if len(modes) > 1:
+            raise RuntimeError(f"ranks disagree on HLSP2P_RCCL_REHEARSAL: {[f[3] for f in flags]}")  # type: ignore[index]
+        self.peer_devices = {r: (f[1], f[2], f[4]) for r, f in enumerate(flags)}  # type: ignore[index]
         # one GPU per rank: RCCL cannot place two ranks of a communicator on one device (it
         # fails deep inside ncclCommInitRank, or worse, a launcher mapped ranks onto a shared
         # card silently); every rank sees the same table, so every rank raises here together
         seen: dict = {}
-        for r, (_, host, bus) in enumerate(flags):  # type: ignore[misc]
+        for r, (_, host, bus, _, _) in enumerate(flags):  # type: ignore[misc]
             if (host, bus) in seen and self.rehearsal is None:
                 raise RuntimeError(f"RCCL data plane: ranks {seen[(host, bus)]} and {r} would share GPU {bus} on "
                                    f"host {host[0]}; RCCL needs one GPU per rank (rehearse ranks that share a "
@@ -271,6 +294,7 @@ class DistComm(SwarmComm):
         return comm
 
     SHM_SLOT_WORDS = 16384  # int64 words per rank and round (128 KiB); larger -> gloo
+    CONTROL_TIMEOUT_S = 300.0  # library default of the control all-gather's deadline
 
     def _open_shm_control(self):
         """Shared-memory control plane when every rank runs on this host (collective).
@@ -439,8 +463,32 @@ class DistComm(SwarmComm):
             out["rccl"] = {"count": int(self._rccl.comm_count()), "rank": int(self._rccl.comm_user_rank()),
                            "device": int(self._rccl.comm_device()), "rounds": int(self._rccl.rounds),
                            "version": _dev().rccl_version()}
+            out["wire"] = self.wire()
         if self._ipc is not None:
             out["ipc_exchanges"] = int(self._ipc.exchanges)
+        return out
+
+    def wire(self) -> dict:
+        """Which wire this rank's RCCL connections run on (parallel/wire.py): RCCL's own
+        per-peer transport from its connection log, its view of the group (ranks / nodes /
+        local ranks), and HIP's link type to each peer's device on this host.  Read after the
+        exchanges ran: RCCL connects a pair at its first send / receive."""
+        from .wire import link_types, read_rccl_log, summarize
+
+        rep = read_rccl_log(self.rccl_log, self.rank)
+        out: dict = {"transport": summarize(rep, self.world_size)}
+        if rep is not None:
+            out.update(peers=rep["peers"], n_ranks=rep["n_ranks"], n_nodes=rep["n_nodes"],
+                       local_ranks=rep["local_ranks"], connections=rep["connections"], log_bytes=rep["log_bytes"])
+        else:
+            out["peers"] = None
+        me = self.peer_devices.get(self.rank)
+        if me is not None:
+            same_host = {r: d[2] for r, d in self.peer_devices.items() if r != self.rank and d[0] == me[0]}
+            try:
+                out["links"] = link_types(me[2], same_host) if same_host else {}
+            except Exception as e:  # noqa: BLE001 - diagnostic only
+                out["links"] = f"error: {e}"
         return out
 
     def _exchange_staged(self, sends, recvs) -> None:

@@ -192,3 +192,119 @@ def bind_to_gpu_numa(device_index: int = 0, min_cpus: int = 8) -> Optional[int]:
         return node if local == allowed else None
     os.sched_setaffinity(0, local)
     return node
+
+
+KFD_TOPOLOGY = "/sys/class/kfd/kfd/topology/nodes"
+
+
+def kfd_gpus(topology: str = KFD_TOPOLOGY, dev_dir: str = "/dev/dri") -> List[dict]:
+    """The GPU agents ROCr would enumerate, read from the KFD topology without any HIP / HSA
+    call: the nodes whose ``properties`` report SIMDs (``simd_count > 0``; CPU nodes have
+    none) in node order, each with its ``gpu_id``, ``drm_render_minor`` and whether this
+    process can open its render node (ROCr skips a GPU whose render node it cannot open, e.g.
+    one a container did not pass through).  Opening a DRM render node creates no HSA queue
+    or KFD mapping."""
+    out: List[dict] = []
+    try:
+        names = sorted(os.listdir(topology), key=lambda s: int(s) if s.isdigit() else 1 << 30)
+    except OSError:
+        return out
+    for name in names:
+        props: dict = {}
+        try:
+            with open(os.path.join(topology, name, "properties")) as f:
+                for ln in f:
+                    k, _, v = ln.strip().partition(" ")
+                    if v.strip().lstrip("-").isdigit():
+                        props[k] = int(v)
+        except OSError:
+            continue
+        if props.get("simd_count", 0) <= 0:
+            continue
+        minor = props.get("drm_render_minor")
+        usable = False
+        if minor is not None and minor >= 0:
+            try:
+                fd = os.open(os.path.join(dev_dir, f"renderD{minor}"), os.O_RDWR | os.O_CLOEXEC)
+                os.close(fd)
+                usable = True
+            except OSError:
+                usable = False
+        out.append({"node": int(name) if name.isdigit() else name, "gpu_id": props.get("gpu_id"),
+                    "render_minor": minor, "usable": usable})
+    return out
+
+
+def _visible_filter(n: int, spec: Optional[str]) -> int:
+    """How many of ``n`` devices a ``*_VISIBLE_DEVICES`` list keeps: its entries up to the first
+    invalid one (the runtimes stop parsing there; ``-1`` hides every device).  UUID entries
+    (``GPU-...``) count as one device each."""
+    if spec is None:
+        return n
+    k = 0
+    seen: set = set()
+    for tok in spec.split(","):
+        tok = tok.strip()
+        if not tok:
+            break
+        if tok.upper().startswith("GPU-"):
+            k += 1
+            continue
+        try:
+            i = int(tok)
+        except ValueError:
+            break
+        if i < 0 or i >= n or i in seen:
+            break
+        seen.add(i)
+        k += 1
+    return min(k, n)
+
+
+def visible_gpu_count(topology: str = KFD_TOPOLOGY, dev_dir: str = "/dev/dri") -> int:
+    """Number of GPUs a HIP process started now would see, computed WITHOUT initialising HIP
+    (``torch.cuda.device_count()`` may fall back to ``hipGetDeviceCount``, which starts the HIP
+    runtime and maps ``/dev/kfd`` in the calling process): the usable KFD GPU agents
+    (:func:`kfd_gpus`), narrowed by ``ROCR_VISIBLE_DEVICES`` and then by ``HIP_VISIBLE_DEVICES``
+    (or ``CUDA_VISIBLE_DEVICES``), as ROCr and HIP apply them."""
+    n = sum(1 for g in kfd_gpus(topology, dev_dir) if g["usable"])
+    n = _visible_filter(n, os.environ.get("ROCR_VISIBLE_DEVICES"))
+    hip = os.environ.get("HIP_VISIBLE_DEVICES")
+    if hip is None:
+        hip = os.environ.get("CUDA_VISIBLE_DEVICES")
+    return _visible_filter(n, hip)
+
+
+def gpu_touched() -> dict:
+    """Has this process initialised the GPU?  ``torch_initialized``: torch's HIP context
+    (``torch.cuda.is_initialized``, without importing torch if it is not loaded);
+    ``kfd_mapped``: some ``/dev/kfd`` mapping in ``/proc/self/maps`` (the HSA runtime maps its
+    doorbells and queues from it); ``kfd_open``: an open ``/dev/kfd`` descriptor.  A process
+    for which any is true must not fork-and-exec or exec another program on this pool."""
+    import sys
+
+    torch_mod = sys.modules.get("torch")
+    init = False
+    if torch_mod is not None:
+        try:
+            init = bool(torch_mod.cuda.is_initialized())
+        except Exception:  # noqa: BLE001 - a torch without the cuda module
+            init = False
+    mapped = False
+    try:
+        with open("/proc/self/maps") as f:
+            mapped = any("/dev/kfd" in ln for ln in f)
+    except OSError:
+        pass
+    opened = False
+    try:
+        for fd in os.listdir("/proc/self/fd"):
+            try:
+                if os.readlink(f"/proc/self/fd/{fd}") == "/dev/kfd":
+                    opened = True
+                    break
+            except OSError:
+                continue
+    except OSError:
+        pass
+    return {"torch_initialized": init, "kfd_mapped": mapped, "kfd_open": opened}

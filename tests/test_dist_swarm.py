@@ -121,6 +121,8 @@ def test_bench_fleet_corrupted_peer_copies_are_refetched(players):
     assert res["config"]["receive_verify"] == "fused-decrypt"
     fails = sum(r["crc_failures"] for r in res["per_rank"])
     assert 1 <= fails <= 6  # at most one per corrupted round on each rank
+    # rejected copies are counted apart: offload_ratio covers verified peer bytes only
+    assert sum(r["p2p_rejected_MB"] for r in res["per_rank"]) > 0
 
 
 def test_bench_eight_ranks_driver_shape():

@@ -197,7 +197,7 @@ def test_consistent_ranks_pass_the_check(origin):
     assert nodes[0].directory.digest == nodes[1].directory.digest != 0
     # every byte rank r received came from the other rank
     assert nodes[0].p2p_from[0] == 0 and nodes[1].p2p_from[1] == 0
-    assert nodes[0].p2p_from[1] + nodes[1].p2p_from[0] == nodes[0].stats["p2p"] + nodes[1].stats["p2p"] > 0
+    assert nodes[0].p2p_from[1] + nodes[1].p2p_from[0] == nodes[0].stats["p2p_wire"] + nodes[1].stats["p2p_wire"] > 0
 
 
 def test_round_timeout_reports_and_dumps_the_plan(tmp_path, monkeypatch):

@@ -104,8 +104,15 @@ def test_native_rccl_plane_with_ranks_sharing_the_gpu(cuda):
     assert res["config"]["parallelism"] == "swarm2-rccl-socket" and "rehearsal" in res["config"]["model"]
     dp = res["data_plane"]
     assert dp["data"] == "rccl-native" and dp["rccl_rehearsal"] == "socket" and dp["launcher"] == "self"
+    # the wire, from RCCL's own connection log: every peer over its socket transport (the
+    # parser's positive control: on an 8-GPU node the same record must say P2P)
+    assert dp["wire"] == ["net"] and dp["transport_degraded"] is False  # a rehearsal, labelled as such
     for r in dp["ranks"]:
         rc = r["comm"]["rccl"]
         assert rc["count"] == 2 and rc["rank"] == r["rank"] and rc["rounds"] > 0
         assert sum(r["recv_bytes_from"]) > 0
+        w = r["comm"]["wire"]
+        assert r["transport"] == "net" and w["peers"] == {str(1 - r["rank"]): ["NET/Socket"]}, w
+        assert w["n_nodes"] == 2 and w["log_bytes"] < (1 << 20), w
+        assert w["links"] == {str(1 - r["rank"]): "same-device"}, w
     assert 1 <= sum(r["crc_failures"] for r in res["per_rank"]) <= 6

@@ -122,6 +122,14 @@ t = c.topology()
 assert t['transport'] == 'rccl-native' and t['world'] == 1, t
 assert t['rccl']['count'] == 1 and t['rccl']['rank'] == 0 and t['rccl']['device'] == 0, t
 assert t['rccl']['rounds'] == 1 and int(t['rccl']['version']) >= 21800, t
+# the wire: a world of one connects nothing (sends to self are local copies); RCCL's own log
+# names the group it built (1 rank, 1 node)
+w = t['wire']
+if '{group}' == 'nccl':  # torch's eager nccl group started RCCL first: its debug output was set already
+    assert w['transport'] == 'unknown' and w['peers'] is None, w
+else:
+    assert w['transport'] == 'self' and w['peers'] == dict() and w['n_ranks'] == 1 and w['n_nodes'] == 1, w
+    assert w['log_bytes'] < (1 << 20), w  # INIT/P2P/NET only: no per-operation lines
 c.close()
 dist.destroy_process_group()
 print('NATIVE_OK')
