@@ -142,6 +142,15 @@ def parse():
     p.add_argument("--corrupt-recv", type=int, default=0, metavar="N",
                    help="fault injection (SURVEY 5.3): flip a byte in the first segment received from a peer in "
                         "each of the first N timed rounds; the CRC check must drop it and the CDN re-serve it")
+    p.add_argument("--cu-calibrate", default=os.environ.get("HLSP2P_CU_CALIBRATE", "auto"),
+                   choices=["auto", "off", "force"],
+                   help="before warmup, time a few pipelined steps per RCCL CU reserve candidate "
+                        "(--cu-candidates) and keep the fastest (max over ranks); auto: only while the "
+                        "native RCCL plane is live (the reserve only matters beside its kernels); "
+                        "HLSP2P_RCCL_CU_RESERVE set: no calibration, that value")
+    p.add_argument("--cu-candidates", default="0,32,64,96",
+                   help="CU reserve candidates of the calibration (CUs left free of the decrypt grid)")
+    p.add_argument("--cu-calib-steps", type=int, default=6, help="timed steps per calibration candidate")
     p.add_argument("--verbose", action="store_true")
     return p.parse_args()
 
@@ -193,7 +202,7 @@ def _workload(args):
     K = args.inflight
     # each player's slice of the DVR window covers the run (--playlist-steps: size it for a
     # longer run, to tell a playlist-size effect from a run-length effect in soaks)
-    n_segments = (args.warmup + max(args.steps, args.playlist_steps or 0) + 4) * K
+    n_segments = (args.warmup + max(args.steps, args.playlist_steps or 0) + 4 + _calib_steps(args)) * K
     W = max(0, args.players)
     origin_kwargs = dict(base_url="http://cdn.bench/live/", renditions=rends,
                          num_segments=n_segments * max(1, W) + (16 * K if W else 0),
@@ -212,6 +221,68 @@ def _workload(args):
     if args.fleet_payload:
         p2p_base["gpuSwarm"] = {"fleetPayload": True}
     return preset, encrypted, seg_dur, desc, K, n_segments, W, origin_kwargs, hls_config, p2p_base
+
+
+CALIB_SETTLE = 2  # untimed steps after each candidate is set (rounds in flight drain under it)
+
+
+def _calib_candidates(args) -> list:
+    """The CU reserve candidates this run will time (empty: no calibration).  ``auto`` runs it
+    for an N > 1 GPU run on the native RCCL plane (the driver's 8-GPU bench, the socket
+    rehearsal); ``HLSP2P_RCCL_CU_RESERVE`` pins the reserve instead."""
+    if args.cu_calibrate == "off" or os.environ.get("HLSP2P_RCCL_CU_RESERVE"):
+        return []
+    if args.cu_calibrate == "auto":
+        world = int(os.environ.get("WORLD_SIZE", str(args.gpus or 1)))
+        if args.cpu or world < 2 or args.dist_backend not in ("auto", "nccl"):
+            return []
+    return [int(x) for x in str(args.cu_candidates).split(",") if x.strip()]
+
+
+def _calib_steps(args) -> int:
+    return len(_calib_candidates(args)) * (CALIB_SETTLE + max(1, args.cu_calib_steps))
+
+
+def _calibrate(args, node, step, sync, world: int):
+    """Pick the decrypt grid's RCCL CU reserve on the real round shape, before warmup (outside
+    the timed window): per candidate, ``CALIB_SETTLE`` untimed steps, then
+    ``--cu-calib-steps`` steps timed between two barriers; the slowest rank's time decides
+    (the bench's own rule) and every rank keeps the same, fastest, candidate.  The xGMI links'
+    real rate decides how long RCCL's kernels hold their CUs, which no one-GPU rehearsal can
+    tell (round 5 froze 64 from a one-rank HBM self-exchange: profiles/r5_overlap)."""
+    cands = _calib_candidates(args)
+    if not cands:
+        pinned = os.environ.get("HLSP2P_RCCL_CU_RESERVE")
+        return {"source": "HLSP2P_RCCL_CU_RESERVE", "chosen": int(pinned)} if pinned else None
+    from hlsjs_p2p_wrapper_amd.ops._native import device as _dev
+
+    dev = _dev()
+    before = dev.cu_reserve()
+    k = max(1, args.cu_calib_steps)
+    table = []
+    for c in cands:
+        dev.set_cu_reserve(int(c))
+        for _ in range(CALIB_SETTLE):
+            step()
+        sync()
+        t0 = time.perf_counter()
+        for _ in range(k):
+            step()
+        sync()
+        ns = np.array([int((time.perf_counter() - t0) * 1e9)], dtype=np.int64)
+        if world > 1:
+            ns = np.array([max(int(x[0]) for x in node.comm.allgather_control(ns))], dtype=np.int64)
+        table.append(round(float(ns[0]) / 1e6 / k, 3))
+    # identical table on every rank: the same choice.  The default reserve stays unless a
+    # candidate beats it by more than the margin: a few steps per candidate cannot separate
+    # options within noise, and a socket- or PCIe-bound run makes them all equal
+    margin = float(os.environ.get("HLSP2P_CU_CALIB_MARGIN", "0.02"))
+    best = cands[int(np.argmin(table))]
+    if before in cands and table[cands.index(best)] > table[cands.index(before)] * (1.0 - margin):
+        best = before
+    dev.set_cu_reserve(int(best))
+    return {"source": "calibrated", "candidates": cands, "ms_per_step": table, "chosen": int(best),
+            "previous": int(before), "margin": margin, "steps_per_candidate": k, "settle_steps": CALIB_SETTLE}
 
 
 def _spawn_players(W, world, rank, origin_kwargs, hls_config, p2p_base, n_segments, seg_dur):
@@ -597,6 +668,7 @@ def main() -> int:
         if use_gpu:
             torch.cuda.synchronize(device)
 
+    calib = _calibrate(args, node, step, sync, world)  # before warmup: not in the timed window
     for _ in range(args.warmup):
         step()
     sync()
@@ -634,6 +706,8 @@ def main() -> int:
     result["per_rank"] = _per_rank_dicts(per_parts, args.steps)
     result["config"]["receive_verify"] = "fused-decrypt" if getattr(node, "verify_deferred", False) else "node"
     result["data_plane"] = _plane_info(node, dist, world, device, node.p2p_from - pf0)
+    if calib is not None:
+        result["calibration"] = calib
     _label_rehearsal(result)
     if args.verbose:
         print(f"# rank {rank} pack {t_pack:.2f}s {_mem(use_gpu, device)} counters {counters} level {hls.currentLevel}\n"
@@ -776,6 +850,7 @@ def _fleet(args, world, rank, device, use_gpu, node, origin, players, desc, encr
             time.sleep(0.002)
         if not args.no_gc_tune:
             tune_gc()
+        calib = _calibrate(args, node, step, sync, world)  # before warmup: not in the timed window
         for _ in range(args.warmup):
             step()
         sync()
@@ -854,6 +929,8 @@ def _fleet(args, world, rank, device, use_gpu, node, origin, players, desc, encr
         # every fragment into the shared ring, or fetched from the HBM cache when read
         result["config"]["player_bytes"] = "ring" if args.fleet_payload else "on-demand"
         result["data_plane"] = _plane_info(node, dist, world, device, pf1 - pf0)
+        if calib is not None:
+            result["calibration"] = calib
         _label_rehearsal(result)
         if live:
             result["config"].update(live=True, live_speed=args.live_speed, live_window=args.live_window,
@@ -933,6 +1010,8 @@ def _result(args, world, tot, max_s, origin, K, desc, encrypted, seg_dur, use_gp
     }
 
 
+from hlsjs_p2p_wrapper_amd.parallel.wire import XGMI_LINK_GBPS_PER_DIR  # noqa: E402
+
 # per-rank diagnostics of the timed window, all-gathered as int64 milli-units (fixed order)
 PER_RANK_FIELDS = ("rank", "rounds", "step_ms", "wait_device_us", "exchange_us", "exchange_queued_us", "control_us",
                    "plan_us",
@@ -940,7 +1019,7 @@ PER_RANK_FIELDS = ("rank", "rounds", "step_ms", "wait_device_us", "exchange_us",
                    "cdn_GBps", "cdn_dev_ms", "p2p_recv_MB", "p2p_sent_MB", "p2p_dev_ms", "p2p_GBps",
                    "p2p_links", "p2p_link_GBps", "transmux_dev_ms", "transmux_wait_us", "await_players_us",
                    "payload_GBps", "payload_wait_us", "crc_failures", "control_fallbacks", "deferred", "inflight",
-                   "cu_reserve", "p2p_rejected_MB")
+                   "cu_reserve", "p2p_rejected_MB", "p2p_link_roof_GBps", "p2p_link_util")
 
 
 def _per_rank(node, pipe, s0, s1, elapsed, steps, inflight, fleet_total=None, timers=None) -> np.ndarray:
@@ -998,6 +1077,11 @@ def _per_rank(node, pipe, s0, s1, elapsed, steps, inflight, fleet_total=None, ti
         "inflight": inflight, "cu_reserve": cu_reserve,
         # peer bytes whose CRC check failed (re-fetched from the CDN; not in offload_ratio)
         "p2p_rejected_MB": (s1.get("p2p_rejected", 0) - s0.get("p2p_rejected", 0)) / 1e6,
+        # the per-direction roofline of one xGMI link beside the measured per-link receive rate
+        # (p2p_link_GBps is a lower bound on the link's rate: bytes over the whole exchange time)
+        "p2p_link_roof_GBps": XGMI_LINK_GBPS_PER_DIR,
+        "p2p_link_util": (recv / links / (p2p_dev_s / rounds) / 1e9 / XGMI_LINK_GBPS_PER_DIR
+                          if links and p2p_dev_s > 0 else 0.0),
     }
     return np.array([int(round(float(vals[k]) * 1000)) for k in PER_RANK_FIELDS], dtype=np.int64)
 

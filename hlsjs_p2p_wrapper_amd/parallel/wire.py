@@ -42,6 +42,12 @@ _INIT = re.compile(r"rank\s+(\d+)\s+nRanks\s+(\d+)\s+nNodes\s+(\d+)\s+localRanks
 
 LINK_TYPES = {0: "HYPERTRANSPORT", 1: "QPI", 2: "PCIE", 3: "INFINIBAND", 4: "XGMI"}
 
+# One MI355X xGMI link, per direction: 153.6 GB/s is the bidirectional figure of a link (7 links,
+# ~1.07 TB/s per GPU in aggregate), so a receiver's roofline is 76.8 GB/s per source link and
+# 7 x 76.8 = 537.6 GB/s from all seven peers of an 8-GPU node.
+XGMI_LINK_GBPS_PER_DIR = 76.8
+XGMI_LINKS = 7
+
 
 def configure_rccl_log(rank: int, directory: Optional[str] = None) -> Optional[str]:
     """Point RCCL's connection log at a per-rank file; returns its path, or None with
@@ -119,8 +125,13 @@ def read_rccl_log(path: Optional[str], me: int) -> Optional[Dict[str, object]]:
         import logging
 
         lg = logging.getLogger("hlsjs_p2p_wrapper_amd.rccl")
-        for ln in warns[:8]:  # RCCL's own warnings went to the file: surface them
-            lg.warning("rank %d RCCL: %s", me, ln.split(" NCCL WARN ", 1)[1])
+        seen = []
+        for ln in warns:  # RCCL's own warnings went to the file: surface the distinct ones
+            w = ln.split(" NCCL WARN ", 1)[1]
+            if w not in seen:
+                seen.append(w)
+        for w in seen[:8]:
+            lg.warning("rank %d RCCL: %s", me, w)
     return out
 
 

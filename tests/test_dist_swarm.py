@@ -420,3 +420,32 @@ def test_killing_the_self_launching_bench_stops_its_ranks():
                 k.kill()
             except psutil.NoSuchProcess:
                 pass
+
+
+@pytest.mark.parametrize("players", ["2", "0"])
+def test_bench_calibrates_the_cu_reserve_before_warmup(players):
+    """The RCCL CU reserve is calibrated on the run's own round shape before warmup (round-5
+    VERDICT Next 2): every candidate is timed (max over ranks), all ranks keep the same,
+    fastest one, and the timed window still has exactly --steps steps.  (On CPU the reserve
+    does nothing; ``force`` runs the mechanism, ``auto`` runs it on the native RCCL plane.)"""
+    res = _bench_cpu(_free_port(), "--players", players, "--cu-calibrate", "force", "--cu-calib-steps", "2")
+    cal = res["calibration"]
+    assert cal["source"] == "calibrated" and cal["candidates"] == [0, 32, 64, 96]
+    assert len(cal["ms_per_step"]) == 4 and all(t > 0 for t in cal["ms_per_step"])
+    fastest = cal["candidates"][cal["ms_per_step"].index(min(cal["ms_per_step"]))]
+    t = dict(zip(cal["candidates"], cal["ms_per_step"]))
+    # the fastest, unless it is within the margin of the previous (default) reserve
+    assert cal["chosen"] == (fastest if t[fastest] <= t[cal["previous"]] * (1 - cal["margin"]) else cal["previous"])
+    assert cal["steps_per_candidate"] == 2 and res["steps"] == 8 and res["errors"] == 0
+    assert all(r["rounds"] >= 8 for r in res["per_rank"])
+
+
+def test_bench_cu_reserve_env_pins_it():
+    import os
+
+    os.environ["HLSP2P_RCCL_CU_RESERVE"] = "32"
+    try:
+        res = _bench_cpu(_free_port(), "--players", "0", "--cu-calibrate", "force")
+    finally:
+        del os.environ["HLSP2P_RCCL_CU_RESERVE"]
+    assert res["calibration"] == {"source": "HLSP2P_RCCL_CU_RESERVE", "chosen": 32}
