@@ -1704,7 +1704,7 @@ class SwarmNode:
             self._retry_cdn(self._vinfo[e], toks[toks >= 0])  # bulk (fleet) tokens: asked again here
             if e in self._vwait:
                 self._release_parked(e, False)
-            if (toks < 0).any():
+            if (toks <= -2).any():  # in-process request tokens (NO_TOKEN = -1: a node sweep)
                 # in-process requests were answered already: their players ask again, from the
                 # CDN.  (Bulk-only entries are re-fetched above; a key nobody will ask for again
                 # must not sit in the set: request_batch checks every key while it is non-empty)

@@ -142,8 +142,8 @@ std::mutex g_scratch_mu;
 bool group_by_window(const Want* in, size_t n, std::vector<uint32_t>* cnt_buf, Want* out) {
   constexpr int kTracks = 8;
   if (n < 16) return false;
-  SegKey tk[kTracks];
-  uint32_t lo[kTracks], hi[kTracks];
+  SegKey tk[kTracks]{};
+  uint32_t lo[kTracks]{}, hi[kTracks]{};
   int nt = 0, last = 0, prev_rank = -1;
   for (size_t i = 0; i < n; ++i) {
     const Want& w = in[i];
@@ -151,7 +151,7 @@ bool group_by_window(const Want* in, size_t n, std::vector<uint32_t>* cnt_buf, W
     prev_rank = w.rank;
     const SegKey& k = w.key;
     int t = last;
-    if (!(tk[t].swarm == k.swarm && tk[t].level == k.level && tk[t].url_id == k.url_id) || t >= nt) {
+    if (t >= nt || !(tk[t].swarm == k.swarm && tk[t].level == k.level && tk[t].url_id == k.url_id)) {
       for (t = 0; t < nt; ++t)
         if (tk[t].swarm == k.swarm && tk[t].level == k.level && tk[t].url_id == k.url_id) break;
       if (t == nt) {

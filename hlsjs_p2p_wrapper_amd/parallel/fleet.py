@@ -570,6 +570,8 @@ class _PayloadRing:
         self.live: "collections.deque" = collections.deque()  # [start, end, {player: batch no} | None]
         self.tensor = None
         self.pinned = False
+        if pin and os.environ.get("HLSP2P_FLEET_RING_PIN", "1") == "0":  # test hook: the fallback path
+            pin = False
         if pin:
             import torch
 
@@ -651,7 +653,10 @@ class FleetServer:
         self._payload = [False] * W
         self._ring: Optional[_PayloadRing] = None
         self._retired: List[_PayloadRing] = []  # replaced rings, closed once their regions are released
-        self._bounce = None  # pinned staging of an unpinned ring's batches
+        # pinned staging of an unpinned ring's batches: one buffer per batch in flight (batch
+        # N+1's D2H is queued before batch N's host copy runs), back to the pool after that copy
+        self._bounce_free: List[Any] = []
+        self.bounce_buffers = 0  # allocated so far (a pool the size of the batches in flight)
         self._pstream = None  # side stream of the payload gathers + D2H
         self.ring_ack_timeout_s = float(os.environ.get("HLSP2P_FLEET_ACK_TIMEOUT", "10"))
         self.revoked: set = set()  # players whose payloads were stopped (stalled on their acks)
@@ -999,13 +1004,12 @@ class FleetServer:
                 if ring.pinned:
                     ring.tensor[start:start + total].copy_(staged[:total], non_blocking=True)
                 else:  # registration failed: D2H into a pinned bounce buffer, host copy at completion
-                    if self._bounce is None or self._bounce.numel() < total:
-                        self._bounce = torch.empty(max(total, 64 << 20), dtype=torch.uint8, pin_memory=True)
-                    bounce = self._bounce
+                    bounce = self._take_bounce(total)
                     bounce[:total].copy_(staged[:total], non_blocking=True)
 
                     def post(buf=ring.buf, bounce=bounce, start=start, total=total):
                         buf[start:start + total] = bounce[:total].numpy()
+                        self._bounce_free.append(bounce)  # this batch's D2H has landed: reusable
                 ev = torch.cuda.Event()
                 ev.record(ps)
         else:
@@ -1013,6 +1017,16 @@ class FleetServer:
             for o, p, k in zip(offs[idx].tolist(), (start + pack).tolist(), n.tolist()):
                 buf[p:p + k] = host[o:o + k]
         return ring_off, region, ev, post
+
+    def _take_bounce(self, total: int):
+        """A pinned bounce buffer of at least ``total`` bytes that no batch in flight uses."""
+        import torch
+
+        for i, b in enumerate(self._bounce_free):
+            if b.numel() >= total:
+                return self._bounce_free.pop(i)
+        self.bounce_buffers += 1
+        return torch.empty(max(total, 64 << 20), dtype=torch.uint8, pin_memory=True)
 
     # -------------------------------------------------------------- payload ring
     def _acked(self, need) -> bool:

@@ -472,13 +472,20 @@ def test_bench_fleet_on_the_gpu():
 
 
 @pytest.mark.gpu
-def test_fleet_player_reads_fragment_bytes_on_the_gpu(cuda):
+@pytest.mark.parametrize("ring_pinned", [True, False])
+def test_fleet_player_reads_fragment_bytes_on_the_gpu(cuda, ring_pinned, monkeypatch):
     """A fleet player that asked for payloads (``gpuSwarm.fleetPayload``) reads each served
     fragment's bytes from ``onSuccess`` — copied from the rank's HBM arena into the shared
     payload ring — and they match the origin's bytes (CRC-32), the reference ``onSuccess``
-    contract (``lib/integration/p2p-loader-generator.js:92-99``)."""
+    contract (``lib/integration/p2p-loader-generator.js:92-99``).  ``ring_pinned=False``: the
+    ring's HIP registration "failed" (``HLSP2P_FLEET_RING_PIN=0``), so each batch goes D2H into
+    a pinned bounce buffer and is copied in on the host -- with two transmux batches in
+    flight, each on a bounce buffer of its own (one shared buffer let batch N+1's
+    D2H overwrite batch N's bytes before they were copied)."""
     import zlib
 
+    if not ring_pinned:
+        monkeypatch.setenv("HLSP2P_FLEET_RING_PIN", "0")
     clear_origins()
     set_current_node(None)
     loop = new_event_loop("real")
@@ -518,7 +525,7 @@ def test_fleet_player_reads_fragment_bytes_on_the_gpu(cuda):
             while loop._ready:
                 loop.run_once(block=False)
             server.poll()
-            server.admit(16)
+            server.admit(3)  # several answer batches: two transmux batches are in flight at once
             hs.append(node.launch_round())
             if len(hs) > 1:
                 node.complete_round(hs.popleft())
@@ -536,6 +543,9 @@ def test_fleet_player_reads_fragment_bytes_on_the_gpu(cuda):
             assert n == seg.numel()
             assert zlib.crc32(data.tobytes()) == crc == zlib.crc32(pool_data[off:off + n].numpy().tobytes())
             assert seg.transmux_result["plain_bytes"] == n  # clear segment: demuxed on the GPU
+        assert server._ring.pinned is ring_pinned
+        if not ring_pinned:
+            assert server.bounce_buffers >= 2  # batch N+1 staged while batch N awaited its host copy
     finally:
         player.close()
         server.close()

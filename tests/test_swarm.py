@@ -177,6 +177,9 @@ def test_deferred_check_of_a_dropped_fragment_is_swept_by_the_node():
     assert node._sweep_pending() == 2
     assert node.pending_verify() == 0 and node.stats["crc_failures"] == 1
     assert node.store.lookup1(3, 0, 0, 1) >= 0 and node.store.lookup1(3, 0, 0, 2) < 0
+    # nobody requested the swept copy: its key must not force a later request to the CDN
+    # (the sweep's NO_TOKEN (-1) was read as an in-process request)
+    assert not node._force_cdn_keys
 
 
 def test_a_late_ticket_report_after_the_sweep_is_ignored():
