@@ -325,16 +325,30 @@ class SwarmNode:
         self._tick_scheduled = False
         self._timer = None
         self._pins: List[Tuple[int, np.ndarray]] = []  # (release at launch #, entry ids)
+        # pin / token ledgers the audit (agent/audit.py) balances against the store's pins:
+        # rounds launched and not completed, cache hits waiting for _serve_local, delayed
+        # deliveries (entry ids, tokens), and outside holders (a fleet's batches) as callables
+        self._inflight: Dict[int, RoundHandle] = {}
+        self._local_hits: Dict[int, int] = {}
+        self._delayed: Dict[int, Tuple[np.ndarray, np.ndarray]] = {}
+        self._delayed_seq = 0
+        self.pin_holders: List[Any] = []  # callables -> entry ids they hold one pin on each
+        self.expect_holders: List[Any] = []  # callables -> entry ids delivered with an expected CRC
+        # HLSP2P_AUDIT=1 / gpuSwarm.audit: check the replicated-state invariants after every
+        # launch_round and complete_round (agent/audit.py); on in the whole test suite
+        self.audit_on = os.environ.get("HLSP2P_AUDIT", "0") == "1"
         self._agents: List[Any] = []
         self._prefetched: Dict[Tuple[int, int, int, int], str] = {}  # key -> "cdn" | "p2p"
         self._net_wants = False  # some want came from a network origin (plans may carry STAGE rows)
         self.peer_online = np.ones(self.world, dtype=bool)
-        # "p2p" / "p2p_segments": peer bytes / segments that PASSED their CRC check (counted when
-        # the check ran: in complete_round, or in verify_done for a check deferred to the
-        # consumer's decrypt); a rejected copy counts in "p2p_rejected" and its CDN re-fetch in
-        # "cdn", so cdn + p2p is what the players were served, and offload = p2p / (cdn + p2p)
-        # stays exact under corruption.  Wire-level: "p2p_wire" (every byte received, checked or
-        # not) and "p2p_links" ((round, source peer) pairs received from): link rates
+        # "p2p" / "p2p_segments": peer copies delivered whose CRC check passed, counted when
+        # they are delivered (complete_round: the node's own check, or -- for a check deferred
+        # to the consumer's decrypt -- provisionally, moved to "p2p_rejected" by verify_done
+        # if it fails).  A copy that fails is never counted as delivered P2P: it counts in
+        # "p2p_rejected" and its CDN re-fetch in "cdn", so cdn + p2p is what the players were
+        # served and offload = p2p / (cdn + p2p) is exact under corruption (counting at
+        # delivery keeps P2P and CDN bytes on the same clock for a timed window).  Wire-level:
+        # "p2p_wire" (every byte received) and "p2p_links" ((round, source peer) pairs): link rates
         self.stats = {"cdn": 0, "p2p": 0, "upload": 0, "cache": 0, "rounds": 0, "crc_failures": 0,
                       "segments": 0, "cdn_segments": 0, "p2p_segments": 0, "prefetched": 0,
                       "p2p_links": 0, "p2p_wire": 0, "p2p_rejected": 0, "p2p_rejected_segments": 0}
@@ -563,6 +577,7 @@ class SwarmNode:
         eid = self.store.lookup1(*k)
         if eid >= 0:  # local cache hit
             self.store.pin(np.array([eid], dtype=np.int64))
+            self._local_hits[eid] = self._local_hits.get(eid, 0) + 1
             self.loop.call_soon(self._serve_local, req, eid)
             return req
         if self._prefetched:
@@ -780,6 +795,11 @@ class SwarmNode:
             self._deliver_req(req, src or "cache", n, 0.0, 0.0, self.arena[off:off + n], -1, eid)
         finally:
             self.store.unpin(np.array([eid], dtype=np.int64))
+            n = self._local_hits.get(eid, 0) - 1
+            if n > 0:
+                self._local_hits[eid] = n
+            else:
+                self._local_hits.pop(eid, None)
 
     def _park_on_pending(self, keys: np.ndarray, tokens: np.ndarray, miss: Optional[np.ndarray]) -> np.ndarray:
         """Requests (rows ``miss`` of ``keys``; all when None) for segments whose received copy
@@ -911,6 +931,22 @@ class SwarmNode:
     def launch_round(self) -> RoundHandle:
         """Collective: exchange control messages, plan, and ENQUEUE this round's device
         work (CDN copies, ingest CRC, RCCL transfers, verify CRC).  Host does not wait."""
+        h = self._launch_round()
+        if self.audit_on:
+            from .audit import audit_node
+
+            audit_node(self, "launch_round")
+        return h
+
+    def complete_round(self, h: RoundHandle) -> None:
+        """Local: wait for the round's device work, verify, commit and deliver."""
+        self._complete_round(h)
+        if self.audit_on:
+            from .audit import audit_node
+
+            audit_node(self, "complete_round")
+
+    def _launch_round(self) -> RoundHandle:
         rt = self.rt
         t0 = time.perf_counter()
         self.round += 1
@@ -957,6 +993,10 @@ class SwarmNode:
             # checked: if they would cross the ring's end, the ring wraps before the first
             if not self.store.wrap_for(need):
                 raise RuntimeError("segment cache cannot wrap for the round (pinned entries block eviction)")
+            if self.audit_on:
+                from .audit import check_region
+
+                check_region(self, need)
         adds, rms = self.store.take_delta()
         try:
             parts = self.comm.allgather_control(self._encode(rows, adds, rms))
@@ -974,6 +1014,7 @@ class SwarmNode:
         self.swarm_stats = {"cdn": int(swarm_tot[0]), "p2p": int(swarm_tot[1]), "upload": int(swarm_tot[2])}
         h = RoundHandle(self.round, all_leaving, t0=t0)
         h.ids = ids
+        self._inflight[h.round] = h
         t_ctrl = time.perf_counter()
         self.timer.add("control", t_ctrl - t0)
         if not len(all_wants):  # (every rank sees the same want rows: all skip planning alike)
@@ -1037,11 +1078,11 @@ class SwarmNode:
         self.timer.add("p2p_enqueue", time.perf_counter() - t_p2p0)
         return h
 
-    def complete_round(self, h: RoundHandle) -> None:
-        """Local: wait for the round's device work, verify, commit and deliver."""
+    def _complete_round(self, h: RoundHandle) -> None:
         if h.completed:
             return
         h.completed = True
+        self._inflight.pop(h.round, None)
         if h.empty:
             self.last_round = {"wants": 0, "ms": (time.perf_counter() - h.t0) * 1e3}
             if h.ids is not None and len(h.ids):  # (a lone rank's wants always plan: defensive)
@@ -1091,13 +1132,14 @@ class SwarmNode:
             commit = good[2] if dgood is None else good[2][~dgood]
             if len(commit):
                 self.store.commit(commit)
-                # checked by the node's verify CRC (rows deferred to their consumer count when
-                # their check comes back: _settle_deferred / verify_done)
-                self._count_p2p(good[4] if dgood is None else good[4][~dgood], True)
+            # delivered now: checked by the node's verify CRC, or deferred to the consumer
+            # (a deferred copy that fails later is moved to p2p_rejected: _settle_deferred /
+            # verify_done)
+            self._count_p2p(good[4], True)
             if bad is not None:
                 self.store.drop(bad[2])
                 self.stats["crc_failures"] += len(bad[0])
-                self._count_p2p(bad[4], False)
+                self._count_p2p(bad[4], False)  # never delivered
         if h.send_pins is not None:
             self.store.unpin(h.send_pins)
         for x in h.release:  # the round's DMAs are done: drop the staged host copies
@@ -1108,6 +1150,10 @@ class SwarmNode:
         # ---- deliveries: served wants leave the table, their tokens come back as columns
         if h.cdn is not None and len(h.cdn[0]):
             wids, eids, offs, lens = h.cdn[0], h.cdn[1], h.cdn[2], h.cdn[3]
+            # CDN and P2P bytes both count when the round delivers them (one clock for a timed
+            # window's offload ratio)
+            self.stats["cdn"] += int(lens.sum())
+            self.stats["cdn_segments"] += len(wids)
             tok, idx, pf = wt.finish(wids)
             self._after_finish(wids, pf, h.cdn[4], "cdn")
             cdn_ms = max(h.cdn_ms, h.shaped_ms)
@@ -1388,9 +1434,7 @@ class SwarmNode:
         # transfer time of this round's CDN bytes
         total = int(lens.sum())
         h.shaped_ms = http.Shaper.transfer_ms(total)
-        self.stats["cdn"] += total
-        self.stats["cdn_segments"] += len(wids)
-        h.cdn = (wids, eids, offs, lens, keys)
+        h.cdn = (wids, eids, offs, lens, keys)  # counted in stats["cdn"] at delivery (complete_round)
 
     def _p2p_phase(self, h: RoundHandle, send_rows: np.ndarray, recv_rows: np.ndarray,
                    send_eids: np.ndarray) -> None:
@@ -1554,12 +1598,11 @@ class SwarmNode:
                 ok_now = _crc.crc32_batch(self.arena, offs[nr], lens[nr], expect=exp)[1].numpy().astype(bool)
             if ok_now.any():
                 self.store.commit(eids[nr[ok_now]])
-                self._count_p2p(lens[nr[ok_now]], True)
             bad = nr[~ok_now]
             if len(bad):
                 self.store.drop(eids[bad])
                 self.stats["crc_failures"] += len(bad)
-                self._count_p2p(lens[bad], False)
+                self._reject_p2p(lens[bad])
                 keep = np.ones(len(tok), dtype=bool)
                 for r in bad.tolist():
                     sel = idx == r
@@ -1578,9 +1621,9 @@ class SwarmNode:
         return tok, idx, exp_row[idx]
 
     def _count_p2p(self, lens: np.ndarray, passed: bool) -> None:
-        """Account peer copies whose CRC check just ran: delivered P2P bytes when it passed,
-        rejected bytes when it failed (the segment is then re-fetched, and counted, from the
-        CDN)."""
+        """Account peer copies: delivered P2P bytes (``passed``), or rejected bytes of copies
+        that failed their CRC check before delivery (the segment is then re-fetched, and
+        counted, from the CDN)."""
         n = len(lens)
         if not n:
             return
@@ -1591,6 +1634,17 @@ class SwarmNode:
         else:
             self.stats["p2p_rejected"] += b
             self.stats["p2p_rejected_segments"] += n
+
+    def _reject_p2p(self, lens: np.ndarray) -> None:
+        """Copies counted as delivered P2P whose deferred check failed: P2P -> rejected."""
+        n = len(lens)
+        if not n:
+            return
+        b = int(np.asarray(lens, dtype=np.int64).sum())
+        self.stats["p2p"] -= b
+        self.stats["p2p_segments"] -= n
+        self.stats["p2p_rejected"] += b
+        self.stats["p2p_rejected_segments"] += n
 
     def _vpend_add(self, eids: np.ndarray, info: np.ndarray, expect: np.ndarray) -> None:
         need = int(eids.max()) + 1
@@ -1686,7 +1740,6 @@ class SwarmNode:
             self._vflag[good] = False
             self.store.commit(good)
             self.store.unpin(good)
-            self._count_p2p(self._vinfo[good, 4], True)
             if self._vwait:
                 for e in good.tolist():
                     if e in self._vwait:
@@ -1699,7 +1752,7 @@ class SwarmNode:
             self.store.detach(arr)
             self.store.unpin(arr)
             self.stats["crc_failures"] += 1
-            self._count_p2p(self._vinfo[e:e + 1, 4], False)
+            self._reject_p2p(self._vinfo[e:e + 1, 4])
             toks = tokens[inv == k]
             self._retry_cdn(self._vinfo[e], toks[toks >= 0])  # bulk (fleet) tokens: asked again here
             if e in self._vwait:
@@ -1728,10 +1781,12 @@ class SwarmNode:
                 le = le[le >= 0]
                 if len(le):
                     self.store.pin(le)
+                self._delayed_seq += 1
+                self._delayed[self._delayed_seq] = (le, tok[li])
                 self.loop.set_timeout(self._deliver_deferred, float(d[li].max()),
                                       (tok[li], src[li], nbytes[li], cdn_ms[li], p2p_ms[li], offs[li], eids[li],
                                        None if peers is None else peers[li], None,
-                                       None if expect is None else expect[li]), le)
+                                       None if expect is None else expect[li]), le, self._delayed_seq)
                 if later.all():
                     return
                 ni = np.flatnonzero(~later)
@@ -1768,7 +1823,8 @@ class SwarmNode:
             self._deliver_req(r, SOURCE_NAMES[int(src[i])], int(nbytes[i]), float(cdn_ms[i]), float(p2p_ms[i]), view,
                               self.rank if peers is None else int(peers[i]), int(eids[i]), pin=False)
 
-    def _deliver_deferred(self, cols, ids: np.ndarray) -> None:
+    def _deliver_deferred(self, cols, ids: np.ndarray, seq: int = 0) -> None:
+        self._delayed.pop(seq, None)
         try:
             self._deliver_cols(*cols)
         finally:
@@ -1967,6 +2023,8 @@ def node_for_config(p2p_config: Any) -> SwarmNode:
         from ..utils.runtime import bind_to_gpu_numa
 
         bind_to_gpu_numa(node.device.index if node.device.index is not None else torch.cuda.current_device())
+    if cfg.get("audit"):
+        node.audit_on = True
     if cfg.get("roundTimeoutMs") is not None:
         node.round_timeout_s = float(cfg["roundTimeoutMs"]) / 1e3
     if cfg.get("controlTimeoutMs") is not None and hasattr(comm, "control_timeout_s"):

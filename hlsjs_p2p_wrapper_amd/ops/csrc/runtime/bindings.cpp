@@ -432,6 +432,60 @@ PYBIND11_MODULE(_runtime, m) {
         return py::make_tuple(as2d(srun, 6), as2d(gath, 4), as2d(rrun, 5), rid, roff);
       })
       .def("fits", &SegmentStore::fits)
+      // ---- replicated-state audit (agent/audit.py)
+      .def("audit", [](const SegmentStore& s) {
+        std::vector<std::string> e;
+        s.audit(&e);
+        return e;
+      })
+      .def_property_readonly("unpin_underflows", &SegmentStore::unpin_underflows)
+      .def("region_start", &SegmentStore::region_start)
+      .def("pin_table", [](const SegmentStore& s) {
+        // -> (ids int64[n], pins int64[n]) of live entries holding pins
+        std::vector<int64_t> ids, pins;
+        for (int64_t i = 0; i < s.max_entries(); ++i) {
+          const Entry& e = s.entry(i);
+          if (e.state != kFree && e.pins != 0) {
+            ids.push_back(i);
+            pins.push_back(e.pins);
+          }
+        }
+        Arr<int64_t> a(static_cast<py::ssize_t>(ids.size())), b(static_cast<py::ssize_t>(pins.size()));
+        if (!ids.empty()) {
+          std::memcpy(a.mutable_data(), ids.data(), ids.size() * sizeof(int64_t));
+          std::memcpy(b.mutable_data(), pins.data(), pins.size() * sizeof(int64_t));
+        }
+        return py::make_tuple(a, b);
+      })
+      .def("live_entries", [](const SegmentStore& s) {
+        // -> int64[n, 9]: id, key x4, offset, alloc bytes, state, indexed (the index names it)
+        std::vector<int64_t> rows;
+        for (int64_t i = 0; i < s.max_entries(); ++i) {
+          const Entry& e = s.entry(i);
+          if (e.state == kFree) continue;
+          const int64_t ix = s.lookup(e.key, true);
+          rows.insert(rows.end(), {i, int64_t(e.key.swarm), int64_t(e.key.level), int64_t(e.key.url_id),
+                                   int64_t(e.key.sn), e.offset, e.alloc_bytes, int64_t(e.state), ix == i ? 1 : 0});
+        }
+        const int64_t n = static_cast<int64_t>(rows.size() / 9);
+        Arr<int64_t> out({n, int64_t(9)});
+        if (n) std::memcpy(out.mutable_data(), rows.data(), rows.size() * sizeof(int64_t));
+        return out;
+      })
+      .def("peek_delta", [](const SegmentStore& s) {
+        // -> (added int64[n,4], removed int64[m,4]) not taken yet
+        std::vector<SegKey> add, rm;
+        s.peek_delta(&add, &rm);
+        auto keys = [](const std::vector<SegKey>& v) {
+          Arr<int64_t> a({int64_t(v.size()), int64_t(4)});
+          int64_t* p = a.mutable_data();
+          for (size_t i = 0; i < v.size(); ++i) {
+            p[4 * i] = v[i].swarm; p[4 * i + 1] = v[i].level; p[4 * i + 2] = v[i].url_id; p[4 * i + 3] = v[i].sn;
+          }
+          return a;
+        };
+        return py::make_tuple(keys(add), keys(rm));
+      })
       .def("wrap_for", &SegmentStore::wrap_for)
       .def("retire_region", &SegmentStore::retire_region)
       .def("resident", [](const SegmentStore& s) {
@@ -494,6 +548,19 @@ PYBIND11_MODULE(_runtime, m) {
         for (int64_t i = 0; i < removes.size() / 4; ++i) d.apply_remove(rank, key_from(removes.data() + 4 * i));
       })
       .def("drop_rank", &Directory::drop_rank)
+      .def("holder_keys", [](const Directory& d, int rank) {
+        // -> int64[n, 5]: key x4, length of the entries `rank` holds
+        std::vector<SegKey> k;
+        std::vector<int64_t> l;
+        d.holder_keys(rank, &k, &l);
+        Arr<int64_t> out({int64_t(k.size()), int64_t(5)});
+        int64_t* p = out.mutable_data();
+        for (size_t i = 0; i < k.size(); ++i) {
+          p[5 * i] = k[i].swarm; p[5 * i + 1] = k[i].level; p[5 * i + 2] = k[i].url_id; p[5 * i + 3] = k[i].sn;
+          p[5 * i + 4] = l[i];
+        }
+        return out;
+      })
       .def("holders", [](const Directory& d, uint32_t swarm, uint32_t level, uint32_t url_id, uint32_t sn) {
         const DirEntry* e = d.find(SegKey{swarm, level, url_id, sn});
         return e ? e->holders : uint64_t(0);
@@ -797,7 +864,30 @@ PYBIND11_MODULE(_runtime, m) {
         return py::make_tuple(a, b, c);
       })
       .def("requeue", [](WantTable& t, Arr<int64_t> ids, bool force_cdn) { t.requeue(ids.data(), ids.size(), force_cdn); },
-           py::arg("ids"), py::arg("force_cdn") = false);
+           py::arg("ids"), py::arg("force_cdn") = false)
+      .def("audit", [](const WantTable& t) {
+        std::vector<std::string> e;
+        t.audit(&e);
+        return e;
+      })
+      .def("ids", [](const WantTable& t) {
+        std::vector<int64_t> v;
+        t.ids(&v);
+        Arr<int64_t> a(static_cast<py::ssize_t>(v.size()));
+        if (!v.empty()) std::memcpy(a.mutable_data(), v.data(), v.size() * sizeof(int64_t));
+        return a;
+      })
+      .def("token_map", [](const WantTable& t) {
+        // -> (tokens int64[n], want ids int64[n])
+        std::vector<int64_t> tk, w;
+        t.token_map(&tk, &w);
+        Arr<int64_t> a(static_cast<py::ssize_t>(tk.size())), b(static_cast<py::ssize_t>(w.size()));
+        if (!tk.empty()) {
+          std::memcpy(a.mutable_data(), tk.data(), tk.size() * sizeof(int64_t));
+          std::memcpy(b.mutable_data(), w.data(), w.size() * sizeof(int64_t));
+        }
+        return py::make_tuple(a, b);
+      });
   m.attr("WANT_FORCE_CDN") = int64_t(kWForceCdn);
   m.attr("WANT_NOT_STAGED") = int64_t(kWNotStaged);
   m.attr("WANT_STAGING") = int64_t(kWStaging);

@@ -94,6 +94,14 @@ class Directory {
   void drop_rank(int rank);  // a rank left: forget everything it held
   const DirEntry* find(const SegKey& k) const;
   int64_t size() const { return size_; }
+  // Keys (and lengths) `rank` is a holder of (the audit's view of what peers believe it holds).
+  void holder_keys(int rank, std::vector<SegKey>* keys, std::vector<int64_t>* lens) const {
+    for (const Slot& s : slots_)
+      if ((s.e.holders >> rank) & 1u) {
+        keys->push_back(s.key);
+        lens->push_back(s.e.length);
+      }
+  }
   // Order-independent 64-bit digest of the whole content (every key with its holder mask
   // and length), kept up to date by every add / remove in O(1).  Every rank replays the same
   // deltas into its replica, so the replicas' digests must agree at every round; ranks

@@ -1,6 +1,7 @@
 #include "store.hpp"
 
 #include <algorithm>
+#include <sstream>
 #include <stdexcept>
 
 namespace hlsp2p {
@@ -248,6 +249,77 @@ void SegmentStore::all_resident(std::vector<SegKey>* keys, std::vector<int64_t>*
       lens->push_back(e.length);
     }
   }
+}
+
+void SegmentStore::audit(std::vector<std::string>* errors) const {
+  auto err = [&](const std::string& m) {
+    if (errors->size() < 64) errors->push_back(m);
+  };
+  const int64_t n = static_cast<int64_t>(entries_.size());
+  int64_t used = 0, live = 0;
+  for (int64_t id = 0; id < n; ++id) {
+    const Entry& e = entries_[id];
+    if (e.state == kFree) continue;
+    ++live;
+    used += e.alloc_bytes;
+    if (e.state != kPending && e.state != kResident) err("entry " + std::to_string(id) + " in state " + std::to_string(e.state));
+    if (e.pins < 0) err("entry " + std::to_string(id) + " has " + std::to_string(e.pins) + " pins");
+    if (e.offset < 0 || e.alloc_bytes < aligned(e.length) || e.offset + e.alloc_bytes > capacity_) {
+      std::ostringstream o;
+      o << "entry " << id << " out of the ring: offset " << e.offset << " alloc " << e.alloc_bytes << " length "
+        << e.length << " capacity " << capacity_;
+      err(o.str());
+    }
+  }
+  if (used != used_) err("used bytes " + std::to_string(used_) + " != sum of live allocations " + std::to_string(used));
+  if (unpin_underflows_) err(std::to_string(unpin_underflows_) + " unpins of live entries that held no pin");
+  // the index names live entries under their own keys
+  for (const auto& kv : index_) {
+    const int64_t id = kv.second;
+    if (id < 0 || id >= n) {
+      err("index names entry id " + std::to_string(id) + " out of range");
+      continue;
+    }
+    const Entry& e = entries_[id];
+    if (e.state == kFree) err("index names free entry " + std::to_string(id));
+    if (!(e.key == kv.first)) err("index key of entry " + std::to_string(id) + " differs from the entry's key");
+  }
+  // every live entry is in the FIFO exactly once (current generation), and the FIFO's live
+  // records lie in allocation order around the ring: at most one wrap, no overlap
+  std::vector<int> seen(static_cast<size_t>(n), 0);
+  int64_t prev_end = -1, first_off = -1, wraps = 0;
+  for (const auto& fe : fifo_) {
+    const int64_t id = fe.first;
+    if (id < 0 || id >= n) {
+      err("FIFO names entry id " + std::to_string(id) + " out of range");
+      continue;
+    }
+    const Entry& e = entries_[id];
+    if (e.state == kFree || e.gen != fe.second) continue;  // stale record
+    seen[static_cast<size_t>(id)] += 1;
+    if (first_off < 0) first_off = e.offset;
+    if (prev_end >= 0 && e.offset < prev_end) {  // the allocation wrapped to the ring's start
+      wraps += 1;
+      if (wraps > 1) err("FIFO wraps the ring more than once (entry " + std::to_string(id) + ")");
+    }
+    if (wraps == 1 && e.offset + e.alloc_bytes > first_off) {  // after the wrap: below the oldest
+      std::ostringstream o;
+      o << "FIFO: entry " << id << " ends at " << e.offset + e.alloc_bytes << " past the oldest live entry at "
+        << first_off;
+      err(o.str());
+    }
+    prev_end = e.offset + e.alloc_bytes;
+  }
+  int64_t in_fifo = 0;
+  for (int64_t id = 0; id < n; ++id) {
+    if (entries_[id].state == kFree) continue;
+    if (seen[static_cast<size_t>(id)] != 1)
+      err("live entry " + std::to_string(id) + " appears " + std::to_string(seen[static_cast<size_t>(id)]) +
+          " times in the FIFO");
+    in_fifo += seen[static_cast<size_t>(id)];
+  }
+  (void)live;
+  (void)in_fifo;
 }
 
 }  // namespace hlsp2p

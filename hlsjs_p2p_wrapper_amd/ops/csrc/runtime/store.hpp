@@ -13,6 +13,7 @@
 #include <cstdint>
 #include <cstddef>
 #include <deque>
+#include <string>
 #include <utility>
 #include <unordered_map>
 #include <vector>
@@ -107,8 +108,29 @@ class SegmentStore {
   void detach(int64_t id);
   void pin(int64_t id) { entries_[id].pins += 1; }
   void unpin(int64_t id) {
-    if (entries_[id].pins > 0) entries_[id].pins -= 1;
+    Entry& e = entries_[id];
+    if (e.pins > 0) {
+      e.pins -= 1;
+    } else if (e.state != kFree) {
+      // a live entry unpinned more often than pinned: some holder gave up a pin it did not
+      // own (the entry may already have been overwritten under another holder).  Clamped as
+      // before, but counted: the audit reports any (a free entry's unpin is the normal end of
+      // a pin on an entry dropped meanwhile, e.g. a received copy that failed its CRC)
+      unpin_underflows_ += 1;
+    }
   }
+  int64_t unpin_underflows() const { return unpin_underflows_; }
+  // Replicated-state audit (HLSP2P_AUDIT, agent/audit.py): the layout invariants of the ring,
+  // index and FIFO, appended as messages (empty: consistent).  O(entries); diagnostics only.
+  void audit(std::vector<std::string>* errors) const;
+  // The delta log not taken yet (what the next control message will announce).
+  void peek_delta(std::vector<SegKey>* added, std::vector<SegKey>* removed) const {
+    *added = delta_add_;
+    *removed = delta_rm_;
+  }
+  // Ring region a reservation of `total` bytes at the head would occupy now (the region
+  // fits() walks): [start, start + total).
+  int64_t region_start(int64_t total) const { return head_ + total > capacity_ ? 0 : head_; }
   // Drop resident, unpinned entries of `swarm` (all tracks) with sn < min_sn.
   int64_t evict_below(uint32_t swarm, uint32_t min_sn);
 
@@ -128,6 +150,7 @@ class SegmentStore {
   int64_t head_ = 0;
   int64_t used_ = 0;
   int64_t evictions_ = 0;
+  int64_t unpin_underflows_ = 0;
   std::vector<Entry> entries_;
   std::vector<int64_t> free_ids_;
   std::deque<std::pair<int64_t, uint64_t>> fifo_;  // (entry id, gen) in allocation order

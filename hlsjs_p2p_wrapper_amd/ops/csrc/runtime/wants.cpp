@@ -2,6 +2,7 @@
 
 #include <algorithm>
 #include <stdexcept>
+#include <unordered_set>
 
 namespace hlsp2p {
 
@@ -210,6 +211,66 @@ int64_t WantTable::waiting() const {
   for (const auto& kv : recs_)
     if (kv.second.round < 0 && !(kv.second.flags & kWStaging)) ++n;
   return n;
+}
+
+void WantTable::audit(std::vector<std::string>* errors) const {
+  auto err = [&](const std::string& m) {
+    if (errors->size() < 64) errors->push_back(m);
+  };
+  for (const auto& kv : index_) {
+    auto it = recs_.find(kv.second);
+    if (it == recs_.end()) {
+      err("index names unknown want " + std::to_string(kv.second));
+    } else if (!(it->second.key == kv.first)) {
+      err("index key of want " + std::to_string(kv.second) + " differs from the want's key");
+    }
+  }
+  std::unordered_set<int64_t> in_order(order_.begin(), order_.end());
+  for (const auto& kv : recs_) {
+    const WantRec& r = kv.second;
+    if (r.id != kv.first) err("want " + std::to_string(kv.first) + " records id " + std::to_string(r.id));
+    auto ix = index_.find(r.key);
+    if (ix == index_.end() || ix->second != kv.first) err("want " + std::to_string(kv.first) + " is not indexed by its key");
+    if (!in_order.count(kv.first)) err("want " + std::to_string(kv.first) + " is missing from the creation order");
+    if (kv.first >= next_id_) err("want id " + std::to_string(kv.first) + " >= next id");
+    std::unordered_set<int64_t> w;
+    for (int64_t t : r.waiters) {
+      if (!w.insert(t).second) err("token " + std::to_string(t) + " waits twice on want " + std::to_string(kv.first));
+      auto tt = token_.find(t);
+      if (tt == token_.end()) {
+        err("waiter " + std::to_string(t) + " of want " + std::to_string(kv.first) + " is not in the token map");
+      } else if (tt->second != kv.first) {
+        err("waiter " + std::to_string(t) + " of want " + std::to_string(kv.first) + " maps to want " +
+            std::to_string(tt->second));
+      }
+    }
+  }
+  for (const auto& kv : token_) {
+    auto it = recs_.find(kv.second);
+    if (it == recs_.end()) {
+      err("token " + std::to_string(kv.first) + " maps to unknown want " + std::to_string(kv.second));
+      continue;
+    }
+    const auto& w = it->second.waiters;
+    if (std::count(w.begin(), w.end(), kv.first) != 1)
+      err("token " + std::to_string(kv.first) + " is not a waiter of its want " + std::to_string(kv.second));
+  }
+}
+
+void WantTable::ids(std::vector<int64_t>* out) const {
+  out->clear();
+  out->reserve(recs_.size());
+  for (const auto& kv : recs_) out->push_back(kv.first);
+  std::sort(out->begin(), out->end());
+}
+
+void WantTable::token_map(std::vector<int64_t>* tokens, std::vector<int64_t>* wants) const {
+  tokens->clear();
+  wants->clear();
+  for (const auto& kv : token_) {
+    tokens->push_back(kv.first);
+    wants->push_back(kv.second);
+  }
 }
 
 }  // namespace hlsp2p

@@ -13,6 +13,7 @@
 #pragma once
 #include <cstdint>
 #include <deque>
+#include <string>
 #include <unordered_map>
 #include <vector>
 
@@ -80,6 +81,13 @@ class WantTable {
   // Back to waiting (announced but not served: kWHeld from now on); `force_cdn`: next time
   // from the CDN (+1 attempt).
   void requeue(const int64_t* ids, int64_t n, bool force_cdn);
+
+  // Replicated-state audit (agent/audit.py): index <-> records, token map <-> waiter lists,
+  // creation order covers every record; messages appended (empty: consistent).
+  void audit(std::vector<std::string>* errors) const;
+  // Every want id; every live token with its want id.
+  void ids(std::vector<int64_t>* out) const;
+  void token_map(std::vector<int64_t>* tokens, std::vector<int64_t>* wants) const;
 
   int64_t size() const { return static_cast<int64_t>(recs_.size()); }
   int64_t waiting() const;  // wants not in flight and not being downloaded

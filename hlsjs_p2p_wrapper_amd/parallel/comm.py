@@ -265,9 +265,9 @@ class DistComm(SwarmComm):
             return None
         # every rank must agree on the rehearsal mode: a rank that skips the duplicate-device
         # check below while another raises would leave the others blocked in the next collective
-        modes = sorted({str(f[3]) for f in flags})  # type: ignore[index]
-        if len(modes) > 1:
-            raise RuntimeError(f"ranks disagree on HLSP2P_RCCL_REHEARSAL: {[f[3] for f in flags]}")  # type: ignore[index]
+        modes = [f[3] for f in flags]  # type: ignore[index]
+        if len(set(modes)) > 1:
+            raise RuntimeError(f"ranks disagree on HLSP2P_RCCL_REHEARSAL: {modes}")
         self.peer_devices = {r: (f[1], f[2], f[4]) for r, f in enumerate(flags)}  # type: ignore[index]
         # one GPU per rank: RCCL cannot place two ranks of a communicator on one device (it
         # fails deep inside ncclCommInitRank, or worse, a launcher mapped ranks onto a shared

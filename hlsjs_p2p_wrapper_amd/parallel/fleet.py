@@ -676,7 +676,13 @@ class FleetServer:
         # batch, so RemoteSegment.data() in its onSuccess finds them cached: per player
         # (answer batch number, time sent, entry ids, their keys)
         self._holds: List["collections.deque"] = [collections.deque() for _ in range(W)]
+        # transmux batches launched and not completed: their delivered entries (deliver's pin)
+        # and those delivered with an expected CRC (the node's audit balances both)
+        self._tx_inflight: Dict[int, Tuple[np.ndarray, np.ndarray]] = {}
         node.set_bulk_sink(self)
+        if hasattr(node, "pin_holders"):
+            node.pin_holders.append(self._pinned_entries)
+            node.expect_holders.append(self._expect_entries)
         # segments received from peers are CRC-checked by the transmux that decrypts them (the
         # CRC fused into the AES kernel), not by a separate read in the node's round: results
         # of a copy that fails go to no player, the node asks the CDN again (verify_done)
@@ -685,6 +691,25 @@ class FleetServer:
         self.verify_failures = 0
         self.bytes_fetched = 0  # segment bytes sent to players on demand (RemoteSegment.data)
         self._fetches: List[tuple] = []  # on-demand copies in flight, answered in order
+
+    # -------------------------------------------------------------- audit ledgers
+    def _pinned_entries(self) -> np.ndarray:
+        """Entry ids this server holds one pin on each (agent/audit.py): delivered and not
+        transmuxed yet, in a transmux batch in flight, answered to an on-demand player that has
+        not handled the batch yet, or being copied for an on-demand fetch."""
+        parts = [it[6] for it in self._delivered]
+        parts += [p for p, _ in self._tx_inflight.values()]
+        parts += [h[2] for q in self._holds for h in q]
+        parts += [f[4] for f in self._fetches]
+        return np.concatenate([np.asarray(p, dtype=np.int64).reshape(-1) for p in parts]) if parts else \
+            np.zeros(0, dtype=np.int64)
+
+    def _expect_entries(self) -> np.ndarray:
+        """Entries delivered with an expected CRC whose check has not been reported yet."""
+        parts = [it[6][np.asarray(it[7]) >= 0] for it in self._delivered]
+        parts += [e for _, e in self._tx_inflight.values()]
+        return np.concatenate([np.asarray(p, dtype=np.int64).reshape(-1) for p in parts]) if parts else \
+            np.zeros(0, dtype=np.int64)
 
     # -------------------------------------------------------------- node sink
     def deliver(self, tok, src, nbytes, cdn_ms, p2p_ms, offs, eids, expect=None) -> None:
@@ -914,13 +939,18 @@ class FleetServer:
         verify = expect >= 0
         pay = self._payload_stage(w, offs, nbytes) if any(self._payload) else None
         tag = (tok, src, nbytes, cdn_ms, p2p_ms, offs, eids, expect if verify.any() else None, pay)
-        return self.pipe.launch_columns(self.node.arena, offs, nbytes, enc, drk, iv, tag, keys=keys,
-                                        expect=expect if verify.any() else None)
+        batch = self.pipe.launch_columns(self.node.arena, offs, nbytes, enc, drk, iv, tag, keys=keys,
+                                         expect=expect if verify.any() else None)
+        if batch is None:  # (every delivered row goes into a batch: a lost one would keep its pins)
+            raise RuntimeError("transmux pipeline returned no batch for delivered fragments")
+        self._tx_inflight[id(batch)] = (eids[eids >= 0], eids[(expect >= 0) & (eids >= 0)])
+        return batch
 
     def complete_transmux(self, batch) -> None:
         """Wait for a launched transmux batch; its info rows go to the players as columns."""
         if batch is None:
             return
+        self._tx_inflight.pop(id(batch), None)
         tag, rows, plain, has, verified = self.pipe.complete_columns(batch)
         tok, src, nbytes, cdn_ms, p2p_ms, offs, eids, expect, pay = tag
         ring_off = None

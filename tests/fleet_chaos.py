@@ -32,6 +32,10 @@ from hlsjs_p2p_wrapper_amd.parallel import LocalComm, ThreadHub
 from hlsjs_p2p_wrapper_amd.parallel.fleet import FleetServer, player_main
 from hlsjs_p2p_wrapper_amd.player.transmux import pipeline_for
 
+# every node of a scenario checks its replicated-state invariants after each round
+# (agent/audit.py); HLSP2P_AUDIT=0 turns it off for a timing sweep
+os.environ.setdefault("HLSP2P_AUDIT", "1")
+
 
 LIVE_SPEED = 20.0  # live scenarios: media seconds per wall second
 LIVE_WALL_S = 6.0  # ... and their wall time
@@ -347,9 +351,9 @@ if __name__ == "__main__":
     lo, hi = (int(argv[0]), int(argv[1])) if len(argv) > 1 else (0, 20)
     bad = []
     for s in range(lo, hi):
-        res = scenario(s, device=device, ranks=nranks, faults=faults, live=live, ring=ring)
         try:
-            check(res)
+            res = scenario(s, device=device, ranks=nranks, faults=faults, live=live, ring=ring)
+            check(res)  # (an AuditError raised in a scenario is an AssertionError: a failed seed)
             ends = sorted(round(m["t"], 1) for m in res["marks"].values())
             st = [n["stats"] for n in res.get("nodes", {}).values()]
             crc, parked = sum(x.get("crc_failures", 0) for x in st), sum(x.get("parked", 0) for x in st)

@@ -8,6 +8,7 @@ sweep: ``python tests/swarm_chaos.py 0 200 [--extras] [--gpu]``.
 """
 from __future__ import annotations
 
+import os
 import sys
 import threading
 
@@ -21,6 +22,10 @@ from hlsjs_p2p_wrapper_amd.net.origin import Rendition, SyntheticHlsOrigin
 from hlsjs_p2p_wrapper_amd.parallel import ThreadHub
 from hlsjs_p2p_wrapper_amd.player import MediaElement
 from hlsjs_p2p_wrapper_amd.player.hls import Hls as Engine
+
+# every node of a scenario checks its replicated-state invariants after each round
+# (agent/audit.py); HLSP2P_AUDIT=0 turns it off for a timing sweep
+os.environ.setdefault("HLSP2P_AUDIT", "1")
 
 
 def scenario(seed: int, extras: bool = False, device: str = "cpu") -> dict:
@@ -132,8 +137,8 @@ if __name__ == "__main__":
     device = "cuda:0" if "--gpu" in sys.argv else "cpu"
     bad = []
     for s in range(lo, hi):
-        res = scenario(s, extras, device)
         try:
+            res = scenario(s, extras, device)  # (an AuditError is an AssertionError: a failed seed)
             check(res)
             print(f"seed {s}: ok ({res['n']} peers)", flush=True)
         except AssertionError as e:

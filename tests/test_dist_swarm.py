@@ -147,7 +147,8 @@ PER_RANK_KEYS = {"rank", "rounds", "step_ms", "wait_device_us", "exchange_us", "
                  "p2p_links", "p2p_link_GBps",
                  "transmux_dev_ms", "transmux_wait_us", "await_players_us", "payload_GBps", "payload_wait_us",
                  "crc_failures", "control_fallbacks",
-                 "deferred", "inflight", "cu_reserve", "bound"}
+                 "deferred", "inflight", "cu_reserve", "p2p_rejected_MB", "p2p_link_roof_GBps", "p2p_link_util",
+                 "bound"}
 
 
 def _check_per_rank(res, world):
