@@ -53,7 +53,9 @@ def save_cache(node, path: str) -> Dict[str, int]:
         _seg.copy_segments(node.arena, staged, offs_src, offs, lens)
         data.copy_(staged)
         if getattr(node, "ingest_crc", True):
+            # the table holds keyed CRCs (crc ^ key digest): the file keeps plain CRC-32s
             crcs = node.crc_dev[torch.from_numpy(ids).to(node.device)].cpu()
+            crcs = torch.from_numpy(crcs.numpy() ^ _crc_mod().key_digest(keys))
         else:  # a one-rank node keeps no CRC table: compute the CRCs the restore verifies
             from ..ops import crc as _crc
 
@@ -66,6 +68,12 @@ def save_cache(node, path: str) -> Dict[str, int]:
                "crcs": crcs.to(torch.int32).contiguous(),
                "data": data}, path, metadata={"format": FORMAT, "align": str(ALIGN)})
     return {"segments": n, "bytes": int(lens.sum()) if n else 0}
+
+
+def _crc_mod():
+    from ..ops import crc as _crc
+
+    return _crc
 
 
 def load_cache(node, path: str) -> Dict[str, int]:
@@ -116,8 +124,8 @@ def load_cache(node, path: str) -> Dict[str, int]:
         _, ok = _crc.crc32_batch(node.arena, dst_offs.tolist(), ln.tolist(), expect_dev=expect)
         ok = ok.cpu().numpy().astype(bool)
         good, bad = ids[ok], ids[~ok]
-        node.crc_dev[torch.from_numpy(good).to(node.device)] = \
-            expect[torch.from_numpy(np.nonzero(ok)[0]).to(node.device)]
+        keyed = crcs[keep].numpy() ^ _crc.key_digest(k)  # the table holds CRCs bound to their keys
+        node.crc_dev[torch.from_numpy(good).to(node.device)] = torch.from_numpy(keyed[ok]).to(node.device)
     if len(good):
         st.commit(good)
     if len(bad):

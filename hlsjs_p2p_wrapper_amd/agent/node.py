@@ -351,10 +351,15 @@ class SwarmNode:
         # "p2p_wire" (every byte received) and "p2p_links" ((round, source peer) pairs): link rates
         self.stats = {"cdn": 0, "p2p": 0, "upload": 0, "cache": 0, "rounds": 0, "crc_failures": 0,
                       "segments": 0, "cdn_segments": 0, "p2p_segments": 0, "prefetched": 0,
-                      "p2p_links": 0, "p2p_wire": 0, "p2p_rejected": 0, "p2p_rejected_segments": 0}
+                      "p2p_links": 0, "p2p_wire": 0, "p2p_rejected": 0, "p2p_rejected_segments": 0,
+                      "cache_segments": 0}
         self.swarm_stats = {"cdn": 0, "p2p": 0, "upload": 0}
         self.last_round: Dict[str, Any] = {}
         self.corrupt_next_recv = 0  # fault injection: flip a byte in the next N received rounds
+        # fault injection: the next N rounds with sends each send one segment from ANOTHER
+        # resident entry of the same length (a sender's bookkeeping bug: its bytes and its table
+        # CRC agree with each other, not with the key the receiver asked for)
+        self.misroute_next_send = 0
         # cross-rank consistency (SURVEY 5.2 state-machine assertions): every rank replays the
         # same control messages into its own directory and plans every round independently; a
         # two-sided data plane (RCCL send / recv) then needs the plans to match exactly.  The
@@ -792,6 +797,7 @@ class SwarmNode:
             src = self._prefetched.pop(req.key, None)
             if src is None:
                 self.stats["cache"] += n
+                self.stats["cache_segments"] += 1
             self._deliver_req(req, src or "cache", n, 0.0, 0.0, self.arena[off:off + n], -1, eid)
         finally:
             self.store.unpin(np.array([eid], dtype=np.int64))
@@ -839,6 +845,7 @@ class SwarmNode:
                 ent = self.store.entries(eids)
                 offs, lens = ent[:, 0].copy(), ent[:, 1].copy()
                 self.stats["cache"] += int(lens.sum())
+                self.stats["cache_segments"] += len(tok)
                 z = np.zeros(len(tok), dtype=np.float64)
                 self._deliver_cols(tok, np.full(len(tok), SRC_CACHE, dtype=np.int8), lens, z, z, offs, eids)
             finally:
@@ -1054,6 +1061,8 @@ class SwarmNode:
             if len(valid):
                 self.store.pin(valid)
                 h.send_pins = valid
+            if self.misroute_next_send > 0:
+                self._misroute(send_rows, send_eids)
         t_cdn0 = time.perf_counter()
         self.timer.add("plan", t_cdn0 - t_ctrl)
         with (torch.cuda.stream(self.stream) if self.is_cuda else contextlib.nullcontext()):
@@ -1126,6 +1135,10 @@ class SwarmNode:
             if h.defer is not None:
                 dgood = h.defer[ok]
                 eh = h.expect_host.numpy() if isinstance(h.expect_host, torch.Tensor) else np.asarray(h.expect_host)
+                # the trailers are keyed CRCs: unbind them with the keys this rank asked for, so
+                # the consumer (the CRC fused into its decrypt) compares plain CRC-32s -- a copy
+                # sent under another key then fails there
+                eh = eh.astype(np.int32) ^ _crc.key_digest(recv[5])
                 exp_good = eh.astype(np.int64)[ok]
                 if not dgood.any():
                     dgood = None
@@ -1427,8 +1440,8 @@ class SwarmNode:
         for i in corrupt.tolist():
             if lens[i]:
                 self.arena[int(offs[i]) + int(lens[i]) // 2] ^= 0xFF
-        if self.ingest_crc:  # the trailers this rank's sends carry
-            _crc.crc32_batch(self.arena, offs, lens, scatter_to=self.crc_dev, scatter_idx=eids)
+        if self.ingest_crc:  # the trailers this rank's sends carry: each CRC bound to its key
+            _crc.crc32_batch(self.arena, offs, lens, scatter_to=self.crc_dev, scatter_idx=eids, keys=keys)
         self.store.commit(eids)  # announced next round; peers' reads are stream-ordered after the H2D
         # CDN bandwidth shaping (xhr-shaper analog): completions are deferred by the modelled
         # transfer time of this round's CDN bytes
@@ -1524,12 +1537,13 @@ class SwarmNode:
             d = (wf & (W_PY | W_PREFETCH)) == 0
             defer = d if d.any() else None
         if defer is None:
-            # verify against the senders' trailers; the combine kernel also scatters the
-            # computed CRCs into the per-entry table (ids ride the descriptor H2D): a
-            # mismatching entry is dropped in complete_round, so the table only ever serves
-            # verified values
+            # verify against the senders' trailers, keyed with the key this rank asked for (a
+            # segment sent under another key fails, even when its bytes match its own CRC);
+            # the combine kernel also scatters the keyed CRCs into the per-entry table (ids
+            # and keys ride the descriptor H2D): a mismatching entry is dropped in
+            # complete_round, so the table only ever serves verified values
             _, ok = _crc.crc32_batch(self.arena, roff_a, recv_rows[:, 4], expect_dev=trailers,
-                                     scatter_to=self.crc_dev, scatter_idx=rid_a)
+                                     scatter_to=self.crc_dev, scatter_idx=rid_a, keys=recv_rows[:, :4])
         else:
             ok = self._defer_verify(h, defer, trailers, roff_a, recv_rows, rid_a)
         if self.is_cuda:
@@ -1559,7 +1573,7 @@ class SwarmNode:
         if len(nd):
             _, ok_nd = _crc.crc32_batch(self.arena, roff_a[nd], recv_rows[nd, 4],
                                         expect_dev=torch.index_select(trailers, 0, ix["nd"]),
-                                        scatter_to=self.crc_dev, scatter_idx=rid_a[nd])
+                                        scatter_to=self.crc_dev, scatter_idx=rid_a[nd], keys=recv_rows[nd, :4])
             ok.index_copy_(0, ix["nd"], ok_nd)
         self.crc_dev.index_copy_(0, ix["rd"], torch.index_select(trailers, 0, ix["dd"]))
         h.defer = defer
@@ -1619,6 +1633,20 @@ class SwarmNode:
         if keep is not None:
             tok, idx = tok[keep], idx[keep]
         return tok, idx, exp_row[idx]
+
+    def _misroute(self, send_rows: np.ndarray, send_eids: np.ndarray) -> None:
+        """Fault injection (``misroute_next_send``): send row i's bytes from another resident
+        entry of the same length -- the receiver's keyed CRC check must reject it."""
+        ids, keys = self.store.resident()
+        if not len(ids):
+            return
+        lens = self.store.entries(ids)[:, 1]
+        for i in np.flatnonzero(send_eids >= 0).tolist():
+            same = np.flatnonzero((lens == send_rows[i, 4]) & (keys != send_rows[i, :4]).any(axis=1))
+            if len(same):
+                send_eids[i] = ids[same[0]]
+                self.misroute_next_send -= 1
+                return
 
     def _count_p2p(self, lens: np.ndarray, passed: bool) -> None:
         """Account peer copies: delivered P2P bytes (``passed``), or rejected bytes of copies

@@ -64,7 +64,8 @@ def crc32_batch(buf: torch.Tensor, offs: Sequence[int], lens: Sequence[int],
                 expect: Optional[Sequence[int]] = None,
                 expect_dev: Optional[torch.Tensor] = None, scatter_to: Optional[torch.Tensor] = None,
                 scatter_idx: Optional[Sequence[int]] = None,
-                variant: Optional[str] = None) -> Tuple[torch.Tensor, Optional[torch.Tensor]]:
+                variant: Optional[str] = None,
+                keys: Optional[np.ndarray] = None) -> Tuple[torch.Tensor, Optional[torch.Tensor]]:
     """CRC-32 of ``buf[offs[i]:offs[i]+lens[i]]``.
 
     Returns ``(crc int32[B], ok uint8[B] | None)`` on ``buf.device``; ``ok`` is produced
@@ -73,6 +74,13 @@ def crc32_batch(buf: torch.Tensor, offs: Sequence[int], lens: Sequence[int],
     ``scatter_to[scatter_idx[i]]`` -- on the device by the combine kernel, whose index
     array rides the same descriptor H2D (no separate index copy / index_put launch).
     ``variant`` picks the residue kernel's matrix-core path (default :data:`MFMA_VARIANT`).
+
+    ``keys`` (int64[B, 4] segment keys ``(swarm, level, urlId, sn)``): keyed mode -- the
+    expected values and the scattered table entries are the CRCs bound to each segment's key,
+    ``crc ^ key_digest(key)`` (computed in the combine kernel from the keys riding the
+    descriptor block; :func:`key_digest` is the host twin).  A node's CRC table and the trailers
+    it sends hold keyed values, so bytes that reach a peer under another key fail its check.
+    The returned ``crc`` is always the plain CRC-32.
     """
     B = len(offs)
     o = np.asarray(offs, dtype=np.int64)
@@ -82,6 +90,11 @@ def crc32_batch(buf: torch.Tensor, offs: Sequence[int], lens: Sequence[int],
         want_ok = expect is not None or expect_dev is not None
         return z, (torch.empty(0, dtype=torch.uint8, device=buf.device) if want_ok else None)
     sidx = None if scatter_to is None else np.asarray(scatter_idx, dtype=np.int64).reshape(-1)
+    kk = None
+    if keys is not None:
+        kk = np.ascontiguousarray(np.asarray(keys, dtype=np.int64).reshape(-1, 4)[:, :4])
+        if len(kk) != B:
+            raise ValueError("crc32_batch: keys must be int64[B, 4]")
     if buf.device.type == "cpu":
         if np.any(o < 0) or np.any(n < 0) or np.any(o + n > buf.numel()):
             raise ValueError("crc32_batch: range out of bounds")
@@ -89,20 +102,29 @@ def crc32_batch(buf: torch.Tensor, offs: Sequence[int], lens: Sequence[int],
             raise ValueError("crc32_batch: scatter index out of range")
         crc = _rt().crc32_batch(buf.numpy(), o, n).view(np.int32)
         crc_t = torch.from_numpy(crc.copy())
+        bound = crc if kk is None else crc ^ key_digest(kk)
+        bound_t = crc_t if kk is None else torch.from_numpy(bound.copy())
         ok = None
         if expect_dev is not None:
-            ok = (crc_t == expect_dev.to(torch.int32)).to(torch.uint8)
+            ok = (bound_t == expect_dev.to(torch.int32)).to(torch.uint8)
         elif expect is not None:
             exp = np.asarray(expect, dtype=np.uint32).view(np.int32)
-            ok = torch.from_numpy((crc == exp).astype(np.uint8))
+            ok = torch.from_numpy((bound == exp).astype(np.uint8))
         if sidx is not None:
-            scatter_to[torch.from_numpy(sidx)] = crc_t
+            scatter_to[torch.from_numpy(sidx)] = bound_t
         return crc_t, ok
     w, tables = _device_consts(buf.device, variant or MFMA_VARIANT)  # bounds / alignment: checked natively
     if expect_dev is None and expect is not None:
         expect_dev = torch.from_numpy(np.asarray(expect, dtype=np.uint32).view(np.int32).copy()).to(buf.device)
     # one native call: descriptor math, one staging H2D, residue + combine launches
-    return _dev().crc32_launch(buf, o, n, w, tables, expect_dev, scatter_to, sidx)
+    return _dev().crc32_launch(buf, o, n, w, tables, expect_dev, scatter_to, sidx, kk)
+
+
+def key_digest(keys: np.ndarray) -> np.ndarray:
+    """int32[n] digests of int64[n, 4] segment keys: the value a keyed CRC is XOR-ed with
+    (``crc32_batch(..., keys=...)``; host twin of the combine kernel's ``key_digest``)."""
+    k = np.ascontiguousarray(np.asarray(keys, dtype=np.int64).reshape(-1, 4)[:, :4])
+    return _rt().key_digest(k).view(np.int32)
 
 
 def _crc32_batch_py(buf: torch.Tensor, o: np.ndarray, n: np.ndarray, expect, expect_dev, scatter_to, sidx,

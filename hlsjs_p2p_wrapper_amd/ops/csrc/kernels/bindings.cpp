@@ -18,7 +18,8 @@ hipError_t launch_aes128_cbc_decrypt(const uint8_t*, uint8_t*, const int64_t*, c
                                      const void*, uint32_t*, const int64_t*, void*);
 hipError_t launch_crc32_batch(const uint8_t*, const int64_t*, const int64_t*, const int64_t*, const int64_t*,
                               const void*, const uint32_t*, uint32_t*, uint32_t*, const uint32_t*, uint8_t*,
-                              const int64_t*, uint32_t*, int64_t, int, int64_t, int, bool, hipStream_t);
+                              const int64_t*, uint32_t*, int64_t, int, int64_t, int, bool, hipStream_t,
+                              const int64_t*);
 hipError_t launch_ts_demux(const uint8_t*, const int64_t*, const int64_t*, const int64_t*, int, int64_t, uint32_t*,
                            int64_t*, int32_t*, uint8_t*, const int64_t*, int64_t*, int64_t, int64_t*, hipStream_t,
                            const void*, const int64_t*);
@@ -135,7 +136,7 @@ void crc32_batch(Tensor buf, Tensor seg_off, Tensor seg_len, Tensor tile_prefix,
   ok(D::launch_crc32_batch(cptr<uint8_t>(buf), cptr<int64_t>(seg_off), cptr<int64_t>(seg_len),
                            cptr<int64_t>(tile_prefix), cptr<int64_t>(res_off), wfrag.data_ptr(),
                            cptr<uint32_t>(tables), mptr<uint32_t>(residues), mptr<uint32_t>(crc_out), ex, okp,
-                           sidx, sout, sn, static_cast<int>(B), total_tiles, num_cus(buf), fp4, stream()),
+                           sidx, sout, sn, static_cast<int>(B), total_tiles, num_cus(buf), fp4, stream(), nullptr),
      "crc32_batch");
 }
 

@@ -256,6 +256,24 @@ constexpr int kNumQ = 12;              // Q_b = A^(-8 * 2^b): pad removal (pad <
 constexpr uint32_t kInitFold256 = 0xf2697aa7u;   // 256-byte groups (crc_host.cpp: init_fold)
 constexpr uint32_t kInitFold4096 = 0x38e3ffeeu;  // 4096-byte chunks of the fused decrypt CRC
 
+// Digest of a segment key (segment-view.js:9-17,59-61): the 12-byte wire key
+// [level, urlId, sn] plus the swarm id, mixed to 32 bits (splitmix64 finalizer, the store's
+// mix64).  The combine below binds a CRC to the key it was computed for (crc ^ digest), so a
+// segment that reaches a peer under another key -- an entry the sender overwrote with another
+// segment, whose table CRC is then consistent with the wrong bytes -- fails the receiver's
+// check.  Host twin: runtime key_digest (store.hpp); tests compare the two.
+__device__ __forceinline__ uint64_t mix64(uint64_t z) {
+  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+  z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+  return z ^ (z >> 31);
+}
+__device__ __forceinline__ uint32_t key_digest(const int64_t* __restrict__ k) {
+  const uint64_t a = uint64_t(uint32_t(k[1])) | (uint64_t(uint32_t(k[2])) << 32);  // level | urlId
+  const uint64_t b = uint64_t(uint32_t(k[3])) | (uint64_t(uint32_t(k[0])) << 32);  // sn | swarm
+  const uint64_t z = mix64(a ^ mix64(b + 0x9E3779B97F4A7C15ull));
+  return uint32_t(z ^ (z >> 32));
+}
+
 // One workgroup per segment.  tables: P_0..P_39 then Q_0..Q_11 (each kSlice u32).  Group
 // residues of 2^kLg bytes: 256-byte groups (the residue kernels above) or 4096-byte chunks
 // (the CRC fused into the decrypt, folded by crc32_fold_combine_kernel).
@@ -265,7 +283,7 @@ __device__ __forceinline__ void combine_segment(
     const uint32_t* __restrict__ residues, const int64_t* __restrict__ res_off, const int64_t* __restrict__ seg_len,
     const uint32_t* __restrict__ tables, uint32_t* __restrict__ crc_out, const uint32_t* __restrict__ expect,
     uint8_t* __restrict__ ok_out, const int64_t* __restrict__ scatter_idx, uint32_t* __restrict__ scatter_out,
-    int64_t scatter_n) {
+    int64_t scatter_n, const int64_t* __restrict__ keys) {
   const int64_t n = seg_len[seg];
   const int64_t G = (n + (int64_t(1) << kLg) - 1) >> kLg;
   // run length L = next pow2 of ceil(G / threads)
@@ -330,12 +348,15 @@ __device__ __forceinline__ void combine_segment(
     }
     const uint32_t crc = raw ^ init ^ 0xFFFFFFFFu;
     crc_out[seg] = crc;
-    if (ok_out) ok_out[seg] = (expect && expect[seg] == crc) ? 1 : 0;
+    // keyed (keys given): the expected value and the table entry are the CRC bound to the
+    // segment's key (a peer's trailer is its table entry)
+    const uint32_t digest = keys ? crc ^ key_digest(keys + 4 * seg) : crc;
+    if (ok_out) ok_out[seg] = (expect && expect[seg] == digest) ? 1 : 0;
     // optional scatter into a per-entry CRC table (the cache's ingest CRCs): saves the
     // caller an index H2D plus an index_put launch per round; out-of-range ids are dropped
     if (scatter_out) {
       const int64_t d = scatter_idx[seg];
-      if (d >= 0 && d < scatter_n) scatter_out[d] = crc;
+      if (d >= 0 && d < scatter_n) scatter_out[d] = digest;
     }
   }
 }
@@ -345,12 +366,12 @@ __global__ __launch_bounds__(kCombineThreads) void crc32_combine_kernel(
     const uint32_t* __restrict__ residues, const int64_t* __restrict__ res_off, const int64_t* __restrict__ seg_len,
     const uint32_t* __restrict__ tables, uint32_t* __restrict__ crc_out, const uint32_t* __restrict__ expect,
     uint8_t* __restrict__ ok_out, const int64_t* __restrict__ scatter_idx, uint32_t* __restrict__ scatter_out,
-    int64_t scatter_n) {
+    int64_t scatter_n, const int64_t* __restrict__ keys) {
   __shared__ __attribute__((aligned(16))) uint32_t s_tab[kCombineLdsTables * kSlice];  // 60 KiB
   __shared__ __attribute__((aligned(16))) uint32_t s_q[kLg * kSlice];                  // 32 / 48 KiB
   __shared__ uint32_t s_acc[kCombineThreads];
   combine_segment<kLg>(blockIdx.x, threadIdx.x, s_tab, s_q, s_acc, residues, res_off, seg_len, tables, crc_out, expect,
-                       ok_out, scatter_idx, scatter_out, scatter_n);
+                       ok_out, scatter_idx, scatter_out, scatter_n, keys);
 }
 
 // The fused decrypt CRC's second level (aes_cbc.hip: crc_chunk_masks writes 64 mask dwords per
@@ -425,7 +446,7 @@ __global__ __launch_bounds__(kCombineThreads) void crc32_fold_combine_kernel(
   for (int64_t t = tid >> 6; t < tiles; t += kCombineThreads / 64) fold_tile(masks, s_w, chunk_res, c0 + 32 * t, cend, lane);
   __syncthreads();  // the segment's chunk residues, written by its own waves, before the combine reads them
   combine_segment<12>(seg, tid, s_tab, s_q, s_acc, chunk_res, chunk_off, seg_len, tables, crc_out, expect, ok_out,
-                      scatter_idx, scatter_out, scatter_n);
+                      scatter_idx, scatter_out, scatter_n, nullptr);
 }
 
 // masks: 64 dwords per 4096-byte chunk for each segment, the segment's chunks starting at
@@ -447,7 +468,8 @@ hipError_t launch_crc32_batch(const uint8_t* buf, const int64_t* seg_off, const 
                               const int64_t* tile_prefix, const int64_t* res_off, const void* wfrag,
                               const uint32_t* tables, uint32_t* residues, uint32_t* crc_out, const uint32_t* expect,
                               uint8_t* ok_out, const int64_t* scatter_idx, uint32_t* scatter_out, int64_t scatter_n,
-                              int nseg, int64_t total_tiles, int num_cu, bool fp4, hipStream_t stream) {
+                              int nseg, int64_t total_tiles, int num_cu, bool fp4, hipStream_t stream,
+                              const int64_t* keys) {
   if (nseg <= 0) return hipSuccess;
   if (total_tiles > 0) {
     const int64_t waves_max = static_cast<int64_t>(num_cu) * 2 * (kCrcThreads / 64);
@@ -467,7 +489,8 @@ hipError_t launch_crc32_batch(const uint8_t* buf, const int64_t* seg_off, const 
     if (e != hipSuccess) return e;
   }
   hipLaunchKernelGGL(crc32_combine_kernel<8>, dim3(static_cast<unsigned>(nseg)), dim3(kCombineThreads), 0, stream,
-                     residues, res_off, seg_len, tables, crc_out, expect, ok_out, scatter_idx, scatter_out, scatter_n);
+                     residues, res_off, seg_len, tables, crc_out, expect, ok_out, scatter_idx, scatter_out, scatter_n,
+                     keys);
   return hipGetLastError();
 }
 

@@ -20,7 +20,8 @@ namespace hlsp2p {
 namespace dev {
 hipError_t launch_crc32_batch(const uint8_t*, const int64_t*, const int64_t*, const int64_t*, const int64_t*,
                               const void*, const uint32_t*, uint32_t*, uint32_t*, const uint32_t*, uint8_t*,
-                              const int64_t*, uint32_t*, int64_t, int, int64_t, int, bool, hipStream_t);
+                              const int64_t*, uint32_t*, int64_t, int, int64_t, int, bool, hipStream_t,
+                              const int64_t*);
 }  // namespace dev
 }  // namespace hlsp2p
 
@@ -49,9 +50,12 @@ void put(std::vector<uint8_t>& blk, int64_t& off, const void* p, int64_t nbytes)
 // CRC-32 (zlib) of buf[offs[i] : offs[i] + lens[i]] (16-byte aligned offsets).  `expect`:
 // int32 device tensor of expected values -> also returns ok (uint8, 1 = match).  `scatter_to`
 // / `scatter_idx`: the combine kernel writes crc[i] to scatter_to[scatter_idx[i]] (ids ride
-// the descriptor block).  `wfrag` selects the matrix-core path (see crc32_batch).
+// the descriptor block).  `wfrag` selects the matrix-core path (see crc32_batch).  `keys`
+// (int64[B, 4] segment keys, riding the descriptor block): keyed mode -- `expect` and the
+// scattered table values are the CRCs bound to each segment's key (crc ^ key_digest); the
+// returned crc stays the plain CRC-32.
 py::tuple crc32_launch(Tensor buf, I64 offs, I64 lens, Tensor wfrag, Tensor tables, c10::optional<Tensor> expect,
-                       c10::optional<Tensor> scatter_to, c10::optional<I64> scatter_idx) {
+                       c10::optional<Tensor> scatter_to, c10::optional<I64> scatter_idx, c10::optional<I64> keys) {
   TORCH_CHECK_VALUE(buf.is_cuda() && buf.is_contiguous() && buf.scalar_type() == torch::kUInt8, "buf: contiguous GPU uint8");
   TORCH_CHECK_VALUE((reinterpret_cast<uintptr_t>(buf.data_ptr()) & 15) == 0, "buf must be 16-byte aligned");
   const int64_t B = offs.size();
@@ -86,7 +90,7 @@ py::tuple crc32_launch(Tensor buf, I64 offs, I64 lens, Tensor wfrag, Tensor tabl
   }
   TORCH_CHECK_VALUE(scatter_to.has_value() == scatter_idx.has_value(), "scatter_to and scatter_idx go together");
   std::vector<uint8_t> blk;
-  int64_t d_o, d_n, d_tp, d_ro, d_si = -1;
+  int64_t d_o, d_n, d_tp, d_ro, d_si = -1, d_k = -1;
   put(blk, d_o, o, B * 8);
   put(blk, d_n, n, B * 8);
   put(blk, d_tp, tile_prefix.data(), (B + 1) * 8);
@@ -102,6 +106,10 @@ py::tuple crc32_launch(Tensor buf, I64 offs, I64 lens, Tensor wfrag, Tensor tabl
     for (int64_t i = 0; i < B; ++i) TORCH_CHECK_VALUE(si.data()[i] >= 0 && si.data()[i] < sn, "scatter index out of range");
     put(blk, d_si, si.data(), B * 8);
     sout = static_cast<uint32_t*>(scatter_to->data_ptr());
+  }
+  if (keys.has_value()) {
+    TORCH_CHECK_VALUE(keys->size() == 4 * B, "keys: int64[B, 4]");
+    put(blk, d_k, keys->data(), B * 32);
   }
   const int64_t nbytes = static_cast<int64_t>(blk.size());
   Tensor host = torch::empty({nbytes}, torch::TensorOptions().dtype(torch::kUInt8).pinned_memory(true));
@@ -122,7 +130,7 @@ py::tuple crc32_launch(Tensor buf, I64 offs, I64 lens, Tensor wfrag, Tensor tabl
       static_cast<const uint8_t*>(buf.data_ptr()), at(d_o), at(d_n), at(d_tp), at(d_ro), wfrag.data_ptr(),
       static_cast<const uint32_t*>(tables.data_ptr()), reinterpret_cast<uint32_t*>(base + d_res),
       reinterpret_cast<uint32_t*>(base + d_crc), ex, ex ? base + d_ok : nullptr, d_si >= 0 ? at(d_si) : nullptr, sout,
-      sn, static_cast<int>(B), tile_prefix[B], cus(device), fp4, st);
+      sn, static_cast<int>(B), tile_prefix[B], cus(device), fp4, st, d_k >= 0 ? at(d_k) : nullptr);
   TORCH_CHECK(e == hipSuccess, "crc32 launch failed: ", hipGetErrorString(e));
   return py::make_tuple(crc, ex ? py::cast(ok) : py::none());
 }
@@ -149,6 +157,6 @@ std::vector<Tensor> arena_views(const Tensor& arena, I64 offs, I64 lens) {
 void register_ingest(py::module& m) {
   m.def("crc32_launch", &crc32_launch, py::arg("buf"), py::arg("offs"), py::arg("lens"), py::arg("wfrag"),
         py::arg("tables"), py::arg("expect") = py::none(), py::arg("scatter_to") = py::none(),
-        py::arg("scatter_idx") = py::none());
+        py::arg("scatter_idx") = py::none(), py::arg("keys") = py::none());
   m.def("arena_views", &arena_views, py::arg("arena"), py::arg("offs"), py::arg("lens"));
 }

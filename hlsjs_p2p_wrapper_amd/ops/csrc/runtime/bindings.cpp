@@ -303,6 +303,14 @@ PYBIND11_MODULE(_runtime, m) {
   m.attr("TS_CLASSES") = ts::kClasses;
 
   // ------------------------------------------------------------------ store
+  m.def("key_digest", [](Arr<int64_t> keys) {
+    // int64[n, 4] segment keys -> uint32[n]: the digest a keyed CRC is bound with
+    if (keys.size() % 4) throw std::invalid_argument("key_digest: keys must be int64[n, 4]");
+    const int64_t n = keys.size() / 4;
+    Arr<uint32_t> out(n);
+    for (int64_t i = 0; i < n; ++i) out.mutable_data()[i] = key_digest(key_from(keys.data() + 4 * i));
+    return out;
+  });
   py::class_<SegmentStore>(m, "SegmentStore")
       .def(py::init<int64_t, int64_t>(), py::arg("capacity"), py::arg("align") = 256)
       .def_property_readonly("capacity", &SegmentStore::capacity)

@@ -268,9 +268,13 @@ void plan_round_into(const Directory& dir, const Want* wants_in, size_t n_in, co
     }
   }
   auto flag = [&](int r, int64_t f) { return (flags[r] & f) != 0; };
-  // may want `wt` receive a peer copy of `size` bytes?  Staged (or in-process) wants always
-  // announce the size they reserved; a not-staged one only once it reserved at least that
-  auto fits_recv = [](const Want& wt, int64_t size) { return !(wt.flags & kNotStaged) || wt.size >= size; };
+  // may want `wt` receive a peer copy of `size` bytes?  Only within what its admission
+  // reserved: the wanter's node retired exactly that much of its ring before announcing the
+  // want (node.py: retire_region), so a larger copy could land on entries a peer is sending
+  // from.  A not-staged network want that does not know the holder's length yet waits a round
+  // (its node reads the length from the directory and reserves it before announcing again); a
+  // staged want whose own size is smaller than the holder's copy fetches from the CDN.
+  auto fits_recv = [](const Want& wt, int64_t size) { return wt.size >= size; };
 
   std::vector<int64_t>& link = S.link;  // bytes src->dst this round
   link.assign(size_t(world) * world, 0);
@@ -365,10 +369,11 @@ void plan_round_into(const Directory& dir, const Want* wants_in, size_t n_in, co
         unserved.push_back(w);
         continue;
       }
-      // a wanter only receives what its admission reserved: a not-staged network want that
-      // does not know the holder's length yet waits a round (its node reads the length from
-      // the directory and reserves it before announcing the want again)
-      if (!fits_recv(wt, de ? de->length : wt.size)) continue;
+      // a wanter only receives what its admission reserved (fits_recv)
+      if (!fits_recv(wt, de ? de->length : wt.size)) {
+        if (!(wt.flags & kNotStaged)) cdn_or_stage(wt, key);
+        continue;
+      }
       int best = -1;
       for (int k = 1; k <= world; ++k) {  // rotation start: the rank after d
         int h = (d + k) % world;
@@ -478,7 +483,10 @@ void plan_round_into(const Directory& dir, const Want* wants_in, size_t n_in, co
       for (size_t m = g.a; m < g.b; ++m) {
         const Want& wt = wants[members[m]];
         if (wt.rank == seeder) continue;
-        if (!fits_recv(wt, sz)) continue;  // (see above) it gets the seeder's copy next round
+        if (!fits_recv(wt, sz)) {  // (fits_recv) a not-staged one gets the seeder's copy next round
+          if (!(wt.flags & kNotStaged)) cdn_or_stage(wt, g.key);
+          continue;
+        }
         p2p.push_back({g.key, sz, seeder, wt.rank, wt.want_id, 1});
         link[size_t(seeder) * world + wt.rank] += sz;
         send_total[seeder] += sz;

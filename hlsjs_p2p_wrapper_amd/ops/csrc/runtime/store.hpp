@@ -39,6 +39,16 @@ inline uint64_t mix64(uint64_t z) {
   return z ^ (z >> 31);
 }
 
+// 32-bit digest of a segment key that binds a CRC to it (crc ^ key_digest): the 12-byte wire
+// key [level, urlId, sn] plus the swarm id.  Device twin: kernels/crc32_mfma.hip key_digest
+// (the CRC combine kernel's keyed mode); the two must agree bit for bit (tests).
+inline uint32_t key_digest(const SegKey& k) {
+  const uint64_t a = uint64_t(k.level) | (uint64_t(k.url_id) << 32);
+  const uint64_t b = uint64_t(k.sn) | (uint64_t(k.swarm) << 32);
+  const uint64_t z = mix64(a ^ mix64(b + 0x9E3779B97F4A7C15ull));
+  return static_cast<uint32_t>(z ^ (z >> 32));
+}
+
 struct SegKeyHash {
   size_t operator()(const SegKey& k) const {
     uint64_t a = (uint64_t(k.swarm) << 32) | k.level;

@@ -91,7 +91,9 @@ def test_two_players_are_served_their_slices(node_side):
     marks = server.marks["end"]
     assert all(m["buffered"] > 0 and m["errors"] == 0 for m in marks.values())
     # each player fetched its own slice: 60 s apart -> disjoint segment keys on the node
-    assert node.stats["cdn_segments"] >= sum(m["buffered"] for m in marks.values())
+    # (a fragment loaded twice -- a retry or a level switch -- is a cache hit the second time;
+    # the node counts a fetch when its round delivers it)
+    assert node.stats["cdn_segments"] + node.stats["cache_segments"] >= sum(m["buffered"] for m in marks.values())
     for c in conns:
         c.send(("stop",))
     for t in threads:

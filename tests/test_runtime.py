@@ -398,3 +398,23 @@ def test_the_nodes_want_flags_match_the_want_table_bits(rt):
     ids, _ = _add(wt, keys(3), size=100, flags=0, tokens=[1])
     wt.requeue(ids, False)
     assert not (wt.info(ids)[0, 7] & n.W_ON_DEV)  # held, not device-resident
+
+
+def test_planner_never_sends_more_than_the_wanter_admitted(rt):
+    """A receive lands in the ring region its wanter's admission retired (the
+    round's reservations could reach past it): the planner never sends a copy larger than the
+    want's announced size.  A staged want smaller than the holder's copy goes to the CDN, a
+    not-staged one (size still unknown) waits for the holder's length; a seeded forward obeys
+    the same rule."""
+    d = rt.Directory()
+    d.apply(0, np.array([[1, 0, 0, 5, 3000]], dtype=np.int64), np.zeros((0, 4), np.int64))
+    # holder transfer: sizes 3000 (fits), 2000 (staged, smaller: CDN), 0 (not staged: waits)
+    plan = rt.plan_round(d, wants([(5, 3000, 11, 1, 0), (5, 2000, 21, 2, 0), (5, 0, 31, 3, 2)]), flags(rt, 4), 4)
+    by = {int(r[6]): (int(r[5]), int(r[4])) for r in plan}
+    assert by[1] == (0, 3000) and by[2] == (-1, 2000) and 3 not in by
+    assert all(r[4] <= {11: 3000, 21: 2000, 31: 0}[int(r[7])] for r in plan)
+    # seeded forwards: the seeder's copy is larger than one wanter's own size
+    plan = rt.plan_round(rt.Directory(), wants([(9, 4000, 12, 1, 0), (9, 4000, 22, 2, 0), (9, 3500, 32, 3, 0)]),
+                         flags(rt, 4), 4)
+    for r in plan:
+        assert r[4] <= {12: 4000, 22: 4000, 32: 3500}[int(r[7])]
