@@ -1164,7 +1164,7 @@ def _plane_info(node, dist, world: int, device, recv_from=None) -> dict:
     rccl = next((r["comm"]["rccl"] for r in ranks if "rccl" in r.get("comm", {})), None)
     # the wire each rank's RCCL connections actually use (RCCL's own connection log: P2P over
     # xGMI, or a NET fallback) and HIP's link type to its peers (parallel/wire.py)
-    from hlsjs_p2p_wrapper_amd.parallel.wire import degraded
+    from hlsjs_p2p_wrapper_amd.parallel.wire import degraded, link_kinds
     for r in ranks:
         w = r.get("comm", {}).get("wire")
         r["transport"] = w.get("transport") if w else None
@@ -1176,7 +1176,7 @@ def _plane_info(node, dist, world: int, device, recv_from=None) -> dict:
             "launcher": os.environ.get("HLSP2P_LAUNCHER") or ("torchrun" if "TORCHELASTIC_RUN_ID" in os.environ
                                                               else "env" if world > 1 else "none"),
             "world": world, "distinct_devices": distinct, "rccl_rehearsal": rehearsal,
-            "rccl_version": rccl["version"] if rccl else None, "wire": wires,
+            "rccl_version": rccl["version"] if rccl else None, "wire": wires, "hip_links": link_kinds(ranks),
             "transport_degraded": degraded(transport, distinct, rehearsal, wires), "ranks": ranks}
 
 

@@ -174,5 +174,20 @@ def link_types(device: int, peers: Dict[int, int]) -> Dict[str, object]:
 def degraded(plane: str, distinct_devices: Optional[bool], rehearsal: Optional[str],
              wires: List[str]) -> bool:
     """A run on the native RCCL plane with one GPU per rank must use RCCL's P2P transport
-    (xGMI); any rank whose peers connected over a network transport is degraded."""
-    return bool(plane.startswith("rccl") and distinct_devices and not rehearsal and "net" in wires)
+    (xGMI); any rank whose peers connected over a network transport, or through host shared
+    memory (P2P access refused between the GPUs), is degraded."""
+    return bool(plane.startswith("rccl") and distinct_devices and not rehearsal
+                and ("net" in wires or "shm" in wires))
+
+
+def link_kinds(ranks: List[dict]) -> List[str]:
+    """The distinct HIP link types (``XGMI``, ``PCIE``, ...) between the ranks' devices, from
+    every rank's ``comm.wire.links`` (one GPU per rank on one host)."""
+    kinds = set()
+    for r in ranks:
+        links = (r.get("comm") or {}).get("wire", {}).get("links")
+        if isinstance(links, dict):
+            for v in links.values():
+                if isinstance(v, str) and "/" in v:
+                    kinds.add(v.split("/")[0])
+    return sorted(kinds)

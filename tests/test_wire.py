@@ -50,6 +50,10 @@ def test_parse_socket_log_is_net():
     assert not wire.degraded("rccl-native", None, "socket", ["net"])
     assert not wire.degraded("rccl-native", True, None, ["p2p"])
     assert not wire.degraded("hip-ipc", True, None, ["net"])
+    assert wire.degraded("rccl-native", True, None, ["p2p", "shm"])  # P2P refused: through host memory
+    ranks = [{"comm": {"wire": {"links": {"1": "XGMI/1", "2": "XGMI/1"}}}},
+             {"comm": {"wire": {"links": {"0": "XGMI/1", "2": "PCIE/2"}}}}, {"comm": {}}]
+    assert wire.link_kinds(ranks) == ["PCIE", "XGMI"]
 
 
 def test_world_of_one_is_self_and_missing_log_unknown():
