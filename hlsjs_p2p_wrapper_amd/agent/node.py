@@ -1546,7 +1546,9 @@ class SwarmNode:
                                      scatter_to=self.crc_dev, scatter_idx=rid_a, keys=recv_rows[:, :4])
         else:
             ok = self._defer_verify(h, defer, trailers, roff_a, recv_rows, rid_a)
-        if self.is_cuda:
+        if isinstance(ok, np.ndarray):  # decided on the host (every row's check deferred)
+            h.ok_host = ok
+        elif self.is_cuda:
             h.ok_host = torch.empty(ok.numel(), dtype=torch.uint8, pin_memory=True)
             h.ok_host.copy_(ok, non_blocking=True)
         else:
@@ -1560,9 +1562,16 @@ class SwarmNode:
         """Received rows under deferred verification (``verify_deferred``): their trailers go
         into the CRC table now (the entries are announced only after the check) and to the
         host with the delivery; the other rows are CRC-read as usual.  Returns the per-row ok
-        flags on the node's device (deferred rows: provisionally 1)."""
+        flags on the node's device (deferred rows: provisionally 1), or on the host when every
+        row is deferred (the fleet's common case: one index H2D, one table write, one D2H of the
+        trailers -- no flags tensor, no copy back)."""
         dev = self.device
         nd, dd = np.flatnonzero(~defer), np.flatnonzero(defer)
+        h.defer = defer
+        if not len(nd):
+            self.crc_dev.index_copy_(0, _dev_index(rid_a, dev), trailers)
+            self._expect_to_host(h, trailers)
+            return np.ones(len(recv_rows), dtype=np.uint8)
         if self.is_cuda:
             from ..ops.desc import pack_to_device
 
@@ -1575,14 +1584,19 @@ class SwarmNode:
                                         expect_dev=torch.index_select(trailers, 0, ix["nd"]),
                                         scatter_to=self.crc_dev, scatter_idx=rid_a[nd], keys=recv_rows[nd, :4])
             ok.index_copy_(0, ix["nd"], ok_nd)
-        self.crc_dev.index_copy_(0, ix["rd"], torch.index_select(trailers, 0, ix["dd"]))
-        h.defer = defer
+        if len(dd):
+            self.crc_dev.index_copy_(0, ix["rd"], torch.index_select(trailers, 0, ix["dd"]))
+        self._expect_to_host(h, trailers)
+        return ok
+
+    def _expect_to_host(self, h: RoundHandle, trailers) -> None:
+        """The senders' (keyed) trailers of a round's receives, to the host for delivery
+        (asynchronous on the GPU: read after the host waited on the round)."""
         if self.is_cuda:
-            h.expect_host = torch.empty(len(recv_rows), dtype=torch.int32, pin_memory=True)
+            h.expect_host = torch.empty(trailers.numel(), dtype=torch.int32, pin_memory=True)
             h.expect_host.copy_(trailers, non_blocking=True)
         else:
             h.expect_host = trailers.clone()
-        return ok
 
     def _settle_deferred(self, h: RoundHandle, good: tuple, dgood: np.ndarray, exp_good: np.ndarray,
                          tok: np.ndarray, idx: np.ndarray, winfo: np.ndarray):
