@@ -276,7 +276,7 @@ def _calibrate(args, node, step, sync, world: int):
     # identical table on every rank: the same choice.  The default reserve stays unless a
     # candidate beats it by more than the margin: a few steps per candidate cannot separate
     # options within noise, and a socket- or PCIe-bound run makes them all equal
-    margin = float(os.environ.get("HLSP2P_CU_CALIB_MARGIN", "0.02"))
+    margin = float(os.environ.get("HLSP2P_CU_CALIB_MARGIN", "0.04"))
     best = cands[int(np.argmin(table))]
     if before in cands and table[cands.index(best)] > table[cands.index(before)] * (1.0 - margin):
         best = before
