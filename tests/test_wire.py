@@ -173,3 +173,33 @@ def test_self_launch_parent_never_touches_the_gpu(cuda):
     rec = json.loads(p.stdout.strip().splitlines()[-1])
     assert rec["visible_gpus"] == n_hip, (rec, n_hip)
     assert not rec["torch_initialized"] and not rec["kfd_mapped"] and not rec["kfd_open"], rec
+
+
+def test_a_degraded_record_says_so(monkeypatch):
+    """bench.py's labelling of an N>1 record whose RCCL pairs fell back to a network transport
+    with one GPU per rank: the model says it is not an xGMI run, the parallelism ends in
+    -degraded; HLSP2P_REQUIRE_XGMI=1 fails the run instead."""
+    import importlib.util
+
+    spec = importlib.util.spec_from_file_location("bench_mod", REPO / "bench.py")
+    bench = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(bench)
+
+    def record():
+        return {"n_gpus": 8, "config": {"model": "1080p, 8 peers (8 x MI355X)", "parallelism": "swarm8-rccl"},
+                "per_rank": [{"bound": "xgmi"}],
+                "data_plane": {"wire": ["net", "p2p"], "transport_degraded": True, "rccl_rehearsal": None,
+                               "ranks": []}}
+
+    monkeypatch.delenv("HLSP2P_REQUIRE_XGMI", raising=False)
+    r = record()
+    bench._label_rehearsal(r)
+    assert r["config"]["model"].endswith("[RCCL fell back to net/p2p: NOT an xGMI run]")
+    assert r["config"]["parallelism"] == "swarm8-rccl-degraded"
+    monkeypatch.setenv("HLSP2P_REQUIRE_XGMI", "1")
+    with pytest.raises(RuntimeError, match="did not use its P2P transport"):
+        bench._label_rehearsal(record())
+    ok = record()
+    ok["data_plane"].update(wire=["p2p"], transport_degraded=False)
+    bench._label_rehearsal(ok)
+    assert ok["config"]["parallelism"] == "swarm8-rccl" and "NOT" not in ok["config"]["model"]
