@@ -44,17 +44,27 @@ def run(n: int, extra: list, cpu: bool, timeout: float) -> dict:
 def table(rows: list) -> str:
     base = next((r["record"]["value"] for r in rows if r["ok"] and r["n"] == 1), None)
     out = ["| GPUs | segments/s | offload | goodput GB/s | ms/step | weak-scaling efficiency | bound per rank "
-           "| data plane |", "|---:|---:|---:|---:|---:|---:|---|---|"]
+           "| data plane | wire | CU reserve |", "|---:|---:|---:|---:|---:|---:|---|---|---|---|"]
     for r in rows:
         if not r["ok"]:
-            out.append(f"| {r['n']} | failed | | | | | {r['error']} | |")
+            out.append(f"| {r['n']} | failed | | | | | {r['error']} | | | |")
             continue
         rec = r["record"]
         eff = f"{rec['value'] / (r['n'] * base):.2f}" if base else "n/a"
         bounds = ",".join(sorted({p.get("bound", "?") for p in rec.get("per_rank", [])})) or "-"
-        plane = rec.get("data_plane", {}).get("data", "local")
+        dp = rec.get("data_plane", {})
+        plane = dp.get("data", "local")
+        # the transport RCCL chose per pair (its connection log) and the HIP link types;
+        # "-degraded" when one-GPU-per-rank pairs fell back to a network / shared-memory path
+        wire = "/".join(dp.get("wire") or []) or "-"
+        if dp.get("hip_links"):
+            wire += f" ({'/'.join(dp['hip_links'])})"
+        if dp.get("transport_degraded"):
+            wire += " DEGRADED"
+        cal = rec.get("calibration") or {}
+        cu = str(cal.get("chosen", "-")) + (" (calibrated)" if cal.get("source") == "calibrated" else "")
         out.append(f"| {r['n']} | {rec['value']:,.0f} | {rec['offload_ratio']:.3f} | {rec['goodput_GBps']:.1f} | "
-                   f"{rec['ms_per_step']:.2f} | {eff} | {bounds} | {plane} |")
+                   f"{rec['ms_per_step']:.2f} | {eff} | {bounds} | {plane} | {wire} | {cu} |")
     return "\n".join(out)
 
 
