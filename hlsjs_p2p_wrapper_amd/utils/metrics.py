@@ -30,7 +30,10 @@ PREFIX = "hlsp2p_"
 # node.stats key -> (metric suffix, help); all cumulative since the node started
 _NODE_COUNTERS = (
     ("cdn", "cdn_bytes_total", "Bytes this rank fetched from the origin (CDN fallback)."),
-    ("p2p", "p2p_bytes_total", "Bytes this rank received from peers over the data plane."),
+    ("p2p", "p2p_bytes_total",
+     "Bytes this rank received from peers and delivered after their CRC check passed (or pending it)."),
+    ("p2p_wire", "p2p_wire_bytes_total", "Bytes this rank received from peers over the data plane (checked or not)."),
+    ("p2p_rejected", "p2p_rejected_bytes_total", "Peer bytes whose CRC check failed (re-fetched from the CDN)."),
     ("upload", "upload_bytes_total", "Bytes this rank sent to peers."),
     ("cache", "cache_hit_bytes_total", "Bytes served from this rank's HBM cache."),
     ("segments", "segments_total", "Segments delivered by this rank."),
@@ -40,6 +43,7 @@ _NODE_COUNTERS = (
     ("rounds", "rounds_total", "Swarm rounds completed."),
     ("crc_failures", "crc_failures_total", "Received segments whose CRC did not match (re-fetched)."),
     ("deferred", "deferred_total", "Wants deferred to a later round by cache backpressure."),
+    ("cache_segments", "cache_hit_segments_total", "Segments served from this rank's HBM cache."),
 )
 
 
@@ -106,6 +110,10 @@ def node_metrics(node: Any, quantiles: Sequence[float] = (0.5, 0.9, 0.99)) -> Li
                  [(dict(base), float(store.num_entries))]))
     fams.append((PREFIX + "cache_evictions_total", "counter", "Segments evicted from the HBM cache.",
                  [(dict(base), float(store.evictions))]))
+    fams.append((PREFIX + "cache_unpin_underflows_total", "counter",
+                 "Unpins of live cache entries that held no pin (a holder gave up a pin it did not own; "
+                 "0 when the bookkeeping is sound, see agent/audit.py).",
+                 [(dict(base), float(getattr(store, "unpin_underflows", 0)))]))
     timer = node.timer
     totals, counts = dict(timer.total), dict(timer.count)  # C-level copies: the round loop keeps adding
     fams.append((PREFIX + "phase_seconds_total", "counter", "Host wall time per round phase.",
