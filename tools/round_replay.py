@@ -39,50 +39,43 @@ from hlsjs_p2p_wrapper_amd.parallel.comm import SwarmComm  # noqa: E402
 
 
 class FakePeers(SwarmComm):
-    """Rank 0 of ``world``: the other ranks' control messages are synthesized each round."""
+    """Rank 0 of ``world``: the other ranks' control messages are synthesized each round.
 
-    def __init__(self, world: int, wants_per_round: int, seg_len: int, swarm: int) -> None:
+    Every peer wants what rank 0 wants this round (same keys and sizes, its own want ids),
+    announces the segments wanted the round before as added (every rank received all of them)
+    and those ``keep`` rounds old as removed (its ring), and echoes rank 0's consistency and
+    counter words, so the planner's replicas and CDN balance see agreeing, even peers."""
+
+    def __init__(self, world: int, keep: int = 8) -> None:
         self.rank, self.world_size = 0, world
-        self.W, self.seg_len, self.swarm = wants_per_round, seg_len, swarm
+        self.keep = keep
         self.rt = runtime()
-        self.round = 0
-        self.next_sn = 0
-        self.held: list = []  # per round: the sns every fake peer announced
+        self.held: list = []  # per round: (keys [n, 4], sizes [n]) every fake peer holds after it
         self.want_id = 1 << 40
         self.exchanges = 0
-
-    def _keys(self, sns) -> np.ndarray:
-        k = np.zeros((len(sns), 4), dtype=np.int64)
-        k[:, 0] = self.swarm
-        k[:, 3] = sns
-        return k
 
     def allgather_control(self, msg):
         msg = np.asarray(msg, dtype=np.int64)
         if msg.size < HDR or msg[0] != MAGIC:  # a barrier / other collective: echo
             return [msg.copy() for _ in range(self.world_size)]
-        self.round += 1
         nw = int(msg[2])
-        sns = msg[HDR:HDR + 6 * nw].reshape(nw, 6)[:, 3].copy() if nw else np.zeros(0, dtype=np.int64)
+        rows = msg[HDR:HDR + 6 * nw].reshape(nw, 6)
         flags = self.rt.FLAG_ONLINE | self.rt.FLAG_UPLOAD | self.rt.FLAG_DOWNLOAD | self.rt.FLAG_CDN_DEDUP
-        # every peer wants what rank 0 wants this round; it announces last round's segments and
-        # drops the ones older than 8 rounds (its ring)
-        adds = self._keys(self.held[-1]) if self.held else np.zeros((0, 4), dtype=np.int64)
-        adds = np.concatenate([adds, np.full((len(adds), 1), self.seg_len, dtype=np.int64)], axis=1)
-        rms = self._keys(self.held[-9]) if len(self.held) > 8 else np.zeros((0, 4), dtype=np.int64)
-        self.held.append(sns)
+        none = np.zeros((0, 5), dtype=np.int64)
+        adds = np.concatenate([self.held[-1][0], self.held[-1][1][:, None]], axis=1) if self.held else none
+        rms = self.held[-1 - self.keep][0] if len(self.held) > self.keep else none[:, :4]
+        self.held.append((rows[:, :4].copy(), rows[:, 4].copy()))
+        if len(self.held) > self.keep + 1:
+            self.held.pop(0)
         parts = [msg.copy()]
         for r in range(1, self.world_size):
             hdr = np.zeros(HDR, dtype=np.int64)
             hdr[0], hdr[1], hdr[2], hdr[3], hdr[4] = MAGIC, flags, nw, len(adds), len(rms)
-            hdr[6] = msg[6]
+            hdr[6:10] = msg[6:10]  # round, cdn / p2p / upload counters: even peers
             hdr[CHECK_WORD:CHECK_WORD + 3] = msg[CHECK_WORD:CHECK_WORD + 3]  # the replicas agree
-            w = np.zeros((nw, 6), dtype=np.int64)
-            if nw:
-                w[:, :4] = self._keys(sns)
-                w[:, 4] = self.seg_len
-                w[:, 5] = self.want_id + np.arange(nw)
-                self.want_id += nw
+            w = rows.copy()
+            w[:, 5] = self.want_id + np.arange(nw)
+            self.want_id += nw
             parts.append(np.concatenate([hdr, w.reshape(-1), adds.reshape(-1), rms.reshape(-1)]))
         return parts
 
@@ -139,7 +132,7 @@ def main() -> int:
                                 segment_duration=args.seg_duration, num_segments=n_seg, encrypted=False, pool_size=8,
                                 pin_memory=args.device != "cpu")
     seg_len = int(max(origin.pools[0].lengths))
-    comm = FakePeers(args.world, W, seg_len, 5)
+    comm = FakePeers(args.world)
     node = SwarmNode(comm, device=args.device, cache_bytes=64 * W * (seg_len + 512) + (64 << 20), auto_tick=False,
                      max_wants_per_round=W)
     node.verify_deferred = True
@@ -148,12 +141,6 @@ def main() -> int:
     sink = Consumer(node)
     node.set_bulk_sink(sink)
     urls = [origin.base_url + origin.segment_path(0, sn) for sn in range(n_seg)]
-    # each origin segment's actual length: the fake peers announce one common length, so give
-    # every want the same key space but rank 0 its real sizes (the planner sizes receives by the
-    # holder's announced length: keep them equal by announcing each key's own length)
-    lens = np.asarray([origin.pools[0].lengths[sn % origin.pool_size] for sn in range(n_seg)], dtype=np.int64)
-    if len(set(lens.tolist())) > 1:  # synthetic segments vary in length: announce the max
-        comm.seg_len = int(lens.max())
     sn = 0
     hs = []
     prof = cProfile.Profile() if args.profile else None
