@@ -16,6 +16,8 @@
 #include <pybind11/stl.h>
 
 #include <algorithm>
+#include <array>
+#include <chrono>
 #include <cstdlib>
 #include <cstring>
 #include <vector>
@@ -48,6 +50,23 @@ constexpr int64_t kInfo = 24;     // int64 words per segment info row (ops/tsdem
 
 int64_t align_up(int64_t n) { return (n + kAlign - 1) / kAlign * kAlign; }
 
+// host time of transmux_launch by stage (transmux_launch_profile): checks + plans,
+// descriptor upload, result allocations, decrypt (+ fused CRC) launches, demux launches + D2H
+// copies, Python results; with the call count
+enum { kStPlan, kStDesc, kStAlloc, kStDecrypt, kStDemux, kStResult, kStDescPin, kStDescCopy, kStDescDev, kStDescH2D,
+       kStages };
+std::array<double, kStages> g_stage_us{};
+int64_t g_calls = 0;
+using Clock = std::chrono::steady_clock;
+struct StageClock {
+  Clock::time_point t = Clock::now();
+  void lap(int stage) {
+    const auto now = Clock::now();
+    g_stage_us[stage] += std::chrono::duration<double, std::micro>(now - t).count();
+    t = now;
+  }
+};
+
 // Host staging of many small arrays, 16-byte aligned, copied to the device in one H2D.
 class Desc {
  public:
@@ -61,12 +80,17 @@ class Desc {
   int64_t add(const std::vector<T>& v) { return add(v.data(), static_cast<int64_t>(v.size() * sizeof(T))); }
   // pinned block from the caching host allocator (recorded on the copy's stream, so reuse
   // waits for the copy), one non-blocking H2D on the current stream
-  Tensor upload(int device) {
+  Tensor upload(int device, StageClock& clk) {
     const int64_t n = std::max<int64_t>(16, static_cast<int64_t>(buf_.size()));
+    clk.lap(kStDesc);
     Tensor host = torch::empty({n}, torch::TensorOptions().dtype(torch::kUInt8).pinned_memory(true));
+    clk.lap(kStDescPin);
     std::memcpy(host.data_ptr<uint8_t>(), buf_.data(), buf_.size());
+    clk.lap(kStDescCopy);
     Tensor d = torch::empty({n}, torch::TensorOptions().dtype(torch::kUInt8).device(torch::kCUDA, device));
+    clk.lap(kStDescDev);
     d.copy_(host, /*non_blocking=*/true);
+    clk.lap(kStDescH2D);
     dev_ = d;
     return d;
   }
@@ -146,6 +170,8 @@ py::tuple transmux_launch(Tensor src, I64 src_off, I64 nbytes, py::array_t<uint8
                           py::array_t<uint8_t, py::array::c_style | py::array::forcecast> iv, Tensor td0, Tensor isb,
                           int64_t max_pes, py::object expect_obj, c10::optional<Tensor> crc_w,
                           c10::optional<Tensor> crc_tables) {
+  StageClock clk;
+  ++g_calls;
   TORCH_CHECK_VALUE(src.is_cuda() && src.is_contiguous() && src.scalar_type() == torch::kUInt8, "src: contiguous GPU uint8");
   TORCH_CHECK_VALUE((reinterpret_cast<uintptr_t>(src.data_ptr()) & 15) == 0, "src must be 16-byte aligned");
   const int64_t B = src_off.size();
@@ -247,6 +273,7 @@ py::tuple transmux_launch(Tensor src, I64 src_off, I64 nbytes, py::array_t<uint8
   plan_demux(pe);
   plan_demux(pc);
 
+  clk.lap(kStPlan);
   // ---- every descriptor of the batch in one staging block, one H2D
   Desc desc;
   int64_t d_so = -1, d_do = -1, d_bp = -1, d_cp = -1, d_drk = -1, d_iv = -1, d_mo = -1, d_vco = -1, d_vl = -1,
@@ -277,7 +304,7 @@ py::tuple transmux_launch(Tensor src, I64 src_off, I64 nbytes, py::array_t<uint8
     pc.d_bp = desc.add(pc.blk_prefix);
     pc.d_eo = desc.add(pc.es_off);
   }
-  desc.upload(device);
+  desc.upload(device, clk);
 
   // ---- host results block: info rows (enc group, then clear group) | enc plaintext lengths
   Tensor host = torch::empty({(ne + nc) * kInfo + ne + 1}, torch::TensorOptions().dtype(torch::kInt64).pinned_memory(true));
@@ -292,8 +319,9 @@ py::tuple transmux_launch(Tensor src, I64 src_off, I64 nbytes, py::array_t<uint8
   }
   Tensor hdr_rec;
   if (ne && hdr_on) hdr_rec = torch::empty({std::max<int64_t>(1, hdr_pos) * 16}, dev_opts.dtype(torch::kUInt8));
+  if (ne) dec = torch::empty({dec_pos + kAlign}, dev_opts.dtype(torch::kUInt8));
+  clk.lap(kStAlloc);
   if (ne) {
-    dec = torch::empty({dec_pos + kAlign}, dev_opts.dtype(torch::kUInt8));
     hip_ok(hlsp2p::dev::launch_aes128_cbc_decrypt(
                static_cast<const uint8_t*>(src.data_ptr()), static_cast<uint8_t*>(dec.data_ptr()),
                desc.at<int64_t>(d_so), desc.at<int64_t>(d_do), desc.at<int64_t>(d_bp), desc.at<int64_t>(d_cp),
@@ -316,6 +344,7 @@ py::tuple transmux_launch(Tensor src, I64 src_off, I64 nbytes, py::array_t<uint8
     v_ok_host = torch::empty({nv}, torch::TensorOptions().dtype(torch::kUInt8).pinned_memory(true));
     v_ok_host.copy_(v_ok, /*non_blocking=*/true);
   }
+  clk.lap(kStDecrypt);
 
   py::list groups, keep;  // keep: scratch the kernels use until the batch completes
   int64_t row0 = 0;
@@ -364,6 +393,7 @@ py::tuple transmux_launch(Tensor src, I64 src_off, I64 nbytes, py::array_t<uint8
     groups.append(py::make_tuple(idx, info, pes, es, eo, hinfo, hlens));
     row0 += n;
   }
+  clk.lap(kStDemux);
   keep.append(dec.defined() ? py::cast(dec) : py::none());
   keep.append(desc.device());
   if (hdr_rec.defined()) keep.append(hdr_rec);
@@ -374,7 +404,9 @@ py::tuple transmux_launch(Tensor src, I64 src_off, I64 nbytes, py::array_t<uint8
     std::memcpy(vi.mutable_data(), v_idx.data(), static_cast<size_t>(nv * 8));
     verify = py::make_tuple(vi, v_ok_host);  // batch indices of the verified segments, ok flags (pinned)
   }
-  return py::make_tuple(groups, keep, host, verify);
+  auto out = py::make_tuple(groups, keep, host, verify);
+  clk.lap(kStResult);
+  return out;
 }
 
 }  // namespace
@@ -383,6 +415,22 @@ void register_transmux(py::module& m) {
   m.def("set_cu_reserve", [](int n) { g_cu_reserve = std::max(0, n); }, py::arg("n"),
         "CUs the persistent decrypt grid leaves free for concurrent (RCCL) kernels");
   m.def("cu_reserve", [] { return g_cu_reserve; });
+  m.def(
+      "transmux_launch_profile",
+      [](bool reset) {
+        py::dict d;
+        const char* names[kStages] = {"plan",          "desc_build",       "alloc",      "decrypt_launch",
+                                      "demux_launch_d2h", "results",       "desc_pinned", "desc_memcpy",
+                                      "desc_dev_alloc",   "desc_h2d"};
+        for (int i = 0; i < kStages; ++i) d[names[i]] = g_stage_us[i];
+        d["calls"] = g_calls;
+        if (reset) {
+          g_stage_us.fill(0.0);
+          g_calls = 0;
+        }
+        return d;
+      },
+      py::arg("reset") = false, "host microseconds of transmux_launch by stage (summed) and the call count");
   m.def("transmux_launch", &transmux_launch, py::arg("src"), py::arg("src_off"), py::arg("nbytes"), py::arg("enc"),
         py::arg("drk"), py::arg("iv"), py::arg("td0"), py::arg("isb"), py::arg("max_pes"),
         py::arg("expect") = py::none(), py::arg("crc_w") = py::none(), py::arg("crc_tables") = py::none());

@@ -162,6 +162,12 @@ def main() -> int:
         print(out.getvalue(), file=sys.stderr)
         return rc or 1
     rec = json.loads(lines[-1])
+    from hlsjs_p2p_wrapper_amd.ops._native import device as _dev
+
+    prof = getattr(_dev(), "transmux_launch_profile", None)
+    tx = prof() if prof is not None else {}
+    calls = max(1, int(tx.pop("calls", 0) or 1))
+    tx_us = {k: round(v / calls, 1) for k, v in tx.items()}
     steps, ms = rec["steps"], rec["ms_per_step"]
     pr = (rec.get("per_rank") or [{}])[0]
     p2p_mb = float(pr.get("p2p_recv_MB", 0.0))  # received per round
@@ -178,6 +184,7 @@ def main() -> int:
         "projected_ms_per_step": round(step_ms, 4), "projected_per_rank_value": round(per_rank, 2),
         "projected_job_value": round(per_rank * args.peers, 2),
         "offload_ratio": rec.get("offload_ratio"), "received_rows": made["plane"].recv_rows,
+        "transmux_launch_us_per_call": tx_us,
         "bench_record": rec}), flush=True)
     return 0
 
