@@ -86,9 +86,10 @@ def parse():
     p.add_argument("--warmup", type=int, default=5)
     p.add_argument("--config", default="1080p6m", choices=sorted(CONFIGS))
     p.add_argument("--inflight", type=int, default=None,
-                   help="fragments in flight per player (per step), default 64 -- chosen by measurement: 128 "
-                        "is flat on the PCIe-bound headline and was -4 %% to +20 %% on the device-bound "
-                        "HBM-origin probe across boxes (profiles/r3_inflight, profiles/r4_ab)")
+                   help="fragments in flight per player (per step), default 64 (96 at N >= 8) -- chosen by "
+                        "measurement: 128 is flat on the PCIe-bound headline and was -4 %% to +20 %% on the "
+                        "device-bound HBM-origin probe across boxes (profiles/r3_inflight, profiles/r4_ab); at "
+                        "N=8 96 amortizes the rank's per-step host work (profiles/r6_inflight)")
     p.add_argument("--pool", type=int, default=64, help="distinct packaged segments per rendition")
     p.add_argument("--cache-gb", type=float, default=None,
                    help="segment-cache arena per GPU (default 8 GB)")
@@ -223,6 +224,7 @@ def _workload(args):
     return preset, encrypted, seg_dur, desc, K, n_segments, W, origin_kwargs, hls_config, p2p_base
 
 
+INFLIGHT_N8 = 96  # default fragments in flight per player at N >= 8 (main)
 CALIB_SETTLE = 2  # untimed steps after each candidate is set (rounds in flight drain under it)
 
 
@@ -467,7 +469,11 @@ def main() -> int:
         # 64, by measurement (profiles/r4_ab): the headline is PCIe-bound and flat at 128; the
         # HBM-origin probe was +10-20 % at 128 on round-3 boxes and -4 % on round 4's.  (The
         # round-3 2-rank fault at 128 was the CRC-table lifetime bug, fixed: profiles/r4_uaf.)
-        args.inflight = 64
+        # 96 from N=8 on: with 1/8 of the bytes on PCIe the rank's per-step host work is
+        # co-bound with the DMA at 64, and more fragments per step amortize it (the single-GPU
+        # projection of an 8-rank swarm, profiles/r6_inflight)
+        world_env = int(os.environ.get("WORLD_SIZE", str(args.gpus or 1)))
+        args.inflight = INFLIGHT_N8 if world_env >= 8 else 64
     if args.cache_gb is None:
         args.cache_gb = 8.0
     if args.config in LIVE and args.players < 1:

@@ -153,6 +153,8 @@ def main() -> int:
         return node
 
     agent.node_for_config = node_for_config
+    if args.peers >= 8 and not any(a == "--inflight" or a.startswith("--inflight=") for a in bench_argv):
+        bench_argv = ["--inflight", str(bench.INFLIGHT_N8), *bench_argv]  # bench.py's own default at N >= 8
     sys.argv = ["bench.py", "--cu-calibrate", "off", *bench_argv]
     out = io.StringIO()
     with contextlib.redirect_stdout(out):
