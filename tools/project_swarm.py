@@ -10,13 +10,18 @@ was sent the round before) and its data plane is local:
 * the plan is the real N-rank plan of the native planner: this rank seeds 1/N of the
   segments from the CDN and forwards each to the N-1 peers (sends: not executed) and receives
   the other (N-1)/N from the N-1 seeders;
-* a receive is a device-to-device copy of the segment's bytes from an HBM copy of the origin
-  pool into the rank's arena run (the HBM traffic of the real send + receive), with the
-  seeder's keyed CRC trailer written beside it, so the consumer's fused decrypt CRC checks
-  every received segment as in production.
+* a receive moves the segment's bytes from an HBM copy of the origin pool into the rank's
+  arena run (the HBM traffic of the real send + receive), with the seeder's keyed CRC trailer
+  written beside it, so the consumer's fused decrypt CRC checks every received segment as in
+  production.  ``--plane copy``: merged ``hipMemcpyAsync`` device-to-device copies on the node
+  stream; ``--plane rccl`` (default): a ONE-rank RCCL communicator sends each contiguous span
+  to itself in one ``ncclGroupStart / ncclSend / ncclRecv / ncclGroupEnd`` call per round on
+  the node stream -- RCCL's own kernels move the bytes, holding CUs beside the decrypt grid as
+  on the real node (the decrypt leaves the CU reserve free, calibratable with
+  ``--cu-calibrate force``).
 
-What it does NOT model: the xGMI links (a receive here is an HBM copy, faster than the links)
-and the CUs the RCCL kernels hold.  The record therefore states the xGMI receive roofline
+What it does NOT model: the xGMI links (a receive here is an HBM-to-HBM copy, faster than the
+links).  The record therefore states the xGMI receive roofline
 of the same bytes, ``(N-1) x 76.8 GB/s`` per direction, and ``projected_ms_per_step`` =
 max(measured step, that roofline).
 
@@ -44,13 +49,34 @@ sys.path.insert(0, str(ROOT / "tools"))
 XGMI_GBPS_PER_DIR = 76.8  # parallel/wire.py:XGMI_LINK_GBPS_PER_DIR
 
 
+def _spans(src: np.ndarray, dst: np.ndarray, lens: np.ndarray, max_gap: int):
+    """Merge rows whose source and destination advance by the same delta with a gap below
+    ``max_gap`` (the arena and the origin pools share the 256-byte alignment) into spans:
+    (source pointers, destination pointers, bytes)."""
+    if not len(src):
+        z = np.zeros(0, dtype=np.int64)
+        return z, z, z
+    ds, ss = np.diff(dst), np.diff(src)
+    brk = (ds != ss) | (ds < lens[:-1]) | (ds - lens[:-1] >= max_gap)
+    start = np.concatenate([[0], np.flatnonzero(brk) + 1])
+    end = np.concatenate([start[1:], [len(src)]]) - 1
+    return src[start].copy(), dst[start].copy(), (dst[end] + lens[end] - dst[start]).astype(np.int64)
+
+
 class DevicePeers:
     """The fake peers' data plane: receives served from an HBM copy of the origin's pools."""
 
-    def __init__(self, comm, node, origins, ring: int = 16) -> None:
+    def __init__(self, comm, node, origins, plane: str = "rccl", ring: int = 16) -> None:
         import torch
 
+        from hlsjs_p2p_wrapper_amd.ops._native import device as _dev
+
         self.comm, self.node = comm, node
+        self.plane = plane
+        self.rccl = None
+        if plane == "rccl":
+            dev = _dev()
+            self.rccl = dev.RcclComm(dev.rccl_unique_id(), 1, 0, node.device.index or 0)
         self.dev = node.device
         # per pool of every synthetic origin: its host allocation base, an HBM copy, the
         # segments' offsets and plain CRC-32s (vectorized lookups: no per-row Python)
@@ -68,6 +94,12 @@ class DevicePeers:
                                             ctypes.c_void_p]
         self.hip.hipMemcpyAsync.restype = ctypes.c_int
         self.recv_rows = 0
+        self.spans = 0
+
+    def close(self) -> None:
+        if self.rccl is not None:
+            self.rccl.close()
+            self.rccl = None
 
     def exchange_spans(self, sp, sb, sd, rp, rb, rs) -> None:
         import torch
@@ -97,9 +129,15 @@ class DevicePeers:
             if (self.offsets[k][np.minimum(at, len(self.offsets[k]) - 1)] != off[m]).any():
                 raise RuntimeError("a received want does not start at a pool segment")
             plain[m] = self.crcs[k][at]
-        # the seeders' bytes: one merged D2D copy per contiguous run, on the node stream
-        _dev().h2d_batch(self.node.arena, np.ascontiguousarray(roff, dtype=np.int64), dptr,
-                         np.ascontiguousarray(lens, dtype=np.int64), dbase, ALIGN, True)
+        roff = np.ascontiguousarray(roff, dtype=np.int64)
+        lens = np.ascontiguousarray(lens, dtype=np.int64)
+        if self.rccl is None:  # the seeders' bytes: one merged D2D copy per contiguous run, on the node stream
+            _dev().h2d_batch(self.node.arena, roff, dptr, lens, dbase, ALIGN, True)
+        else:  # one RCCL group call: a send + receive to itself per contiguous span
+            s_ptr, r_ptr, nb = _spans(dptr, self.node.arena.data_ptr() + roff, lens, ALIGN)
+            peer = np.zeros(len(s_ptr), dtype=np.int64)
+            self.rccl.exchange(s_ptr, nb, peer, r_ptr, nb.copy(), peer.copy(), torch.cuda.current_stream().cuda_stream)
+            self.spans += len(s_ptr)
         # their trailers: keyed CRCs, as the seeders' ingest CRC tables hold them.  The
         # receive runs' trailer slices are back to back from row 0 (node._span_columns)
         keyed = plain.view(np.int32) ^ _crc.key_digest(keys)
@@ -120,6 +158,8 @@ class DevicePeers:
 def main() -> int:
     ap = argparse.ArgumentParser(description=__doc__, formatter_class=argparse.RawDescriptionHelpFormatter)
     ap.add_argument("--peers", type=int, default=8, help="the swarm size N this rank is one of")
+    ap.add_argument("--plane", default="rccl", choices=["rccl", "copy"],
+                    help="how received bytes move: a one-rank RCCL self-exchange, or merged D2D copies")
     args, bench_argv = ap.parse_known_args()
     if args.peers < 2:
         raise SystemExit("--peers must be >= 2")
@@ -131,7 +171,7 @@ def main() -> int:
     from round_replay import FakePeers
 
     comm = FakePeers(args.peers)
-    comm.data_transport = f"projection: {args.peers - 1} synthetic peers, HBM-copy receives"
+    comm.data_transport = f"projection: {args.peers - 1} synthetic peers, {args.plane} receives"
     orig = agent.node_for_config
     made = {}
 
@@ -147,7 +187,12 @@ def main() -> int:
         node = orig({**p2p_config, "gpuSwarm": cfg})
         if not node.is_cuda:
             raise SystemExit("project_swarm.py needs the GPU")
-        plane = DevicePeers(comm, node, list(_http._registry.values()))
+        plane = DevicePeers(comm, node, list(_http._registry.values()), args.plane)
+        if args.plane == "rccl":  # as DistComm does once its native RCCL plane is open
+            from hlsjs_p2p_wrapper_amd.ops._native import device as _dev
+            from hlsjs_p2p_wrapper_amd.parallel.comm import RCCL_CU_RESERVE
+
+            _dev().set_cu_reserve(int(os.environ.get("HLSP2P_RCCL_CU_RESERVE", str(RCCL_CU_RESERVE))))
         comm.exchange_spans = plane.exchange_spans
         made["plane"] = plane
         return node
@@ -157,8 +202,12 @@ def main() -> int:
         bench_argv = ["--inflight", str(bench.INFLIGHT_N8), *bench_argv]  # bench.py's own default at N >= 8
     sys.argv = ["bench.py", "--cu-calibrate", "off", *bench_argv]
     out = io.StringIO()
-    with contextlib.redirect_stdout(out):
-        rc = bench.main()
+    try:
+        with contextlib.redirect_stdout(out):
+            rc = bench.main()
+    finally:
+        if "plane" in made:
+            made["plane"].close()
     lines = [ln for ln in out.getvalue().splitlines() if ln.startswith("{")]
     if rc or not lines:
         print(out.getvalue(), file=sys.stderr)
@@ -179,7 +228,8 @@ def main() -> int:
     per_rank = rec["value"] * ms / step_ms
     print(json.dumps({
         "projection": f"one rank of a {args.peers}-rank swarm on one MI355X (synthetic peers; receives are HBM "
-                      "copies; xGMI links and RCCL's CUs not modelled)",
+                      f"copies by {'a one-rank RCCL self-exchange' if args.plane == 'rccl' else 'hipMemcpyAsync'}; "
+                      "the xGMI links not modelled)", "plane": args.plane, "rccl_spans": made["plane"].spans,
         "peers": args.peers, "metric": rec["metric"], "unit": rec["unit"],
         "measured_ms_per_step": ms, "measured_per_rank_value": rec["value"],
         "xgmi_receive_roof_ms_per_step": round(roof_ms, 4),
