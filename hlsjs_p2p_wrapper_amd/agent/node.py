@@ -993,7 +993,10 @@ class SwarmNode:
         if len(rows):
             # the entries this round's reservations overwrite leave the directory in this
             # round's control message, so no peer plans a transfer from them: a send would pin
-            # them after admission and the reservation would find them pinned
+            # them after admission and the reservation would find them pinned.  Sizes are the
+            # admitted ones (the planner never sends a copy larger than a want announced); a
+            # want the planner then holds back (at most once, kWHeld) retired its share too --
+            # the hold is decided from every rank's wants, after this message must go out
             need = int(np.maximum((rows[:, 4] + (ALIGN - 1)) // ALIGN * ALIGN, ALIGN).sum())
             self.store.retire_region(need)
             # the round's runs (CDN + one per source peer) all land in the region admission
