@@ -429,7 +429,10 @@ void plan_round_into(const Directory& dir, const Want* wants_in, size_t n_in, co
   // Seeder assignment, run-affine: consecutive keys (sorted: same track, ascending sn) go
   // to the same rank until it holds its share of the round's seed bytes.  Load stays
   // balanced, and each rank's CDN fetches form ONE contiguous sn run, i.e. one merged
-  // pinned-host -> HBM DMA instead of every world-th segment.
+  // pinned-host -> HBM DMA instead of every world-th segment.  The rotation starts at a rank
+  // drawn from the round's first seed key (the same on every replica): a round with fewer
+  // seeds than wanters -- the live edge, one new segment per round -- would otherwise give
+  // every seed to the lowest wanting rank, whose CDN link then fetches for the whole swarm.
   if (!seeds.empty()) {
     int64_t seed_bytes = 0;
     uint64_t all = 0;
@@ -444,13 +447,16 @@ void plan_round_into(const Directory& dir, const Want* wants_in, size_t n_in, co
     const int64_t quota = (seed_bytes + nseed - 1) / std::max(nseed, 1);
     std::vector<int64_t>& seeded = S.seeded;
     seeded.assign(world, 0);
+    const SegKey& k0 = seeds.front().key;
+    const int start = int(fmix64((uint64_t(k0.swarm) << 32) ^ (uint64_t(k0.level) << 48) ^
+                                 (uint64_t(k0.url_id) << 16) ^ uint64_t(k0.sn)) % uint64_t(world));
     int cur = -1;
     for (const auto& g : seeds) {
       int seeder = -1;
       if (cur >= 0 && ((g.cands >> cur) & 1u) && seeded[cur] < quota) seeder = cur;
       if (seeder < 0) {  // next rank (in rank order) with room, else the least loaded
         for (int k = 1; k <= world && seeder < 0; ++k) {
-          const int r = ((cur < 0 ? -1 : cur) + k + world) % world;
+          const int r = ((cur < 0 ? start - 1 : cur) + k + world) % world;
           if (((g.cands >> r) & 1u) && seeded[r] < quota) seeder = r;
         }
         for (int r = 0; r < world && seeder < 0; ++r) {

@@ -114,7 +114,15 @@ class DevicePeers:
             return
         wids, _, _, roff, lens, keys = h.recv
         info = self.node._wt.info(np.ascontiguousarray(wids))
-        ptrs, bases = info[:, 5], info[:, 6]
+        ptrs, bases = info[:, 5].copy(), info[:, 6].copy()
+        for i in np.flatnonzero(bases == 0).tolist():  # live origins: the node resolves these in Python
+            x = self.node._wx.get(int(wids[i]))
+            if x is None or x.src is None:
+                continue
+            origin, path, rng = x.src
+            data, off, _, _ = origin.resource(path)
+            bases[i] = data.data_ptr()
+            ptrs[i] = bases[i] + int(off) + (int(rng[0]) if rng is not None else 0)
         j = np.searchsorted(self.host_base, bases)
         jc = np.minimum(j, len(self.host_base) - 1)
         if ((j >= len(self.host_base)) | (self.host_base[jc] != bases)).any():
@@ -194,6 +202,7 @@ def main() -> int:
 
             _dev().set_cu_reserve(int(os.environ.get("HLSP2P_RCCL_CU_RESERVE", str(RCCL_CU_RESERVE))))
         comm.exchange_spans = plane.exchange_spans
+        comm.node = node  # the peers' CDN counters follow what they seeded to this rank
         made["plane"] = plane
         return node
 

@@ -53,11 +53,27 @@ class FakePeers(SwarmComm):
         self.held: list = []  # per round: (keys [n, 4], sizes [n]) every fake peer holds after it
         self.want_id = 1 << 40
         self.exchanges = 0
+        # each peer's cumulative CDN bytes (header word 7, the planner's CDN balance): what it
+        # seeded to this rank -- a seeder sends every segment it fetched to all wanters -- read
+        # from the node's last posted plan when the caller sets `node`
+        self.node = None
+        self.cdn = np.zeros(world, dtype=np.int64)
+        self._credited = -1
+
+    def _credit_seeders(self) -> None:
+        h = getattr(self.node, "_last_posted", None) if self.node is not None else None
+        if h is None or h.plan is None or h.round == self._credited:
+            return
+        self._credited = h.round
+        recv = h.plan[1]
+        if len(recv):
+            np.add.at(self.cdn, recv[:, 5], recv[:, 4])
 
     def allgather_control(self, msg):
         msg = np.asarray(msg, dtype=np.int64)
         if msg.size < HDR or msg[0] != MAGIC:  # a barrier / other collective: echo
             return [msg.copy() for _ in range(self.world_size)]
+        self._credit_seeders()
         nw = int(msg[2])
         rows = msg[HDR:HDR + 6 * nw].reshape(nw, 6)
         flags = self.rt.FLAG_ONLINE | self.rt.FLAG_UPLOAD | self.rt.FLAG_DOWNLOAD | self.rt.FLAG_CDN_DEDUP
@@ -71,7 +87,9 @@ class FakePeers(SwarmComm):
         for r in range(1, self.world_size):
             hdr = np.zeros(HDR, dtype=np.int64)
             hdr[0], hdr[1], hdr[2], hdr[3], hdr[4] = MAGIC, flags, nw, len(adds), len(rms)
-            hdr[6:10] = msg[6:10]  # round, cdn / p2p / upload counters: even peers
+            hdr[6:10] = msg[6:10]  # round, p2p / upload counters: even peers
+            if self.node is not None:
+                hdr[7] = self.cdn[r]
             hdr[CHECK_WORD:CHECK_WORD + 3] = msg[CHECK_WORD:CHECK_WORD + 3]  # the replicas agree
             w = rows.copy()
             w[:, 5] = self.want_id + np.arange(nw)
@@ -136,6 +154,7 @@ def main() -> int:
     node = SwarmNode(comm, device=args.device, cache_bytes=64 * W * (seg_len + 512) + (64 << 20), auto_tick=False,
                      max_wants_per_round=W)
     node.verify_deferred = True
+    comm.node = node
     node._grow_crc(1 << 17)  # tiny segments fill the ring with more entries than its sizing assumes
     node.divergence_check = False  # the fake peers echo rank 0's check words; nothing to compare
     sink = Consumer(node)
