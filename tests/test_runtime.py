@@ -418,3 +418,27 @@ def test_planner_never_sends_more_than_the_wanter_admitted(rt):
                          flags(rt, 4), 4)
     for r in plan:
         assert r[4] <= {12: 4000, 22: 4000, 32: 3500}[int(r[7])]
+
+
+def test_planner_spreads_lone_seeds_across_the_wanters(rt):
+    """The live edge: every rank wants the same one new segment per round and nobody holds it.
+    The seeder rotation starts at a rank drawn from the round's first seed key, so over many
+    rounds every wanting rank seeds its share (it started at rank 0 every round, which made
+    the lowest rank fetch the whole channel from the CDN); every replica draws the same rank."""
+    world, rounds = 8, 400
+    seeds = np.zeros(world, dtype=np.int64)
+    for sn in range(rounds):
+        rows = wants([(sn, 3000, 100 * sn + r, r, 0) for r in range(world)])
+        plan = rt.plan_round(rt.Directory(), rows, flags(rt, world), world)
+        cdn = [int(r[6]) for r in plan if r[5] == -1]
+        assert len(cdn) == 1  # one fetch, forwarded to the 7 others
+        assert sorted(int(r[6]) for r in plan if r[5] == cdn[0]) == [r for r in range(world) if r != cdn[0]]
+        assert np.array_equal(rt.plan_round(rt.Directory(), rows, flags(rt, world), world), plan)
+        seeds[cdn[0]] += 1
+    assert seeds.min() >= rounds / world / 2, seeds  # ~50 each; rank 0 alone seeded all 400 before
+    # a round with many seeds still gives every rank one contiguous run of its quota
+    rows = wants([(sn, 3000, 1000 * r + sn, r, 0) for r in range(world) for sn in range(64)])
+    plan = rt.plan_round(rt.Directory(), rows, flags(rt, world), world)
+    for r in range(world):
+        sns = sorted(int(p[3]) for p in plan if p[5] == -1 and p[6] == r)
+        assert len(sns) == 8 and sns == list(range(sns[0], sns[0] + 8))
