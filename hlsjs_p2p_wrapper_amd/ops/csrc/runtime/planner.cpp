@@ -16,6 +16,12 @@ inline uint64_t fmix64(uint64_t x) {  // murmur3 finalizer: full avalanche of ev
   x *= 0xC4CEB9FE1A85EC53ull;
   return x ^ (x >> 33);
 }
+// a well-mixed 64-bit draw from a segment key (planner tie-breaks that must agree on every
+// replica but not favour low ranks)
+inline uint64_t key_draw(const SegKey& k) {
+  return fmix64((uint64_t(k.swarm) << 32) ^ (uint64_t(k.level) << 48) ^ (uint64_t(k.url_id) << 16) ^
+                uint64_t(k.sn));
+}
 }  // namespace
 
 uint64_t Directory::entry_terms(const Slot& s) {
@@ -357,6 +363,9 @@ void plan_round_into(const Directory& dir, const Want* wants_in, size_t n_in, co
         if (((de->holders >> r) & 1u) && flag(r, kOnline) && flag(r, kUploadOn)) holders |= uint64_t(1) << r;
     }
     unserved.clear();
+    // holder rotation offset drawn from the key (same on every replica): a lone wanter's
+    // equal-load holders take turns across rounds instead of the rank after it every time
+    const int koff = world > 1 ? int(key_draw(key) % uint64_t(world)) : 0;
     for (size_t w = i; w < j; ++w) {
       const Want& wt = wants[w];
       const int d = wt.rank;
@@ -375,8 +384,8 @@ void plan_round_into(const Directory& dir, const Want* wants_in, size_t n_in, co
         continue;
       }
       int best = -1;
-      for (int k = 1; k <= world; ++k) {  // rotation start: the rank after d
-        int h = (d + k) % world;
+      for (int k = 1; k <= world; ++k) {  // rotation start: the rank after d, shifted by the key
+        int h = (d + koff + k) % world;
         if (!((cand >> h) & 1u)) continue;
         if (best < 0) { best = h; continue; }
         int64_t lh = link[size_t(h) * world + d], lb = link[size_t(best) * world + d];
@@ -447,9 +456,7 @@ void plan_round_into(const Directory& dir, const Want* wants_in, size_t n_in, co
     const int64_t quota = (seed_bytes + nseed - 1) / std::max(nseed, 1);
     std::vector<int64_t>& seeded = S.seeded;
     seeded.assign(world, 0);
-    const SegKey& k0 = seeds.front().key;
-    const int start = int(fmix64((uint64_t(k0.swarm) << 32) ^ (uint64_t(k0.level) << 48) ^
-                                 (uint64_t(k0.url_id) << 16) ^ uint64_t(k0.sn)) % uint64_t(world));
+    const int start = int(key_draw(seeds.front().key) % uint64_t(world));
     int cur = -1;
     for (const auto& g : seeds) {
       int seeder = -1;

@@ -442,3 +442,20 @@ def test_planner_spreads_lone_seeds_across_the_wanters(rt):
     for r in range(world):
         sns = sorted(int(p[3]) for p in plan if p[5] == -1 and p[6] == r)
         assert len(sns) == 8 and sns == list(range(sns[0], sns[0] + 8))
+
+
+def test_planner_spreads_a_lone_wanters_holders(rt):
+    """A late joiner wants segments every other rank already holds: the holders take turns
+    across rounds (the holder rotation is shifted by a key-drawn offset) instead of the rank
+    after the wanter serving every one."""
+    world, n = 8, 400
+    d = rt.Directory()
+    adds = np.array([[1, 0, 0, sn, 3000] for sn in range(n)], dtype=np.int64)
+    for r in range(1, world):
+        d.apply(r, adds, np.zeros((0, 4), np.int64))
+    served = np.zeros(world, dtype=np.int64)
+    for sn in range(n):
+        plan = rt.plan_round(d, wants([(sn, 3000, sn, 0, 0)]), flags(rt, world), world)
+        assert len(plan) == 1 and plan[0][6] == 0 and plan[0][5] >= 1
+        served[int(plan[0][5])] += 1
+    assert served[0] == 0 and served[1:].min() >= n / (world - 1) / 2, served
