@@ -46,8 +46,9 @@ def test_projection_of_an_eight_rank_swarm_on_one_gpu(cuda):
     assert rec["errors"] == 0
     pr = rec["per_rank"][0]
     assert pr["crc_failures"] == 0 and pr["p2p_rejected_MB"] == 0.0
-    # 7/8 of the bytes arrive from the synthetic seeders and pass the fused decrypt CRC
-    assert 0.85 <= rec["offload_ratio"] <= 0.876
+    # ~7/8 of the bytes arrive from the synthetic seeders and pass the fused decrypt CRC (the
+    # seeder rotation starts at a key-drawn rank: this rank's share of a short window varies)
+    assert 0.84 <= rec["offload_ratio"] <= 0.91
     assert res["received_rows"] > 0
     assert res["projected_ms_per_step"] >= res["xgmi_receive_roof_ms_per_step"] > 0
     assert set(res["transmux_launch_us_per_call"]) >= {"plan", "decrypt_launch", "demux_launch_d2h"}
