@@ -142,7 +142,15 @@ class DevicePeers:
         if self.rccl is None:  # the seeders' bytes: one merged D2D copy per contiguous run, on the node stream
             _dev().h2d_batch(self.node.arena, roff, dptr, lens, dbase, ALIGN, True)
         else:  # one RCCL group call: a send + receive to itself per contiguous span
-            s_ptr, r_ptr, nb = _spans(dptr, self.node.arena.data_ptr() + roff, lens, ALIGN)
+            a0 = self.node.arena.data_ptr()
+            s_ptr, r_ptr, nb = _spans(dptr, a0 + roff, lens, ALIGN)
+            # host-side bounds of every span before RCCL's kernels touch them: receives inside
+            # the arena, sends inside the pool copy they start in
+            ends = self.dev_base + np.array([t.numel() for t in self.dev_copy], dtype=np.int64)
+            js = np.searchsorted(self.dev_base, s_ptr, side="right") - 1
+            if ((r_ptr < a0) | (r_ptr + nb > a0 + self.node.arena.numel()) | (js < 0) |
+                    (s_ptr + nb > ends[np.maximum(js, 0)])).any():
+                raise RuntimeError("a receive span falls outside the arena or its source pool copy")
             peer = np.zeros(len(s_ptr), dtype=np.int64)
             self.rccl.exchange(s_ptr, nb, peer, r_ptr, nb.copy(), peer.copy(), torch.cuda.current_stream().cuda_stream)
             self.spans += len(s_ptr)
@@ -152,6 +160,8 @@ class DevicePeers:
         n = len(keyed)
         if n > self.ring[0].numel():
             raise RuntimeError("more received rows in one round than the trailer staging ring holds")
+        # (a staging buffer is reused 16 rounds later: its H2D, queued on the node stream with
+        # this round, completed rounds before -- the bench keeps at most lag + 1 in flight)
         stage = self.ring[self.ring_i]
         self.ring_i = (self.ring_i + 1) % len(self.ring)
         stage.numpy()[:n] = keyed
