@@ -188,7 +188,13 @@ def main() -> int:
     from hlsjs_p2p_wrapper_amd.net import http as _http
     from round_replay import FakePeers
 
-    comm = FakePeers(args.peers)
+    churn = 0
+    for i, a in enumerate(bench_argv):  # bench.py's --churn rotation, applied to the synthetic peers
+        if a == "--churn" and i + 1 < len(bench_argv):
+            churn = int(bench_argv[i + 1])
+        elif a.startswith("--churn="):
+            churn = int(a.split("=", 1)[1])
+    comm = FakePeers(args.peers, churn=churn)
     comm.data_transport = f"projection: {args.peers - 1} synthetic peers, {args.plane} receives"
     orig = agent.node_for_config
     made = {}

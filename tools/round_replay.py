@@ -46,9 +46,14 @@ class FakePeers(SwarmComm):
     and those ``keep`` rounds old as removed (its ring), and echoes rank 0's consistency and
     counter words, so the planner's replicas and CDN balance see agreeing, even peers."""
 
-    def __init__(self, world: int, keep: int = 8) -> None:
+    def __init__(self, world: int, keep: int = 8, churn: int = 0) -> None:
         self.rank, self.world_size = 0, world
         self.keep = keep
+        # churn (BASELINE config 3): every `churn` rounds the next peer goes offline for `churn`
+        # rounds (masked in the control plane: it neither serves nor receives P2P and fetches
+        # its wants from the CDN), then one all-online period -- bench.py's --churn rotation
+        self.churn = churn
+        self.rounds = 0
         self.rt = runtime()
         self.held: list = []  # per round: (keys [n, 4], sizes [n]) every fake peer holds after it
         self.want_id = 1 << 40
@@ -84,9 +89,12 @@ class FakePeers(SwarmComm):
         if len(self.held) > self.keep + 1:
             self.held.pop(0)
         parts = [msg.copy()]
+        off = (self.rounds // self.churn) % (self.world_size + 1) if self.churn > 0 else -1
+        self.rounds += 1
         for r in range(1, self.world_size):
             hdr = np.zeros(HDR, dtype=np.int64)
-            hdr[0], hdr[1], hdr[2], hdr[3], hdr[4] = MAGIC, flags, nw, len(adds), len(rms)
+            f = flags & ~self.rt.FLAG_ONLINE if r == off else flags
+            hdr[0], hdr[1], hdr[2], hdr[3], hdr[4] = MAGIC, f, nw, len(adds), len(rms)
             hdr[6:10] = msg[6:10]  # round, p2p / upload counters: even peers
             if self.node is not None:
                 hdr[7] = self.cdn[r]
@@ -136,6 +144,7 @@ def main() -> int:
     ap.add_argument("--rounds", type=int, default=200)
     ap.add_argument("--warmup", type=int, default=20)
     ap.add_argument("--lag", type=int, default=2, help="rounds in flight (the bench's lag-2 pipeline)")
+    ap.add_argument("--churn", type=int, default=0, help="peers go offline in rotation every N rounds")
     ap.add_argument("--seg-duration", type=float, default=0.1, help="seconds per synthetic segment (its size)")
     ap.add_argument("--device", default="cpu", help="cpu, or cuda (the node's arena and kernels on the GPU)")
     ap.add_argument("--profile", default=None, help="write a cProfile of the timed rounds here")
@@ -150,7 +159,7 @@ def main() -> int:
                                 segment_duration=args.seg_duration, num_segments=n_seg, encrypted=False, pool_size=8,
                                 pin_memory=args.device != "cpu")
     seg_len = int(max(origin.pools[0].lengths))
-    comm = FakePeers(args.world)
+    comm = FakePeers(args.world, churn=args.churn)
     node = SwarmNode(comm, device=args.device, cache_bytes=64 * W * (seg_len + 512) + (64 << 20), auto_tick=False,
                      max_wants_per_round=W)
     node.verify_deferred = True
