@@ -49,15 +49,18 @@ sys.path.insert(0, str(ROOT / "tools"))
 XGMI_GBPS_PER_DIR = 76.8  # parallel/wire.py:XGMI_LINK_GBPS_PER_DIR
 
 
-def _spans(src: np.ndarray, dst: np.ndarray, lens: np.ndarray, max_gap: int):
+def _spans(src: np.ndarray, dst: np.ndarray, lens: np.ndarray, max_gap: int, alloc=None):
     """Merge rows whose source and destination advance by the same delta with a gap below
-    ``max_gap`` (the arena and the origin pools share the 256-byte alignment) into spans:
-    (source pointers, destination pointers, bytes)."""
+    ``max_gap`` (the arena and the origin pools share the 256-byte alignment) -- and, given
+    ``alloc``, whose sources lie in the same allocation -- into spans: (source pointers,
+    destination pointers, bytes)."""
     if not len(src):
         z = np.zeros(0, dtype=np.int64)
         return z, z, z
     ds, ss = np.diff(dst), np.diff(src)
     brk = (ds != ss) | (ds < lens[:-1]) | (ds - lens[:-1] >= max_gap)
+    if alloc is not None:  # never across two pool copies, even when they happen to be adjacent
+        brk |= np.diff(alloc) != 0
     start = np.concatenate([[0], np.flatnonzero(brk) + 1])
     end = np.concatenate([start[1:], [len(src)]]) - 1
     return src[start].copy(), dst[start].copy(), (dst[end] + lens[end] - dst[start]).astype(np.int64)
@@ -143,13 +146,15 @@ class DevicePeers:
             _dev().h2d_batch(self.node.arena, roff, dptr, lens, dbase, ALIGN, True)
         else:  # one RCCL group call: a send + receive to itself per contiguous span
             a0 = self.node.arena.data_ptr()
-            s_ptr, r_ptr, nb = _spans(dptr, a0 + roff, lens, ALIGN)
+            s_ptr, r_ptr, nb = _spans(dptr, a0 + roff, lens, ALIGN, j)
             # host-side bounds of every span before RCCL's kernels touch them: receives inside
             # the arena, sends inside the pool copy they start in
             ends = self.dev_base + np.array([t.numel() for t in self.dev_copy], dtype=np.int64)
-            js = np.searchsorted(self.dev_base, s_ptr, side="right") - 1
+            order = np.argsort(self.dev_base)  # the pool copies' device addresses, ascending
+            js = np.searchsorted(self.dev_base[order], s_ptr, side="right") - 1
+            pool = order[np.maximum(js, 0)]
             if ((r_ptr < a0) | (r_ptr + nb > a0 + self.node.arena.numel()) | (js < 0) |
-                    (s_ptr + nb > ends[np.maximum(js, 0)])).any():
+                    (s_ptr + nb > ends[pool])).any():
                 raise RuntimeError("a receive span falls outside the arena or its source pool copy")
             peer = np.zeros(len(s_ptr), dtype=np.int64)
             self.rccl.exchange(s_ptr, nb, peer, r_ptr, nb.copy(), peer.copy(), torch.cuda.current_stream().cuda_stream)
@@ -171,6 +176,21 @@ class DevicePeers:
         if rc != 0:
             raise RuntimeError(f"hipMemcpyAsync of the trailers failed: {rc}")
         self.recv_rows += n
+
+
+def _status_mib() -> dict:
+    """This process's resident memory by kind (``/proc/self/status``): RssAnon is heap and
+    pinned host buffers, RssShmem shared / device-mapped pages, VmHWM the peak."""
+    out = {}
+    try:
+        with open("/proc/self/status") as f:
+            for ln in f:
+                k = ln.split(":", 1)[0]
+                if k in ("VmHWM", "VmRSS", "RssAnon", "RssFile", "RssShmem"):
+                    out[k] = round(int(ln.split()[1]) / 1024, 1)
+    except OSError:
+        pass
+    return out
 
 
 def main() -> int:
@@ -261,7 +281,7 @@ def main() -> int:
         "projected_ms_per_step": round(step_ms, 4), "projected_per_rank_value": round(per_rank, 2),
         "projected_job_value": round(per_rank * args.peers, 2),
         "offload_ratio": rec.get("offload_ratio"), "received_rows": made["plane"].recv_rows,
-        "transmux_launch_us_per_call": tx_us,
+        "transmux_launch_us_per_call": tx_us, "host_memory_MiB": _status_mib(),
         "bench_record": rec}), flush=True)
     return 0
 
