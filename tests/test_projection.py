@@ -52,3 +52,14 @@ def test_projection_of_an_eight_rank_swarm_on_one_gpu(cuda):
     assert res["received_rows"] > 0
     assert res["projected_ms_per_step"] >= res["xgmi_receive_roof_ms_per_step"] > 0
     assert set(res["transmux_launch_us_per_call"]) >= {"plan", "decrypt_launch", "demux_launch_d2h"}
+
+
+def test_round_replay_under_churn_seeds_more_and_answers_everything():
+    """bench.py's churn rotation on the synthetic peers (config 3): while one of the 7 peers
+    is offline this rank seeds 1/7 of the round instead of 1/8, and every want is still
+    answered once."""
+    res = _run([str(REPO / "tools" / "round_replay.py"), "--world", "8", "--wants", "64", "--rounds", "36",
+                "--warmup", "0", "--churn", "2"])
+    assert res["delivered"] == 64 * 36 and res["crc_failures"] == 0
+    assert 64 / 8 < res["per_round"]["cdn"] < 64 / 6
+    assert res["per_round"]["recv"] == 64 - res["per_round"]["cdn"]
