@@ -38,17 +38,20 @@ def test_round_replay_builds_the_n_rank_plan(world):
 
 
 @pytest.mark.gpu
-def test_projection_of_an_eight_rank_swarm_on_one_gpu(cuda):
+@pytest.mark.parametrize("config,churn", [("1080p6m", 0), ("abr5", 2)])
+def test_projection_of_an_eight_rank_swarm_on_one_gpu(cuda, config, churn):
+    """The headline shape, and config 3 (the ABR ladder with peers going offline in rotation)."""
     res = _run([str(REPO / "tools" / "project_swarm.py"), "--peers", "8", "--steps", "12", "--warmup", "4",
-                "--cache-gb", "2"], timeout=420)
+                "--cache-gb", "2", "--config", config, "--churn", str(churn)], timeout=420)
     rec = res["bench_record"]
     assert rec["n_gpus"] == 1 and res["peers"] == 8
     assert rec["errors"] == 0
     pr = rec["per_rank"][0]
     assert pr["crc_failures"] == 0 and pr["p2p_rejected_MB"] == 0.0
     # ~7/8 of the bytes arrive from the synthetic seeders and pass the fused decrypt CRC (the
-    # seeder rotation starts at a key-drawn rank: this rank's share of a short window varies)
-    assert 0.84 <= rec["offload_ratio"] <= 0.91
+    # seeder rotation starts at a key-drawn rank: this rank's share of a short window varies;
+    # under churn an offline peer leaves this rank up to 1/7 to seed)
+    assert (0.80 if churn else 0.84) <= rec["offload_ratio"] <= 0.91
     assert res["received_rows"] > 0
     assert res["projected_ms_per_step"] >= res["xgmi_receive_roof_ms_per_step"] > 0
     assert set(res["transmux_launch_us_per_call"]) >= {"plan", "decrypt_launch", "demux_launch_d2h"}
