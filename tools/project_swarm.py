@@ -77,9 +77,11 @@ class DevicePeers:
         self.comm, self.node = comm, node
         self.plane = plane
         self.rccl = None
+        self.rss = {"before_rccl": _rss_hwm()}
         if plane == "rccl":
             dev = _dev()
             self.rccl = dev.RcclComm(dev.rccl_unique_id(), 1, 0, node.device.index or 0)
+            self.rss["after_rccl_init"] = _rss_hwm()
         self.dev = node.device
         # per pool of every synthetic origin: its host allocation base, an HBM copy, the
         # segments' offsets and plain CRC-32s (vectorized lookups: no per-row Python)
@@ -176,6 +178,11 @@ class DevicePeers:
         if rc != 0:
             raise RuntimeError(f"hipMemcpyAsync of the trailers failed: {rc}")
         self.recv_rows += n
+        if self.comm.exchanges in (1, 2, 10, 100, 1000):  # resident memory as the rounds go
+            import torch as _t
+
+            _t.cuda.current_stream().synchronize()
+            self.rss[f"after_exchange_{self.comm.exchanges}"] = _rss_hwm()
 
 
 def _status_mib() -> dict:
@@ -191,6 +198,11 @@ def _status_mib() -> dict:
     except OSError:
         pass
     return out
+
+
+def _rss_hwm() -> list:
+    st = _status_mib()
+    return [st.get("VmRSS"), st.get("VmHWM")]
 
 
 def main() -> int:
@@ -252,7 +264,9 @@ def main() -> int:
             rc = bench.main()
     finally:
         if "plane" in made:
+            made["plane"].rss["before_close"] = _rss_hwm()
             made["plane"].close()
+            made["plane"].rss["after_close"] = _rss_hwm()
     lines = [ln for ln in out.getvalue().splitlines() if ln.startswith("{")]
     if rc or not lines:
         print(out.getvalue(), file=sys.stderr)
@@ -282,6 +296,7 @@ def main() -> int:
         "projected_job_value": round(per_rank * args.peers, 2),
         "offload_ratio": rec.get("offload_ratio"), "received_rows": made["plane"].recv_rows,
         "transmux_launch_us_per_call": tx_us, "host_memory_MiB": _status_mib(),
+        "rss_MiB_by_stage": made["plane"].rss,
         "bench_record": rec}), flush=True)
     return 0
 
