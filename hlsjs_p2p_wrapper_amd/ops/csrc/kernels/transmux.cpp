@@ -52,7 +52,8 @@ int64_t align_up(int64_t n) { return (n + kAlign - 1) / kAlign * kAlign; }
 
 // host time of transmux_launch by stage (transmux_launch_profile): checks + plans,
 // descriptor upload, result allocations, decrypt (+ fused CRC) launches, demux launches + D2H
-// copies, Python results; with the call count
+// copies, Python results; with the call count.  Plain globals: every call holds the GIL (the
+// binding never releases it), so calls from several Python threads are serialized
 enum { kStPlan, kStDesc, kStAlloc, kStDecrypt, kStDemux, kStResult, kStDescPin, kStDescCopy, kStDescDev, kStDescH2D,
        kStages };
 std::array<double, kStages> g_stage_us{};
