@@ -303,6 +303,10 @@ class SwarmNode:
         self.max_wants_per_round = max_wants_per_round
         self.leaving = False
         self.closed = False
+        # health (utils/metrics.py GET /healthz): the first replicated-state or collective failure
+        # this rank saw (divergence, a lost peer), and when its last round completed
+        self.failed: Optional[str] = None
+        self.last_complete: Optional[float] = None
         # the want table: every wanted segment and the tokens waiting for it (native rows)
         self._wt = self.rt.WantTable()
         self._wx: Dict[int, _WantX] = {}  # want id -> Python-side state (network / live origins)
@@ -1096,6 +1100,7 @@ class SwarmNode:
         h.completed = True
         self._inflight.pop(h.round, None)
         if h.empty:
+            self.last_complete = time.monotonic()
             self.last_round = {"wants": 0, "ms": (time.perf_counter() - h.t0) * 1e3}
             if h.ids is not None and len(h.ids):  # (a lone rank's wants always plan: defensive)
                 self._wt.requeue(h.ids, False)
@@ -1225,6 +1230,7 @@ class SwarmNode:
             self._cdn_busy = min(1.0, self._cdn_num / self._cdn_den) if self._cdn_den > 0 else 0.0
         self._cdn_t = now
         self.timer.add("dev_p2p_ms", h.p2p_ms / 1e3)
+        self.last_complete = time.monotonic()
         self.last_round = {"wants": h.n_wants, "cdn": 0 if h.cdn is None else len(h.cdn[0]), "send": h.n_send,
                            "recv": 0 if h.recv is None else len(h.recv[0]), "cdn_ms": h.cdn_ms, "dmas": h.dmas,
                            "p2p_ms": h.p2p_ms, "ms": (time.perf_counter() - h.t0) * 1e3}
@@ -1276,12 +1282,14 @@ class SwarmNode:
         while not ev.query():
             err = check() if check is not None else ""
             if err:
+                self.failed = self.failed or f"round {h.round}: data plane error: {err}"
                 raise RuntimeError(f"rank {self.rank}: swarm round {h.round} failed in the data plane: {err}")
             if time.perf_counter() > deadline:
                 summary = self.plan_summary(h)
                 log.error("rank %d: swarm round %d did not complete; this rank's plan: %s", self.rank, h.round,
                           summary)
                 self._dump_plan(h)
+                self.failed = self.failed or f"round {h.round} did not complete within {self.round_deadline_s():g} s"
                 raise SwarmPeerLost(f"rank {self.rank}: swarm round {h.round} did not complete on the device "
                                     f"within {self.round_deadline_s():g} s (gpuSwarm.roundTimeoutMs); a peer may have "
                                     f"stopped.  Plan: {summary}")
@@ -1339,6 +1347,8 @@ class SwarmNode:
     def _diverged(self, what: str) -> None:
         """Replicated state differs across ranks: no rank may post another data-plane group.
         Abort the communicator (transfers already posted would never be matched) and log."""
+        if self.failed is None:
+            self.failed = what
         log.error("rank %d: %s", self.rank, what)
         abort = getattr(self.comm, "abort", None)
         if abort is not None:

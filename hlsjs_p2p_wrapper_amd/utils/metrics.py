@@ -11,14 +11,19 @@ Prometheus text exposition format, so a serving fleet scrapes every rank the sam
 * :func:`node_metrics` — one snapshot ``[(name, type, help, [(labels, value)])]``.
 * :func:`render` — the text format (``# HELP`` / ``# TYPE`` / samples).
 * :class:`MetricsServer` — ``GET /metrics`` on a daemon thread (stdlib ``http.server``;
-  nothing GPU-side runs on that thread, it reads host counters only).
+  nothing GPU-side runs on that thread, it reads host counters only), and ``GET /healthz``
+  (:func:`health`: ``ok`` / ``starting`` / ``failed`` with the reason -- a divergence, a lost
+  peer, a failed or stalled round -- as JSON, HTTP 503 once failed) for a serving fleet's
+  liveness probe.
 
 No dependency on ``prometheus_client``: the format is small and a registry would copy
 counters the node already keeps.
 """
 from __future__ import annotations
 
+import json
 import threading
+import time
 from http.server import BaseHTTPRequestHandler, ThreadingHTTPServer
 from typing import Any, Dict, Iterable, List, Optional, Sequence, Tuple
 
@@ -101,6 +106,13 @@ def node_metrics(node: Any, quantiles: Sequence[float] = (0.5, 0.9, 0.99)) -> Li
     fams.append((PREFIX + "peers", "gauge", "Peers online in the swarm (excluding this rank).",
                  [(dict(base), float(max(0, peers)))]))
     fams.append((PREFIX + "world_size", "gauge", "Ranks in the swarm.", [(dict(base), float(node.world))]))
+    fams.append((PREFIX + "node_failed", "gauge",
+                 "1 once this rank saw a divergence, a lost peer or a failed round (GET /healthz says which).",
+                 [(dict(base), 1.0 if getattr(node, "failed", None) else 0.0)]))
+    last = getattr(node, "last_complete", None)
+    if last is not None:
+        fams.append((PREFIX + "seconds_since_last_round", "gauge", "Seconds since this rank's last round completed.",
+                     [(dict(base), max(0.0, time.monotonic() - last))]))
     store = node.store
     fams.append((PREFIX + "cache_capacity_bytes", "gauge", "HBM segment-cache arena size.",
                  [(dict(base), float(store.capacity))]))
@@ -154,8 +166,32 @@ def agent_metrics(agent: Any, index: int = 0, rank: Optional[int] = None) -> Lis
     ]
 
 
+def health(node: Any, stall_s: Optional[float] = None) -> Dict[str, Any]:
+    """Liveness of one node for ``GET /healthz``: ``ok`` (rounds completing), ``starting`` (no
+    round completed yet), or ``failed`` -- the node saw a divergence, a lost peer or a failed
+    round (``reason``), is closed, or its last round completed longer ago than ``stall_s``
+    (default: the node's round deadline, ``gpuSwarm.roundTimeoutMs``)."""
+    last = getattr(node, "last_complete", None)
+    since = None if last is None else max(0.0, time.monotonic() - last)
+    if stall_s is None:
+        deadline = getattr(node, "round_deadline_s", None)
+        stall_s = float(deadline()) if callable(deadline) else 60.0
+    out: Dict[str, Any] = {"rank": int(getattr(node, "rank", 0)), "world": int(getattr(node, "world", 1)),
+                           "round": int(getattr(node, "round", 0)), "seconds_since_last_round": since}
+    reason = getattr(node, "failed", None)
+    if reason is None and getattr(node, "closed", False):
+        reason = "node closed"
+    if reason is None and since is not None and getattr(node, "auto_tick", False) and since > stall_s:
+        reason = f"no round completed for {since:.1f} s (> {stall_s:g} s)"
+    out["status"] = "failed" if reason else ("starting" if since is None else "ok")
+    if reason:
+        out["reason"] = reason
+    return out
+
+
 class MetricsServer:
-    """``GET /metrics`` for one node (and optionally its agents) on a daemon thread.
+    """``GET /metrics`` for one node (and optionally its agents) on a daemon thread, and
+    ``GET /healthz`` (:func:`health` as JSON; HTTP 503 once the node failed).
 
     ``port=0`` binds an ephemeral port (``.port`` reports it).  Binds 127.0.0.1 unless told
     otherwise: the counters are not secret, but exposure is the operator's choice."""
@@ -167,7 +203,17 @@ class MetricsServer:
 
         class _Handler(BaseHTTPRequestHandler):
             def do_GET(self) -> None:  # noqa: N802 - http.server API
-                if self.path.split("?")[0] != "/metrics":
+                path = self.path.split("?")[0]
+                if path == "/healthz":
+                    h = health(outer.node)
+                    body = json.dumps(h).encode()
+                    self.send_response(503 if h["status"] == "failed" else 200)
+                    self.send_header("Content-Type", "application/json")
+                    self.send_header("Content-Length", str(len(body)))
+                    self.end_headers()
+                    self.wfile.write(body)
+                    return
+                if path != "/metrics":
                     self.send_error(404)
                     return
                 body = outer.text().encode()

@@ -255,3 +255,41 @@ def test_metrics_on_gpu_node():
             assert node.metrics_server is None
         clear_origins()
         set_current_node(None)
+
+
+def test_healthz_reports_rounds_and_failures():
+    """``GET /healthz`` (a serving fleet's liveness probe): ``starting`` before the first round,
+    ``ok`` once rounds complete, and HTTP 503 ``failed`` with the reason once the node saw a
+    divergence; the ``node_failed`` / ``seconds_since_last_round`` gauges follow."""
+    import json
+    import urllib.error
+
+    from hlsjs_p2p_wrapper_amd.agent.node import SwarmNode
+    from hlsjs_p2p_wrapper_amd.parallel.comm import LocalComm
+
+    node = SwarmNode(LocalComm(), device="cpu", cache_bytes=1 << 24, auto_tick=False)
+    srv = MetricsServer(node, port=0, agents=[])
+
+    def get():
+        try:
+            with urllib.request.urlopen(f"http://127.0.0.1:{srv.port}/healthz", timeout=10) as resp:
+                return resp.status, json.loads(resp.read())
+        except urllib.error.HTTPError as e:
+            return e.code, json.loads(e.read())
+
+    try:
+        code, h = get()
+        assert code == 200 and h["status"] == "starting" and h["seconds_since_last_round"] is None
+        node.tick()
+        code, h = get()
+        assert code == 200 and h["status"] == "ok" and h["round"] == 1 and h["seconds_since_last_round"] >= 0
+        fams = parse(srv.text())
+        assert value(fams, "hlsp2p_node_failed", rank=0) == 0
+        assert value(fams, "hlsp2p_seconds_since_last_round", rank=0) >= 0
+        node._diverged("replica digest mismatch (test)")
+        code, h = get()
+        assert code == 503 and h["status"] == "failed" and "digest mismatch" in h["reason"]
+        assert value(parse(srv.text()), "hlsp2p_node_failed", rank=0) == 1
+    finally:
+        srv.close()
+        node.close()
